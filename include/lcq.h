@@ -1,0 +1,116 @@
+/*
+ * lcq.h — C ABI of the MI355X-native LightCompress weight-quantization hot path.
+ *
+ * The reference (zhangbilang/LightCompress, package `llmc`) is pure Python/torch and has no
+ * FFI of its own; every entry point below replaces one reference function (cited file:line,
+ * paths relative to the reference root) and is what a ctypes / cffi binding of that function
+ * binds.
+ *
+ * Conventions
+ *   - All tensor arguments are raw DEVICE pointers (hipMalloc'd / torch CUDA storage),
+ *     row-major, contiguous, with explicit sizes. No torch types cross this boundary.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream). Launches are
+ *     asynchronous on that stream; the caller synchronises.
+ *   - The caller owns every buffer; the library never allocates device memory.
+ *   - Return value: 0 on success, negative LCQ_E* code on error; lcq_last_error() returns a
+ *     thread-local message for the last failing call.
+ *   - Numerics follow the reference op by op: every intermediate is rounded to the compute
+ *     dtype (the dtype torch's type promotion gives the reference expression), divisions
+ *     are IEEE true divisions, torch.round is round-half-to-even.
+ */
+#ifndef LCQ_H_
+#define LCQ_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* dtype codes (mirror the torch dtypes the reference uses on this path) */
+enum lcq_dtype {
+  LCQ_F32 = 0,
+  LCQ_F16 = 1,
+  LCQ_BF16 = 2,
+  LCQ_I8 = 3,
+  LCQ_U8 = 4,
+  LCQ_I32 = 5,
+  LCQ_FP8E4M3 = 6,
+  LCQ_F64 = 7,
+};
+
+enum lcq_status {
+  LCQ_OK = 0,
+  LCQ_EINVAL = -1,  /* bad argument (shape, dtype, divisibility) */
+  LCQ_ELAUNCH = -2, /* HIP launch / runtime error */
+  LCQ_EUNSUP = -3,  /* combination not supported */
+};
+
+int lcq_version(void);
+const char* lcq_last_error(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Grouped integer quantization, dynamic (min/max) qparams.
+ * Replaces IntegerQuantizer.get_tensor_qparams + quant/dequant/quant_dequant +
+ * fake_quant_weight_dynamic / real_quant_weight_dynamic
+ *   (llmc/compression/quantization/quant.py:132-143, 545-559, 690-717, 833-869, 916-953)
+ * optionally fused with:
+ *   - the AWQ column pre-scale W * s (awq.py:39-46, 147-164)            [pre_scale != NULL]
+ *   - the AWQ clip v1 clamp(W, min, max) per group (auto_clip.py:193-212)  [clip_max != NULL]
+ *   - VllmRealQuantLinear.pack (module_utils.py:929-955)                  [packed_out != NULL]
+ *
+ * x        [rows, cols] dtype x_dtype (F32/F16/BF16); the compute dtype is x_dtype.
+ * group    elements per group along cols; 0 or == cols means per-channel (reduce over a row).
+ *          cols % group == 0; group % 8 == 0.
+ * pre_scale  optional [cols] in x_dtype: x <- round_ct(x * pre_scale[col]) before anything.
+ * clip_max/clip_min optional [rows*cols/group] in x_dtype: x <- clamp(x, clip_min, clip_max)
+ *          (clip_min may be NULL with clip_max set: symmetric clip, min = -max).
+ * qmin, qmax  integer range (IntegerQuantizer.__init__, quant.py:662-678); sym selects the
+ *          symmetric qparams formula (zeros = 0).
+ * fq_out   optional [rows, cols] fake-quant output, dtype fq_dtype (F32/F16/BF16: final .to()).
+ * codes_out optional [rows, cols] integer codes, dtype codes_dtype (I8/U8/I32).
+ * packed_out optional [rows, ceil(cols / (32/pack_bits))] int32, vLLM little-endian pack of
+ *          (code + 2^(pack_bits-1)) & 0xFF; pack_bits in {4, 8}.
+ * scales_out / zeros_out optional [rows*cols/group] in x_dtype (zeros_out unused when sym).
+ * ------------------------------------------------------------------------------------- */
+int lcq_int_quant_dynamic(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                          int64_t group, const void* pre_scale, const void* clip_max,
+                          const void* clip_min, int qmin, int qmax, int sym,
+                          void* fq_out, int fq_dtype, void* codes_out, int codes_dtype,
+                          void* packed_out, int pack_bits, void* scales_out, void* zeros_out,
+                          void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Grouped integer quantization with GIVEN qparams.
+ * Replaces IntegerQuantizer.fake_quant_weight_static / real_quant_weight_static
+ *   (quant.py:699-717, 785-831, 871-914); used by GPTQ deploy (gptq.py:411-452).
+ * scales [rows*cols/group] dtype s_dtype; zeros [rows*cols/group] dtype z_dtype or NULL (= 0).
+ * ct_dtype is the compute dtype (torch result_type of x, scales, zeros); every input is
+ * converted (exactly) to ct_dtype and every op is rounded to ct_dtype.
+ * ------------------------------------------------------------------------------------- */
+int lcq_int_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                         int64_t group, const void* scales, int s_dtype, const void* zeros,
+                         int z_dtype, int ct_dtype, int qmin, int qmax, void* fq_out,
+                         int fq_dtype, void* codes_out, int codes_dtype, void* packed_out,
+                         int pack_bits, void* stream);
+
+/* vLLM pack of existing integer codes (module_utils.py:929-955).
+ * codes [rows, cols] I8/U8/I32 -> packed [rows, ceil(cols*bits/32)] int32. */
+int lcq_pack_vllm(const void* codes, int codes_dtype, int64_t rows, int64_t cols, int bits,
+                  void* packed_out, void* stream);
+
+/* AutoAWQ GEMM pack (AutoawqRealQuantLinear.gemm_pack, module_utils.py:1097-1158), incl. its
+ * un-clamped fp32 re-quantisation round((W + z*s16)/s16) and raw int32 shift-or packing.
+ * w [oc, ic] (BF16/F16/F32), scales [oc, ic/group] s_dtype, zeros [oc, ic/group] I32.
+ * qweight_out [ic, oc/8] int32, scales_t_out [ic/group, oc] fp16, qzeros_out [ic/group, oc/8].
+ * Only bits == 4 (as the reference). */
+int lcq_pack_autoawq_gemm(const void* w, int w_dtype, int64_t oc, int64_t ic, int64_t group,
+                          const void* scales, int s_dtype, const void* zeros, int bits,
+                          void* qweight_out, void* scales_t_out, void* qzeros_out,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LCQ_H_ */

@@ -1,0 +1,109 @@
+"""ctypes binding of the lcq C ABI (``include/lcq.h``).
+
+The product path has no CPU fallback: if ``liblcq.so`` is missing or a tensor is not on a
+ROCm device, the call raises. This is the binding a maintainer adds to the reference
+(INTEGRATION.md shows the same stub against ``llmc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from pathlib import Path
+
+import torch
+
+_LIB_PATH = Path(__file__).resolve().parent / '_lib' / 'liblcq.so'
+_HEADER = Path(__file__).resolve().parent.parent / 'include' / 'lcq.h'
+
+F32, F16, BF16, I8, U8, I32, FP8E4M3, F64 = range(8)
+_DT = {
+    torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16, torch.int8: I8,
+    torch.uint8: U8, torch.int32: I32, torch.float8_e4m3fn: FP8E4M3, torch.float64: F64,
+}
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_f32 = ctypes.c_float
+_f64 = ctypes.c_double
+
+# argument signatures of every exported entry point (kept in sync with include/lcq.h;
+# tests/test_native_abi.py checks the two agree)
+SIGNATURES = {
+    'lcq_version': ([], _int),
+    'lcq_last_error': ([], ctypes.c_char_p),
+    'lcq_int_quant_dynamic': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _vp, _int, _int, _int,
+                               _vp, _int, _vp, _int, _vp, _int, _vp, _vp, _vp], _int),
+    'lcq_int_quant_static': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _int, _int,
+                              _int, _vp, _int, _vp, _int, _vp, _int, _vp], _int),
+    'lcq_pack_vllm': ([_vp, _int, _i64, _i64, _int, _vp, _vp], _int),
+    'lcq_pack_autoawq_gemm': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _vp, _vp,
+                               _vp, _vp], _int),
+}
+
+_lib = None
+
+
+class LcqError(RuntimeError):
+    pass
+
+
+def lib_path() -> Path:
+    return _LIB_PATH
+
+
+def header_symbols() -> list[str]:
+    """Names of all functions declared in include/lcq.h."""
+    text = _HEADER.read_text()
+    return sorted(set(re.findall(r'\b(lcq_[a-z0-9_]+)\s*\(', text)))
+
+
+def load():
+    """Load liblcq.so (raises if it is missing: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not _LIB_PATH.exists():
+        raise LcqError(f'{_LIB_PATH} not built: run `python -m lightcompress_amd._build` '
+                       '(or __graft_entry__.build()) first; there is no CPU fallback')
+    lib = ctypes.CDLL(str(_LIB_PATH), mode=getattr(os, 'RTLD_NOW', 2))
+    for name, (args, res) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def dt(t: torch.Tensor | torch.dtype) -> int:
+    d = t if isinstance(t, torch.dtype) else t.dtype
+    if d not in _DT:
+        raise LcqError(f'unsupported dtype {d}')
+    return _DT[d]
+
+
+def ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise LcqError('lightcompress_amd ops run on the GPU only (no CPU fallback); '
+                       f'got a tensor on {t.device}')
+    if not t.is_contiguous():
+        raise LcqError('tensor must be contiguous')
+    return t.data_ptr()
+
+
+def stream_of(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.lcq_last_error().decode(errors='replace')
+        if rc == -1:
+            raise ValueError(msg)
+        raise LcqError(f'{name} failed ({rc}): {msg}')
+    return rc

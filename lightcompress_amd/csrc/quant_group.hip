@@ -1,0 +1,404 @@
+// Grouped integer quantization (fake quant / real quant / vLLM pack) for gfx950.
+//
+// Reference semantics: llmc/compression/quantization/quant.py
+//   get_minmax_range  :132-143   get_qparams :545-559   quant/dequant :699-717
+//   fake_quant_weight_dynamic :833-869   real_quant_weight_dynamic :916-953
+//   fake/real_quant_weight_static :785-831, 871-914
+// and VllmRealQuantLinear.pack (module_utils.py:929-955).
+//
+// Design (HBM-bound streaming, no MFMA): one lane owns 8 consecutive elements (one 16-byte
+// load for bf16/fp16), a group of G elements is G/8 adjacent lanes of one wave, and the group
+// min/max is a butterfly over those lanes (__shfl_xor) -- no LDS, one pass over HBM:
+// read 2 B/elem, write 2 B (fake quant) or 0.5 B (int4 packed) per element.
+// Groups wider than 512 (per-channel rows) use one 256-thread workgroup per group.
+#include "lcq_common.h"
+
+namespace lcq {
+
+struct QuantArgs {
+  const void* x;
+  const void* pre;   // optional [cols] pre-scale (x dtype)
+  const void* cmax;  // optional [ngroups] clip max (x dtype)
+  const void* cmin;  // optional [ngroups] clip min (x dtype); NULL + cmax => -cmax
+  const void* s_in;  // static: scales
+  const void* z_in;  // static: zeros (nullable)
+  int s_dt, z_dt;
+  int64_t rows, cols, group;
+  float qmin, qmax;
+  int sym;
+  void* fq;
+  int fq_dt;
+  void* codes;
+  int codes_dt;
+  void* packed;
+  int pack_bits;
+  void* s_out;
+  void* z_out;
+};
+
+__device__ __forceinline__ float ld_rt(const void* p, int dt, int64_t i) {
+  switch (dt) {
+    case LCQ_F32: return ld1<LCQ_F32>(p, i);
+    case LCQ_BF16: return ld1<LCQ_BF16>(p, i);
+    case LCQ_F16: return ld1<LCQ_F16>(p, i);
+    case LCQ_I32: return ld1<LCQ_I32>(p, i);
+    case LCQ_I8: return ld1<LCQ_I8>(p, i);
+    case LCQ_U8: return ld1<LCQ_U8>(p, i);
+    default: return 0.f;
+  }
+}
+
+// quant.py:545-559 (get_qparams), every op rounded to the compute dtype CT.
+template <int CT>
+__device__ __forceinline__ void qparams(float mn, float mx, float qmin, float qmax, int sym,
+                                        float& s, float& z) {
+  const float lo = rnd<CT>(1e-5f);
+  if (sym) {
+    float am = fmaxf(fabsf(mx), fabsf(mn));
+    am = fmaxf(am, lo);           // .clamp(min=1e-5)
+    s = rnd<CT>(am / qmax);       // abs_max / qmax
+    z = 0.f;
+  } else {
+    float r = rnd<CT>(mx - mn);
+    r = fmaxf(r, lo);
+    s = rnd<CT>(r / (qmax - qmin));
+    float t = rnd<CT>(rintf(rnd<CT>(mn / s)));  // torch.round(min_val / scales)
+    t = rnd<CT>(qmin - t);
+    z = fminf(fmaxf(t, qmin), qmax);              // .clamp(qmin, qmax)
+  }
+}
+
+// quant.py:699-717: q = clamp(round(x/s) + z, qmin, qmax); x^ = (q - z) * s
+template <int CT>
+__device__ __forceinline__ void qdq8(const float (&w)[8], float s, float z, float qmin,
+                                     float qmax, float (&q)[8], float (&dq)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = rintf(rnd<CT>(w[j] / s));
+    t = rnd<CT>(t + z);
+    t = fminf(fmaxf(t, qmin), qmax);
+    q[j] = t;
+    dq[j] = rnd<CT>(rnd<CT>(t - z) * s);
+  }
+}
+
+__device__ __forceinline__ void store_fq8(void* fq, int dt, int64_t e0, const float (&v)[8]) {
+  switch (dt) {
+    case LCQ_F32: st8<LCQ_F32>(fq, e0, v); break;
+    case LCQ_BF16: st8<LCQ_BF16>(fq, e0, v); break;
+    case LCQ_F16: st8<LCQ_F16>(fq, e0, v); break;
+    default: break;
+  }
+}
+
+__device__ __forceinline__ void store_codes8(void* codes, int dt, int64_t e0,
+                                             const float (&q)[8]) {
+  if (dt == LCQ_I32) {
+    int4* p = reinterpret_cast<int4*>(reinterpret_cast<int32_t*>(codes) + e0);
+    p[0] = make_int4((int)q[0], (int)q[1], (int)q[2], (int)q[3]);
+    p[1] = make_int4((int)q[4], (int)q[5], (int)q[6], (int)q[7]);
+  } else {
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lo |= ((uint32_t)((int)q[j]) & 0xffu) << (8 * j);
+      hi |= ((uint32_t)((int)q[4 + j]) & 0xffu) << (8 * j);
+    }
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(codes) + e0) = make_uint2(lo, hi);
+  }
+}
+
+// module_utils.py:929-955: u = uint8(code + 2^(b-1)); packed |= u << (b*i) (uint32)
+__device__ __forceinline__ void store_packed8(void* packed, int bits, int64_t e0,
+                                              const float (&q)[8]) {
+  const uint32_t off = 1u << (bits - 1);
+  uint32_t* p = reinterpret_cast<uint32_t*>(packed);
+  if (bits == 4) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w |= (((uint32_t)((int)q[j]) + off) & 0xffu) << (4 * j);
+    p[e0 >> 3] = w;
+  } else {  // 8
+    uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      w0 |= (((uint32_t)((int)q[j]) + off) & 0xffu) << (8 * j);
+      w1 |= (((uint32_t)((int)q[4 + j]) + off) & 0xffu) << (8 * j);
+    }
+    *reinterpret_cast<uint2*>(p + (e0 >> 2)) = make_uint2(w0, w1);
+  }
+}
+
+template <int CT>
+__device__ __forceinline__ void load_pre_clip(const QuantArgs& a, int64_t e0, int64_t gi,
+                                              float (&w)[8]) {
+  ld8<CT>(a.x, e0, w);
+  if (a.pre) {  // awq.py:39-46 w.mul_(scales.view(1,-1)) in the weight dtype
+    float s[8];
+    ld8<CT>(a.pre, e0 % a.cols, s);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = rnd<CT>(w[j] * s[j]);
+  }
+  if (a.cmax) {  // auto_clip.py:206 torch.clamp(w, min_val, max_val)
+    float mx = ld1<CT>(a.cmax, gi);
+    float mn = a.cmin ? ld1<CT>(a.cmin, gi) : -mx;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = fminf(fmaxf(w[j], mn), mx);
+  }
+}
+
+template <int CT>
+__device__ __forceinline__ void emit(const QuantArgs& a, int64_t e0, const float (&q)[8],
+                                     const float (&dq)[8]) {
+  if (a.fq) store_fq8(a.fq, a.fq_dt, e0, dq);
+  if (a.codes) store_codes8(a.codes, a.codes_dt, e0, q);
+  if (a.packed) store_packed8(a.packed, a.pack_bits, e0, q);
+}
+
+// ---------------------------------------------------------------------------------------
+// dynamic, group of L*8 elements = L adjacent lanes (L in {1..64}, power of two)
+// ---------------------------------------------------------------------------------------
+template <int CT, int L>
+__global__ void __launch_bounds__(256) k_quant_dyn_lanes(QuantArgs a) {
+  const int64_t n8 = a.rows * a.cols / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // all lanes of a group stay in the loop together: n8 is a multiple of L
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
+    const int64_t e0 = t * 8;
+    const int64_t gi = e0 / a.group;
+    float w[8];
+    load_pre_clip<CT>(a, e0, gi, w);
+    float mn = w[0], mx = w[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+      mn = fminf(mn, w[j]);
+      mx = fmaxf(mx, w[j]);
+    }
+#pragma unroll
+    for (int m = L / 2; m >= 1; m >>= 1) {
+      mn = fminf(mn, __shfl_xor(mn, m, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+    }
+    float s, z;
+    qparams<CT>(mn, mx, a.qmin, a.qmax, a.sym, s, z);
+    float q[8], dq[8];
+    qdq8<CT>(w, s, z, a.qmin, a.qmax, q, dq);
+    emit<CT>(a, e0, q, dq);
+    if ((e0 % a.group) == 0) {
+      if (a.s_out) st1<CT>(a.s_out, gi, s);
+      if (a.z_out && !a.sym) st1<CT>(a.z_out, gi, z);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// dynamic, one 256-thread workgroup per (wide) group, e.g. per-channel rows of 4096..28672
+// ---------------------------------------------------------------------------------------
+template <int CT>
+__global__ void __launch_bounds__(256) k_quant_dyn_rows(QuantArgs a) {
+  __shared__ float red[2][4];
+  const int64_t gi = blockIdx.x;
+  const int64_t base = gi * a.group;
+  const int64_t n8 = a.group / 8;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int64_t c = threadIdx.x; c < n8; c += blockDim.x) {
+    float w[8];
+    load_pre_clip<CT>(a, base + c * 8, gi, w);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mn = fminf(mn, w[j]);
+      mx = fmaxf(mx, w[j]);
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, m, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+  }
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wid] = mn;
+    red[1][wid] = mx;
+  }
+  __syncthreads();
+  mn = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
+  mx = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  float s, z;
+  qparams<CT>(mn, mx, a.qmin, a.qmax, a.sym, s, z);
+  for (int64_t c = threadIdx.x; c < n8; c += blockDim.x) {
+    float w[8], q[8], dq[8];
+    load_pre_clip<CT>(a, base + c * 8, gi, w);
+    qdq8<CT>(w, s, z, a.qmin, a.qmax, q, dq);
+    emit<CT>(a, base + c * 8, q, dq);
+  }
+  if (threadIdx.x == 0) {
+    if (a.s_out) st1<CT>(a.s_out, gi, s);
+    if (a.z_out && !a.sym) st1<CT>(a.z_out, gi, z);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// static qparams: element-parallel, compute dtype CT, input dtype XT
+// ---------------------------------------------------------------------------------------
+template <int XT, int CT>
+__global__ void __launch_bounds__(256) k_quant_static(QuantArgs a) {
+  const int64_t n8 = a.rows * a.cols / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
+    const int64_t e0 = t * 8;
+    const int64_t gi = e0 / a.group;
+    float w[8];
+    ld8<XT>(a.x, e0, w);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = rnd<CT>(w[j]);  // .to(compute dtype)
+    const float s = rnd<CT>(ld_rt(a.s_in, a.s_dt, gi));
+    const float z = a.z_in ? rnd<CT>(ld_rt(a.z_in, a.z_dt, gi)) : 0.f;
+    float q[8], dq[8];
+    qdq8<CT>(w, s, z, a.qmin, a.qmax, q, dq);
+    emit<CT>(a, e0, q, dq);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// standalone vLLM pack of integer codes (module_utils.py:929-955), incl. zero padding
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_pack_vllm(const void* codes, int dt, int64_t rows,
+                                                   int64_t cols, int bits, uint32_t* out) {
+  const int pf = 32 / bits;
+  const int64_t pcols = (cols + pf - 1) / pf;
+  const int64_t n = rows * pcols;
+  const uint32_t off = 1u << (bits - 1);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+    const int64_t r = t / pcols, pc = t % pcols;
+    uint32_t w = 0;
+    for (int i = 0; i < pf; ++i) {
+      const int64_t c = pc * pf + i;
+      uint32_t u = 0;  // np.pad(..., constant_values=0) pads AFTER the offset/uint8 step
+      if (c < cols) u = ((uint32_t)(int)ld_rt(codes, dt, r * cols + c) + off) & 0xffu;
+      w |= u << (bits * i);
+    }
+    out[t] = w;
+  }
+}
+
+static bool pow2_le64(int64_t v) { return v >= 1 && v <= 64 && (v & (v - 1)) == 0; }
+
+template <int CT>
+static int launch_dyn(const QuantArgs& a, hipStream_t st) {
+  const int64_t lanes = a.group / 8;
+  const int64_t n8 = a.rows * a.cols / 8;
+  if (pow2_le64(lanes)) {
+    const unsigned grid = stream_grid(n8, 256);
+    switch (lanes) {
+      case 1: hipLaunchKernelGGL((k_quant_dyn_lanes<CT, 1>), grid, 256, 0, st, a); break;
+      case 2: hipLaunchKernelGGL((k_quant_dyn_lanes<CT, 2>), grid, 256, 0, st, a); break;
+      case 4: hipLaunchKernelGGL((k_quant_dyn_lanes<CT, 4>), grid, 256, 0, st, a); break;
+      case 8: hipLaunchKernelGGL((k_quant_dyn_lanes<CT, 8>), grid, 256, 0, st, a); break;
+      case 16: hipLaunchKernelGGL((k_quant_dyn_lanes<CT, 16>), grid, 256, 0, st, a); break;
+      case 32: hipLaunchKernelGGL((k_quant_dyn_lanes<CT, 32>), grid, 256, 0, st, a); break;
+      case 64: hipLaunchKernelGGL((k_quant_dyn_lanes<CT, 64>), grid, 256, 0, st, a); break;
+    }
+  } else {
+    const int64_t ng = a.rows * a.cols / a.group;
+    LCQ_REQUIRE(ng <= 0x7fffffffLL, "too many groups for the row kernel");
+    hipLaunchKernelGGL((k_quant_dyn_rows<CT>), dim3((unsigned)ng), 256, 0, st, a);
+  }
+  return check_launch("lcq_int_quant_dynamic");
+}
+
+template <int XT>
+static int launch_static_x(const QuantArgs& a, int ct, hipStream_t st) {
+  const unsigned grid = stream_grid(a.rows * a.cols / 8, 256);
+  switch (ct) {
+    case LCQ_F32: hipLaunchKernelGGL((k_quant_static<XT, LCQ_F32>), grid, 256, 0, st, a); break;
+    case LCQ_BF16: hipLaunchKernelGGL((k_quant_static<XT, LCQ_BF16>), grid, 256, 0, st, a); break;
+    case LCQ_F16: hipLaunchKernelGGL((k_quant_static<XT, LCQ_F16>), grid, 256, 0, st, a); break;
+    default: return fail(LCQ_EINVAL, "lcq_int_quant_static: bad compute dtype");
+  }
+  return check_launch("lcq_int_quant_static");
+}
+
+static int common_checks(const char* fn, int x_dtype, int64_t rows, int64_t cols,
+                         int64_t& group, int qmin, int qmax, void* fq_out, int fq_dtype,
+                         void* codes_out, int codes_dtype, void* packed_out, int pack_bits) {
+  std::string f(fn);
+  if (!is_float_dt(x_dtype)) return fail(LCQ_EINVAL, f + ": x dtype must be f32/f16/bf16");
+  if (rows <= 0 || cols <= 0) return fail(LCQ_EINVAL, f + ": empty tensor");
+  if (group <= 0) group = cols;
+  if (cols % group != 0) return fail(LCQ_EINVAL, f + ": cols not divisible by group size");
+  if (group % 8 != 0) return fail(LCQ_EINVAL, f + ": group size must be a multiple of 8");
+  if (qmax <= qmin) return fail(LCQ_EINVAL, f + ": qmax <= qmin");
+  if (fq_out && !is_float_dt(fq_dtype)) return fail(LCQ_EINVAL, f + ": bad fq dtype");
+  if (codes_out && !is_code_dt(codes_dtype)) return fail(LCQ_EINVAL, f + ": bad codes dtype");
+  if (packed_out && pack_bits != 4 && pack_bits != 8)
+    return fail(LCQ_EUNSUP, f + ": pack_bits must be 4 or 8");
+  return 0;
+}
+
+}  // namespace lcq
+
+using namespace lcq;
+
+extern "C" int lcq_int_quant_dynamic(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                                     int64_t group, const void* pre_scale, const void* clip_max,
+                                     const void* clip_min, int qmin, int qmax, int sym,
+                                     void* fq_out, int fq_dtype, void* codes_out,
+                                     int codes_dtype, void* packed_out, int pack_bits,
+                                     void* scales_out, void* zeros_out, void* stream) {
+  int rc = common_checks("lcq_int_quant_dynamic", x_dtype, rows, cols, group, qmin, qmax,
+                         fq_out, fq_dtype, codes_out, codes_dtype, packed_out, pack_bits);
+  if (rc) return rc;
+  QuantArgs a{};
+  a.x = x; a.pre = pre_scale; a.cmax = clip_max; a.cmin = clip_min;
+  a.rows = rows; a.cols = cols; a.group = group;
+  a.qmin = (float)qmin; a.qmax = (float)qmax; a.sym = sym;
+  a.fq = fq_out; a.fq_dt = fq_dtype; a.codes = codes_out; a.codes_dt = codes_dtype;
+  a.packed = packed_out; a.pack_bits = pack_bits; a.s_out = scales_out; a.z_out = zeros_out;
+  hipStream_t st = as_stream(stream);
+  switch (x_dtype) {
+    case LCQ_F32: return launch_dyn<LCQ_F32>(a, st);
+    case LCQ_BF16: return launch_dyn<LCQ_BF16>(a, st);
+    default: return launch_dyn<LCQ_F16>(a, st);
+  }
+}
+
+extern "C" int lcq_int_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                                    int64_t group, const void* scales, int s_dtype,
+                                    const void* zeros, int z_dtype, int ct_dtype, int qmin,
+                                    int qmax, void* fq_out, int fq_dtype, void* codes_out,
+                                    int codes_dtype, void* packed_out, int pack_bits,
+                                    void* stream) {
+  int rc = common_checks("lcq_int_quant_static", x_dtype, rows, cols, group, qmin, qmax,
+                         fq_out, fq_dtype, codes_out, codes_dtype, packed_out, pack_bits);
+  if (rc) return rc;
+  LCQ_REQUIRE(scales != nullptr, "scales required");
+  LCQ_REQUIRE(is_float_dt(s_dtype), "scales dtype must be float");
+  LCQ_REQUIRE(zeros == nullptr || is_float_dt(z_dtype) || is_code_dt(z_dtype),
+              "bad zeros dtype");
+  LCQ_REQUIRE(is_float_dt(ct_dtype), "compute dtype must be float");
+  QuantArgs a{};
+  a.x = x; a.s_in = scales; a.s_dt = s_dtype; a.z_in = zeros; a.z_dt = z_dtype;
+  a.rows = rows; a.cols = cols; a.group = group;
+  a.qmin = (float)qmin; a.qmax = (float)qmax; a.sym = zeros == nullptr;
+  a.fq = fq_out; a.fq_dt = fq_dtype; a.codes = codes_out; a.codes_dt = codes_dtype;
+  a.packed = packed_out; a.pack_bits = pack_bits;
+  hipStream_t st = as_stream(stream);
+  switch (x_dtype) {
+    case LCQ_F32: return launch_static_x<LCQ_F32>(a, ct_dtype, st);
+    case LCQ_BF16: return launch_static_x<LCQ_BF16>(a, ct_dtype, st);
+    default: return launch_static_x<LCQ_F16>(a, ct_dtype, st);
+  }
+}
+
+extern "C" int lcq_pack_vllm(const void* codes, int codes_dtype, int64_t rows, int64_t cols,
+                             int bits, void* packed_out, void* stream) {
+  LCQ_REQUIRE(is_code_dt(codes_dtype), "codes dtype must be int8/uint8/int32");
+  LCQ_REQUIRE(bits >= 1 && bits <= 8 && 32 % bits == 0, "bits must divide 32 and be <= 8");
+  LCQ_REQUIRE(rows > 0 && cols > 0, "empty tensor");
+  const int pf = 32 / bits;
+  const int64_t n = rows * ((cols + pf - 1) / pf);
+  hipLaunchKernelGGL(k_pack_vllm, stream_grid(n, 256), 256, 0, as_stream(stream), codes,
+                     codes_dtype, rows, cols, bits, reinterpret_cast<uint32_t*>(packed_out));
+  return check_launch("lcq_pack_vllm");
+}

@@ -1,0 +1,260 @@
+"""Linear wrappers and real-quant packers (drop-in for llmc ``module_utils``).
+
+Same class names, ``new(...)`` constructors, buffer names and pack layouts as the reference
+(module_utils.py:679-1231); packing runs on the device through ``liblcq.so`` instead of the
+reference's CPU numpy loop (vLLM) and per-column Python loop (AutoAWQ).
+"""
+from __future__ import annotations
+
+from functools import partial
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+
+def _fname(fn):
+    if fn is None:
+        return 'None'
+    return fn.func.__name__ if isinstance(fn, partial) else getattr(fn, '__name__', str(fn))
+
+
+class FakeQuantLinear(nn.Module):
+    """module_utils.py:679-771 — weight fake-quantised lazily on first forward (w_qdq)."""
+
+    def __init__(self, weight, bias, ori_module, w_qdq, a_qdq):
+        super().__init__()
+        self.register_buffer('weight', weight)
+        if bias is not None:
+            self.register_buffer('bias', bias)
+        else:
+            self.bias = None
+        self.a_qdq, self.w_qdq = a_qdq, w_qdq
+        for name, buf in list(ori_module.named_buffers()) + list(ori_module.named_parameters()):
+            if name.startswith('buf_'):
+                self.register_buffer(name, buf.data)
+        self.buf_rotate = False
+        self.dynamic_quant_weight = False
+        self.dynamic_quant_tmp_weight = False
+
+    def forward(self, x):
+        if self.a_qdq is not None:
+            x = self.a_qdq(x, self)
+        if not hasattr(self, 'tmp_weight'):
+            self.register_buffer('tmp_weight', self.w_qdq(self), persistent=False)
+            self.tmp_bias = self.bias
+        elif self.dynamic_quant_weight:
+            self.tmp_weight = self.w_qdq(self)
+            self.tmp_bias = self.bias
+        elif self.dynamic_quant_tmp_weight:
+            self.tmp_weight = self.w_qdq(self)
+        return F.linear(x, self.tmp_weight, self.tmp_bias)
+
+    @classmethod
+    @torch.no_grad()
+    def new(cls, module, w_qdq, a_qdq):
+        bias = module.bias.data if getattr(module, 'bias', None) is not None else None
+        m = cls(module.weight.data, bias, ori_module=module, w_qdq=w_qdq, a_qdq=a_qdq)
+        m.in_features, m.out_features = module.in_features, module.out_features
+        m.w_qdq_name, m.a_qdq_name = _fname(w_qdq), _fname(a_qdq)
+        return m
+
+    def __repr__(self):
+        return (f'FakeQuantLinear(in_features={self.in_features},out_features={self.out_features},'
+                f' bias={self.bias is not None},weight_quant={self.w_qdq_name},'
+                f'act_quant={self.a_qdq_name})')
+
+
+class EffcientFakeQuantLinear(nn.Module):
+    """module_utils.py:774-852 — weight fake-quantised once at construction (deploy)."""
+
+    def __init__(self, weight, bias, ori_module, a_qdq):
+        super().__init__()
+        self.register_buffer('weight', weight)
+        if bias is not None:
+            self.register_buffer('bias', bias)
+        else:
+            self.bias = None
+        self.a_qdq = a_qdq
+        for name, buf in ori_module.named_buffers():
+            if name.startswith('buf_'):
+                self.register_buffer(name, buf.data)
+        self.buf_rotate = False
+
+    @torch.no_grad()
+    def forward(self, x):
+        if self.a_qdq is not None:
+            x = self.a_qdq(x, self)
+        return F.linear(x, self.weight, self.bias)
+
+    @classmethod
+    @torch.no_grad()
+    def new(cls, module, w_qdq, a_qdq, debug_print={}):
+        weight = w_qdq(module)
+        bias = module.bias.data if module.bias is not None else None
+        m = cls(weight, bias, ori_module=module, a_qdq=a_qdq)
+        m.in_features, m.out_features = module.in_features, module.out_features
+        m.w_qdq_name, m.a_qdq_name = _fname(w_qdq), _fname(a_qdq)
+        m.debug_print = debug_print
+        return m
+
+
+class OriginFloatLinear(nn.Module):
+    """module_utils.py OriginFloatLinear: keeps the float (transformed) weight."""
+
+    def __init__(self, weight, bias, ori_module):
+        super().__init__()
+        self.register_buffer('weight', weight)
+        if bias is not None:
+            self.register_buffer('bias', bias)
+        else:
+            self.bias = None
+        for name, buf in ori_module.named_buffers():
+            if name.startswith('buf_'):
+                self.register_buffer(name, buf.data)
+
+    @torch.no_grad()
+    def forward(self, x):
+        return F.linear(x, self.weight, self.bias)
+
+    @classmethod
+    @torch.no_grad()
+    def new(cls, module):
+        bias = module.bias.data if module.bias is not None else None
+        m = cls(module.weight.data, bias, module)
+        m.in_features, m.out_features = module.in_features, module.out_features
+        return m
+
+
+class VllmRealQuantLinear(nn.Module):
+    """module_utils.py:855-955 — vLLM compressed-tensors int layout."""
+
+    def __init__(self, weight, bias, scales, input_scale, need_pack, scales_name):
+        super().__init__()
+        self.register_buffer('weight_packed' if need_pack else 'weight', weight)
+        if bias is not None:
+            self.register_buffer('bias', bias)
+        else:
+            self.bias = None
+        self.register_buffer(scales_name, scales)
+        self.register_buffer('input_scale', input_scale)
+
+    @torch.no_grad()
+    def forward(self, x):
+        raise NotImplementedError
+
+    @classmethod
+    @torch.no_grad()
+    def new(cls, module, w_q, quant_config):
+        weight, scales = cls.quant_pack(module, w_q, quant_config)
+        input_scale = getattr(module, 'buf_act_scales_0', None)
+        bias = module.bias.data if module.bias is not None else None
+        need_pack = quant_config['weight'].get('need_pack', False)
+        scales_name = ('weight_scale_inv' if quant_config['weight']['granularity'] == 'per_block'
+                       else 'weight_scale')
+        m = cls(weight, bias, scales, input_scale, need_pack, scales_name)
+        m.in_features, m.out_features = module.in_features, module.out_features
+        m.weight_shape, m.weight_dtype = weight.shape, weight.dtype
+        m.scales_shape, m.scales_dtype = scales.shape, scales.dtype
+        m.zeros_shape = m.zeros_dtype = None
+        return m
+
+    @classmethod
+    @torch.no_grad()
+    def quant_pack(cls, module, w_q, quant_config):
+        weight, scales, zeros = w_q(module)
+        if quant_config['weight'].get('need_pack', False):
+            weight, scales = cls.pack(weight, scales, quant_config)
+        return weight, scales
+
+    @classmethod
+    @torch.no_grad()
+    def pack(cls, weight, scales, quant_config):
+        """Device pack: int32 [rows, ceil(cols*b/32)], scales -> fp16 (module_utils.py:929-955)."""
+        bits = quant_config['weight']['bit']
+        return ops.pack_vllm(weight.contiguous(), bits), scales.to(torch.float16)
+
+
+class SglRealQuantLinear(VllmRealQuantLinear):
+    pass
+
+
+class LightllmRealQuantLinear(VllmRealQuantLinear):
+    pass
+
+
+class Lightx2vRealQuantLinear(VllmRealQuantLinear):
+    pass
+
+
+class AutoawqRealQuantLinear(nn.Module):
+    """module_utils.py:1025-1158 — AutoAWQ GEMM layout (qweight [IC, OC/8])."""
+
+    def __init__(self, weight, bias, scales, zeros):
+        super().__init__()
+        self.register_buffer('qweight', weight)
+        if bias is not None:
+            self.register_buffer('bias', bias)
+        else:
+            self.bias = None
+        self.register_buffer('scales', scales)
+        if zeros is not None:
+            self.register_buffer('qzeros', zeros)
+        else:
+            self.qzeros = None
+
+    @torch.no_grad()
+    def forward(self, x):
+        raise NotImplementedError
+
+    @classmethod
+    @torch.no_grad()
+    def new(cls, module, w_q, quant_config):
+        weight, scales, zeros = cls.quant_pack(module, w_q, quant_config)
+        bias = module.bias.data if module.bias is not None else None
+        m = cls(weight, bias, scales, zeros)
+        m.in_features, m.out_features = module.in_features, module.out_features
+        m.weight_shape, m.weight_dtype = weight.shape, weight.dtype
+        m.scales_shape, m.scales_dtype = scales.shape, scales.dtype
+        m.zeros_shape = zeros.shape if zeros is not None else None
+        m.zeros_dtype = zeros.dtype if zeros is not None else None
+        return m
+
+    @classmethod
+    @torch.no_grad()
+    def quant_pack(cls, module, w_q, quant_config):
+        _, scales, zeros = w_q(module)
+        if quant_config['weight']['pack_version'] != 'gemm_pack':
+            raise NotImplementedError(f"Not support {quant_config['weight']['pack_version']}.")
+        return cls.gemm_pack(module, module.weight.data, scales, zeros, quant_config)
+
+    @classmethod
+    @torch.no_grad()
+    def gemm_pack(cls, module, weight, scales, zeros, quant_config):
+        assert scales is not None and zeros is not None
+        bit = quant_config['weight']['bit']
+        if bit != 4:
+            raise NotImplementedError('Only 4-bit are supported for now.')
+        return ops.pack_autoawq_gemm(weight.contiguous(), scales, zeros,
+                                     quant_config['weight']['group_size'], bit)
+
+
+class MlcllmRealQuantLinear(AutoawqRealQuantLinear):
+    pass
+
+
+_REALQUANT_LINEAR_MAP_ = {
+    'vllm_quant': VllmRealQuantLinear,
+    'lightllm_quant': LightllmRealQuantLinear,
+    'sgl_quant': SglRealQuantLinear,
+    'autoawq_quant': AutoawqRealQuantLinear,
+    'mlcllm_quant': MlcllmRealQuantLinear,
+    'lightx2v_quant': Lightx2vRealQuantLinear,
+}
+
+_LLMC_LINEAR_TYPES_ = [OriginFloatLinear, FakeQuantLinear, EffcientFakeQuantLinear,
+                       VllmRealQuantLinear, SglRealQuantLinear, AutoawqRealQuantLinear,
+                       MlcllmRealQuantLinear, LightllmRealQuantLinear, Lightx2vRealQuantLinear]
+_TRANSFORMERS_LINEAR_TYPES_ = [nn.Linear]

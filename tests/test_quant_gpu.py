@@ -1,0 +1,129 @@
+"""GPU parity: HIP grouped quant / pack kernels vs golden vectors and vs the oracle.
+
+Bar: bit-exact (codes, packed words, bf16/fp16/fp32 scales, zeros, fake-quant values).
+"""
+import numpy as np
+import pytest
+import torch
+
+import fixtures as F
+from oracle import quant_ref as Q
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(t):
+    t = t.detach().cpu()
+    if t.dtype in (torch.bfloat16, torch.float16):
+        return t.view(torch.int16)
+    if t.dtype == torch.float32:
+        return t.view(torch.int32)
+    return t
+
+
+def assert_bit_equal(got, exp, what=''):
+    assert got.dtype == exp.dtype, (what, got.dtype, exp.dtype)
+    assert tuple(got.shape) == tuple(exp.shape), (what, got.shape, exp.shape)
+    g, e = _bits(got), _bits(exp)
+    n = (g != e).sum().item()
+    assert n == 0, f'{what}: {n} / {g.numel()} elements differ'
+
+
+@pytest.mark.parametrize('name', F.names('quant_int'))
+def test_golden_dynamic(dev, name):
+    from lightcompress_amd.quant import IntegerQuantizer
+    from lightcompress_amd.module_utils import VllmRealQuantLinear
+    c = F.load(name)
+    bit, sym, gs, qmin, qmax = c['meta'].tolist()
+    gran = 'per_channel' if 'pc' in name else 'per_group'
+    kw = {'group_size': gs} if gran == 'per_group' else {}
+    wq = IntegerQuantizer(bit, bool(sym), gran, **kw)
+    w = c['w'].to(dev)
+    assert_bit_equal(wq.fake_quant_weight_dynamic(w), c['fq'], 'fq')
+    codes, s, z = wq.real_quant_weight_dynamic(w)
+    assert_bit_equal(codes, c['codes'], 'codes')
+    assert_bit_equal(s, c['scales'], 'scales')
+    if sym:
+        assert z is None
+    else:
+        assert_bit_equal(z, c['zeros'], 'zeros')
+    if 'packed' in c:
+        packed, s16 = VllmRealQuantLinear.pack(codes, s, {'weight': {'bit': bit}})
+        assert_bit_equal(packed, c['packed'], 'packed')
+        assert_bit_equal(s16, c['scales_fp16'], 'scales fp16')
+    _, s2, z2, _, _ = wq.get_tensor_qparams(w)
+    assert_bit_equal(s2.view(s.shape), c['scales'], 'get_tensor_qparams scales')
+
+
+def test_golden_prescale(dev):
+    from lightcompress_amd import ops
+    c = F.load('quant_awq_prescale_int4_sym_g128_bf16')
+    r = ops.int_quant_dynamic(c['w'].to(dev), 128, -8, 7, True, pre_scale=c['pre'].to(dev))
+    assert_bit_equal(r['fq'], c['fq'], 'awq prescale fq')
+
+
+@pytest.mark.parametrize('sym', [True, False])
+def test_golden_clip(dev, sym):
+    from lightcompress_amd import ops
+    c = F.load(f'quant_clip_int4_{"sym" if sym else "asym"}_g128_bf16')
+    qmin, qmax = (-8, 7) if sym else (0, 15)
+    r = ops.int_quant_dynamic(c['w'].to(dev), 128, qmin, qmax, sym,
+                              clip_max=c['cmax'].reshape(-1).to(dev),
+                              clip_min=c['cmin'].reshape(-1).to(dev))
+    assert_bit_equal(r['fq'], c['fq'], 'clip fq')
+
+
+def test_golden_static(dev):
+    from lightcompress_amd.quant import IntegerQuantizer
+    c = F.load('quant_static_int4_asym_g128_f32')
+    wq = IntegerQuantizer(4, False, 'per_group', group_size=128)
+    args = {'scales': c['scales'].to(dev), 'zeros': c['zeros'].to(dev),
+            'qmax': wq.qmax, 'qmin': wq.qmin}
+    fq = wq.fake_quant_weight_static(c['w'].to(dev), args).to(torch.bfloat16)
+    assert_bit_equal(fq, c['fq_bf16'], 'static fq')
+    args['scales'] = args['scales'].to(torch.bfloat16)
+    codes, s, z = wq.real_quant_weight_static(c['w'].to(dev), args)
+    assert_bit_equal(codes, c['codes'], 'static codes')
+    assert_bit_equal(s, c['scales_rq'], 'static scales')
+    assert_bit_equal(z, c['zeros_rq'], 'static zeros')
+
+
+@pytest.mark.parametrize('name', F.names('awqpack_'))
+def test_golden_gemm_pack(dev, name):
+    from lightcompress_amd import ops
+    c = F.load(name)
+    qw, s16, qz = ops.pack_autoawq_gemm(c['w'].to(dev), c['scales'].to(dev),
+                                        c['zeros'].to(dev), 128)
+    assert_bit_equal(qw, c['qweight'], 'qweight')
+    assert_bit_equal(s16, c['scales_t'], 'scales_t')
+    assert_bit_equal(qz, c['qzeros'], 'qzeros')
+
+
+# ---- larger random shapes vs the oracle (Llama-3-8B linear shapes included) -------------
+SHAPES = [(1024, 4096), (4096, 14336), (14336, 4096)]
+
+
+@pytest.mark.parametrize('shape', SHAPES)
+@pytest.mark.parametrize('bit,sym,gran,g', [(4, True, 'per_group', 128),
+                                             (4, False, 'per_group', 128),
+                                             (8, True, 'per_channel', None)])
+def test_random_vs_oracle(dev, shape, bit, sym, gran, g):
+    from lightcompress_amd.quant import IntegerQuantizer
+    gen = torch.Generator().manual_seed(hash((shape, bit, sym)) & 0xffff)
+    w = (torch.randn(*shape, generator=gen) * 0.02).to(torch.bfloat16)
+    kw = {'group_size': g} if g else {}
+    wq = IntegerQuantizer(bit, sym, gran, **kw)
+    fq_ref, _, _ = Q.fake_quant_dynamic(w, bit, sym, gran, g)
+    codes_ref, s_ref, z_ref = Q.real_quant_dynamic(w, bit, sym, gran, g)
+    wd = w.to(dev)
+    assert_bit_equal(wq.fake_quant_weight_dynamic(wd), fq_ref, 'fq')
+    codes, s, z = wq.real_quant_weight_dynamic(wd)
+    assert_bit_equal(codes, codes_ref, 'codes')
+    assert_bit_equal(s, s_ref, 'scales')
+    if not sym:
+        assert_bit_equal(z, z_ref, 'zeros')
+    if bit in (4, 8):
+        from lightcompress_amd import ops
+        r = ops.int_quant_dynamic(wd.reshape(-1, shape[1]), g or shape[1],
+                                  int(wq.qmin), int(wq.qmax), sym, fq=False, pack_bits=bit)
+        assert np.array_equal(r['packed'].cpu().numpy(), Q.pack_vllm(codes_ref, bit))
