@@ -109,6 +109,32 @@ int lcq_pack_autoawq_gemm(const void* w, int w_dtype, int64_t oc, int64_t ic, in
                           void* qweight_out, void* scales_t_out, void* qzeros_out,
                           void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * GPTQ Hessian: H = beta*H + alpha * X^T X   (GPTQ.add_batch, gptq.py:253-295)
+ * x [n, ic] BF16/F16 token-major activations; H [ic, ic] fp32 (kept symmetric).
+ * The reference's per-sample running average maps to beta = n/(n+b),
+ * alpha = fp32(sqrt(2/(n+b)))^2. bf16/fp16 MFMA with fp32 accumulation, upper-triangle tiles
+ * mirrored.
+ * ------------------------------------------------------------------------------------- */
+int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t ic, void* H, float alpha,
+                      float beta, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * GPTQ in-block column loop for one 128-column block (GPTQ.weight_transform, gptq.py:198-244,
+ * group qparams gptq.py:358-366). W [rows, ld] fp32 in (act-order permuted) column space:
+ * columns [col0, col0+count) are replaced by the error-compensated weights (`tmp`);
+ * err [rows, 128] receives Err1 for the caller's trailing update
+ * W[:, col0+count:] -= err @ U[col0:col0+count, col0+count:].
+ * U [ldu, ldu] fp32 upper Cholesky factor of H^-1. group in {32, 64, 128}: per-group minmax
+ * qparams from the block-start weights written to s_out/z_out [rows, ng_total] (fp32);
+ * group == 0: fixed per-row qparams s_in/z_in [rows] (per-channel).
+ * losses optional [rows, ld] fp32: (w-q)^2 / (2 d^2).
+ * ------------------------------------------------------------------------------------- */
+int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, const void* U,
+                   int64_t ldu, int64_t group, int qmin, int qmax, int sym, const void* s_in,
+                   const void* z_in, void* s_out, void* z_out, int64_t ng_total, void* err,
+                   void* losses, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

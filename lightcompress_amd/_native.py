@@ -40,6 +40,9 @@ SIGNATURES = {
     'lcq_pack_vllm': ([_vp, _int, _i64, _i64, _int, _vp, _vp], _int),
     'lcq_pack_autoawq_gemm': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _vp, _vp,
                                _vp, _vp], _int),
+    'lcq_hessian_accum': ([_vp, _int, _i64, _i64, _vp, _f32, _f32, _vp], _int),
+    'lcq_gptq_block': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _int, _int, _int, _vp,
+                        _vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
 }
 
 _lib = None

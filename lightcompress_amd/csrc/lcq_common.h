@@ -59,6 +59,30 @@ __device__ __forceinline__ float rnd(float v) {
   else return v;
 }
 
+// quant.py:545-559 (get_qparams) with every op rounded to the compute dtype CT.
+template <int CT>
+__device__ __forceinline__ void qparams_ct(float mn, float mx, float qmin, float qmax, int sym,
+                                           float& s, float& z) {
+  const float lo = rnd<CT>(1e-5f);
+  if (sym) {
+    float am = fmaxf(fabsf(mx), fabsf(mn));
+    am = fmaxf(am, lo);           // .clamp(min=1e-5)
+    s = rnd<CT>(am / qmax);       // abs_max / qmax
+    z = 0.f;
+  } else {
+    float r = rnd<CT>(mx - mn);
+    r = fmaxf(r, lo);
+    s = rnd<CT>(r / (qmax - qmin));
+    float t = rnd<CT>(rintf(rnd<CT>(mn / s)));  // torch.round(min_val / scales)
+    t = rnd<CT>(qmin - t);
+    z = fminf(fmaxf(t, qmin), qmax);              // .clamp(qmin, qmax)
+  }
+}
+__device__ __forceinline__ void qparams_f32(float mn, float mx, float qmin, float qmax, int sym,
+                                            float& s, float& z) {
+  qparams_ct<LCQ_F32>(mn, mx, qmin, qmax, sym, s, z);
+}
+
 // load/store one element of dtype DT as float
 template <int DT>
 __device__ __forceinline__ float ld1(const void* p, int64_t i) {

@@ -48,26 +48,6 @@ __device__ __forceinline__ float ld_rt(const void* p, int dt, int64_t i) {
   }
 }
 
-// quant.py:545-559 (get_qparams), every op rounded to the compute dtype CT.
-template <int CT>
-__device__ __forceinline__ void qparams(float mn, float mx, float qmin, float qmax, int sym,
-                                        float& s, float& z) {
-  const float lo = rnd<CT>(1e-5f);
-  if (sym) {
-    float am = fmaxf(fabsf(mx), fabsf(mn));
-    am = fmaxf(am, lo);           // .clamp(min=1e-5)
-    s = rnd<CT>(am / qmax);       // abs_max / qmax
-    z = 0.f;
-  } else {
-    float r = rnd<CT>(mx - mn);
-    r = fmaxf(r, lo);
-    s = rnd<CT>(r / (qmax - qmin));
-    float t = rnd<CT>(rintf(rnd<CT>(mn / s)));  // torch.round(min_val / scales)
-    t = rnd<CT>(qmin - t);
-    z = fminf(fmaxf(t, qmin), qmax);              // .clamp(qmin, qmax)
-  }
-}
-
 // quant.py:699-717: q = clamp(round(x/s) + z, qmin, qmax); x^ = (q - z) * s
 template <int CT>
 __device__ __forceinline__ void qdq8(const float (&w)[8], float s, float z, float qmin,
@@ -180,7 +160,7 @@ __global__ void __launch_bounds__(256) k_quant_dyn_lanes(QuantArgs a) {
       mx = fmaxf(mx, __shfl_xor(mx, m, 64));
     }
     float s, z;
-    qparams<CT>(mn, mx, a.qmin, a.qmax, a.sym, s, z);
+    qparams_ct<CT>(mn, mx, a.qmin, a.qmax, a.sym, s, z);
     float q[8], dq[8];
     qdq8<CT>(w, s, z, a.qmin, a.qmax, q, dq);
     emit<CT>(a, e0, q, dq);
@@ -224,7 +204,7 @@ __global__ void __launch_bounds__(256) k_quant_dyn_rows(QuantArgs a) {
   mn = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
   mx = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
   float s, z;
-  qparams<CT>(mn, mx, a.qmin, a.qmax, a.sym, s, z);
+  qparams_ct<CT>(mn, mx, a.qmin, a.qmax, a.sym, s, z);
   for (int64_t c = threadIdx.x; c < n8; c += blockDim.x) {
     float w[8], q[8], dq[8];
     load_pre_clip<CT>(a, base + c * 8, gi, w);

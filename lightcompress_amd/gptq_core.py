@@ -1,0 +1,115 @@
+"""Device GPTQ layer transform (the math of GPTQ.layer_transform, gptq.py:113-244).
+
+Kept separate from the plugin class (``gptq.py``) so the algorithm can be driven per layer
+(tests, bench, multi-GPU row sharding) without a model.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+
+BLOCK = 128
+
+
+class HessianAccumulator:
+    """Running-average Hessian of one linear input (GPTQ.add_batch, gptq.py:253-295).
+
+    ``H_n = H_{n-1} * n_{prev}/n + (2/n) x^T x`` per calibration batch, with the product on
+    MFMA (``lcq_hessian_accum``). Multiple-GPU sample sharding is reconciled by the caller
+    (``gptq.GPTQ``) with one all-reduce per layer instead of one per sample.
+    """
+
+    def __init__(self, ic: int, device):
+        self.H = torch.zeros((ic, ic), dtype=torch.float32, device=device)
+        self.nsamples = 0
+        self.ic = ic
+
+    @torch.no_grad()
+    def add_batch(self, inp: torch.Tensor):
+        if inp.dim() == 2:
+            inp = inp.unsqueeze(0)
+        b = inp.shape[0]
+        x = inp.reshape(-1, inp.shape[-1])
+        if x.dtype not in (torch.bfloat16, torch.float16):
+            x = x.to(torch.bfloat16)  # fp32 activations: bf16 MFMA path (documented tolerance)
+        beta = self.nsamples / (self.nsamples + b)
+        self.nsamples += b
+        c = torch.tensor(math.sqrt(2 / self.nsamples), dtype=torch.float32).item()
+        alpha = float(torch.tensor(c * c, dtype=torch.float32).item())
+        ops.hessian_accum(x, self.H, alpha, beta)
+
+
+@torch.no_grad()
+def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
+    """Dead columns, act-order permutation, damping, Cholesky -> inverse -> upper Cholesky
+    (gptq.py:58-64, 128-176). H is consumed. Returns (W fp32 permuted, U, perm | None)."""
+    perm = torch.argsort(torch.diag(H), descending=True, stable=True) if actorder else None
+    W = W.float().clone()
+    dead = torch.diag(H) == 0
+    if bool(dead.any()):
+        idx = torch.nonzero(dead).flatten()
+        H[idx, idx] = 1
+        W[:, dead] = 0
+    if perm is not None:
+        W = W[:, perm].contiguous()
+        H = H[perm][:, perm]
+    cols = H.shape[0]
+    damp = percdamp * torch.mean(torch.diag(H))
+    d = torch.arange(cols, device=H.device)
+    H[d, d] += damp
+    L = torch.linalg.cholesky(H)
+    Hinv = torch.cholesky_inverse(L)
+    del L
+    U = torch.linalg.cholesky(Hinv, upper=True).contiguous()
+    return W, U, perm
+
+
+@torch.no_grad()
+def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
+                qmin: int, qmax: int, fixed=None, losses: bool = False):
+    """Blocked OBS loop (gptq.py:198-244) on permuted fp32 W, in place.
+
+    Per 128-column block: the HIP kernel runs the in-block sequential loop (bit-exact rank-1
+    updates), then the trailing update ``W[:, i2:] -= Err @ U[i1:i2, i2:]`` (fp32 GEMM)."""
+    rows, cols = W.shape
+    dev = W.device
+    ng = 0 if group is None else -(-cols // group)
+    s_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng else None
+    z_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng and not sym else None
+    err = torch.empty((rows, BLOCK), dtype=torch.float32, device=dev)
+    L = torch.zeros_like(W) if losses else None
+    s_in = z_in = None
+    if group is None:
+        s_in = fixed[0].reshape(-1).float().contiguous()
+        z_in = None if sym else fixed[1].reshape(-1).float().contiguous()
+    for i1 in range(0, cols, BLOCK):
+        i2 = min(i1 + BLOCK, cols)
+        cnt = i2 - i1
+        ops.gptq_block(W, i1, cnt, U, group or 0, qmin, qmax, sym, s_out, z_out, err, L,
+                       s_in, z_in)
+        if i2 < cols:
+            W[:, i2:] -= err[:, :cnt].matmul(U[i1:i2, i2:])
+    return s_out, z_out, L
+
+
+@torch.no_grad()
+def quantize_layer(W: torch.Tensor, H: torch.Tensor, wquantizer, actorder=True,
+                   percdamp=0.01, fixed=None, losses=False):
+    """Full GPTQ transform of one linear. Returns dict(weight fp32 (original column order),
+    scales / zeros [rows*ng, 1] fp32 (merge_qparams order, permuted groups), perm, invperm,
+    loss)."""
+    bit, sym = wquantizer.bit, wquantizer.sym
+    qmin, qmax = int(wquantizer.qmin.item()), int(wquantizer.qmax.item())
+    group = wquantizer.group_size if wquantizer.granularity == 'per_group' else None
+    if group is not None and group not in (32, 64, 128):
+        raise NotImplementedError('device GPTQ supports group_size 32/64/128')
+    Wp, U, perm = prepare(W, H, actorder, percdamp)
+    s, z, L = column_loop(Wp, U, bit, sym, group, qmin, qmax, fixed=fixed, losses=losses)
+    invperm = torch.argsort(perm) if perm is not None else None
+    weight = Wp[:, invperm] if invperm is not None else Wp
+    return dict(weight=weight, scales=None if s is None else s.reshape(-1, 1),
+                zeros=None if z is None else z.reshape(-1, 1), perm=perm, invperm=invperm,
+                loss=None if L is None else L.sum())

@@ -10,7 +10,8 @@ import torch
 
 from . import _native as N
 
-__all__ = ['int_quant_dynamic', 'int_quant_static', 'pack_vllm', 'pack_autoawq_gemm']
+__all__ = ['int_quant_dynamic', 'int_quant_static', 'pack_vllm', 'pack_autoawq_gemm',
+           'hessian_accum', 'gptq_block']
 
 
 def _code_dtype(bit: int, qmin: int) -> torch.dtype:
@@ -140,6 +141,30 @@ def pack_autoawq_gemm(weight: torch.Tensor, scales: torch.Tensor, zeros: torch.T
            N.ptr(scales), N.dt(scales), N.ptr(zeros), int(bits), N.ptr(qweight),
            N.ptr(scales_t), N.ptr(qzeros), N.stream_of(weight))
     return qweight, scales_t, qzeros
+
+
+def hessian_accum(x: torch.Tensor, H: torch.Tensor, alpha: float, beta: float) -> torch.Tensor:
+    """H <- beta*H + alpha * x^T x (in place); x [n, ic] bf16/fp16, H [ic, ic] fp32."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    n, ic = x2.shape
+    if H.dtype != torch.float32 or tuple(H.shape) != (ic, ic):
+        raise ValueError('H must be fp32 [ic, ic]')
+    N.call('lcq_hessian_accum', N.ptr(x2), N.dt(x2), n, ic, N.ptr(H), float(alpha),
+           float(beta), N.stream_of(x2))
+    return H
+
+
+def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: int,
+               qmin: int, qmax: int, sym: bool, s_out, z_out, err: torch.Tensor,
+               losses=None, s_in=None, z_in=None):
+    """One 128-column GPTQ block in place on fp32 W (see include/lcq.h lcq_gptq_block)."""
+    rows, ld = W.shape
+    ng_total = s_out.shape[1] if s_out is not None else 0
+    N.call('lcq_gptq_block', N.ptr(W), rows, ld, int(col0), int(count), N.ptr(U), U.shape[1],
+           int(group), int(qmin), int(qmax), int(sym), N.ptr(s_in), N.ptr(z_in), N.ptr(s_out),
+           N.ptr(z_out), int(ng_total), N.ptr(err), N.ptr(losses), N.stream_of(W))
 
 
 code_dtype = _code_dtype

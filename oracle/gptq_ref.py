@@ -1,0 +1,116 @@
+"""ORACLE (test infrastructure only) — GPTQ layer algorithm, CPU restatement.
+
+Follows llmc/compression/quantization/gptq.py op by op in fp32 torch-CPU:
+Hessian running average (add_batch :253-295, world_size 1), act-order permutation
+(hessian_sorting :58-64), dead columns + damping + Cholesky chain (process_hessian_and_weights
+:128-176), blocked OBS column loop with per-group min/max qparams from the block-start weights
+(weight_transform :198-244, search_column_qparams :358-366), inverse permutation and merged
+group qparams (update_layer_with_transformed_weights :178-196, merge_qparams :344-356).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import quant_ref as Q
+
+
+def hessian(samples, ic: int):
+    """gptq.py:253-295 — running average over per-sample batches; returns (H, nsamples)."""
+    H = torch.zeros((ic, ic))
+    n = 0
+    for inp in samples:
+        if inp.dim() == 2:
+            inp = inp.unsqueeze(0)
+        b = inp.shape[0]
+        x = inp.reshape(-1, inp.shape[-1]).t()
+        H *= n / (n + b)
+        n += b
+        x = math.sqrt(2 / n) * x.float()
+        H += x.matmul(x.t())
+    return H, n
+
+
+def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
+    """gptq.py:58-64, 128-176. Returns (W fp32 permuted, U upper chol of H^-1, perm|None)."""
+    H = H.clone()
+    perm = torch.argsort(torch.diag(H), descending=True) if actorder else None
+    W = W.clone().float()
+    dead = torch.diag(H) == 0
+    H[dead, dead] = 1
+    W[:, dead] = 0
+    if perm is not None:
+        W = W[:, perm]
+        H = H[perm][:, perm]
+    cols = H.shape[0]
+    damp = percdamp * torch.mean(torch.diag(H))
+    d = torch.arange(cols)
+    H[d, d] += damp
+    H = torch.linalg.cholesky(H)
+    H = torch.cholesky_inverse(H)
+    U = torch.linalg.cholesky(H, upper=True)
+    return W, U, perm
+
+
+def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
+                blocksize: int = 128, fixed=None):
+    """gptq.py:198-244 on permuted fp32 W (modified in place to the compensated weights).
+
+    group=None with fixed=(scale[rows,1], zero) -> per-channel fixed qparams.
+    Returns (tmp, Losses, scales [rows, ng], zeros [rows, ng] | None)."""
+    qmin, qmax = Q.int_range(bit, sym)
+    rows, cols = W.shape
+    Losses = torch.zeros_like(W)
+    tmp = torch.zeros_like(W)
+    groups = {}
+    qp = fixed
+    for i1 in range(0, cols, blocksize):
+        i2 = min(i1 + blocksize, cols)
+        W1, U1 = W[:, i1:i2].clone(), U[i1:i2, i1:i2]
+        tmp1, Err1, L1 = torch.zeros_like(W1), torch.zeros_like(W1), torch.zeros_like(W1)
+        for i in range(i2 - i1):
+            w, d = W1[:, i], U1[i, i]
+            if group is not None and (i1 + i) % group == 0:
+                ct = W[:, i1 + i:min(i1 + i + group, cols)]
+                t = Q.group_view(ct, 'per_group', group)
+                mn, mx = Q.minmax(t)
+                s, z = Q.qparams(mn, mx, qmin, qmax, sym)
+                qp = (s, z)
+                groups[(i1 + i) // group] = qp
+            s, z = qp
+            q = Q.dequant(Q.quant(w.unsqueeze(1), s, z, qmin, qmax), s, z).squeeze(1)
+            tmp1[:, i] = w
+            L1[:, i] = ((w - q) ** 2) / (2 * d ** 2)
+            err1 = (w - q) / d
+            W1[:, i:] -= err1.unsqueeze(1).matmul(U1[i, i:].unsqueeze(0))
+            Err1[:, i] = err1
+        tmp[:, i1:i2], Losses[:, i1:i2] = tmp1, L1
+        W[:, i2:] -= Err1.matmul(U[i1:i2, i2:])
+    if group is None:
+        return tmp, Losses, None, None
+    ng = len(groups)
+    scales = torch.stack([groups[g][0] for g in range(ng)], dim=1).reshape(rows, ng)
+    zeros = None
+    if not sym:
+        zeros = torch.stack([groups[g][1] for g in range(ng)], dim=1).reshape(rows, ng)
+    return tmp, Losses, scales, zeros
+
+
+def quantize_layer(W: torch.Tensor, H: torch.Tensor, bit=4, sym=False, group=128,
+                   actorder=True, percdamp=0.01, blocksize=128):
+    """Whole GPTQ layer transform. Returns dict(weight (fp32, original column order),
+    scales/zeros [rows*ng, 1] (merge_qparams order), perm, invperm, U, loss)."""
+    Wp, U, perm = prepare(W, H, actorder, percdamp)
+    tmp, Losses, s, z = column_loop(Wp, U, bit, sym, group, blocksize)
+    invperm = torch.argsort(perm) if perm is not None else None
+    weight = tmp[:, invperm] if invperm is not None else tmp
+    return dict(weight=weight, scales=s.reshape(-1, 1), zeros=None if z is None else z.reshape(-1, 1),
+                perm=perm, invperm=invperm, U=U, loss=Losses.sum().item())
+
+
+def deploy_fake(weight, scales, zeros, perm, invperm, bit, sym, group, model_dtype):
+    """GPTQ.w_qdq (gptq.py:424-452): static fake quant in permuted space, then invperm."""
+    w = weight[:, perm] if perm is not None else weight
+    out = Q.fake_quant_static(w, scales, zeros, bit, sym, 'per_group', group).to(model_dtype)
+    return out[:, invperm] if invperm is not None else out

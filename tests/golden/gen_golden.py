@@ -116,7 +116,79 @@ def gen_quant():
     print('quant fixtures written')
 
 
-GENERATORS = {'quant': gen_quant}
+def _acts(n_samples, seq, ic, seed, dtype=torch.bfloat16):
+    """Calibration activations with log-normal per-channel magnitudes (outlier channels)."""
+    g = torch.Generator().manual_seed(seed)
+    mag = torch.exp(torch.randn(ic, generator=g))
+    return [(torch.randn(1, seq, ic, generator=g) * mag).to(dtype) for _ in range(n_samples)]
+
+
+def gen_gptq():
+    """Drive the reference GPTQ layer methods (gptq.py) on one linear: Hessian via add_batch,
+    qparams via collect_block_qparams' quantizer call, layer_transform, w_qdq / w_q deploy."""
+    import torch.nn as nn
+    R.init_dist()
+    q = R.quant_module()
+    import llmc.compression.quantization.gptq as gm
+    cases = [
+        # name, oc, ic, bit, sym, group, actorder, dead_cols
+        ('int4_asym_g128_act', 192, 512, 4, False, 128, True, False),
+        ('int4_sym_g128_noact', 128, 384, 4, True, 128, False, False),
+        ('int4_asym_g64_act_dead', 128, 256, 4, False, 64, True, True),
+        ('int8_sym_g128_act', 64, 256, 8, True, 128, True, False),
+    ]
+    for i, (name, oc, ic, bit, sym, gs, act, dead) in enumerate(cases):
+        torch.manual_seed(1000 + i)
+        layer = nn.Linear(ic, oc, bias=False)
+        layer.weight.data = weights(oc, ic, torch.bfloat16, 200 + i, edge=False)
+        xs = _acts(3, 48, ic, 300 + i)
+        if dead:
+            for x in xs:
+                x[..., 5] = 0
+                x[..., 77] = 0
+        obj = gm.GPTQ.__new__(gm.GPTQ)
+        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_group', group_size=gs)
+        obj.dev = torch.device('cpu')
+        obj.model_dtype = torch.bfloat16
+        obj.owq, obj.actorder, obj.static_groups = False, act, False
+        obj.percdamp, obj.blocksize, obj.chunk_num = 0.01, 128, 1
+        obj.true_sequential = True
+        obj.need_perm = act
+        obj.layers_cache = {'l': {}}
+        obj.qparams = {}
+        gm.GPTQ.layer_init(obj, layer, 'l')
+        for x in xs:
+            gm.GPTQ.add_batch(obj, layer, 'l', x, None)
+        H = obj.layers_cache['l']['H'].clone()
+        # collect_block_qparams (base_blockwise_quantization.py:337-365)
+        _, s0, z0, qmax, qmin = obj.wquantizer.get_tensor_qparams(layer.weight.data)
+        layer.register_buffer('buf_scales', s0)
+        layer.register_buffer('buf_zeros', z0)
+        layer.register_buffer('buf_qmax', torch.tensor(qmax))
+        layer.register_buffer('buf_qmin', torch.tensor(qmin))
+        w_in = layer.weight.data.clone()
+        # capture U through process_hessian_and_weights on a copy of the state
+        obj.layers_cache['l']['H'] = H.clone()
+        obj.initialize_qparams_and_prepare_weights(layer, 'l')
+        Wp, U = obj.process_hessian_and_weights(layer, 'l')
+        # fresh transform for the outputs
+        obj.layers_cache['l']['H'] = H.clone()
+        obj.qparams = {}
+        layer.weight.data = w_in.clone()
+        obj.layer_transform(layer, 'l')
+        out = dict(x=torch.cat(xs, 0), w=w_in, H=H, U=U,
+                   perm=getattr(layer, 'buf_perm', None), weight=layer.weight.data.clone(),
+                   scales=layer.buf_scales, zeros=None if sym else layer.buf_zeros,
+                   meta=torch.tensor([bit, int(sym), gs, int(act), oc, ic]))
+        out['fq'] = obj.w_qdq(layer, obj.wquantizer)
+        if not act:
+            codes, s_rq, z_rq = obj.w_q(layer, obj.wquantizer)
+            out.update(codes=codes, scales_rq=s_rq, zeros_rq=z_rq)
+        F.save(f'gptq_{name}', **out)
+    print('gptq fixtures written')
+
+
+GENERATORS = {'quant': gen_quant, 'gptq': gen_gptq}
 
 
 if __name__ == '__main__':
