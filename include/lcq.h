@@ -135,6 +135,46 @@ int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, c
                    const void* z_in, void* s_out, void* z_out, int64_t ng_total, void* err,
                    void* losses, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * AWQ (awq.py) and auto-clip (auto_clip.py) building blocks. dtype = BF16/F16/F32; each op
+ * rounds to dtype like the reference's torch expressions.
+ * ------------------------------------------------------------------------------------- */
+/* Awq.get_act_scale (awq.py:74-85): out[c] = mean_t |x[t, c]|. x [n, c]; workspace holds
+ * splits*c fp64 partial sums (deterministic two-pass reduction). */
+int lcq_absmean_cols(const void* x, int dtype, int64_t n, int64_t c, void* out,
+                     void* workspace, int splits, void* stream);
+
+/* Awq.get_scales, trans_version v2 (awq.py:87-108): s = pow(x, ratio_dt) (exponent already
+ * rounded to dtype by the caller, correctly rounded pow) ; clamp(min=1e-4) ;
+ * s / sqrt(max(s) * min(s)). xmean, out [c]. */
+int lcq_awq_scales(const void* xmean, int dtype, int64_t c, float ratio_dt, void* out,
+                   void* stream);
+
+/* Broadcast scale: out = x * s (op 0) or x / s (op 1), s per column (axis 0, [cols]) or per
+ * row (axis 1, [rows]); in place allowed. Replaces scaling_input / update_input_feat /
+ * scale_ln_fcs / scale_fc_fc / scaling_weight (base_blockwise_quantization.py:631-778,
+ * 880-897; awq.py:39-46). */
+int lcq_scale_bcast(const void* x, int dtype, int64_t rows, int64_t cols, const void* s,
+                    int op, int axis, void* out, void* stream);
+
+/* Awq.calculate_loss (awq.py:134-145): out_f32[slot] = fp32(sum((a-b)_dtype^2)) / n, fp64
+ * partial sums in workspace (nparts doubles). Losses stay on device (no per-ratio sync). */
+int lcq_sq_diff_mean(const void* a, const void* b, int dtype, int64_t n, void* workspace,
+                     int nparts, void* out_f32, int slot, void* stream);
+
+/* AutoClipper.auto_clip_layer, clip v1 (auto_clip.py:83-191) for bf16 weights:
+ * w [oc, ic], x [T, ic] (already token-subsampled), group 128, nsteps shrink steps with
+ * factors[nsteps] = fp32(1 - i/n_grid) (device array). best_max / best_min [oc, ic/128] bf16.
+ * Exact emulation of the reference's bf16 products and sums (VALU, not MFMA). */
+int lcq_auto_clip_search(const void* w, const void* x, int64_t oc, int64_t ic, int64_t T,
+                         int group, int nsteps, const void* factors, int qmin, int qmax,
+                         int sym, int clip_sym, void* best_max, void* best_min, void* stream);
+
+/* AutoClipper.apply_clip, v1 (auto_clip.py:193-212): out = clamp(x, cmin, cmax) per group;
+ * cmin NULL -> -cmax. In place allowed. */
+int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t cols, int64_t group,
+                   const void* cmax, const void* cmin, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

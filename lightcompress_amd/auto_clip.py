@@ -1,0 +1,93 @@
+"""AWQ weight clipping (drop-in for llmc ``quantization/auto_clip.py``, clip_version v1).
+
+``auto_clip_layer`` is one HIP launch per linear (``lcq_auto_clip_search``): the reference
+materialises a [256, T, ng, 128] bf16 broadcast product per shrink step and batch of rows
+(1 GiB at ng=32); the kernel keeps weights in VGPRs and streams token tiles through LDS.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .module_utils import _LLMC_LINEAR_TYPES_, _TRANSFORMERS_LINEAR_TYPES_
+from .utils import world
+
+_LINEAR_TYPES = tuple(_LLMC_LINEAR_TYPES_ + _TRANSFORMERS_LINEAR_TYPES_)
+
+
+class AutoClipper:
+    """auto_clip.py:22-281."""
+
+    def __init__(self, w_only, wquantizer, aquantizer, clip_version, clip_sym, save_clip,
+                 padding_mask):
+        self.wquantizer = wquantizer
+        self.aquantizer = aquantizer
+        self.clip_version = clip_version
+        self.clip_sym = clip_sym
+        self.save_clip = save_clip
+        self.padding_mask = padding_mask
+        self.weight_clips = {}
+        self.w_only = w_only
+        if clip_version != 'v1':
+            raise NotImplementedError('clip_version v2 (learnable) is not on the device path')
+        if not w_only:
+            raise NotImplementedError('auto-clip with activation fake-quant is not on the '
+                                      'device path yet')
+
+    @torch.no_grad()
+    def run(self, block, block_idx, input_feat, n_sample_token):
+        """auto_clip.py:43-81: every block linear except q/k projections."""
+        for n, m in block.named_modules():
+            if not isinstance(m, _LINEAR_TYPES):
+                continue
+            if any(k in n for k in ('q_', 'k_', 'query', 'key', 'Wqkv')):
+                continue
+            feats = input_feat[n]
+            inputs = [torch.cat(feats)] if len(feats) != 1 else feats
+            max_val, min_val = self.auto_clip_layer(block_idx, n, m.weight, inputs,
+                                                    n_sample_token=n_sample_token)
+            _, ws, _ = world()
+            if ws > 1 and dist.is_initialized():
+                dist.all_reduce(max_val, op=dist.ReduceOp.SUM)
+                max_val /= ws
+                dist.all_reduce(min_val, op=dist.ReduceOp.SUM)
+                min_val /= ws
+            self.apply_clip(block_idx, m, min_val, max_val, n)
+
+    @staticmethod
+    def sample_tokens(x: torch.Tensor, n_sample_token):
+        """auto_clip.py:134-147: flatten tokens and keep every step-th one."""
+        x = x.reshape(-1, x.shape[-1])
+        if n_sample_token is None:
+            n_sample_token = min(x.shape[0], 512)
+        step = max(1, x.shape[0] // n_sample_token)
+        return x[0::step].contiguous()
+
+    @torch.no_grad()
+    def auto_clip_layer(self, block_idx, layer_name, w, inputs, n_grid=20, max_shrink=0.5,
+                        n_sample_token=512, eps=0.0):
+        """Returns (best_max_val, best_min_val) shaped [oc, ng, 1] like the reference."""
+        assert w.dim() == 2
+        wq = self.wquantizer
+        group = wq.group_size if wq.granularity == 'per_group' else w.shape[1]
+        if len(inputs) != 1:
+            raise NotImplementedError('auto-clip over several calibration tensors')
+        if w.dtype != torch.bfloat16:
+            raise NotImplementedError('device auto-clip kernel is bf16')
+        x = self.sample_tokens(inputs[0], n_sample_token)
+        qmin, qmax = int(wq.qmin.item()), int(wq.qmax.item())
+        return ops.auto_clip_search(w.data, x, group, int(max_shrink * n_grid), n_grid, qmin,
+                                    qmax, wq.sym, self.clip_sym)
+
+    @torch.no_grad()
+    def apply_clip(self, block_idx, layer, min_val, max_val, layer_name):
+        """auto_clip.py:193-212 (v1): clamp the weight per group in place."""
+        w = layer.weight.data
+        group = w.shape[1] // max_val.shape[1]
+        cmax = max_val.reshape(-1).to(w.dtype)
+        cmin = None if self.clip_sym else min_val.reshape(-1).to(w.dtype)
+        ops.clip_apply(w, group, cmax, cmin, out=w)
+        if self.save_clip:
+            self.weight_clips.setdefault(block_idx, {})[f'{layer_name}.weight_quantizer.'
+                                                        'upbound_factor'] = max_val.cpu()

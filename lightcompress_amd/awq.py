@@ -1,0 +1,145 @@
+"""AWQ (drop-in for llmc ``quantization/awq.py``; trans_version v2, clip v1).
+
+Device design of ``search_scale_subset`` (awq.py:178-278):
+* the calibration input, the original module output and the original weights stay in HBM;
+  the reference copies inputs CPU->GPU per ratio and restores weights from a CPU state dict;
+* per ratio: ``lcq_awq_scales`` (one workgroup), ``lcq_int_quant_dynamic`` with the fused
+  ``W * s`` pre-scale writing into a reusable buffer that the module's weight points to,
+  ``lcq_scale_bcast`` for ``x / s`` into a reusable buffer, the inspect module's own forward,
+  and ``lcq_sq_diff_mean`` writing the loss into a device slot — one host sync per subset
+  instead of one ``.item()`` + ``gc.collect()`` per ratio.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .base_blockwise_quantization import BaseBlockwiseQuantization, is_norm
+from .module_utils import FakeQuantLinear
+from .registry import ALGO_REGISTRY
+
+
+@ALGO_REGISTRY
+class Awq(BaseBlockwiseQuantization):
+    def __init__(self, model, quant_config, input, padding_mask, config):
+        super().__init__(model, quant_config, input, padding_mask, config)
+        special = self.quant_config.get('special', {}) or {}
+        self.trans = special.get('trans', True)
+        self.trans_version = special.get('trans_version', 'v2')
+        self.save_scale = special.get('save_scale', False)
+        self.awq_bs = special.get('awq_bs', None)
+        self.save_mem = special.get('save_mem', True)
+        if self.trans_version != 'v2':
+            raise NotImplementedError('trans_version v1 (weight-scale term) is not on the '
+                                      'device path yet')
+        self.n_grid = 20
+        self.last_search = {}
+
+    # -- awq.py:74-108 ----------------------------------------------------------------------
+    def get_act_scale(self, x):
+        if x.shape[0] == self._bs:
+            return ops.absmean_cols(x)
+        means = [ops.absmean_cols(x[i * self._bs:(i + 1) * self._bs])
+                 for i in range(x.shape[0] // self._bs)]
+        return sum(means) / len(means)
+
+    def get_scales(self, prev_op, x_mean, ratio, out=None):
+        return ops.awq_scales(x_mean, ratio, out=out)
+
+    def inspect_module_forward(self, x, inspect_module, kwargs):
+        if self._bs == x.shape[0]:
+            out = inspect_module(x, **kwargs)
+            return out[0] if isinstance(out, tuple) else out
+        outs = []
+        for i in range(x.shape[0] // self._bs):
+            o = inspect_module(x[i * self._bs:(i + 1) * self._bs], **kwargs)
+            outs.append(o[0] if isinstance(o, tuple) else o)
+        return torch.cat(outs, dim=0)
+
+    def fake_quantize_weight(self, fc, scales, out):
+        """awq.py:147-164: Q(W * s) in the weight dtype, fused in one kernel."""
+        wq = self.wquantizer
+        w = fc.weight.data
+        x2, group = wq._kernel_view(w)
+        ops.int_quant_dynamic(x2, group, int(wq.qmin.item()), int(wq.qmax.item()), wq.sym,
+                              pre_scale=scales.to(w.dtype), qparams=False, out=out)
+        return out
+
+    # -- awq.py:178-278 --------------------------------------------------------------------
+    @torch.no_grad()
+    def search_scale_subset(self, prev_op, layers_dict, input, inspect_module, is_gqa,
+                            subset_kwargs):
+        if is_gqa:
+            raise NotImplementedError('GQA scale transfer is not on the device path')
+        if len(input) != 1:
+            raise NotImplementedError('multiple calibration tensors per subset')
+        x = input[0]
+        self._bs = x.shape[0] if self.awq_bs is None else self.awq_bs
+        kwargs = subset_kwargs[0] if isinstance(subset_kwargs, list) else subset_kwargs
+        layers = list(layers_dict.values())
+        orig_w = [fc.weight.data for fc in layers]
+        qbufs = [torch.empty_like(w) for w in orig_w]
+        x_tmp = torch.empty_like(x)
+        x_mean = self.get_act_scale(x)
+        org_out = self.inspect_module_forward(x, inspect_module, kwargs)
+        all_scales = torch.empty((self.n_grid, x.shape[-1]), dtype=x.dtype, device=x.device)
+        losses = ops.LossBuffer(self.n_grid, x.device)
+        try:
+            for n in range(self.n_grid):
+                ratio = n * 1 / self.n_grid
+                s = self.get_scales(prev_op, x_mean, ratio, out=all_scales[n])
+                for fc, buf in zip(layers, qbufs):
+                    fc.weight.data = self.fake_quantize_weight(fc, s, buf)
+                self.scaling_input(x, s, False, out=x_tmp)
+                xin = x_tmp
+                if not self.w_only:
+                    xin = self.aquantizer.fake_quant_act_dynamic(x_tmp)
+                out = self.inspect_module_forward(xin, inspect_module, kwargs)
+                losses.record(org_out, out, n)
+                for fc, w in zip(layers, orig_w):
+                    fc.weight.data = w
+        finally:
+            for fc, w in zip(layers, orig_w):
+                fc.weight.data = w
+        loss_list = losses.out.tolist()  # the one host sync of the search
+        best_i, best = -1, float('inf')
+        for n, lo in enumerate(loss_list):
+            if lo < best:  # strict: the first minimum wins, as the reference's is_best
+                best, best_i = lo, n
+        self.last_search = {'losses': loss_list, 'best_index': best_i}
+        return all_scales[best_i].clone()
+
+    @torch.no_grad()
+    def block_transform(self, block, input_feat, block_kwargs):
+        if self.trans:
+            super().block_transform(block, input_feat, block_kwargs)
+        if self.weight_clip:
+            n_tok = self.config.get('calib', {}).get('seq_len', None)
+            self.auto_clipper.run(block, self.block_idx, input_feat, n_sample_token=n_tok)
+
+    @torch.no_grad()
+    def subset_transform(self, subset, input_feat, subset_kwargs):
+        """awq.py:298-372."""
+        layers_dict = subset['layers']
+        prev_op = subset['prev_op']
+        input_name = subset['input'][0]
+        inspect_module = subset['inspect']
+        if not subset.get('do_trans', True):
+            return
+        if len(prev_op) == 0 or prev_op[0] is None:
+            return
+        layers = list(layers_dict.values())
+        if isinstance(prev_op[0], (nn.Linear, FakeQuantLinear)):
+            of = prev_op[0].out_features
+            if of not in (layers[0].in_features, 2 * layers[0].in_features,
+                          3 * layers[0].in_features):
+                if self.has_gqa and self.do_gqa_trans:
+                    raise NotImplementedError('do_gqa_trans is not on the device path')
+                return  # 'Cannot apply scale. Do not transform this subset.'
+        elif not is_norm(prev_op[0]):
+            return
+        scale = self.search_scale_subset(prev_op[0], layers_dict, input_feat[input_name],
+                                         inspect_module, False, subset_kwargs)
+        self.apply_scale(scale, prev_op, layers)
+        self.update_input_feat(scale, input_feat, layers_dict, False)

@@ -1,0 +1,352 @@
+"""Block-wise driver + quantization plugin base (drop-in for llmc
+``compression/blockwise_optimization.py`` and ``quantization/base_blockwise_quantization.py``).
+
+Same hook points and call order as the reference (block_opt -> run -> block_transform ->
+subset_transform, true_sequential re-hooking, quant_out forwarding, deploy / save_model) so the
+reference's algorithm subclasses and YAML configs keep working. MI355X-first differences:
+
+* the whole model stays resident in HBM (288 GB holds Llama-3-70B bf16), so there are no
+  per-block ``.cuda()/.cpu()`` round trips;
+* cached linear inputs stay on the device and are shared, not copied, between linears that
+  read the same tensor (q/k/v, gate/up) — the reference keeps one CPU copy per linear;
+* every weight/activation transform (AWQ scaling, clipping, fake/real quant, packing) is a HIP
+  kernel from ``liblcq.so``; block forwards are the model's own torch modules.
+"""
+from __future__ import annotations
+
+import functools
+from collections import defaultdict
+from functools import partial
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import ops
+from .module_utils import (_LLMC_LINEAR_TYPES_, _REALQUANT_LINEAR_MAP_,
+                           _TRANSFORMERS_LINEAR_TYPES_, EffcientFakeQuantLinear,
+                           FakeQuantLinear, OriginFloatLinear)
+from .quant import FloatQuantizer, IntegerQuantizer
+from .utils import world
+
+_LINEAR_TYPES = tuple(_LLMC_LINEAR_TYPES_ + _TRANSFORMERS_LINEAR_TYPES_)
+
+
+def is_norm(m) -> bool:
+    """RMSNorm / LayerNorm of any HF model (the reference registers them per adapter)."""
+    n = type(m).__name__.lower()
+    return isinstance(m, nn.LayerNorm) or n.endswith('rmsnorm') or n.endswith('layernorm')
+
+
+class BlockwiseOpt:
+    """llmc/compression/blockwise_optimization.py:8-114."""
+
+    def __init__(self, model, compress_config, input, padding_mask, config):
+        self.model = model
+        self.blocks = model.get_blocks()
+        self.quant_config = compress_config
+        self.input = input
+        self.padding_mask = padding_mask
+        self.data_free = not input
+        self.config = config
+        self.block_idx = None
+        self.num_blocks = len(self.blocks)
+        if self.input:
+            for kw in input['kwargs']:
+                kw.pop('use_cache', None)
+                if 'past_key_value' in kw:
+                    kw['past_key_value'] = None
+                if 'past_key_values' in kw:
+                    kw['past_key_values'] = None
+            self.n_samples = sum(d.shape[0] for d in input['data'])
+
+    def run_block_loop(self):
+        for i in range(len(self.blocks)):
+            self.block_idx = i
+            self.block_opt(self.blocks[i])
+
+    def cache_input_hook(self, m, x, y, name, feat_dict):
+        # device-resident, shared (no copy): see module docstring
+        inputs = [t.detach() for t in x]
+        if len(inputs) == 1:
+            inp = inputs[0]
+            if inp.dim() == 2:
+                inp = inp.unsqueeze(0)
+            feat_dict[name].append(inp)
+        else:
+            feat_dict[name].append(tuple(inputs))
+
+    def block_opt(self, block):
+        raise NotImplementedError
+
+    def layer_init(self, layer, name=None):
+        pass
+
+    def subset_init(self, subset):
+        pass
+
+    def block_init(self, block):
+        pass
+
+
+class BaseBlockwiseQuantization(BlockwiseOpt):
+    """llmc/compression/quantization/base_blockwise_quantization.py:41-1029 (hot-path part)."""
+
+    def __init__(self, model, quant_config, input, padding_mask, config):
+        super().__init__(model, quant_config, input, padding_mask, config)
+        self.dev = torch.device('cuda', torch.cuda.current_device()) \
+            if torch.cuda.is_available() else torch.device('cpu')
+        self.set_quant_config()
+
+    # ---- weight / activation quant callbacks (:46-82) ---------------------------------------
+    def w_qdq(self, module, wquantizer):
+        args = {'lowbound_factor': getattr(module, 'buf_lowbound_factor', None),
+                'upbound_factor': getattr(module, 'buf_upbound_factor', None)}
+        return wquantizer.fake_quant_weight_dynamic(module.weight, args)
+
+    def w_q(self, module, wquantizer):
+        return wquantizer.real_quant_weight_dynamic(module.weight.data)
+
+    def a_qdq(self, act, module, aquantizer, input_index=0):
+        if self.act_static:
+            args = {k: getattr(module, f'buf_act_{k}_{input_index}', None)
+                    for k in ('scales', 'zeros', 'qmax', 'qmin')}
+            return aquantizer.fake_quant_act_static(act, args)
+        return aquantizer.fake_quant_act_dynamic(act)
+
+    def get_replacement_params(self, mode='fake_quant', w_only=False, name=None):
+        params = {}
+        if mode in ('fake_quant', 'fake_quant_wo_kv'):
+            params['a_qdq'] = None if w_only else partial(self.a_qdq, aquantizer=self.aquantizer)
+            params['w_qdq'] = partial(self.w_qdq, wquantizer=self.wquantizer)
+        elif mode in _REALQUANT_LINEAR_MAP_:
+            params['w_q'] = partial(self.w_q, wquantizer=self.wquantizer)
+            params['quant_config'] = self.quant_config
+        return params
+
+    # ---- config (:133-268) ---------------------------------------------------------------
+    def set_quant_config(self):
+        qc = self.quant_config
+        self.mixed_precision = 'ignored_layers' in self.config
+        self.quant_out = qc.get('quant_out', False)
+        self.tp = qc.get('tp', 1)
+        qc['weight']['tp'] = self.tp
+        qtype = qc['weight'].get('quant_type', 'int-quant')
+        self.weight_quant_module = IntegerQuantizer if qtype == 'int-quant' else FloatQuantizer
+        self.wquantizer = self.weight_quant_module(**qc['weight'])
+        if 'act' in qc:
+            self.w_only = False
+            atype = qc['act'].get('quant_type', 'int-quant')
+            self.act_quant_module = IntegerQuantizer if atype == 'int-quant' else FloatQuantizer
+            qc['act']['tp'] = self.tp
+            self.aquantizer = self.act_quant_module(**qc['act'])
+            self.act_static = qc['act'].get('static', False)
+            if self.act_static:
+                raise NotImplementedError('static activation calibration is not on the device '
+                                          'path yet (SURVEY.md §8f rank 3)')
+        else:
+            self.w_only, self.aquantizer, self.act_static = True, None, False
+        self.quant_kvcache = 'kvcache' in qc
+        if self.quant_kvcache:
+            raise NotImplementedError('kv-cache quantization is out of scope (SURVEY.md §2)')
+        special = qc.get('special', {}) or {}
+        self.true_sequential = special.get('true_sequential', False)
+        self.weight_clip = special.get('weight_clip', False)
+        if self.weight_clip or special.get('search_clip_init', False):
+            from .auto_clip import AutoClipper
+            self.save_clip = special.get('save_clip', False)
+            self.clip_version = special.get('clip_version', 'v1')
+            clip_sym = special.get('clip_sym', self.wquantizer.sym)
+            self.auto_clipper = AutoClipper(w_only=self.w_only, wquantizer=self.wquantizer,
+                                            aquantizer=self.aquantizer,
+                                            clip_version=self.clip_version, clip_sym=clip_sym,
+                                            save_clip=self.save_clip,
+                                            padding_mask=self.padding_mask)
+        self.save_scale = special.get('save_scale', False)
+        self.online_rotate = special.get('online_rotate', False)
+        if self.online_rotate:
+            raise NotImplementedError('online rotation (QuaRot) is out of scope')
+        self.modality = qc.get('modality', 'language')
+        self.set_model_config()
+        self.do_gqa_trans = special.get('do_gqa_trans', False)
+
+    def set_model_config(self):
+        mc = self.model.model_config
+        self.hidden_size = mc.hidden_size
+        self.num_heads = mc.num_attention_heads
+        self.head_dim = getattr(mc, 'head_dim', None) or self.hidden_size // self.num_heads
+        self.intermediate_size = getattr(mc, 'intermediate_size', None)
+        kv = getattr(mc, 'num_key_value_heads', None)
+        if kv is not None:
+            self.num_key_value_heads = kv
+            self.num_key_value_groups = self.num_heads // kv
+            self.has_gqa = self.num_key_value_groups > 1
+        else:
+            self.has_gqa = False
+
+    # ---- block driver (:337-526) -----------------------------------------------------------
+    @torch.no_grad()
+    def collect_block_qparams(self, block):
+        for n, m in self.model.get_block_linears(block).items():
+            _, s, z, qmax, qmin = self.wquantizer.get_tensor_qparams(m.weight.data)
+            m.register_buffer('buf_scales', s.detach())
+            m.register_buffer('buf_zeros', z.detach() if torch.is_tensor(z) else torch.tensor(z))
+            m.register_buffer('buf_qmax', qmax.clone().to(m.weight.device))
+            m.register_buffer('buf_qmin', qmin.clone().to(m.weight.device))
+
+    @torch.no_grad()
+    def block_forward(self, block, input_data=None):
+        if input_data is None:
+            input_data = self.input['data']
+        out = []
+        for i, x in enumerate(input_data):
+            y = block(x, **self.input['kwargs'][i])
+            out.append(y[0] if isinstance(y, tuple) else y)
+        return out
+
+    def block_opt(self, block):
+        named_linears = self.model.get_block_linears(block)
+        extra = self.model.get_extra_modules(block)
+        modules = {**named_linears, **extra}
+        input_feat = defaultdict(list)
+        handles = self.register_hooks(modules, input_feat)
+        self.block_init(block)
+        self.run(block, input_feat, handles)
+        del input_feat
+
+    def register_hooks(self, modules, input_feat):
+        if self.data_free:
+            return []
+        return [m.register_forward_hook(functools.partial(self.cache_input_hook, name=n,
+                                                          feat_dict=input_feat))
+                for n, m in modules.items()]
+
+    def run(self, block, input_feat, handles):
+        if not self.data_free:
+            if self.quant_out:
+                self.block_forward(block)
+            else:
+                self.input['data'] = self.block_forward(block)
+            for h in handles:
+                h.remove()
+            self.block_transform(block, input_feat, self.input['kwargs'])
+        else:
+            self.block_transform(block)
+        if not self.data_free and self.quant_out:
+            self.model.replace_module_block(FakeQuantLinear, block, self.block_idx,
+                                            self.get_replacement_params('fake_quant',
+                                                                        self.w_only))
+            self.input['data'] = self.block_forward(block)
+
+    def block_transform(self, block, input_feat=None, block_kwargs=None):
+        subsets = self.model.get_subsets_in_block(block)
+        for index, subset in enumerate(subsets):
+            if subset.get('has_kwargs', False):
+                if 'sub_keys' in subset:
+                    subset_kwargs = [{k: kw[v] for k, v in subset['sub_keys'].items()}
+                                     for kw in block_kwargs]
+                else:
+                    subset_kwargs = block_kwargs
+            else:
+                subset_kwargs = {}
+            self.subset_transform(subset, input_feat, subset_kwargs)
+            if self.true_sequential and index != len(subsets) - 1:
+                nxt = subsets[index + 1]
+                input_feat.update(self.rehook_next_subset(block, subset, nxt))
+
+    def subset_transform(self, subset, input_feat, subset_kwargs):
+        raise NotImplementedError
+
+    def rehook_next_subset(self, block, subset, next_subset):
+        self.subset_init(next_subset)
+        self.model.replace_module_subset(FakeQuantLinear, block, subset, self.block_idx,
+                                         self.get_replacement_params('fake_quant', self.w_only))
+        feat = defaultdict(list)
+        handles = self.register_hooks(next_subset['layers'], feat)
+        self.block_forward(block)
+        for h in handles:
+            h.remove()
+        return feat
+
+    # ---- scale application (:596-778, 880-897) ------------------------------------------------
+    @torch.no_grad()
+    def apply_scale(self, scales, prev_op, layers):
+        assert len(prev_op) == 1, 'Only support single prev_op.'
+        if isinstance(prev_op[0], _LINEAR_TYPES):
+            assert len(layers) == 1
+            self.scale_fc_fc(prev_op[0], layers[0], scales)
+        elif is_norm(prev_op[0]):
+            self.scale_ln_fcs(prev_op[0], layers, scales)
+        else:
+            raise NotImplementedError(f'prev_op {type(prev_op[0])} not supported yet!')
+
+    @torch.no_grad()
+    def scale_fc_fc(self, fc1, fc2, scales):
+        scales = scales.to(fc1.weight.device)
+        if fc1.out_features == fc2.in_features:
+            if getattr(fc1, 'bias', None) is not None:
+                ops.scale_bcast(fc1.bias.data.view(1, -1), scales.to(fc1.bias.dtype), 'div',
+                                out=fc1.bias.data.view(1, -1))
+            ops.scale_bcast(fc1.weight.data, scales.to(fc1.weight.dtype), 'div', axis=1,
+                            out=fc1.weight.data)
+        elif fc1.out_features == fc2.in_features * 2:
+            half = fc1.weight.data[fc1.weight.data.shape[0] // 2:]
+            ops.scale_bcast(half, scales.to(half.dtype), 'div', axis=1, out=half)
+        else:
+            raise NotImplementedError('fc-fc scaling for this shape is not on the device path')
+        ops.scale_bcast(fc2.weight.data, scales.to(fc2.weight.dtype), 'mul', axis=0,
+                        out=fc2.weight.data)
+
+    @torch.no_grad()
+    def scale_ln_fcs(self, ln, fcs, scales):
+        if not isinstance(fcs, list):
+            fcs = [fcs]
+        scales = scales.to(ln.weight.device).to(ln.weight.dtype)
+        ops.scale_bcast(ln.weight.data.view(1, -1), scales, 'div', out=ln.weight.data.view(1, -1))
+        if getattr(ln, 'bias', None) is not None:
+            ops.scale_bcast(ln.bias.data.view(1, -1), scales, 'div', out=ln.bias.data.view(1, -1))
+        for fc in fcs:
+            ops.scale_bcast(fc.weight.data, scales.to(fc.weight.dtype), 'mul', axis=0,
+                            out=fc.weight.data)
+
+    @torch.no_grad()
+    def scaling_input(self, x, scales, is_gqa=False, out=None):
+        if is_gqa:
+            raise NotImplementedError('GQA scale transfer (do_gqa_trans) is not on the device path')
+        return ops.scale_bcast(x, scales.to(x.dtype), 'div', out=out)
+
+    @torch.no_grad()
+    def update_input_feat(self, scale, input_feat, layers_dict, is_gqa=False):
+        done = {}
+        for name in layers_dict:
+            for i, inp in enumerate(input_feat[name]):
+                key = id(inp)
+                if key not in done:
+                    done[key] = self.scaling_input(inp, scale.to(inp.device), is_gqa)
+                input_feat[name][i] = done[key]
+
+    # ---- deploy / save (:932-1029) ---------------------------------------------------------
+    @torch.no_grad()
+    def deploy(self, quant_format, keep_device=True):
+        mapping = {'origin_float': OriginFloatLinear, 'fake_quant': EffcientFakeQuantLinear,
+                   'fake_quant_wo_kv': EffcientFakeQuantLinear, **_REALQUANT_LINEAR_MAP_}
+        if quant_format not in mapping:
+            raise NotImplementedError(f"Quant format '{quant_format}' is not implemented.")
+        self.model.replace_module_all(mapping[quant_format],
+                                      self.get_replacement_params(quant_format, self.w_only))
+
+    @torch.no_grad()
+    def save_model(self, path):
+        rank, _, _ = world()
+        if rank != 0:
+            return
+        self.model.save_pretrained(path)
+
+
+def all_reduce_mean_(t: torch.Tensor):
+    """all_reduce(SUM) / world_size in place (the reference's statistic averaging)."""
+    _, ws, _ = world()
+    if ws > 1 and dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t /= ws
+    return t

@@ -18,6 +18,7 @@
 namespace lcq {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 typedef _Float16 v8h __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -32,28 +33,19 @@ __device__ __forceinline__ int swz(int r, int c) {
   return r * kRowBytes + chunk * 8 + (c & 3) * 2;
 }
 
+// Operands are assembled with one whole-vector shuffle + bitcast: an element-wise
+// bit_cast repack of the two transposed reads was mis-scheduled by hipcc (ROCm 7.2) into a
+// duplicated first dword (observed in the .s), so keep this form.
 template <bool FP16>
 __device__ __forceinline__ v4f mfma(const v4s (&a)[2], const v4s (&b)[2], v4f c) {
+  const v8s as = __builtin_shufflevector(a[0], a[1], 0, 1, 2, 3, 4, 5, 6, 7);
+  const v8s bs = __builtin_shufflevector(b[0], b[1], 0, 1, 2, 3, 4, 5, 6, 7);
   if constexpr (FP16) {
-    v8h av, bv;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      av[i] = __builtin_bit_cast(_Float16, a[0][i]);
-      av[i + 4] = __builtin_bit_cast(_Float16, a[1][i]);
-      bv[i] = __builtin_bit_cast(_Float16, b[0][i]);
-      bv[i + 4] = __builtin_bit_cast(_Float16, b[1][i]);
-    }
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, as),
+                                                  __builtin_bit_cast(v8h, bs), c, 0, 0, 0);
   } else {
-    v8bf av, bv;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      av[i] = __builtin_bit_cast(__bf16, a[0][i]);
-      av[i + 4] = __builtin_bit_cast(__bf16, a[1][i]);
-      bv[i] = __builtin_bit_cast(__bf16, b[0][i]);
-      bv[i + 4] = __builtin_bit_cast(__bf16, b[1][i]);
-    }
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, as),
+                                                   __builtin_bit_cast(v8bf, bs), c, 0, 0, 0);
   }
 }
 

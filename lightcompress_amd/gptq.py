@@ -1,0 +1,162 @@
+"""GPTQ (drop-in for llmc ``quantization/gptq.py``).
+
+Same plugin hooks as the reference (block_init / subset_init / layer_init, cache_input_hook ->
+add_batch, subset_transform -> layer_transform, w_q / w_qdq with act-order permutation,
+deploy). Device differences: the Hessian update is the MFMA SYRK (``lcq_hessian_accum``),
+the column loop is the HIP in-block kernel + fp32 trailing GEMM, and layers that read the same
+input (q/k/v, gate/up) share one Hessian accumulator instead of accumulating identical copies.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import gptq_core
+from .base_blockwise_quantization import BaseBlockwiseQuantization
+from .module_utils import _LLMC_LINEAR_TYPES_, _TRANSFORMERS_LINEAR_TYPES_
+from .registry import ALGO_REGISTRY
+from .utils import world
+
+_LINEAR_TYPES = tuple(_LLMC_LINEAR_TYPES_ + _TRANSFORMERS_LINEAR_TYPES_)
+
+
+@ALGO_REGISTRY
+class GPTQ(BaseBlockwiseQuantization):
+    def __init__(self, model, quant_config, input, padding_mask, config, modality='language'):
+        super().__init__(model, quant_config, input, padding_mask, config)
+        self.model_dtype = next(self.model.model.parameters()).dtype
+        self.add_quant_config()
+        self.layers_cache = {}
+        self.collect_model_qparams()
+
+    def add_quant_config(self):
+        sp = self.quant_config['special']
+        self.true_sequential = sp['true_sequential']
+        self.static_groups = sp['static_groups']
+        self.actorder = sp['actorder']
+        self.percdamp = sp['percdamp']
+        self.blocksize = sp['blocksize']
+        self.owq = sp.get('owq', False)
+        self.chunk_num = sp.get('chunk_num', 1)
+        if self.owq:
+            raise NotImplementedError('OWQ is not on the device path yet (SURVEY.md §8f)')
+        if self.static_groups:
+            raise NotImplementedError('static_groups is not on the device path yet')
+        if self.blocksize != gptq_core.BLOCK:
+            raise NotImplementedError('device GPTQ uses blocksize 128')
+        self.need_perm = (self.wquantizer.granularity == 'per_group' and not self.static_groups
+                          and self.actorder)
+
+    @torch.no_grad()
+    def collect_model_qparams(self):
+        for block in self.blocks:
+            self.collect_block_qparams(block)
+
+    # ---- Hessian collection (gptq.py:246-322) -------------------------------------------------
+    # The reference keeps one Hessian per linear, each fed by that linear's own hook. Linears of
+    # one subset read the same tensor (q/k/v, gate/up), so their Hessians are identical: here the
+    # subset's input layer (subset['input'][0]) owns one accumulator that its members share.
+    def _init_subset(self, subset):
+        layers = subset['layers']
+        owner = subset['input'][0]
+        acc = None
+        for name, m in layers.items():
+            if acc is None:
+                acc = gptq_core.HessianAccumulator(m.weight.shape[1], m.weight.device)
+            self.layers_cache[name] = {'acc': acc, 'owner': name == owner,
+                                       'columns': m.weight.shape[1]}
+
+    @torch.no_grad()
+    def subset_init(self, subset):
+        self.named_layers = subset['layers']
+        self._init_subset(subset)
+
+    @torch.no_grad()
+    def block_init(self, block):
+        self.named_layers = self.model.get_block_linears(block)
+        subsets = self.model.get_subsets_in_block(block)
+        # with true_sequential the reference re-initialises every later subset's Hessian in
+        # rehook_next_subset, so only the first subset's first-pass Hessian is ever used
+        for subset in (subsets[:1] if self.true_sequential else subsets):
+            self._init_subset(subset)
+
+    @torch.no_grad()
+    def cache_input_hook(self, m, inp, out, name, feat_dict):
+        if isinstance(m, _LINEAR_TYPES):
+            self.add_batch(m, name, inp[0].data, out.data)
+
+    @torch.no_grad()
+    def add_batch(self, layer, name, inp, out):
+        """gptq.py:253-295 (one call per calibration batch, on the owner's hook)."""
+        entry = self.layers_cache.get(name)
+        if entry is None or not entry['owner']:
+            return
+        entry['acc'].add_batch(inp)
+
+    # ---- transform (gptq.py:96-244) -------------------------------------------------------------
+    @torch.no_grad()
+    def subset_transform(self, subset, input_feat, subset_kwargs):
+        for name, layer in subset['layers'].items():
+            if not isinstance(layer, _LINEAR_TYPES):
+                continue
+            self.layer_transform(layer, name)
+            self.free(name)
+
+    @torch.no_grad()
+    def layer_transform(self, layer, name):
+        H = self.layers_cache[name]['acc'].H.clone()  # consumed by prepare(); shared by members
+        _, ws, _ = world()
+        if ws > 1 and dist.is_initialized():
+            # one all-reduce of the finished Hessian per layer (the reference reduces after
+            # every sample); averaging matches its H /= world_size
+            dist.all_reduce(H, op=dist.ReduceOp.SUM)
+            H /= ws
+        fixed = None
+        if self.wquantizer.granularity != 'per_group':
+            fixed = (layer.buf_scales, getattr(layer, 'buf_zeros', None))
+        r = gptq_core.quantize_layer(layer.weight.data, H, self.wquantizer,
+                                     actorder=self.actorder, percdamp=self.percdamp,
+                                     fixed=fixed)
+        layer.weight.data = r['weight']
+        if r['perm'] is not None:
+            layer.register_buffer('buf_perm', r['perm'])
+            layer.register_buffer('buf_invperm', r['invperm'])
+        if r['scales'] is not None:
+            layer.buf_scales = r['scales']
+            if not self.wquantizer.sym:
+                layer.buf_zeros = r['zeros']
+
+    @torch.no_grad()
+    def free(self, name):
+        self.layers_cache.pop(name, None)
+
+    # ---- deploy (gptq.py:411-459) --------------------------------------------------------------
+    @torch.no_grad()
+    def w_q(self, module, wquantizer):
+        args = {'scales': module.buf_scales.to(self.model_dtype), 'zeros': module.buf_zeros,
+                'qmax': module.buf_qmax, 'qmin': module.buf_qmin}
+        return wquantizer.real_quant_weight_static(module.weight.data, args)
+
+    @torch.no_grad()
+    def w_qdq(self, module, wquantizer):
+        weight = module.weight
+        if self.need_perm:
+            weight = module.weight[:, module.buf_perm].contiguous()
+        args = {'scales': module.buf_scales, 'zeros': getattr(module, 'buf_zeros', None),
+                'qmax': module.buf_qmax, 'qmin': module.buf_qmin}
+        weight = wquantizer.fake_quant_weight_static(weight, args).to(self.model_dtype)
+        if self.need_perm:
+            weight = weight[:, module.buf_invperm].contiguous()
+        return weight
+
+    @torch.no_grad()
+    def deploy(self, quant_format, keep_device=True):
+        if quant_format not in ('fake_quant', 'origin_float'):
+            assert not self.need_perm
+        super().deploy(quant_format)
+        self.model.convert_dtype(self.model_dtype)
+
+    @torch.no_grad()
+    def save_model(self, path):
+        self.model.convert_dtype(self.model_dtype)
+        super().save_model(path)

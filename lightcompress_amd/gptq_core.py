@@ -76,6 +76,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     updates), then the trailing update ``W[:, i2:] -= Err @ U[i1:i2, i2:]`` (fp32 GEMM)."""
     rows, cols = W.shape
     dev = W.device
+    U = U.contiguous()
     ng = 0 if group is None else -(-cols // group)
     s_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng else None
     z_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng and not sym else None

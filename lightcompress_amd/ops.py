@@ -11,7 +11,8 @@ import torch
 from . import _native as N
 
 __all__ = ['int_quant_dynamic', 'int_quant_static', 'pack_vllm', 'pack_autoawq_gemm',
-           'hessian_accum', 'gptq_block']
+           'hessian_accum', 'gptq_block', 'absmean_cols', 'awq_scales', 'scale_bcast',
+           'sq_diff_mean', 'auto_clip_search', 'clip_apply']
 
 
 def _code_dtype(bit: int, qmin: int) -> torch.dtype:
@@ -165,6 +166,97 @@ def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: i
     N.call('lcq_gptq_block', N.ptr(W), rows, ld, int(col0), int(count), N.ptr(U), U.shape[1],
            int(group), int(qmin), int(qmax), int(sym), N.ptr(s_in), N.ptr(z_in), N.ptr(s_out),
            N.ptr(z_out), int(ng_total), N.ptr(err), N.ptr(losses), N.stream_of(W))
+
+
+def absmean_cols(x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+    """mean over all leading dims of |x| per channel (Awq.get_act_scale, awq.py:74-85)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    n, c = x2.shape
+    if splits is None:
+        splits = max(1, min(256, n // 64))
+    ws = torch.empty((splits, c), dtype=torch.float64, device=x.device)
+    out = torch.empty((c,), dtype=x.dtype, device=x.device)
+    N.call('lcq_absmean_cols', N.ptr(x2), N.dt(x2), n, c, N.ptr(out), N.ptr(ws), int(splits),
+           N.stream_of(x2))
+    return out
+
+
+def ratio_in_dtype(ratio: float, dtype: torch.dtype) -> float:
+    """The exponent as torch applies it to a `dtype` tensor (rounded to dtype)."""
+    return float(torch.tensor(ratio, dtype=torch.float32).to(dtype).item())
+
+
+def awq_scales(xmean: torch.Tensor, ratio: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    """AWQ v2 scales for one grid ratio (awq.py:87-108)."""
+    out = torch.empty_like(xmean) if out is None else out
+    N.call('lcq_awq_scales', N.ptr(xmean), N.dt(xmean), xmean.numel(),
+           ratio_in_dtype(ratio, xmean.dtype), N.ptr(out), N.stream_of(xmean))
+    return out
+
+
+def scale_bcast(x: torch.Tensor, s: torch.Tensor, op: str, axis: int = 0,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """out = x * s or x / s broadcast over columns (axis 0) or rows (axis 1); in place if
+    out is x. Per-op rounding in x.dtype."""
+    x2 = x.reshape(-1, x.shape[-1])
+    rows, cols = x2.shape
+    if s.dtype != x.dtype:
+        raise ValueError('scale must have the tensor dtype')
+    s = s.contiguous()
+    if s.numel() != (cols if axis == 0 else rows):
+        raise ValueError('scale length does not match the broadcast axis')
+    o = torch.empty_like(x) if out is None else out
+    N.call('lcq_scale_bcast', N.ptr(x2), N.dt(x2), rows, cols, N.ptr(s),
+           0 if op == 'mul' else 1, int(axis), N.ptr(o), N.stream_of(x2))
+    return o
+
+
+class LossBuffer:
+    """Device-resident loss slots + fp64 workspace for lcq_sq_diff_mean (no per-ratio sync)."""
+
+    def __init__(self, slots: int, device, nparts: int = 1024):
+        self.out = torch.zeros((slots,), dtype=torch.float32, device=device)
+        self.ws = torch.empty((nparts,), dtype=torch.float64, device=device)
+        self.nparts = nparts
+
+    def record(self, a: torch.Tensor, b: torch.Tensor, slot: int):
+        a = a.contiguous()
+        b = b.contiguous()
+        N.call('lcq_sq_diff_mean', N.ptr(a), N.ptr(b), N.dt(a), a.numel(), N.ptr(self.ws),
+               self.nparts, N.ptr(self.out), int(slot), N.stream_of(a))
+
+
+def sq_diff_mean(a: torch.Tensor, b: torch.Tensor) -> float:
+    lb = LossBuffer(1, a.device)
+    lb.record(a, b, 0)
+    return float(lb.out[0].item())
+
+
+def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, n_grid: int,
+                     qmin: int, qmax: int, sym: bool, clip_sym: bool):
+    """AutoClipper.auto_clip_layer (v1) on device: returns (best_max, best_min) [oc, ng, 1]."""
+    oc, ic = w.shape
+    T = x.shape[0]
+    factors = torch.tensor([float(1 - i / n_grid) for i in range(nsteps)], dtype=torch.float32,
+                           device=w.device)
+    ng = ic // group
+    bmax = torch.empty((oc, ng, 1), dtype=w.dtype, device=w.device)
+    bmin = torch.empty((oc, ng, 1), dtype=w.dtype, device=w.device)
+    N.call('lcq_auto_clip_search', N.ptr(w.contiguous()), N.ptr(x.contiguous()), oc, ic, T,
+           int(group), int(nsteps), N.ptr(factors), int(qmin), int(qmax), int(sym),
+           int(clip_sym), N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
+    return bmax, bmin
+
+
+def clip_apply(w: torch.Tensor, group: int, cmax: torch.Tensor, cmin: torch.Tensor | None,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    rows, cols = w.shape
+    o = torch.empty_like(w) if out is None else out
+    N.call('lcq_clip_apply', N.ptr(w), N.dt(w), rows, cols, int(group), N.ptr(cmax.contiguous()),
+           N.ptr(cmin.contiguous() if cmin is not None else None), N.ptr(o), N.stream_of(w))
+    return o
 
 
 code_dtype = _code_dtype

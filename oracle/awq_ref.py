@@ -1,0 +1,100 @@
+"""ORACLE (test infrastructure only) — AWQ scale search and auto-clip, CPU restatement.
+
+Follows llmc/compression/quantization/awq.py (trans_version v2, w_only, awq_bs None) and
+auto_clip.py (clip_version v1, w_only) op by op in torch-CPU with the reference's dtypes.
+The inspect module forward (HF Llama attention / MLP / Linear) is the same third-party
+torch module the reference calls.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import quant_ref as Q
+
+
+def act_scale(x: torch.Tensor) -> torch.Tensor:
+    """awq.py:74-85 (batch == _bs)."""
+    return x.abs().view(-1, x.shape[-1]).mean(0)
+
+
+def scales_v2(x_mean: torch.Tensor, ratio: float) -> torch.Tensor:
+    """awq.py:87-108 (trans_version v2, not GQA)."""
+    s = x_mean.pow(ratio).clamp(min=1e-4).view(-1)
+    return s / (s.max() * s.min()).sqrt()
+
+
+def fake_quant_scaled(w: torch.Tensor, s: torch.Tensor, bit, sym, group):
+    """awq.py:39-46 + 147-164: W.mul_(s) then fake_quant_weight_dynamic, weight dtype."""
+    ws = w.clone().mul_(s.view(1, -1))
+    return Q.fake_quant_dynamic(ws, bit, sym, 'per_group', group)[0]
+
+
+def loss(org_out: torch.Tensor, out: torch.Tensor) -> float:
+    """awq.py:134-145."""
+    return (org_out - out).float().pow(2).mean().item()
+
+
+def search_scale(x: torch.Tensor, weights: list, forward, bit, sym, group, n_grid=20):
+    """awq.py:178-278 for one input tensor (len(input)==1, world_size 1).
+
+    ``forward(x, qweights)`` runs the inspect module with the given (fake-quantised) weights.
+    Returns (losses[n_grid], best_index, best_scales)."""
+    x_mean = act_scale(x)
+    org_out = forward(x, None)
+    best, best_i, best_s = float('inf'), -1, None
+    losses = []
+    for n in range(n_grid):
+        ratio = n * 1 / n_grid
+        s = scales_v2(x_mean, ratio)
+        qw = [fake_quant_scaled(w, s, bit, sym, group) for w in weights]
+        out = forward(x / s.view(1, -1), qw)
+        lo = loss(org_out, out)
+        lm = x.shape[0] * 1.0 / x.shape[0] * lo
+        losses.append(lm)
+        if lm < best:
+            best, best_i, best_s = lm, n, x.shape[0] * 1.0 / x.shape[0] * s
+    return losses, best_i, best_s
+
+
+def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_grid=20,
+               max_shrink=0.5, n_sample_token=512):
+    """auto_clip.py:83-191 (clip v1, w_only, single input). Returns (best_max, best_min)
+    shaped [oc, ng, 1]."""
+    w = w.reshape(w.shape[0], 1, -1, group)
+    ocb = 256 if w.shape[0] % 256 == 0 else 64
+    x = x.view(-1, x.shape[-1]).reshape(1, -1, x.shape[-1] // group, group)
+    step = max(1, x.shape[1] // n_sample_token)
+    x = x[:, 0::step]
+    bmx_all, bmn_all = [], []
+    for ib in range(w.shape[0] // ocb):
+        wb = w[ib * ocb:(ib + 1) * ocb]
+        org_max = wb.abs().amax(dim=-1, keepdim=True) if clip_sym else wb.amax(dim=-1, keepdim=True)
+        org_min = wb.amin(dim=-1, keepdim=True)
+        best_max, best_min = org_max.clone(), org_min.clone()
+        min_errs = torch.ones_like(org_max) * 1e9
+        org_out = (x * wb).sum(dim=-1)
+        for i_s in range(int(max_shrink * n_grid)):
+            max_val = org_max * (1 - i_s / n_grid)
+            min_val = -max_val if clip_sym else org_min * (1 - i_s / n_grid)
+            cur = torch.clamp(wb, min_val, max_val)
+            q_w = Q.fake_quant_dynamic(cur, bit, sym, 'per_group', group)[0]
+            cur_out = (x * q_w).sum(dim=-1)
+            err = (cur_out - org_out).pow(2).mean(dim=1).view(min_errs.shape)
+            err_mean = 0 + err
+            err_mean /= 1
+            idx = err_mean < min_errs
+            min_errs[idx] = err_mean[idx]
+            best_max[idx] = max_val[idx]
+            best_min[idx] = min_val[idx]
+        bmx_all.append(best_max)
+        bmn_all.append(best_min)
+    return torch.cat(bmx_all, 0).squeeze(1), torch.cat(bmn_all, 0).squeeze(1)
+
+
+def apply_clip(w: torch.Tensor, max_val, min_val, clip_sym):
+    """auto_clip.py:193-212 (v1)."""
+    shape = w.shape
+    wg = w.reshape(*max_val.shape[:2], -1)
+    if clip_sym:
+        min_val = -max_val
+    return torch.clamp(wg, min_val, max_val).reshape(shape)

@@ -188,7 +188,128 @@ def gen_gptq():
     print('gptq fixtures written')
 
 
-GENERATORS = {'quant': gen_quant, 'gptq': gen_gptq}
+def tiny_llama(seed=0, hidden=256, inter=512, heads=4, kv=2):
+    """A random-init HF Llama decoder layer (bf16) + its rotary embedding, CPU."""
+    from transformers import LlamaConfig
+    from transformers.models.llama import modeling_llama as ml
+    cfg = LlamaConfig(hidden_size=hidden, intermediate_size=inter, num_attention_heads=heads,
+                      num_key_value_heads=kv, num_hidden_layers=1, vocab_size=128,
+                      max_position_embeddings=2048, rms_norm_eps=1e-5)
+    cfg._attn_implementation = 'sdpa'
+    torch.manual_seed(seed)
+    layer = ml.LlamaDecoderLayer(cfg, layer_idx=0)
+    with torch.no_grad():
+        for n, p in layer.named_parameters():
+            if p.dim() == 2:
+                p.normal_(0, 0.02)
+            else:
+                p.uniform_(0.5, 1.5)
+    layer = layer.to(torch.bfloat16).eval()
+    rot = ml.LlamaRotaryEmbedding(cfg)
+    return cfg, layer, rot
+
+
+def _awq_obj(wq, nsamples):
+    import llmc.compression.quantization.awq as am
+    obj = am.Awq.__new__(am.Awq)
+    obj.wquantizer = wq
+    obj.trans_version, obj.awq_bs, obj.save_mem = 'v2', None, True
+    obj.padding_mask, obj.w_only, obj.n_samples = None, True, nsamples
+    obj.losses_seen = []
+    orig = am.Awq.calculate_loss
+
+    def rec(org_out, out, _o=obj):
+        v = orig(_o, org_out, out)
+        _o.losses_seen.append(v)
+        return v
+    obj.calculate_loss = rec
+    return obj
+
+
+def gen_awq():
+    """Reference Awq.search_scale_subset (+ apply_scale) on the three Llama subsets that AWQ
+    transforms (qkv / gate-up / down; o_proj is skipped under GQA) of a tiny bf16 layer."""
+    R.init_dist()
+    q = R.quant_module()
+    cfg, layer, rot = tiny_llama()
+    # base_model.py registers the model's norm class as an LN type (what the adapter does)
+    mu = R.module_utils()
+    if type(layer.input_layernorm) not in mu._TRANSFORMERS_LN_TYPES_:
+        mu._TRANSFORMERS_LN_TYPES_.append(type(layer.input_layernorm))
+    n, seq = 4, 32
+    g = torch.Generator().manual_seed(5)
+    hidden = (torch.randn(n, seq, cfg.hidden_size, generator=g) *
+              torch.exp(torch.randn(cfg.hidden_size, generator=g) * 0.5)).to(torch.bfloat16)
+    pos = torch.arange(seq).unsqueeze(0)
+    cos, sin = rot(hidden, pos)
+    kwargs = {'position_embeddings': (cos, sin), 'attention_mask': None, 'position_ids': pos}
+    for sym in (True, False):
+        wq = q.IntegerQuantizer(4, sym, 'per_group', group_size=128)
+        tag = 'sym' if sym else 'asym'
+        import copy
+        lay = copy.deepcopy(layer)
+        with torch.no_grad():
+            x_qkv = lay.input_layernorm(hidden)
+            attn_out = lay.self_attn(x_qkv, **kwargs)[0]
+            h2 = hidden + attn_out
+            x_mlp = lay.post_attention_layernorm(h2)
+            x_down = lay.mlp.act_fn(lay.mlp.gate_proj(x_mlp)) * lay.mlp.up_proj(x_mlp)
+        subsets = [
+            ('qkv', lay.input_layernorm, {'q': lay.self_attn.q_proj, 'k': lay.self_attn.k_proj,
+                                          'v': lay.self_attn.v_proj}, x_qkv, lay.self_attn, [kwargs]),
+            ('mlp', lay.post_attention_layernorm, {'gate': lay.mlp.gate_proj,
+                                                   'up': lay.mlp.up_proj}, x_mlp, lay.mlp, {}),
+            ('down', lay.mlp.up_proj, {'down': lay.mlp.down_proj}, x_down, lay.mlp.down_proj, {}),
+        ]
+        for name, prev, layers, x, inspect, kw in subsets:
+            obj = _awq_obj(wq, n)
+            w_before = {k: m.weight.data.clone() for k, m in layers.items()}
+            prev_before = prev.weight.data.clone()
+            best = obj.search_scale_subset(prev, layers, [x.clone()], inspect, False, kw)
+            losses = torch.tensor(obj.losses_seen, dtype=torch.float64)
+            obj.num_key_value_heads, obj.has_gqa = cfg.num_key_value_heads, True
+            obj.apply_scale(best, [prev], list(layers.values()))
+            out = dict(x=x, scales=best, losses=losses, prev_w=prev_before,
+                       prev_w_after=prev.weight.data.clone())
+            for k in layers:
+                out[f'w_{k}'] = w_before[k]
+                out[f'w_{k}_after'] = layers[k].weight.data.clone()
+            F.save(f'awq_{name}_{tag}', **out)
+    # layer weights/config for re-building the module on the test side
+    F.save('awq_layer', **{k.replace('.', '__'): v for k, v in layer.state_dict().items()},
+           hidden=hidden, cos=cos, sin=sin,
+           cfg=torch.tensor([cfg.hidden_size, cfg.intermediate_size,
+                             cfg.num_attention_heads, cfg.num_key_value_heads]))
+    print('awq fixtures written')
+
+
+def gen_clip():
+    """Reference AutoClipper.auto_clip_layer (clip v1) + apply_clip on bf16 layers."""
+    R.init_dist()
+    q = R.quant_module()
+    import llmc.compression.quantization.auto_clip as ac
+    cases = [('sym_s', True, True, 128, 256, 512, 64),
+             ('asym_s', False, False, 128, 256, 512, 64),
+             ('sym_w_asym_clip', True, False, 256, 512, 1024, 128)]
+    for i, (name, sym, clip_sym, oc, ic, ntok, nst) in enumerate(cases):
+        wq = q.IntegerQuantizer(4, sym, 'per_group', group_size=128)
+        clipper = ac.AutoClipper(w_only=True, wquantizer=wq, aquantizer=None,
+                                 clip_version='v1', clip_sym=clip_sym, save_clip=False,
+                                 padding_mask=None)
+        w = weights(oc, ic, torch.bfloat16, 400 + i, edge=False)
+        x = _acts(1, ntok, ic, 500 + i)[0]
+        bmax, bmin = clipper.auto_clip_layer(0, 'l', w.clone(), [x.clone()],
+                                             n_sample_token=nst)
+        m = torch.nn.Linear(ic, oc, bias=False).to(torch.bfloat16)
+        m.weight.data = w.clone()
+        clipper.apply_clip(0, m, bmin.clone(), bmax.clone(), 'l')
+        F.save(f'clip_{name}', w=w, x=x, best_max=bmax, best_min=bmin,
+               w_clipped=m.weight.data.clone(),
+               meta=torch.tensor([int(sym), int(clip_sym), nst]))
+    print('clip fixtures written')
+
+
+GENERATORS = {'quant': gen_quant, 'gptq': gen_gptq, 'awq': gen_awq, 'clip': gen_clip}
 
 
 if __name__ == '__main__':

@@ -1,0 +1,121 @@
+"""GPU parity for the AWQ / auto-clip kernels and the device scale search (tier T3 of
+SURVEY.md §8c: bit-exact building blocks; chosen ratio + scales equal to the reference on the
+golden subsets; clip argmins equal)."""
+import pytest
+import torch
+
+import fixtures as F
+from awq_helpers import SUBSETS, build_layer, forward_fn
+from oracle import awq_ref as A
+from oracle import quant_ref as Q
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(t):
+    return t.detach().cpu().view(torch.int16)
+
+
+def test_awq_scales_exhaustive_pow(dev):
+    """Every positive normal bf16 in [2^-12, 2^8) x 20 ratios: device == torch-CPU."""
+    from lightcompress_amd import ops
+    u = torch.arange(0x3980, 0x4380, dtype=torch.int32).to(torch.int16)
+    xm = u.view(torch.bfloat16).clone()
+    xd = xm.to(dev)
+    for n in range(20):
+        r = n / 20
+        exp = A.scales_v2(xm, r)
+        got = ops.awq_scales(xd, r)
+        assert torch.equal(bits(got), bits(exp)), f'ratio {r}'
+
+
+@pytest.mark.parametrize('seed', [0, 1, 2])
+def test_awq_scales_random(dev, seed):
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(seed)
+    xm = torch.exp(torch.randn(4096, generator=g) * 2).to(torch.bfloat16)
+    xm[:3] = 0  # pow(0, r) and the clamp(1e-4) floor
+    for n in range(20):
+        assert torch.equal(bits(ops.awq_scales(xm.to(dev), n / 20)), bits(A.scales_v2(xm, n / 20)))
+
+
+@pytest.mark.parametrize('n,c', [(128, 256), (4096, 4096), (1000, 1024)])
+def test_absmean(dev, n, c):
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(n)
+    x = (torch.randn(n, c, generator=g) * torch.exp(torch.randn(c, generator=g))).to(torch.bfloat16)
+    got = ops.absmean_cols(x.to(dev)).cpu()
+    exp = A.act_scale(x)
+    # exact-sum mean vs torch's fp32 summation: equal up to rare 1-ulp bf16 roundings
+    diff = (bits(got).int() - bits(exp).int()).abs()
+    assert diff.max().item() <= 1
+    assert (diff == 0).float().mean().item() >= 0.995
+
+
+def test_scale_bcast(dev):
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(64, 512, generator=g).to(torch.bfloat16)
+    sc = torch.exp(torch.randn(512, generator=g)).to(torch.bfloat16)
+    sr = torch.exp(torch.randn(64, generator=g)).to(torch.bfloat16)
+    xd = x.to(dev)
+    assert torch.equal(bits(ops.scale_bcast(xd, sc.to(dev), 'div')), bits(x / sc.view(1, -1)))
+    assert torch.equal(bits(ops.scale_bcast(xd, sc.to(dev), 'mul')), bits(x * sc.view(1, -1)))
+    assert torch.equal(bits(ops.scale_bcast(xd, sr.to(dev), 'div', axis=1)),
+                       bits(x / sr.view(-1, 1)))
+    y = xd.clone()
+    ops.scale_bcast(y, sc.to(dev), 'mul', out=y)
+    assert torch.equal(bits(y), bits(x * sc.view(1, -1)))
+
+
+def test_sq_diff_mean(dev):
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(4)
+    a = torch.randn(32, 64, 256, generator=g).to(torch.bfloat16)
+    b = (a.float() + torch.randn(a.shape, generator=g) * 0.01).to(torch.bfloat16)
+    got = ops.sq_diff_mean(a.to(dev), b.to(dev))
+    exp = A.loss(a, b)
+    assert abs(got - exp) <= 1e-6 * abs(exp)
+
+
+@pytest.mark.parametrize('name', F.names('clip_'))
+def test_auto_clip_vs_reference(dev, name):
+    from lightcompress_amd import ops
+    from lightcompress_amd.auto_clip import AutoClipper
+    c = F.load(name)
+    sym, clip_sym, nst = c['meta'].tolist()
+    qmin, qmax = (-8, 7) if sym else (0, 15)
+    x = AutoClipper.sample_tokens(c['x'].to(dev), nst)
+    bmax, bmin = ops.auto_clip_search(c['w'].to(dev), x, 128, 10, 20, qmin, qmax, bool(sym),
+                                      bool(clip_sym))
+    eq_max = (bits(bmax) == bits(c['best_max'])).float().mean().item()
+    eq_min = (bits(bmin) == bits(c['best_min'])).float().mean().item()
+    assert eq_max == 1.0 and eq_min == 1.0, (eq_max, eq_min)
+    w = c['w'].to(dev).clone()
+    ops.clip_apply(w, 128, bmax.reshape(-1), None if clip_sym else bmin.reshape(-1), out=w)
+    assert torch.equal(bits(w), bits(c['w_clipped']))
+
+
+@pytest.mark.parametrize('subset', ['qkv', 'mlp', 'down'])
+@pytest.mark.parametrize('sym', [True, False])
+def test_search_scale_vs_reference(dev, subset, sym):
+    """Device search on the HF module (GPU GEMMs / SDPA): same chosen ratio and bit-equal
+    scales as the reference CPU run; losses agree to the bf16-output level."""
+    from lightcompress_amd.awq import Awq
+    from lightcompress_amd.quant import IntegerQuantizer
+    c = F.load(f'awq_{subset}_{"sym" if sym else "asym"}')
+    cfg, layer, kwargs = build_layer(dev)
+    names, inspect_name, has_kw = SUBSETS[subset]
+    obj = Awq.__new__(Awq)
+    obj.wquantizer = IntegerQuantizer(4, sym, 'per_group', group_size=128)
+    obj.awq_bs, obj.w_only, obj.n_grid = None, True, 20
+    layers = {n: layer.get_submodule(n) for n in names}
+    inspect = layer.get_submodule(inspect_name)
+    best = obj.search_scale_subset(None, layers, [c['x'].to(dev)], inspect, False,
+                                   [kwargs] if has_kw else {})
+    ref_losses = c['losses'].tolist()
+    ref_best = min(range(20), key=lambda i: (ref_losses[i], i))
+    assert obj.last_search['best_index'] == ref_best
+    assert torch.equal(bits(best), bits(c['scales']))
+    got = torch.tensor(obj.last_search['losses'], dtype=torch.float64)
+    assert torch.allclose(got, c['losses'], rtol=5e-2, atol=1e-9)

@@ -1,0 +1,87 @@
+"""End-to-end plugin pipeline on a tiny random Llama (2 blocks) on the GPU: Awq (+clip),
+GPTQ (act-order, true_sequential, quant_out) and RTN through run_block_loop + deploy, with the
+reference's YAML config schema."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def tiny_model(dev, layers=2):
+    from transformers import LlamaConfig
+    from lightcompress_amd.llama import Llama
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                      num_key_value_heads=2, num_hidden_layers=layers, vocab_size=128,
+                      max_position_embeddings=512, rms_norm_eps=1e-5)
+    return Llama.random(cfg, device=dev, seed=1)
+
+
+def calib(model, n=4, seq=64, seed=0):
+    g = torch.Generator(device=model.blocks[0].self_attn.q_proj.weight.device).manual_seed(seed)
+    dev = model.blocks[0].self_attn.q_proj.weight.device
+    x = torch.randn(n, seq, model.model_config.hidden_size, generator=g, device=dev)
+    return {'data': [x.to(torch.bfloat16)], 'kwargs': [model.rotary_kwargs(seq)]}
+
+
+AWQ_CFG = {'calib': {'seq_len': 64},
+           'quant': {'method': 'Awq', 'weight': {'bit': 4, 'symmetric': True,
+                                                 'granularity': 'per_group', 'group_size': 128},
+                     'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True,
+                                 'clip_sym': True}, 'quant_out': True}}
+
+GPTQ_CFG = {'quant': {'method': 'GPTQ', 'weight': {'bit': 4, 'symmetric': False,
+                                                   'granularity': 'per_group',
+                                                   'group_size': 128},
+                      'special': {'actorder': True, 'static_groups': False, 'percdamp': 0.01,
+                                  'blocksize': 128, 'true_sequential': True},
+                      'quant_out': True}}
+
+
+@pytest.mark.parametrize('cfg', [AWQ_CFG, GPTQ_CFG], ids=['awq', 'gptq'])
+def test_pipeline_runs_and_deploys(dev, cfg):
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.utils import load_config
+    model = tiny_model(dev)
+    config = load_config(cfg)
+    algo = build_algo(model, config, calib(model))
+    algo.run_block_loop()
+    for b in model.blocks:
+        for n, m in model.get_block_linears(b).items():
+            assert torch.isfinite(m.weight).all(), n
+    algo.deploy('fake_quant')
+    x = torch.randn(2, 16, 256, device=dev, dtype=torch.bfloat16)
+    kw = model.rotary_kwargs(16)
+    y = model.blocks[0](x, **kw)
+    y = y[0] if isinstance(y, tuple) else y
+    assert torch.isfinite(y).all()
+    # deployed fake-quant weights take at most 16 values per 128-group
+    w = model.blocks[0].mlp.down_proj.weight.float().reshape(-1, 128)
+    assert max(len(torch.unique(r)) for r in w[:64]) <= 16
+
+
+def test_awq_vllm_pack_deploy(dev):
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.utils import load_config
+    cfg = {**AWQ_CFG, 'quant': {**AWQ_CFG['quant'],
+                                'weight': {**AWQ_CFG['quant']['weight'], 'need_pack': True}}}
+    model = tiny_model(dev)
+    algo = build_algo(model, load_config(cfg), calib(model))
+    algo.run_block_loop()
+    algo.deploy('vllm_quant')
+    m = model.blocks[0].mlp.gate_proj
+    assert m.weight_packed.dtype == torch.int32 and m.weight_packed.shape == (512, 256 // 8)
+    assert m.weight_scale.dtype == torch.float16 and m.weight_scale.shape == (512, 2)
+
+
+def test_rtn_autoawq_deploy(dev):
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.utils import load_config
+    cfg = {'quant': {'method': 'RTN', 'weight': {'bit': 4, 'symmetric': False,
+                                                 'granularity': 'per_group', 'group_size': 128,
+                                                 'pack_version': 'gemm_pack'}}}
+    model = tiny_model(dev)
+    algo = build_algo(model, load_config(cfg), None)
+    algo.run_block_loop()
+    algo.deploy('autoawq_quant')
+    m = model.blocks[1].self_attn.o_proj
+    assert m.qweight.shape == (256, 256 // 8) and m.scales.dtype == torch.float16
