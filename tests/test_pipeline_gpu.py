@@ -54,8 +54,13 @@ def test_pipeline_runs_and_deploys(dev, cfg):
     y = model.blocks[0](x, **kw)
     y = y[0] if isinstance(y, tuple) else y
     assert torch.isfinite(y).all()
-    # deployed fake-quant weights take at most 16 values per 128-group
-    w = model.blocks[0].mlp.down_proj.weight.float().reshape(-1, 128)
+    # deployed fake-quant weights take at most 16 values per 128-group (groups live in the
+    # act-order permuted column space for GPTQ)
+    m = model.blocks[0].mlp.down_proj
+    w = m.weight.float()
+    if hasattr(m, 'buf_perm'):
+        w = w[:, m.buf_perm]
+    w = w.reshape(-1, 128)
     assert max(len(torch.unique(r)) for r in w[:64]) <= 16
 
 
