@@ -1,0 +1,311 @@
+"""Benchmark: LightCompress per-layer weight-quantization hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): Llama-3-8B AWQ w4a16 g128 (symmetric, weight_clip,
+trans_version v2 -- configs/quantization/methods/Awq/awq_w_only.yml) with 128 calibration
+samples x 512 tokens, deployed to vLLM packed int4 (need_pack). One step = one Llama-3-8B
+decoder block through the reference's block_opt (calibration forward with input capture, AWQ
+scale search on the qkv / gate-up / down subsets -- o_proj is skipped under GQA exactly as the
+reference does -- scale application, auto-clip of v/o/gate/up/down) plus the real-quant + vLLM
+pack of its 7 linears. Random-init weights and synthetic activations of the real shapes
+(no network: no checkpoints / datasets).
+
+metric: linear layers quantized per second (whole job, all ranks). Multi-GPU: one process per
+GPU (torchrun); with quant_out=False AWQ blocks are independent given the float activations
+(SURVEY.md §8e), so every rank quantizes its own blocks -- weak scaling, no data-path collective.
+
+Also reported: the roofline of the dominant kernel (the bf16 projection GEMMs of the AWQ loss
+search, timed live with device events around every linear launch), live timings of every lcq
+HIP kernel family, and a CPU baseline (the oracle = reference algorithm restated on torch-CPU,
+timed on a bounded sample of the same step on the host cores and extrapolated).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+LLAMA3_8B = dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
+                 num_key_value_heads=8, head_dim=128, rope_theta=500000.0,
+                 max_position_embeddings=8192, rms_norm_eps=1e-5, num_hidden_layers=32,
+                 vocab_size=128256)
+N_LINEARS_PER_BLOCK = 7
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--n-samples', type=int, default=128)
+    ap.add_argument('--seq-len', type=int, default=512)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-budget-s', type=float, default=20.0)
+    return ap.parse_args()
+
+
+def awq_config(seq_len):
+    from lightcompress_amd.utils import load_config
+    return load_config({
+        'base': {'seed': 42},
+        'calib': {'name': 'pileval', 'n_samples': 128, 'bs': -1, 'seq_len': seq_len,
+                  'preproc': 'pileval_awq'},
+        'quant': {'method': 'Awq',
+                  'weight': {'bit': 4, 'symmetric': True, 'granularity': 'per_group',
+                             'group_size': 128, 'need_pack': True},
+                  'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True,
+                              'clip_sym': True},
+                  'quant_out': False},
+    })
+
+
+def synthetic_hidden(n, seq, hidden, device, seed):
+    """Calibration hidden states with log-normal per-channel magnitudes (outlier channels,
+    SURVEY.md §8d), bf16."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    mag = torch.exp(torch.randn(hidden, generator=g, device=device))
+    x = torch.randn(n, seq, hidden, generator=g, device=device) * mag
+    return x.to(torch.bfloat16)
+
+
+class GemmMeter:
+    """Device events around every nn.Linear forward (one hipBLASLt GEMM each: no bias)."""
+
+    def __init__(self, blocks):
+        self.records = []
+        self.handles = []
+        self.active = False
+        for b in blocks:
+            for m in b.modules():
+                if isinstance(m, torch.nn.Linear):
+                    self.handles.append(m.register_forward_pre_hook(self._pre))
+                    self.handles.append(m.register_forward_hook(self._post))
+
+    def _pre(self, m, inp):
+        if self.active:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            m._lcq_ev = e
+
+    def _post(self, m, inp, out):
+        if self.active and hasattr(m, '_lcq_ev'):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            x = inp[0]
+            flops = 2.0 * x.numel() // x.shape[-1] * m.in_features * m.out_features
+            self.records.append((m._lcq_ev, e, flops))
+            del m._lcq_ev
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b, _ in self.records]
+        fl = [f for _, _, f in self.records]
+        if not ms:
+            return None
+        return {'launches': len(ms), 'avg_ms': sum(ms) / len(ms), 'total_ms': sum(ms),
+                'flops_per_launch': sum(fl) / len(fl),
+                'tflops': sum(fl) / (sum(ms) * 1e-3) / 1e12}
+
+    def close(self):
+        for h in self.handles:
+            h.remove()
+
+
+def deploy_block(algo, model, block, idx):
+    from lightcompress_amd.module_utils import VllmRealQuantLinear
+    model.replace_module_block(VllmRealQuantLinear, block, idx,
+                               algo.get_replacement_params('vllm_quant', algo.w_only))
+
+
+def cpu_baseline(args, budget_s):
+    """Oracle (reference algorithm restated on torch-CPU) on a bounded sample of one step,
+    extrapolated to the full step. Returns the cpu_baseline object."""
+    from transformers import LlamaConfig
+    from transformers.models.llama import modeling_llama as ml
+    from oracle import awq_ref as A
+    from oracle import quant_ref as Q
+    torch.manual_seed(0)
+    threads = torch.get_num_threads()
+    cfg = LlamaConfig(**LLAMA3_8B)
+    cfg._attn_implementation = 'sdpa'
+    layer = ml.LlamaDecoderLayer(cfg, layer_idx=0).to(torch.bfloat16).eval()
+    with torch.no_grad():
+        for p in layer.parameters():
+            if p.dim() == 2:
+                p.normal_(0, 0.02)
+    rot = ml.LlamaRotaryEmbedding(cfg)
+    seq = args.seq_len
+    x = synthetic_hidden(1, seq, cfg.hidden_size, 'cpu', 7)
+    pos = torch.arange(seq).unsqueeze(0)
+    kw = {'position_embeddings': rot(x, pos), 'attention_mask': None, 'position_ids': pos}
+    t_total_est = 0.0
+    parts = {}
+    t_start = time.perf_counter()
+    with torch.no_grad():
+        xq = layer.input_layernorm(x)
+        h = x + layer.self_attn(xq, **kw)[0]
+        xm = layer.post_attention_layernorm(h)
+        xd = layer.mlp.act_fn(layer.mlp.gate_proj(xm)) * layer.mlp.up_proj(xm)
+        subsets = {
+            'qkv': (xq, [layer.self_attn.q_proj, layer.self_attn.k_proj, layer.self_attn.v_proj],
+                    lambda t: layer.self_attn(t, **kw)[0]),
+            'mlp': (xm, [layer.mlp.gate_proj, layer.mlp.up_proj], layer.mlp),
+            'down': (xd, [layer.mlp.down_proj], layer.mlp.down_proj),
+        }
+        # one sample (seq tokens), org forward + ONE ratio (scales, fake quant, forward, loss)
+        for name, (xin, mods, fwd) in subsets.items():
+            t0 = time.perf_counter()
+            org = fwd(xin)
+            t1 = time.perf_counter()
+            s = A.scales_v2(A.act_scale(xin), 0.5)
+            saved = [m.weight.data for m in mods]
+            for m in mods:
+                m.weight.data = A.fake_quant_scaled(m.weight.data, s, 4, True, 128)
+            out = fwd(xin / s.view(1, -1))
+            A.loss(org, out)
+            for m, w in zip(mods, saved):
+                m.weight.data = w
+            t2 = time.perf_counter()
+            per_sample = (t1 - t0) + 20 * (t2 - t1)       # org + 20 ratios
+            est = per_sample * args.n_samples               # linear in tokens
+            parts[f'search_{name}'] = est
+            t_total_est += est
+        # auto-clip: 64 rows of gate_proj on the 512 sampled tokens, extrapolated by OC*IC
+        w = layer.mlp.gate_proj.weight.data[:64].clone()
+        xs = xm.reshape(-1, cfg.hidden_size)[: seq]
+        t0 = time.perf_counter()
+        A.clip_layer(w, xs, 4, True, 128, True, n_sample_token=seq)
+        t_clip = time.perf_counter() - t0
+        clipped = (cfg.num_key_value_heads * cfg.head_dim * cfg.hidden_size
+                   + cfg.hidden_size ** 2 + 3 * cfg.intermediate_size * cfg.hidden_size)
+        parts['auto_clip'] = t_clip * clipped / w.numel()
+        t_total_est += parts['auto_clip']
+        # deploy: real quant + vLLM pack of one gate_proj, extrapolated to the 7 linears
+        t0 = time.perf_counter()
+        codes, sc, _ = Q.real_quant_dynamic(layer.mlp.gate_proj.weight.data, 4, True)
+        Q.pack_vllm(codes, 4)
+        t_dep = time.perf_counter() - t0
+        all_params = clipped + (cfg.hidden_size + cfg.num_key_value_heads * cfg.head_dim) * cfg.hidden_size
+        parts['deploy'] = t_dep * all_params / layer.mlp.gate_proj.weight.numel()
+        t_total_est += parts['deploy']
+    wall = time.perf_counter() - t_start
+    return {'value': N_LINEARS_PER_BLOCK / t_total_est, 'unit': 'linears/s', 'cores': threads,
+            'kind': 'port',
+            'sample': (f'oracle (torch-CPU restatement of awq.py/auto_clip.py/quant.py) on one '
+                       f'Llama-3-8B block: 1 of {args.n_samples} calibration samples x org+1 of '
+                       f'20 ratios per subset, auto-clip on 64 gate_proj rows, real-quant+pack '
+                       f'of one gate_proj; extrapolated linearly to the full step '
+                       f'({t_total_est:.0f} s/block est., {wall:.1f} s measured)'),
+            'est_s_per_block': t_total_est, 'parts_s': parts}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+    from transformers import LlamaConfig
+    from lightcompress_amd import _native
+    from lightcompress_amd.llama import Llama
+    from lightcompress_amd.pipeline import build_algo
+
+    _native.load()
+    cfg = LlamaConfig(**LLAMA3_8B)
+    nblk = args.warmup + args.steps
+    model = Llama.random(cfg, num_layers=nblk, device=dev, seed=1000 + rank)
+    hidden = synthetic_hidden(args.n_samples, args.seq_len, cfg.hidden_size, dev, 17 + rank)
+    calib = {'data': [hidden], 'kwargs': [model.rotary_kwargs(args.seq_len)]}
+    config = awq_config(args.seq_len)
+    algo = build_algo(model, config, calib)
+    blocks = model.get_blocks()
+
+    def step(i):
+        algo.block_idx = i
+        algo.block_opt(blocks[i])
+        deploy_block(algo, model, blocks[i], i)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    meter = GemmMeter([blocks[i] for i in range(args.warmup, nblk)])
+    meter.active = True
+    timer = _native.KernelTimer()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with timer:
+        for i in range(args.warmup, nblk):
+            step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    meter.active = False
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    gemm = meter.summary()
+    kern = timer.summary()
+    meter.close()
+    linears = N_LINEARS_PER_BLOCK * args.steps * world
+    value = linears / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        roofline = None
+        if gemm:
+            roofline = {'kernel': 'bf16 projection GEMM of the AWQ loss search (q/k/v/o/gate/up/'
+                                  'down, hipBLASLt via the HF module forward)',
+                        'bound': 'mfma', 'achieved': round(gemm['tflops'], 1),
+                        'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
+                        'frac': round(gemm['tflops'] / PEAK_BF16_TFLOPS, 4), 'traffic': None,
+                        'avg_launch_ms': round(gemm['avg_ms'], 4),
+                        'flops_per_launch': gemm['flops_per_launch'],
+                        'share_of_step': round(gemm['total_ms'] / (elapsed * 1e3), 3)}
+        kernels = {k: {'launches': v['launches'], 'avg_ms': round(v['avg_ms'], 4),
+                       'share_of_step': round(v['total_ms'] / (elapsed * 1e3), 4)}
+                   for k, v in sorted(kern.items(), key=lambda kv: -kv[1]['total_ms'])}
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, args.cpu_budget_s)
+        line = {
+            'metric': 'linear-layers quantized/sec (Llama-3-8B AWQ w4a16 g128)',
+            'value': round(value, 3), 'unit': 'linears/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 2),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
+            'data': 'synthetic (random-init Llama-3-8B blocks, log-normal-channel activations)',
+            'config': {'workload': 'Llama-3-8B AWQ w4a16 g128 sym, weight_clip, v2, '
+                                   f'{args.n_samples}x{args.seq_len} calib tokens, vLLM int4 '
+                                   'pack; 1 step = 1 decoder block (7 linears)',
+                       'model': 'Llama-3-8B (4096/14336, 32q/8kv heads)',
+                       'global_batch': args.n_samples * world, 'seq_len': args.seq_len,
+                       'parallelism': f'blocks sharded over {world} GPU(s), no collective'},
+            'extrapolated_model_wall_s': round(ms_per_step * 32 / 1e3, 2),
+            'roofline': roofline,
+            'lcq_kernels': kernels,
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -108,9 +108,46 @@ def stream_of(t: torch.Tensor):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+class KernelTimer:
+    """Records a device event pair around every lcq call while active (bench.py uses this to
+    time each kernel family live, on the stream the kernel is launched on)."""
+
+    def __init__(self):
+        self.events = {}
+
+    def __enter__(self):
+        global _timer
+        _timer = self
+        return self
+
+    def __exit__(self, *exc):
+        global _timer
+        _timer = None
+
+    def summary(self):
+        import torch as _t
+        _t.cuda.synchronize()
+        out = {}
+        for name, pairs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in pairs]
+            out[name] = {'launches': len(ms), 'total_ms': sum(ms), 'avg_ms': sum(ms) / len(ms)}
+        return out
+
+
+_timer = None
+
+
 def call(name: str, *args):
     lib = load()
-    rc = getattr(lib, name)(*args)
+    if _timer is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib, name)(*args)
+        e1.record()
+        _timer.events.setdefault(name, []).append((e0, e1))
+    else:
+        rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.lcq_last_error().decode(errors='replace')
         if rc == -1:
