@@ -159,170 +159,190 @@ __global__ void k_sqdiff_p2(const double* part, int nparts, int64_t n, float* ou
 }
 
 // ----------------------------------------------------------------------------------------
-// auto_clip search (auto_clip.py:83-191), one wave = 64 output rows x one 128-wide group.
+// auto_clip search (auto_clip.py:83-191). A workgroup = 128 output rows (one per lane, two
+// waves) x one 128-wide group; the group's sampled-token tiles are shared through LDS.
 // For every (row o, group g):
 //   org[t]  = bf16( sum_k bf16(x[t,g,k] * w[o,g,k]) )          (t over the T sampled tokens)
 //   step i: max_i = bf16(org_max * (1 - i/n_grid)), min_i = -max_i | bf16(org_min * (..))
 //           q = fake_quant(clamp(w, min_i, max_i)) (bf16, per-group min/max qparams)
 //           cur[t] = bf16( sum_k bf16(x * q) );  err_i = bf16(mean_t bf16(bf16(cur-org)^2))
 //   keep the first strictly smaller err (min_errs starts at bf16(1e9)).
-// The per-product bf16 rounding of the reference's materialised broadcast product rules out
-// MFMA (which accumulates exact products), so this is a VALU kernel: weights stay in VGPRs,
-// token tiles of x are staged in LDS and read as wave-uniform broadcasts. Sums over k use 16
-// partial accumulators + a halving tree (torch-CPU's vectorised reduction order).
+// The reference materialises the bf16 broadcast product, so every product is rounded to bf16
+// before the fp32 sum: that rules out MFMA (exact products). VALU design: the candidate
+// weights live unpacked in VGPRs, x tiles are fp32 in LDS and read as wave-uniform broadcasts,
+// products go through v_pk_mul_f32 + v_cvt_pk_bf16_f32 (RNE) and v_pk_add_f32 into 8 partial
+// sums (k mod 8) reduced by a halving tree (torch-CPU's vectorised order), the per-step
+// squared-error sums and the original outputs sit in LDS so the token loop stays rolled.
 // ----------------------------------------------------------------------------------------
-constexpr int CG = 128;  // group size
-constexpr int CT = 32;   // tokens per LDS tile
+constexpr int CG = 128;        // group size
+constexpr int CROWS = 128;     // rows per workgroup (2 lanes per row -> 256 threads)
+constexpr int CT = 32;         // sampled tokens per LDS tile
 constexpr int CMAXSTEPS = 16;
+constexpr int CH = CG / 2;     // weights per lane: k = 8i + 4h + j, h = lane parity
 
-__device__ __forceinline__ float bf(uint32_t u, int hi) {
-  return __uint_as_float(hi ? (u & 0xffff0000u) : (u << 16));
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bf16r(float f) {  // RNE to bf16 (v_cvt_pk_bf16_f32)
+  const __bf16 h = (__bf16)f;
+  return __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, h) << 16);
 }
 
-__device__ __forceinline__ float bf16r(float f) {  // finite-only RNE
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return __uint_as_float(u & 0xffff0000u);
+// products of a pair rounded to bf16 and widened back to fp32
+__device__ __forceinline__ v2f bf16r2(v2f p) {
+  const v2bf h = __builtin_convertvector(p, v2bf);
+  const uint32_t u = __builtin_bit_cast(uint32_t, h);
+  v2f r;
+  r.x = __uint_as_float(u << 16);
+  r.y = __uint_as_float(u & 0xffff0000u);
+  return r;
 }
 
-// dot of one LDS token row (64 packed dwords) with 64 packed weight dwords
-__device__ __forceinline__ float dot_bf16(const uint32_t* xr, const uint32_t (&wp)[64]) {
-  float acc[16];
+// IEEE quotient a/b given rb = RN(1/b) (Markstein: e = a - b*q0 is exact, one fma rounds)
+__device__ __forceinline__ float div_rn(float a, float b, float rb) {
+  const float q0 = a * rb;
+  const float e = __fmaf_rn(-b, q0, a);
+  return __fmaf_rn(e, rb, q0);
+}
+
+__device__ __forceinline__ float xor1(float v) {  // value of the partner lane (lane ^ 1)
+  return __shfl_xor(v, 1, 64);
+}
+
+// sum_k bf16(x[k] * q[k]) over one 128-wide group, split over a lane pair: this lane owns
+// k = 8i + 4h + j (j = 0..3) i.e. partial sums acc_{4h+j} of the 8-way (k mod 8) order; the
+// pair exchange forms l_j = acc_j + acc_{j+4} and both lanes finish the halving tree.
+__device__ __forceinline__ float dot_row(const float* __restrict__ xr, const float (&q)[CH],
+                                         int h) {
+  v2f a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-#pragma unroll
-  for (int c = 0; c < 128; c += 16) {
-#pragma unroll
-    for (int j = 0; j < 16; j += 2) {
-      const uint32_t xv = xr[(c + j) >> 1];
-      const uint32_t wv = wp[(c + j) >> 1];
-      acc[j] += bf16r(bf(xv, 0) * bf(wv, 0));
-      acc[j + 1] += bf16r(bf(xv, 1) * bf(wv, 1));
-    }
+  for (int i = 0; i < CG / 8; ++i) {
+    const float4 xv = *reinterpret_cast<const float4*>(xr + 8 * i + 4 * h);
+    a0 += bf16r2(v2f{xv.x, xv.y} * v2f{q[4 * i], q[4 * i + 1]});
+    a1 += bf16r2(v2f{xv.z, xv.w} * v2f{q[4 * i + 2], q[4 * i + 3]});
   }
-#pragma unroll
-  for (int h = 8; h >= 1; h >>= 1)
-#pragma unroll
-    for (int j = 0; j < h; ++j) acc[j] += acc[j + h];
-  return bf16r(acc[0]);
+  // lane h=0 holds acc0..3, h=1 holds acc4..7: l_j = acc_j + acc_{j+4}. The partner values
+  // are read in uniform control flow (a cross-lane read inside a divergent branch would see
+  // inactive lanes); the operand order is then fixed with selects so both lanes agree.
+  const float p0 = xor1(a0.x), p1 = xor1(a0.y), p2 = xor1(a1.x), p3 = xor1(a1.y);
+  const float l0 = (h ? p0 : a0.x) + (h ? a0.x : p0);
+  const float l1 = (h ? p1 : a0.y) + (h ? a0.y : p1);
+  const float l2 = (h ? p2 : a1.x) + (h ? a1.x : p2);
+  const float l3 = (h ? p3 : a1.y) + (h ? a1.y : p3);
+  return bf16r((l0 + l2) + (l1 + l3));
 }
 
-__global__ void __launch_bounds__(64)
+__device__ __forceinline__ void load_half(const uint16_t* __restrict__ wrow, int h,
+                                          float (&q)[CH]) {
+#pragma unroll
+  for (int i = 0; i < CG / 8; ++i) {
+    const uint2 v = *reinterpret_cast<const uint2*>(wrow + 8 * i + 4 * h);
+    q[4 * i] = __uint_as_float(v.x << 16);
+    q[4 * i + 1] = __uint_as_float(v.x & 0xffff0000u);
+    q[4 * i + 2] = __uint_as_float(v.y << 16);
+    q[4 * i + 3] = __uint_as_float(v.y & 0xffff0000u);
+  }
+}
+
+__global__ void __launch_bounds__(2 * CROWS, 2)
     k_auto_clip(const uint16_t* __restrict__ w, const uint16_t* __restrict__ x, int64_t oc,
                 int64_t ic, int T, int nsteps, const float* __restrict__ factors, float qmin,
                 float qmax, int sym, int clip_sym, uint16_t* best_max, uint16_t* best_min) {
-  __shared__ __attribute__((aligned(16))) uint32_t xs[CT * 64];
-  const int lane = threadIdx.x;
-  const int64_t o = (int64_t)blockIdx.x * 64 + lane;
+  __shared__ __attribute__((aligned(16))) float xs[CT * CG];     // 16 KB
+  __shared__ float orgs[CT * CROWS];                              // 16 KB
+  __shared__ float es[CMAXSTEPS * CROWS];                          // 8 KB
+  const int tid = threadIdx.x;
+  const int r = tid >> 1, h = tid & 1;
+  const int64_t o = (int64_t)blockIdx.x * CROWS + r;
   const int64_t g = blockIdx.y;
   const int64_t ng = ic / CG;
   const bool live = o < oc;
-  uint32_t wp[64];
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(w + (live ? o : 0) * ic + g * CG);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      uint4 v = src[i];
-      wp[4 * i] = v.x; wp[4 * i + 1] = v.y; wp[4 * i + 2] = v.z; wp[4 * i + 3] = v.w;
-    }
-  }
+  const uint16_t* wrow = w + (live ? o : 0) * ic + g * CG;
+
   float mxs = -INFINITY, mn = INFINITY, amax = 0.f;
+  {
+    float q[CH];
+    load_half(wrow, h, q);
 #pragma unroll
-  for (int i = 0; i < 64; ++i) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float v = bf(wp[i], h);
-      mxs = fmaxf(mxs, v);
-      mn = fminf(mn, v);
-      amax = fmaxf(amax, fabsf(v));
+    for (int k = 0; k < CH; ++k) {
+      mxs = fmaxf(mxs, q[k]);
+      mn = fminf(mn, q[k]);
+      amax = fmaxf(amax, fabsf(q[k]));
     }
+    mxs = fmaxf(mxs, xor1(mxs));
+    mn = fminf(mn, xor1(mn));
+    amax = fmaxf(amax, xor1(amax));
   }
   const float org_max = clip_sym ? amax : mxs;
   const float org_min = mn;
-  float smax[CMAXSTEPS], smin[CMAXSTEPS], qs[CMAXSTEPS], qz[CMAXSTEPS], err[CMAXSTEPS];
-#pragma unroll
-  for (int s = 0; s < CMAXSTEPS; ++s) {
-    if (s < nsteps) {
-      const float f = factors[s];
-      smax[s] = bf16r(org_max * f);
-      smin[s] = clip_sym ? -smax[s] : bf16r(org_min * f);
-      // min/max of clamp(w, min, max) = clamp of the group's min/max (clamp is monotone)
-      const float cmn = fminf(fmaxf(mn, smin[s]), smax[s]);
-      const float cmx = fminf(fmaxf(mxs, smin[s]), smax[s]);
-      qparams_ct<LCQ_BF16>(cmn, cmx, qmin, qmax, sym, qs[s], qz[s]);
-    }
-    err[s] = 0.f;
-  }
+  if (h == 0)
+    for (int s = 0; s < nsteps; ++s) es[s * CROWS + r] = 0.f;
 
   for (int t0 = 0; t0 < T; t0 += CT) {
-    __syncthreads();
-    // stage CT token rows of this group (CT x 256 B) into LDS: 8 x 16 B per lane
+    __syncthreads();  // previous tile fully consumed
+    // stage CT token rows of this group as fp32: 512 chunks of 8 bf16, 2 per thread
 #pragma unroll
-    for (int i = 0; i < (CT * 16) / 64; ++i) {
-      const int idx = i * 64 + lane;
+    for (int i = 0; i < (CT * CG / 8) / (2 * CROWS); ++i) {
+      const int idx = i * 2 * CROWS + tid;
       const int row = idx >> 4, ch = idx & 15;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (t0 + row < T)
         v = *reinterpret_cast<const uint4*>(x + (int64_t)(t0 + row) * ic + g * CG + ch * 8);
-      *reinterpret_cast<uint4*>(&xs[row * 64 + ch * 4]) = v;
+      float4 a, b;
+      a.x = __uint_as_float(v.x << 16); a.y = __uint_as_float(v.x & 0xffff0000u);
+      a.z = __uint_as_float(v.y << 16); a.w = __uint_as_float(v.y & 0xffff0000u);
+      b.x = __uint_as_float(v.z << 16); b.y = __uint_as_float(v.z & 0xffff0000u);
+      b.z = __uint_as_float(v.w << 16); b.w = __uint_as_float(v.w & 0xffff0000u);
+      *reinterpret_cast<float4*>(&xs[row * CG + ch * 8]) = a;
+      *reinterpret_cast<float4*>(&xs[row * CG + ch * 8 + 4]) = b;
     }
     __syncthreads();
     const int tn = min(CT, T - t0);
-    float org[CT];
+    // pass p = 0: original outputs; p = s + 1: shrink step s
+    for (int p = 0; p <= nsteps; ++p) {
+      float q[CH];
+      load_half(wrow, h, q);
+      if (p > 0) {
+        const float f = factors[p - 1];
+        const float smax = bf16r(org_max * f);
+        const float smin = clip_sym ? -smax : bf16r(org_min * f);
+        const float cmn = fminf(fmaxf(mn, smin), smax);
+        const float cmx = fminf(fmaxf(mxs, smin), smax);
+        float qs, qz;
+        qparams_ct<LCQ_BF16>(cmn, cmx, qmin, qmax, sym, qs, qz);
+        const float rs = 1.0f / qs;  // correctly rounded reciprocal (IEEE division)
 #pragma unroll
-    for (int t = 0; t < CT; ++t) org[t] = (t < tn) ? dot_bf16(&xs[t * 64], wp) : 0.f;
-    for (int s = 0; s < nsteps; ++s) {
-      uint32_t qp[64];
-      const float lo = smin[0], hi = smax[0];
-      float a_lo = lo, a_hi = hi, a_s = qs[0], a_z = qz[0];
-#pragma unroll
-      for (int k = 1; k < CMAXSTEPS; ++k)
-        if (k == s) {
-          a_lo = smin[k]; a_hi = smax[k]; a_s = qs[k]; a_z = qz[k];
-        }
-      (void)lo; (void)hi;
-#pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        float q2[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const float v = fminf(fmaxf(bf(wp[i], h), a_lo), a_hi);
-          float tq = rintf(bf16r(v / a_s));
-          tq = bf16r(tq + a_z);
+        for (int k = 0; k < CH; ++k) {
+          const float v = fminf(fmaxf(q[k], smin), smax);
+          float tq = rintf(bf16r(div_rn(v, qs, rs)));
+          if (!sym) tq = bf16r(tq + qz);
           tq = fminf(fmaxf(tq, qmin), qmax);
-          q2[h] = bf16r(bf16r(tq - a_z) * a_s);
-        }
-        qp[i] = (__float_as_uint(q2[0]) >> 16) | (__float_as_uint(q2[1]) & 0xffff0000u);
-      }
-      // running fp32 sum over t in token order (sum of the bf16 squares, then / T)
-      float e = err[0];
-#pragma unroll
-      for (int k = 1; k < CMAXSTEPS; ++k)
-        if (k == s) e = err[k];
-#pragma unroll
-      for (int t = 0; t < CT; ++t) {
-        if (t < tn) {
-          const float cur = dot_bf16(&xs[t * 64], qp);
-          const float d = bf16r(cur - org[t]);
-          e += bf16r(d * d);
+          q[k] = bf16r((sym ? tq : bf16r(tq - qz)) * qs);
         }
       }
-#pragma unroll
-      for (int k = 0; k < CMAXSTEPS; ++k)
-        if (k == s) err[k] = e;
+      float e = (p > 0) ? es[(p - 1) * CROWS + r] : 0.f;
+      for (int t = 0; t < tn; ++t) {
+        const float d = dot_row(&xs[t * CG], q, h);
+        if (p == 0) {
+          if (h == 0) orgs[t * CROWS + r] = d;
+        } else {
+          const float dd = bf16r(d - orgs[t * CROWS + r]);
+          e += bf16r(dd * dd);
+        }
+      }
+      if (p > 0 && h == 0) es[(p - 1) * CROWS + r] = e;
+      if (p == 0) __syncthreads();  // orgs written by the even lanes, read by both
     }
   }
-  if (!live) return;
+  if (!live || h) return;
   float bmax = org_max, bmin = org_min, best = bf16r(1e9f);
-#pragma unroll
-  for (int s = 0; s < CMAXSTEPS; ++s) {
-    if (s < nsteps) {
-      const float em = bf16r(err[s] / (float)T);
-      if (em < best) {
-        best = em;
-        bmax = smax[s];
-        bmin = smin[s];
-      }
+  for (int s = 0; s < nsteps; ++s) {
+    const float em = bf16r(es[s * CROWS + r] / (float)T);
+    if (em < best) {
+      best = em;
+      const float f = factors[s];
+      bmax = bf16r(org_max * f);
+      bmin = clip_sym ? -bmax : bf16r(org_min * f);
     }
   }
   best_max[o * ng + g] = (uint16_t)(__float_as_uint(bmax) >> 16);
@@ -442,8 +462,8 @@ extern "C" int lcq_auto_clip_search(const void* w, const void* x, int64_t oc, in
   LCQ_REQUIRE(oc > 0 && ic > 0 && ic % CG == 0, "ic must be a multiple of 128");
   LCQ_REQUIRE(T > 0 && nsteps >= 1 && nsteps <= CMAXSTEPS, "bad T / nsteps (<= 16)");
   LCQ_REQUIRE(qmax > qmin, "qmax <= qmin");
-  dim3 grid((unsigned)((oc + 63) / 64), (unsigned)(ic / CG));
-  hipLaunchKernelGGL(k_auto_clip, grid, 64, 0, as_stream(stream),
+  dim3 grid((unsigned)((oc + CROWS - 1) / CROWS), (unsigned)(ic / CG));
+  hipLaunchKernelGGL(k_auto_clip, grid, 2 * CROWS, 0, as_stream(stream),
                      reinterpret_cast<const uint16_t*>(w), reinterpret_cast<const uint16_t*>(x),
                      oc, ic, (int)T, nsteps, reinterpret_cast<const float*>(factors),
                      (float)qmin, (float)qmax, sym, clip_sym,
