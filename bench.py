@@ -283,7 +283,7 @@ def main():
                        'share_of_step': round(v['total_ms'] / (elapsed * 1e3), 4)}
                    for k, v in sorted(kern.items(), key=lambda kv: -kv[1]['total_ms'])}
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             cpu = cpu_baseline(args, args.cpu_budget_s)
         line = {
             'metric': 'linear-layers quantized/sec (Llama-3-8B AWQ w4a16 g128)',
