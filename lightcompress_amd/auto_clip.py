@@ -29,6 +29,7 @@ class AutoClipper:
         self.padding_mask = padding_mask
         self.weight_clips = {}
         self.w_only = w_only
+        self.reduce_across_ranks = False  # set by the algorithm in replicate (DP) mode
         if clip_version != 'v1':
             raise NotImplementedError('clip_version v2 (learnable) is not on the device path')
         if not w_only:
@@ -48,7 +49,7 @@ class AutoClipper:
             max_val, min_val = self.auto_clip_layer(block_idx, n, m.weight, inputs,
                                                     n_sample_token=n_sample_token)
             _, ws, _ = world()
-            if ws > 1 and dist.is_initialized():
+            if self.reduce_across_ranks and ws > 1 and dist.is_initialized():
                 dist.all_reduce(max_val, op=dist.ReduceOp.SUM)
                 max_val /= ws
                 dist.all_reduce(min_val, op=dist.ReduceOp.SUM)

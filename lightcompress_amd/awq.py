@@ -108,7 +108,11 @@ class Awq(BaseBlockwiseQuantization):
             if lo < best:  # strict: the first minimum wins, as the reference's is_best
                 best, best_i = lo, n
         self.last_search = {'losses': loss_list, 'best_index': best_i}
-        return all_scales[best_i].clone()
+        best_scales = all_scales[best_i].clone()
+        if self.parallel_mode() == 'replicate':
+            from .parallel import awq_pick_best
+            best_scales = awq_pick_best(best, best_scales)  # awq.py:255-273
+        return best_scales
 
     @torch.no_grad()
     def block_transform(self, block, input_feat, block_kwargs):
@@ -116,6 +120,7 @@ class Awq(BaseBlockwiseQuantization):
             super().block_transform(block, input_feat, block_kwargs)
         if self.weight_clip:
             n_tok = self.config.get('calib', {}).get('seq_len', None)
+            self.auto_clipper.reduce_across_ranks = self.parallel_mode() == 'replicate'
             self.auto_clipper.run(block, self.block_idx, input_feat, n_sample_token=n_tok)
 
     @torch.no_grad()

@@ -23,6 +23,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import ops
+from . import parallel as P
 from .module_utils import (_LLMC_LINEAR_TYPES_, _REALQUANT_LINEAR_MAP_,
                            _TRANSFORMERS_LINEAR_TYPES_, EffcientFakeQuantLinear,
                            FakeQuantLinear, OriginFloatLinear)
@@ -60,10 +61,36 @@ class BlockwiseOpt:
                     kw['past_key_values'] = None
             self.n_samples = sum(d.shape[0] for d in input['data'])
 
+    def parallel_mode(self) -> str:
+        """'single' | 'shard_blocks' | 'replicate' (reference DP semantics).
+
+        Blocks can be sharded when each block's input does not depend on the quantization of
+        the previous one (quant_out False); otherwise ranks run the reference's
+        data-parallel replica scheme (statistics reconciled by collectives)."""
+        _, world = P.dist_world()
+        if world == 1:
+            return 'single'
+        mode = (self.quant_config.get('special', {}) or {}).get('parallel', None)
+        if mode:
+            return mode
+        if not self.data_free and not self.quant_config.get('quant_out', False):
+            return 'shard_blocks'
+        return 'replicate'
+
     def run_block_loop(self):
+        mode = self.parallel_mode()
+        rank, world = P.dist_world()
         for i in range(len(self.blocks)):
             self.block_idx = i
+            if mode == 'shard_blocks' and i % world != rank:
+                # not ours: only advance the float activation chain (quant_out False)
+                if not self.data_free:
+                    self.input['data'] = self.block_forward(self.blocks[i])
+                continue
             self.block_opt(self.blocks[i])
+        if mode == 'shard_blocks':
+            for i, block in enumerate(self.blocks):
+                P.broadcast_block(block, owner=i % world)
 
     def cache_input_hook(self, m, x, y, name, feat_dict):
         # device-resident, shared (no copy): see module docstring

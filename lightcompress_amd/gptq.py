@@ -106,7 +106,8 @@ class GPTQ(BaseBlockwiseQuantization):
     def layer_transform(self, layer, name):
         H = self.layers_cache[name]['acc'].H.clone()  # consumed by prepare(); shared by members
         _, ws, _ = world()
-        if ws > 1 and dist.is_initialized():
+        replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
+        if replicate:
             # one all-reduce of the finished Hessian per layer (the reference reduces after
             # every sample); averaging matches its H /= world_size
             dist.all_reduce(H, op=dist.ReduceOp.SUM)
@@ -116,7 +117,7 @@ class GPTQ(BaseBlockwiseQuantization):
             fixed = (layer.buf_scales, getattr(layer, 'buf_zeros', None))
         r = gptq_core.quantize_layer(layer.weight.data, H, self.wquantizer,
                                      actorder=self.actorder, percdamp=self.percdamp,
-                                     fixed=fixed)
+                                     fixed=fixed, shard_rows=replicate)
         layer.weight.data = r['weight']
         if r['perm'] is not None:
             layer.register_buffer('buf_perm', r['perm'])

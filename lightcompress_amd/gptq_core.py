@@ -98,7 +98,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
 
 @torch.no_grad()
 def quantize_layer(W: torch.Tensor, H: torch.Tensor, wquantizer, actorder=True,
-                   percdamp=0.01, fixed=None, losses=False):
+                   percdamp=0.01, fixed=None, losses=False, shard_rows=False):
     """Full GPTQ transform of one linear. Returns dict(weight fp32 (original column order),
     scales / zeros [rows*ng, 1] fp32 (merge_qparams order, permuted groups), perm, invperm,
     loss)."""
@@ -108,7 +108,22 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor, wquantizer, actorder=True,
     if group is not None and group not in (32, 64, 128):
         raise NotImplementedError('device GPTQ supports group_size 32/64/128')
     Wp, U, perm = prepare(W, H, actorder, percdamp)
-    s, z, L = column_loop(Wp, U, bit, sym, group, qmin, qmax, fixed=fixed, losses=losses)
+    if shard_rows:
+        # rows are independent given U: every rank runs the column loop on its
+        # row range, then the quantized rows + qparams are all-gathered (bit-identical to 1 GPU)
+        from . import parallel as P
+        rank, world = P.dist_world()
+        r0, r1 = P.row_shard(Wp.shape[0], rank, world)
+        Wl = Wp[r0:r1].contiguous()
+        fx = None if fixed is None else tuple(None if f is None else f.reshape(-1)[r0:r1]
+                                              for f in fixed)
+        s, z, L = column_loop(Wl, U, bit, sym, group, qmin, qmax, fixed=fx, losses=losses)
+        Wp = P.gather_rows(Wl, Wp.shape[0])
+        s = None if s is None else P.gather_rows(s, Wp.shape[0])
+        z = None if z is None else P.gather_rows(z, Wp.shape[0])
+        L = None if L is None else P.gather_rows(L, Wp.shape[0])
+    else:
+        s, z, L = column_loop(Wp, U, bit, sym, group, qmin, qmax, fixed=fixed, losses=losses)
     invperm = torch.argsort(perm) if perm is not None else None
     weight = Wp[:, invperm] if invperm is not None else Wp
     return dict(weight=weight, scales=None if s is None else s.reshape(-1, 1),

@@ -1,0 +1,88 @@
+"""Two ranks on one GPU (gloo over device tensors): block-sharded AWQ (quant_out False) and
+row-sharded GPTQ must reproduce the single-process result bit for bit (the
+per-unit math is identical, only the placement changes)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model_and_calib(layers):
+    from transformers import LlamaConfig
+    from lightcompress_amd.llama import Llama
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                      num_key_value_heads=2, num_hidden_layers=layers, vocab_size=128,
+                      max_position_embeddings=512, rms_norm_eps=1e-5)
+    model = Llama.random(cfg, device='cuda:0', seed=3)
+    g = torch.Generator(device='cuda:0').manual_seed(9)
+    x = torch.randn(4, 64, 256, generator=g, device='cuda:0').to(torch.bfloat16)
+    return model, {'data': [x], 'kwargs': [model.rotary_kwargs(64)]}
+
+
+AWQ = {'calib': {'seq_len': 64},
+       'quant': {'method': 'Awq', 'weight': {'bit': 4, 'symmetric': True,
+                                             'granularity': 'per_group', 'group_size': 128},
+                 'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True,
+                             'clip_sym': True}, 'quant_out': False}}
+GPTQ = {'quant': {'method': 'GPTQ', 'weight': {'bit': 4, 'symmetric': False,
+                                               'granularity': 'per_group', 'group_size': 128},
+                  'special': {'actorder': True, 'static_groups': False, 'percdamp': 0.01,
+                              'blocksize': 128, 'true_sequential': True},
+                  'quant_out': True}}
+
+
+def _run(cfg_dict, layers):
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.utils import load_config
+    model, calib = _model_and_calib(layers)
+    algo = build_algo(model, load_config(cfg_dict), calib)
+    algo.run_block_loop()
+    return {f'{i}.{n}': m.weight.detach().float().cpu()
+            for i, b in enumerate(model.blocks) for n, m in model.get_block_linears(b).items()}
+
+
+def _worker(rank, world, port, cfg, layers, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK='0')
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        out = _run(cfg, layers)
+        q.put((rank, out if rank == 0 else None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('name,cfg,layers', [('awq_shard_blocks', AWQ, 4),
+                                             ('gptq_shard_rows', GPTQ, 2)])
+def test_two_ranks_match_single(dev, name, cfg, layers):
+    for k in ('RANK', 'WORLD_SIZE'):
+        os.environ.pop(k, None)
+    single = _run(cfg, layers)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, cfg, layers, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    multi = res[0]
+    assert single.keys() == multi.keys()
+    for k in single:
+        assert torch.equal(single[k], multi[k]), k
