@@ -135,6 +135,12 @@ int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, c
                    const void* z_in, void* s_out, void* z_out, int64_t ng_total, void* err,
                    void* losses, void* stream);
 
+/* GPTQ trailing update W[:, c1:] -= err[:, :cnt] @ U[c0:c0+cnt, c1:] (gptq.py:244) on fp32
+ * MFMA (k-ordered fma chain: deterministic and independent of the row range, so row-sharded
+ * GPTQ is bit-identical to one GPU). err [rows, 128] fp32 from lcq_gptq_block. */
+int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, int cnt, int64_t c1,
+                      const void* err, const void* U, int64_t ldu, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * AWQ (awq.py) and auto-clip (auto_clip.py) building blocks. dtype = BF16/F16/F32; each op
  * rounds to dtype like the reference's torch expressions.

@@ -148,3 +148,113 @@ extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, i
   }
   return check_launch("lcq_gptq_block");
 }
+
+// ---------------------------------------------------------------------------------------
+// GPTQ trailing update  W[:, c1:] -= E[:, :cnt] @ U[c0:c0+cnt, c1:]   (gptq.py:244)
+// fp32 MFMA v_mfma_f32_32x32x2_f32: bit-for-bit a k-ordered fmaf chain, so every output
+// element's value is independent of the tiling / row range (row-sharded GPTQ on N GPUs is
+// bit-identical to one GPU). The product is rounded to fp32 and then subtracted, like the
+// reference's `W -= Err @ Hinv` (two roundings). 128x128 tile per 256-thread workgroup,
+// 2x2 waves of 64x64 = 2x2 MFMA 32x32 tiles, K staged through LDS 32 at a time.
+// ---------------------------------------------------------------------------------------
+namespace lcq {
+
+typedef float v16f __attribute__((ext_vector_type(16)));
+constexpr int TT = 128;   // output tile
+constexpr int TK = 32;    // k chunk
+
+__global__ void __launch_bounds__(256)
+    k_gptq_trailing(float* __restrict__ W, int64_t rows, int64_t ld, int64_t c0, int cnt,
+                    int64_t c1, const float* __restrict__ E, const float* __restrict__ U,
+                    int64_t ldu) {
+  __shared__ float As[TK][TT];  // As[k][row]
+  __shared__ float Bs[TK][TT];  // Bs[k][col]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t r0 = (int64_t)blockIdx.y * TT;
+  const int64_t j0 = c1 + (int64_t)blockIdx.x * TT;
+  v16f acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+  for (int k0 = 0; k0 < GB; k0 += TK) {
+    __syncthreads();
+    // E tile: 128 rows x 32 k, float4 along k, stored transposed As[k][row]
+#pragma unroll
+    for (int it = 0; it < (TT * TK / 4) / 256; ++it) {
+      const int idx = it * 256 + tid;
+      const int row = idx / (TK / 4), k4 = (idx % (TK / 4)) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r0 + row < rows) v = *reinterpret_cast<const float4*>(E + (r0 + row) * GB + k0 + k4);
+      As[k4 + 0][row] = (k0 + k4 + 0 < cnt) ? v.x : 0.f;
+      As[k4 + 1][row] = (k0 + k4 + 1 < cnt) ? v.y : 0.f;
+      As[k4 + 2][row] = (k0 + k4 + 2 < cnt) ? v.z : 0.f;
+      As[k4 + 3][row] = (k0 + k4 + 3 < cnt) ? v.w : 0.f;
+    }
+    // U tile: 32 k x 128 cols, float4 along cols
+#pragma unroll
+    for (int it = 0; it < (TT * TK / 4) / 256; ++it) {
+      const int idx = it * 256 + tid;
+      const int k = idx / (TT / 4), c4 = (idx % (TT / 4)) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k0 + k < cnt) {
+        const float* src = U + (c0 + k0 + k) * ldu + j0 + c4;
+        if (j0 + c4 + 3 < ld) {
+          v = *reinterpret_cast<const float4*>(src);
+        } else {
+          if (j0 + c4 + 0 < ld) v.x = src[0];
+          if (j0 + c4 + 1 < ld) v.y = src[1];
+          if (j0 + c4 + 2 < ld) v.z = src[2];
+        }
+      }
+      *reinterpret_cast<float4*>(&Bs[k][c4]) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < TK; kk += 2) {
+      float a[2], b[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        a[t] = As[kk + (lane >> 5)][wr * 64 + t * 32 + (lane & 31)];
+        b[t] = Bs[kk + (lane >> 5)][wc * 64 + t * 32 + (lane & 31)];
+      }
+#pragma unroll
+      for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+        for (int tb = 0; tb < 2; ++tb)
+          acc[ta][tb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
+    }
+  }
+  // epilogue (C layout: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5))
+#pragma unroll
+  for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int64_t r = r0 + wr * 64 + ta * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+        const int64_t c = j0 + wc * 64 + tb * 32 + (lane & 31);
+        if (r < rows && c < ld) W[r * ld + c] = W[r * ld + c] - acc[ta][tb][reg];
+      }
+}
+
+}  // namespace lcq
+
+extern "C" int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, int cnt,
+                                 int64_t c1, const void* err, const void* U, int64_t ldu,
+                                 void* stream) {
+  LCQ_REQUIRE(rows > 0 && ld > 0 && cnt > 0 && cnt <= GB, "bad shape");
+  LCQ_REQUIRE(c0 >= 0 && c0 + cnt <= ldu && c1 >= c0 + cnt && c1 <= ld && ld <= ldu,
+              "bad column ranges");
+  if (c1 == ld) return LCQ_OK;
+  const dim3 grid((unsigned)((ld - c1 + TT - 1) / TT), (unsigned)((rows + TT - 1) / TT));
+  hipLaunchKernelGGL(k_gptq_trailing, grid, 256, 0, as_stream(stream),
+                     reinterpret_cast<float*>(W), rows, ld, c0, cnt, c1,
+                     reinterpret_cast<const float*>(err), reinterpret_cast<const float*>(U),
+                     ldu);
+  return check_launch("lcq_gptq_trailing");
+}

@@ -73,7 +73,8 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     """Blocked OBS loop (gptq.py:198-244) on permuted fp32 W, in place.
 
     Per 128-column block: the HIP kernel runs the in-block sequential loop (bit-exact rank-1
-    updates), then the trailing update ``W[:, i2:] -= Err @ U[i1:i2, i2:]`` (fp32 GEMM)."""
+    updates), then the trailing update ``W[:, i2:] -= Err @ U[i1:i2, i2:]`` (fp32 MFMA kernel,
+    deterministic k order)."""
     rows, cols = W.shape
     dev = W.device
     U = U.contiguous()
@@ -92,7 +93,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
         ops.gptq_block(W, i1, cnt, U, group or 0, qmin, qmax, sym, s_out, z_out, err, L,
                        s_in, z_in)
         if i2 < cols:
-            W[:, i2:] -= err[:, :cnt].matmul(U[i1:i2, i2:])
+            ops.gptq_trailing(W, i1, cnt, i2, err, U)
     return s_out, z_out, L
 
 

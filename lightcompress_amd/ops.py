@@ -168,6 +168,14 @@ def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: i
            N.ptr(z_out), int(ng_total), N.ptr(err), N.ptr(losses), N.stream_of(W))
 
 
+def gptq_trailing(W: torch.Tensor, c0: int, cnt: int, c1: int, err: torch.Tensor,
+                  U: torch.Tensor):
+    """W[:, c1:] -= err[:, :cnt] @ U[c0:c0+cnt, c1:] in place (fp32 MFMA, deterministic)."""
+    rows, ld = W.shape
+    N.call('lcq_gptq_trailing', N.ptr(W), rows, ld, int(c0), int(cnt), int(c1), N.ptr(err),
+           N.ptr(U), U.shape[1], N.stream_of(W))
+
+
 def absmean_cols(x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
     """mean over all leading dims of |x| per channel (Awq.get_act_scale, awq.py:74-85)."""
     x2 = x.reshape(-1, x.shape[-1])

@@ -122,3 +122,26 @@ def test_layer_end_to_end_vs_reference(dev, name):
     same = (fq == ref).float().mean().item()
     assert same >= 0.999, same
     assert torch.allclose(fq.float(), ref.float(), atol=2 * c['scales'].abs().max().item())
+
+
+@pytest.mark.parametrize('rows,ic,c0', [(300, 512, 128), (256, 4096, 0), (129, 392, 128)])
+def test_trailing_update(dev, rows, ic, c0):
+    """lcq_gptq_trailing vs fp64, and bit-identical on any row sub-range (row sharding)."""
+    from lightcompress_amd import ops
+    g = torch.Generator(device=dev).manual_seed(rows + ic)
+    W = torch.randn(rows, ic, generator=g, device=dev)
+    U = torch.randn(ic, ic, generator=g, device=dev).triu().contiguous()
+    err = torch.randn(rows, 128, generator=g, device=dev)
+    cnt = min(128, ic - c0)
+    c1 = c0 + cnt
+    ref = W.double().clone()
+    ref[:, c1:] -= err[:, :cnt].double() @ U[c0:c1, c1:].double()
+    out = W.clone()
+    ops.gptq_trailing(out, c0, cnt, c1, err, U)
+    assert torch.equal(out[:, :c1], W[:, :c1])
+    tol = 1e-5 * math.sqrt(cnt) * (1 + ref[:, c1:].abs())
+    assert ((out[:, c1:].double() - ref[:, c1:]).abs() <= tol).all()
+    h = rows // 3
+    part = W[h:].clone()
+    ops.gptq_trailing(part, c0, cnt, c1, err[h:].contiguous(), U)
+    assert torch.equal(part, out[h:])
