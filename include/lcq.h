@@ -37,6 +37,7 @@ enum lcq_dtype {
   LCQ_I32 = 5,
   LCQ_FP8E4M3 = 6,
   LCQ_F64 = 7,
+  LCQ_FP8E5M2 = 8,
 };
 
 enum lcq_status {
@@ -180,6 +181,56 @@ int lcq_auto_clip_search(const void* w, const void* x, int64_t oc, int64_t ic, i
  * cmin NULL -> -cmax. In place allowed. */
 int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t cols, int64_t group,
                    const void* cmax, const void* cmin, void* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * FP8 (FloatQuantizer, quant.py:963-1229; kernel.py:7-138; quant.py:18-43).
+ * fmt = LCQ_FP8E4M3 (float8_e4m3fn) or LCQ_FP8E5M2. The fp8 rounding is
+ * torch's native cast (c10 Float8_e4m3fn / Float8_e5m2, RNE); the reference's qtorch
+ * float_quantize step is absent from this image, so that step is parity-unpinned.
+ * ------------------------------------------------------------------------------------- */
+/* max |x| over n elements -> out (one fp32 on device; zeroed by the call). Per-tensor
+ * get_minmax_range (quant.py:133-135): max(|torch.max|, |torch.min|) == max|x|. */
+int lcq_absmax(const void* x, int x_dtype, int64_t n, void* out, void* stream);
+
+/* Dynamic FP8 quant over groups of `group` consecutive elements of x [rows, cols]
+ * (per_group / per_channel / per_token; kernel.py act_quant = group 128, ct F32, clamp 0,
+ * add_zero 0), or per tensor when tensor_amax (device fp32 from lcq_absmax) is given.
+ * s = rnd_ct(max(amax, clamp_min) / qmax) (clamp skipped when clamp_min == 0; qmax = finfo.max
+ * of the format, 448 / 57344, or the config's float_range; per tensor the division is fp32);
+ * add_zero (quant.py quant()): s == 0 -> 1 and `+ 0` after the division;
+ * code = cast(rnd_ct(x / s) [+ 0]); fq = rnd_fq(float(code) * s).
+ * ct_dtype = x dtype (quant.py) or F32 (kernel.py). Any of codes_out (uint8 [rows, cols]),
+ * fq_out, scales_out (ct dtype per group; one fp32 per tensor) may be NULL. */
+int lcq_fp8_quant(const void* x, int x_dtype, int64_t rows, int64_t cols, int64_t group,
+                  int fmt, int ct_dtype, float qmax, float clamp_min, int add_zero,
+                  const void* tensor_amax, void* codes_out, void* fq_out, int fq_dtype,
+                  void* scales_out, void* stream);
+
+/* FP8 quant with given scales (fake/real_quant_*_static, quant.py:1061-1076, 1119-1159):
+ * s = rnd_ct(scales[e / group]) (0 -> 1); same cast / fake-quant rules as lcq_fp8_quant.
+ * ct_dtype = torch.promote_types(x, scales). */
+int lcq_fp8_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols, int64_t group,
+                         int fmt, int ct_dtype, const void* scales, int s_dtype, int add_zero,
+                         void* codes_out, void* fq_out, int fq_dtype, void* stream);
+
+/* 128x128-block FP8 quant of x [M, N] (N % 8 == 0): per_block FloatQuantizer (clamp_min 1e-5,
+ * add_zero 1; quant.py:132-143, 636-641) and weight_cast_to_fp8 (kernel.py:57-81: clamp 0,
+ * add_zero 0). scales_out fp32 [ceil(M/128), ceil(N/128)]; codes uint8 [M, N]. */
+int lcq_fp8_quant_blocks(const void* x, int x_dtype, int64_t M, int64_t N, int block, int fmt,
+                         float qmax, float clamp_min, int add_zero, void* codes_out, void* fq_out,
+                         int fq_dtype, void* scales_out, void* stream);
+
+/* weight_cast_to_bf16 (kernel.py:84-138, quant.py:18-31): out = rnd_out(float(code) *
+ * scales[r / block][c / block]); codes uint8 [M, N], scales fp32 [ceil(M/b), ceil(N/b)]. */
+int lcq_fp8_dequant_blocks(const void* codes, int fmt, int64_t M, int64_t N, int block,
+                           const void* scales, void* out, int out_dtype, void* stream);
+
+/* FloatQuantizer use_qtorch=False fake quant (get_float_qparams, quant.py:1005-1027, and
+ * quant/dequant :1061-1076): per group of `group` elements, power-of-two per-element scales
+ * for an e_bits/m_bits float format; every op rounds to the tensor dtype (fp32 when
+ * e_bits >= 5, quant.py:1014). */
+int lcq_fp_emul_quant(const void* x, int x_dtype, int64_t rows, int64_t cols, int64_t group,
+                      int e_bits, int m_bits, void* fq_out, int fq_dtype, void* stream);
 
 #ifdef __cplusplus
 }

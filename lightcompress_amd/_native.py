@@ -16,10 +16,11 @@ import torch
 _LIB_PATH = Path(__file__).resolve().parent / '_lib' / 'liblcq.so'
 _HEADER = Path(__file__).resolve().parent.parent / 'include' / 'lcq.h'
 
-F32, F16, BF16, I8, U8, I32, FP8E4M3, F64 = range(8)
+F32, F16, BF16, I8, U8, I32, FP8E4M3, F64, FP8E5M2 = range(9)
 _DT = {
     torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16, torch.int8: I8,
     torch.uint8: U8, torch.int32: I32, torch.float8_e4m3fn: FP8E4M3, torch.float64: F64,
+    torch.float8_e5m2: FP8E5M2,
 }
 
 _vp = ctypes.c_void_p
@@ -51,6 +52,15 @@ SIGNATURES = {
     'lcq_auto_clip_search': ([_vp, _vp, _i64, _i64, _i64, _int, _int, _vp, _int, _int, _int,
                               _int, _vp, _vp, _vp], _int),
     'lcq_clip_apply': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _vp, _vp], _int),
+    'lcq_absmax': ([_vp, _int, _i64, _vp, _vp], _int),
+    'lcq_fp8_quant': ([_vp, _int, _i64, _i64, _i64, _int, _int, _f32, _f32, _int, _vp, _vp, _vp,
+                       _int, _vp, _vp], _int),
+    'lcq_fp8_quant_static': ([_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int, _int, _vp,
+                              _vp, _int, _vp], _int),
+    'lcq_fp8_quant_blocks': ([_vp, _int, _i64, _i64, _int, _int, _f32, _f32, _int, _vp, _vp,
+                              _int, _vp, _vp], _int),
+    'lcq_fp8_dequant_blocks': ([_vp, _int, _i64, _i64, _int, _vp, _vp, _int, _vp], _int),
+    'lcq_fp_emul_quant': ([_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int, _vp], _int),
 }
 
 _lib = None

@@ -127,8 +127,18 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
 
     # ---- weight / activation quant callbacks (:46-82) ---------------------------------------
     def w_qdq(self, module, wquantizer):
+        """:46-66; block-fp8 weights (DeepSeek-V3 checkpoints) round-trip through bf16 with
+        the kernel.py casts, which the reference selects on FP8-capable GPUs (:20-26)."""
         args = {'lowbound_factor': getattr(module, 'buf_lowbound_factor', None),
                 'upbound_factor': getattr(module, 'buf_upbound_factor', None)}
+        if module.weight.data.dtype == torch.float8_e4m3fn:
+            from .kernel import weight_cast_to_bf16, weight_cast_to_fp8
+            bs = getattr(self, 'fp8_block_size', 128)
+            tmp = weight_cast_to_bf16(module.weight, module.weight_scale_inv,
+                                      bs).to(torch.bfloat16)
+            tmp = wquantizer.fake_quant_weight_dynamic(tmp, args)
+            tmp, module.weight_scale_inv.data = weight_cast_to_fp8(tmp, bs)
+            return tmp
         return wquantizer.fake_quant_weight_dynamic(module.weight, args)
 
     def w_q(self, module, wquantizer):

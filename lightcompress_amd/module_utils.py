@@ -164,6 +164,11 @@ class VllmRealQuantLinear(nn.Module):
     @classmethod
     @torch.no_grad()
     def quant_pack(cls, module, w_q, quant_config):
+        if module.weight.data.dtype == torch.float8_e4m3fn:  # module_utils.py:917-922
+            from .kernel import weight_cast_to_bf16
+            module.weight.data = weight_cast_to_bf16(
+                module.weight.data, module.weight_scale_inv.data,
+                module.block_size).to(torch.bfloat16)
         weight, scales, zeros = w_q(module)
         if quant_config['weight'].get('need_pack', False):
             weight, scales = cls.pack(weight, scales, quant_config)

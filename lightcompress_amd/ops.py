@@ -268,3 +268,141 @@ def clip_apply(w: torch.Tensor, group: int, cmax: torch.Tensor, cmin: torch.Tens
 
 
 code_dtype = _code_dtype
+
+
+# ---------------------------------------------------------------------------------------
+# FP8 (FloatQuantizer / kernel.py)
+# ---------------------------------------------------------------------------------------
+_FP8 = {'e4m3': torch.float8_e4m3fn, 'e5m2': torch.float8_e5m2}
+
+
+def fp8_dtype(bit: str) -> torch.dtype:
+    if bit not in _FP8:
+        raise NotImplementedError(f'FP8 real quant supports e4m3 / e5m2, not {bit}')
+    return _FP8[bit]
+
+
+def absmax(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """max |x| as a device fp32 scalar (shape [1])."""
+    x = x.contiguous()
+    if out is None:
+        out = torch.empty(1, dtype=torch.float32, device=x.device)
+    N.call('lcq_absmax', N.ptr(x), N.dt(x.dtype), x.numel(), N.ptr(out), N.stream_of(x))
+    return out
+
+
+def fp8_max(fp8: torch.dtype) -> float:
+    return float(torch.finfo(fp8).max)
+
+
+def fp8_quant(x: torch.Tensor, group: int, fp8: torch.dtype, *, ct_dtype=None,
+              qmax: float | None = None, clamp_min: float = 1e-5, add_zero: bool = True, per_tensor: bool = False,
+              codes: bool = True, fq: bool = False, fq_dtype=None,
+              scales: bool = True) -> dict:
+    """Dynamic FP8 quantization of a 2-D ``x`` over groups of ``group`` columns, or per tensor.
+
+    Defaults follow FloatQuantizer (quant.py:545-559, 1061-1076): compute dtype = x dtype,
+    scale clamp 1e-5, ``+ zeros``. kernel.py ``act_quant`` = ct fp32, clamp 0, no add_zero.
+    """
+    assert x.dim() == 2, 'x must be 2-D'
+    x = x.contiguous()
+    rows, cols = x.shape
+    ct = x.dtype if ct_dtype is None else ct_dtype
+    res = {}
+    amax = absmax(x) if per_tensor else None
+    if per_tensor:
+        group = cols
+    c = torch.empty((rows, cols), dtype=fp8, device=x.device) if codes else None
+    f = torch.empty((rows, cols), dtype=fq_dtype or x.dtype, device=x.device) if fq else None
+    ns = 1 if per_tensor else rows * cols // group
+    sdt = torch.float32 if per_tensor else ct  # 0-dim / 0-dim promotes to fp32
+    s = torch.empty((ns, 1), dtype=sdt, device=x.device) if scales else None
+    qmax = fp8_max(fp8) if qmax is None else float(qmax)
+    N.call('lcq_fp8_quant', N.ptr(x), N.dt(x.dtype), rows, cols, group, N.dt(fp8), N.dt(ct),
+           qmax, float(clamp_min), int(add_zero), N.ptr(amax), N.ptr(c), N.ptr(f),
+           N.dt(f.dtype) if f is not None else 0, N.ptr(s), N.stream_of(x))
+    if codes:
+        res['codes'] = c
+    if fq:
+        res['fq'] = f
+    if scales:
+        res['scales'] = s
+    return res
+
+
+def fp8_quant_static(x: torch.Tensor, scales: torch.Tensor, fp8: torch.dtype, *,
+                     ct_dtype=None, add_zero: bool = True, codes: bool = True,
+                     fq: bool = False, fq_dtype=None) -> dict:
+    """FP8 quant of ``x`` with given scales; one scale per ``x.numel() / scales.numel()``
+    consecutive elements (per tensor / per row / per group layouts)."""
+    x = x.contiguous()
+    s = scales.contiguous()
+    if x.numel() % s.numel():
+        raise ValueError('scales do not tile the tensor')
+    group = x.numel() // s.numel()
+    ct = ct_dtype or torch.promote_types(x.dtype, s.dtype)
+    c = torch.empty(x.shape, dtype=fp8, device=x.device) if codes else None
+    f = torch.empty(x.shape, dtype=fq_dtype or x.dtype, device=x.device) if fq else None
+    rows = x.shape[0] if x.dim() > 1 else 1
+    N.call('lcq_fp8_quant_static', N.ptr(x), N.dt(x.dtype), rows, x.numel() // rows, group,
+           N.dt(fp8), N.dt(ct), N.ptr(s), N.dt(s.dtype), int(add_zero), N.ptr(c), N.ptr(f),
+           N.dt(f.dtype) if f is not None else 0, N.stream_of(x))
+    res = {}
+    if codes:
+        res['codes'] = c
+    if fq:
+        res['fq'] = f
+    return res
+
+
+def fp8_quant_blocks(x: torch.Tensor, fp8: torch.dtype = torch.float8_e4m3fn, block: int = 128,
+                     *, qmax: float | None = None, clamp_min: float = 1e-5, add_zero: bool = True, codes: bool = True,
+                     fq: bool = False, fq_dtype=None) -> dict:
+    """128x128-block FP8 quant (per_block FloatQuantizer / weight_cast_to_fp8)."""
+    assert x.dim() == 2, 'x must be 2-D'
+    x = x.contiguous()
+    M, Nn = x.shape
+    c = torch.empty((M, Nn), dtype=fp8, device=x.device) if codes else None
+    f = torch.empty((M, Nn), dtype=fq_dtype or x.dtype, device=x.device) if fq else None
+    s = torch.empty(((M + block - 1) // block, (Nn + block - 1) // block), dtype=torch.float32,
+                    device=x.device)
+    qmax = fp8_max(fp8) if qmax is None else float(qmax)
+    N.call('lcq_fp8_quant_blocks', N.ptr(x), N.dt(x.dtype), M, Nn, block, N.dt(fp8), qmax,
+           float(clamp_min), int(add_zero), N.ptr(c), N.ptr(f),
+           N.dt(f.dtype) if f is not None else 0, N.ptr(s), N.stream_of(x))
+    res = {'scales': s}
+    if codes:
+        res['codes'] = c
+    if fq:
+        res['fq'] = f
+    return res
+
+
+def fp8_dequant_blocks(codes: torch.Tensor, scales: torch.Tensor, block: int = 128,
+                       out_dtype: torch.dtype = torch.bfloat16,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """weight_cast_to_bf16: rnd_out(float(code) * scale[block])."""
+    assert codes.dim() == 2 and scales.dim() == 2
+    codes = codes.contiguous()
+    scales = scales.contiguous().float()
+    M, Nn = codes.shape
+    if scales.shape != ((M + block - 1) // block, (Nn + block - 1) // block):
+        raise ValueError(f'scale shape {tuple(scales.shape)} does not tile {M}x{Nn} by {block}')
+    if out is None:
+        out = torch.empty((M, Nn), dtype=out_dtype, device=codes.device)
+    N.call('lcq_fp8_dequant_blocks', N.ptr(codes), N.dt(codes.dtype), M, Nn, block,
+           N.ptr(scales), N.ptr(out), N.dt(out.dtype), N.stream_of(codes))
+    return out
+
+
+def fp_emul_quant(x: torch.Tensor, group: int, e_bits: int, m_bits: int,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """FloatQuantizer use_qtorch=False fake quant over groups of ``group`` columns."""
+    assert x.dim() == 2, 'x must be 2-D'
+    x = x.contiguous()
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    N.call('lcq_fp_emul_quant', N.ptr(x), N.dt(x.dtype), rows, cols, group, e_bits, m_bits,
+           N.ptr(out), N.dt(out.dtype), N.stream_of(x))
+    return out

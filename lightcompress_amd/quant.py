@@ -7,9 +7,9 @@ reproduce the reference's per-op dtype rounding bit for bit. There is no CPU pat
 live on the GPU.
 
 Supported on the device path (the hot path of SURVEY.md §8a): calib_algo ``minmax``,
-granularity per_group / per_channel / per_token / per_tensor / per_head, round_zp=True,
-bit 2..8, dynamic and static qparams, fake quant, real quant (+ vLLM / AutoAWQ packing in
-``module_utils``). Not yet supported (raise NotImplementedError): mse / hqq / learnable / static
+granularity per_group / per_channel / per_token / per_tensor / per_head (+ per_block for FP8),
+round_zp=True, bit 2..8, dynamic and static qparams, fake quant, real quant (+ vLLM / AutoAWQ
+packing in ``module_utils``); FP8 e4m3 / e5m2 (``FloatQuantizer``). Not yet supported (raise NotImplementedError): mse / hqq / learnable / static
 histogram calibration, ``int_indices`` mixed precision, STE rounding, ``rounding`` overrides.
 """
 from __future__ import annotations
@@ -18,7 +18,23 @@ import torch
 
 from . import ops
 
-__all__ = ['BaseQuantizer', 'IntegerQuantizer', 'FloatQuantizer']
+__all__ = ['BaseQuantizer', 'IntegerQuantizer', 'FloatQuantizer', 'weight_cast_to_bf16',
+           'weight_cast_to_fp8']
+
+
+def weight_cast_to_bf16(weight, scale, block_size):
+    """quant.py:18-31: dequant(weight.float(), scale) per block, then bf16."""
+    return ops.fp8_dequant_blocks(weight.contiguous(), scale, block_size,
+                                  out_dtype=torch.bfloat16)
+
+
+def weight_cast_to_fp8(weight, block_size):
+    """quant.py:34-43: per_block FloatQuantizer real quant (clamp 1e-5, ``+ zeros``)."""
+    if block_size != 128:
+        raise NotImplementedError('block-fp8 supports block_size 128')
+    r = ops.fp8_quant_blocks(weight, torch.float8_e4m3fn, 128, qmax=448.0, clamp_min=1e-5,
+                             add_zero=True)
+    return r['codes'], r['scales']
 
 
 class BaseQuantizer:
@@ -61,11 +77,23 @@ class BaseQuantizer:
             return tensor
         if self.granularity == 'per_head':
             return tensor.reshape(self.head_num, -1)
+        if self.granularity == 'per_block':  # quant.py:636-641 (zero pad to block multiples)
+            m, n = tensor.shape
+            b = self.block_size
+            pm, pn = -(-m // b) * b, -(-n // b) * b
+            t = torch.zeros((pm, pn), dtype=tensor.dtype, device=tensor.device)
+            t[:m, :n] = tensor
+            return t.view(-1, b, pn // b, b)
         return tensor
 
     def restore_tensor(self, tensor, shape):
         if tensor.shape == shape:
             return tensor
+        if self.granularity == 'per_block':  # quant.py:648-652
+            try:
+                return tensor.reshape(-1, shape[-1])[:shape[0], :]
+            except RuntimeError:
+                return tensor.reshape(shape[0], -1)[:, :shape[1]]
         try:
             return tensor.reshape(shape)
         except RuntimeError:
@@ -277,19 +305,251 @@ class IntegerQuantizer(BaseQuantizer):
                 f'kwargs={self.kwargs}, qmin={self.qmin}, qmax={self.qmax})')
 
 
+_FLOAT_RANGES = {  # quant.py:982-996
+    ('e4m3', 8): torch.float8_e4m3fn,
+    ('e5m2', 8): torch.float8_e5m2,
+    ('e3m2', 6): (-28, 28),
+    ('e4m7', 12): (-510, 510),
+    ('e2m1', 4): (-6, 6),
+}
+
+
 class FloatQuantizer(BaseQuantizer):
-    """FloatQuantizer (quant.py:963-1229). Device path: FP8 e4m3 with native OCP cast
-    (``use_qtorch`` semantics; qtorch itself is absent, so that path is parity-unpinned)."""
+    """FloatQuantizer (quant.py:963-1229) on the lcq FP8 kernels.
+
+    ``use_qtorch=True``: absmax scales in the tensor dtype (fp32 for per_block), then the
+    value rounding. qtorch's ``float_quantize`` is not in this image, so the rounding is the
+    native cast (torch / c10 ``Float8_e4m3fn`` / ``Float8_e5m2`` RNE) -- exact for the scales
+    and every surrounding op, parity-unpinned for qtorch's own rounding.
+    Only e4m3 / e5m2 have a native cast; other formats need qtorch and raise.
+    ``use_qtorch=False``: ``get_float_qparams`` emulation (per-element power-of-two scales),
+    bit-exact for bf16 / fp16 tensors (``lcq_fp_emul_quant``).
+    """
 
     def __init__(self, bit, symmetric, granularity, **kwargs):
         super().__init__(bit, symmetric, granularity, **kwargs)
         self.sym = True
         self.quant_type = 'float-quant'
-        self.e_bits = int(bit[1])
-        self.m_bits = int(bit[-1])
-        self.num_bits = self.e_bits + self.m_bits + 1
-        self.use_qtorch = kwargs.get('use_qtorch')
+        self.e_bits = int(self.bit[1])
+        self.m_bits = int(self.bit[-1])
+        self.sign_bits = 1
+        self.num_bits = self.e_bits + self.m_bits + self.sign_bits
+        self.default_bias = 2 ** (self.e_bits - 1)
+        self.dst_nbins = 2 ** self.num_bits
+        self.use_qtorch = self.kwargs.get('use_qtorch')
+        self.fp8_dtype = {'e4m3': torch.float8_e4m3fn, 'e5m2': torch.float8_e5m2}.get(bit)
+        if self.use_qtorch:
+            if 'float_range' in self.kwargs:
+                self.qmin, self.qmax = self.kwargs['float_range']
+            else:
+                key = (self.bit, self.num_bits)
+                if key not in _FLOAT_RANGES:
+                    raise NotImplementedError('Only 4, 6, 8, and 12-bit quantization is supported.')
+                r = _FLOAT_RANGES[key]
+                if isinstance(r, tuple):
+                    self.qmin, self.qmax = r
+                else:
+                    fi = torch.finfo(r)
+                    self.qmin, self.qmax = fi.min, fi.max
+            self.qmax = torch.tensor(self.qmax)
+            self.qmin = torch.tensor(self.qmin)
+
+    # -- helpers ---------------------------------------------------------------------------
+    def _cast_dtype(self):
+        if self.fp8_dtype is None:
+            raise NotImplementedError(f'{self.bit}: only e4m3 / e5m2 have a native cast; the '
+                                      'qtorch rounding of other formats is not available')
+        return self.fp8_dtype
+
+    def _check(self, args):
+        if self.calib_algo not in ('minmax',):
+            raise NotImplementedError(f'calib_algo={self.calib_algo} is not on the device path')
+        if 'rounding' in args:
+            raise NotImplementedError("args['rounding'] is not on the device path")
+
+    def _qmax_f(self):
+        return float(self.qmax.item())
+
+    def _view(self, tensor):
+        """(2-D view, group, per_tensor) for the row/group kernels."""
+        g = self.granularity
+        if g == 'per_tensor':
+            return tensor.reshape(1, -1), tensor.numel(), True
+        x2, group = self._kernel_view(tensor)
+        return x2, group, False
+
+    def _dyn(self, tensor, *, codes, fq, fq_dtype=None):
+        """Dynamic FP8 over the quantizer's granularity: dict(codes, fq, scales)."""
+        fp8 = self._cast_dtype()
+        t = tensor.contiguous()
+        if self.granularity == 'per_block':
+            if self.block_size != 128:
+                raise NotImplementedError('per_block FP8 supports block_size 128')
+            r = ops.fp8_quant_blocks(t, fp8, 128, qmax=self._qmax_f(), clamp_min=1e-5,
+                                     add_zero=True, codes=codes, fq=fq, fq_dtype=fq_dtype)
+            return r
+        x2, group, pt = self._view(t)
+        r = ops.fp8_quant(x2, group, fp8, qmax=self._qmax_f(), clamp_min=1e-5, add_zero=True,
+                          per_tensor=pt, codes=codes, fq=fq, fq_dtype=fq_dtype)
+        if codes:
+            r['codes'] = r['codes'].reshape(tensor.shape)
+        if fq:
+            r['fq'] = r['fq'].reshape(tensor.shape)
+        return r
+
+    def _emul(self, tensor):
+        if self.granularity in ('per_tensor', 'per_block'):
+            raise NotImplementedError(f'use_qtorch=False with {self.granularity} (the reference '
+                                      'indexes maxval.shape[0] / pads differently here)')
+        x2, group, _ = self._view(tensor.contiguous())
+        return ops.fp_emul_quant(x2, group, self.e_bits, self.m_bits).reshape(tensor.shape)
+
+    # -- qparams (API parity; quant.py:1005-1059) --------------------------------------------
+    def get_float_qparams(self, tensor, tensor_range, device):
+        """quant.py:1005-1027 in torch on the tensor's device (API helper)."""
+        min_val, max_val = tensor_range
+        maxval = torch.max(max_val, -min_val)
+        e_bits = torch.tensor(self.e_bits, dtype=torch.float32, device=device)
+        m_bits = torch.tensor(self.m_bits, dtype=torch.float32, device=device)
+        if maxval.shape[0] != 1 and len(maxval.shape) != len(tensor.shape):
+            maxval = maxval.view([-1] + [1] * (len(tensor.shape) - 1))
+        if e_bits >= 5:
+            maxval = maxval.to(dtype=torch.float32)
+        bias = 2 ** e_bits - torch.log2(maxval) + torch.log2(2 - 2 ** (-m_bits)) - 1
+        xc = torch.min(torch.max(tensor, -maxval), maxval)
+        log_scales = torch.clamp((torch.floor(torch.log2(torch.abs(xc)) + bias)).detach(), 1.0)
+        return xc, 2.0 ** (log_scales - m_bits - bias)
+
+    def get_qparams(self, tensor_range, device):
+        min_val, max_val = tensor_range
+        abs_max = torch.max(max_val.abs(), min_val.abs()).clamp(min=1e-5)
+        qmax = self.qmax.to(device)
+        return abs_max / qmax, torch.tensor(0.0), qmax, self.qmin.to(device)
+
+    def get_minmax_range(self, tensor):
+        if self.granularity == 'per_block':
+            return (tensor.abs().float().amin(dim=(1, 3), keepdim=True),
+                    tensor.abs().float().amax(dim=(1, 3), keepdim=True))
+        return super().get_minmax_range(tensor)
+
+    def get_tensor_qparams(self, tensor, args={}):
+        """quant.py:1044-1059: (tensor, scales, zeros, qmax, qmin)."""
+        self._check(args)
+        if not self.use_qtorch:
+            t = self.reshape_tensor(tensor)
+            xc, scales = self.get_float_qparams(t, self.get_minmax_range(t), t.device)
+            return xc, scales, torch.tensor(0), None, None
+        r = self._dyn(tensor, codes=False, fq=False)
+        s = r['scales']
+        if self.granularity == 'per_tensor':
+            s = s.reshape(())
+        elif self.granularity == 'per_block':
+            s = s.view(s.shape[0], 1, s.shape[1], 1)
+        dev = tensor.device
+        return (self.reshape_tensor(tensor), s, torch.tensor(0.0), self.qmax.to(dev),
+                self.qmin.to(dev))
+
+    # -- elementwise with given qparams (quant.py:1061-1080) ----------------------------------
+    def _static(self, tensor, scales, want, fq_dtype=None):
+        fp8 = self._cast_dtype()
+        s = scales
+        s.masked_fill_(s == 0, 1)  # quant.py:1062 mutates the caller's scales
+        if self.granularity == 'per_block' and s.dim() == 4:
+            raise NotImplementedError('static per_block: use the dynamic path')
+        ct = tensor.dtype if s.dim() == 0 else torch.promote_types(tensor.dtype, s.dtype)
+        r = ops.fp8_quant_static(tensor.reshape(tensor.shape[0] if tensor.dim() else 1, -1),
+                                 s.reshape(-1), fp8, ct_dtype=ct, add_zero=True,
+                                 codes=want == 'codes', fq=want == 'fq', fq_dtype=fq_dtype)
+        return r[want].reshape(tensor.shape)
+
+    def quant(self, tensor, scales, zeros, qmax, qmin):
+        if not self.use_qtorch:
+            scales[scales == 0] = 1
+            return self.round_func(tensor / scales + zeros)
+        return self._static(tensor, scales, 'codes').float()
+
+    def dequant(self, tensor, scales, zeros):
+        return (tensor - zeros) * scales
+
+    def quant_dequant(self, tensor, scales, zeros, qmax, qmin):
+        if not self.use_qtorch:
+            return self.dequant(self.quant(tensor, scales, zeros, qmax, qmin), scales, zeros)
+        return self._static(tensor, scales, 'fq', fq_dtype=torch.float32)
+
+    # -- weights / activations -----------------------------------------------------------------
+    @staticmethod
+    def _tr(args):
+        return 'dim' in args and 'ic' in args['dim']
+
+    def fake_quant_weight_dynamic(self, weight, args={}):
+        """quant.py:1119-1139."""
+        self._check(args)
+        w = weight.T if self._tr(args) else weight
+        if self.use_qtorch:
+            out = self._dyn(w, codes=False, fq=True, fq_dtype=w.dtype)['fq']
+        else:
+            out = self._emul(w)
+        return out.T if self._tr(args) else out
+
+    def fake_quant_weight_static(self, weight, args):
+        """quant.py:1084-1117."""
+        self._check(args)
+        if not self.use_qtorch:
+            raise NotImplementedError('static use_qtorch=False fake quant is not on the device '
+                                      'path')
+        w = weight.T if self._tr(args) else weight
+        out = self._static(w, args['scales'], 'fq', fq_dtype=w.dtype)
+        return out.T if self._tr(args) else out
+
+    def fake_quant_act_dynamic(self, act, args={}):
+        """quant.py:1072-1081."""
+        self._check(args)
+        if not self.use_qtorch:
+            return self._emul(act)
+        return self._dyn(act, codes=False, fq=True, fq_dtype=act.dtype)['fq']
+
+    def fake_quant_act_static(self, act, args={}):
+        """quant.py:1058-1070."""
+        self._check(args)
+        if not self.use_qtorch:
+            raise NotImplementedError('static use_qtorch=False fake quant is not on the device '
+                                      'path')
+        return self._static(act, args['scales'], 'fq', fq_dtype=act.dtype)
+
+    def _qshape(self, codes, scales):
+        if self.granularity == 'per_tensor':
+            return 1
+        if self.granularity == 'per_block':
+            return tuple(scales.shape)
+        return (codes.shape[0], -1)
+
+    def real_quant_weight_dynamic(self, weight, args={}):
+        """quant.py:1191-1221: (fp8 weight, scales, None)."""
+        assert self.bit in ['e4m3', 'e5m2'], 'Only FP8 E4M3 and E5M2 support real quant'
+        if not self.use_qtorch:
+            raise NotImplementedError('use_qtorch=False real quant is not on the device path')
+        osf = args.pop('output_scale_factor', 1) if 'output_scale_factor' in args else 1
+        self._check(args)
+        r = self._dyn(weight, codes=True, fq=False)
+        codes, scales = r['codes'], r['scales']
+        if osf != 1:
+            scales = scales * osf
+        return codes, scales.view(self._qshape(codes, scales)), None
+
+    def real_quant_weight_static(self, weight, args):
+        """quant.py:1161-1189."""
+        assert self.bit in ['e4m3', 'e5m2'], 'Only FP8 E4M3 and E5M2 support real quant'
+        if not self.use_qtorch:
+            raise NotImplementedError('use_qtorch=False real quant is not on the device path')
+        osf = args.pop('output_scale_factor', 1) if 'output_scale_factor' in args else 1
+        scales = args['scales']
+        codes = self._static(weight, scales, 'codes')
+        scales = scales * osf
+        if self.granularity == 'per_block':
+            return codes, scales.view(scales.shape[0], scales.shape[2]), None
+        return codes, scales.view(self._qshape(codes, scales)), None
 
     def __repr__(self):
         return (f'FloatQuantizer(bit={self.bit},e_bits={self.e_bits}, m_bits={self.m_bits},'
-                f'granularity={self.granularity},kwargs={self.kwargs})')
+                f'granularity={self.granularity},kwargs={self.kwargs}, '
+                f'qmin={getattr(self, "qmin", None)}, qmax={getattr(self, "qmax", None)})')

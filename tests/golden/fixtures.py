@@ -12,8 +12,11 @@ import torch
 
 GOLDEN_DIR = Path(__file__).resolve().parent
 
-_VIEW = {torch.bfloat16: (torch.int16, 'bfloat16'), torch.float8_e4m3fn: (torch.uint8, 'float8_e4m3fn')}
-_BACK = {'bfloat16': torch.bfloat16, 'float8_e4m3fn': torch.float8_e4m3fn}
+_VIEW = {torch.bfloat16: (torch.int16, 'bfloat16'),
+         torch.float8_e4m3fn: (torch.uint8, 'float8_e4m3fn'),
+         torch.float8_e5m2: (torch.uint8, 'float8_e5m2')}
+_BACK = {'bfloat16': torch.bfloat16, 'float8_e4m3fn': torch.float8_e4m3fn,
+         'float8_e5m2': torch.float8_e5m2}
 
 
 def _to_np(t):

@@ -17,6 +17,7 @@ HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE))
 import _ref_import as R  # noqa: E402
 import fixtures as F  # noqa: E402
+from inputs import fp8_inputs  # noqa: E402
 
 
 def weights(rows, cols, dtype, seed, edge=True):
@@ -310,6 +311,66 @@ def gen_clip():
 
 
 GENERATORS = {'quant': gen_quant, 'gptq': gen_gptq, 'awq': gen_awq, 'clip': gen_clip}
+
+
+def gen_fp8():
+    """FloatQuantizer pieces the reference runs without qtorch: the use_qtorch=False
+    (get_float_qparams) fake quant end to end, the use_qtorch scales (get_minmax_range +
+    get_qparams with qmax = finfo.max, as quant.py:982-996 sets it), and the per_block
+    weight_cast_to_bf16 sequence (reshape_tensor -> dequant -> restore_tensor)."""
+    q = R.quant_module()
+    emul = [
+        # name, bit, gran, group, dtype
+        ('e4m3_pc_bf16', 'e4m3', 'per_channel', None, torch.bfloat16),
+        ('e4m3_g128_bf16', 'e4m3', 'per_group', 128, torch.bfloat16),
+        ('e5m2_pc_bf16', 'e5m2', 'per_channel', None, torch.bfloat16),
+        ('e4m3_pc_f16', 'e4m3', 'per_channel', None, torch.float16),
+        ('e3m2_pc_bf16', 'e3m2', 'per_channel', None, torch.bfloat16),
+    ]
+    for i, (name, bit, gran, gs, dt) in enumerate(emul):
+        kw = {'group_size': gs} if gs else {}
+        fq = q.FloatQuantizer(bit, True, gran, **kw)
+        w = fp8_inputs(16, 512, dt, 200 + i)
+        aq = q.FloatQuantizer(bit, True, 'per_token')
+        a = fp8_inputs(24, 256, dt, 300 + i)
+        F.save(f'fp8emul_{name}', w=w, fq=fq.fake_quant_weight_dynamic(w.clone()), act=a,
+               act_fq=aq.fake_quant_act_dynamic(a.clone()),
+               meta=torch.tensor([int(bit[1]), int(bit[-1]), gs or 512]))
+
+    scl = [
+        ('e4m3_pc_bf16', 'e4m3', 'per_channel', {}, torch.bfloat16, (16, 512)),
+        ('e4m3_g128_bf16', 'e4m3', 'per_group', {'group_size': 128}, torch.bfloat16, (16, 512)),
+        ('e4m3_pt_bf16', 'e4m3', 'per_tensor', {}, torch.bfloat16, (16, 512)),
+        ('e5m2_pc_f16', 'e5m2', 'per_channel', {}, torch.float16, (16, 512)),
+        ('e4m3_blk_bf16', 'e4m3', 'per_block', {'block_size': 128}, torch.bfloat16, (256, 384)),
+        ('e4m3_blk_ragged_bf16', 'e4m3', 'per_block', {'block_size': 128}, torch.bfloat16,
+         (200, 256)),
+    ]
+    fp8 = {'e4m3': torch.float8_e4m3fn, 'e5m2': torch.float8_e5m2}
+    for i, (name, bit, gran, kw, dt, shape) in enumerate(scl):
+        qz = q.FloatQuantizer(bit, True, gran, **kw)
+        fi = torch.finfo(fp8[bit])
+        qz.qmin, qz.qmax = torch.tensor(fi.min), torch.tensor(fi.max)
+        w = fp8_inputs(*shape, dt, 400 + i)
+        t = qz.reshape_tensor(w)
+        s, z, _, _ = qz.get_qparams(qz.get_minmax_range(t), 'cpu')
+        F.save(f'fp8scale_{name}', w=w, scales=s)
+
+    # weight_cast_to_bf16 (quant.py:18-31) through the reference's own per_block methods
+    for name, (M, N) in {'even': (256, 384), 'ragged_m': (200, 256)}.items():
+        g = torch.Generator().manual_seed(500 + M)
+        codes = torch.randint(0, 256, (M, N), generator=g, dtype=torch.uint8)
+        codes[(codes & 0x7f) == 0x7f] = 0x3c  # no NaN encodings
+        codes = codes.view(torch.float8_e4m3fn)
+        sc = (torch.rand(-(-M // 128), -(-N // 128), generator=g) * 1e-3 + 1e-4).float()
+        qz = q.FloatQuantizer('e4m3', True, 'per_block', block_size=128)
+        t = qz.reshape_tensor(codes)
+        deq = qz.dequant(t.float(), sc.view(sc.shape[0], 1, sc.shape[1], 1), 0)
+        out = qz.restore_tensor(deq, codes.shape).to(torch.bfloat16)
+        F.save(f'fp8cast_bf16_{name}', codes=codes, scales=sc, out=out)
+
+
+GENERATORS['fp8'] = gen_fp8
 
 
 if __name__ == '__main__':

@@ -1,0 +1,119 @@
+"""FP8 kernels (lcq_fp8_* / lcq_fp_emul_quant) vs the oracle and the reference fixtures."""
+import pytest
+import torch
+
+import fixtures as F
+from oracle import fp8_ref as O
+
+pytestmark = pytest.mark.gpu
+
+
+def same(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return torch.equal(a.isnan(), b.isnan()) and torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
+
+
+def bits(t):
+    return t.cpu().view(torch.uint8)
+
+
+@pytest.mark.parametrize('fp8', [torch.float8_e4m3fn, torch.float8_e5m2])
+def test_cast_exhaustive_bf16_and_random_f32(dev, fp8):
+    from lightcompress_amd import ops
+    allb = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    one = torch.ones(1, dtype=torch.float32, device=dev)
+    r = ops.fp8_quant_static(allb.to(dev).reshape(256, 256), one, fp8, ct_dtype=torch.float32,
+                             add_zero=False)
+    want = allb.float().to(fp8).view(torch.uint8).reshape(256, 256)
+    nan = allb.float().isnan().reshape(256, 256)
+    assert torch.equal(bits(r['codes'])[~nan], want[~nan])
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(512, 1024, generator=g) * torch.exp(torch.randn(512, 1, generator=g) * 4)
+    r = ops.fp8_quant_static(x.to(dev), one, fp8, add_zero=False)
+    assert torch.equal(bits(r['codes']), x.to(fp8).view(torch.uint8))
+
+
+EMUL = ['e4m3_pc_bf16', 'e4m3_g128_bf16', 'e5m2_pc_bf16', 'e4m3_pc_f16', 'e3m2_pc_bf16']
+
+
+@pytest.mark.parametrize('name', EMUL)
+def test_emulation_vs_reference(dev, name):
+    from lightcompress_amd.quant import FloatQuantizer
+    c = F.load(f'fp8emul_{name}')
+    e, m, gs = (int(v) for v in c['meta'])
+    bit = f'e{e}m{m}'
+    kw = {'group_size': gs} if gs != c['w'].shape[1] else {}
+    gran = 'per_group' if kw else 'per_channel'
+    q = FloatQuantizer(bit, True, gran, **kw)
+    out = q.fake_quant_weight_dynamic(c['w'].to(dev))
+    assert out.dtype == c['fq'].dtype and same(out, c['fq'])
+    aq = FloatQuantizer(bit, True, 'per_token')
+    assert same(aq.fake_quant_act_dynamic(c['act'].to(dev)), c['act_fq'])
+
+
+CASES = [('e4m3', 'per_channel', {}, torch.bfloat16, (64, 512)),
+         ('e4m3', 'per_group', {'group_size': 128}, torch.bfloat16, (64, 512)),
+         ('e4m3', 'per_token', {}, torch.bfloat16, (48, 7168)),
+         ('e4m3', 'per_tensor', {}, torch.bfloat16, (256, 1024)),
+         ('e4m3', 'per_block', {'block_size': 128}, torch.bfloat16, (384, 256)),
+         ('e4m3', 'per_block', {'block_size': 128}, torch.bfloat16, (200, 264)),
+         ('e5m2', 'per_channel', {}, torch.float16, (64, 512)),
+         ('e4m3', 'per_channel', {}, torch.float32, (32, 256))]
+
+
+@pytest.mark.parametrize('bit,gran,kw,dt,shape', CASES)
+def test_qtorch_path_vs_oracle(dev, bit, gran, kw, dt, shape):
+    from lightcompress_amd.quant import FloatQuantizer
+    from inputs import fp8_inputs
+    w = fp8_inputs(*shape, dt, 77)
+    q = FloatQuantizer(bit, True, gran, use_qtorch=True, **kw)
+    fq_ref, codes_ref, s_ref = O.fp8_qdq(w, bit, gran, kw.get('group_size'))
+    fq = q.fake_quant_weight_dynamic(w.to(dev))
+    assert fq.dtype == dt and same(fq, fq_ref)
+    codes, s, z = q.real_quant_weight_dynamic(w.to(dev))
+    assert z is None and codes.dtype == O.FP8[bit]
+    assert torch.equal(bits(codes), codes_ref.view(torch.uint8))
+    assert s.shape == s_ref.shape and s.dtype == s_ref.dtype and torch.equal(s.cpu(), s_ref)
+    if gran != 'per_block':  # static path with the dynamic scales reproduces the dynamic one
+        _, s4, zz, qmax, qmin = q.get_tensor_qparams(w.to(dev))
+        st = q.fake_quant_weight_static(w.to(dev), {'scales': s4, 'zeros': zz, 'qmax': qmax,
+                                                     'qmin': qmin})
+        assert same(st, fq_ref)
+
+
+@pytest.mark.parametrize('name', ['even', 'ragged_m'])
+def test_block_dequant_vs_reference(dev, name):
+    from lightcompress_amd.quant import weight_cast_to_bf16
+    c = F.load(f'fp8cast_bf16_{name}')
+    out = weight_cast_to_bf16(c['codes'].to(dev), c['scales'].to(dev), 128)
+    assert torch.equal(out.cpu().view(torch.int16), c['out'].view(torch.int16))
+
+
+@pytest.mark.parametrize('shape', [(256, 384), (200, 264), (2048, 7168)])
+def test_kernel_py_casts_vs_oracle(dev, shape):
+    from lightcompress_amd import kernel as K
+    g = torch.Generator().manual_seed(shape[0])
+    x = (torch.randn(*shape, generator=g) * 0.02).to(torch.bfloat16)
+    x[:128, :128] = 0  # all-zero block: s = 0 -> NaN, as the Triton kernel
+    y, s = K.weight_cast_to_fp8(x.to(dev))
+    y_ref, s_ref = O.weight_cast_to_fp8(x)
+    assert torch.equal(s.cpu(), s_ref) if not s_ref.isnan().any() else same(s, s_ref)
+    assert torch.equal(bits(y), y_ref.view(torch.uint8))
+    back = K.weight_cast_to_bf16(y, s).to(torch.bfloat16)
+    assert same(back, O.weight_cast_to_bf16(y_ref, s_ref))
+    a = (torch.randn(4, shape[1] // 128 * 128, generator=g)).to(torch.bfloat16)
+    ya, sa = K.act_quant(a.to(dev))
+    ya_ref, sa_ref = O.act_quant(a)
+    assert torch.equal(sa.cpu(), sa_ref) and torch.equal(bits(ya), ya_ref.view(torch.uint8))
+
+
+def test_per_tensor_expert_shape(dev):
+    """A DeepSeek-V3 expert linear (2048 x 7168) per-tensor real quant: bit-exact codes."""
+    from lightcompress_amd.quant import FloatQuantizer
+    g = torch.Generator().manual_seed(11)
+    w = (torch.randn(2048, 7168, generator=g) * 0.02).to(torch.bfloat16)
+    q = FloatQuantizer('e4m3', True, 'per_tensor', use_qtorch=True)
+    codes, s, _ = q.real_quant_weight_dynamic(w.to(dev))
+    _, codes_ref, s_ref = O.fp8_qdq(w, 'e4m3', 'per_tensor')
+    assert torch.equal(s.cpu(), s_ref)
+    assert torch.equal(bits(codes), codes_ref.view(torch.uint8))
