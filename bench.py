@@ -13,6 +13,12 @@ metric: linear layers quantized per second (whole job, all ranks). Multi-GPU: on
 GPU (torchrun); with quant_out=False AWQ blocks are independent given the float activations
 (SURVEY.md §8e), so every rank quantizes its own blocks -- weak scaling, no data-path collective.
 
+GPTQ leg (BASELINE.json configs[2], reported under "gptq"): Llama-3-8B GPTQ w4a16 g128 asym,
+act-order, true_sequential, quant_out (configs/quantization/methods/GPTQ/gptq_w_only.yml),
+128 x 2048 calibration tokens at bs 1 (128 inputs per block, as the reference's Catcher
+stores them); one step = one block through block_opt (Hessians, column loops, fake-quant
+forward of the next block's input). Its roofline is the XᵀX Hessian kernel.
+
 Also reported: the roofline of the dominant kernel (the bf16 projection GEMMs of the AWQ loss
 search, timed live with device events around every linear launch), live timings of every lcq
 HIP kernel family, and a CPU baseline (the oracle = reference algorithm restated on torch-CPU,
@@ -51,6 +57,10 @@ def parse():
     ap.add_argument('--n-samples', type=int, default=128)
     ap.add_argument('--seq-len', type=int, default=512)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--algo', choices=['awq', 'gptq', 'both'], default='both')
+    ap.add_argument('--gptq-steps', type=int, default=2)
+    ap.add_argument('--gptq-samples', type=int, default=128)
+    ap.add_argument('--gptq-seq-len', type=int, default=2048)
     ap.add_argument('--cpu-budget-s', type=float, default=20.0)
     return ap.parse_args()
 
@@ -67,6 +77,21 @@ def awq_config(seq_len):
                   'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True,
                               'clip_sym': True},
                   'quant_out': False},
+    })
+
+
+def gptq_config(seq_len, n_samples):
+    from lightcompress_amd.utils import load_config
+    return load_config({
+        'base': {'seed': 42},
+        'calib': {'name': 'wikitext2', 'n_samples': n_samples, 'bs': 1, 'seq_len': seq_len,
+                  'preproc': 'wikitext2_gptq'},
+        'quant': {'method': 'GPTQ',
+                  'weight': {'bit': 4, 'symmetric': False, 'granularity': 'per_group',
+                             'group_size': 128},
+                  'special': {'actorder': True, 'static_groups': False, 'percdamp': 0.01,
+                              'blocksize': 128, 'true_sequential': True},
+                  'quant_out': True},
     })
 
 
@@ -210,6 +235,84 @@ def cpu_baseline(args, budget_s):
             'est_s_per_block': t_total_est, 'parts_s': parts}
 
 
+def timed_blocks(step, warmup, steps, world, dev):
+    """Run `warmup` untimed then `steps` timed steps; barrier + sync on both sides; max over
+    ranks. Returns elapsed seconds."""
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(warmup, warmup + steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return elapsed
+
+
+def kernel_table(kern, elapsed):
+    return {k: {'launches': v['launches'], 'avg_ms': round(v['avg_ms'], 4),
+                'share_of_step': round(v['total_ms'] / (elapsed * 1e3), 4)}
+            for k, v in sorted(kern.items(), key=lambda kv: -kv[1]['total_ms'])}
+
+
+def bench_gptq(args, rank, world, dev):
+    """GPTQ leg: per-block wall-clock and the Hessian kernel's roofline."""
+    from transformers import LlamaConfig
+    from lightcompress_amd import _native
+    from lightcompress_amd.llama import Llama
+    from lightcompress_amd.pipeline import build_algo
+    cfg = LlamaConfig(**LLAMA3_8B)
+    warm, steps = 1, args.gptq_steps
+    model = Llama.random(cfg, num_layers=warm + steps, device=dev, seed=2000 + rank)
+    seq = args.gptq_seq_len
+    hidden = synthetic_hidden(args.gptq_samples, seq, cfg.hidden_size, dev, 31 + rank)
+    kw = model.rotary_kwargs(seq)
+    calib = {'data': [hidden[i:i + 1] for i in range(args.gptq_samples)],
+             'kwargs': [kw] * args.gptq_samples}
+    algo = build_algo(model, gptq_config(seq, args.gptq_samples), calib)
+    blocks = model.get_blocks()
+
+    def step(i):
+        algo.block_idx = i
+        algo.block_opt(blocks[i])
+
+    timer = _native.KernelTimer()
+    for i in range(warm):
+        step(i)
+    torch.cuda.synchronize()
+    with timer:
+        elapsed = timed_blocks(lambda i: step(i + warm), 0, steps, world, dev)
+    kern = timer.summary()
+    ms = elapsed / steps * 1e3
+    out = {'linears_per_s': round(N_LINEARS_PER_BLOCK * steps * world / elapsed, 3),
+           'ms_per_block': round(ms, 1), 'steps': steps, 'warmup': warm,
+           'extrapolated_model_wall_s': round(ms * 32 / 1e3, 2),
+           'workload': (f'Llama-3-8B GPTQ w4a16 g128 asym act-order true_sequential quant_out, '
+                        f'{args.gptq_samples}x{seq} calib tokens (bs 1)'),
+           'lcq_kernels': kernel_table(kern, elapsed)}
+    h = kern.get('lcq_hessian_accum')
+    if h:
+        # algorithmic: symmetric rank-n update n*ic*(ic+1) flops per launch (SURVEY.md §8d);
+        # KernelTimer records the flops each launch was given
+        tf = h['flops'] / (h['total_ms'] * 1e-3) / 1e12
+        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_hessian_syrk, bf16 MFMA XᵀX)',
+                           'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
+                           'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4),
+                           'traffic': None, 'avg_launch_ms': round(h['avg_ms'], 4)}
+    del algo, model, hidden, calib
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     rank = int(os.environ.get('RANK', 0))
@@ -225,6 +328,15 @@ def main():
     from lightcompress_amd.pipeline import build_algo
 
     _native.load()
+    gptq = bench_gptq(args, rank, world, dev) if args.algo in ('gptq', 'both') else None
+    if args.algo == 'gptq':
+        if rank == 0:
+            print(json.dumps({'metric': 'linear-layers quantized/sec (Llama-3-8B GPTQ w4a16 '
+                              'g128 act-order)', 'value': gptq['linears_per_s'],
+                              'unit': 'linears/s', 'n_gpus': world, 'gptq': gptq}))
+        if world > 1:
+            dist.destroy_process_group()
+        return
     cfg = LlamaConfig(**LLAMA3_8B)
     nblk = args.warmup + args.steps
     model = Llama.random(cfg, num_layers=nblk, device=dev, seed=1000 + rank)
@@ -279,9 +391,7 @@ def main():
                         'avg_launch_ms': round(gemm['avg_ms'], 4),
                         'flops_per_launch': gemm['flops_per_launch'],
                         'share_of_step': round(gemm['total_ms'] / (elapsed * 1e3), 3)}
-        kernels = {k: {'launches': v['launches'], 'avg_ms': round(v['avg_ms'], 4),
-                       'share_of_step': round(v['total_ms'] / (elapsed * 1e3), 4)}
-                   for k, v in sorted(kern.items(), key=lambda kv: -kv[1]['total_ms'])}
+        kernels = kernel_table(kern, elapsed)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             cpu = cpu_baseline(args, args.cpu_budget_s)
@@ -298,6 +408,7 @@ def main():
                        'global_batch': args.n_samples * world, 'seq_len': args.seq_len,
                        'parallelism': f'blocks sharded over {world} GPU(s), no collective'},
             'extrapolated_model_wall_s': round(ms_per_step * 32 / 1e3, 2),
+            'gptq': gptq,
             'roofline': roofline,
             'lcq_kernels': kernels,
             'cpu_baseline': cpu,

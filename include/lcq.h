@@ -114,11 +114,13 @@ int lcq_pack_autoawq_gemm(const void* w, int w_dtype, int64_t oc, int64_t ic, in
  * GPTQ Hessian: H = beta*H + alpha * X^T X   (GPTQ.add_batch, gptq.py:253-295)
  * x [n, ic] BF16/F16 token-major activations; H [ic, ic] fp32 (kept symmetric).
  * The reference's per-sample running average maps to beta = n/(n+b),
- * alpha = fp32(sqrt(2/(n+b)))^2. bf16/fp16 MFMA with fp32 accumulation, upper-triangle tiles
- * mirrored.
+ * alpha = fp32(sqrt(2/(n+b)))^2. 256x256-tile MFMA SYRK (bf16/fp16 products, fp32
+ * accumulation) over the upper triangle, mirrored. workspace >= lcq_hessian_workspace_bytes
+ * (a zero-padded X^T copy + split-K slabs when ic is small); caller-owned, device memory.
  * ------------------------------------------------------------------------------------- */
+int64_t lcq_hessian_workspace_bytes(int64_t n, int64_t ic);
 int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t ic, void* H, float alpha,
-                      float beta, void* stream);
+                      float beta, void* workspace, int64_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * GPTQ in-block column loop for one 128-column block (GPTQ.weight_transform, gptq.py:198-244,

@@ -41,7 +41,8 @@ SIGNATURES = {
     'lcq_pack_vllm': ([_vp, _int, _i64, _i64, _int, _vp, _vp], _int),
     'lcq_pack_autoawq_gemm': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _vp, _vp,
                                _vp, _vp], _int),
-    'lcq_hessian_accum': ([_vp, _int, _i64, _i64, _vp, _f32, _f32, _vp], _int),
+    'lcq_hessian_workspace_bytes': ([_i64, _i64], _i64),
+    'lcq_hessian_accum': ([_vp, _int, _i64, _i64, _vp, _f32, _f32, _vp, _i64, _vp], _int),
     'lcq_gptq_block': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _int, _int, _int, _vp,
                         _vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
     'lcq_gptq_trailing': ([_vp, _i64, _i64, _i64, _int, _i64, _vp, _vp, _i64, _vp], _int),
@@ -125,6 +126,7 @@ class KernelTimer:
 
     def __init__(self):
         self.events = {}
+        self.work = {}
 
     def __enter__(self):
         global _timer
@@ -142,10 +144,18 @@ class KernelTimer:
         for name, pairs in self.events.items():
             ms = [a.elapsed_time(b) for a, b in pairs]
             out[name] = {'launches': len(ms), 'total_ms': sum(ms), 'avg_ms': sum(ms) / len(ms)}
+            if name in self.work:
+                out[name]['flops'] = self.work[name]
         return out
 
 
 _timer = None
+
+
+def note_work(name: str, units: float):
+    """Attribute algorithmic work (flops or bytes) to the last `name` launch while timing."""
+    if _timer is not None:
+        _timer.work[name] = _timer.work.get(name, 0.0) + float(units)
 
 
 def call(name: str, *args):

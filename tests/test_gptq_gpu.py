@@ -31,11 +31,14 @@ def test_hessian_vs_reference(dev, name):
     assert torch.equal(H, H.t()), 'Hessian must be exactly symmetric'
 
 
-@pytest.mark.parametrize('n,ic', [(2048, 4096), (1000, 1032), (37, 136)])
-def test_hessian_large_vs_fp64(dev, n, ic):
+@pytest.mark.parametrize('n,ic,dt', [(2048, 4096, torch.bfloat16), (1000, 1032, torch.bfloat16),
+                                     (37, 136, torch.bfloat16), (640, 8192, torch.bfloat16),
+                                     (300, 520, torch.float16)])
+def test_hessian_large_vs_fp64(dev, n, ic, dt):
+    """Covers split-K (few tiles), the single-pass path (ic 8192: 528 tiles), ragged ic / n."""
     from lightcompress_amd import ops
     g = torch.Generator().manual_seed(n + ic)
-    x = (torch.randn(n, ic, generator=g) * torch.exp(torch.randn(ic, generator=g))).to(torch.bfloat16)
+    x = (torch.randn(n, ic, generator=g) * torch.exp(torch.randn(ic, generator=g))).to(dt)
     H = torch.full((ic, ic), 0.5, device=dev)
     ops.hessian_accum(x.to(dev), H, 0.25, 0.5)
     xd = x.double()
@@ -43,6 +46,7 @@ def test_hessian_large_vs_fp64(dev, n, ic):
     bound = 0.25 * (xd.abs().t() @ xd.abs()) + 0.25
     err = (H.cpu().double() - ref).abs()
     assert (err <= 1e-6 * bound + 1e-30).all(), (err / bound).max().item()
+    assert torch.equal(H, H.t())
 
 
 @pytest.mark.parametrize('group,sym', [(128, False), (64, True), (32, False)])
