@@ -119,6 +119,10 @@ class BlockwiseOpt:
         pass
 
 
+class _StopForward(Exception):
+    """Raised by a capture hook once every input a discarded forward exists for is captured."""
+
+
 def _same(a, b):
     if a is b:
         return True
@@ -267,12 +271,40 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
             m.register_buffer('buf_qmin', qmin.clone().to(m.weight.device))
 
     @torch.no_grad()
-    def block_forward(self, block, input_data=None):
+    def capture_names(self, names):
+        """Hooked modules whose inputs a forward exists to capture (all of them by default;
+        GPTQ narrows this to the Hessian owners)."""
+        return set(names)
+
+    def _capture_hook(self, m, x, y, name, feat_dict):
+        self.cache_input_hook(m, x, y, name=name, feat_dict=feat_dict)
+        pending = getattr(self, '_capture_pending', None)
+        if pending is not None:
+            pending.discard(name)
+            if not pending:
+                raise _StopForward
+
+    def _call_block(self, block, x, kw, stop_after):
+        self._capture_pending = set(stop_after) if stop_after else None
+        try:
+            y = block(x, **kw)
+        except _StopForward:
+            return None
+        finally:
+            self._capture_pending = None
+        return y[0] if isinstance(y, tuple) else y
+
+    def block_forward(self, block, input_data=None, stop_after=None):
         """base_blockwise_quantization.py:367-381. Calibration inputs stored one sample per
         entry (bs 1, e.g. GPTQ's 128 x 2048) whose kwargs are equal run as ONE batch: the
         per-sample loop launches 128x more, 128x smaller GEMMs and elementwise kernels. The
         math per sample is unchanged (hooks see the stacked batch; GPTQ's running-average
-        Hessian over one batch of b samples equals b single-sample updates)."""
+        Hessian over one batch of b samples equals b single-sample updates).
+
+        ``stop_after``: the caller discards the output (GPTQ's quant_out first pass, the
+        true_sequential re-forwards) -> each forward ends right after the hooks of these modules
+        have captured their inputs; the layers behind them would only feed the discarded output.
+        """
         if input_data is None:
             input_data = self.input['data']
         kwargs = self.input['kwargs']
@@ -280,14 +312,14 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         if self.batch_calib and (self._batch_ok is None or self._batch_ok[0] != key):
             self._batch_ok = (key, _batchable(input_data, kwargs))
         if self.batch_calib and self._batch_ok[1]:
-            y = block(torch.cat(list(input_data), dim=0), **kwargs[0])
-            y = y[0] if isinstance(y, tuple) else y
+            y = self._call_block(block, torch.cat(list(input_data), dim=0), kwargs[0], stop_after)
+            if y is None:
+                return None
             return list(torch.split(y, [x.shape[0] for x in input_data], dim=0))
         out = []
         for i, x in enumerate(input_data):
-            y = block(x, **kwargs[i])
-            out.append(y[0] if isinstance(y, tuple) else y)
-        return out
+            out.append(self._call_block(block, x, kwargs[i], stop_after))
+        return None if stop_after else out
 
     def block_opt(self, block):
         named_linears = self.model.get_block_linears(block)
@@ -302,14 +334,15 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
     def register_hooks(self, modules, input_feat):
         if self.data_free:
             return []
-        return [m.register_forward_hook(functools.partial(self.cache_input_hook, name=n,
+        self._hooked_names = list(modules)
+        return [m.register_forward_hook(functools.partial(self._capture_hook, name=n,
                                                           feat_dict=input_feat))
                 for n, m in modules.items()]
 
     def run(self, block, input_feat, handles):
         if not self.data_free:
             if self.quant_out:
-                self.block_forward(block)
+                self.block_forward(block, stop_after=self.capture_names(self._hooked_names))
             else:
                 self.input['data'] = self.block_forward(block)
             for h in handles:
@@ -348,7 +381,7 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                                          self.get_replacement_params('fake_quant', self.w_only))
         feat = defaultdict(list)
         handles = self.register_hooks(next_subset['layers'], feat)
-        self.block_forward(block)
+        self.block_forward(block, stop_after=self.capture_names(next_subset['layers']))
         for h in handles:
             h.remove()
         return feat

@@ -80,6 +80,10 @@ class GPTQ(BaseBlockwiseQuantization):
         for subset in (subsets[:1] if self.true_sequential else subsets):
             self._init_subset(subset)
 
+    def capture_names(self, names):
+        """Only the Hessian owners' inputs are consumed (the forward output is discarded)."""
+        return {n for n in names if self.layers_cache.get(n, {}).get('owner', False)}
+
     @torch.no_grad()
     def cache_input_hook(self, m, inp, out, name, feat_dict):
         if isinstance(m, _LINEAR_TYPES):
