@@ -234,6 +234,22 @@ int lcq_fp8_dequant_blocks(const void* codes, int fmt, int64_t M, int64_t N, int
 int lcq_fp_emul_quant(const void* x, int x_dtype, int64_t rows, int64_t cols, int64_t group,
                       int e_bits, int m_bits, void* fq_out, int fq_dtype, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Calibration-forward fusions (the Llama block forward the reference runs through
+ * transformers: modeling_llama.apply_rotary_pos_emb / LlamaMLP.forward, llmc/models/llama.py).
+ * ------------------------------------------------------------------------------------- */
+/* q' = q*cos + rotate_half(q)*sin and the same for k, per-op rounding in dtype (bit-identical
+ * to the unfused torch ops). q [B, S, Hq, D], k [B, S, Hk, D] contiguous (the projection
+ * outputs before the head transpose); cos / sin [*, S, D] with batch stride cos_bstride
+ * (0 = broadcast). D % 16 == 0. Outputs have the q / k layout. */
+int lcq_rotary(const void* q, const void* k, const void* cos, const void* sin, int dtype,
+               int64_t B, int64_t S, int Hq, int Hk, int D, int64_t cos_bstride, void* out_q,
+               void* out_k, void* stream);
+
+/* out = rnd(rnd(g / (1 + exp(-g))) * u): act_fn(gate_proj(x)) * up_proj(x) with SiLU. */
+int lcq_silu_mul(const void* gate, const void* up, int dtype, int64_t n, void* out,
+                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,6 +5,8 @@ replacement, first-block input capture. The model lives in HBM for the whole run
 from __future__ import annotations
 
 import inspect
+import os
+import types
 from collections import defaultdict
 
 import torch
@@ -14,6 +16,52 @@ from .module_utils import _LLMC_LINEAR_TYPES_, _TRANSFORMERS_LINEAR_TYPES_
 from .registry import MODEL_REGISTRY
 
 _LINEAR_TYPES = tuple(_LLMC_LINEAR_TYPES_ + _TRANSFORMERS_LINEAR_TYPES_)
+
+
+_ORIG_ROTARY = None
+
+
+def _fused_apply_rotary(q, k, cos, sin, unsqueeze_dim=1):
+    """modeling_llama.apply_rotary_pos_emb on one lcq_rotary pass (bit-identical); other
+    layouts / dtypes / devices go to the original function."""
+    from . import ops
+    if (unsqueeze_dim == 1 and q.is_cuda and q.dim() == 4 and k.dim() == 4
+            and q.dtype in (torch.bfloat16, torch.float16) and k.dtype == q.dtype
+            and cos.dtype == q.dtype and sin.dtype == q.dtype and cos.dim() == 3
+            and q.shape[-1] % 16 == 0 and q.transpose(1, 2).is_contiguous()
+            and k.transpose(1, 2).is_contiguous() and cos.shape[0] in (1, q.shape[0])
+            and cos.shape[1:] == (q.shape[2], q.shape[3])):
+        return ops.rotary(q, k, cos, sin)
+    return _ORIG_ROTARY(q, k, cos, sin, unsqueeze_dim)
+
+
+def _fused_mlp_forward(self, x):
+    """LlamaMLP.forward with act_fn(gate) * up on one lcq_silu_mul pass; the projections are
+    still called as modules (hooks fire in the original order: gate, up, down)."""
+    from . import ops
+    g = self.gate_proj(x)
+    u = self.up_proj(x)
+    if g.is_cuda and g.dtype in (torch.bfloat16, torch.float16) and g.shape == u.shape \
+            and u.dtype == g.dtype and g.numel() % 8 == 0:
+        h = ops.silu_mul(g, u)
+    else:
+        h = self.act_fn(g) * u
+    return self.down_proj(h)
+
+
+def install_fused_forward(model: nn.Module):
+    """Route the Llama calibration forward's elementwise chains through the lcq fusions
+    (env LCQ_FUSED_FORWARD=0 disables)."""
+    global _ORIG_ROTARY
+    if os.environ.get('LCQ_FUSED_FORWARD', '1') == '0':
+        return
+    from transformers.models.llama import modeling_llama as ml
+    if _ORIG_ROTARY is None:
+        _ORIG_ROTARY = ml.apply_rotary_pos_emb
+        ml.apply_rotary_pos_emb = _fused_apply_rotary
+    for m in model.modules():
+        if isinstance(m, ml.LlamaMLP) and getattr(m.config, 'hidden_act', None) == 'silu':
+            m.forward = types.MethodType(_fused_mlp_forward, m)
 
 
 class _Blocks(nn.Module):
@@ -45,6 +93,7 @@ class Llama:
         self.embed_tokens = getattr(inner, 'embed_tokens', None)
         self.torch_dtype = next(self.model.parameters()).dtype
         self.mm_model = None
+        install_fused_forward(self.model)
 
     # -- random-init constructor (synthetic benchmark / tests) --------------------------------
     @classmethod

@@ -409,3 +409,38 @@ def fp_emul_quant(x: torch.Tensor, group: int, e_bits: int, m_bits: int,
     N.call('lcq_fp_emul_quant', N.ptr(x), N.dt(x.dtype), rows, cols, group, e_bits, m_bits,
            N.ptr(out), N.dt(out.dtype), N.stream_of(x))
     return out
+
+
+# ---------------------------------------------------------------------------------------
+# calibration-forward fusions
+# ---------------------------------------------------------------------------------------
+def rotary(q: torch.Tensor, k: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor):
+    """apply_rotary_pos_emb for head-transposed views q [B, Hq, S, D], k [B, Hk, S, D] whose
+    storage is [B, S, H, D] (the projection output); cos / sin [Bc, S, D]. Returns (q', k') in
+    the same layout, bit-identical to the torch ops."""
+    B, Hq, S, D = q.shape
+    Hk = k.shape[1]
+    qs, ks = q.transpose(1, 2), k.transpose(1, 2)
+    if not (qs.is_contiguous() and ks.is_contiguous()):
+        raise ValueError('rotary expects head-transposed views of contiguous projections')
+    cos = cos.contiguous()
+    sin = sin.contiguous()
+    if cos.dim() != 3 or cos.shape[-2:] != (S, D) or cos.shape[0] not in (1, B) or sin.shape != cos.shape:
+        raise ValueError('cos / sin must be [1 or B, S, D]')
+    oq = torch.empty_like(qs)
+    ok = torch.empty_like(ks)
+    N.call('lcq_rotary', N.ptr(qs), N.ptr(ks), N.ptr(cos), N.ptr(sin), N.dt(q.dtype), B, S, Hq,
+           Hk, D, 0 if cos.shape[0] == 1 else S * D, N.ptr(oq), N.ptr(ok), N.stream_of(q))
+    return oq.transpose(1, 2), ok.transpose(1, 2)
+
+
+def silu_mul(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    """act_fn(gate) * up with SiLU, one pass."""
+    gate = gate.contiguous()
+    up = up.contiguous()
+    if gate.shape != up.shape or gate.dtype != up.dtype:
+        raise ValueError('gate / up must match')
+    out = torch.empty_like(gate)
+    N.call('lcq_silu_mul', N.ptr(gate), N.ptr(up), N.dt(gate.dtype), gate.numel(), N.ptr(out),
+           N.stream_of(gate))
+    return out
