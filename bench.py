@@ -128,23 +128,39 @@ class GemmMeter:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
             x = inp[0]
-            flops = 2.0 * x.numel() // x.shape[-1] * m.in_features * m.out_features
-            self.records.append((m._lcq_ev, e, flops))
+            rows = x.numel() // x.shape[-1]
+            flops = 2.0 * rows * m.in_features * m.out_features
+            nbytes = 2.0 * (rows * m.in_features + m.in_features * m.out_features
+                            + rows * m.out_features)  # bf16 x, W, y once each
+            self.records.append((m._lcq_ev, e, flops, nbytes))
             del m._lcq_ev
 
     def summary(self):
         torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for a, b, _ in self.records]
-        fl = [f for _, _, f in self.records]
+        ms = [a.elapsed_time(b) for a, b, _, _ in self.records]
+        fl = [f for _, _, f, _ in self.records]
+        by = [b for _, _, _, b in self.records]
         if not ms:
             return None
         return {'launches': len(ms), 'avg_ms': sum(ms) / len(ms), 'total_ms': sum(ms),
-                'flops_per_launch': sum(fl) / len(fl),
+                'flops_per_launch': sum(fl) / len(fl), 'bytes_per_launch': sum(by) / len(by),
                 'tflops': sum(fl) / (sum(ms) * 1e-3) / 1e12}
 
     def close(self):
         for h in self.handles:
             h.remove()
+
+
+def pmc_traffic(leg, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
+    round (profiles/*_pmc_traffic_<leg>.json, made by scripts/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2 FETCH correction), or None."""
+    files = sorted((ROOT / 'profiles').glob(f'*_pmc_traffic_{leg}.json'))
+    if not files:
+        return None, None
+    d = json.loads(files[-1].read_text())
+    k = d.get('kernels', {}).get(kernel)
+    return (k['hbm_bytes'] if k else None), str(files[-1].relative_to(ROOT))
 
 
 def deploy_block(algo, model, block, idx):
@@ -154,8 +170,12 @@ def deploy_block(algo, model, block, idx):
 
 
 def cpu_baseline(args, budget_s):
-    """Oracle (reference algorithm restated on torch-CPU) on a bounded sample of one step,
-    extrapolated to the full step. Returns the cpu_baseline object."""
+    """Oracle (the reference algorithm restated on torch-CPU, pinned to the reference's
+    outputs by tests/golden) timed on a bounded sample of one AWQ block step on the host
+    cores, then extrapolated linearly to the full step. The sample is sized by wall time
+    (~budget_s): as many calibration samples x (org + one ratio) per subset as fit in ~60% of
+    the budget, auto-clip on as many 64-row chunks of gate_proj as fit in the next ~25%, and
+    the real-quant + vLLM pack of one gate_proj."""
     from transformers import LlamaConfig
     from transformers.models.llama import modeling_llama as ml
     from oracle import awq_ref as A
@@ -171,51 +191,66 @@ def cpu_baseline(args, budget_s):
                 p.normal_(0, 0.02)
     rot = ml.LlamaRotaryEmbedding(cfg)
     seq = args.seq_len
-    x = synthetic_hidden(1, seq, cfg.hidden_size, 'cpu', 7)
     pos = torch.arange(seq).unsqueeze(0)
-    kw = {'position_embeddings': rot(x, pos), 'attention_mask': None, 'position_ids': pos}
-    t_total_est = 0.0
-    parts = {}
     t_start = time.perf_counter()
+    fwd_t, org_t, ratio_t = [], {}, {}
+    n_done = 0
     with torch.no_grad():
-        xq = layer.input_layernorm(x)
-        h = x + layer.self_attn(xq, **kw)[0]
-        xm = layer.post_attention_layernorm(h)
-        xd = layer.mlp.act_fn(layer.mlp.gate_proj(xm)) * layer.mlp.up_proj(xm)
-        subsets = {
-            'qkv': (xq, [layer.self_attn.q_proj, layer.self_attn.k_proj, layer.self_attn.v_proj],
-                    lambda t: layer.self_attn(t, **kw)[0]),
-            'mlp': (xm, [layer.mlp.gate_proj, layer.mlp.up_proj], layer.mlp),
-            'down': (xd, [layer.mlp.down_proj], layer.mlp.down_proj),
-        }
-        # one sample (seq tokens), org forward + ONE ratio (scales, fake quant, forward, loss)
-        for name, (xin, mods, fwd) in subsets.items():
+        while True:
+            x = synthetic_hidden(1, seq, cfg.hidden_size, 'cpu', 7 + n_done)
+            kw = {'position_embeddings': rot(x, pos), 'attention_mask': None, 'position_ids': pos}
             t0 = time.perf_counter()
-            org = fwd(xin)
-            t1 = time.perf_counter()
-            s = A.scales_v2(A.act_scale(xin), 0.5)
-            saved = [m.weight.data for m in mods]
-            for m in mods:
-                m.weight.data = A.fake_quant_scaled(m.weight.data, s, 4, True, 128)
-            out = fwd(xin / s.view(1, -1))
-            A.loss(org, out)
-            for m, w in zip(mods, saved):
-                m.weight.data = w
-            t2 = time.perf_counter()
-            per_sample = (t1 - t0) + 20 * (t2 - t1)       # org + 20 ratios
-            est = per_sample * args.n_samples               # linear in tokens
-            parts[f'search_{name}'] = est
-            t_total_est += est
-        # auto-clip: 64 rows of gate_proj on the 512 sampled tokens, extrapolated by OC*IC
-        w = layer.mlp.gate_proj.weight.data[:64].clone()
+            xq = layer.input_layernorm(x)
+            h = x + layer.self_attn(xq, **kw)[0]
+            xm = layer.post_attention_layernorm(h)
+            xd = layer.mlp.act_fn(layer.mlp.gate_proj(xm)) * layer.mlp.up_proj(xm)
+            h + layer.mlp.down_proj(xd)
+            fwd_t.append(time.perf_counter() - t0)
+            subsets = {
+                'qkv': (xq, [layer.self_attn.q_proj, layer.self_attn.k_proj,
+                             layer.self_attn.v_proj], lambda t: layer.self_attn(t, **kw)[0]),
+                'mlp': (xm, [layer.mlp.gate_proj, layer.mlp.up_proj], layer.mlp),
+                'down': (xd, [layer.mlp.down_proj], layer.mlp.down_proj),
+            }
+            for name, (xin, mods, fwd) in subsets.items():
+                t0 = time.perf_counter()
+                org = fwd(xin)
+                t1 = time.perf_counter()
+                ratio = ((n_done % 20) + 1) / 20
+                s = A.scales_v2(A.act_scale(xin), ratio)
+                saved = [m.weight.data for m in mods]
+                for m in mods:
+                    m.weight.data = A.fake_quant_scaled(m.weight.data, s, 4, True, 128)
+                out = fwd(xin / s.view(1, -1))
+                A.loss(org, out)
+                for m, w in zip(mods, saved):
+                    m.weight.data = w
+                t2 = time.perf_counter()
+                org_t.setdefault(name, []).append(t1 - t0)
+                ratio_t.setdefault(name, []).append(t2 - t1)
+            n_done += 1
+            if time.perf_counter() - t_start > 0.6 * budget_s or n_done >= args.n_samples:
+                break
+        parts = {'block_forward': sum(fwd_t) / len(fwd_t) * args.n_samples}
+        for name in org_t:
+            per_sample = (sum(org_t[name]) / len(org_t[name])
+                          + 20 * sum(ratio_t[name]) / len(ratio_t[name]))
+            parts[f'search_{name}'] = per_sample * args.n_samples  # linear in tokens
+        # auto-clip of gate_proj rows in 64-row chunks on the 512 sampled tokens, extrapolated
+        # by OC*IC to every clipped linear (v, o, gate, up, down)
         xs = xm.reshape(-1, cfg.hidden_size)[: seq]
-        t0 = time.perf_counter()
-        A.clip_layer(w, xs, 4, True, 128, True, n_sample_token=seq)
-        t_clip = time.perf_counter() - t0
+        t_clip, rows = 0.0, 0
+        while rows < cfg.intermediate_size:
+            w = layer.mlp.gate_proj.weight.data[rows:rows + 64].clone()
+            t0 = time.perf_counter()
+            A.clip_layer(w, xs, 4, True, 128, True, n_sample_token=seq)
+            t_clip += time.perf_counter() - t0
+            rows += 64
+            if time.perf_counter() - t_start > 0.85 * budget_s:
+                break
         clipped = (cfg.num_key_value_heads * cfg.head_dim * cfg.hidden_size
                    + cfg.hidden_size ** 2 + 3 * cfg.intermediate_size * cfg.hidden_size)
-        parts['auto_clip'] = t_clip * clipped / w.numel()
-        t_total_est += parts['auto_clip']
+        parts['auto_clip'] = t_clip * clipped / (rows * cfg.hidden_size)
         # deploy: real quant + vLLM pack of one gate_proj, extrapolated to the 7 linears
         t0 = time.perf_counter()
         codes, sc, _ = Q.real_quant_dynamic(layer.mlp.gate_proj.weight.data, 4, True)
@@ -223,16 +258,18 @@ def cpu_baseline(args, budget_s):
         t_dep = time.perf_counter() - t0
         all_params = clipped + (cfg.hidden_size + cfg.num_key_value_heads * cfg.head_dim) * cfg.hidden_size
         parts['deploy'] = t_dep * all_params / layer.mlp.gate_proj.weight.numel()
-        t_total_est += parts['deploy']
+    t_total_est = sum(parts.values())
     wall = time.perf_counter() - t_start
     return {'value': N_LINEARS_PER_BLOCK / t_total_est, 'unit': 'linears/s', 'cores': threads,
             'kind': 'port',
-            'sample': (f'oracle (torch-CPU restatement of awq.py/auto_clip.py/quant.py) on one '
-                       f'Llama-3-8B block: 1 of {args.n_samples} calibration samples x org+1 of '
-                       f'20 ratios per subset, auto-clip on 64 gate_proj rows, real-quant+pack '
-                       f'of one gate_proj; extrapolated linearly to the full step '
-                       f'({t_total_est:.0f} s/block est., {wall:.1f} s measured)'),
-            'est_s_per_block': t_total_est, 'parts_s': parts}
+            'sample': (f'oracle (torch-CPU restatement of awq.py/auto_clip.py/quant.py, pinned to '
+                       f'the reference by tests/golden) on one Llama-3-8B block: {n_done} of '
+                       f'{args.n_samples} calibration samples x (org + 1 of 20 ratios) per '
+                       f'subset, auto-clip of {rows} gate_proj rows, real-quant+pack of one '
+                       f'gate_proj; {wall:.1f} s measured, extrapolated linearly to '
+                       f'{t_total_est:.0f} s per block step'),
+            'est_s_per_block': round(t_total_est, 1),
+            'parts_s': {k: round(v, 1) for k, v in parts.items()}}
 
 
 def timed_blocks(step, warmup, steps, world, dev):
@@ -304,10 +341,13 @@ def bench_gptq(args, rank, world, dev):
         # algorithmic: symmetric rank-n update n*ic*(ic+1) flops per launch;
         # KernelTimer records the flops each launch was given
         tf = h['flops'] / (h['total_ms'] * 1e-3) / 1e12
-        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_hessian_syrk, bf16 MFMA XᵀX)',
+        traffic, src = pmc_traffic('gptq', 'k_syrk256')
+        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_xt_pack + k_syrk256, bf16 MFMA XᵀX)',
                            'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
                            'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4),
-                           'traffic': None, 'avg_launch_ms': round(h['avg_ms'], 4)}
+                           'traffic': traffic, 'traffic_source': src,
+                           'avg_launch_ms': round(h['avg_ms'], 4),
+                           'flops_per_launch': h['flops'] / h['launches']}
     del algo, model, hidden, calib
     torch.cuda.empty_cache()
     return out
@@ -383,11 +423,14 @@ def main():
     if rank == 0:
         roofline = None
         if gemm:
+            traffic, src = pmc_traffic('awq', 'hipblaslt_gemm')
             roofline = {'kernel': 'bf16 projection GEMM of the AWQ loss search (q/k/v/o/gate/up/'
                                   'down, hipBLASLt via the HF module forward)',
                         'bound': 'mfma', 'achieved': round(gemm['tflops'], 1),
                         'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
-                        'frac': round(gemm['tflops'] / PEAK_BF16_TFLOPS, 4), 'traffic': None,
+                        'frac': round(gemm['tflops'] / PEAK_BF16_TFLOPS, 4),
+                        'traffic': traffic, 'traffic_source': src,
+                        'algorithmic_bytes_per_launch': gemm['bytes_per_launch'],
                         'avg_launch_ms': round(gemm['avg_ms'], 4),
                         'flops_per_launch': gemm['flops_per_launch'],
                         'share_of_step': round(gemm['total_ms'] / (elapsed * 1e3), 3)}
