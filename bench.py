@@ -57,7 +57,8 @@ def parse():
     ap.add_argument('--n-samples', type=int, default=128)
     ap.add_argument('--seq-len', type=int, default=512)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--algo', choices=['awq', 'gptq', 'both'], default='both')
+    ap.add_argument('--algo', choices=['awq', 'gptq', 'fp8', 'both', 'all'], default='all')
+    ap.add_argument('--fp8-experts', type=int, default=32)
     ap.add_argument('--gptq-steps', type=int, default=2)
     ap.add_argument('--gptq-samples', type=int, default=128)
     ap.add_argument('--gptq-seq-len', type=int, default=2048)
@@ -301,6 +302,67 @@ def kernel_table(kern, elapsed):
             for k, v in sorted(kern.items(), key=lambda kv: -kv[1]['total_ms'])}
 
 
+DSV3_EXPERT = dict(hidden=7168, moe_inter=2048, block=128)
+
+
+def bench_fp8(args, rank, world, dev):
+    """FP8 leg (BASELINE.json configs[4]): DeepSeek-V3 expert linears (gate/up 2048x7168,
+    down 7168x2048) stored block-fp8 (128x128, fp32 scale_inv) as in the checkpoints; one unit
+    = one expert linear through the reference's real-quant deploy for an fp8 weight:
+    weight_cast_to_bf16 (module_utils.py:917-922) + FloatQuantizer(e4m3, per_tensor)
+    .real_quant_weight_dynamic (quant.py:1191-1221). One step = args.fp8_experts experts x 3
+    linears per rank (experts shard across ranks: weak scaling, no collective)."""
+    from lightcompress_amd import _native, ops
+    from lightcompress_amd.quant import FloatQuantizer
+    E = args.fp8_experts
+    H, I = DSV3_EXPERT['hidden'], DSV3_EXPERT['moe_inter']
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    shapes = [(I, H), (I, H), (H, I)]
+    weights = []
+    for e in range(E):
+        for (m, n) in shapes:
+            w = (torch.randn(m, n, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+            r = ops.fp8_quant_blocks(w, torch.float8_e4m3fn, 128, qmax=448.0, clamp_min=0.0,
+                                     add_zero=False)
+            weights.append((r['codes'], r['scales']))
+        del w
+    q = FloatQuantizer('e4m3', True, 'per_tensor', use_qtorch=True)
+
+    def step(_):
+        for codes, sinv in weights:
+            q.real_quant_weight_from_block_fp8(codes, sinv, 128)
+
+    timer = _native.KernelTimer()
+    step(0)
+    torch.cuda.synchronize()
+    steps = args.steps
+    with timer:
+        elapsed = timed_blocks(step, 0, steps, world, dev)
+    kern = timer.summary()
+    units = 3 * E * steps * world
+    elems = sum(c.numel() for c, _ in weights)
+    out = {'linears_per_s': round(units / elapsed, 1), 'ms_per_step': round(elapsed / steps * 1e3, 3),
+           'steps': steps, 'warmup': 1,
+           'workload': (f'DeepSeek-V3 MoE expert linears (gate/up 2048x7168, down 7168x2048), '
+                        f'block-fp8 source -> bf16 -> FP8 e4m3 per-tensor real quant; '
+                        f'{E} experts x 3 linears per rank per step'),
+           'lcq_kernels': kernel_table(kern, elapsed)}
+    t = kern.get('lcq_fp8_block_to_tensor')
+    if t:
+        # algorithmic bytes per expert linear: 1 B fp8 read + 1 B fp8 written per element
+        # (+ fp32 block scales); the amax pass re-reads the 1 B codes (counted as overhead)
+        gbs = elems * 2.0 * steps / (t['total_ms'] * 1e-3) / 1e9
+        traffic, src = pmc_traffic('fp8', 'k_requant_blockfp8')
+        out['roofline'] = {'kernel': 'lcq_fp8_block_to_tensor (k_absmax_blockfp8 + '
+                                     'k_requant_blockfp8)', 'bound': 'hbm',
+                           'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+                           'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic,
+                           'traffic_source': src, 'avg_launch_ms': round(t['avg_ms'], 4)}
+    del weights
+    torch.cuda.empty_cache()
+    return out
+
+
 def bench_gptq(args, rank, world, dev):
     """GPTQ leg: per-block wall-clock and the Hessian kernel's roofline."""
     from transformers import LlamaConfig
@@ -358,17 +420,36 @@ def main():
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    # one process per GPU (RCCL). LCQ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
+    # (ranks then share devices round-robin); the driver's runs use the default.
+    backend = os.environ.get('LCQ_DIST_BACKEND', 'nccl')
+    ndev = torch.cuda.device_count()
+    if backend == 'nccl' and world > ndev:
+        raise SystemExit(f'{world} ranks need {world} GPUs ({ndev} visible)')
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from transformers import LlamaConfig
     from lightcompress_amd import _native
     from lightcompress_amd.llama import Llama
     from lightcompress_amd.pipeline import build_algo
 
     _native.load()
-    gptq = bench_gptq(args, rank, world, dev) if args.algo in ('gptq', 'both') else None
+    fp8 = bench_fp8(args, rank, world, dev) if args.algo in ('fp8', 'all') else None
+    if args.algo == 'fp8':
+        if rank == 0:
+            print(json.dumps({'metric': 'FP8 expert linears quantized/sec (DSv3 MoE, e4m3 '
+                              'per-tensor)', 'value': fp8['linears_per_s'], 'unit': 'linears/s',
+                              'n_gpus': world, 'fp8': fp8}))
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    gptq = bench_gptq(args, rank, world, dev) if args.algo in ('gptq', 'both', 'all') else None
     if args.algo == 'gptq':
         if rank == 0:
             print(json.dumps({'metric': 'linear-layers quantized/sec (Llama-3-8B GPTQ w4a16 '
@@ -452,6 +533,7 @@ def main():
                        'parallelism': f'blocks sharded over {world} GPU(s), no collective'},
             'extrapolated_model_wall_s': round(ms_per_step * 32 / 1e3, 2),
             'gptq': gptq,
+            'fp8': fp8,
             'roofline': roofline,
             'lcq_kernels': kernels,
             'cpu_baseline': cpu,

@@ -126,7 +126,7 @@ int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t ic, void* H
  * GPTQ in-block column loop for one 128-column block (GPTQ.weight_transform, gptq.py:198-244,
  * group qparams gptq.py:358-366). W [rows, ld] fp32 in (act-order permuted) column space:
  * columns [col0, col0+count) are replaced by the error-compensated weights (`tmp`);
- * err [rows, 128] receives Err1 for the caller's trailing update
+ * err (k-major [128, rows]: err[k * rows + r]) receives Err1 for the caller's trailing update
  * W[:, col0+count:] -= err @ U[col0:col0+count, col0+count:].
  * U [ldu, ldu] fp32 upper Cholesky factor of H^-1. group in {32, 64, 128}: per-group minmax
  * qparams from the block-start weights written to s_out/z_out [rows, ng_total] (fp32);
@@ -140,7 +140,7 @@ int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, c
 
 /* GPTQ trailing update W[:, c1:] -= err[:, :cnt] @ U[c0:c0+cnt, c1:] (gptq.py:244) on fp32
  * MFMA (k-ordered fma chain: deterministic and independent of the row range, so row-sharded
- * GPTQ is bit-identical to one GPU). err [rows, 128] fp32 from lcq_gptq_block. */
+ * GPTQ is bit-identical to one GPU). err k-major [128, rows] fp32 from lcq_gptq_block. */
 int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, int cnt, int64_t c1,
                       const void* err, const void* U, int64_t ldu, void* stream);
 
@@ -226,6 +226,16 @@ int lcq_fp8_quant_blocks(const void* x, int x_dtype, int64_t M, int64_t N, int b
  * scales[r / block][c / block]); codes uint8 [M, N], scales fp32 [ceil(M/b), ceil(N/b)]. */
 int lcq_fp8_dequant_blocks(const void* codes, int fmt, int64_t M, int64_t N, int block,
                            const void* scales, void* out, int out_dtype, void* stream);
+
+/* Deploy of a block-fp8 checkpoint weight to per-tensor fp8 (module_utils.py:917-922 +
+ * quant.py:1191-1221): w = bf16(float(code) * scales_inv[block]) (weight_cast_to_bf16) kept in
+ * registers, then per-tensor FloatQuantizer real quant of w (bf16 compute, fp32 scale).
+ * amax_ws: one device fp32 of scratch. scale_out: one fp32. Bit-identical to the composed
+ * lcq_fp8_dequant_blocks -> lcq_absmax -> lcq_fp8_quant chain at 3 instead of 8 B/element. */
+int lcq_fp8_block_to_tensor(const void* codes, int fmt_in, int64_t M, int64_t N, int block,
+                            const void* scales_inv, int fmt_out, float qmax, float clamp_min,
+                            int add_zero, void* amax_ws, void* codes_out, void* scale_out,
+                            void* stream);
 
 /* FloatQuantizer use_qtorch=False fake quant (get_float_qparams, quant.py:1005-1027, and
  * quant/dequant :1061-1076): per group of `group` elements, power-of-two per-element scales

@@ -309,6 +309,66 @@ __global__ void __launch_bounds__(256) k_fp8_blocks(Fp8Args a, int64_t M, int64_
     reinterpret_cast<float*>(a.s_out)[blockIdx.y * gridDim.x + blockIdx.x] = s;
 }
 
+// ---- block-fp8 -> per-tensor fp8, bf16 intermediate kept in registers ------------------
+// The reference deploy of an fp8 checkpoint weight (module_utils.py:917-922 + quant.py:
+// 1191-1221): w = bf16(float(code) * s_inv[block]) (weight_cast_to_bf16), then per-tensor
+// FloatQuantizer real quant of w. Pass 1 = max|w| over the dequantized values, pass 2 =
+// dequantize again and quantize: 1 + 1 B read, 1 B written per element (the composed chain
+// moves 8 B per element).
+template <int FIN>
+__device__ __forceinline__ void deq8_bf16(const uint8_t* codes, const float* s, int64_t N,
+                                          int bs, int64_t nb, int64_t e0, float (&w)[8]) {
+  const int64_t r = e0 / N, c = e0 % N;
+  const float sc = s[(r / bs) * nb + c / bs];
+  const uint2 u = *reinterpret_cast<const uint2*>(codes + e0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    w[j] = bf16_rne(dec<FIN>((u.x >> (8 * j)) & 0xffu) * sc);
+    w[4 + j] = bf16_rne(dec<FIN>((u.y >> (8 * j)) & 0xffu) * sc);
+  }
+}
+
+template <int FIN>
+__global__ void __launch_bounds__(256) k_absmax_blockfp8(const uint8_t* codes, const float* s,
+                                                         int64_t M, int64_t N, int bs,
+                                                         uint32_t* out) {
+  __shared__ float red[4];
+  const int64_t n8 = M * N / 8, nb = (N + bs - 1) / bs;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float am = 0.f;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
+    float w[8];
+    deq8_bf16<FIN>(codes, s, N, bs, nb, t * 8, w);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(w[j]));
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) am = fmaxf(am, __shfl_xor(am, m, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]),
+                                                             fmaxf(red[2], red[3]))));
+}
+
+template <int FIN, int FOUT>
+__global__ void __launch_bounds__(256) k_requant_blockfp8(const uint8_t* codes, const float* s,
+                                                          int64_t M, int64_t N, int bs,
+                                                          const float* amax, float qmax,
+                                                          float clamp_min, int add_zero,
+                                                          uint8_t* out, float* s_out) {
+  const float sc = fp8_scale<LCQ_BF16, LCQ_F32>(*amax, qmax, clamp_min, add_zero);
+  const int64_t n8 = M * N / 8, nb = (N + bs - 1) / bs;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
+    float w[8], dq[8];
+    uint32_t c[8];
+    deq8_bf16<FIN>(codes, s, N, bs, nb, t * 8, w);
+    fp8_qdq8<LCQ_BF16, FOUT>(w, sc, add_zero, c, dq);
+    st_codes8(out, t * 8, c);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && s_out) *s_out = sc;
+}
+
 // ---- block dequant: out = rnd_out(float(code) * s[block])  (weight_cast_to_bf16) --------
 template <int FMT, int OT>
 __global__ void __launch_bounds__(256) k_fp8_dequant_blocks(const uint8_t* codes,
@@ -594,6 +654,45 @@ extern "C" int lcq_fp8_dequant_blocks(const void* codes, int fmt, int64_t M, int
   }
 #undef LCQ_DQ
   return check_launch("lcq_fp8_dequant_blocks");
+}
+
+extern "C" int lcq_fp8_block_to_tensor(const void* codes, int fmt_in, int64_t M, int64_t N,
+                                       int block, const void* scales_inv, int fmt_out,
+                                       float qmax, float clamp_min, int add_zero,
+                                       void* amax_ws, void* codes_out, void* scale_out,
+                                       void* stream) {
+  LCQ_REQUIRE(fmt_in == LCQ_FP8E4M3 || fmt_in == LCQ_FP8E5M2, "bad input format");
+  LCQ_REQUIRE(fmt_out == LCQ_FP8E4M3 || fmt_out == LCQ_FP8E5M2, "bad output format");
+  LCQ_REQUIRE(block > 0 && M > 0 && N > 0 && N % 8 == 0, "N must be a positive multiple of 8");
+  LCQ_REQUIRE(amax_ws != nullptr && codes_out != nullptr && qmax > 0.f, "missing buffers");
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(amax_ws, 0, sizeof(float), st) != hipSuccess)
+    return fail(LCQ_ELAUNCH, "lcq_fp8_block_to_tensor: memset failed");
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(codes);
+  const float* s = reinterpret_cast<const float*>(scales_inv);
+  const unsigned g1 = std::min<unsigned>(stream_grid(M * N / 8, 256), 2048u);
+  if (fmt_in == LCQ_FP8E4M3)
+    hipLaunchKernelGGL(k_absmax_blockfp8<LCQ_FP8E4M3>, g1, 256, 0, st, c, s, M, N, block,
+                       reinterpret_cast<uint32_t*>(amax_ws));
+  else
+    hipLaunchKernelGGL(k_absmax_blockfp8<LCQ_FP8E5M2>, g1, 256, 0, st, c, s, M, N, block,
+                       reinterpret_cast<uint32_t*>(amax_ws));
+  int rc = check_launch("lcq_fp8_block_to_tensor: amax");
+  if (rc) return rc;
+  const unsigned g2 = stream_grid(M * N / 8, 256);
+  const float* am = reinterpret_cast<const float*>(amax_ws);
+  uint8_t* o = reinterpret_cast<uint8_t*>(codes_out);
+  float* so = reinterpret_cast<float*>(scale_out);
+#define LCQ_RQ(FI, FO) \
+  hipLaunchKernelGGL((k_requant_blockfp8<FI, FO>), g2, 256, 0, st, c, s, M, N, block, am, qmax, \
+                     clamp_min, add_zero, o, so)
+  if (fmt_in == LCQ_FP8E4M3) {
+    if (fmt_out == LCQ_FP8E4M3) LCQ_RQ(LCQ_FP8E4M3, LCQ_FP8E4M3); else LCQ_RQ(LCQ_FP8E4M3, LCQ_FP8E5M2);
+  } else {
+    if (fmt_out == LCQ_FP8E4M3) LCQ_RQ(LCQ_FP8E5M2, LCQ_FP8E4M3); else LCQ_RQ(LCQ_FP8E5M2, LCQ_FP8E5M2);
+  }
+#undef LCQ_RQ
+  return check_launch("lcq_fp8_block_to_tensor: requant");
 }
 
 extern "C" int lcq_fp_emul_quant(const void* x, int x_dtype, int64_t rows, int64_t cols,

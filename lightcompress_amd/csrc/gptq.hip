@@ -35,77 +35,141 @@ struct GptqArgs {
   float* losses;      // optional [rows, ld]
 };
 
+// 8 lanes per row, 16 consecutive block columns per lane (32 rows per 256-thread workgroup).
+// Column c's owner lane (c / 16) quantizes it; its error is broadcast to the row's other 7
+// lanes with one shuffle; every lane applies the rank-1 update to its own columns > c. W, err
+// and losses are written once at the end with 16-byte stores (a row's 8 lanes cover 512
+// contiguous bytes). err is written k-major ([128][rows]) for the trailing GEMM's staging.
+constexpr int LPR = 8, CPL = GB / LPR;
+
 template <int GS>
 __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
   __shared__ float u[GB * GB];
   const int tid = threadIdx.x;
-  for (int idx = tid; idx < GB * GB; idx += 256) {
+  for (int idx = tid * 4; idx < GB * GB; idx += 256 * 4) {
     const int i = idx / GB, j = idx % GB;
-    u[idx] = (i < a.count && j < a.count) ? a.U[(a.col0 + i) * a.ldu + a.col0 + j] : 0.f;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < a.count) {
+      const float* src = a.U + (a.col0 + i) * a.ldu + a.col0 + j;
+      if (j + 3 < a.count) {
+        v = *reinterpret_cast<const float4*>(src);
+      } else {
+        if (j + 0 < a.count) v.x = src[0];
+        if (j + 1 < a.count) v.y = src[1];
+        if (j + 2 < a.count) v.z = src[2];
+      }
+    }
+    *reinterpret_cast<float4*>(&u[idx]) = v;
   }
   __syncthreads();
-  const int64_t r = (int64_t)blockIdx.x * 256 + tid;
-  if (r >= a.rows) return;  // no barriers below
-  float* wrow = a.W + r * a.ld + a.col0;
-  float w[GB];
+  const int sub = tid & (LPR - 1);
+  const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + (tid >> 3);
+  const bool valid = r < a.rows;  // invalid lanes still run (shuffles), never store
+  const int cb = sub * CPL;       // first block column of this lane
+  float* wrow = a.W + (valid ? r : 0) * a.ld + a.col0;
+  float w[CPL];
 #pragma unroll
-  for (int j = 0; j < GB; j += 4) {
-    if (j + 3 < a.count) {
-      float4 v = *reinterpret_cast<const float4*>(wrow + j);
-      w[j] = v.x; w[j + 1] = v.y; w[j + 2] = v.z; w[j + 3] = v.w;
+  for (int k = 0; k < CPL; k += 4) {
+    if (valid && cb + k + 3 < a.count) {
+      const float4 v = *reinterpret_cast<const float4*>(wrow + cb + k);
+      w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
     } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) w[j + k] = (j + k < a.count) ? wrow[j + k] : 0.f;
+      for (int q = 0; q < 4; ++q) w[k + q] = (valid && cb + k + q < a.count) ? wrow[cb + k + q] : 0.f;
     }
   }
-  // group qparams from the block-start weights (gptq.py:215-223 reads W, not W1)
-  constexpr int NG = (GS > 0) ? GB / GS : 1;
-  float qs[NG], qz[NG];
+  // group qparams from the block-start weights (gptq.py:215-223 reads W, not W1); GS >= 32
+  // so a lane's 16 columns lie in one group of GS / 16 adjacent lanes
+  float qs, qz;
   if constexpr (GS > 0) {
+    constexpr int LG = GS / CPL;  // lanes per group (2, 4, 8)
+    float mn = INFINITY, mx = -INFINITY;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      float mn = w[g * GS], mx = w[g * GS];
+    for (int k = 0; k < CPL; ++k)
+      if (cb + k < a.count) {  // a group cut by the end of the columns uses its valid part
+        mn = fminf(mn, w[k]);
+        mx = fmaxf(mx, w[k]);
+      }
 #pragma unroll
-      for (int j = 1; j < GS; ++j) {
-        // a group truncated by the end of the quantized columns uses only its valid part
-        if (g * GS + j < a.count) {
-          mn = fminf(mn, w[g * GS + j]);
-          mx = fmaxf(mx, w[g * GS + j]);
-        }
-      }
-      qparams_f32(mn, mx, a.qmin, a.qmax, a.sym, qs[g], qz[g]);
-      if (g * GS < a.count) {
-        const int64_t gi = (a.col0 + g * GS) / GS;
-        a.s_out[r * a.ng_total + gi] = qs[g];
-        if (a.z_out && !a.sym) a.z_out[r * a.ng_total + gi] = qz[g];
-      }
+    for (int m = LG / 2; m >= 1; m >>= 1) {
+      mn = fminf(mn, __shfl_xor(mn, m, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+    }
+    qparams_f32(mn, mx, a.qmin, a.qmax, a.sym, qs, qz);
+    if (valid && (sub % LG) == 0 && cb < a.count) {
+      const int64_t gi = (a.col0 + cb) / GS;
+      a.s_out[r * a.ng_total + gi] = qs;
+      if (a.z_out && !a.sym) a.z_out[r * a.ng_total + gi] = qz;
     }
   } else {
-    qs[0] = a.s_in[r];
-    qz[0] = a.z_in ? a.z_in[r] : 0.f;
+    qs = valid ? a.s_in[r] : 1.f;
+    qz = (valid && a.z_in) ? a.z_in[r] : 0.f;
   }
-  float* erow = a.err + r * GB;
+  float ek[CPL], lk[CPL];
+  const int rowlane = tid & ~(LPR - 1);
 #pragma unroll
   for (int c = 0; c < GB; ++c) {
     if (c < a.count) {
-      const float s = qs[(GS > 0) ? c / (GS > 0 ? GS : 1) : 0];
-      const float z = qz[(GS > 0) ? c / (GS > 0 ? GS : 1) : 0];
+      const int owner = c / CPL, jl = c % CPL;
+      // every lane evaluates its own column jl; only the owner's value is used
       const float d = u[c * GB + c];
-      const float wc = w[c];
-      float t = rintf(wc / s);
-      t = t + z;
+      const float wc = w[jl];
+      float t = rintf(wc / qs);
+      t = t + qz;
       t = fminf(fmaxf(t, a.qmin), a.qmax);
-      const float q = (t - z) * s;
+      const float q = (t - qz) * qs;
       const float diff = wc - q;
-      const float e = diff / d;
-      wrow[c] = wc;  // tmp1[:, i] = w
-      erow[c] = e;
-      if (a.losses) a.losses[r * a.ld + a.col0 + c] = (diff * diff) / (2.f * (d * d));
+      const float e = __shfl(diff / d, rowlane | owner, 64);
+      if (sub == owner) {
+        ek[jl] = e;
+        lk[jl] = (diff * diff) / (2.f * (d * d));
+      }
+      const bool ge = sub >= owner, gt = sub > owner;
+      const float* urow = u + c * GB + cb;
 #pragma unroll
-      for (int j = c + 1; j < GB; ++j) w[j] = w[j] - e * u[c * GB + j];
+      for (int k = 0; k < CPL; k += 4) {
+        const float4 uv = *reinterpret_cast<const float4*>(urow + k);
+        const float uu[4] = {uv.x, uv.y, uv.z, uv.w};
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const bool upd = (k + q4 > jl) ? ge : gt;  // block column cb + k + q4 > c
+          const float nw = w[k + q4] - e * uu[q4];
+          w[k + q4] = upd ? nw : w[k + q4];
+        }
+      }
     } else {
-      erow[c] = 0.f;
+      const int jl = c % CPL;
+      if (sub == c / CPL) {
+        ek[jl] = 0.f;
+        lk[jl] = 0.f;
+      }
     }
+  }
+  if (!valid) return;
+  // tmp1 / Err1 / Losses1 (gptq.py:234-238): w[k] is final once its column was processed
+#pragma unroll
+  for (int k = 0; k < CPL; k += 4) {
+    if (cb + k + 3 < a.count) {
+      *reinterpret_cast<float4*>(wrow + cb + k) = make_float4(w[k], w[k + 1], w[k + 2], w[k + 3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (cb + k + q < a.count) wrow[cb + k + q] = w[k + q];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) a.err[(int64_t)(cb + k) * a.rows + r] = ek[k];
+  if (a.losses) {
+#pragma unroll
+    for (int k = 0; k < CPL; k += 4)
+      if (cb + k + 3 < a.count) {
+        *reinterpret_cast<float4*>(a.losses + r * a.ld + a.col0 + cb + k) =
+            make_float4(lk[k], lk[k + 1], lk[k + 2], lk[k + 3]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (cb + k + q < a.count) a.losses[r * a.ld + a.col0 + cb + k + q] = lk[k + q];
+      }
   }
 }
 
@@ -121,6 +185,7 @@ extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, i
   LCQ_REQUIRE(rows > 0 && ld > 0 && count > 0 && count <= GB, "bad block shape");
   LCQ_REQUIRE(col0 >= 0 && col0 + count <= ld && col0 + count <= ldu, "block out of range");
   LCQ_REQUIRE(col0 % GB == 0, "col0 must be a multiple of the 128-column blocksize");
+  LCQ_REQUIRE(ld % 4 == 0 && ldu % 4 == 0, "row lengths must be multiples of 4 (16-B rows)");
   LCQ_REQUIRE(qmax > qmin, "qmax <= qmin");
   GptqArgs a{};
   a.W = reinterpret_cast<float*>(W);
@@ -134,7 +199,9 @@ extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, i
   a.ng_total = ng_total;
   a.err = reinterpret_cast<float*>(err);
   a.losses = reinterpret_cast<float*>(losses);
-  const dim3 grid((unsigned)((rows + 255) / 256));
+  LCQ_REQUIRE(group == 0 || group == 32 || group == 64 || group == 128,
+              "group must be 0 (per-row qparams), 32, 64 or 128");
+  const dim3 grid((unsigned)((rows + (256 / LPR) - 1) / (256 / LPR)));
   hipStream_t st = as_stream(stream);
   switch (group) {
     case 32: hipLaunchKernelGGL((k_gptq_block<32>), grid, 256, 0, st, a); break;
@@ -154,25 +221,55 @@ extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, i
 // fp32 MFMA v_mfma_f32_32x32x2_f32: bit-for-bit a k-ordered fmaf chain, so every output
 // element's value is independent of the tiling / row range (row-sharded GPTQ on N GPUs is
 // bit-identical to one GPU). The product is rounded to fp32 and then subtracted, like the
-// reference's `W -= Err @ Hinv` (two roundings). 128x128 tile per 256-thread workgroup,
-// 2x2 waves of 64x64 = 2x2 MFMA 32x32 tiles, K staged through LDS 32 at a time.
+// reference's `W -= Err @ Hinv` (two roundings). 128x128 output tile per 256-thread
+// workgroup (2x2 waves of 64x64 = 2x2 MFMA 32x32 tiles); the whole K = 128 of both operands
+// is staged once in LDS (err arrives k-major [128][rows] from lcq_gptq_block, U rows are
+// k-major already), with conflict-free 16-byte copies and conflict-free operand reads.
 // ---------------------------------------------------------------------------------------
 namespace lcq {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr int TT = 128;   // output tile
-constexpr int TK = 32;    // k chunk
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 1)
     k_gptq_trailing(float* __restrict__ W, int64_t rows, int64_t ld, int64_t c0, int cnt,
-                    int64_t c1, const float* __restrict__ E, const float* __restrict__ U,
+                    int64_t c1, const float* __restrict__ ET, const float* __restrict__ U,
                     int64_t ldu) {
-  __shared__ float As[TK][TT];  // As[k][row]
-  __shared__ float Bs[TK][TT];  // Bs[k][col]
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* As = sm;              // As[k][row]  (128 x 128)
+  float* Bs = sm + GB * TT;    // Bs[k][col]  (128 x 128)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int64_t r0 = (int64_t)blockIdx.y * TT;
   const int64_t j0 = c1 + (int64_t)blockIdx.x * TT;
+#pragma unroll 4
+  for (int it = 0; it < (GB * TT / 4) / 256; ++it) {
+    const int idx = it * 256 + tid;
+    const int k = idx / (TT / 4), c4 = (idx % (TT / 4)) * 4;
+    float4 ea = make_float4(0.f, 0.f, 0.f, 0.f), ub = ea;
+    if (k < cnt) {
+      const float* es = ET + (int64_t)k * rows + r0 + c4;
+      if (r0 + c4 + 3 < rows && (rows & 3) == 0) {
+        ea = *reinterpret_cast<const float4*>(es);
+      } else {
+        if (r0 + c4 + 0 < rows) ea.x = es[0];
+        if (r0 + c4 + 1 < rows) ea.y = es[1];
+        if (r0 + c4 + 2 < rows) ea.z = es[2];
+        if (r0 + c4 + 3 < rows) ea.w = es[3];
+      }
+      const float* us = U + (c0 + k) * ldu + j0 + c4;
+      if (j0 + c4 + 3 < ld) {
+        ub = *reinterpret_cast<const float4*>(us);
+      } else {
+        if (j0 + c4 + 0 < ld) ub.x = us[0];
+        if (j0 + c4 + 1 < ld) ub.y = us[1];
+        if (j0 + c4 + 2 < ld) ub.z = us[2];
+      }
+    }
+    *reinterpret_cast<float4*>(&As[k * TT + c4]) = ea;
+    *reinterpret_cast<float4*>(&Bs[k * TT + c4]) = ub;
+  }
+  __syncthreads();
   v16f acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -180,54 +277,20 @@ __global__ void __launch_bounds__(256)
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
-
-  for (int k0 = 0; k0 < GB; k0 += TK) {
-    __syncthreads();
-    // E tile: 128 rows x 32 k, float4 along k, stored transposed As[k][row]
+#pragma unroll 8
+  for (int kk = 0; kk < GB; kk += 2) {
+    const int k = kk + (lane >> 5);
+    float av[2], bv[2];
 #pragma unroll
-    for (int it = 0; it < (TT * TK / 4) / 256; ++it) {
-      const int idx = it * 256 + tid;
-      const int row = idx / (TK / 4), k4 = (idx % (TK / 4)) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r0 + row < rows) v = *reinterpret_cast<const float4*>(E + (r0 + row) * GB + k0 + k4);
-      As[k4 + 0][row] = (k0 + k4 + 0 < cnt) ? v.x : 0.f;
-      As[k4 + 1][row] = (k0 + k4 + 1 < cnt) ? v.y : 0.f;
-      As[k4 + 2][row] = (k0 + k4 + 2 < cnt) ? v.z : 0.f;
-      As[k4 + 3][row] = (k0 + k4 + 3 < cnt) ? v.w : 0.f;
+    for (int t = 0; t < 2; ++t) {
+      av[t] = As[k * TT + wr * 64 + t * 32 + (lane & 31)];
+      bv[t] = Bs[k * TT + wc * 64 + t * 32 + (lane & 31)];
     }
-    // U tile: 32 k x 128 cols, float4 along cols
 #pragma unroll
-    for (int it = 0; it < (TT * TK / 4) / 256; ++it) {
-      const int idx = it * 256 + tid;
-      const int k = idx / (TT / 4), c4 = (idx % (TT / 4)) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k0 + k < cnt) {
-        const float* src = U + (c0 + k0 + k) * ldu + j0 + c4;
-        if (j0 + c4 + 3 < ld) {
-          v = *reinterpret_cast<const float4*>(src);
-        } else {
-          if (j0 + c4 + 0 < ld) v.x = src[0];
-          if (j0 + c4 + 1 < ld) v.y = src[1];
-          if (j0 + c4 + 2 < ld) v.z = src[2];
-        }
-      }
-      *reinterpret_cast<float4*>(&Bs[k][c4]) = v;
-    }
-    __syncthreads();
+    for (int ta = 0; ta < 2; ++ta)
 #pragma unroll
-    for (int kk = 0; kk < TK; kk += 2) {
-      float a[2], b[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        a[t] = As[kk + (lane >> 5)][wr * 64 + t * 32 + (lane & 31)];
-        b[t] = Bs[kk + (lane >> 5)][wc * 64 + t * 32 + (lane & 31)];
-      }
-#pragma unroll
-      for (int ta = 0; ta < 2; ++ta)
-#pragma unroll
-        for (int tb = 0; tb < 2; ++tb)
-          acc[ta][tb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
-    }
+      for (int tb = 0; tb < 2; ++tb)
+        acc[ta][tb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ta], bv[tb], acc[ta][tb], 0, 0, 0);
   }
   // epilogue (C layout: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5))
 #pragma unroll
@@ -251,8 +314,14 @@ extern "C" int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, 
   LCQ_REQUIRE(c0 >= 0 && c0 + cnt <= ldu && c1 >= c0 + cnt && c1 <= ld && ld <= ldu,
               "bad column ranges");
   if (c1 == ld) return LCQ_OK;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)k_gptq_trailing,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * GB * TT * 4);
+    attr = true;
+  }
   const dim3 grid((unsigned)((ld - c1 + TT - 1) / TT), (unsigned)((rows + TT - 1) / TT));
-  hipLaunchKernelGGL(k_gptq_trailing, grid, 256, 0, as_stream(stream),
+  hipLaunchKernelGGL(k_gptq_trailing, grid, 256, 2 * GB * TT * 4, as_stream(stream),
                      reinterpret_cast<float*>(W), rows, ld, c0, cnt, c1,
                      reinterpret_cast<const float*>(err), reinterpret_cast<const float*>(U),
                      ldu);

@@ -124,7 +124,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     ng = 0 if group is None else -(-cols // group)
     s_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng else None
     z_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng and not sym else None
-    err = torch.empty((rows, BLOCK), dtype=torch.float32, device=dev)
+    err = torch.empty((BLOCK, rows), dtype=torch.float32, device=dev)  # k-major Err1
     L = torch.zeros_like(W) if losses else None
     s_in = z_in = None
     if group is None:

@@ -164,6 +164,14 @@ class VllmRealQuantLinear(nn.Module):
     @classmethod
     @torch.no_grad()
     def quant_pack(cls, module, w_q, quant_config):
+        wq = getattr(w_q, 'keywords', {}).get('wquantizer')
+        if (module.weight.data.dtype == torch.float8_e4m3fn and wq is not None
+                and hasattr(wq, 'real_quant_weight_from_block_fp8')
+                and not quant_config['weight'].get('need_pack', False)):
+            # fp8 checkpoint -> per-tensor fp8 without materialising the bf16 weight
+            weight, scales, _ = wq.real_quant_weight_from_block_fp8(
+                module.weight.data, module.weight_scale_inv.data, module.block_size)
+            return weight, scales
         if module.weight.data.dtype == torch.float8_e4m3fn:  # module_utils.py:917-922
             from .kernel import weight_cast_to_bf16
             module.weight.data = weight_cast_to_bf16(

@@ -163,7 +163,8 @@ def hessian_accum(x: torch.Tensor, H: torch.Tensor, alpha: float, beta: float) -
 def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: int,
                qmin: int, qmax: int, sym: bool, s_out, z_out, err: torch.Tensor,
                losses=None, s_in=None, z_in=None):
-    """One 128-column GPTQ block in place on fp32 W (see include/lcq.h lcq_gptq_block)."""
+    """One 128-column GPTQ block in place on fp32 W (see include/lcq.h lcq_gptq_block);
+    err is k-major [128, rows]."""
     rows, ld = W.shape
     ng_total = s_out.shape[1] if s_out is not None else 0
     N.call('lcq_gptq_block', N.ptr(W), rows, ld, int(col0), int(count), N.ptr(U), U.shape[1],
@@ -173,7 +174,8 @@ def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: i
 
 def gptq_trailing(W: torch.Tensor, c0: int, cnt: int, c1: int, err: torch.Tensor,
                   U: torch.Tensor):
-    """W[:, c1:] -= err[:, :cnt] @ U[c0:c0+cnt, c1:] in place (fp32 MFMA, deterministic)."""
+    """W[:, c1:] -= err.T[:, :cnt] @ U[c0:c0+cnt, c1:] in place (err k-major [128, rows];
+    fp32 MFMA, deterministic k order)."""
     rows, ld = W.shape
     N.call('lcq_gptq_trailing', N.ptr(W), rows, ld, int(c0), int(cnt), int(c1), N.ptr(err),
            N.ptr(U), U.shape[1], N.stream_of(W))
@@ -396,6 +398,23 @@ def fp8_dequant_blocks(codes: torch.Tensor, scales: torch.Tensor, block: int = 1
     N.call('lcq_fp8_dequant_blocks', N.ptr(codes), N.dt(codes.dtype), M, Nn, block,
            N.ptr(scales), N.ptr(out), N.dt(out.dtype), N.stream_of(codes))
     return out
+
+
+def fp8_block_to_tensor(codes: torch.Tensor, scales_inv: torch.Tensor, block: int = 128,
+                        fp8: torch.dtype = torch.float8_e4m3fn, qmax: float | None = None):
+    """Block-fp8 weight -> bf16 (weight_cast_to_bf16) -> per-tensor fp8 real quant, fused.
+    Returns (codes [M, N] fp8, scale [1] fp32)."""
+    codes = codes.contiguous()
+    scales_inv = scales_inv.contiguous().float()
+    M, Nn = codes.shape
+    ws = torch.empty(1, dtype=torch.float32, device=codes.device)
+    out = torch.empty((M, Nn), dtype=fp8, device=codes.device)
+    s = torch.empty(1, dtype=torch.float32, device=codes.device)
+    qmax = fp8_max(fp8) if qmax is None else float(qmax)
+    N.call('lcq_fp8_block_to_tensor', N.ptr(codes), N.dt(codes.dtype), M, Nn, block,
+           N.ptr(scales_inv), N.dt(fp8), qmax, 1e-5, 1, N.ptr(ws), N.ptr(out), N.ptr(s),
+           N.stream_of(codes))
+    return out, s
 
 
 def fp_emul_quant(x: torch.Tensor, group: int, e_bits: int, m_bits: int,

@@ -536,6 +536,17 @@ class FloatQuantizer(BaseQuantizer):
             scales = scales * osf
         return codes, scales.view(self._qshape(codes, scales)), None
 
+    def real_quant_weight_from_block_fp8(self, codes, scale_inv, block_size):
+        """The deploy chain of a block-fp8 checkpoint weight: weight_cast_to_bf16 then
+        real_quant_weight_dynamic (module_utils.py:917-922). Per-tensor e4m3/e5m2 runs fused
+        (lcq_fp8_block_to_tensor, bit-identical, 3 B/element); other granularities compose."""
+        if self.granularity == 'per_tensor' and self.use_qtorch and self.fp8_dtype is not None:
+            c, s = ops.fp8_block_to_tensor(codes, scale_inv, block_size, self.fp8_dtype,
+                                           qmax=self._qmax_f())
+            return c, s, None
+        w = weight_cast_to_bf16(codes, scale_inv, block_size)
+        return self.real_quant_weight_dynamic(w)
+
     def real_quant_weight_static(self, weight, args):
         """quant.py:1161-1189."""
         assert self.bit in ['e4m3', 'e5m2'], 'Only FP8 E4M3 and E5M2 support real quant'

@@ -117,3 +117,23 @@ def test_per_tensor_expert_shape(dev):
     _, codes_ref, s_ref = O.fp8_qdq(w, 'e4m3', 'per_tensor')
     assert torch.equal(s.cpu(), s_ref)
     assert torch.equal(bits(codes), codes_ref.view(torch.uint8))
+
+
+@pytest.mark.parametrize('M,N', [(2048, 7168), (7168, 2048), (200, 264)])
+def test_block_fp8_to_tensor_fused_equals_composed(dev, M, N):
+    """The fused deploy of a block-fp8 weight equals weight_cast_to_bf16 + per-tensor real
+    quant bit for bit (and the oracle)."""
+    from lightcompress_amd import ops
+    from lightcompress_amd.quant import FloatQuantizer, weight_cast_to_bf16
+    g = torch.Generator().manual_seed(M + N)
+    w = (torch.randn(M, N, generator=g) * 0.02).to(torch.bfloat16)
+    r = ops.fp8_quant_blocks(w.to(dev), torch.float8_e4m3fn, 128, qmax=448.0, clamp_min=0.0,
+                             add_zero=False)
+    c, s = r['codes'], r['scales']
+    q = FloatQuantizer('e4m3', True, 'per_tensor', use_qtorch=True)
+    fc, fs, _ = q.real_quant_weight_from_block_fp8(c, s, 128)
+    wb = weight_cast_to_bf16(c, s, 128)
+    cc, cs, _ = q.real_quant_weight_dynamic(wb)
+    assert torch.equal(bits(fc), bits(cc)) and torch.equal(fs.cpu(), cs.cpu())
+    _, oc, os_ = O.fp8_qdq(O.weight_cast_to_bf16(c.cpu(), s.cpu()), 'e4m3', 'per_tensor')
+    assert torch.equal(bits(fc), oc.view(torch.uint8)) and torch.equal(fs.cpu(), os_)

@@ -61,13 +61,34 @@ def test_single_block_bit_exact(dev, group, sym):
     U = torch.linalg.cholesky(torch.cholesky_inverse(torch.linalg.cholesky(Hm)), upper=True)
     bit = 4
     qmin, qmax = (-8, 7) if sym else (0, 15)
-    tmp, _, s, z = G.column_loop(W.clone(), U, bit, sym, group)
+    tmp, L, s, z = G.column_loop(W.clone(), U, bit, sym, group)
     Wd = W.clone().to(dev)
-    s_d, z_d, _ = gptq_core.column_loop(Wd, U.to(dev), bit, sym, group, qmin, qmax)
+    s_d, z_d, L_d = gptq_core.column_loop(Wd, U.to(dev), bit, sym, group, qmin, qmax,
+                                          losses=True)
     assert torch.equal(Wd.cpu(), tmp)
     assert torch.equal(s_d.cpu(), s)
+    assert torch.equal(L_d.cpu(), L)
     if not sym:
         assert torch.equal(z_d.cpu(), z)
+
+
+@pytest.mark.parametrize('rows,cols', [(77, 128), (300, 100)])
+def test_single_block_fixed_qparams_bit_exact(dev, rows, cols):
+    """per_channel GPTQ (fixed per-row qparams, group None), incl. a ragged last block."""
+    from lightcompress_amd import gptq_core
+    g = torch.Generator().manual_seed(rows)
+    W = torch.randn(rows, cols, generator=g) * 0.02
+    A = torch.randn(cols, 2 * cols, generator=g)
+    Hm = A @ A.t() / cols + 0.1 * torch.eye(cols)
+    U = torch.linalg.cholesky(torch.cholesky_inverse(torch.linalg.cholesky(Hm)), upper=True)
+    mn, mx = W.amin(1, keepdim=True), W.amax(1, keepdim=True)
+    s, z = Q.qparams(mn, mx, 0.0, 15, False)
+    tmp, L, _, _ = G.column_loop(W.clone(), U, 4, False, None, fixed=(s, z))
+    Wd = W.clone().to(dev)
+    _, _, L_d = gptq_core.column_loop(Wd, U.to(dev), 4, False, None, 0, 15,
+                                      fixed=(s.to(dev), z.to(dev)), losses=True)
+    assert torch.equal(Wd.cpu(), tmp)
+    assert torch.equal(L_d.cpu(), L)
 
 
 @pytest.mark.parametrize('name', F.names('gptq_'))
@@ -135,11 +156,11 @@ def test_trailing_update(dev, rows, ic, c0):
     g = torch.Generator(device=dev).manual_seed(rows + ic)
     W = torch.randn(rows, ic, generator=g, device=dev)
     U = torch.randn(ic, ic, generator=g, device=dev).triu().contiguous()
-    err = torch.randn(rows, 128, generator=g, device=dev)
+    err = torch.randn(128, rows, generator=g, device=dev)  # k-major, as lcq_gptq_block writes
     cnt = min(128, ic - c0)
     c1 = c0 + cnt
     ref = W.double().clone()
-    ref[:, c1:] -= err[:, :cnt].double() @ U[c0:c1, c1:].double()
+    ref[:, c1:] -= err.t()[:, :cnt].double() @ U[c0:c1, c1:].double()
     out = W.clone()
     ops.gptq_trailing(out, c0, cnt, c1, err, U)
     assert torch.equal(out[:, :c1], W[:, :c1])
@@ -147,5 +168,5 @@ def test_trailing_update(dev, rows, ic, c0):
     assert ((out[:, c1:].double() - ref[:, c1:]).abs() <= tol).all()
     h = rows // 3
     part = W[h:].clone()
-    ops.gptq_trailing(part, c0, cnt, c1, err[h:].contiguous(), U)
+    ops.gptq_trailing(part, c0, cnt, c1, err[:, h:].contiguous(), U)
     assert torch.equal(part, out[h:])
