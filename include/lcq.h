@@ -237,6 +237,14 @@ int lcq_fp8_block_to_tensor(const void* codes, int fmt_in, int64_t M, int64_t N,
                             int add_zero, void* amax_ws, void* codes_out, void* scale_out,
                             void* stream);
 
+/* Batched lcq_fp8_block_to_tensor over n weights (e.g. the 257 x 3 expert linears of a
+ * DeepSeek-V3 MoE layer) in one launch pair. descs: device array of n records
+ * {const uint8_t* codes; const float* scales_inv; uint8_t* codes_out; int64_t M, N} (40 B);
+ * max_elems = the largest M*N; amax_ws: n device fp32; scales_out: n fp32. */
+int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t max_elems, int fmt_in,
+                                 int block, int fmt_out, float qmax, float clamp_min,
+                                 int add_zero, void* amax_ws, void* scales_out, void* stream);
+
 /* FloatQuantizer use_qtorch=False fake quant (get_float_qparams, quant.py:1005-1027, and
  * quant/dequant :1061-1076): per group of `group` elements, power-of-two per-element scales
  * for an e_bits/m_bits float format; every op rounds to the tensor dtype (fp32 when
@@ -259,6 +267,11 @@ int lcq_rotary(const void* q, const void* k, const void* cos, const void* sin, i
 /* out = rnd(rnd(g / (1 + exp(-g))) * u): act_fn(gate_proj(x)) * up_proj(x) with SiLU. */
 int lcq_silu_mul(const void* gate, const void* up, int dtype, int64_t n, void* out,
                  void* stream);
+
+/* LlamaRMSNorm.forward: out = weight * rnd(x_f32 * rsqrt(mean(x_f32^2) + eps)), one pass per
+ * row; x, out [rows, H] contiguous, weight [H] (same dtype). */
+int lcq_rmsnorm(const void* x, const void* weight, int dtype, int64_t rows, int64_t H,
+                float eps, void* out, void* stream);
 
 #ifdef __cplusplus
 }

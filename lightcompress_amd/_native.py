@@ -64,8 +64,11 @@ SIGNATURES = {
     'lcq_rotary': ([_vp, _vp, _vp, _vp, _int, _i64, _i64, _int, _int, _int, _i64, _vp, _vp, _vp],
                    _int),
     'lcq_silu_mul': ([_vp, _vp, _int, _i64, _vp, _vp], _int),
+    'lcq_rmsnorm': ([_vp, _vp, _int, _i64, _i64, _f32, _vp, _vp], _int),
     'lcq_fp8_block_to_tensor': ([_vp, _int, _i64, _i64, _int, _vp, _int, _f32, _f32, _int, _vp,
                                  _vp, _vp, _vp], _int),
+    'lcq_fp8_block_to_tensor_many': ([_int, _vp, _i64, _int, _int, _int, _f32, _f32, _int, _vp,
+                                      _vp, _vp], _int),
     'lcq_fp_emul_quant': ([_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int, _vp], _int),
 }
 

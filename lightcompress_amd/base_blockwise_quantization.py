@@ -312,10 +312,18 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         if self.batch_calib and (self._batch_ok is None or self._batch_ok[0] != key):
             self._batch_ok = (key, _batchable(input_data, kwargs))
         if self.batch_calib and self._batch_ok[1]:
-            y = self._call_block(block, torch.cat(list(input_data), dim=0), kwargs[0], stop_after)
+            cached = getattr(self, '_split_cache', None)
+            if cached is not None and len(cached[0]) == len(input_data) and all(
+                    a is b for a, b in zip(cached[0], input_data)):
+                xb = cached[1]  # the entries are the split views of this batch: no re-cat
+            else:
+                xb = torch.cat(list(input_data), dim=0)
+            y = self._call_block(block, xb, kwargs[0], stop_after)
             if y is None:
                 return None
-            return list(torch.split(y, [x.shape[0] for x in input_data], dim=0))
+            outs = list(torch.split(y, [x.shape[0] for x in input_data], dim=0))
+            self._split_cache = (outs, y)
+            return outs
         out = []
         for i, x in enumerate(input_data):
             out.append(self._call_block(block, x, kwargs[i], stop_after))
@@ -450,8 +458,36 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                    'fake_quant_wo_kv': EffcientFakeQuantLinear, **_REALQUANT_LINEAR_MAP_}
         if quant_format not in mapping:
             raise NotImplementedError(f"Quant format '{quant_format}' is not implemented.")
+        if quant_format in _REALQUANT_LINEAR_MAP_:
+            self._prequant_fp8_blocks()
         self.model.replace_module_all(mapping[quant_format],
                                       self.get_replacement_params(quant_format, self.w_only))
+
+    @torch.no_grad()
+    def _prequant_fp8_blocks(self):
+        """Block-fp8 checkpoint linears (DeepSeek-V3 experts) headed for a per-tensor FP8
+        real-quant format: requantize every such linear of a block in ONE batched launch
+        (lcq_fp8_block_to_tensor_many) instead of one dequant + quant chain per linear;
+        quant_pack picks the results up (bit-identical to the per-linear chain)."""
+        wq = self.wquantizer
+        if not (isinstance(wq, FloatQuantizer) and wq.granularity == 'per_tensor'
+                and wq.use_qtorch and wq.fp8_dtype is not None):
+            return
+        if self.quant_config['weight'].get('need_pack', False):
+            return
+        from . import ops
+        for block in self.blocks:
+            mods = [m for m in self.model.get_block_linears(block).values()
+                    if getattr(m, 'weight', None) is not None
+                    and m.weight.dtype == torch.float8_e4m3fn and hasattr(m, 'weight_scale_inv')]
+            if not mods:
+                continue
+            bs = getattr(mods[0], 'block_size', getattr(self, 'fp8_block_size', 128))
+            codes, scales = ops.fp8_block_to_tensor_many(
+                [m.weight.data for m in mods], [m.weight_scale_inv.data for m in mods], bs,
+                wq.fp8_dtype, qmax=wq._qmax_f())
+            for i, m in enumerate(mods):
+                m._lcq_prequant = (codes[i], scales[i:i + 1].view(1))
 
     @torch.no_grad()
     def save_model(self, path):

@@ -71,9 +71,58 @@ __global__ void __launch_bounds__(256) k_silu_mul(const void* __restrict__ g, co
   }
 }
 
+// RMSNorm (modeling_llama.LlamaRMSNorm.forward): v = mean(x_f32^2); y = x_f32 * rsqrt(v + eps)
+// rounded to the dtype; out = weight * y rounded. One workgroup per row, the row read once
+// (the torch chain makes 6 passes: cast, pow, mean, rsqrt-mul, cast, weight-mul). The sum of
+// squares uses a fixed per-lane + tree order (deterministic; not torch's reduction order, so
+// outputs can differ from the unfused chain by one rounding of the variance).
+template <int DT>
+__global__ void __launch_bounds__(256) k_rmsnorm(const void* __restrict__ x,
+                                                 const void* __restrict__ w, int64_t H,
+                                                 float eps, void* __restrict__ out) {
+  __shared__ float red[4];
+  const int64_t row = blockIdx.x;
+  const int64_t base = row * H;
+  float ss = 0.f;
+  for (int64_t c = threadIdx.x * 8; c < H; c += 256 * 8) {
+    float v[8];
+    ld8<DT>(x, base + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss = __fadd_rn(ss, __fmul_rn(v[j], v[j]));
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) ss = __fadd_rn(ss, __shfl_xor(ss, m, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float var = __fdiv_rn(__fadd_rn(__fadd_rn(red[0], red[1]), __fadd_rn(red[2], red[3])),
+                              (float)H);
+  const float r = rsqrtf(__fadd_rn(var, eps));
+  for (int64_t c = threadIdx.x * 8; c < H; c += 256 * 8) {
+    float v[8], g[8], o[8];
+    ld8<DT>(x, base + c, v);
+    ld8<DT>(w, c, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = rnd<DT>(g[j] * rnd<DT>(v[j] * r));
+    st8<DT>(out, base + c, o);
+  }
+}
+
 }  // namespace lcq
 
 using namespace lcq;
+
+extern "C" int lcq_rmsnorm(const void* x, const void* weight, int dtype, int64_t rows,
+                           int64_t H, float eps, void* out, void* stream) {
+  LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16, "dtype must be bf16 or fp16");
+  LCQ_REQUIRE(rows > 0 && rows <= 0x7fffffffLL && H > 0 && H % 8 == 0,
+              "H must be a positive multiple of 8");
+  hipStream_t st = as_stream(stream);
+  if (dtype == LCQ_BF16)
+    hipLaunchKernelGGL(k_rmsnorm<LCQ_BF16>, dim3((unsigned)rows), 256, 0, st, x, weight, H, eps, out);
+  else
+    hipLaunchKernelGGL(k_rmsnorm<LCQ_F16>, dim3((unsigned)rows), 256, 0, st, x, weight, H, eps, out);
+  return check_launch("lcq_rmsnorm");
+}
 
 extern "C" int lcq_rotary(const void* q, const void* k, const void* cos, const void* sin,
                           int dtype, int64_t B, int64_t S, int Hq, int Hk, int D,

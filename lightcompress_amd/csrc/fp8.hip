@@ -316,11 +316,8 @@ __global__ void __launch_bounds__(256) k_fp8_blocks(Fp8Args a, int64_t M, int64_
 // dequantize again and quantize: 1 + 1 B read, 1 B written per element (the composed chain
 // moves 8 B per element).
 template <int FIN>
-__device__ __forceinline__ void deq8_bf16(const uint8_t* codes, const float* s, int64_t N,
-                                          int bs, int64_t nb, int64_t e0, float (&w)[8]) {
-  const int64_t r = e0 / N, c = e0 % N;
-  const float sc = s[(r / bs) * nb + c / bs];
-  const uint2 u = *reinterpret_cast<const uint2*>(codes + e0);
+__device__ __forceinline__ void deq8_row(const uint8_t* crow, float sc, int c, float (&w)[8]) {
+  const uint2 u = *reinterpret_cast<const uint2*>(crow + c);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     w[j] = bf16_rne(dec<FIN>((u.x >> (8 * j)) & 0xffu) * sc);
@@ -328,20 +325,31 @@ __device__ __forceinline__ void deq8_bf16(const uint8_t* codes, const float* s, 
   }
 }
 
+// Row-walking traversal shared by the block-fp8 kernels: workgroup b takes rows b, b+G, ...;
+// its 256 threads stride the row in 8-element chunks. Index math is 32-bit and per row (no
+// per-element 64-bit division).
+#define LCQ_ROWS_BEGIN(M, N, bs, ROWVAR)                                               \
+  for (int64_t ROWVAR = blockIdx.x; ROWVAR < (M); ROWVAR += gridDim.x) {               \
+    const int nb_ = (int)(((N) + (bs)-1) / (bs));                                      \
+    const int rb_ = (int)(ROWVAR / (bs));                                              \
+    for (int c = threadIdx.x * 8; c < (int)(N); c += 256 * 8) {                        \
+      const int cbk_ = c / (bs);
+#define LCQ_ROWS_END \
+  }                  \
+  }
+
 template <int FIN>
 __global__ void __launch_bounds__(256) k_absmax_blockfp8(const uint8_t* codes, const float* s,
                                                          int64_t M, int64_t N, int bs,
                                                          uint32_t* out) {
   __shared__ float red[4];
-  const int64_t n8 = M * N / 8, nb = (N + bs - 1) / bs;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   float am = 0.f;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
+  LCQ_ROWS_BEGIN(M, N, bs, r)
     float w[8];
-    deq8_bf16<FIN>(codes, s, N, bs, nb, t * 8, w);
+    deq8_row<FIN>(codes + r * N, s[rb_ * nb_ + cbk_], c, w);
 #pragma unroll
     for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(w[j]));
-  }
+  LCQ_ROWS_END
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) am = fmaxf(am, __shfl_xor(am, m, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
@@ -357,16 +365,59 @@ __global__ void __launch_bounds__(256) k_requant_blockfp8(const uint8_t* codes, 
                                                           float clamp_min, int add_zero,
                                                           uint8_t* out, float* s_out) {
   const float sc = fp8_scale<LCQ_BF16, LCQ_F32>(*amax, qmax, clamp_min, add_zero);
-  const int64_t n8 = M * N / 8, nb = (N + bs - 1) / bs;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
+  LCQ_ROWS_BEGIN(M, N, bs, r)
     float w[8], dq[8];
-    uint32_t c[8];
-    deq8_bf16<FIN>(codes, s, N, bs, nb, t * 8, w);
-    fp8_qdq8<LCQ_BF16, FOUT>(w, sc, add_zero, c, dq);
-    st_codes8(out, t * 8, c);
-  }
+    uint32_t cc[8];
+    deq8_row<FIN>(codes + r * N, s[rb_ * nb_ + cbk_], c, w);
+    fp8_qdq8<LCQ_BF16, FOUT>(w, sc, add_zero, cc, dq);
+    st_codes8(out, r * N + c, cc);
+  LCQ_ROWS_END
   if (blockIdx.x == 0 && threadIdx.x == 0 && s_out) *s_out = sc;
+}
+
+// ---- batched form: blockIdx.y = tensor; descriptors in device memory ------------------
+struct Fp8Desc {
+  const uint8_t* codes;
+  const float* s_inv;
+  uint8_t* out;
+  int64_t M, N;
+};
+
+template <int FIN>
+__global__ void __launch_bounds__(256) k_absmax_blockfp8_many(const Fp8Desc* d, int bs,
+                                                              uint32_t* amax) {
+  __shared__ float red[4];
+  const Fp8Desc t = d[blockIdx.y];
+  float am = 0.f;
+  LCQ_ROWS_BEGIN(t.M, t.N, bs, r)
+    float w[8];
+    deq8_row<FIN>(t.codes + r * t.N, t.s_inv[rb_ * nb_ + cbk_], c, w);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(w[j]));
+  LCQ_ROWS_END
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) am = fmaxf(am, __shfl_xor(am, m, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(amax + blockIdx.y, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+template <int FIN, int FOUT>
+__global__ void __launch_bounds__(256) k_requant_blockfp8_many(const Fp8Desc* d, int bs,
+                                                               const float* amax, float qmax,
+                                                               float clamp_min, int add_zero,
+                                                               float* s_out) {
+  const Fp8Desc t = d[blockIdx.y];
+  const float sc = fp8_scale<LCQ_BF16, LCQ_F32>(amax[blockIdx.y], qmax, clamp_min, add_zero);
+  LCQ_ROWS_BEGIN(t.M, t.N, bs, r)
+    float w[8], dq[8];
+    uint32_t cc[8];
+    deq8_row<FIN>(t.codes + r * t.N, t.s_inv[rb_ * nb_ + cbk_], c, w);
+    fp8_qdq8<LCQ_BF16, FOUT>(w, sc, add_zero, cc, dq);
+    st_codes8(t.out, r * t.N + c, cc);
+  LCQ_ROWS_END
+  if (blockIdx.x == 0 && threadIdx.x == 0) s_out[blockIdx.y] = sc;
 }
 
 // ---- block dequant: out = rnd_out(float(code) * s[block])  (weight_cast_to_bf16) --------
@@ -374,22 +425,17 @@ template <int FMT, int OT>
 __global__ void __launch_bounds__(256) k_fp8_dequant_blocks(const uint8_t* codes,
                                                             const float* s, int64_t M,
                                                             int64_t N, int bs, void* out) {
-  const int64_t n8 = M * N / 8;
-  const int64_t nb = (N + bs - 1) / bs;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
-    const int64_t e0 = t * 8;
-    const int64_t r = e0 / N, c = e0 % N;
-    const float sc = s[(r / bs) * nb + c / bs];
-    const uint2 u = *reinterpret_cast<const uint2*>(codes + e0);
+  LCQ_ROWS_BEGIN(M, N, bs, r)
+    const float sc = s[rb_ * nb_ + cbk_];
+    const uint2 u = *reinterpret_cast<const uint2*>(codes + r * N + c);
     float v[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       v[j] = dec<FMT>((u.x >> (8 * j)) & 0xffu) * sc;
       v[4 + j] = dec<FMT>((u.y >> (8 * j)) & 0xffu) * sc;
     }
-    st8<OT>(out, e0, v);
-  }
+    st8<OT>(out, r * N + c, v);
+  LCQ_ROWS_END
 }
 
 // ---- use_qtorch=False: get_float_qparams emulation (quant.py:1005-1027, 1061-1076) ------
@@ -632,8 +678,9 @@ extern "C" int lcq_fp8_dequant_blocks(const void* codes, int fmt, int64_t M, int
                                       void* stream) {
   LCQ_REQUIRE(fmt == LCQ_FP8E4M3 || fmt == LCQ_FP8E5M2, "fmt must be e4m3fn or e5m2");
   LCQ_REQUIRE(block > 0 && M > 0 && N > 0 && N % 8 == 0, "N must be a positive multiple of 8");
+  LCQ_REQUIRE(N < 0x7fffffffLL, "rows longer than 2^31 elements");
   LCQ_REQUIRE(is_float_dt(out_dtype), "out dtype must be f32/f16/bf16");
-  const unsigned grid = stream_grid(M * N / 8, 256);
+  const unsigned grid = (unsigned)std::min<int64_t>(M, 65535);
   hipStream_t st = as_stream(stream);
   const uint8_t* c = reinterpret_cast<const uint8_t*>(codes);
   const float* s = reinterpret_cast<const float*>(scales);
@@ -670,7 +717,7 @@ extern "C" int lcq_fp8_block_to_tensor(const void* codes, int fmt_in, int64_t M,
     return fail(LCQ_ELAUNCH, "lcq_fp8_block_to_tensor: memset failed");
   const uint8_t* c = reinterpret_cast<const uint8_t*>(codes);
   const float* s = reinterpret_cast<const float*>(scales_inv);
-  const unsigned g1 = std::min<unsigned>(stream_grid(M * N / 8, 256), 2048u);
+  const unsigned g1 = (unsigned)std::min<int64_t>(M, 2048);
   if (fmt_in == LCQ_FP8E4M3)
     hipLaunchKernelGGL(k_absmax_blockfp8<LCQ_FP8E4M3>, g1, 256, 0, st, c, s, M, N, block,
                        reinterpret_cast<uint32_t*>(amax_ws));
@@ -679,7 +726,7 @@ extern "C" int lcq_fp8_block_to_tensor(const void* codes, int fmt_in, int64_t M,
                        reinterpret_cast<uint32_t*>(amax_ws));
   int rc = check_launch("lcq_fp8_block_to_tensor: amax");
   if (rc) return rc;
-  const unsigned g2 = stream_grid(M * N / 8, 256);
+  const unsigned g2 = (unsigned)std::min<int64_t>(M, 65535);
   const float* am = reinterpret_cast<const float*>(amax_ws);
   uint8_t* o = reinterpret_cast<uint8_t*>(codes_out);
   float* so = reinterpret_cast<float*>(scale_out);
@@ -693,6 +740,42 @@ extern "C" int lcq_fp8_block_to_tensor(const void* codes, int fmt_in, int64_t M,
   }
 #undef LCQ_RQ
   return check_launch("lcq_fp8_block_to_tensor: requant");
+}
+
+extern "C" int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t max_elems,
+                                            int fmt_in, int block, int fmt_out, float qmax,
+                                            float clamp_min, int add_zero, void* amax_ws,
+                                            void* scales_out, void* stream) {
+  LCQ_REQUIRE(n > 0 && n <= 65535 && descs && amax_ws && scales_out, "bad batch");
+  LCQ_REQUIRE(fmt_in == LCQ_FP8E4M3 || fmt_in == LCQ_FP8E5M2, "bad input format");
+  LCQ_REQUIRE(fmt_out == LCQ_FP8E4M3 || fmt_out == LCQ_FP8E5M2, "bad output format");
+  LCQ_REQUIRE(block > 0 && max_elems > 0 && qmax > 0.f, "bad block / sizes");
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(amax_ws, 0, sizeof(float) * n, st) != hipSuccess)
+    return fail(LCQ_ELAUNCH, "lcq_fp8_block_to_tensor_many: memset failed");
+  const Fp8Desc* d = reinterpret_cast<const Fp8Desc*>(descs);
+  // row-walking workgroups per tensor (blockIdx.y = tensor)
+  unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(max_elems / 65536, 256));
+  const dim3 grid(gx, (unsigned)n);
+  uint32_t* am = reinterpret_cast<uint32_t*>(amax_ws);
+  if (fmt_in == LCQ_FP8E4M3)
+    hipLaunchKernelGGL(k_absmax_blockfp8_many<LCQ_FP8E4M3>, grid, 256, 0, st, d, block, am);
+  else
+    hipLaunchKernelGGL(k_absmax_blockfp8_many<LCQ_FP8E5M2>, grid, 256, 0, st, d, block, am);
+  int rc = check_launch("lcq_fp8_block_to_tensor_many: amax");
+  if (rc) return rc;
+  const float* amf = reinterpret_cast<const float*>(amax_ws);
+  float* so = reinterpret_cast<float*>(scales_out);
+#define LCQ_RQM(FI, FO) \
+  hipLaunchKernelGGL((k_requant_blockfp8_many<FI, FO>), grid, 256, 0, st, d, block, amf, qmax, \
+                     clamp_min, add_zero, so)
+  if (fmt_in == LCQ_FP8E4M3) {
+    if (fmt_out == LCQ_FP8E4M3) LCQ_RQM(LCQ_FP8E4M3, LCQ_FP8E4M3); else LCQ_RQM(LCQ_FP8E4M3, LCQ_FP8E5M2);
+  } else {
+    if (fmt_out == LCQ_FP8E4M3) LCQ_RQM(LCQ_FP8E5M2, LCQ_FP8E4M3); else LCQ_RQM(LCQ_FP8E5M2, LCQ_FP8E5M2);
+  }
+#undef LCQ_RQM
+  return check_launch("lcq_fp8_block_to_tensor_many: requant");
 }
 
 extern "C" int lcq_fp_emul_quant(const void* x, int x_dtype, int64_t rows, int64_t cols,

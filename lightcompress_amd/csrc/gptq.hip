@@ -222,30 +222,26 @@ extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, i
 // element's value is independent of the tiling / row range (row-sharded GPTQ on N GPUs is
 // bit-identical to one GPU). The product is rounded to fp32 and then subtracted, like the
 // reference's `W -= Err @ Hinv` (two roundings). 128x128 output tile per 256-thread
-// workgroup (2x2 waves of 64x64 = 2x2 MFMA 32x32 tiles); the whole K = 128 of both operands
-// is staged once in LDS (err arrives k-major [128][rows] from lcq_gptq_block, U rows are
-// k-major already), with conflict-free 16-byte copies and conflict-free operand reads.
+// workgroup (2x2 waves of 64x64 = 2x2 MFMA 32x32 tiles); K in 32-deep chunks, double-
+// buffered through 64 KB of LDS with register staging (the next chunk's loads overlap the
+// current chunk's MFMAs; 2 workgroups per CU). err arrives k-major [128][rows] from
+// lcq_gptq_block and U rows are k-major, so both stage with conflict-free 16-byte copies.
 // ---------------------------------------------------------------------------------------
 namespace lcq {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr int TT = 128;   // output tile
 
-__global__ void __launch_bounds__(256, 1)
-    k_gptq_trailing(float* __restrict__ W, int64_t rows, int64_t ld, int64_t c0, int cnt,
-                    int64_t c1, const float* __restrict__ ET, const float* __restrict__ U,
-                    int64_t ldu) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* As = sm;              // As[k][row]  (128 x 128)
-  float* Bs = sm + GB * TT;    // Bs[k][col]  (128 x 128)
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const int64_t r0 = (int64_t)blockIdx.y * TT;
-  const int64_t j0 = c1 + (int64_t)blockIdx.x * TT;
-#pragma unroll 4
-  for (int it = 0; it < (GB * TT / 4) / 256; ++it) {
-    const int idx = it * 256 + tid;
-    const int k = idx / (TT / 4), c4 = (idx % (TT / 4)) * 4;
+constexpr int KC = 32;     // K chunk (double-buffered through LDS)
+
+__device__ __forceinline__ void trail_load(const float* __restrict__ ET, const float* __restrict__ U,
+                                           int64_t rows, int64_t ld, int64_t ldu, int64_t c0,
+                                           int cnt, int64_t r0, int64_t j0, int k0, int tid,
+                                           float4 (&ra)[4], float4 (&rb)[4]) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = it * 256 + tid;           // 0..1023 float4 of a 32 x 128 chunk
+    const int k = k0 + idx / (TT / 4), c4 = (idx % (TT / 4)) * 4;
     float4 ea = make_float4(0.f, 0.f, 0.f, 0.f), ub = ea;
     if (k < cnt) {
       const float* es = ET + (int64_t)k * rows + r0 + c4;
@@ -266,10 +262,21 @@ __global__ void __launch_bounds__(256, 1)
         if (j0 + c4 + 2 < ld) ub.z = us[2];
       }
     }
-    *reinterpret_cast<float4*>(&As[k * TT + c4]) = ea;
-    *reinterpret_cast<float4*>(&Bs[k * TT + c4]) = ub;
+    ra[it] = ea;
+    rb[it] = ub;
   }
-  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256, 2)
+    k_gptq_trailing(float* __restrict__ W, int64_t rows, int64_t ld, int64_t c0, int cnt,
+                    int64_t c1, const float* __restrict__ ET, const float* __restrict__ U,
+                    int64_t ldu) {
+  __shared__ __attribute__((aligned(16))) float As[2][KC * TT];  // [k][row]
+  __shared__ __attribute__((aligned(16))) float Bs[2][KC * TT];  // [k][col]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t r0 = (int64_t)blockIdx.y * TT;
+  const int64_t j0 = c1 + (int64_t)blockIdx.x * TT;
   v16f acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -277,20 +284,43 @@ __global__ void __launch_bounds__(256, 1)
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
-#pragma unroll 8
-  for (int kk = 0; kk < GB; kk += 2) {
-    const int k = kk + (lane >> 5);
-    float av[2], bv[2];
+  float4 ra[4], rb[4];
+  trail_load(ET, U, rows, ld, ldu, c0, cnt, r0, j0, 0, tid, ra, rb);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      av[t] = As[k * TT + wr * 64 + t * 32 + (lane & 31)];
-      bv[t] = Bs[k * TT + wc * 64 + t * 32 + (lane & 31)];
+  for (int it = 0; it < 4; ++it) {
+    const int idx = it * 256 + tid;
+    *reinterpret_cast<float4*>(&As[0][idx * 4]) = ra[it];
+    *reinterpret_cast<float4*>(&Bs[0][idx * 4]) = rb[it];
+  }
+  __syncthreads();
+  const int nch = (cnt + KC - 1) / KC;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int cur = ch & 1;
+    if (ch + 1 < nch) trail_load(ET, U, rows, ld, ldu, c0, cnt, r0, j0, (ch + 1) * KC, tid, ra, rb);
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 2) {
+      const int k = kk + (lane >> 5);
+      float av[2], bv[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        av[t] = As[cur][k * TT + wr * 64 + t * 32 + (lane & 31)];
+        bv[t] = Bs[cur][k * TT + wc * 64 + t * 32 + (lane & 31)];
+      }
+#pragma unroll
+      for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+        for (int tb = 0; tb < 2; ++tb)
+          acc[ta][tb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ta], bv[tb], acc[ta][tb], 0, 0, 0);
     }
+    if (ch + 1 < nch) {
 #pragma unroll
-    for (int ta = 0; ta < 2; ++ta)
-#pragma unroll
-      for (int tb = 0; tb < 2; ++tb)
-        acc[ta][tb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ta], bv[tb], acc[ta][tb], 0, 0, 0);
+      for (int it = 0; it < 4; ++it) {
+        const int idx = it * 256 + tid;
+        *reinterpret_cast<float4*>(&As[cur ^ 1][idx * 4]) = ra[it];
+        *reinterpret_cast<float4*>(&Bs[cur ^ 1][idx * 4]) = rb[it];
+      }
+    }
+    __syncthreads();
   }
   // epilogue (C layout: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5))
 #pragma unroll
@@ -314,14 +344,8 @@ extern "C" int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, 
   LCQ_REQUIRE(c0 >= 0 && c0 + cnt <= ldu && c1 >= c0 + cnt && c1 <= ld && ld <= ldu,
               "bad column ranges");
   if (c1 == ld) return LCQ_OK;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)k_gptq_trailing,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * GB * TT * 4);
-    attr = true;
-  }
   const dim3 grid((unsigned)((ld - c1 + TT - 1) / TT), (unsigned)((rows + TT - 1) / TT));
-  hipLaunchKernelGGL(k_gptq_trailing, grid, 256, 2 * GB * TT * 4, as_stream(stream),
+  hipLaunchKernelGGL(k_gptq_trailing, grid, 256, 0, as_stream(stream),
                      reinterpret_cast<float*>(W), rows, ld, c0, cnt, c1,
                      reinterpret_cast<const float*>(err), reinterpret_cast<const float*>(U),
                      ldu);

@@ -49,6 +49,20 @@ def _fused_mlp_forward(self, x):
     return self.down_proj(h)
 
 
+def _fused_rmsnorm_forward(self, hidden_states):
+    """LlamaRMSNorm.forward on one lcq_rmsnorm pass (same formula; the variance is summed in
+    a fixed order of its own)."""
+    from . import ops
+    if (hidden_states.is_cuda and hidden_states.dtype in (torch.bfloat16, torch.float16)
+            and self.weight.dtype == hidden_states.dtype and hidden_states.shape[-1] % 8 == 0):
+        return ops.rmsnorm(hidden_states, self.weight, self.variance_epsilon)
+    input_dtype = hidden_states.dtype
+    h = hidden_states.to(torch.float32)
+    variance = h.pow(2).mean(-1, keepdim=True)
+    h = h * torch.rsqrt(variance + self.variance_epsilon)
+    return self.weight * h.to(input_dtype)
+
+
 def install_fused_forward(model: nn.Module):
     """Route the Llama calibration forward's elementwise chains through the lcq fusions
     (env LCQ_FUSED_FORWARD=0 disables)."""
@@ -62,6 +76,8 @@ def install_fused_forward(model: nn.Module):
     for m in model.modules():
         if isinstance(m, ml.LlamaMLP) and getattr(m.config, 'hidden_act', None) == 'silu':
             m.forward = types.MethodType(_fused_mlp_forward, m)
+        elif isinstance(m, ml.LlamaRMSNorm):
+            m.forward = types.MethodType(_fused_rmsnorm_forward, m)
 
 
 class _Blocks(nn.Module):

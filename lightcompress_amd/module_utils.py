@@ -164,6 +164,10 @@ class VllmRealQuantLinear(nn.Module):
     @classmethod
     @torch.no_grad()
     def quant_pack(cls, module, w_q, quant_config):
+        pre = getattr(module, '_lcq_prequant', None)
+        if pre is not None:  # batched by BaseBlockwiseQuantization._prequant_fp8_blocks
+            del module._lcq_prequant
+            return pre
         wq = getattr(w_q, 'keywords', {}).get('wquantizer')
         if (module.weight.data.dtype == torch.float8_e4m3fn and wq is not None
                 and hasattr(wq, 'real_quant_weight_from_block_fp8')

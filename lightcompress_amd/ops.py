@@ -417,6 +417,33 @@ def fp8_block_to_tensor(codes: torch.Tensor, scales_inv: torch.Tensor, block: in
     return out, s
 
 
+def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
+                             fp8: torch.dtype = torch.float8_e4m3fn, qmax: float | None = None):
+    """Batched fp8_block_to_tensor: one launch pair for a list of block-fp8 weights (all on
+    one device). Returns (list of fp8 codes, fp32 scales [n])."""
+    n = len(codes)
+    if n == 0:
+        return [], torch.empty(0)
+    dev = codes[0].device
+    codes = [c.contiguous() for c in codes]
+    sinv = [s.contiguous().float() for s in scales_inv]
+    outs = [torch.empty(c.shape, dtype=fp8, device=dev) for c in codes]
+    rec = []
+    for c, s, o in zip(codes, sinv, outs):
+        M, Nn = c.shape
+        if Nn % 8:
+            raise ValueError('N must be a multiple of 8')
+        rec += [N.ptr(c), N.ptr(s), N.ptr(o), M, Nn]
+    descs = torch.tensor(rec, dtype=torch.int64).to(dev, non_blocking=False)
+    ws = torch.empty(n, dtype=torch.float32, device=dev)
+    sc = torch.empty(n, dtype=torch.float32, device=dev)
+    qmax = fp8_max(fp8) if qmax is None else float(qmax)
+    N.call('lcq_fp8_block_to_tensor_many', n, N.ptr(descs), max(c.numel() for c in codes),
+           N.dt(codes[0].dtype), block, N.dt(fp8), qmax, 1e-5, 1, N.ptr(ws), N.ptr(sc),
+           N.stream_of(codes[0]))
+    return outs, sc
+
+
 def fp_emul_quant(x: torch.Tensor, group: int, e_bits: int, m_bits: int,
                   out: torch.Tensor | None = None) -> torch.Tensor:
     """FloatQuantizer use_qtorch=False fake quant over groups of ``group`` columns."""
@@ -463,3 +490,17 @@ def silu_mul(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
     N.call('lcq_silu_mul', N.ptr(gate), N.ptr(up), N.dt(gate.dtype), gate.numel(), N.ptr(out),
            N.stream_of(gate))
     return out
+
+
+def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
+    """LlamaRMSNorm.forward in one pass per row (x [..., H], weight [H], same dtype)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    w = weight.contiguous()
+    if w.dtype != x.dtype or w.numel() != x2.shape[1]:
+        raise ValueError('weight must match x dtype and hidden size')
+    out = torch.empty_like(x2)
+    N.call('lcq_rmsnorm', N.ptr(x2), N.ptr(w), N.dt(x.dtype), x2.shape[0], x2.shape[1],
+           float(eps), N.ptr(out), N.stream_of(x2))
+    return out.view(x.shape)

@@ -547,6 +547,16 @@ class FloatQuantizer(BaseQuantizer):
         w = weight_cast_to_bf16(codes, scale_inv, block_size)
         return self.real_quant_weight_dynamic(w)
 
+    def real_quant_weights_from_block_fp8(self, codes, scales_inv, block_size):
+        """Batched real_quant_weight_from_block_fp8 over lists (per-tensor e4m3/e5m2: one
+        launch pair for all of them). Returns a list of (codes, scale[1], None)."""
+        if self.granularity == 'per_tensor' and self.use_qtorch and self.fp8_dtype is not None:
+            cs, ss = ops.fp8_block_to_tensor_many(codes, scales_inv, block_size, self.fp8_dtype,
+                                                  qmax=self._qmax_f())
+            return [(c, ss[i:i + 1], None) for i, c in enumerate(cs)]
+        return [self.real_quant_weight_from_block_fp8(c, s, block_size)
+                for c, s in zip(codes, scales_inv)]
+
     def real_quant_weight_static(self, weight, args):
         """quant.py:1161-1189."""
         assert self.bit in ['e4m3', 'e5m2'], 'Only FP8 E4M3 and E5M2 support real quant'

@@ -13,7 +13,9 @@ KEYS = {'hipblaslt_gemm': 'Cijk_', 'k_syrk256': 'k_syrk256', 'k_auto_clip': 'k_a
         'attn_fwd': 'attn_fwd', 'k_silu_mul': 'k_silu_mul', 'k_scale_bcast': 'k_scale_bcast',
         'k_quant_dyn_lanes': 'k_quant_dyn_lanes', 'k_rotary': 'k_rotary',
         'k_sqdiff_p1': 'k_sqdiff_p1', 'k_gptq_block': 'k_gptq_block',
-        'k_gptq_trailing': 'k_gptq_trailing', 'k_xt_pack': 'k_xt_pack'}
+        'k_gptq_trailing': 'k_gptq_trailing', 'k_xt_pack': 'k_xt_pack',
+        'k_requant_blockfp8_many': 'k_requant_blockfp8_many',
+        'k_absmax_blockfp8_many': 'k_absmax_blockfp8_many'}
 
 
 def load(path):

@@ -56,12 +56,34 @@ def test_block_forward_unchanged(dev):
     fused = fused[0] if isinstance(fused, tuple) else fused
     saved = ml.apply_rotary_pos_emb
     ml.apply_rotary_pos_emb = L._ORIG_ROTARY
-    mlp_fwd = blk.mlp.forward
-    del blk.mlp.forward  # back to the class method
+    patched = [m for m in blk.modules() if 'forward' in m.__dict__]
+    fwds = [m.__dict__['forward'] for m in patched]
+    for m in patched:
+        del m.forward  # back to the class methods
     try:
         ref = blk(x, **kw)
         ref = ref[0] if isinstance(ref, tuple) else ref
     finally:
         ml.apply_rotary_pos_emb = saved
-        blk.mlp.forward = mlp_fwd
-    assert torch.equal(fused, ref)
+        for m, f in zip(patched, fwds):
+            m.forward = f
+    # rotary and silu*up are bit-identical; RMSNorm's variance order may move a rounding
+    torch.testing.assert_close(fused.float(), ref.float(), rtol=2e-2, atol=2e-2)
+    assert (fused != ref).float().mean().item() < 0.02
+
+
+@pytest.mark.parametrize('rows,H,dt', [(300, 4096, torch.bfloat16), (17, 256, torch.float16)])
+def test_rmsnorm_close_to_torch(dev, rows, H, dt):
+    """One-pass RMSNorm vs the HF chain: identical except where the variance's summation
+    order moves a bf16 rounding (<= 1 ulp, on a tiny fraction of elements)."""
+    from lightcompress_amd import ops
+    g = torch.Generator(device=dev).manual_seed(rows)
+    x = (torch.randn(rows, H, generator=g, device=dev) * 3).to(dt)
+    w = (torch.rand(H, generator=g, device=dev) + 0.5).to(dt)
+    h = x.float()
+    ref = w * (h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + 1e-5)).to(dt)
+    out = ops.rmsnorm(x, w, 1e-5)
+    diff = (out.float() - ref.float()).abs()
+    ulp = ref.float().abs() * (2 ** -7 if dt == torch.bfloat16 else 2 ** -10)
+    assert (diff <= ulp + 1e-30).all()
+    assert (diff > 0).float().mean().item() < 0.01

@@ -137,3 +137,20 @@ def test_block_fp8_to_tensor_fused_equals_composed(dev, M, N):
     assert torch.equal(bits(fc), bits(cc)) and torch.equal(fs.cpu(), cs.cpu())
     _, oc, os_ = O.fp8_qdq(O.weight_cast_to_bf16(c.cpu(), s.cpu()), 'e4m3', 'per_tensor')
     assert torch.equal(bits(fc), oc.view(torch.uint8)) and torch.equal(fs.cpu(), os_)
+
+
+def test_block_fp8_to_tensor_batched_equals_single(dev):
+    """One launch pair over a list of expert weights == the per-weight fused path."""
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(5)
+    cs, ss = [], []
+    for (m, n) in [(256, 512), (512, 256), (200, 264), (128, 128)]:
+        w = (torch.randn(m, n, generator=g) * 0.03).to(torch.bfloat16).to(dev)
+        r = ops.fp8_quant_blocks(w, torch.float8_e4m3fn, 128, qmax=448.0, clamp_min=0.0,
+                                 add_zero=False)
+        cs.append(r['codes'])
+        ss.append(r['scales'])
+    outs, scales = ops.fp8_block_to_tensor_many(cs, ss, 128)
+    for i, (c, s) in enumerate(zip(cs, ss)):
+        oc, os_ = ops.fp8_block_to_tensor(c, s, 128)
+        assert torch.equal(bits(outs[i]), bits(oc)) and scales[i].item() == os_.item()
