@@ -338,6 +338,8 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         self.block_init(block)
         self.run(block, input_feat, handles)
         del input_feat
+        if hasattr(self.model, 'clear_block_cache'):
+            self.model.clear_block_cache(block)
 
     def register_hooks(self, modules, input_feat):
         if self.data_free:

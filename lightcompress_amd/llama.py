@@ -63,6 +63,103 @@ def _fused_rmsnorm_forward(self, hidden_states):
     return self.weight * h.to(input_dtype)
 
 
+def _mkey(*mods):
+    """Identity + weight storage/version of the modules a cached stage depends on (an in-place
+    weight update bumps _version, a replaced module or re-pointed .data changes the rest)."""
+    out = []
+    for m in mods:
+        w = getattr(m, 'weight', None)
+        out.append((id(m), type(m).__name__, None if w is None else
+                    (w.data_ptr(), w._version, tuple(w.shape), w.dtype)))
+    return tuple(out)
+
+
+def _hooked(*mods):
+    return any(m._forward_hooks or m._forward_pre_hooks for m in mods)
+
+
+def _stage(cache, name, key, mods, fn):
+    hit = cache.get(name)
+    if hit is not None and hit[0] == key and not _hooked(*mods):
+        return hit[1]
+    val = fn()
+    cache[name] = (key, val)
+    return val
+
+
+def _attn_core(attn, xn, position_embeddings, attention_mask, **kwargs):
+    """LlamaAttention.forward up to (not including) o_proj, exactly as transformers runs it."""
+    from transformers.models.llama import modeling_llama as ml
+    input_shape = xn.shape[:-1]
+    hidden_shape = (*input_shape, -1, attn.head_dim)
+    q = attn.q_proj(xn).view(hidden_shape).transpose(1, 2)
+    k = attn.k_proj(xn).view(hidden_shape).transpose(1, 2)
+    v = attn.v_proj(xn).view(hidden_shape).transpose(1, 2)
+    cos, sin = position_embeddings
+    q, k = ml.apply_rotary_pos_emb(q, k, cos, sin)
+    iface = ml.ALL_ATTENTION_FUNCTIONS.get_interface(attn.config._attn_implementation,
+                                                      ml.eager_attention_forward)
+    out, _ = iface(attn, q, k, v, attention_mask,
+                   dropout=0.0 if not attn.training else attn.attention_dropout,
+                   scaling=attn.scaling, **kwargs)
+    return out.reshape(*input_shape, -1).contiguous()
+
+
+_STOCK_DECODER_FORWARD = None
+
+
+def _staged_decoder_forward(self, hidden_states, attention_mask=None, position_ids=None,
+                            past_key_values=None, use_cache=False, position_embeddings=None,
+                            **kwargs):
+    """LlamaDecoderLayer.forward as four memoised stages: [norm1, q/k/v, attention],
+    [o_proj + residual], [norm2, gate/up, SiLU product], [down + residual].
+
+    GPTQ's true_sequential re-forwards and its quant_out forward re-run a block on the same
+    input with one subset replaced each time (o_proj, then gate/up, then down): the stages
+    before the replaced modules are identical and come from the memo. A stage is recomputed
+    when its input, a module object or a weight (storage or in-place version) changed, and
+    always when one of its modules carries hooks (so input captures keep firing)."""
+    attn, mlp = self.self_attn, self.mlp
+    if (past_key_values is not None or not hidden_states.is_cuda
+            or _hooked(self, attn, mlp)):
+        return _STOCK_DECODER_FORWARD(self, hidden_states, attention_mask=attention_mask,
+                                      position_ids=position_ids,
+                                      past_key_values=past_key_values, use_cache=use_cache,
+                                      position_embeddings=position_embeddings, **kwargs)
+    cache = self.__dict__.setdefault('_lcq_stage', {})
+    key = (id(hidden_states), hidden_states.data_ptr(), hidden_states._version,
+           tuple(hidden_states.shape), id(attention_mask), id(position_embeddings),
+           id(position_ids), tuple(sorted(kwargs)))
+    key = key + _mkey(self.input_layernorm, attn.q_proj, attn.k_proj, attn.v_proj)
+    core = _stage(cache, 'core', key,
+                  (self.input_layernorm, attn.q_proj, attn.k_proj, attn.v_proj),
+                  lambda: _attn_core(attn, self.input_layernorm(hidden_states),
+                                     position_embeddings, attention_mask,
+                                     position_ids=position_ids, use_cache=use_cache, **kwargs))
+    key = key + _mkey(attn.o_proj)
+    h = _stage(cache, 'h', key, (attn.o_proj,), lambda: hidden_states + attn.o_proj(core))
+    key = key + _mkey(self.post_attention_layernorm, mlp.gate_proj, mlp.up_proj)
+
+    def _mlp_in():
+        from . import ops
+        hn = self.post_attention_layernorm(h)
+        g = mlp.gate_proj(hn)
+        u = mlp.up_proj(hn)
+        if g.is_cuda and g.dtype in (torch.bfloat16, torch.float16) and g.shape == u.shape \
+                and getattr(mlp.config, 'hidden_act', None) == 'silu' and g.numel() % 8 == 0:
+            return ops.silu_mul(g, u)
+        return mlp.act_fn(g) * u
+
+    m = _stage(cache, 'm', key, (self.post_attention_layernorm, mlp.gate_proj, mlp.up_proj),
+               _mlp_in)
+    return h + mlp.down_proj(m)
+
+
+def clear_stage_cache(block: nn.Module):
+    for mod in block.modules():
+        mod.__dict__.pop('_lcq_stage', None)
+
+
 def install_fused_forward(model: nn.Module):
     """Route the Llama calibration forward's elementwise chains through the lcq fusions
     (env LCQ_FUSED_FORWARD=0 disables)."""
@@ -73,11 +170,17 @@ def install_fused_forward(model: nn.Module):
     if _ORIG_ROTARY is None:
         _ORIG_ROTARY = ml.apply_rotary_pos_emb
         ml.apply_rotary_pos_emb = _fused_apply_rotary
+    global _STOCK_DECODER_FORWARD
+    if _STOCK_DECODER_FORWARD is None:
+        _STOCK_DECODER_FORWARD = ml.LlamaDecoderLayer.forward
+    staged = os.environ.get('LCQ_STAGED_FORWARD', '1') != '0'
     for m in model.modules():
         if isinstance(m, ml.LlamaMLP) and getattr(m.config, 'hidden_act', None) == 'silu':
             m.forward = types.MethodType(_fused_mlp_forward, m)
         elif isinstance(m, ml.LlamaRMSNorm):
             m.forward = types.MethodType(_fused_rmsnorm_forward, m)
+        elif isinstance(m, ml.LlamaDecoderLayer) and staged:
+            m.forward = types.MethodType(_staged_decoder_forward, m)
 
 
 class _Blocks(nn.Module):
@@ -153,6 +256,10 @@ class Llama:
 
     def get_extra_modules(self, block):
         return {}
+
+    def clear_block_cache(self, block):
+        """Drop the staged forward's memo of a finished block (its tensors are large)."""
+        clear_stage_cache(block)
 
     def get_num_attention_heads(self):
         return self.model_config.num_attention_heads

@@ -87,3 +87,37 @@ def test_rmsnorm_close_to_torch(dev, rows, H, dt):
     ulp = ref.float().abs() * (2 ** -7 if dt == torch.bfloat16 else 2 ** -10)
     assert (diff <= ulp + 1e-30).all()
     assert (diff > 0).float().mean().item() < 0.01
+
+
+def test_staged_forward_memo_invalidation(dev):
+    """The memoised decoder forward equals the stock one after in-place weight updates,
+    module replacement and with hooks registered (hooked stages recompute and fire)."""
+    from transformers import LlamaConfig
+    from transformers.models.llama import modeling_llama as ml
+    from lightcompress_amd import llama as L
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                      num_key_value_heads=2, num_hidden_layers=1, vocab_size=128)
+    model = L.Llama.random(cfg, device=dev, seed=6)
+    blk = model.get_blocks()[0]
+    x = torch.randn(2, 32, 256, device=dev).to(torch.bfloat16)
+    kw = model.rotary_kwargs(32)
+
+    def stock():
+        return L._STOCK_DECODER_FORWARD(blk, x, **kw)
+
+    out1 = blk(x, **kw)
+    assert torch.equal(out1, stock())
+    assert torch.equal(blk(x, **kw), out1)                      # memo hit
+    with torch.no_grad():
+        blk.mlp.up_proj.weight.mul_(1.5)                        # in-place: _version bump
+    assert torch.equal(blk(x, **kw), stock())
+    new_o = torch.nn.Linear(256, 256, bias=False).to(dev, torch.bfloat16)
+    blk.self_attn.o_proj = new_o                                # module replaced
+    assert torch.equal(blk(x, **kw), stock())
+    seen = []
+    h = blk.mlp.gate_proj.register_forward_hook(lambda m, i, o: seen.append(i[0].shape))
+    blk(x, **kw)                                                # hooked stage recomputes
+    h.remove()
+    assert len(seen) == 1
+    L.clear_stage_cache(blk)
+    assert '_lcq_stage' not in blk.__dict__
