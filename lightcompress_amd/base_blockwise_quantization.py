@@ -312,12 +312,15 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         if self.batch_calib and (self._batch_ok is None or self._batch_ok[0] != key):
             self._batch_ok = (key, _batchable(input_data, kwargs))
         if self.batch_calib and self._batch_ok[1]:
-            cached = getattr(self, '_split_cache', None)
-            if cached is not None and len(cached[0]) == len(input_data) and all(
-                    a is b for a, b in zip(cached[0], input_data)):
-                xb = cached[1]  # the entries are the split views of this batch: no re-cat
-            else:
+            xb = None
+            for cached in (getattr(self, '_split_cache', None), getattr(self, '_cat_cache', None)):
+                if cached is not None and len(cached[0]) == len(input_data) and all(
+                        a is b for a, b in zip(cached[0], input_data)):
+                    xb = cached[1]  # same entries as a batch we already hold: no re-cat
+                    break
+            if xb is None:
                 xb = torch.cat(list(input_data), dim=0)
+                self._cat_cache = (list(input_data), xb)
             y = self._call_block(block, xb, kwargs[0], stop_after)
             if y is None:
                 return None

@@ -78,10 +78,20 @@ def _hooked(*mods):
     return any(m._forward_hooks or m._forward_pre_hooks for m in mods)
 
 
+STAGE_STATS = {}  # (stage, 'hit' | 'miss' | 'hooked') -> count, for diagnostics
+
+
 def _stage(cache, name, key, mods, fn):
     hit = cache.get(name)
-    if hit is not None and hit[0] == key and not _hooked(*mods):
+    hooked = _hooked(*mods)
+    if hit is not None and hit[0] == key and not hooked:
+        STAGE_STATS[(name, 'hit')] = STAGE_STATS.get((name, 'hit'), 0) + 1
         return hit[1]
+    why = 'hooked' if hooked else ('miss' if hit is None else 'stale')
+    STAGE_STATS[(name, why)] = STAGE_STATS.get((name, why), 0) + 1
+    if hit is not None and hit[0] != key and os.environ.get('LCQ_STAGE_DEBUG'):
+        diff = [i for i, (a, b) in enumerate(zip(hit[0], key)) if a != b]
+        print(f'[stage {name}] stale: key fields {diff[:6]}', flush=True)
     val = fn()
     cache[name] = (key, val)
     return val
@@ -283,9 +293,29 @@ class Llama:
              'inspect': block.mlp.down_proj, 'has_kwargs': False, 'is_mlp': True},
         ]
 
+    @staticmethod
+    def _same_fake_quant(m, module, params_dict):
+        """m is already `module` (exact class) built with the same quant callbacks: a new one
+        would re-derive the identical fake-quant weight from the same weight and buffers, so
+        the existing object is kept (the staged forward's memo stays valid)."""
+        if type(m) is not module or not hasattr(m, 'w_qdq'):
+            return False
+
+        def same(a, b):
+            if a is b:
+                return True
+            fa, fb = getattr(a, 'func', None), getattr(b, 'func', None)
+            return (fa is not None and fa == fb and a.args == b.args
+                    and a.keywords.keys() == b.keywords.keys()
+                    and all(a.keywords[k] is b.keywords[k] for k in a.keywords))
+        return (same(m.w_qdq, params_dict.get('w_qdq')) and
+                same(m.a_qdq, params_dict.get('a_qdq')))
+
     def replace_module_subset(self, module, block, subset, block_idx, params_dict):
         for name, m in subset['layers'].items():
             if not isinstance(m, _LINEAR_TYPES) or getattr(m, 'no_quant', False):
+                continue
+            if self._same_fake_quant(m, module, params_dict):
                 continue
             new = module.new(m, **params_dict)
             parent_name, _, child = name.rpartition('.')
