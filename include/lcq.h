@@ -138,11 +138,13 @@ int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, c
                    const void* z_in, void* s_out, void* z_out, int64_t ng_total, void* err,
                    void* losses, void* stream);
 
-/* GPTQ trailing update W[:, c1:] -= err[:, :cnt] @ U[c0:c0+cnt, c1:] (gptq.py:244) on fp32
- * MFMA (k-ordered fma chain: deterministic and independent of the row range, so row-sharded
- * GPTQ is bit-identical to one GPU). err k-major [128, rows] fp32 from lcq_gptq_block. */
+/* GPTQ trailing update W[:, c1:c2] -= err^T[:, :cnt] @ U[c0:c0+cnt, c1:c2] (gptq.py:244) on
+ * fp32 MFMA (k-ordered fma chain: deterministic and independent of the row range, so
+ * row-sharded GPTQ is bit-identical to one GPU). err k-major [cnt, rows] fp32 (cnt <= 8192):
+ * one block's Err1 from lcq_gptq_block, or the stacked Err1 of several blocks (the host's
+ * two-level lazy update applies a 1024-column superblock's errors to the far columns at once). */
 int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, int cnt, int64_t c1,
-                      const void* err, const void* U, int64_t ldu, void* stream);
+                      int64_t c2, const void* err, const void* U, int64_t ldu, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * AWQ (awq.py) and auto-clip (auto_clip.py) building blocks. dtype = BF16/F16/F32; each op

@@ -269,8 +269,8 @@ __device__ __forceinline__ void trail_load(const float* __restrict__ ET, const f
 
 __global__ void __launch_bounds__(256, 2)
     k_gptq_trailing(float* __restrict__ W, int64_t rows, int64_t ld, int64_t c0, int cnt,
-                    int64_t c1, const float* __restrict__ ET, const float* __restrict__ U,
-                    int64_t ldu) {
+                    int64_t c1, int64_t c2, const float* __restrict__ ET,
+                    const float* __restrict__ U, int64_t ldu) {
   __shared__ __attribute__((aligned(16))) float As[2][KC * TT];  // [k][row]
   __shared__ __attribute__((aligned(16))) float Bs[2][KC * TT];  // [k][col]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
   float4 ra[4], rb[4];
-  trail_load(ET, U, rows, ld, ldu, c0, cnt, r0, j0, 0, tid, ra, rb);
+  trail_load(ET, U, rows, c2, ldu, c0, cnt, r0, j0, 0, tid, ra, rb);
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int idx = it * 256 + tid;
@@ -296,7 +296,7 @@ __global__ void __launch_bounds__(256, 2)
   const int nch = (cnt + KC - 1) / KC;
   for (int ch = 0; ch < nch; ++ch) {
     const int cur = ch & 1;
-    if (ch + 1 < nch) trail_load(ET, U, rows, ld, ldu, c0, cnt, r0, j0, (ch + 1) * KC, tid, ra, rb);
+    if (ch + 1 < nch) trail_load(ET, U, rows, c2, ldu, c0, cnt, r0, j0, (ch + 1) * KC, tid, ra, rb);
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 2) {
       const int k = kk + (lane >> 5);
@@ -331,22 +331,23 @@ __global__ void __launch_bounds__(256, 2)
       for (int reg = 0; reg < 16; ++reg) {
         const int64_t r = r0 + wr * 64 + ta * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
         const int64_t c = j0 + wc * 64 + tb * 32 + (lane & 31);
-        if (r < rows && c < ld) W[r * ld + c] = W[r * ld + c] - acc[ta][tb][reg];
+        if (r < rows && c < c2) W[r * ld + c] = W[r * ld + c] - acc[ta][tb][reg];
       }
 }
 
 }  // namespace lcq
 
 extern "C" int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, int cnt,
-                                 int64_t c1, const void* err, const void* U, int64_t ldu,
-                                 void* stream) {
-  LCQ_REQUIRE(rows > 0 && ld > 0 && cnt > 0 && cnt <= GB, "bad shape");
-  LCQ_REQUIRE(c0 >= 0 && c0 + cnt <= ldu && c1 >= c0 + cnt && c1 <= ld && ld <= ldu,
+                                 int64_t c1, int64_t c2, const void* err, const void* U,
+                                 int64_t ldu, void* stream) {
+  LCQ_REQUIRE(rows > 0 && ld > 0 && cnt > 0 && cnt <= 8192, "bad shape");
+  LCQ_REQUIRE(c0 >= 0 && c0 + cnt <= ldu && c1 >= c0 + cnt && c2 >= c1 && c2 <= ld &&
+                  ld <= ldu,
               "bad column ranges");
-  if (c1 == ld) return LCQ_OK;
-  const dim3 grid((unsigned)((ld - c1 + TT - 1) / TT), (unsigned)((rows + TT - 1) / TT));
+  if (c2 == c1) return LCQ_OK;
+  const dim3 grid((unsigned)((c2 - c1 + TT - 1) / TT), (unsigned)((rows + TT - 1) / TT));
   hipLaunchKernelGGL(k_gptq_trailing, grid, 256, 0, as_stream(stream),
-                     reinterpret_cast<float*>(W), rows, ld, c0, cnt, c1,
+                     reinterpret_cast<float*>(W), rows, ld, c0, cnt, c1, c2,
                      reinterpret_cast<const float*>(err), reinterpret_cast<const float*>(U),
                      ldu);
   return check_launch("lcq_gptq_trailing");

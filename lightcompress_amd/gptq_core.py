@@ -6,6 +6,7 @@ Kept separate from the plugin class (``gptq.py``) so the algorithm can be driven
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -112,31 +113,44 @@ def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
 
 @torch.no_grad()
 def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
-                qmin: int, qmax: int, fixed=None, losses: bool = False):
+                qmin: int, qmax: int, fixed=None, losses: bool = False,
+                superblock: int | None = None):
     """Blocked OBS loop (gptq.py:198-244) on permuted fp32 W, in place.
 
     Per 128-column block: the HIP kernel runs the in-block sequential loop (bit-exact rank-1
-    updates), then the trailing update ``W[:, i2:] -= Err @ U[i1:i2, i2:]`` (fp32 MFMA kernel,
-    deterministic k order)."""
+    updates). The reference then applies ``W[:, i2:] -= Err @ U[i1:i2, i2:]`` to every later
+    column; here that update is two-level: inside a superblock of ``superblock`` columns each
+    block updates only the rest of its superblock, and the far columns receive the
+    superblock's stacked errors in ONE K = superblock update (same terms, grouped differently
+    -> T2; every element still has a fixed k order, so row sharding stays bit-identical).
+    fp32 MFMA kernel (``lcq_gptq_trailing``)."""
     rows, cols = W.shape
     dev = W.device
     U = U.contiguous()
     ng = 0 if group is None else -(-cols // group)
     s_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng else None
     z_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng and not sym else None
-    err = torch.empty((BLOCK, rows), dtype=torch.float32, device=dev)  # k-major Err1
+    if superblock is None:
+        superblock = int(os.environ.get('LCQ_GPTQ_SUPERBLOCK', '1024'))
+    SB = max(BLOCK, superblock // BLOCK * BLOCK)
+    errT = torch.empty((SB, rows), dtype=torch.float32, device=dev)  # k-major stacked Err1
     L = torch.zeros_like(W) if losses else None
     s_in = z_in = None
     if group is None:
         s_in = fixed[0].reshape(-1).float().contiguous()
         z_in = None if sym else fixed[1].reshape(-1).float().contiguous()
-    for i1 in range(0, cols, BLOCK):
-        i2 = min(i1 + BLOCK, cols)
-        cnt = i2 - i1
-        ops.gptq_block(W, i1, cnt, U, group or 0, qmin, qmax, sym, s_out, z_out, err, L,
-                       s_in, z_in)
-        if i2 < cols:
-            ops.gptq_trailing(W, i1, cnt, i2, err, U)
+    for sb0 in range(0, cols, SB):
+        sb1 = min(sb0 + SB, cols)
+        for i1 in range(sb0, sb1, BLOCK):
+            i2 = min(i1 + BLOCK, cols)
+            cnt = i2 - i1
+            e = errT[i1 - sb0:]
+            ops.gptq_block(W, i1, cnt, U, group or 0, qmin, qmax, sym, s_out, z_out, e, L,
+                           s_in, z_in)
+            if i2 < sb1:  # near columns: the rest of this superblock
+                ops.gptq_trailing(W, i1, cnt, i2, e, U, c2=sb1)
+        if sb1 < cols:    # far columns: the whole superblock's errors at once
+            ops.gptq_trailing(W, sb0, sb1 - sb0, sb1, errT, U, c2=cols)
     return s_out, z_out, L
 
 

@@ -173,11 +173,12 @@ def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: i
 
 
 def gptq_trailing(W: torch.Tensor, c0: int, cnt: int, c1: int, err: torch.Tensor,
-                  U: torch.Tensor):
-    """W[:, c1:] -= err.T[:, :cnt] @ U[c0:c0+cnt, c1:] in place (err k-major [128, rows];
-    fp32 MFMA, deterministic k order)."""
+                  U: torch.Tensor, c2: int | None = None):
+    """W[:, c1:c2] -= err.T[:, :cnt] @ U[c0:c0+cnt, c1:c2] in place (err k-major [cnt, rows];
+    fp32 MFMA, deterministic k order). c2 defaults to the last column."""
     rows, ld = W.shape
-    N.call('lcq_gptq_trailing', N.ptr(W), rows, ld, int(c0), int(cnt), int(c1), N.ptr(err),
+    c2 = ld if c2 is None else int(c2)
+    N.call('lcq_gptq_trailing', N.ptr(W), rows, ld, int(c0), int(cnt), int(c1), c2, N.ptr(err),
            N.ptr(U), U.shape[1], N.stream_of(W))
 
 

@@ -149,24 +149,28 @@ def test_layer_end_to_end_vs_reference(dev, name):
     assert torch.allclose(fq.float(), ref.float(), atol=2 * c['scales'].abs().max().item())
 
 
-@pytest.mark.parametrize('rows,ic,c0', [(300, 512, 128), (256, 4096, 0), (129, 392, 128)])
-def test_trailing_update(dev, rows, ic, c0):
-    """lcq_gptq_trailing vs fp64, and bit-identical on any row sub-range (row sharding)."""
+@pytest.mark.parametrize('rows,ic,c0,K,c2', [(300, 512, 128, 128, None), (256, 4096, 0, 128, None),
+                                            (129, 392, 128, 128, None), (200, 2048, 0, 1024, None),
+                                            (200, 2048, 128, 128, 1024)])
+def test_trailing_update(dev, rows, ic, c0, K, c2):
+    """lcq_gptq_trailing vs fp64 (incl. K = 1024 superblock updates and a column window),
+    and bit-identical on any row sub-range (row sharding)."""
     from lightcompress_amd import ops
     g = torch.Generator(device=dev).manual_seed(rows + ic)
     W = torch.randn(rows, ic, generator=g, device=dev)
     U = torch.randn(ic, ic, generator=g, device=dev).triu().contiguous()
-    err = torch.randn(128, rows, generator=g, device=dev)  # k-major, as lcq_gptq_block writes
-    cnt = min(128, ic - c0)
+    err = torch.randn(K, rows, generator=g, device=dev)  # k-major, as lcq_gptq_block writes
+    cnt = min(K, ic - c0)
     c1 = c0 + cnt
+    end = ic if c2 is None else c2
     ref = W.double().clone()
-    ref[:, c1:] -= err.t()[:, :cnt].double() @ U[c0:c1, c1:].double()
+    ref[:, c1:end] -= err.t()[:, :cnt].double() @ U[c0:c1, c1:end].double()
     out = W.clone()
-    ops.gptq_trailing(out, c0, cnt, c1, err, U)
-    assert torch.equal(out[:, :c1], W[:, :c1])
-    tol = 1e-5 * math.sqrt(cnt) * (1 + ref[:, c1:].abs())
-    assert ((out[:, c1:].double() - ref[:, c1:]).abs() <= tol).all()
+    ops.gptq_trailing(out, c0, cnt, c1, err, U, c2=end)
+    assert torch.equal(out[:, :c1], W[:, :c1]) and torch.equal(out[:, end:], W[:, end:])
+    tol = 1e-5 * math.sqrt(cnt) * (1 + ref[:, c1:end].abs())
+    assert ((out[:, c1:end].double() - ref[:, c1:end]).abs() <= tol).all()
     h = rows // 3
     part = W[h:].clone()
-    ops.gptq_trailing(part, c0, cnt, c1, err[:, h:].contiguous(), U)
+    ops.gptq_trailing(part, c0, cnt, c1, err[:, h:].contiguous(), U, c2=end)
     assert torch.equal(part, out[h:])
