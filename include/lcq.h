@@ -138,6 +138,14 @@ int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, c
                    const void* z_in, void* s_out, void* z_out, int64_t ng_total, void* err,
                    void* losses, void* stream);
 
+/* Diagonal tile of the recursive fp32 factorisation behind U = chol(H^-1, upper)
+ * (gptq.py:169-174): for SPD A (n x n, n <= 128, row-major fp32, leading dim lda), X <- L^-1
+ * and, if L is not NULL, L <- the lower Cholesky factor (upper parts zeroed). A is only read.
+ * info (int32): row0 + the first non-positive pivot of the tile (1-based), written only on
+ * failure and only if still 0 (the order of the leading minor torch.linalg.cholesky reports). */
+int lcq_chol_inv_tile(const void* A, int64_t lda, int n, void* L, int64_t ldl, void* X,
+                      int64_t ldx, void* info, int64_t row0, void* stream);
+
 /* GPTQ trailing update W[:, c1:c2] -= err^T[:, :cnt] @ U[c0:c0+cnt, c1:c2] (gptq.py:244) on
  * fp32 MFMA (k-ordered fma chain: deterministic and independent of the row range, so
  * row-sharded GPTQ is bit-identical to one GPU). err k-major [cnt, rows] fp32 (cnt <= 8192):

@@ -1,0 +1,347 @@
+// Diagonal-tile kernel of the recursive fp32 Cholesky / triangular inverse behind GPTQ's
+// U = chol(H^-1, upper) (gptq.py:169-174; computed as J chol(J H J)^-1 J, see gptq_core).
+// The recursion (host side) does the large updates as fp32 GEMMs; this kernel factors a
+// <= 128 x 128 diagonal tile and inverts its factor, in one workgroup with both in LDS.
+//
+// Right-looking over PW-column panels on the augmented [A | R], R = I initially; after panel P
+// R's rows P hold X_P = L_PP^-1 R_P, the rows of L^-1 (blocked forward substitution of L X = I):
+//   S1 (one wave, registers): every lane factors the whole PW x PW diagonal block redundantly
+//      in its own registers (no cross-lane traffic, no barriers), then lane j computes column
+//      j of Z = L_PP^-1;
+//   S2 (threads 0-127) X_P = Z R_P, one thread per column; (threads 128-255)
+//      L_below = A_below Z^T, one thread per row;
+//   S3 (all threads, two tile loops): A22 -= L_below L_below^T (lower) and
+//      R_below -= L_below X_P, 4x4 register tiles with every LDS read issued before the FMAs.
+// Two barriers per panel; nothing leaves LDS until the end. Only X = L^-1 is needed by the
+// recursion (gptq_core._chol_inv_rec); L is written back only when asked for (L may alias A:
+// every read of A precedes the first barrier, every write of L follows the last).
+// Measured (scripts/probes/chol_tile_prof.py, one 128-tile): PW 16 / 256 threads 70 us, PW 8 /
+// 256 threads 60 us, PW 8 / 1024 threads 51 us -- S1 is VALU-bound in one wave at ~PW^3/6 FMAs
+// per panel, S3 is LDS-latency-bound; what remains is the S1 -> S2 -> S3 chain per panel.
+#include "lcq_common.h"
+
+namespace lcq {
+
+constexpr int CTILE = 128;
+constexpr int CLD = CTILE + 4;  // LDS row pitch: 16-byte aligned rows (ds_read_b128 of row
+                                // segments); 132 = 4 mod 64 banks, 16 rows per bank sweep
+#ifndef LCQ_CHOL_PW
+#define LCQ_CHOL_PW 8
+#endif
+constexpr int PW = LCQ_CHOL_PW;  // panel width
+#ifndef LCQ_CHOL_NT
+#define LCQ_CHOL_NT 1024
+#endif
+constexpr int NT = LCQ_CHOL_NT;  // threads; > 256 hides the LDS latency of the S3 tiles
+constexpr int VEC_PER_THREAD = CTILE * CTILE / 4 / NT;
+
+#ifdef LCQ_CHOL_PROF  // probe builds only (scripts/probes/chol_tile_prof.py): stage timestamps
+#define PROF_STAMP(k)                                                                 \
+  if (threadIdx.x == 0)                                                               \
+    reinterpret_cast<unsigned long long*>(info)[1 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define PROF_STAMP(k)
+#endif
+
+// lower-triangle 4x4 tile index t -> (ti, tk), tk <= ti
+__device__ __forceinline__ void tri_tile(int t, int& ti, int& tk) {
+  ti = (int)((__builtin_amdgcn_sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);  // corrected below
+  while (ti * (ti + 1) / 2 > t) --ti;
+  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+  tk = t - ti * (ti + 1) / 2;
+}
+
+// S1: factor a[c0:c0+cw, c0:c0+cw] (lower) in every lane's registers; lane 0 writes L_PP back,
+// lanes < PW write column `lane` of Z = L_PP^-1 to zs[r*PW+lane]. Returns the first bad pivot
+// (1-based within the block) or 0 -- uniform.
+__device__ __forceinline__ int factor_diag(float* a, float* zs, int c0, int cw, int lane) {
+  float l[PW][PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const float4* row = reinterpret_cast<const float4*>(a + (c0 + i) * CLD + c0);
+#pragma unroll
+    for (int q = 0; q < PW / 4; ++q) {
+      if (4 * q <= i) {
+        const float4 v = row[q];  // broadcast: every lane reads the same address
+        l[i][4 * q] = v.x;
+        l[i][4 * q + 1] = v.y;
+        l[i][4 * q + 2] = v.z;
+        l[i][4 * q + 3] = v.w;
+      }
+    }
+    if (i >= cw) {  // rows past the tile edge: identity, keeps the unrolled code finite
+#pragma unroll
+      for (int k = 0; k < PW; ++k) l[i][k] = (k == i) ? 1.f : 0.f;
+    }
+  }
+  float rinv[PW];
+  int bad = 0;
+#pragma unroll
+  for (int c = 0; c < PW; ++c) {
+    const float d = l[c][c];
+    const bool nb = !(d > 0.f);
+    if (nb && bad == 0) bad = c + 1;
+    const float sq = nb ? 1.f : sqrtf(d);
+    rinv[c] = 1.f / sq;
+    l[c][c] = sq;
+#pragma unroll
+    for (int i = c + 1; i < PW; ++i) l[i][c] *= rinv[c];
+#pragma unroll
+    for (int i = c + 1; i < PW; ++i)
+#pragma unroll
+      for (int k = c + 1; k <= i; ++k) l[i][k] = fmaf(-l[i][c], l[k][c], l[i][k]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      if (i < cw)
+#pragma unroll
+        for (int k = 0; k <= i; ++k) a[(c0 + i) * CLD + c0 + k] = l[i][k];
+  }
+  // Z column `lane`: z[r] = (e_lane[r] - sum_{q<r} L[r][q] z[q]) / L[r][r]
+  float z[PW];
+#pragma unroll
+  for (int r = 0; r < PW; ++r) {
+    float sacc = (lane == r) ? 1.f : 0.f;
+#pragma unroll
+    for (int q = 0; q < r; ++q) sacc = fmaf(-l[r][q], z[q], sacc);
+    z[r] = sacc * rinv[r];
+  }
+  if (lane < PW) {
+#pragma unroll
+    for (int r = 0; r < PW; ++r) zs[r * PW + lane] = (r < cw && lane < cw) ? z[r] : 0.f;
+  }
+  return bad;
+}
+
+// S3 tile: rows i0..i0+3 of L_below (panel columns c0..c0+PW-1) times either rows k0..k0+3 of
+// the panel (LOWER: A22 tile, lower part only) or X_P[:, k0..k0+3] (R tile); all b128
+// reads are issued before any FMA
+template <bool LOWER>
+__device__ __forceinline__ void rank16_tile(float* a, float* x, int c0, int i0, int k0, int n) {
+  float4 pi[4][PW / 4], pk[4][PW / 4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int q = 0; q < PW / 4; ++q)
+      pi[u][q] = *reinterpret_cast<const float4*>(a + (i0 + u) * CLD + c0 + 4 * q);
+  if (LOWER) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < PW / 4; ++q)
+        pk[u][q] = *reinterpret_cast<const float4*>(a + (k0 + u) * CLD + c0 + 4 * q);
+  } else {
+    // pk[v][q].{x,y,z,w} = X[c0+4q+{0..3}][k0+v], from X rows (k0..k0+3 contiguous)
+#pragma unroll
+    for (int q = 0; q < PW / 4; ++q) {
+      const float4 r0 = *reinterpret_cast<const float4*>(x + (c0 + 4 * q) * CLD + k0);
+      const float4 r1 = *reinterpret_cast<const float4*>(x + (c0 + 4 * q + 1) * CLD + k0);
+      const float4 r2 = *reinterpret_cast<const float4*>(x + (c0 + 4 * q + 2) * CLD + k0);
+      const float4 r3 = *reinterpret_cast<const float4*>(x + (c0 + 4 * q + 3) * CLD + k0);
+      pk[0][q] = make_float4(r0.x, r1.x, r2.x, r3.x);
+      pk[1][q] = make_float4(r0.y, r1.y, r2.y, r3.y);
+      pk[2][q] = make_float4(r0.z, r1.z, r2.z, r3.z);
+      pk[3][q] = make_float4(r0.w, r1.w, r2.w, r3.w);
+    }
+  }
+  float acc[4][4] = {};
+#pragma unroll
+  for (int q = 0; q < PW / 4; ++q)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        acc[u][v] = fmaf(pi[u][q].x, pk[v][q].x, acc[u][v]);
+        acc[u][v] = fmaf(pi[u][q].y, pk[v][q].y, acc[u][v]);
+        acc[u][v] = fmaf(pi[u][q].z, pk[v][q].z, acc[u][v]);
+        acc[u][v] = fmaf(pi[u][q].w, pk[v][q].w, acc[u][v]);
+      }
+  float* dst = LOWER ? a : x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int i = i0 + u, k = k0 + v;
+      if (i < n && (!LOWER || k <= i)) dst[i * CLD + k] -= acc[u][v];
+    }
+}
+
+__global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t lda,
+                                                       int n, float* Lout,
+                                                       int64_t ldl, float* __restrict__ X,
+                                                       int64_t ldx, int* __restrict__ info,
+                                                       int64_t row0, int vec) {
+  __shared__ __attribute__((aligned(16))) float a[CTILE * CLD];
+  __shared__ __attribute__((aligned(16))) float x[CTILE * CLD];
+  __shared__ __attribute__((aligned(16))) float zs[PW * PW];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  PROF_STAMP(0)
+  if (vec) {  // n == 128, lda % 4 == 0, 16-byte aligned: one batch of float4 loads per thread
+    float4 v[VEC_PER_THREAD];
+#pragma unroll
+    for (int u = 0; u < VEC_PER_THREAD; ++u) {
+      const int e = tid + NT * u, i = e >> 5, j = (e & 31) * 4;
+      v[u] = *reinterpret_cast<const float4*>(A + (int64_t)i * lda + j);
+    }
+#pragma unroll
+    for (int u = 0; u < VEC_PER_THREAD; ++u) {
+      const int e = tid + NT * u, i = e >> 5, j = (e & 31) * 4;
+      *reinterpret_cast<float4*>(a + i * CLD + j) = v[u];
+    }
+  } else {
+#pragma unroll
+    for (int it0 = 0; it0 < CTILE * CTILE / NT; it0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int idx = tid + NT * (it0 + u), i = idx >> 7, j = idx & 127;
+        v[u] = (i < n && j < n) ? A[(int64_t)i * lda + j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int idx = tid + NT * (it0 + u), i = idx >> 7, j = idx & 127;
+        a[i * CLD + j] = v[u];
+      }
+    }
+  }
+  for (int idx = tid; idx < CTILE * CTILE; idx += NT) {
+    const int i = idx >> 7, j = idx & 127;
+    x[i * CLD + j] = (i == j) ? 1.f : 0.f;
+  }
+  __syncthreads();
+  PROF_STAMP(1)
+
+  for (int c0 = 0; c0 < n; c0 += PW) {
+    const int cw = min(PW, n - c0);
+    const int b0 = c0 + PW, m2 = n - b0;
+    if (wave == 0) {
+      const int bad = factor_diag(a, zs, c0, cw, lane);
+      if (bad && lane == 0 && info) atomicCAS(info, 0, (int)(row0 + c0 + bad));
+    }
+    PROF_STAMP(2 + 4 * (c0 / PW))
+    __syncthreads();
+    if (tid < 128) {
+      // X_P = Z R_P for column j (columns >= c0 + cw of R_P are zero)
+      const int j = tid;
+      if (j < c0 + cw) {
+        float rp[PW], t[PW];
+#pragma unroll
+        for (int q = 0; q < PW; ++q) rp[q] = (q < cw) ? x[(c0 + q) * CLD + j] : 0.f;
+#pragma unroll
+        for (int r = 0; r < PW; ++r) {
+          const float4* z4 = reinterpret_cast<const float4*>(zs + r * PW);
+          float sacc = 0.f;
+#pragma unroll
+          for (int q4 = 0; q4 < PW / 4; ++q4) {
+            const float4 zz = z4[q4];
+            sacc = fmaf(zz.x, rp[4 * q4], sacc);
+            sacc = fmaf(zz.y, rp[4 * q4 + 1], sacc);
+            sacc = fmaf(zz.z, rp[4 * q4 + 2], sacc);
+            sacc = fmaf(zz.w, rp[4 * q4 + 3], sacc);
+          }
+          t[r] = sacc;
+        }
+#pragma unroll
+        for (int r = 0; r < PW; ++r)
+          if (r < cw) x[(c0 + r) * CLD + j] = t[r];
+      }
+    } else if (m2 > 0) {
+      // L_below row i = A row i (panel columns) Z^T
+      const int i = b0 + tid - 128;
+      if (i < n) {
+        float ar[PW];
+#pragma unroll
+        for (int q = 0; q < PW / 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(a + i * CLD + c0 + 4 * q);
+          ar[4 * q] = v.x;
+          ar[4 * q + 1] = v.y;
+          ar[4 * q + 2] = v.z;
+          ar[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int c = 0; c < PW; ++c) {
+          const float4* z4 = reinterpret_cast<const float4*>(zs + c * PW);
+          float sacc = 0.f;
+#pragma unroll
+          for (int q4 = 0; q4 < PW / 4; ++q4) {
+            const float4 zz = z4[q4];
+            sacc = fmaf(zz.x, ar[4 * q4], sacc);
+            sacc = fmaf(zz.y, ar[4 * q4 + 1], sacc);
+            sacc = fmaf(zz.z, ar[4 * q4 + 2], sacc);
+            sacc = fmaf(zz.w, ar[4 * q4 + 3], sacc);
+          }
+          a[i * CLD + c0 + c] = sacc;
+        }
+      }
+    }
+    PROF_STAMP(3 + 4 * (c0 / PW))
+    __syncthreads();
+    PROF_STAMP(4 + 4 * (c0 / PW))
+    if (m2 > 0) {
+      // S3: tiles of A22 (lower) then tiles of R_below (columns < c0 + PW); rows stay < 128
+      const int nt = (m2 + 3) >> 2, T = nt * (nt + 1) / 2, nc = (c0 + PW) >> 2;
+      int t = tid;
+      for (; t < T; t += NT) {
+        int ti, tk;
+        tri_tile(t, ti, tk);
+        rank16_tile<true>(a, x, c0, b0 + 4 * ti, b0 + 4 * tk, n);
+      }
+      for (; t < T + nt * nc; t += NT) {
+        const int t2 = t - T;
+        rank16_tile<false>(a, x, c0, b0 + 4 * (t2 / nc), 4 * (t2 % nc), n);
+      }
+    }
+    PROF_STAMP(5 + 4 * (c0 / PW))
+    __syncthreads();
+  }
+  PROF_STAMP(70)
+
+  if (vec) {
+#pragma unroll
+    for (int u = 0; u < VEC_PER_THREAD; ++u) {
+      const int e = tid + NT * u, i = e >> 5, j = (e & 31) * 4;
+      float4 o = *reinterpret_cast<const float4*>(x + i * CLD + j);
+      if (j > i) o.x = 0.f;
+      if (j + 1 > i) o.y = 0.f;
+      if (j + 2 > i) o.z = 0.f;
+      if (j + 3 > i) o.w = 0.f;
+      *reinterpret_cast<float4*>(X + (int64_t)i * ldx + j) = o;
+      if (Lout) {
+        o = *reinterpret_cast<const float4*>(a + i * CLD + j);
+        if (j > i) o.x = 0.f;
+        if (j + 1 > i) o.y = 0.f;
+        if (j + 2 > i) o.z = 0.f;
+        if (j + 3 > i) o.w = 0.f;
+        *reinterpret_cast<float4*>(Lout + (int64_t)i * ldl + j) = o;
+      }
+    }
+  } else {
+#pragma unroll 8
+    for (int it = 0; it < CTILE * CTILE / NT; ++it) {
+      const int idx = tid + NT * it, i = idx >> 7, j = idx & 127;
+      if (i < n && j < n) {
+        X[(int64_t)i * ldx + j] = (j <= i) ? x[i * CLD + j] : 0.f;
+        if (Lout) Lout[(int64_t)i * ldl + j] = (j <= i) ? a[i * CLD + j] : 0.f;
+      }
+    }
+  }
+  PROF_STAMP(71)
+}
+
+}  // namespace lcq
+
+using namespace lcq;
+
+extern "C" int lcq_chol_inv_tile(const void* A, int64_t lda, int n, void* L, int64_t ldl,
+                                 void* X, int64_t ldx, void* info, int64_t row0, void* stream) {
+  LCQ_REQUIRE(n > 0 && n <= CTILE && lda >= n && ldx >= n && (!L || ldl >= n),
+              "tile must be 1..128 wide");
+  const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int vec = n == CTILE && lda % 4 == 0 && ldx % 4 == 0 && al(A) && al(X) &&
+                  (!L || (ldl % 4 == 0 && al(L)));
+  hipLaunchKernelGGL(k_chol_inv_tile, dim3(1), NT, 0, as_stream(stream),
+                     reinterpret_cast<const float*>(A), lda, n, reinterpret_cast<float*>(L), ldl,
+                     reinterpret_cast<float*>(X), ldx, reinterpret_cast<int*>(info), row0, vec);
+  return check_launch("lcq_chol_inv_tile");
+}

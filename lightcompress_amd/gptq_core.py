@@ -65,11 +65,15 @@ def prepare_hessian(H: torch.Tensor, actorder: bool, percdamp: float):
     damp = percdamp * torch.mean(torch.diag(H))
     d = torch.arange(cols, device=H.device)
     H[d, d] += damp
-    with _linalg_backend():
-        C = torch.linalg.cholesky(H.flip(0, 1))
-        del H
-        eye = torch.eye(cols, dtype=C.dtype, device=C.device)
-        U = torch.linalg.solve_triangular(C, eye, upper=False).flip(0, 1).contiguous()
+    backend = os.environ.get('LCQ_CHOL', 'lcq')
+    if backend == 'lcq':
+        U = inverse_cholesky_upper(H)
+    else:
+        with _linalg_backend():
+            C = torch.linalg.cholesky(H.flip(0, 1))
+            del H
+            eye = torch.eye(cols, dtype=C.dtype, device=C.device)
+            U = torch.linalg.solve_triangular(C, eye, upper=False).flip(0, 1).contiguous()
     return U, perm, dead
 
 
@@ -93,6 +97,52 @@ class _linalg_backend:
     def __exit__(self, *exc):
         if self.want != 'default':
             torch.backends.cuda.preferred_linalg_library(self.prev)
+
+
+_TILE = 128
+
+
+def _split(n):
+    return max(_TILE, (n // 2 + _TILE - 1) // _TILE * _TILE)
+
+
+def _chol_inv_rec(A: torch.Tensor, info: torch.Tensor, row0: int = 0) -> torch.Tensor:
+    """A (square fp32 row-major view) <- its lower Cholesky factor L; returns L^-1.
+
+    [[A11, .], [A21, A22]]: L11 = chol(A11), X11 = L11^-1 (recursion); L21 = A21 X11^T;
+    A22 -= L21 L21^T; L22 = chol(A22), X22 = L22^-1 (recursion); X21 = -X22 L21 X11.
+    Tiles of <= 128 are factored and inverted in one workgroup (lcq_chol_inv_tile); everything
+    else is fp32 GEMM (fp32 MFMA, no reduced-precision path on gfx950)."""
+    n = A.shape[0]
+    if n <= _TILE:
+        return ops.chol_inv_tile(A, info, row0)
+    n1 = _split(n)
+    A11, A21, A22 = A[:n1, :n1], A[n1:, :n1], A[n1:, n1:]
+    X11 = _chol_inv_rec(A11, info, row0)
+    L21 = A21 @ X11.t()
+    A21.copy_(L21)
+    A22.addmm_(L21, L21.t(), alpha=-1.0)
+    X22 = _chol_inv_rec(A22, info, row0 + n1)
+    X = torch.zeros((n, n), dtype=torch.float32, device=A.device)
+    X[:n1, :n1] = X11
+    X[n1:, n1:] = X22
+    X[n1:, :n1] = -(X22 @ (L21 @ X11))
+    return X
+
+
+def inverse_cholesky_upper(H: torch.Tensor) -> torch.Tensor:
+    """U = chol(H^-1, upper) = J chol(J H J)^-1 J for SPD fp32 H (H is consumed)."""
+    Hr = H.flip(0, 1).contiguous()
+    del H
+    info = torch.zeros(1, dtype=torch.int32, device=Hr.device)
+    X = _chol_inv_rec(Hr, info)
+    bad = int(info.item())
+    if bad:
+        raise torch.linalg.LinAlgError(
+            f'linalg.cholesky: The factorization could not be completed because the input '
+            f'is not positive-definite (the leading minor of order {bad} is not '
+            f'positive-definite).')
+    return X.flip(0, 1).contiguous()
 
 
 def prepare_weight(W: torch.Tensor, perm, dead):

@@ -172,6 +172,28 @@ def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: i
            N.ptr(z_out), int(ng_total), N.ptr(err), N.ptr(losses), N.stream_of(W))
 
 
+def _ld(t: torch.Tensor) -> int:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError('expected a row-major 2-D view')
+    return t.stride(0)
+
+
+def chol_inv_tile(A: torch.Tensor, info: torch.Tensor, row0: int = 0,
+                  L: torch.Tensor | None = None) -> torch.Tensor:
+    """Returns L^-1 for the lower Cholesky factor L of A (<= 128 x 128 fp32 view, unit column
+    stride); L itself is written to `L` when given (may be A). info (int32, 1 element) receives
+    row0 + the first non-positive pivot (1-based) on failure."""
+    if A.dtype != torch.float32 or A.shape[0] != A.shape[1]:
+        raise ValueError('chol_inv_tile expects a square fp32 tile')
+    if L is not None and (L.shape != A.shape or L.dtype != torch.float32):
+        raise ValueError('L must match A')
+    X = torch.empty((A.shape[0], A.shape[0]), dtype=torch.float32, device=A.device)
+    N.call('lcq_chol_inv_tile', A.data_ptr(), _ld(A), A.shape[0],
+           0 if L is None else L.data_ptr(), 0 if L is None else _ld(L),
+           N.ptr(X), X.shape[1], N.ptr(info), row0, N.stream_of(A))
+    return X
+
+
 def gptq_trailing(W: torch.Tensor, c0: int, cnt: int, c1: int, err: torch.Tensor,
                   U: torch.Tensor, c2: int | None = None):
     """W[:, c1:c2] -= err.T[:, :cnt] @ U[c0:c0+cnt, c1:c2] in place (err k-major [cnt, rows];

@@ -1,4 +1,4 @@
-"""Time the GPTQ Cholesky chain (gptq.py:58-64) with torch's linalg backends on the GPU."""
+"""Time the GPTQ Cholesky chain (gptq.py:169-174) with torch's linalg backends on the GPU."""
 import time
 import torch
 

@@ -174,3 +174,65 @@ def test_trailing_update(dev, rows, ic, c0, K, c2):
     part = W[h:].clone()
     ops.gptq_trailing(part, c0, cnt, c1, err[:, h:].contiguous(), U, c2=end)
     assert torch.equal(part, out[h:])
+
+
+@pytest.mark.parametrize('n', [100, 128, 300, 1000, 4096])
+def test_inverse_cholesky_upper(dev, n):
+    """Recursive lcq factorisation: U^T U = H^-1 with U upper (fp64 check), equal to the
+    reference chain cholesky -> cholesky_inverse -> cholesky(upper) to fp32 accuracy."""
+    from lightcompress_amd import gptq_core
+    g = torch.Generator().manual_seed(n)
+    A = torch.randn(n, 2 * n, generator=g, dtype=torch.float64)
+    H = A @ A.t() / n + 0.05 * torch.eye(n, dtype=torch.float64)
+    U = gptq_core.inverse_cholesky_upper(H.float().to(dev)).double().cpu()
+    assert torch.equal(U, U.triu())
+    ref = torch.linalg.cholesky(torch.cholesky_inverse(torch.linalg.cholesky(H)), upper=True)
+    rel = ((U - ref).abs().max() / ref.abs().max()).item()
+    assert rel < 5e-4, rel
+
+
+def test_inverse_cholesky_not_pd(dev):
+    from lightcompress_amd import gptq_core
+    H = torch.eye(256, device=dev)
+    H[200, 200] = -1.0
+    with pytest.raises(torch.linalg.LinAlgError):
+        gptq_core.inverse_cholesky_upper(H)
+
+
+@pytest.mark.parametrize('n', [1, 5, 16, 17, 100, 127, 128, -128])
+def test_chol_inv_tile(dev, n):
+    """lcq_chol_inv_tile on a strided view: L == torch cholesky, L X == I (fp32 accuracy).
+    n = -128: a 16-byte aligned 128-tile with 4-aligned leading dim (the float4 load path)."""
+    from lightcompress_amd import ops
+    vec = n < 0
+    n = abs(n)
+    g = torch.Generator().manual_seed(n)
+    A = torch.randn(n, 2 * n + 3, generator=g, dtype=torch.float64)
+    H = A @ A.t() / n + 0.1 * torch.eye(n, dtype=torch.float64)
+    if vec:
+        big = torch.full((n + 8, n + 8), float('nan'), device=dev)
+        view = big[4:4 + n, 4:4 + n]
+    else:
+        big = torch.full((n + 7, n + 9), float('nan'), device=dev)
+        view = big[3:3 + n, 5:5 + n]
+    view.copy_(H.float().to(dev))
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    X = ops.chol_inv_tile(view, info, L=view)
+    assert int(info.item()) == 0
+    Lref = torch.linalg.cholesky(H)
+    L = view.double().cpu()
+    assert ((L - Lref).abs().max() / Lref.abs().max()).item() < 1e-5
+    assert torch.equal(X.cpu(), X.cpu().tril())
+    eye = torch.eye(n, dtype=torch.float64)
+    assert (Lref @ X.double().cpu() - eye).abs().max().item() < 1e-4
+    assert torch.isnan(big[:3]).all() and torch.isnan(big[:, :3]).all()  # nothing outside the view
+    assert torch.isnan(big[3 + n + vec:]).all() and torch.isnan(big[:, 4 + n + 1:]).all()
+
+
+def test_chol_inv_tile_info(dev):
+    from lightcompress_amd import ops
+    H = torch.eye(100, device=dev)
+    H[40, 40] = -2.0
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.chol_inv_tile(H, info, row0=256)
+    assert int(info.item()) == 256 + 41
