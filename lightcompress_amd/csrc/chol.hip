@@ -118,7 +118,7 @@ __device__ __forceinline__ int factor_diag(float* a, float* zs, int c0, int cw, 
 // the panel (LOWER: A22 tile, lower part only) or X_P[:, k0..k0+3] (R tile); all b128
 // reads are issued before any FMA
 template <bool LOWER>
-__device__ __forceinline__ void rank16_tile(float* a, float* x, int c0, int i0, int k0, int n) {
+__device__ __forceinline__ void rank_tile(float* a, float* x, int c0, int i0, int k0, int n) {
   float4 pi[4][PW / 4], pk[4][PW / 4];
 #pragma unroll
   for (int u = 0; u < 4; ++u)
@@ -285,11 +285,11 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
       for (; t < T; t += NT) {
         int ti, tk;
         tri_tile(t, ti, tk);
-        rank16_tile<true>(a, x, c0, b0 + 4 * ti, b0 + 4 * tk, n);
+        rank_tile<true>(a, x, c0, b0 + 4 * ti, b0 + 4 * tk, n);
       }
       for (; t < T + nt * nc; t += NT) {
         const int t2 = t - T;
-        rank16_tile<false>(a, x, c0, b0 + 4 * (t2 / nc), 4 * (t2 % nc), n);
+        rank_tile<false>(a, x, c0, b0 + 4 * (t2 / nc), 4 * (t2 % nc), n);
       }
     }
     PROF_STAMP(5 + 4 * (c0 / PW))

@@ -100,34 +100,88 @@ class _linalg_backend:
 
 
 _TILE = 128
+_TRI_MIN = 1024  # triangular / symmetric products split while both halves stay >= this
 
 
 def _split(n):
     return max(_TILE, (n // 2 + _TILE - 1) // _TILE * _TILE)
 
 
-def _chol_inv_rec(A: torch.Tensor, info: torch.Tensor, row0: int = 0) -> torch.Tensor:
-    """A (square fp32 row-major view) <- its lower Cholesky factor L; returns L^-1.
+def _mm_lowT(A, Xl, out, alpha, beta):
+    """out = beta out + alpha A Xl^T, Xl lower-triangular: A Xl^T = [A1 X11^T, A1 X21^T + A2 X22^T]
+    -- the zero block skipped, 3/4 of the flops per split level."""
+    k = Xl.shape[0]
+    if k < 2 * _TRI_MIN:
+        out.addmm_(A, Xl.t(), beta=beta, alpha=alpha)
+        return
+    h = _split(k)
+    _mm_lowT(A[:, :h], Xl[:h, :h], out[:, :h], alpha, beta)
+    _mm_lowT(A[:, h:], Xl[h:, h:], out[:, h:], alpha, beta)
+    out[:, h:].addmm_(A[:, :h], Xl[h:, :h].t(), alpha=alpha)
 
-    [[A11, .], [A21, A22]]: L11 = chol(A11), X11 = L11^-1 (recursion); L21 = A21 X11^T;
-    A22 -= L21 L21^T; L22 = chol(A22), X22 = L22^-1 (recursion); X21 = -X22 L21 X11.
-    Tiles of <= 128 are factored and inverted in one workgroup (lcq_chol_inv_tile); everything
-    else is fp32 GEMM (fp32 MFMA, no reduced-precision path on gfx950)."""
+
+def _mm_low_right(A, Xl, out, alpha, beta):
+    """out = beta out + alpha A Xl, Xl lower: A Xl = [A1 X11 + A2 X21, A2 X22]."""
+    k = Xl.shape[0]
+    if k < 2 * _TRI_MIN:
+        out.addmm_(A, Xl, beta=beta, alpha=alpha)
+        return
+    h = _split(k)
+    _mm_low_right(A[:, :h], Xl[:h, :h], out[:, :h], alpha, beta)
+    out[:, :h].addmm_(A[:, h:], Xl[h:, :h], alpha=alpha)
+    _mm_low_right(A[:, h:], Xl[h:, h:], out[:, h:], alpha, beta)
+
+
+def _mm_low_left(Xl, B, out, alpha, beta):
+    """out = beta out + alpha Xl B, Xl lower: Xl B = [X11 B1; X21 B1 + X22 B2]."""
+    k = Xl.shape[0]
+    if k < 2 * _TRI_MIN:
+        out.addmm_(Xl, B, beta=beta, alpha=alpha)
+        return
+    h = _split(k)
+    _mm_low_left(Xl[:h, :h], B[:h], out[:h], alpha, beta)
+    _mm_low_left(Xl[h:, h:], B[h:], out[h:], alpha, beta)
+    out[h:].addmm_(Xl[h:, :h], B[:h], alpha=alpha)
+
+
+def _syrk_lower(L, C, alpha):
+    """Lower part of C += alpha L L^T (the upper part of C is never read by the recursion;
+    diagonal blocks are updated whole)."""
+    m = C.shape[0]
+    if m < 2 * _TRI_MIN:
+        C.addmm_(L, L.t(), alpha=alpha)
+        return
+    h = _split(m)
+    _syrk_lower(L[:h], C[:h, :h], alpha)
+    C[h:, :h].addmm_(L[h:], L[:h].t(), alpha=alpha)
+    _syrk_lower(L[h:], C[h:, h:], alpha)
+
+
+def _chol_inv_rec(A: torch.Tensor, X: torch.Tensor, info: torch.Tensor, row0: int = 0):
+    """X (zeroed square fp32 view) <- L^-1 for the lower Cholesky factor L of A (square fp32
+    row-major view, lower part read; consumed as workspace).
+
+    [[A11, .], [A21, A22]]: X11 = chol(A11)^-1 (recursion); L21 = A21 X11^T; A22 -= L21 L21^T;
+    X22 = chol(A22)^-1 (recursion); X21 = -X22 (L21 X11). Tiles of <= 128 are factored and
+    inverted in one workgroup (lcq_chol_inv_tile); everything else is fp32 GEMM on hipBLASLt
+    (127-145 TF/s at these shapes), written in place through strided views, with the
+    triangular / symmetric structure skipped block-wise (_mm_* / _syrk_lower)."""
     n = A.shape[0]
     if n <= _TILE:
-        return ops.chol_inv_tile(A, info, row0)
+        ops.chol_inv_tile(A, info, row0, out=X)
+        return
     n1 = _split(n)
-    A11, A21, A22 = A[:n1, :n1], A[n1:, :n1], A[n1:, n1:]
-    X11 = _chol_inv_rec(A11, info, row0)
-    L21 = A21 @ X11.t()
-    A21.copy_(L21)
-    A22.addmm_(L21, L21.t(), alpha=-1.0)
-    X22 = _chol_inv_rec(A22, info, row0 + n1)
-    X = torch.zeros((n, n), dtype=torch.float32, device=A.device)
-    X[:n1, :n1] = X11
-    X[n1:, n1:] = X22
-    X[n1:, :n1] = -(X22 @ (L21 @ X11))
-    return X
+    A21, A22 = A[n1:, :n1], A[n1:, n1:]
+    X11, X22 = X[:n1, :n1], X[n1:, n1:]
+    _chol_inv_rec(A[:n1, :n1], X11, info, row0)
+    L21 = torch.empty_like(A21)
+    _mm_lowT(A21, X11, L21, 1.0, 0.0)
+    _syrk_lower(L21, A22, -1.0)
+    _chol_inv_rec(A22, X22, info, row0 + n1)
+    T = torch.empty_like(A21)
+    _mm_low_right(L21, X11, T, 1.0, 0.0)
+    del L21
+    _mm_low_left(X22, T, X[n1:, :n1], -1.0, 0.0)
 
 
 def inverse_cholesky_upper(H: torch.Tensor) -> torch.Tensor:
@@ -135,7 +189,9 @@ def inverse_cholesky_upper(H: torch.Tensor) -> torch.Tensor:
     Hr = H.flip(0, 1).contiguous()
     del H
     info = torch.zeros(1, dtype=torch.int32, device=Hr.device)
-    X = _chol_inv_rec(Hr, info)
+    X = torch.zeros_like(Hr)
+    _chol_inv_rec(Hr, X, info)
+    del Hr
     bad = int(info.item())
     if bad:
         raise torch.linalg.LinAlgError(

@@ -179,18 +179,21 @@ def _ld(t: torch.Tensor) -> int:
 
 
 def chol_inv_tile(A: torch.Tensor, info: torch.Tensor, row0: int = 0,
-                  L: torch.Tensor | None = None) -> torch.Tensor:
+                  L: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """Returns L^-1 for the lower Cholesky factor L of A (<= 128 x 128 fp32 view, unit column
     stride); L itself is written to `L` when given (may be A). info (int32, 1 element) receives
-    row0 + the first non-positive pivot (1-based) on failure."""
+    row0 + the first non-positive pivot (1-based) on failure. `out` (a view like A) receives
+    L^-1 in place of a new tensor."""
     if A.dtype != torch.float32 or A.shape[0] != A.shape[1]:
         raise ValueError('chol_inv_tile expects a square fp32 tile')
-    if L is not None and (L.shape != A.shape or L.dtype != torch.float32):
-        raise ValueError('L must match A')
-    X = torch.empty((A.shape[0], A.shape[0]), dtype=torch.float32, device=A.device)
+    for t in (L, out):
+        if t is not None and (t.shape != A.shape or t.dtype != torch.float32):
+            raise ValueError('L / out must match A')
+    X = torch.empty((A.shape[0], A.shape[0]), dtype=torch.float32, device=A.device) \
+        if out is None else out
     N.call('lcq_chol_inv_tile', A.data_ptr(), _ld(A), A.shape[0],
            0 if L is None else L.data_ptr(), 0 if L is None else _ld(L),
-           N.ptr(X), X.shape[1], N.ptr(info), row0, N.stream_of(A))
+           X.data_ptr(), _ld(X), N.ptr(info), row0, N.stream_of(A))
     return X
 
 

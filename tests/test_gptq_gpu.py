@@ -176,7 +176,7 @@ def test_trailing_update(dev, rows, ic, c0, K, c2):
     assert torch.equal(part, out[h:])
 
 
-@pytest.mark.parametrize('n', [100, 128, 300, 1000, 4096])
+@pytest.mark.parametrize('n', [100, 128, 300, 1000, 4096, 4500])
 def test_inverse_cholesky_upper(dev, n):
     """Recursive lcq factorisation: U^T U = H^-1 with U upper (fp64 check), equal to the
     reference chain cholesky -> cholesky_inverse -> cholesky(upper) to fp32 accuracy."""
