@@ -160,8 +160,11 @@ def pmc_traffic(leg, kernel):
     if not files:
         return None, None
     d = json.loads(files[-1].read_text())
-    k = d.get('kernels', {}).get(kernel)
-    return (k['hbm_bytes'] if k else None), str(files[-1].relative_to(ROOT))
+    names = kernel if isinstance(kernel, tuple) else (kernel,)   # a tuple: one call's kernels
+    ks = [d.get('kernels', {}).get(k) for k in names]
+    if not all(ks):
+        return None, str(files[-1].relative_to(ROOT))
+    return sum(k['hbm_bytes'] for k in ks), str(files[-1].relative_to(ROOT))
 
 
 def deploy_block(algo, model, block, idx):
@@ -354,9 +357,9 @@ def bench_fp8(args, rank, world, dev):
         # algorithmic bytes per expert linear: 1 B fp8 read + 1 B fp8 written per element
         # (+ fp32 block scales); the amax pass re-reads the 1 B codes (counted as overhead)
         gbs = elems * 2.0 * t['launches'] / (t['total_ms'] * 1e-3) / 1e9
-        traffic, src = pmc_traffic('fp8', 'k_requant_blockfp8_many')
-        out['roofline'] = {'kernel': 'lcq_fp8_block_to_tensor_many (k_absmax_blockfp8_many + '
-                                     'k_requant_blockfp8_many)', 'bound': 'hbm',
+        traffic, src = pmc_traffic('fp8', ('k_bmax16_many', 'k_requant16_many'))
+        out['roofline'] = {'kernel': 'lcq_fp8_block_to_tensor_many (k_bmax16_many + '
+                                     'k_requant16_many)', 'bound': 'hbm',
                            'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                            'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic,
                            'traffic_source': src, 'avg_launch_ms': round(t['avg_ms'], 4)}

@@ -200,9 +200,13 @@ int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t cols, int64_t
  * torch's native cast (c10 Float8_e4m3fn / Float8_e5m2, RNE); the reference's qtorch
  * float_quantize step is absent from this image, so that step is parity-unpinned.
  * ------------------------------------------------------------------------------------- */
-/* max |x| over n elements -> out (one fp32 on device; zeroed by the call). Per-tensor
- * get_minmax_range (quant.py:133-135): max(|torch.max|, |torch.min|) == max|x|. */
-int lcq_absmax(const void* x, int x_dtype, int64_t n, void* out, void* stream);
+/* Scratch (fp32 count) the per-tensor max reductions take: one partial per workgroup. */
+#define LCQ_FP8_PARTIALS 256
+
+/* max |x| over n elements -> out (one fp32 on device). Per-tensor get_minmax_range
+ * (quant.py:133-135): max(|torch.max|, |torch.min|) == max|x|. workspace: LCQ_FP8_PARTIALS
+ * device fp32 of scratch. */
+int lcq_absmax(const void* x, int x_dtype, int64_t n, void* out, void* workspace, void* stream);
 
 /* Dynamic FP8 quant over groups of `group` consecutive elements of x [rows, cols]
  * (per_group / per_channel / per_token; kernel.py act_quant = group 128, ct F32, clamp 0,
@@ -240,7 +244,7 @@ int lcq_fp8_dequant_blocks(const void* codes, int fmt, int64_t M, int64_t N, int
 /* Deploy of a block-fp8 checkpoint weight to per-tensor fp8 (module_utils.py:917-922 +
  * quant.py:1191-1221): w = bf16(float(code) * scales_inv[block]) (weight_cast_to_bf16) kept in
  * registers, then per-tensor FloatQuantizer real quant of w (bf16 compute, fp32 scale).
- * amax_ws: one device fp32 of scratch. scale_out: one fp32. Bit-identical to the composed
+ * amax_ws: LCQ_FP8_PARTIALS device fp32 of scratch. scale_out: one fp32. Bit-identical to the composed
  * lcq_fp8_dequant_blocks -> lcq_absmax -> lcq_fp8_quant chain at 3 instead of 8 B/element. */
 int lcq_fp8_block_to_tensor(const void* codes, int fmt_in, int64_t M, int64_t N, int block,
                             const void* scales_inv, int fmt_out, float qmax, float clamp_min,
@@ -250,7 +254,8 @@ int lcq_fp8_block_to_tensor(const void* codes, int fmt_in, int64_t M, int64_t N,
 /* Batched lcq_fp8_block_to_tensor over n weights (e.g. the 257 x 3 expert linears of a
  * DeepSeek-V3 MoE layer) in one launch pair. descs: device array of n records
  * {const uint8_t* codes; const float* scales_inv; uint8_t* codes_out; int64_t M, N} (40 B);
- * max_elems = the largest M*N; amax_ws: n device fp32; scales_out: n fp32. */
+ * max_elems = the largest M*N; amax_ws: n * LCQ_FP8_PARTIALS device fp32 of scratch
+ * (per-workgroup partial maxima, no atomics); scales_out: n fp32. */
 int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t max_elems, int fmt_in,
                                  int block, int fmt_out, float qmax, float clamp_min,
                                  int add_zero, void* amax_ws, void* scales_out, void* stream);

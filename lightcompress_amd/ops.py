@@ -313,12 +313,17 @@ def fp8_dtype(bit: str) -> torch.dtype:
     return _FP8[bit]
 
 
+FP8_PARTIALS = 256  # LCQ_FP8_PARTIALS (include/lcq.h): scratch fp32 per per-tensor max
+
+
 def absmax(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """max |x| as a device fp32 scalar (shape [1])."""
     x = x.contiguous()
     if out is None:
         out = torch.empty(1, dtype=torch.float32, device=x.device)
-    N.call('lcq_absmax', N.ptr(x), N.dt(x.dtype), x.numel(), N.ptr(out), N.stream_of(x))
+    ws = torch.empty(FP8_PARTIALS, dtype=torch.float32, device=x.device)
+    N.call('lcq_absmax', N.ptr(x), N.dt(x.dtype), x.numel(), N.ptr(out), N.ptr(ws),
+           N.stream_of(x))
     return out
 
 
@@ -433,7 +438,7 @@ def fp8_block_to_tensor(codes: torch.Tensor, scales_inv: torch.Tensor, block: in
     codes = codes.contiguous()
     scales_inv = scales_inv.contiguous().float()
     M, Nn = codes.shape
-    ws = torch.empty(1, dtype=torch.float32, device=codes.device)
+    ws = torch.empty(FP8_PARTIALS, dtype=torch.float32, device=codes.device)
     out = torch.empty((M, Nn), dtype=fp8, device=codes.device)
     s = torch.empty(1, dtype=torch.float32, device=codes.device)
     qmax = fp8_max(fp8) if qmax is None else float(qmax)
@@ -461,7 +466,7 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
             raise ValueError('N must be a multiple of 8')
         rec += [N.ptr(c), N.ptr(s), N.ptr(o), M, Nn]
     descs = torch.tensor(rec, dtype=torch.int64).to(dev, non_blocking=False)
-    ws = torch.empty(n, dtype=torch.float32, device=dev)
+    ws = torch.empty(n * FP8_PARTIALS, dtype=torch.float32, device=dev)
     sc = torch.empty(n, dtype=torch.float32, device=dev)
     qmax = fp8_max(fp8) if qmax is None else float(qmax)
     N.call('lcq_fp8_block_to_tensor_many', n, N.ptr(descs), max(c.numel() for c in codes),

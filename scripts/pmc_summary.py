@@ -15,7 +15,8 @@ KEYS = {'hipblaslt_gemm': 'Cijk_', 'k_syrk256': 'k_syrk256', 'k_auto_clip': 'k_a
         'k_sqdiff_p1': 'k_sqdiff_p1', 'k_gptq_block': 'k_gptq_block',
         'k_gptq_trailing': 'k_gptq_trailing', 'k_xt_pack': 'k_xt_pack',
         'k_requant_blockfp8_many': 'k_requant_blockfp8_many',
-        'k_absmax_blockfp8_many': 'k_absmax_blockfp8_many'}
+        'k_absmax_blockfp8_many': 'k_absmax_blockfp8_many',
+        'k_bmax16_many': 'k_bmax16_many', 'k_requant16_many': 'k_requant16_many'}
 
 
 def load(path):

@@ -154,3 +154,67 @@ def test_block_fp8_to_tensor_batched_equals_single(dev):
     for i, (c, s) in enumerate(zip(cs, ss)):
         oc, os_ = ops.fp8_block_to_tensor(c, s, 128)
         assert torch.equal(bits(outs[i]), bits(oc)) and scales[i].item() == os_.item()
+
+
+def _random_block_fp8(shape, fin, seed, dev, nan_free=True):
+    """Random code bytes (every finite code of ``fin`` reachable) + random-sign block scales."""
+    g = torch.Generator().manual_seed(seed)
+    M, N = shape
+    b = torch.randint(0, 256, (M, N), generator=g, dtype=torch.int32).to(torch.uint8)
+    if nan_free:
+        v = b.view(fin).float()
+        b[~torch.isfinite(v)] = 0x11
+    s = torch.randn((M + 127) // 128, (N + 127) // 128, generator=g) * 1e-3
+    return b.view(fin).to(dev), s.to(dev)
+
+
+@pytest.mark.parametrize('fin', [torch.float8_e4m3fn, torch.float8_e5m2])
+@pytest.mark.parametrize('fout', [torch.float8_e4m3fn, torch.float8_e5m2])
+def test_block_fp8_to_tensor_many_random_codes(dev, fin, fout):
+    """The 16-codes-per-lane path of lcq_fp8_block_to_tensor_many (byte-max amax, hardware
+    OCP conversions) equals the oracle for every finite input code, both formats, on
+    expert-sized and ragged tensors (ragged ones take the row-walk fallback)."""
+    from lightcompress_amd import ops
+    shapes = [(2048, 7168), (7168, 2048), (200, 264), (384, 136)]
+    cs, ss = zip(*[_random_block_fp8(sh, fin, 11 + i, dev) for i, sh in enumerate(shapes)])
+    outs, scales = ops.fp8_block_to_tensor_many(list(cs), list(ss), 128, fout)
+    bit = 'e4m3' if fout == torch.float8_e4m3fn else 'e5m2'
+    for i, (c, s) in enumerate(zip(cs, ss)):
+        _, oc, os_ = O.fp8_qdq(O.weight_cast_to_bf16(c.cpu(), s.cpu()), bit, 'per_tensor')
+        assert torch.equal(bits(outs[i]), oc.view(torch.uint8)), shapes[i]
+        assert scales[i].item() == os_.item()
+        sc, ssc = ops.fp8_block_to_tensor(c, s, 128, fout)
+        assert torch.equal(bits(outs[i]), bits(sc)) and scales[i].item() == ssc.item()
+
+
+@pytest.mark.parametrize('fout,qmax', [(torch.float8_e4m3fn, 1000.0), (torch.float8_e5m2, 90000.0)])
+def test_block_fp8_to_tensor_many_overflow_band(dev, fout, qmax):
+    """A qmax above the format's range pushes quotients into c10's overflow band (e4m3fn
+    (464, 480) -> NaN code, e5m2 -> inf): the fast path's software-encoder fallback must give
+    the same codes as the generic path."""
+    from lightcompress_amd import ops
+    cs, ss = zip(*[_random_block_fp8((512, 1024), torch.float8_e4m3fn, 40 + i, dev)
+                   for i in range(3)])
+    outs, scales = ops.fp8_block_to_tensor_many(list(cs), list(ss), 128, fout, qmax=qmax)
+    for i, (c, s) in enumerate(zip(cs, ss)):
+        sc, ssc = ops.fp8_block_to_tensor(c, s, 128, fout, qmax=qmax)
+        assert torch.equal(bits(outs[i]), bits(sc)) and scales[i].item() == ssc.item()
+
+
+@pytest.mark.parametrize('block', [64, 128])
+@pytest.mark.parametrize('shape', [(300, 520), (1024, 2048)])
+def test_block_fp8_to_tensor_single_vs_oracle(dev, block, shape):
+    """lcq_fp8_block_to_tensor (one weight, descriptor by value) on both the 16-code path
+    (block 128) and the row-walk path (other block sizes), vs the oracle."""
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(block + shape[0])
+    M, N = shape
+    b = torch.randint(0, 256, (M, N), generator=g, dtype=torch.int32).to(torch.uint8)
+    b[~torch.isfinite(b.view(torch.float8_e4m3fn).float())] = 0x22
+    s = torch.rand((M + block - 1) // block, (N + block - 1) // block, generator=g) * 1e-2
+    c = b.view(torch.float8_e4m3fn)
+    oc, os_ = ops.fp8_block_to_tensor(c.to(dev), s.to(dev), block)
+    _, rc, rs = O.fp8_qdq(O.weight_cast_to_bf16(c, s, block), 'e4m3', 'per_tensor')
+    assert torch.equal(bits(oc), rc.view(torch.uint8)) and os_.item() == rs.item()
+    am = ops.absmax(O.weight_cast_to_bf16(c, s, block).to(dev))
+    assert am.item() == O.weight_cast_to_bf16(c, s, block).float().abs().max().item()
