@@ -276,6 +276,10 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         GPTQ narrows this to the Hessian owners)."""
         return set(names)
 
+    # cache_input_hook reads only the module's input (GPTQ's add_batch, gptq.py:245-295): the
+    # forward that exists to capture inputs stops BEFORE the last needed module runs
+    hook_needs_output = True
+
     def _capture_hook(self, m, x, y, name, feat_dict):
         self.cache_input_hook(m, x, y, name=name, feat_dict=feat_dict)
         pending = getattr(self, '_capture_pending', None)
@@ -283,6 +287,13 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
             pending.discard(name)
             if not pending:
                 raise _StopForward
+
+    def _capture_pre_hook(self, m, x, name, feat_dict):
+        pending = getattr(self, '_capture_pending', None)
+        if pending is not None and pending == {name}:
+            self.cache_input_hook(m, x, None, name=name, feat_dict=feat_dict)
+            pending.discard(name)
+            raise _StopForward   # the module's own output is never used
 
     def _call_block(self, block, x, kw, stop_after):
         self._capture_pending = set(stop_after) if stop_after else None
@@ -348,9 +359,14 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         if self.data_free:
             return []
         self._hooked_names = list(modules)
-        return [m.register_forward_hook(functools.partial(self._capture_hook, name=n,
-                                                          feat_dict=input_feat))
+        handles = [m.register_forward_hook(functools.partial(self._capture_hook, name=n,
+                                                             feat_dict=input_feat))
+                   for n, m in modules.items()]
+        if not self.hook_needs_output:
+            handles += [m.register_forward_pre_hook(functools.partial(
+                self._capture_pre_hook, name=n, feat_dict=input_feat))
                 for n, m in modules.items()]
+        return handles
 
     def run(self, block, input_feat, handles):
         if not self.data_free:

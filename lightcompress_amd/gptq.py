@@ -84,10 +84,12 @@ class GPTQ(BaseBlockwiseQuantization):
         """Only the Hessian owners' inputs are consumed (the forward output is discarded)."""
         return {n for n in names if self.layers_cache.get(n, {}).get('owner', False)}
 
+    hook_needs_output = False  # add_batch never reads `out` (gptq.py:253-295)
+
     @torch.no_grad()
     def cache_input_hook(self, m, inp, out, name, feat_dict):
         if isinstance(m, _LINEAR_TYPES):
-            self.add_batch(m, name, inp[0].data, out.data)
+            self.add_batch(m, name, inp[0].data, None if out is None else out.data)
 
     @torch.no_grad()
     def add_batch(self, layer, name, inp, out):
