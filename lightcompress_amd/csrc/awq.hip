@@ -66,6 +66,7 @@ __global__ void __launch_bounds__(1024) k_awq_scales(const void* xmean, int64_t 
     s = fmaxf(s, lo);
     mx = fmaxf(mx, s);
     mn = fminf(mn, s);
+    st1<DT>(out, j, s);  // s is a DT value: parked losslessly in out for the second pass
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
@@ -85,12 +86,7 @@ __global__ void __launch_bounds__(1024) k_awq_scales(const void* xmean, int64_t 
     mn = fminf(mn, red[1][i]);
   }
   const float d = rnd<DT>(sqrtf(rnd<DT>(mx * mn)));
-  for (int64_t j = threadIdx.x; j < c; j += blockDim.x) {
-    const float xv = ld1<DT>(xmean, j);
-    float s = rnd<DT>((float)pow((double)xv, (double)r));
-    s = fmaxf(s, lo);
-    st1<DT>(out, j, s / d);
-  }
+  for (int64_t j = threadIdx.x; j < c; j += blockDim.x) st1<DT>(out, j, ld1<DT>(out, j) / d);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -151,11 +147,14 @@ __global__ void __launch_bounds__(256) k_sqdiff_p1(const void* a, const void* b,
   if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ void k_sqdiff_p2(const double* part, int nparts, int64_t n, float* out, int slot) {
-  if (threadIdx.x != 0) return;
+// one wave: lane l sums parts l, l+64, ... in order, then a fixed xor tree (deterministic)
+__global__ void __launch_bounds__(64) k_sqdiff_p2(const double* part, int nparts, int64_t n,
+                                                  float* out, int slot) {
   double s = 0.0;
-  for (int i = 0; i < nparts; ++i) s += part[i];
-  out[slot] = (float)s / (float)n;
+  for (int i = threadIdx.x; i < nparts; i += 64) s += part[i];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (threadIdx.x == 0) out[slot] = (float)s / (float)n;
 }
 
 // ----------------------------------------------------------------------------------------
