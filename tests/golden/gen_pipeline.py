@@ -1,0 +1,163 @@
+"""End-to-end pipeline goldens: the REAL reference's ``run_block_loop`` + ``deploy('fake_quant')``
+on a tiny random Llama (2 decoder layers), CPU, in the build container only.
+
+    python tests/golden/gen_pipeline.py
+
+Pins what the subset-level fixtures cannot: the block driver (SURVEY.md §8c "Python harness
+counterparts"): block order, subset order and skip rules (o_proj skipped under GQA,
+awq.py:338-351; q/k clip skip, auto_clip.py:56-60), GPTQ's true_sequential rehook Hessians
+from fake-quantized predecessors (base_blockwise_quantization.py:498-526), quant_out
+(:436-462) and AWQ's input-feature rescaling (:891-897).
+
+Writes ``tests/golden/pipeline_llama/`` (HF config + safetensors of the random model, so the
+test loads the very same weights through the Llama adapter) and ``pipe_<algo>.npz`` with the
+calibration token ids and every deployed linear weight of both blocks. Calibration data are
+token ids fed through the reference's own Catcher (base_model.py:279-336); the embedding table
+has log-normal per-channel magnitudes so that AWQ's scale search has outlier channels to find.
+"""
+from __future__ import annotations
+
+import copy
+import shutil
+import sys
+import types
+from pathlib import Path
+
+import torch
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE))
+import _ref_import as R  # noqa: E402
+import fixtures as F  # noqa: E402
+
+from pipeline_configs import CONFIGS, MODEL_DIR  # noqa: E402
+
+
+class ED(dict):
+    """EasyDict stand-in (easydict is not installed): attribute access, nested."""
+
+    def __init__(self, d=None, **kw):
+        super().__init__()
+        for k, v in dict(d or {}, **kw).items():
+            self[k] = v
+
+    def __setitem__(self, k, v):
+        if isinstance(v, dict) and not isinstance(v, ED):
+            v = ED(v)
+        super().__setitem__(k, v)
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+def make_model():
+    from transformers import LlamaConfig, LlamaForCausalLM
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                      num_key_value_heads=2, num_hidden_layers=2, vocab_size=128,
+                      max_position_embeddings=512, rms_norm_eps=1e-5, tie_word_embeddings=False)
+    cfg._attn_implementation = 'sdpa'
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(cfg)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if p.dim() == 2:
+                p.normal_(0, 0.02, generator=g)
+            else:
+                p.uniform_(0.8, 1.2, generator=g)
+        emb = m.model.embed_tokens.weight
+        emb.copy_(torch.randn(emb.shape, generator=g) *
+                  torch.exp(torch.randn(emb.shape[1], generator=g) * 0.8))
+    m = m.to(torch.bfloat16)
+    if MODEL_DIR.exists():
+        shutil.rmtree(MODEL_DIR)
+    m.save_pretrained(MODEL_DIR)
+    return cfg
+
+
+def run_reference(name, spec):
+    import llmc.models.base_model as bm
+    from llmc.models.llama import Llama
+    bm.BaseModel.build_tokenizer = lambda self: setattr(self, 'tokenizer', None)
+    if spec['quant']['method'] == 'GPTQ':
+        import llmc.compression.quantization.gptq as mod
+        algo_cls = mod.GPTQ
+    elif spec['quant']['method'] == 'Awq':
+        import llmc.compression.quantization.awq as mod
+        algo_cls = mod.Awq
+    else:
+        import llmc.compression.quantization.rtn as mod
+        algo_cls = mod.RTN
+    config = ED({'model': {'type': 'Llama', 'path': str(MODEL_DIR), 'torch_dtype': 'torch.bfloat16'},
+                 'quant': dict(copy.deepcopy(spec['quant']), modality='language')})
+    if spec['calib']:
+        config['calib'] = dict(spec['calib'])
+    model = Llama(config)
+    calib = spec['calib']
+    ids = None
+    if calib is None:
+        algo = algo_cls(model, config.quant, None, None, config)
+    else:
+        g = torch.Generator().manual_seed(7)
+        ids = torch.randint(0, model.model_config.vocab_size,
+                            (calib['n_samples'], calib['seq_len']), generator=g)
+        if calib['bs'] == -1:
+            batches = [{'input_ids': ids}]
+        else:
+            batches = [{'input_ids': ids[i:i + 1]} for i in range(ids.shape[0])]
+        model.collect_first_block_input(batches, None)
+        algo = algo_cls(model, config.quant, model.get_first_block_input(),
+                        model.get_padding_mask(), config)
+    diag = {}
+    if spec['quant']['method'] == 'GPTQ':   # diagnostics: each layer's finished Hessian
+        orig = algo_cls.initialize_qparams_and_prepare_weights
+
+        def snap(self, layer, lname, _o=orig):
+            diag[f'H_b{self.block_idx}__{lname.replace(".", "__")}'] = \
+                self.layers_cache[lname]['H'].clone()
+            return _o(self, layer, lname)
+        algo.initialize_qparams_and_prepare_weights = types.MethodType(snap, algo)
+    elif spec['quant']['method'] == 'Awq':  # diagnostics: each subset's losses + chosen scales
+        orig = algo_cls.search_scale_subset
+        orig_loss = algo_cls.calculate_loss
+        seen = []
+
+        def rec(self, org_out, out, _o=orig_loss):
+            v = _o(self, org_out, out)
+            seen.append(float(v))
+            return v
+
+        def snap(self, *a, _o=orig, **k):
+            seen.clear()
+            best = _o(self, *a, **k)
+            n = len([d for d in diag if d.startswith(f'S_b{self.block_idx}')])
+            diag[f'S_b{self.block_idx}__{n}'] = best.clone()
+            diag[f'L_b{self.block_idx}__{n}'] = torch.tensor(seen, dtype=torch.float64)
+            return best
+        algo.search_scale_subset = types.MethodType(snap, algo)
+        algo.calculate_loss = types.MethodType(rec, algo)
+    algo.run_block_loop()
+    algo.deploy('fake_quant')
+    if diag:
+        F.save(f'pipe_{name}_diag', **diag)
+    out = {'ids': ids if ids is not None else torch.zeros(0, dtype=torch.int64)}
+    for bi, block in enumerate(model.get_blocks()):
+        for ln, lin in model.get_block_linears(block).items():
+            out[f'b{bi}__{ln.replace(".", "__")}'] = lin.weight.data.clone()
+    F.save(f'pipe_{name}', **out)
+    print(f'pipe_{name}: {len(out) - 1} deployed linears')
+
+
+if __name__ == '__main__':
+    R.install()
+    R.init_dist()
+    make_model()
+    which = sys.argv[1:] or list(CONFIGS)
+    for k in which:
+        run_reference(k, CONFIGS[k])
