@@ -17,9 +17,9 @@ What "match" means here (SURVEY.md §8c tiers):
   codes perturb them (measured 1e-4 .. 2e-2). That is the reference's own noise floor: its
   Hessians move by 2.5e-3 (b0 o_proj), 1.0e-2 (b0 down), 1.4e-2 / 2.1e-2 (b1 o / down) when
   the last mantissa bit of 0.1 % of its first-block inputs flips (measured on torch-CPU); a
-  wrong driver semantic, e.g. float instead of fake-quant predecessors, moves them by several %. Deployed first-subset weights >= 99.5 %
-  bit-equal; GPTQ's error feedback spreads every flip along its row, so later layers are
-  compared through their Hessians, not element-wise.
+  wrong driver semantic, e.g. float instead of fake-quant predecessors, moves them by
+  several %. Deployed first-subset weights >= 99.5 % bit-equal; GPTQ's error feedback spreads
+  every flip along its row, so later layers are compared through their Hessians.
 """
 import pytest
 import torch
