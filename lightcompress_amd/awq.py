@@ -16,6 +16,7 @@ import torch.nn as nn
 
 from . import ops
 from .base_blockwise_quantization import BaseBlockwiseQuantization, is_norm
+from .llama import _mkey
 from .module_utils import FakeQuantLinear
 from .registry import ALGO_REGISTRY
 
@@ -35,6 +36,73 @@ class Awq(BaseBlockwiseQuantization):
                                       'device path yet')
         self.n_grid = 20
         self.last_search = {}
+        self._org_cache = {}
+        self._org_capture_active = False
+        self.org_reuse_stats = {'reused': 0, 'recomputed': 0}
+        self.reuse_org = True
+
+    # -- original inspect outputs from the block's own forward ------------------------------
+    # search_scale_subset starts from the inspect module's output on the captured input
+    # (awq.py:204-206: one extra forward of self_attn / mlp / down_proj per subset). The
+    # block's capture forward already ran every inspect module on exactly that input and
+    # batch (quant_out False: the forward that feeds the next block; True: the capture
+    # forward, then run to completion instead of stopping after the last input is seen), so
+    # its outputs are kept: same modules, kernels and shapes -> bit-identical, one forward
+    # per subset saved. An output is used only if the module's linear weights are unchanged
+    # since the capture (identity + storage + in-place version) and the search runs the
+    # whole batch at once (awq_bs unset); otherwise the forward is recomputed.
+    class _EndCapture:
+        def __init__(self, algo):
+            self.algo = algo
+
+        def remove(self):
+            self.algo._org_capture_active = False
+
+    def run(self, block, input_feat, handles):
+        self._org_cache = {}
+        extra = []
+        if self.trans and not self.data_free:
+            extra = self._hook_org_outputs(block) + [Awq._EndCapture(self)]
+            self._org_capture_active = True
+        try:
+            super().run(block, input_feat, list(handles) + extra)
+        finally:
+            self._org_cache = {}
+            self._org_capture_active = False
+
+    def capture_names(self, names):
+        if self._org_capture_active:
+            return set()  # run the capture forward to completion: its outputs are kept
+        return super().capture_names(names)
+
+    def _hook_org_outputs(self, block):
+        handles = []
+        for subset in self.model.get_subsets_in_block(block):
+            m = subset.get('inspect')
+            if m is None or not subset.get('do_trans', True):
+                continue
+            lins = [x for x in m.modules() if isinstance(x, (nn.Linear, FakeQuantLinear))]
+
+            def hook(mod, inp, out, _lins=lins):
+                if not self._org_capture_active:
+                    return
+                if id(mod) in self._org_cache:  # called twice in one forward: do not reuse
+                    self._org_cache[id(mod)] = None
+                    return
+                o = out[0] if isinstance(out, tuple) else out
+                self._org_cache[id(mod)] = (o.detach(), _mkey(*_lins), _lins)
+            handles.append(m.register_forward_hook(hook))
+        return handles
+
+    def _org_output(self, x, inspect_module, kwargs):
+        hit = getattr(self, '_org_cache', {}).pop(id(inspect_module), None)
+        if (getattr(self, 'reuse_org', False) and hit is not None and self._bs == x.shape[0] and hit[1] == _mkey(*hit[2])
+                and tuple(hit[0].shape[:-1]) == tuple(x.shape[:-1])):
+            self.org_reuse_stats['reused'] += 1
+            return hit[0]
+        if hasattr(self, 'org_reuse_stats'):
+            self.org_reuse_stats['recomputed'] += 1
+        return self.inspect_module_forward(x, inspect_module, kwargs)
 
     # -- awq.py:74-108 ----------------------------------------------------------------------
     def get_act_scale(self, x):
@@ -82,7 +150,7 @@ class Awq(BaseBlockwiseQuantization):
         qbufs = [torch.empty_like(w) for w in orig_w]
         x_tmp = torch.empty_like(x)
         x_mean = self.get_act_scale(x)
-        org_out = self.inspect_module_forward(x, inspect_module, kwargs)
+        org_out = self._org_output(x, inspect_module, kwargs)
         all_scales = torch.empty((self.n_grid, x.shape[-1]), dtype=x.dtype, device=x.device)
         losses = ops.LossBuffer(self.n_grid, x.device)
         try:

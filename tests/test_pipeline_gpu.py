@@ -90,3 +90,36 @@ def test_rtn_autoawq_deploy(dev):
     algo.deploy('autoawq_quant')
     m = model.blocks[1].self_attn.o_proj
     assert m.qweight.shape == (256, 256 // 8) and m.scales.dtype == torch.float16
+
+
+@pytest.mark.parametrize('quant_out', [False, True])
+def test_awq_org_output_reuse_is_bit_identical(dev, quant_out):
+    """Reusing the capture forward's inspect outputs as the search's original outputs gives
+    the same losses, scales and deployed weights as recomputing them (awq.py:204-206)."""
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.utils import load_config
+    import copy
+    cfg = copy.deepcopy(AWQ_CFG)
+    cfg['quant']['quant_out'] = quant_out
+    results = []
+    for reuse in (True, False):
+        model = tiny_model(dev)
+        algo = build_algo(model, load_config(copy.deepcopy(cfg)), calib(model))
+        algo.reuse_org = reuse
+        losses = []
+        orig = algo.search_scale_subset
+
+        def rec(*a, _o=orig, **k):
+            r = _o(*a, **k)
+            losses.append(list(algo.last_search['losses']))
+            return r
+        algo.search_scale_subset = rec
+        algo.run_block_loop()
+        algo.deploy('fake_quant')
+        w = [m.weight.detach().clone() for b in model.blocks
+             for m in model.get_block_linears(b).values()]
+        results.append((losses, w, dict(algo.org_reuse_stats)))
+    (l1, w1, st1), (l0, w0, st0) = results
+    assert st1['reused'] == 3 * len(w1) // 7 and st0['reused'] == 0
+    assert l1 == l0
+    assert all(torch.equal(a.view(torch.int16), b.view(torch.int16)) for a, b in zip(w1, w0))
