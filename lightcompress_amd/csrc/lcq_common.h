@@ -44,11 +44,19 @@ inline bool is_code_dt(int dt) { return dt == LCQ_I8 || dt == LCQ_U8 || dt == LC
 // rounding to the compute dtype: every reference torch op on a bf16/fp16 tensor computes in
 // fp32 and rounds its result (RNE) to the tensor dtype; we apply the same after each op.
 // ----------------------------------------------------------------------------------------
+// RNE to bf16 and back: v_cvt_pk_bf16_f32 (gfx950; a NaN stays a NaN, payload not kept)
 __device__ __forceinline__ float bf16_rne(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return __uint_as_float((u | 0x00400000u) & 0xffff0000u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return __uint_as_float(u & 0xffff0000u);
+  const __bf16 h = (__bf16)f;
+  return __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, h) << 16);
+}
+
+// IEEE quotient a / b from rb = RN(1 / b) (Markstein: the residual a - b*q0 is exact in one
+// fma, the second fma rounds once). Equal to a / b whenever a, b and the quotient are finite
+// and the quotient is not subnormal; callers guarantee finite inputs and bounded quotients.
+__device__ __forceinline__ float div_mk(float a, float b, float rb) {
+  const float q0 = a * rb;
+  const float e = __fmaf_rn(-b, q0, a);
+  return __fmaf_rn(e, rb, q0);
 }
 __device__ __forceinline__ float f16_rne(float f) { return (float)(_Float16)f; }
 

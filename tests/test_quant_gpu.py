@@ -25,7 +25,10 @@ def assert_bit_equal(got, exp, what=''):
     assert got.dtype == exp.dtype, (what, got.dtype, exp.dtype)
     assert tuple(got.shape) == tuple(exp.shape), (what, got.shape, exp.shape)
     g, e = _bits(got), _bits(exp)
-    n = (g != e).sum().item()
+    diff = g != e
+    if got.is_floating_point():  # NaN sign / payload is not part of the value semantics
+        diff &= ~(got.detach().cpu().isnan() & exp.isnan())
+    n = diff.sum().item()
     assert n == 0, f'{what}: {n} / {g.numel()} elements differ'
 
 
@@ -127,3 +130,34 @@ def test_random_vs_oracle(dev, shape, bit, sym, gran, g):
         r = ops.int_quant_dynamic(wd.reshape(-1, shape[1]), g or shape[1],
                                   int(wq.qmin), int(wq.qmax), sym, fq=False, pack_bits=bit)
         assert np.array_equal(r['packed'].cpu().numpy(), Q.pack_vllm(codes_ref, bit))
+
+
+@pytest.mark.parametrize('bit,sym,gran,g', [(4, True, 'per_group', 128),
+                                             (4, False, 'per_group', 128),
+                                             (3, False, 'per_group', 64),
+                                             (8, True, 'per_channel', None)])
+def test_every_bf16_value_vs_oracle(dev, bit, sym, gran, g):
+    """Every finite bf16 bit pattern (subnormals, signed zeros, extremes), shuffled into
+    groups so each group's scale differs: the kernels' Markstein quotient (div_mk) and
+    hardware bf16 rounding must equal torch-CPU's IEEE x / s and RNE bit for bit."""
+    from lightcompress_amd.quant import IntegerQuantizer
+    allb = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    fin = allb[torch.isfinite(allb.float())]
+    gen = torch.Generator().manual_seed(bit * 10 + int(sym))
+    # magnitudes grouped by exponent band so groups keep a mix of scales and tiny values
+    w = fin[torch.randperm(fin.numel(), generator=gen)]
+    w = w[: (w.numel() // 1024) * 1024].reshape(-1, 1024)
+    kw = {'group_size': g} if g else {}
+    wq = IntegerQuantizer(bit, sym, gran, **kw)
+    fq_ref, _, _ = Q.fake_quant_dynamic(w, bit, sym, gran, g)
+    codes_ref, s_ref, z_ref = Q.real_quant_dynamic(w, bit, sym, gran, g)
+    wd = w.to(dev)
+    assert_bit_equal(wq.fake_quant_weight_dynamic(wd), fq_ref, 'fq')
+    codes, s, z = wq.real_quant_weight_dynamic(wd)
+    assert_bit_equal(codes, codes_ref, 'codes')
+    assert_bit_equal(s, s_ref, 'scales')
+    # small-magnitude rows: every value of a group within a few binades of the others
+    small = fin[(fin.float().abs() < 1e-30)]
+    small = small[: (small.numel() // 1024) * 1024].reshape(-1, 1024)
+    fq_ref, _, _ = Q.fake_quant_dynamic(small, bit, sym, gran, g)
+    assert_bit_equal(wq.fake_quant_weight_dynamic(small.to(dev)), fq_ref, 'fq small')
