@@ -258,6 +258,9 @@ class Llama:
         return {'position_embeddings': (cos, sin), 'attention_mask': None, 'position_ids': pos}
 
     # -- BaseModel contract ---------------------------------------------------------------------
+    def skip_layer_name(self):
+        return ['lm_head']
+
     def get_blocks(self):
         return self.blocks
 
@@ -340,7 +343,17 @@ class Llama:
         self.modality = modality
 
     def save_pretrained(self, path):
-        self.model.save_pretrained(path)
+        if hasattr(self.model, 'save_pretrained'):
+            self.model.save_pretrained(path)
+            return
+        # decoder-only stand-in (Llama.random): safetensors of the blocks + the HF config
+        import os
+        from safetensors.torch import save_file
+        os.makedirs(path, exist_ok=True)
+        sd = {f'model.{k}': v.detach().contiguous() for k, v in self.model.state_dict().items()
+              if torch.is_tensor(v)}
+        save_file(sd, os.path.join(path, 'model.safetensors'))
+        self.model_config.to_json_file(os.path.join(path, 'config.json'))
 
     # -- calibration capture (base_model.py:174-192, 279-336) -----------------------------------
     @torch.no_grad()

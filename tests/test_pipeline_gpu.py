@@ -123,3 +123,37 @@ def test_awq_org_output_reuse_is_bit_identical(dev, quant_out):
     assert st1['reused'] == 3 * len(w1) // 7 and st0['reused'] == 0
     assert l1 == l0
     assert all(torch.equal(a.view(torch.int16), b.view(torch.int16)) for a, b in zip(w1, w0))
+
+
+@pytest.mark.parametrize('target', ['save_vllm', 'save_autoawq'])
+def test_save_quantized_checkpoint(dev, tmp_path, target):
+    """__main__.py:96-160 real-quant save flow: deploy + safetensors + serving config."""
+    import json
+    from safetensors import safe_open
+    from lightcompress_amd.export import save_quantized
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.utils import load_config
+    sym = target == 'save_vllm'
+    w = {'bit': 4, 'symmetric': sym, 'granularity': 'per_group', 'group_size': 128}
+    if sym:
+        w['need_pack'] = True
+    else:
+        w['pack_version'] = 'gemm_pack'
+    cfg = load_config({'quant': {'method': 'RTN', 'weight': w}, 'save': {target: True}})
+    model = tiny_model(dev)
+    algo = build_algo(model, cfg, None)
+    algo.run_block_loop()
+    save_quantized(algo, cfg, str(tmp_path))
+    conf = json.loads((tmp_path / 'config.json').read_text())
+    keys = []
+    for f in tmp_path.glob('*.safetensors'):
+        with safe_open(str(f), 'pt') as fh:
+            keys += list(fh.keys())
+    if sym:
+        assert conf['compression_config']['format'] == 'pack-quantized'
+        assert any(k.endswith('q_proj.weight_packed') for k in keys)
+        assert any(k.endswith('q_proj.weight_scale') for k in keys)
+    else:
+        assert conf['quantization_config']['quant_method'] == 'awq'
+        assert any(k.endswith('q_proj.qweight') for k in keys)
+        assert any(k.endswith('q_proj.qzeros') for k in keys)
