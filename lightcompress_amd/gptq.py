@@ -8,6 +8,8 @@ input (q/k/v, gate/up) share one Hessian accumulator instead of accumulating ide
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -100,19 +102,31 @@ class GPTQ(BaseBlockwiseQuantization):
         entry['acc'].add_batch(inp)
 
     # ---- transform (gptq.py:96-244) -------------------------------------------------------------
+    # Linears fed the same input (q/k/v, gate/up) share H, perm, damping and U, and GPTQ's
+    # rows are independent given U, so their column loops run as ONE loop over
+    # the concatenated rows: the same per-row arithmetic (each element's update order is fixed
+    # by its column, not by the row count), one latency-bound chain of block / trailing kernels
+    # instead of one per linear. LCQ_GPTQ_CONCAT=0 quantizes them one by one.
+    concat_rows = os.environ.get('LCQ_GPTQ_CONCAT', '1') != '0'
+
     @torch.no_grad()
     def subset_transform(self, subset, input_feat, subset_kwargs):
+        groups = {}
         for name, layer in subset['layers'].items():
             if not isinstance(layer, _LINEAR_TYPES):
                 continue
-            self.layer_transform(layer, name)
-            self.free(name)
+            acc = self.layers_cache[name]['acc']
+            groups.setdefault(id(acc), []).append((name, layer))
+        for grp in groups.values():
+            if len(grp) > 1 and self.concat_rows:
+                self.group_transform(grp)
+            else:
+                for name, layer in grp:
+                    self.layer_transform(layer, name)
+            for name, _ in grp:
+                self.free(name)
 
-    @torch.no_grad()
-    def layer_transform(self, layer, name):
-        acc = self.layers_cache[name]['acc']  # shared by the linears fed the same input
-        _, ws, _ = world()
-        replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
+    def _prepared(self, acc, replicate, ws):
         if getattr(acc, 'prepared', None) is None:
             H = acc.H.clone()
             if replicate:
@@ -121,6 +135,45 @@ class GPTQ(BaseBlockwiseQuantization):
                 dist.all_reduce(H, op=dist.ReduceOp.SUM)
                 H /= ws
             acc.prepared = gptq_core.prepare_hessian(H, self.actorder, self.percdamp)
+        return acc.prepared
+
+    @torch.no_grad()
+    def group_transform(self, grp):
+        """layer_transform of several linears sharing one Hessian, as one column loop."""
+        acc = self.layers_cache[grp[0][0]]['acc']
+        _, ws, _ = world()
+        replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
+        prepared = self._prepared(acc, replicate, ws)
+        W = torch.cat([layer.weight.data for _, layer in grp], 0)
+        fixed = None
+        if self.wquantizer.granularity != 'per_group':
+            s = torch.cat([layer.buf_scales.reshape(-1, 1) for _, layer in grp], 0)
+            z = None if self.wquantizer.sym else torch.cat(
+                [layer.buf_zeros.reshape(-1, 1) for _, layer in grp], 0)
+            fixed = (s, z)
+        r = gptq_core.quantize_layer(W, None, self.wquantizer, actorder=self.actorder,
+                                     percdamp=self.percdamp, fixed=fixed, shard_rows=replicate,
+                                     prepared=prepared)
+        ng = 1 if r['scales'] is None else r['scales'].shape[0] // W.shape[0]
+        o0 = 0
+        for _, layer in grp:
+            o1 = o0 + layer.weight.shape[0]
+            layer.weight.data = r['weight'][o0:o1].clone()
+            if r['perm'] is not None:
+                layer.register_buffer('buf_perm', r['perm'])
+                layer.register_buffer('buf_invperm', r['invperm'])
+            if r['scales'] is not None:
+                layer.buf_scales = r['scales'][o0 * ng:o1 * ng].clone()
+                if not self.wquantizer.sym:
+                    layer.buf_zeros = r['zeros'][o0 * ng:o1 * ng].clone()
+            o0 = o1
+
+    @torch.no_grad()
+    def layer_transform(self, layer, name):
+        acc = self.layers_cache[name]['acc']  # shared by the linears fed the same input
+        _, ws, _ = world()
+        replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
+        self._prepared(acc, replicate, ws)
         fixed = None
         if self.wquantizer.granularity != 'per_group':
             fixed = (layer.buf_scales, getattr(layer, 'buf_zeros', None))

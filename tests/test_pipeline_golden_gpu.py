@@ -45,7 +45,15 @@ def run_ours(name, dev, monkeypatch=None):
             diag[f'H_b{self.block_idx}__{lname.replace(".", "__")}'] = \
                 self.layers_cache[lname]['acc'].H.detach().cpu().clone()
             return orig(self, layer, lname)
+        orig_g = GPTQ.group_transform
+
+        def gt(self, grp):
+            for lname, _ in grp:
+                diag[f'H_b{self.block_idx}__{lname.replace(".", "__")}'] = \
+                    self.layers_cache[lname]['acc'].H.detach().cpu().clone()
+            return orig_g(self, grp)
         monkeypatch.setattr(GPTQ, 'layer_transform', lt)
+        monkeypatch.setattr(GPTQ, 'group_transform', gt)
     elif monkeypatch is not None and spec['quant']['method'] == 'Awq':
         from lightcompress_amd.awq import Awq
         orig = Awq.search_scale_subset

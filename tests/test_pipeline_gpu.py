@@ -157,3 +157,28 @@ def test_save_quantized_checkpoint(dev, tmp_path, target):
         assert conf['quantization_config']['quant_method'] == 'awq'
         assert any(k.endswith('q_proj.qweight') for k in keys)
         assert any(k.endswith('q_proj.qzeros') for k in keys)
+
+
+def test_gptq_concatenated_rows_bit_identical(dev):
+    """q/k/v (and gate/up) quantized as one column loop over their concatenated rows give the
+    same weights and qparams, bit for bit, as one loop per linear."""
+    import copy
+    from lightcompress_amd.gptq import GPTQ
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.utils import load_config
+    out = []
+    for concat in (True, False):
+        model = tiny_model(dev)
+        algo = build_algo(model, load_config(copy.deepcopy(GPTQ_CFG)), calib(model))
+        algo.concat_rows = concat
+        algo.run_block_loop()
+        st = {}
+        for bi, b in enumerate(model.blocks):
+            for n, m in model.get_block_linears(b).items():
+                st[f'{bi}.{n}.w'] = m.weight.detach().clone()
+                st[f'{bi}.{n}.s'] = m.buf_scales.detach().clone()
+                st[f'{bi}.{n}.z'] = m.buf_zeros.detach().clone()
+        out.append(st)
+    assert GPTQ.concat_rows  # the default path is the concatenated one
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k
