@@ -95,6 +95,16 @@ int lcq_int_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols,
                          int fq_dtype, void* codes_out, int codes_dtype, void* packed_out,
                          int pack_bits, void* stream);
 
+/* Static quant with a column -> group map: element (r, c) uses scales/zeros group
+ * r * ngc + col_group[c] (int32 [cols], 16-byte aligned). GPTQ's act-order deploy
+ * (gptq.py:411-459 w_qdq: fake_quant_static(W[:, perm])[:, invperm]) with
+ * col_group[c] = invperm[c] / group, without the two column gathers. cols % 8 == 0. */
+int lcq_int_quant_static_cols(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                              const int32_t* col_group, int64_t ngc, const void* scales,
+                              int s_dtype, const void* zeros, int z_dtype, int ct_dtype,
+                              int qmin, int qmax, void* fq_out, int fq_dtype, void* codes_out,
+                              int codes_dtype, void* stream);
+
 /* vLLM pack of existing integer codes (module_utils.py:929-955).
  * codes [rows, cols] I8/U8/I32 -> packed [rows, ceil(cols*bits/32)] int32. */
 int lcq_pack_vllm(const void* codes, int codes_dtype, int64_t rows, int64_t cols, int bits,

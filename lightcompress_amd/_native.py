@@ -38,6 +38,8 @@ SIGNATURES = {
                                _vp, _int, _vp, _int, _vp, _int, _vp, _vp, _vp], _int),
     'lcq_int_quant_static': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _int, _int,
                               _int, _vp, _int, _vp, _int, _vp, _int, _vp], _int),
+    'lcq_int_quant_static_cols': ([_vp, _int, _i64, _i64, _vp, _i64, _vp, _int, _vp, _int,
+                                   _int, _int, _int, _vp, _int, _vp, _int, _vp], _int),
     'lcq_pack_vllm': ([_vp, _int, _i64, _i64, _int, _vp, _vp], _int),
     'lcq_pack_autoawq_gemm': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _vp, _vp,
                                _vp, _vp], _int),

@@ -270,6 +270,42 @@ __global__ void __launch_bounds__(256) k_quant_static(QuantArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// static qparams with a column -> group map (GPTQ act-order deploy, gptq.py:411-459):
+// element (r, c) uses group r * ngc + cgroup[c]. With cgroup[c] = invperm[c] / group this is
+// fake_quant_static(W[:, perm])[:, invperm] without the two column gathers (the same
+// per-element arithmetic, so bit-identical). cols % 8 == 0.
+// ---------------------------------------------------------------------------------------
+template <int XT, int CT>
+__global__ void __launch_bounds__(256) k_quant_static_cols(QuantArgs a, const int32_t* cgroup,
+                                                           int64_t ngc) {
+  const int64_t n8 = a.rows * a.cols / 8;
+  const int64_t c8 = a.cols / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
+    const int64_t r = t / c8, c0 = (t - r * c8) * 8;
+    const int64_t e0 = t * 8;
+    float w[8], q[8], dq[8];
+    ld8<XT>(a.x, e0, w);
+    const int4 ga = *reinterpret_cast<const int4*>(cgroup + c0);
+    const int4 gb = *reinterpret_cast<const int4*>(cgroup + c0 + 4);
+    const int g[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t gi = r * ngc + g[j];
+      const float x = rnd<CT>(w[j]);  // .to(compute dtype)
+      const float sc = rnd<CT>(ld_rt(a.s_in, a.s_dt, gi));
+      const float z = a.z_in ? rnd<CT>(ld_rt(a.z_in, a.z_dt, gi)) : 0.f;
+      float t1 = rintf(rnd<CT>(x / sc));
+      t1 = rnd<CT>(t1 + z);
+      t1 = fminf(fmaxf(t1, a.qmin), a.qmax);
+      q[j] = t1;
+      dq[j] = rnd<CT>(rnd<CT>(t1 - z) * sc);
+    }
+    emit<CT>(a, e0, q, dq);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // standalone vLLM pack of integer codes (module_utils.py:929-955), incl. zero padding
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_pack_vllm(const void* codes, int dt, int64_t rows,
@@ -411,4 +447,44 @@ extern "C" int lcq_pack_vllm(const void* codes, int codes_dtype, int64_t rows, i
   hipLaunchKernelGGL(k_pack_vllm, stream_grid(n, 256), 256, 0, as_stream(stream), codes,
                      codes_dtype, rows, cols, bits, reinterpret_cast<uint32_t*>(packed_out));
   return check_launch("lcq_pack_vllm");
+}
+
+extern "C" int lcq_int_quant_static_cols(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                                         const int32_t* col_group, int64_t ngc,
+                                         const void* scales, int s_dtype, const void* zeros,
+                                         int z_dtype, int ct_dtype, int qmin, int qmax,
+                                         void* fq_out, int fq_dtype, void* codes_out,
+                                         int codes_dtype, void* stream) {
+  int64_t group = 8;  // only the shared shape / dtype checks apply here
+  int rc = common_checks("lcq_int_quant_static_cols", x_dtype, rows, cols, group, qmin, qmax,
+                         fq_out, fq_dtype, codes_out, codes_dtype, nullptr, 0);
+  if (rc) return rc;
+  LCQ_REQUIRE(cols % 8 == 0, "cols must be a multiple of 8");
+  LCQ_REQUIRE(col_group != nullptr && ngc > 0 && scales != nullptr, "col_group / scales required");
+  LCQ_REQUIRE((reinterpret_cast<uintptr_t>(col_group) & 15) == 0, "col_group must be 16-byte aligned");
+  LCQ_REQUIRE(is_float_dt(s_dtype), "scales dtype must be float");
+  QuantArgs a{};
+  a.x = x; a.s_in = scales; a.s_dt = s_dtype; a.z_in = zeros; a.z_dt = z_dtype;
+  a.rows = rows; a.cols = cols; a.group = 0;
+  a.qmin = (float)qmin; a.qmax = (float)qmax;
+  a.fq = fq_out; a.fq_dt = fq_dtype; a.codes = codes_out; a.codes_dt = codes_dtype;
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = stream_grid(rows * cols / 8, 256);
+#define LCQ_SC(XT, CT) \
+  hipLaunchKernelGGL((k_quant_static_cols<XT, CT>), grid, 256, 0, st, a, col_group, ngc)
+#define LCQ_SC_X(XT)                                                         \
+  switch (ct_dtype) {                                                        \
+    case LCQ_F32: LCQ_SC(XT, LCQ_F32); break;                                \
+    case LCQ_BF16: LCQ_SC(XT, LCQ_BF16); break;                              \
+    case LCQ_F16: LCQ_SC(XT, LCQ_F16); break;                                \
+    default: return fail(LCQ_EINVAL, "lcq_int_quant_static_cols: bad compute dtype"); \
+  }
+  switch (x_dtype) {
+    case LCQ_F32: LCQ_SC_X(LCQ_F32); break;
+    case LCQ_BF16: LCQ_SC_X(LCQ_BF16); break;
+    default: LCQ_SC_X(LCQ_F16);
+  }
+#undef LCQ_SC_X
+#undef LCQ_SC
+  return check_launch("lcq_int_quant_static_cols");
 }

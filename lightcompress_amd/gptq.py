@@ -13,7 +13,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import gptq_core
+from . import gptq_core, ops
 from .base_blockwise_quantization import BaseBlockwiseQuantization
 from .module_utils import _LLMC_LINEAR_TYPES_, _TRANSFORMERS_LINEAR_TYPES_
 from .registry import ALGO_REGISTRY
@@ -202,6 +202,9 @@ class GPTQ(BaseBlockwiseQuantization):
 
     @torch.no_grad()
     def w_qdq(self, module, wquantizer):
+        fast = self._w_qdq_cols(module, wquantizer)
+        if fast is not None:
+            return fast
         weight = module.weight
         if self.need_perm:
             weight = module.weight[:, module.buf_perm].contiguous()
@@ -211,6 +214,35 @@ class GPTQ(BaseBlockwiseQuantization):
         if self.need_perm:
             weight = weight[:, module.buf_invperm].contiguous()
         return weight
+
+    @torch.no_grad()
+    def _w_qdq_cols(self, module, wquantizer):
+        """w_qdq under act-order, per-group int quant: fake_quant_static(W[:, perm])[:, invperm]
+        as ONE pass over W in its own column order (lcq_int_quant_static_cols: column c takes
+        group invperm[c] // group) -- the same per-element arithmetic without the two column
+        gathers. None when the layout is not that case."""
+        from .quant import IntegerQuantizer
+        if not (self.need_perm and isinstance(wquantizer, IntegerQuantizer)
+                and wquantizer.granularity == 'per_group' and module.weight.dim() == 2
+                and module.weight.is_cuda and module.weight.shape[1] % 8 == 0):
+            return None
+        W = module.weight.data
+        s = module.buf_scales
+        z = getattr(module, 'buf_zeros', None)
+        zz = z if (torch.is_tensor(z) and z.dim() > 0) else None
+        if zz is None and torch.is_tensor(z) and z.numel() == 1 and float(z) != 0:
+            return None
+        cg = getattr(module, '_lcq_cgroup', None)
+        if cg is None or cg.numel() != W.shape[1]:
+            cg = (module.buf_invperm // wquantizer.group_size).to(torch.int32).contiguous()
+            module._lcq_cgroup = cg
+        ct = torch.promote_types(W.dtype, s.dtype)   # quant.py _static's compute dtype
+        if zz is not None and zz.is_floating_point():
+            ct = torch.promote_types(ct, zz.dtype)
+        qmin, qmax = wquantizer._iq
+        return ops.int_quant_static_cols(W, cg, s.reshape(-1), None if zz is None else
+                                         zz.reshape(-1), qmin, qmax, ct_dtype=ct,
+                                         fq_dtype=self.model_dtype)
 
     @torch.no_grad()
     def deploy(self, quant_format, keep_device=True):

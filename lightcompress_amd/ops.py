@@ -113,6 +113,31 @@ def int_quant_static(x: torch.Tensor, group: int, scales: torch.Tensor,
     return res
 
 
+def int_quant_static_cols(x: torch.Tensor, col_group: torch.Tensor, scales: torch.Tensor,
+                          zeros: torch.Tensor | None, qmin: int, qmax: int, *,
+                          ct_dtype: torch.dtype, fq_dtype: torch.dtype) -> torch.Tensor:
+    """Static fake quant of x [rows, cols] where element (r, c) uses group
+    r * ngc + col_group[c] of scales / zeros ([rows * ngc] flat). Returns fq [rows, cols]."""
+    assert x.dim() == 2 and col_group.dtype == torch.int32 and col_group.numel() == x.shape[1]
+    x = x.contiguous()
+    rows, cols = x.shape
+    scales = scales.contiguous()
+    ngc = scales.numel() // rows
+    if ngc * rows != scales.numel():
+        raise ValueError('scales do not tile the rows')
+    if zeros is not None:
+        zeros = zeros.contiguous()
+        if zeros.numel() != scales.numel():
+            raise ValueError('zeros / scales size mismatch')
+    cg = col_group.contiguous()
+    out = torch.empty((rows, cols), dtype=fq_dtype, device=x.device)
+    N.call('lcq_int_quant_static_cols', N.ptr(x), N.dt(x), rows, cols, N.ptr(cg), ngc,
+           N.ptr(scales), N.dt(scales), N.ptr(zeros), N.dt(zeros) if zeros is not None else 0,
+           N.dt(ct_dtype), int(qmin), int(qmax), N.ptr(out), N.dt(fq_dtype), None, 0,
+           N.stream_of(x))
+    return out
+
+
 def pack_vllm(codes: torch.Tensor, bits: int) -> torch.Tensor:
     """VllmRealQuantLinear.pack bit layout (module_utils.py:929-955) on device."""
     assert codes.dim() == 2

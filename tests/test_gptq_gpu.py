@@ -236,3 +236,28 @@ def test_chol_inv_tile_info(dev):
     info = torch.zeros(1, dtype=torch.int32, device=dev)
     ops.chol_inv_tile(H, info, row0=256)
     assert int(info.item()) == 256 + 41
+
+
+@pytest.mark.parametrize('sym,group', [(False, 128), (True, 128), (False, 64)])
+def test_static_cols_equals_permuted_static(dev, sym, group):
+    """lcq_int_quant_static_cols with col_group = invperm // group == GPTQ.w_qdq's
+    fake_quant_static(W[:, perm]).to(bf16)[:, invperm], bit for bit."""
+    from lightcompress_amd import ops
+    from lightcompress_amd.quant import IntegerQuantizer
+    g = torch.Generator().manual_seed(group + int(sym))
+    rows, cols = 192, 1024
+    W = (torch.randn(rows, cols, generator=g) * 0.02).to(dev)
+    perm = torch.randperm(cols, generator=g).to(dev)
+    invperm = torch.argsort(perm)
+    wq = IntegerQuantizer(4, sym, 'per_group', group_size=group)
+    Wp = W[:, perm].contiguous()
+    _, s, z, _, _ = wq.get_tensor_qparams(Wp)
+    args = {'scales': s, 'zeros': z if not sym else torch.tensor(0.0), 'qmax': wq.qmax,
+            'qmin': wq.qmin}
+    ref = wq.fake_quant_weight_static(Wp, args).to(torch.bfloat16)[:, invperm]
+    cg = (invperm // group).to(torch.int32)
+    qmin, qmax = wq._iq
+    got = ops.int_quant_static_cols(W, cg, s.reshape(-1), None if sym else z.reshape(-1),
+                                    qmin, qmax, ct_dtype=torch.float32,
+                                    fq_dtype=torch.bfloat16)
+    assert torch.equal(got.view(torch.int16), ref.contiguous().view(torch.int16))
