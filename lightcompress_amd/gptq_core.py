@@ -99,6 +99,32 @@ class _linalg_backend:
             torch.backends.cuda.preferred_linalg_library(self.prev)
 
 
+class _blas_backend:
+    """Scoped torch BLAS library for the recursion's fp32 GEMMs (env LCQ_CHOL_BLAS = cublas
+    (rocBLAS on ROCm; default) | cublaslt (hipBLASLt) | default). Measured on MI355X: the
+    Cholesky-inverse recursion takes 33.6 ms (n 14336) / 3.5 ms (n 4096) on rocBLAS vs
+    42.1 / 5.8 ms on hipBLASLt, whose kernel choices for the many <= 256 and strided
+    mid-size products are slow. Restores the caller's choice on exit."""
+
+    def __enter__(self):
+        import os
+        self.want = os.environ.get('LCQ_CHOL_BLAS', 'cublas')
+        self.prev = None
+        if self.want != 'default' and torch.cuda.is_available():
+            import warnings
+            with warnings.catch_warnings():
+                warnings.simplefilter('ignore')
+                self.prev = torch.backends.cuda.preferred_blas_library()
+                torch.backends.cuda.preferred_blas_library(self.want)
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            import warnings
+            with warnings.catch_warnings():
+                warnings.simplefilter('ignore')
+                torch.backends.cuda.preferred_blas_library(self.prev)
+
+
 _TILE = 128
 _TRI_MIN = 1024  # triangular / symmetric products split while both halves stay >= this
 
@@ -190,7 +216,8 @@ def inverse_cholesky_upper(H: torch.Tensor) -> torch.Tensor:
     del H
     info = torch.zeros(1, dtype=torch.int32, device=Hr.device)
     X = torch.zeros_like(Hr)
-    _chol_inv_rec(Hr, X, info)
+    with _blas_backend():
+        _chol_inv_rec(Hr, X, info)
     del Hr
     bad = int(info.item())
     if bad:
