@@ -13,7 +13,8 @@ from pathlib import Path
 
 import torch
 
-_LIB_PATH = Path(__file__).resolve().parent / '_lib' / 'liblcq.so'
+_LIB_PATH = Path(os.environ.get('LCQ_LIB_PATH') or
+                 Path(__file__).resolve().parent / '_lib' / 'liblcq.so')  # env: A/B probes
 _HEADER = Path(__file__).resolve().parent.parent / 'include' / 'lcq.h'
 
 F32, F16, BF16, I8, U8, I32, FP8E4M3, F64, FP8E5M2 = range(9)

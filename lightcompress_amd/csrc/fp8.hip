@@ -16,6 +16,7 @@
 // Design: HBM-bound streaming, 16-byte loads (8 elements per lane), scales reduced with
 // wave butterflies / one LDS hop; the 128x128 block kernel keeps its block in VGPRs between
 // the amax and the cast (one HBM read). No MFMA: this is byte work, not a GEMM.
+#define LCQ_BF16_HW 1  // bf16 rounding on v_cvt_pk_bf16_f32 (see lcq_common.h)
 #include "lcq_common.h"
 
 namespace lcq {

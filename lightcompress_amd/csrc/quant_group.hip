@@ -11,6 +11,7 @@
 // min/max is a butterfly over those lanes (__shfl_xor) -- no LDS, one pass over HBM:
 // read 2 B/elem, write 2 B (fake quant) or 0.5 B (int4 packed) per element.
 // Groups wider than 512 (per-channel rows) use one 256-thread workgroup per group.
+#define LCQ_BF16_HW 1  // bf16 rounding on v_cvt_pk_bf16_f32 (see lcq_common.h)
 #include "lcq_common.h"
 
 namespace lcq {
