@@ -119,3 +119,24 @@ def test_search_scale_vs_reference(dev, subset, sym):
     assert torch.equal(bits(best), bits(c['scales']))
     got = torch.tensor(obj.last_search['losses'], dtype=torch.float64)
     assert torch.allclose(got, c['losses'], rtol=5e-2, atol=1e-9)
+
+
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16, torch.float32])
+def test_scale_bcast_every_value(dev, dt):
+    """x / s and x * s per column for every finite bf16 value against up to 64 scales from
+    1e-30 to 1e30: bit-equal to torch-CPU, including subnormal, zero and overflowing results."""
+    from lightcompress_amd import ops
+    allb = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    fin = allb[torch.isfinite(allb.float())]
+    x = fin[: (fin.numel() // 64) * 64].reshape(-1, 64).to(dt)
+    g = torch.Generator().manual_seed(9)
+    s = torch.cat([torch.logspace(-30, 30, 32), torch.rand(32, generator=g) * 4 + 0.01]).to(dt)
+    s = s[torch.isfinite(s.float()) & (s.float() != 0)]
+    s = s[: s.numel() // 8 * 8]
+    x = x[:, : s.numel()].contiguous()
+    for op, ref in (('div', x / s.view(1, -1)), ('mul', x * s.view(1, -1))):
+        got = ops.scale_bcast(x.to(dev), s.to(dev), op).cpu()
+        same = (got.view(torch.int16 if dt != torch.float32 else torch.int32) ==
+                ref.view(torch.int16 if dt != torch.float32 else torch.int32))
+        same |= got.isnan() & ref.isnan()
+        assert bool(same.all()), (op, int((~same).sum()))
