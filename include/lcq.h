@@ -270,6 +270,18 @@ int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t max_elems, in
                                  int block, int fmt_out, float qmax, float clamp_min,
                                  int add_zero, void* amax_ws, void* scales_out, void* stream);
 
+/* Causal flash-attention forward of the calibration forwards (the sdpa call inside
+ * LlamaAttention.forward, reached from awq.py:110-126 inspect forwards and the block forwards
+ * of base_blockwise_quantization.py:367-381): out[b, s, h, :] = softmax(q k^T * scale, causal)
+ * v with GQA (kv head = h / (H / KVH)). q/k/v bf16 viewed as [B, heads, S, 128] with element
+ * strides {batch, head, seq} (host int64[3] each; head dim contiguous, strides multiples of 8,
+ * 16-byte aligned); out bf16 [B, S, H, 128] contiguous. fp32 scores and online softmax,
+ * bf16 P.V. */
+int lcq_attn_fwd_causal(const void* q, const void* k, const void* v, int dtype, int64_t B,
+                        int64_t S, int H, int KVH, int D, const int64_t* q_strides,
+                        const int64_t* k_strides, const int64_t* v_strides, float scale,
+                        void* out, void* stream);
+
 /* FloatQuantizer use_qtorch=False fake quant (get_float_qparams, quant.py:1005-1027, and
  * quant/dequant :1061-1076): per group of `group` elements, power-of-two per-element scales
  * for an e_bits/m_bits float format; every op rounds to the tensor dtype (fp32 when

@@ -41,6 +41,8 @@ SIGNATURES = {
                               _int, _vp, _int, _vp, _int, _vp, _int, _vp], _int),
     'lcq_int_quant_static_cols': ([_vp, _int, _i64, _i64, _vp, _i64, _vp, _int, _vp, _int,
                                    _int, _int, _int, _vp, _int, _vp, _int, _vp], _int),
+    'lcq_attn_fwd_causal': ([_vp, _vp, _vp, _int, _i64, _i64, _int, _int, _int, _vp, _vp, _vp,
+                             _f32, _vp, _vp], _int),
     'lcq_pack_vllm': ([_vp, _int, _i64, _i64, _int, _vp, _vp], _int),
     'lcq_pack_autoawq_gemm': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _vp, _vp,
                                _vp, _vp], _int),
@@ -125,6 +127,14 @@ def ptr(t):
                        f'got a tensor on {t.device}')
     if not t.is_contiguous():
         raise LcqError('tensor must be contiguous')
+    return t.data_ptr()
+
+
+def ptr_strided(t):
+    """Device pointer of a possibly strided tensor (the kernel takes its strides)."""
+    if not t.is_cuda:
+        raise LcqError('lightcompress_amd ops run on the GPU only (no CPU fallback); '
+                       f'got a tensor on {t.device}')
     return t.data_ptr()
 
 

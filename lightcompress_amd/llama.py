@@ -35,6 +35,34 @@ def _fused_apply_rotary(q, k, cos, sin, unsqueeze_dim=1):
     return _ORIG_ROTARY(q, k, cos, sin, unsqueeze_dim)
 
 
+_ORIG_SDPA = None
+# the lcq flash kernel beats torch's SDPA (aotriton) up to this sequence length on MI355X
+# (S 512: 0.99 vs 1.65 ms; S 2048: 11.9 vs 10.8 ms, scripts/attn_rate.py); env override
+_LCQ_ATTN_MAX_S = int(os.environ.get('LCQ_ATTN_MAX_S', '1024'))
+
+
+def _lcq_sdpa(module, query, key, value, attention_mask, dropout=0.0, scaling=None,
+              is_causal=None, **kwargs):
+    """transformers' sdpa attention function with the calibration case routed to
+    lcq_attn_fwd_causal: causal, no mask / dropout / position bias, bf16, head dim 128,
+    q_len == kv_len. Anything else goes to the original sdpa_attention_forward."""
+    from . import ops
+    causal = is_causal if is_causal is not None else getattr(module, 'is_causal', True)
+    S = query.shape[2]
+    if (causal and attention_mask is None and dropout == 0.0 and query.is_cuda
+            and query.dtype == torch.bfloat16 and key.dtype == torch.bfloat16
+            and value.dtype == torch.bfloat16 and query.shape[-1] == 128
+            and key.shape[2] == S and 1 < S <= _LCQ_ATTN_MAX_S
+            and kwargs.get('position_bias') is None and not kwargs.get('output_attentions')
+            and query.shape[1] % key.shape[1] == 0
+            and all(t.stride(-1) == 1 and all(st % 8 == 0 for st in t.stride()[:3])
+                    for t in (query, key, value))):
+        scale = scaling if scaling is not None else query.shape[-1] ** -0.5
+        return ops.attn_fwd_causal(query, key, value, scale), None
+    return _ORIG_SDPA(module, query, key, value, attention_mask, dropout=dropout,
+                      scaling=scaling, is_causal=is_causal, **kwargs)
+
+
 def _fused_mlp_forward(self, x):
     """LlamaMLP.forward with act_fn(gate) * up on one lcq_silu_mul pass; the projections are
     still called as modules (hooks fire in the original order: gate, up, down)."""
@@ -180,6 +208,11 @@ def install_fused_forward(model: nn.Module):
     if _ORIG_ROTARY is None:
         _ORIG_ROTARY = ml.apply_rotary_pos_emb
         ml.apply_rotary_pos_emb = _fused_apply_rotary
+    global _ORIG_SDPA
+    if _ORIG_SDPA is None and os.environ.get('LCQ_FLASH_ATTN', '1') != '0':
+        from transformers.modeling_utils import AttentionInterface
+        _ORIG_SDPA = AttentionInterface._global_mapping['sdpa']
+        AttentionInterface.register('sdpa', _lcq_sdpa)
     global _STOCK_DECODER_FORWARD
     if _STOCK_DECODER_FORWARD is None:
         _STOCK_DECODER_FORWARD = ml.LlamaDecoderLayer.forward

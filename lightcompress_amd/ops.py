@@ -560,3 +560,27 @@ def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
     N.call('lcq_rmsnorm', N.ptr(x2), N.ptr(w), N.dt(x.dtype), x2.shape[0], x2.shape[1],
            float(eps), N.ptr(out), N.stream_of(x2))
     return out.view(x.shape)
+
+
+def attn_fwd_causal(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
+                    scale: float) -> torch.Tensor:
+    """Causal softmax(q k^T * scale) v for q [B, H, S, 128], k / v [B, KVH, S, 128] bf16 (any
+    strides with a contiguous head dim, e.g. the head-transposed projection views). Returns
+    [B, S, H, 128] contiguous (the layout LlamaAttention reshapes to [B, S, H * 128])."""
+    import ctypes
+    B, H, S, D = q.shape
+    KVH = k.shape[1]
+    if tuple(k.shape) != (B, KVH, S, D) or tuple(v.shape) != tuple(k.shape):
+        raise ValueError('k / v must be [B, KVH, S, D] matching q')
+    strides = []
+    for t in (q, k, v):
+        if t.stride(-1) != 1:
+            raise ValueError('head dim must be contiguous')
+        strides.append((ctypes.c_int64 * 3)(t.stride(0), t.stride(1), t.stride(2)))
+    out = torch.empty((B, S, H, D), dtype=q.dtype, device=q.device)
+    N.call('lcq_attn_fwd_causal', N.ptr_strided(q), N.ptr_strided(k), N.ptr_strided(v),
+           N.dt(q.dtype), B, S, H, KVH, D, ctypes.addressof(strides[0]),
+           ctypes.addressof(strides[1]), ctypes.addressof(strides[2]), float(scale), N.ptr(out),
+           N.stream_of(q))
+    N.note_work('lcq_attn_fwd_causal', 2.0 * B * H * S * (S + 1) * D)  # causal QK^T + PV flops
+    return out

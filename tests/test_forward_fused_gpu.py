@@ -54,8 +54,12 @@ def test_block_forward_unchanged(dev):
     kw = model.rotary_kwargs(64)
     fused = blk(x, **kw)
     fused = fused[0] if isinstance(fused, tuple) else fused
+    from transformers.modeling_utils import AttentionInterface
     saved = ml.apply_rotary_pos_emb
     ml.apply_rotary_pos_emb = L._ORIG_ROTARY
+    saved_sdpa = AttentionInterface._global_mapping['sdpa']
+    if L._ORIG_SDPA is not None:
+        AttentionInterface.register('sdpa', L._ORIG_SDPA)
     patched = [m for m in blk.modules() if 'forward' in m.__dict__]
     fwds = [m.__dict__['forward'] for m in patched]
     for m in patched:
@@ -65,9 +69,11 @@ def test_block_forward_unchanged(dev):
         ref = ref[0] if isinstance(ref, tuple) else ref
     finally:
         ml.apply_rotary_pos_emb = saved
+        AttentionInterface.register('sdpa', saved_sdpa)
         for m, f in zip(patched, fwds):
             m.forward = f
-    # rotary and silu*up are bit-identical; RMSNorm's variance order may move a rounding
+    # rotary and silu*up are bit-identical; RMSNorm's variance order may move a rounding; the
+    # flash kernel vs torch's SDPA differ within bf16 rounding of the attention output
     torch.testing.assert_close(fused.float(), ref.float(), rtol=2e-2, atol=2e-2)
     assert (fused != ref).float().mean().item() < 0.02
 
