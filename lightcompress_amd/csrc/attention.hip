@@ -89,38 +89,56 @@ __device__ __forceinline__ void stage_kv(char* kst, char* vst, const uint16_t* k
   }
 }
 
-__global__ void __launch_bounds__(256, 2) k_attn_fwd_causal(AttnArgs a) {
-  // two stages of [K image | V image], 16 KB each: 64 KB
+// QB query blocks of 32 rows per wave (a workgroup covers 128 QB rows): every K / V fragment
+// read from LDS feeds QB MFMAs. QB 2 halves the LDS traffic per flop but needs 492 VGPRs, so
+// one wave per SIMD: without a hand-pipelined schedule its MFMA, softmax and LDS phases
+// serialise (measured: 164 vs 277 TFLOP/s at S 512, 194 vs 379 at S 2048). QB 1 (two
+// workgroups per CU, MFMA of one wave under the softmax of the other) is the default;
+// LCQ_ATTN_QB=2 selects the other for probes.
+template <int QB>
+__global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnArgs a) {
+  constexpr int QT = AQT * QB;
+  // two stages of [K image | V image], 16 KB each: 64 KB (reused to stage the output tile)
   __shared__ __attribute__((aligned(1024))) char smem[2][2][AKT * 256];
-  __shared__ float xch[4][32];
+  __shared__ float xch[4][32 * QB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int qt = (int)gridDim.x - 1 - (int)blockIdx.x;  // longest (last) query tiles first
   const int hq = blockIdx.y, b = blockIdx.z;
   const int hk = hq / (a.H / a.KVH);
-  const int q0 = qt * AQT;
-  const int qrow = q0 + 32 * w + c;  // this lane's query row (both halves)
+  const int q0 = qt * QT;
   const uint16_t* qp = a.q + b * a.qsb + hq * a.qsh;
   const uint16_t* kp = a.k + b * a.ksb + hk * a.ksh;
   const uint16_t* vp = a.v + b * a.vsb + hk * a.vsh;
-  const int kend = min(a.S, q0 + AQT);
+  const int kend = min(a.S, q0 + QT);
   stage_kv(smem[0][0], smem[0][1], kp, vp, a.kss, a.vss, 0, a.S, w, lane);
 
+  int qrow[QB];  // this lane's query row in block qb (both lane halves)
   // Q^T as the B operand of mfma(K, Q^T): lane holds Q[qrow][16 kk + 8 h + j]
-  v8s_t qf[8];
+  v8s_t qf[QB][8];
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    if (qrow < a.S)
-      qf[kk] = *reinterpret_cast<const v8s_t*>(qp + (int64_t)qrow * a.qss + 16 * kk + 8 * h);
-    else
-      qf[kk] = (v8s_t){0, 0, 0, 0, 0, 0, 0, 0};
+  for (int qb = 0; qb < QB; ++qb) {
+    qrow[qb] = q0 + 32 * (QB * w + qb) + c;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      if (qrow[qb] < a.S)
+        qf[qb][kk] = *reinterpret_cast<const v8s_t*>(qp + (int64_t)qrow[qb] * a.qss + 16 * kk +
+                                                     8 * h);
+      else
+        qf[qb][kk] = (v8s_t){0, 0, 0, 0, 0, 0, 0, 0};
+    }
   }
-  float m = -INFINITY, l = 0.f;
-  v16f_t o[4];
+  float m[QB], l[QB];
+  v16f_t o[QB][4];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+  for (int qb = 0; qb < QB; ++qb) {
+    m[qb] = -INFINITY;
+    l[qb] = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[qb][dt][r] = 0.f;
+  }
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
 
   int it = 0;
@@ -137,71 +155,84 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd_causal(AttnArgs a) {
     const char* kimg = smem[cur][0];
     const char* vimg = smem[cur][1];
 
-    // S^T tiles t = 0, 1: register r holds key k0 + 32 t + (r & 3) + 8 (r >> 2) + 4 h of row qrow
-    v16f_t s[2];
+    // S^T tiles t = 0, 1: register r holds key k0 + 32 t + (r & 3) + 8 (r >> 2) + 4 h of the
+    // lane's query row
+    v16f_t s[QB][2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[t][r] = 0.f;
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[qb][t][r] = 0.f;
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
         const v8s_t kf = *reinterpret_cast<const v8s_t*>(kimg + img_off(32 * t + c, 2 * kk + h));
-        s[t] = mfma32(kf, qf[kk], s[t]);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) s[qb][t] = mfma32(kf, qf[qb][kk], s[qb][t]);
       }
     }
-    // scale, causal mask, online softmax (exp2 domain)
-    const bool diag = k0 + AKT - 1 > q0 + 32 * w;  // some key of the tile can exceed a row
-    float mx = -INFINITY;
+    // scale, causal mask, online softmax (exp2 domain), per query block
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int qb = 0; qb < QB; ++qb) {
+      const bool diag = k0 + AKT - 1 > q0 + 32 * (QB * w + qb);  // a key can exceed a row
+      float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = s[t][r] * a.sl2;
-        if (diag) {
-          const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (key > qrow || key >= a.S) v = -INFINITY;
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = s[qb][t][r] * a.sl2;
+          if (diag) {
+            const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (key > qrow[qb] || key >= a.S) v = -INFINITY;
+          }
+          s[qb][t][r] = v;
+          mx = fmaxf(mx, v);
         }
-        s[t][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
-    const float msub = (mn == -INFINITY) ? 0.f : mn;
-    float rs = 0.f;
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[qb], mx);
+      const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[qb] - mn);
+      const float msub = (mn == -INFINITY) ? 0.f : mn;
+      float rs = 0.f;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(s[t][r] - msub);
-        s[t][r] = p;
-        rs += p;
-      }
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
-    // rescale O: its registers hold rows (r & 3) + 8 (r >> 2) + 4 h of this wave's 32
-    if (h == 0) xch[w][c] = alpha;
-    __builtin_amdgcn_wave_barrier();
-    float ar[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ar[r] = xch[w][(r & 3) + 8 * (r >> 2) + 4 * h];
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(s[qb][t][r] - msub);
+          s[qb][t][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l[qb] = l[qb] * alpha + rs;
+      m[qb] = mn;
+      if (h == 0) xch[w][32 * qb + c] = alpha;
+    }
+    // rescale O: its registers hold rows (r & 3) + 8 (r >> 2) + 4 h of each 32-row block
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int qb = 0; qb < QB; ++qb) {
+      float ar[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[dt][r] *= ar[r];
+      for (int r = 0; r < 16; ++r) ar[r] = xch[w][32 * qb + (r & 3) + 8 * (r >> 2) + 4 * h];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[qb][dt][r] *= ar[r];
+    }
+    __builtin_amdgcn_wave_barrier();
     // P.V: k-step (t, s2) takes score registers 8 s2 .. 8 s2 + 7 of tile t; element j is key
     // 32 t + 16 s2 + 8 (j >> 2) + 4 h + (j & 3); V^T fragments by transposed reads of those rows
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        v8s_t pf;
-        uint32_t* pw = reinterpret_cast<uint32_t*>(&pf);
+        v8s_t pf[QB];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          pw[j] = pack_bf16(s[t][8 * s2 + 2 * j], s[t][8 * s2 + 2 * j + 1]);
+        for (int qb = 0; qb < QB; ++qb) {
+          uint32_t* pw = reinterpret_cast<uint32_t*>(&pf[qb]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            pw[j] = pack_bf16(s[qb][t][8 * s2 + 2 * j], s[qb][t][8 * s2 + 2 * j + 1]);
+        }
         const int r0 = 32 * t + 16 * s2 + 4 * (g >> 1);  // this 16-lane group's first key row
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
@@ -209,38 +240,41 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd_causal(AttnArgs a) {
           const v4s_t lo = tr_read(vimg, img_off(r0 + qq, ch) + 8 * (pp & 1));
           const v4s_t hi = tr_read(vimg, img_off(r0 + 8 + qq, ch) + 8 * (pp & 1));
           const v8s_t vf = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-          o[dt] = mfma32(pf, vf, o[dt]);
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) o[qb][dt] = mfma32(pf[qb], vf, o[qb][dt]);
         }
       }
   }
   // normalise: rows of O take 1 / l of their query row
-  if (h == 0) xch[w][c] = 1.f / l;
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb)
+    if (h == 0) xch[w][32 * qb + c] = 1.f / l[qb];
   __syncthreads();  // also: every wave is past its last read of the K / V images
-  char* kimg = smem[0][0];
-  char* vimg = smem[0][1];
-  float il[16];
+  // stage the QT x 128 bf16 output tile (QT rows of 256 B = 32 KB per 128 rows) in the stage
+  // buffers, then store whole 256-byte rows of out[b, q, hq, :]
+  char* ost = &smem[0][0][0];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) il[r] = xch[w][(r & 3) + 8 * (r >> 2) + 4 * h];
-  // stage the 128 x 128 bf16 output tile in the K / V images (rows 0-63 / 64-127), then store
-  // whole 256-byte rows of out[b, q, hq, :]
+  for (int qb = 0; qb < QB; ++qb) {
+    float il[16];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+    for (int r = 0; r < 16; ++r) il[r] = xch[w][32 * qb + (r & 3) + 8 * (r >> 2) + 4 * h];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int col = 32 * dt + c;
-      char* base = row < 64 ? kimg : vimg;
-      *reinterpret_cast<__bf16*>(base + img_off(row & 63, col >> 3) + 2 * (col & 7)) =
-          (__bf16)(o[dt][r] * il[r]);
-    }
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * (QB * w + qb) + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = 32 * dt + c;
+        *reinterpret_cast<__bf16*>(ost + img_off(row, col >> 3) + 2 * (col & 7)) =
+            (__bf16)(o[qb][dt][r] * il[r]);
+      }
+  }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {  // 128 rows x 16 chunks, 8 per thread
+  for (int i = 0; i < 8 * QB; ++i) {  // QT rows x 16 chunks
     const int idx = i * 256 + tid, row = idx >> 4, ch = idx & 15;
     const int qr = q0 + row;
     if (qr < a.S) {
-      const char* base = row < 64 ? kimg : vimg;
-      const uint4 val = *reinterpret_cast<const uint4*>(base + img_off(row & 63, ch));
+      const uint4 val = *reinterpret_cast<const uint4*>(ost + img_off(row, ch));
       *reinterpret_cast<uint4*>(a.out + (((int64_t)b * a.S + qr) * a.H + hq) * AHD + ch * 8) = val;
     }
   }
@@ -276,7 +310,16 @@ extern "C" int lcq_attn_fwd_causal(const void* q, const void* k, const void* v, 
               "attention kernel: 16-byte aligned tensors required");
   a.S = (int)S; a.H = H; a.KVH = KVH;
   a.sl2 = scale * 1.44269504088896340736f;
-  const dim3 grid((unsigned)((S + AQT - 1) / AQT), (unsigned)H, (unsigned)B);
-  hipLaunchKernelGGL(k_attn_fwd_causal, grid, 256, 0, as_stream(stream), a);
+  static const int qb_env = [] {
+    const char* e = getenv("LCQ_ATTN_QB");  // probe override
+    return e ? atoi(e) : 1;
+  }();
+  if (qb_env != 2) {
+    const dim3 grid((unsigned)((S + AQT - 1) / AQT), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL(k_attn_fwd_causal<1>, grid, 256, 0, as_stream(stream), a);
+  } else {
+    const dim3 grid((unsigned)((S + 2 * AQT - 1) / (2 * AQT)), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL(k_attn_fwd_causal<2>, grid, 256, 0, as_stream(stream), a);
+  }
   return check_launch("lcq_attn_fwd_causal");
 }
