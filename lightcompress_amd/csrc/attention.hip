@@ -171,52 +171,60 @@ __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnAr
         for (int qb = 0; qb < QB; ++qb) s[qb][t] = mfma32(kf, qf[qb][kk], s[qb][t]);
       }
     }
-    // scale, causal mask, online softmax (exp2 domain), per query block
+    // causal mask, online softmax in the exp2 domain (scores scaled by scale * log2 e inside
+    // the exponent's fma; v_exp_f32 directly: results below 2^-126 flush to 0), per block
+    bool rescale = false;
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
       const bool diag = k0 + AKT - 1 > q0 + 32 * (QB * w + qb);  // a key can exceed a row
       float mx = -INFINITY;
+      if (diag) {  // wave-uniform; the per-key mask is an added 0 / -inf (no branches)
+        const int lim = min(qrow[qb], a.S - 1) - k0 - 4 * h;  // largest visible key offset
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int kofs = 32 * t + (r & 3) + 8 * (r >> 2);
+            s[qb][t][r] += (kofs > lim) ? -INFINITY : 0.f;
+          }
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float v = s[qb][t][r] * a.sl2;
-          if (diag) {
-            const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (key > qrow[qb] || key >= a.S) v = -INFINITY;
-          }
-          s[qb][t][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[qb][t][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * a.sl2;  // sl2 > 0: max commutes with the scale
       const float mn = fmaxf(m[qb], mx);
-      const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[qb] - mn);
+      const float alpha = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m[qb] - mn);
       const float msub = (mn == -INFINITY) ? 0.f : mn;
       float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[qb][t][r] - msub);
+          const float p = __builtin_amdgcn_exp2f(__fmaf_rn(s[qb][t][r], a.sl2, -msub));
           s[qb][t][r] = p;
           rs += p;
         }
       rs += __shfl_xor(rs, 32, 64);
       l[qb] = l[qb] * alpha + rs;
       m[qb] = mn;
+      rescale |= alpha != 1.f;
       if (h == 0) xch[w][32 * qb + c] = alpha;
     }
-    // rescale O: its registers hold rows (r & 3) + 8 (r >> 2) + 4 h of each 32-row block
+    // rescale O (skipped when no row's max moved: a multiply by 1 is exact): its registers
+    // hold rows (r & 3) + 8 (r >> 2) + 4 h of each 32-row block
     __builtin_amdgcn_wave_barrier();
+    if (__builtin_amdgcn_read_exec() && __any(rescale)) {
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      float ar[16];
+      for (int qb = 0; qb < QB; ++qb) {
+        float ar[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ar[r] = xch[w][32 * qb + (r & 3) + 8 * (r >> 2) + 4 * h];
+        for (int r = 0; r < 16; ++r) ar[r] = xch[w][32 * qb + (r & 3) + 8 * (r >> 2) + 4 * h];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
+        for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[qb][dt][r] *= ar[r];
+          for (int r = 0; r < 16; ++r) o[qb][dt][r] *= ar[r];
+      }
     }
     __builtin_amdgcn_wave_barrier();
     // P.V: k-step (t, s2) takes score registers 8 s2 .. 8 s2 + 7 of tile t; element j is key

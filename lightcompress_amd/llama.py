@@ -36,9 +36,10 @@ def _fused_apply_rotary(q, k, cos, sin, unsqueeze_dim=1):
 
 
 _ORIG_SDPA = None
-# the lcq flash kernel beats torch's SDPA (aotriton) up to this sequence length on MI355X
-# (S 512: 0.99 vs 1.65 ms; S 2048: 11.9 vs 10.8 ms, scripts/attn_rate.py); env override
-_LCQ_ATTN_MAX_S = int(os.environ.get('LCQ_ATTN_MAX_S', '1024'))
+# measured on MI355X (scripts/attn_rate.py, B 128, H 32, KV 8): the lcq flash kernel vs torch's
+# SDPA (aotriton) 0.87 vs 1.66 ms at S 512 (AWQ calibration), 9.26 vs 10.79 ms at S 2048 (GPTQ);
+# longer sequences (not measured) go to torch. Env override.
+_LCQ_ATTN_MAX_S = int(os.environ.get('LCQ_ATTN_MAX_S', '4096'))
 
 
 def _lcq_sdpa(module, query, key, value, attention_mask, dropout=0.0, scaling=None,
