@@ -397,7 +397,13 @@ def bench_gptq(args, rank, world, dev):
         elapsed = timed_blocks(lambda i: step(i + warm), 0, steps, world, dev)
     kern = timer.summary()
     ms = elapsed / steps * 1e3
-    out = {'linears_per_s': round(N_LINEARS_PER_BLOCK * steps * world / elapsed, 3),
+    # N > 1 runs the reference's data-parallel replica scheme (quant_out makes blocks
+    # sequential): every rank holds its own 128 x 2048 calibration tokens, the
+    # Hessians are all-reduced and the column loop is row-sharded, so the job quantizes the
+    # SAME 7 linears per block whatever N is (no x world in the linear count)
+    out = {'linears_per_s': round(N_LINEARS_PER_BLOCK * steps / elapsed, 3),
+           'parallelism': ('single GPU' if world == 1 else
+                           f'{world} replicas (Hessian all-reduce, row-sharded column loop)'),
            'ms_per_block': round(ms, 1), 'steps': steps, 'warmup': warm,
            'extrapolated_model_wall_s': round(ms * 32 / 1e3, 2),
            'workload': (f'Llama-3-8B GPTQ w4a16 g128 asym act-order true_sequential quant_out, '
