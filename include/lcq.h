@@ -148,6 +148,14 @@ int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, c
                    const void* z_in, void* s_out, void* z_out, int64_t ng_total, void* err,
                    void* losses, void* stream);
 
+/* GPTQ static groups (gptq.py:224-227, static_groups: True): the same block loop with fixed
+ * qparams per (row, ORIGINAL group): permuted column c uses s_in / z_in [rows, ngc] at group
+ * col_group[c] = perm[c] / group_size (int32 [ld]). z_in NULL for symmetric. */
+int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t col0, int count,
+                        const void* U, int64_t ldu, int qmin, int qmax, const void* s_in,
+                        const void* z_in, const int32_t* col_group, int64_t ngc, void* err,
+                        void* losses, void* stream);
+
 /* Diagonal tile of the recursive fp32 factorisation behind U = chol(H^-1, upper)
  * (gptq.py:169-174): for SPD A (n x n, n <= 128, row-major fp32, leading dim lda), X <- L^-1
  * and, if L is not NULL, L <- the lower Cholesky factor (upper parts zeroed). A is only read.

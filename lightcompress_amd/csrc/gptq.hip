@@ -33,6 +33,8 @@ struct GptqArgs {
   int64_t ng_total;
   float* err;         // [rows, 128]
   float* losses;      // optional [rows, ld]
+  const int32_t* cgroup;  // static groups: group of every (permuted) column, [ld]
+  int64_t ngc;            // static groups: groups per row of s_in / z_in
 };
 
 // 8 lanes per row, 16 consecutive block columns per lane (32 rows per 256-thread workgroup).
@@ -105,6 +107,17 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
     qs = valid ? a.s_in[r] : 1.f;
     qz = (valid && a.z_in) ? a.z_in[r] : 0.f;
   }
+  // static groups (GS < 0, gptq.py:224-227): column c takes the precomputed qparams of its
+  // ORIGINAL group, groups[perm[c] // group_size] -- per column, held per lane
+  float qsk[GS < 0 ? CPL : 1], qzk[GS < 0 ? CPL : 1];
+  if constexpr (GS < 0) {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int g = (cb + k < a.count) ? a.cgroup[a.col0 + cb + k] : 0;
+      qsk[k] = valid ? a.s_in[r * a.ngc + g] : 1.f;
+      qzk[k] = (valid && a.z_in) ? a.z_in[r * a.ngc + g] : 0.f;
+    }
+  }
   float ek[CPL], lk[CPL];
   const int rowlane = tid & ~(LPR - 1);
 #pragma unroll
@@ -114,10 +127,11 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
       // every lane evaluates its own column jl; only the owner's value is used
       const float d = u[c * GB + c];
       const float wc = w[jl];
-      float t = rintf(wc / qs);
-      t = t + qz;
+      const float cs = (GS < 0) ? qsk[jl] : qs, cz = (GS < 0) ? qzk[jl] : qz;
+      float t = rintf(wc / cs);
+      t = t + cz;
       t = fminf(fmaxf(t, a.qmin), a.qmax);
-      const float q = (t - qz) * qs;
+      const float q = (t - cz) * cs;
       const float diff = wc - q;
       const float e = __shfl(diff / d, rowlane | owner, 64);
       if (sub == owner) {
@@ -352,3 +366,29 @@ extern "C" int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, 
                      ldu);
   return check_launch("lcq_gptq_trailing");
 }
+
+extern "C" int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t col0, int count,
+                                   const void* U, int64_t ldu, int qmin, int qmax,
+                                   const void* s_in, const void* z_in, const int32_t* col_group,
+                                   int64_t ngc, void* err, void* losses, void* stream) {
+  LCQ_REQUIRE(rows > 0 && ld > 0 && count > 0 && count <= GB, "bad block shape");
+  LCQ_REQUIRE(col0 >= 0 && col0 + count <= ld && col0 + count <= ldu, "block out of range");
+  LCQ_REQUIRE(col0 % GB == 0, "col0 must be a multiple of the 128-column blocksize");
+  LCQ_REQUIRE(ld % 4 == 0 && ldu % 4 == 0, "row lengths must be multiples of 4 (16-B rows)");
+  LCQ_REQUIRE(qmax > qmin, "qmax <= qmin");
+  LCQ_REQUIRE(s_in != nullptr && col_group != nullptr && ngc > 0, "static groups need qparams");
+  GptqArgs a{};
+  a.W = reinterpret_cast<float*>(W);
+  a.rows = rows; a.ld = ld; a.col0 = col0; a.count = count;
+  a.U = reinterpret_cast<const float*>(U); a.ldu = ldu;
+  a.qmin = (float)qmin; a.qmax = (float)qmax;
+  a.s_in = reinterpret_cast<const float*>(s_in);
+  a.z_in = reinterpret_cast<const float*>(z_in);
+  a.cgroup = col_group; a.ngc = ngc;
+  a.err = reinterpret_cast<float*>(err);
+  a.losses = reinterpret_cast<float*>(losses);
+  const dim3 grid((unsigned)((rows + (256 / LPR) - 1) / (256 / LPR)));
+  hipLaunchKernelGGL((k_gptq_block<-1>), grid, 256, 0, as_stream(stream), a);
+  return check_launch("lcq_gptq_block_cols");
+}
+

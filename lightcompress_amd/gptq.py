@@ -42,8 +42,6 @@ class GPTQ(BaseBlockwiseQuantization):
         self.chunk_num = sp.get('chunk_num', 1)
         if self.owq:
             raise NotImplementedError('OWQ is not on the device path yet (SURVEY.md §8f)')
-        if self.static_groups:
-            raise NotImplementedError('static_groups is not on the device path yet')
         if self.blocksize != gptq_core.BLOCK:
             raise NotImplementedError('device GPTQ uses blocksize 128')
         self.need_perm = (self.wquantizer.granularity == 'per_group' and not self.static_groups
@@ -146,14 +144,14 @@ class GPTQ(BaseBlockwiseQuantization):
         prepared = self._prepared(acc, replicate, ws)
         W = torch.cat([layer.weight.data for _, layer in grp], 0)
         fixed = None
-        if self.wquantizer.granularity != 'per_group':
+        if self.wquantizer.granularity != 'per_group' or self.static_groups:
             s = torch.cat([layer.buf_scales.reshape(-1, 1) for _, layer in grp], 0)
             z = None if self.wquantizer.sym else torch.cat(
                 [layer.buf_zeros.reshape(-1, 1) for _, layer in grp], 0)
             fixed = (s, z)
         r = gptq_core.quantize_layer(W, None, self.wquantizer, actorder=self.actorder,
                                      percdamp=self.percdamp, fixed=fixed, shard_rows=replicate,
-                                     prepared=prepared)
+                                     prepared=prepared, static_groups=self.static_groups)
         ng = 1 if r['scales'] is None else r['scales'].shape[0] // W.shape[0]
         o0 = 0
         for _, layer in grp:
@@ -175,11 +173,12 @@ class GPTQ(BaseBlockwiseQuantization):
         replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
         self._prepared(acc, replicate, ws)
         fixed = None
-        if self.wquantizer.granularity != 'per_group':
+        if self.wquantizer.granularity != 'per_group' or self.static_groups:
             fixed = (layer.buf_scales, getattr(layer, 'buf_zeros', None))
         r = gptq_core.quantize_layer(layer.weight.data, None, self.wquantizer,
                                      actorder=self.actorder, percdamp=self.percdamp,
-                                     fixed=fixed, shard_rows=replicate, prepared=acc.prepared)
+                                     fixed=fixed, shard_rows=replicate, prepared=acc.prepared,
+                                     static_groups=self.static_groups)
         layer.weight.data = r['weight']
         if r['perm'] is not None:
             layer.register_buffer('buf_perm', r['perm'])
@@ -196,7 +195,8 @@ class GPTQ(BaseBlockwiseQuantization):
     # ---- deploy (gptq.py:411-459) --------------------------------------------------------------
     @torch.no_grad()
     def w_q(self, module, wquantizer):
-        args = {'scales': module.buf_scales.to(self.model_dtype), 'zeros': module.buf_zeros,
+        args = {'scales': module.buf_scales.to(self.model_dtype),
+                'zeros': getattr(module, 'buf_zeros', None),
                 'qmax': module.buf_qmax, 'qmin': module.buf_qmin}
         return wquantizer.real_quant_weight_static(module.weight.data, args)
 

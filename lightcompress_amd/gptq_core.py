@@ -247,7 +247,7 @@ def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
 @torch.no_grad()
 def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
                 qmin: int, qmax: int, fixed=None, losses: bool = False,
-                superblock: int | None = None):
+                superblock: int | None = None, col_group: torch.Tensor | None = None):
     """Blocked OBS loop (gptq.py:198-244) on permuted fp32 W, in place.
 
     Per 128-column block: the HIP kernel runs the in-block sequential loop (bit-exact rank-1
@@ -260,7 +260,8 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     rows, cols = W.shape
     dev = W.device
     U = U.contiguous()
-    ng = 0 if group is None else -(-cols // group)
+    static = col_group is not None  # static_groups: fixed qparams of the original groups
+    ng = 0 if (group is None or static) else -(-cols // group)
     s_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng else None
     z_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng and not sym else None
     if superblock is None:
@@ -269,7 +270,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     errT = torch.empty((SB, rows), dtype=torch.float32, device=dev)  # k-major stacked Err1
     L = torch.zeros_like(W) if losses else None
     s_in = z_in = None
-    if group is None:
+    if group is None or static:
         s_in = fixed[0].reshape(-1).float().contiguous()
         z_in = None if sym else fixed[1].reshape(-1).float().contiguous()
     for sb0 in range(0, cols, SB):
@@ -278,8 +279,11 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
             i2 = min(i1 + BLOCK, cols)
             cnt = i2 - i1
             e = errT[i1 - sb0:]
-            ops.gptq_block(W, i1, cnt, U, group or 0, qmin, qmax, sym, s_out, z_out, e, L,
-                           s_in, z_in)
+            if static:
+                ops.gptq_block_cols(W, i1, cnt, U, qmin, qmax, s_in, z_in, col_group, e, L)
+            else:
+                ops.gptq_block(W, i1, cnt, U, group or 0, qmin, qmax, sym, s_out, z_out, e, L,
+                               s_in, z_in)
             if i2 < sb1:  # near columns: the rest of this superblock
                 ops.gptq_trailing(W, i1, cnt, i2, e, U, c2=sb1)
         if sb1 < cols:    # far columns: the whole superblock's errors at once
@@ -289,7 +293,8 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
 
 @torch.no_grad()
 def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder=True,
-                   percdamp=0.01, fixed=None, losses=False, shard_rows=False, prepared=None):
+                   percdamp=0.01, fixed=None, losses=False, shard_rows=False, prepared=None,
+                   static_groups=False):
     """Full GPTQ transform of one linear. Returns dict(weight fp32 (original column order),
     scales / zeros [rows*ng, 1] fp32 (merge_qparams order, permuted groups), perm, invperm,
     loss). ``prepared`` = prepare_hessian(...) output shared by linears with the same input
@@ -297,12 +302,19 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
     bit, sym = wquantizer.bit, wquantizer.sym
     qmin, qmax = int(wquantizer.qmin.item()), int(wquantizer.qmax.item())
     group = wquantizer.group_size if wquantizer.granularity == 'per_group' else None
-    if group is not None and group not in (32, 64, 128):
+    if group is not None and not static_groups and group not in (32, 64, 128):
         raise NotImplementedError('device GPTQ supports group_size 32/64/128')
     if prepared is None:
         prepared = prepare_hessian(H, actorder, percdamp)
     U, perm, dead = prepared
     Wp = prepare_weight(W, perm, dead)
+    col_group = None
+    if static_groups and group is not None:
+        # gptq.py:224-227: permuted column j quantizes with groups[perm[j] // group_size], the
+        # qparams collected from the ORIGINAL weights (fixed = buf_scales / buf_zeros)
+        cols = Wp.shape[1]
+        src = perm if perm is not None else torch.arange(cols, device=Wp.device)
+        col_group = (src // group).to(torch.int32).contiguous()
     if shard_rows:
         # rows are independent given U: every rank runs the column loop on its
         # row range, then the quantized rows + qparams are all-gathered (bit-identical to 1 GPU)
@@ -310,15 +322,17 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
         rank, world = P.dist_world()
         r0, r1 = P.row_shard(Wp.shape[0], rank, world)
         Wl = Wp[r0:r1].contiguous()
-        fx = None if fixed is None else tuple(None if f is None else f.reshape(-1)[r0:r1]
-                                              for f in fixed)
-        s, z, L = column_loop(Wl, U, bit, sym, group, qmin, qmax, fixed=fx, losses=losses)
+        fx = None if fixed is None else tuple(
+            None if f is None else f.reshape(Wp.shape[0], -1)[r0:r1] for f in fixed)
+        s, z, L = column_loop(Wl, U, bit, sym, group, qmin, qmax, fixed=fx, losses=losses,
+                              col_group=col_group)
         Wp = P.gather_rows(Wl, Wp.shape[0])
         s = None if s is None else P.gather_rows(s, Wp.shape[0])
         z = None if z is None else P.gather_rows(z, Wp.shape[0])
         L = None if L is None else P.gather_rows(L, Wp.shape[0])
     else:
-        s, z, L = column_loop(Wp, U, bit, sym, group, qmin, qmax, fixed=fixed, losses=losses)
+        s, z, L = column_loop(Wp, U, bit, sym, group, qmin, qmax, fixed=fixed, losses=losses,
+                              col_group=col_group)
     invperm = torch.argsort(perm) if perm is not None else None
     weight = Wp[:, invperm] if invperm is not None else Wp
     return dict(weight=weight, scales=None if s is None else s.reshape(-1, 1),

@@ -197,6 +197,18 @@ def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: i
            N.ptr(z_out), int(ng_total), N.ptr(err), N.ptr(losses), N.stream_of(W))
 
 
+def gptq_block_cols(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, qmin: int,
+                    qmax: int, s_in: torch.Tensor, z_in, col_group: torch.Tensor,
+                    err: torch.Tensor, losses=None):
+    """gptq_block with static per-(row, original group) qparams s_in / z_in [rows, ngc] and
+    the permuted column -> group map col_group (int32 [ld])."""
+    rows, ld = W.shape
+    ngc = s_in.numel() // rows
+    N.call('lcq_gptq_block_cols', N.ptr(W), rows, ld, int(col0), int(count), N.ptr(U), U.shape[1],
+           int(qmin), int(qmax), N.ptr(s_in), N.ptr(z_in), N.ptr(col_group), int(ngc), N.ptr(err),
+           N.ptr(losses), N.stream_of(W))
+
+
 def _ld(t: torch.Tensor) -> int:
     if t.dim() != 2 or t.stride(1) != 1:
         raise ValueError('expected a row-major 2-D view')

@@ -54,10 +54,12 @@ def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
 
 
 def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
-                blocksize: int = 128, fixed=None):
+                blocksize: int = 128, fixed=None, static=None):
     """gptq.py:198-244 on permuted fp32 W (modified in place to the compensated weights).
 
     group=None with fixed=(scale[rows,1], zero) -> per-channel fixed qparams.
+    static=(scales [rows, ng], zeros | None, perm | None): static_groups (gptq.py:224-227,
+    split_qparams :333-341) -- permuted column j uses original group perm[j] // group.
     Returns (tmp, Losses, scales [rows, ng], zeros [rows, ng] | None)."""
     qmin, qmax = Q.int_range(bit, sym)
     rows, cols = W.shape
@@ -71,7 +73,11 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
         tmp1, Err1, L1 = torch.zeros_like(W1), torch.zeros_like(W1), torch.zeros_like(W1)
         for i in range(i2 - i1):
             w, d = W1[:, i], U1[i, i]
-            if group is not None and (i1 + i) % group == 0:
+            if static is not None:
+                ss, zs, sp = static
+                g = (int(sp[i1 + i]) if sp is not None else i1 + i) // group
+                qp = (ss[:, g:g + 1], torch.tensor(0.0) if zs is None else zs[:, g:g + 1])
+            elif group is not None and (i1 + i) % group == 0:
                 ct = W[:, i1 + i:min(i1 + i + group, cols)]
                 t = Q.group_view(ct, 'per_group', group)
                 mn, mx = Q.minmax(t)
@@ -87,7 +93,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
             Err1[:, i] = err1
         tmp[:, i1:i2], Losses[:, i1:i2] = tmp1, L1
         W[:, i2:] -= Err1.matmul(U[i1:i2, i2:])
-    if group is None:
+    if group is None or static is not None:
         return tmp, Losses, None, None
     ng = len(groups)
     scales = torch.stack([groups[g][0] for g in range(ng)], dim=1).reshape(rows, ng)
@@ -107,6 +113,20 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor, bit=4, sym=False, group=128
     weight = tmp[:, invperm] if invperm is not None else tmp
     return dict(weight=weight, scales=s.reshape(-1, 1), zeros=None if z is None else z.reshape(-1, 1),
                 perm=perm, invperm=invperm, U=U, loss=Losses.sum().item())
+
+
+def quantize_layer_static(W: torch.Tensor, H: torch.Tensor, scales, zeros, bit=4, sym=False,
+                          group=128, actorder=True, percdamp=0.01, blocksize=128):
+    """GPTQ with static_groups: the group qparams (buf_scales / buf_zeros [rows*ng, 1],
+    collected from the original weights) are used as they are and stay the layer's qparams."""
+    Wp, U, perm = prepare(W, H, actorder, percdamp)
+    rows = Wp.shape[0]
+    st = (scales.reshape(rows, -1), None if sym else zeros.reshape(rows, -1), perm)
+    tmp, Losses, _, _ = column_loop(Wp, U, bit, sym, group, blocksize, static=st)
+    invperm = torch.argsort(perm) if perm is not None else None
+    weight = tmp[:, invperm] if invperm is not None else tmp
+    return dict(weight=weight, scales=scales, zeros=zeros, perm=perm, invperm=invperm, U=U,
+                loss=Losses.sum().item())
 
 
 def deploy_fake(weight, scales, zeros, perm, invperm, bit, sym, group, model_dtype):

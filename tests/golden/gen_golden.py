@@ -373,6 +373,71 @@ def gen_fp8():
 GENERATORS['fp8'] = gen_fp8
 
 
+def gen_gptq_static():
+    """GPTQ with static_groups (gptq.py:224-227): the group qparams collected from the
+    original weights before the transform are used unchanged; with actorder the permuted
+    column j takes group perm[j] // group_size."""
+    import torch.nn as nn
+    R.init_dist()
+    q = R.quant_module()
+    import llmc.compression.quantization.gptq as gm
+    cases = [
+        # name, oc, ic, bit, sym, group, actorder, dead_cols
+        ('int4_asym_g128_act', 192, 512, 4, False, 128, True, False),
+        ('int4_sym_g64_act_dead', 128, 384, 4, True, 64, True, True),
+        ('int4_asym_g128_noact', 128, 256, 4, False, 128, False, False),
+        ('int8_asym_g32_act', 64, 256, 8, False, 32, True, False),
+    ]
+    for i, (name, oc, ic, bit, sym, gs, act, dead) in enumerate(cases):
+        torch.manual_seed(2000 + i)
+        layer = nn.Linear(ic, oc, bias=False)
+        layer.weight.data = weights(oc, ic, torch.bfloat16, 400 + i, edge=False)
+        xs = _acts(3, 48, ic, 500 + i)
+        if dead:
+            for x in xs:
+                x[..., 3] = 0
+                x[..., 101] = 0
+        obj = gm.GPTQ.__new__(gm.GPTQ)
+        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_group', group_size=gs)
+        obj.dev = torch.device('cpu')
+        obj.model_dtype = torch.bfloat16
+        obj.owq, obj.actorder, obj.static_groups = False, act, True
+        obj.percdamp, obj.blocksize, obj.chunk_num = 0.01, 128, 1
+        obj.true_sequential = True
+        obj.need_perm = False  # gptq.py:52-56
+        obj.layers_cache = {'l': {}}
+        obj.qparams = {}
+        gm.GPTQ.layer_init(obj, layer, 'l')
+        for x in xs:
+            gm.GPTQ.add_batch(obj, layer, 'l', x, None)
+        H = obj.layers_cache['l']['H'].clone()
+        _, s0, z0, qmax, qmin = obj.wquantizer.get_tensor_qparams(layer.weight.data)
+        layer.register_buffer('buf_scales', s0)
+        layer.register_buffer('buf_zeros', z0)
+        layer.register_buffer('buf_qmax', torch.tensor(qmax))
+        layer.register_buffer('buf_qmin', torch.tensor(qmin))
+        w_in = layer.weight.data.clone()
+        obj.layers_cache['l']['H'] = H.clone()
+        obj.initialize_qparams_and_prepare_weights(layer, 'l')
+        Wp, U = obj.process_hessian_and_weights(layer, 'l')
+        obj.layers_cache['l']['H'] = H.clone()
+        obj.qparams = {}
+        layer.weight.data = w_in.clone()
+        obj.layer_transform(layer, 'l')
+        out = dict(x=torch.cat(xs, 0), w=w_in, H=H, U=U,
+                   perm=getattr(layer, 'buf_perm', None), weight=layer.weight.data.clone(),
+                   scales=layer.buf_scales, zeros=None if sym else layer.buf_zeros,
+                   meta=torch.tensor([bit, int(sym), gs, int(act), oc, ic]))
+        out['fq'] = obj.w_qdq(layer, obj.wquantizer)
+        codes, s_rq, z_rq = obj.w_q(layer, obj.wquantizer)
+        out.update(codes=codes, scales_rq=s_rq, zeros_rq=z_rq)
+        F.save(f'gptqsg_{name}', **out)
+    print('gptq static_groups fixtures written')
+
+
+GENERATORS['gptq_static'] = gen_gptq_static
+
+
 if __name__ == '__main__':
     which = sys.argv[1] if len(sys.argv) > 1 else 'all'
     R.install()

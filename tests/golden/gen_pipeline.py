@@ -115,7 +115,9 @@ def run_reference(name, spec):
         algo = algo_cls(model, config.quant, model.get_first_block_input(),
                         model.get_padding_mask(), config)
     diag = {}
-    if spec['quant']['method'] == 'GPTQ':   # diagnostics: each layer's finished Hessian
+    if not spec.get('diag', True):
+        pass
+    elif spec['quant']['method'] == 'GPTQ':   # diagnostics: each layer's finished Hessian
         orig = algo_cls.initialize_qparams_and_prepare_weights
 
         def snap(self, layer, lname, _o=orig):

@@ -13,6 +13,15 @@ CONFIGS = {
                                    'blocksize': 128, 'true_sequential': True},
                        'quant_out': True},
              'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}},
+    # static_groups (gptq.py:224-227); deployed weights only (Hessians pinned by 'gptq')
+    'gptq_static': {'quant': {'method': 'GPTQ',
+                              'weight': {'bit': 4, 'symmetric': False,
+                                         'granularity': 'per_group', 'group_size': 64},
+                              'special': {'actorder': True, 'static_groups': True,
+                                          'percdamp': 0.01, 'blocksize': 128,
+                                          'true_sequential': True},
+                              'quant_out': True},
+                    'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}, 'diag': False},
     'awq': {'quant': {'method': 'Awq',
                       'weight': {'bit': 4, 'symmetric': True, 'granularity': 'per_group',
                                  'group_size': 128},

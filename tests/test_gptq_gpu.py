@@ -261,3 +261,108 @@ def test_static_cols_equals_permuted_static(dev, sym, group):
                                     qmin, qmax, ct_dtype=torch.float32,
                                     fq_dtype=torch.bfloat16)
     assert torch.equal(got.view(torch.int16), ref.contiguous().view(torch.int16))
+
+
+# ---- static_groups (gptq.py:224-227) ---------------------------------------------------------
+def _static_inputs(c, sym, act):
+    W = c['w'].float().clone()
+    dead = torch.diag(c['H']) == 0
+    W[:, dead] = 0
+    perm = c['perm'] if act else None
+    if act:
+        W = W[:, perm]
+    rows = W.shape[0]
+    s = c['scales'].reshape(rows, -1).float()
+    z = None if sym else c['zeros'].reshape(rows, -1).float()
+    return W, s, z, perm
+
+
+@pytest.mark.parametrize('name', F.names('gptqsg_'))
+def test_static_block_bit_exact_vs_oracle(dev, name):
+    """lcq_gptq_block_cols on the first 128 permuted columns (no trailing GEMM): bit-exact
+    against the oracle's static_groups column loop, losses included."""
+    from lightcompress_amd import gptq_core
+    c = F.load(name)
+    bit, sym, gs, act, oc, ic = _meta(c)
+    qmin, qmax = Q.int_range(bit, sym)
+    W, s, z, perm = _static_inputs(c, sym, act)
+    W = W[:, :128].contiguous()
+    U = c['U'][:128, :128].contiguous()
+    tmp, L, _, _ = G.column_loop(W.clone(), U, bit, sym, gs,
+                                 static=(s, z, None if perm is None else perm[:128]))
+    src = perm[:128] if perm is not None else torch.arange(128)
+    cg = (src // gs).to(torch.int32).to(dev)
+    Wd = W.to(dev)
+    _, _, L_d = gptq_core.column_loop(Wd, U.to(dev), bit, sym, gs, int(qmin), int(qmax),
+                                      fixed=(s.to(dev), None if z is None else z.to(dev)),
+                                      losses=True, col_group=cg)
+    assert torch.equal(Wd.cpu(), tmp)
+    assert torch.equal(L_d.cpu(), L)
+
+
+@pytest.mark.parametrize('name', F.names('gptqsg_'))
+def test_static_column_loop_given_reference_U(dev, name):
+    from lightcompress_amd import gptq_core
+    c = F.load(name)
+    bit, sym, gs, act, oc, ic = _meta(c)
+    qmin, qmax = Q.int_range(bit, sym)
+    W, s, z, perm = _static_inputs(c, sym, act)
+    src = perm if perm is not None else torch.arange(ic)
+    cg = (src // gs).to(torch.int32).to(dev)
+    Wd = W.contiguous().to(dev)
+    so, zo, _ = gptq_core.column_loop(Wd, c['U'].to(dev), bit, sym, gs, int(qmin), int(qmax),
+                                      fixed=(s.to(dev), None if z is None else z.to(dev)),
+                                      col_group=cg)
+    assert so is None and zo is None  # static qparams are not re-estimated
+    w = Wd.cpu()
+    if act:
+        w = w[:, torch.argsort(perm)]
+    torch.testing.assert_close(w, c['weight'], rtol=1e-4, atol=1e-6)
+    zz = c['zeros'] if not sym else torch.tensor(0.0)
+    def codes(wt):  # need_perm is False: original column order
+        return Q.quant(Q.group_view(wt, 'per_group', gs), c['scales'], zz, qmin, qmax)
+    agree = (codes(w) == codes(c['weight'])).float().mean().item()
+    assert agree >= 0.999, agree
+
+
+@pytest.mark.parametrize('name', F.names('gptqsg_'))
+def test_static_plugin_layer_vs_reference(dev, name):
+    """The GPTQ plugin's layer_transform with static_groups (MFMA Hessian, device Cholesky,
+    HIP loop) vs the reference: qparams untouched, deployed fake-quant >= 99.9 % equal, and
+    real-quant codes from w_q equal where the weights agree."""
+    from lightcompress_amd import gptq_core
+    from lightcompress_amd.gptq import GPTQ
+    from lightcompress_amd.gptq_core import HessianAccumulator
+    from lightcompress_amd.quant import IntegerQuantizer
+    c = F.load(name)
+    bit, sym, gs, act, oc, ic = _meta(c)
+    wq = IntegerQuantizer(bit, sym, 'per_group', group_size=gs)
+    layer = torch.nn.Linear(ic, oc, bias=False, device=dev, dtype=torch.bfloat16)
+    layer.weight.data = c['w'].to(dev)
+    s0 = c['scales'].to(dev)
+    layer.register_buffer('buf_scales', s0.clone())
+    if not sym:
+        layer.register_buffer('buf_zeros', c['zeros'].to(dev).clone())
+    layer.register_buffer('buf_qmax', wq.qmax.clone().to(dev))
+    layer.register_buffer('buf_qmin', wq.qmin.clone().to(dev))
+    obj = GPTQ.__new__(GPTQ)
+    obj.wquantizer = wq
+    obj.actorder, obj.static_groups, obj.percdamp = act, True, 0.01
+    obj.need_perm = False
+    obj.model_dtype = torch.bfloat16
+    obj.config = {}
+    acc = HessianAccumulator(ic, dev)
+    for x in c['x']:
+        acc.add_batch(x.unsqueeze(0).to(dev))
+    acc.prepared = None
+    obj.layers_cache = {'l': {'acc': acc, 'owner': True, 'columns': ic}}
+    obj.parallel_mode = lambda: 'single'
+    obj.layer_transform(layer, 'l')
+    assert torch.equal(layer.buf_scales, s0)  # gptq.py:195: static groups keep their qparams
+    fq = obj.w_qdq(layer, wq).cpu()
+    same = (fq == c['fq']).float().mean().item()
+    assert same >= 0.999, same
+    assert torch.allclose(fq.float(), c['fq'].float(), atol=2 * c['scales'].abs().max().item())
+    codes, _, _ = obj.w_q(layer, wq)
+    eq = (codes.cpu() == c['codes']).float().mean().item()
+    assert eq >= 0.999, eq

@@ -59,3 +59,47 @@ def test_column_loop_exact_given_reference_U(name):
     assert torch.equal(s.reshape(-1, 1), c['scales'])
     if not sym:
         assert torch.equal(z.reshape(-1, 1), c['zeros'])
+
+
+SG_CASES = F.names('gptqsg_')
+
+
+@pytest.mark.parametrize('name', SG_CASES)
+def test_static_groups_exact_given_reference_U(name):
+    """static_groups (gptq.py:224-227): with the reference's U, the oracle column loop under
+    the construction-time group qparams reproduces the reference weights bit for bit, and the
+    layer's qparams are left as collected."""
+    c = F.load(name)
+    bit, sym, gs, act, oc, ic = _meta(c)
+    W = c['w'].float().clone()
+    dead = torch.diag(c['H']) == 0
+    W[:, dead] = 0
+    perm = c['perm'] if act else None
+    if act:
+        W = W[:, perm]
+    rows = W.shape[0]
+    st = (c['scales'].reshape(rows, -1), None if sym else c['zeros'].reshape(rows, -1), perm)
+    tmp, _, _, _ = G.column_loop(W, c['U'], bit, sym, gs, static=st)
+    if act:
+        tmp = tmp[:, torch.argsort(perm)]
+    assert torch.equal(tmp, c['weight'])
+    # the qparams the reference kept are those of the ORIGINAL weights
+    s0 = Q.qparams(*Q.minmax(Q.group_view(c['w'], 'per_group', gs)), *Q.int_range(bit, sym),
+                   sym)[0]
+    torch.testing.assert_close(s0.float().reshape(-1, 1), c['scales'].float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize('name', SG_CASES)
+def test_static_groups_layer_and_deploy(name):
+    c = F.load(name)
+    bit, sym, gs, act, oc, ic = _meta(c)
+    r = G.quantize_layer_static(c['w'], c['H'], c['scales'], c.get('zeros'), bit, sym, gs, act)
+    if act:
+        assert torch.equal(r['perm'], c['perm'])
+    same_w = (r['weight'] == c['weight']).float().mean().item()
+    assert same_w > 0.999, same_w
+    # need_perm is False with static_groups: w_qdq quantizes the original column order
+    fq = G.deploy_fake(r['weight'], c['scales'], c.get('zeros'), None, None, bit, sym, gs,
+                       torch.bfloat16)
+    agree = (fq == c['fq']).float().mean().item()
+    assert agree > 0.9999, agree

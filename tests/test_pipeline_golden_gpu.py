@@ -160,3 +160,20 @@ def test_gptq_pipeline_vs_reference(dev, monkeypatch):
             assert rel < 2e-2, k
         else:
             assert rel < 5e-2, k
+
+
+def test_gptq_static_groups_pipeline_vs_reference(dev):
+    """static_groups + act-order (group 64) through the whole block loop: the group qparams
+    are the construction-time ones, so the first subset (identical inputs) deploys >= 99.5 %
+    bit-equal (measured 100 %) and every later linear stays close to the reference (T2)."""
+    ref, got, _ = run_ours('gptq_static', dev)
+    res = compare(ref, got)
+    for k in ('b0__self_attn__q_proj', 'b0__self_attn__k_proj', 'b0__self_attn__v_proj'):
+        assert res[k] >= 0.995, k
+    # later layers: inputs already differ in the last bits (module docstring) and GPTQ's error
+    # feedback spreads each flipped code along its row (measured 78 .. 99 % bit-equal, every
+    # max |dw| 2.7e-2)
+    for k, eq in res.items():
+        assert eq >= 0.7, k
+        d = (ref[k].float() - got[k].float()).abs().max().item()
+        assert d < 0.05, k

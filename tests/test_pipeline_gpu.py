@@ -1,6 +1,8 @@
 """End-to-end plugin pipeline on a tiny random Llama (2 blocks) on the GPU: Awq (+clip),
 GPTQ (act-order, true_sequential, quant_out) and RTN through run_block_loop + deploy, with the
 reference's YAML config schema."""
+import copy
+
 import pytest
 import torch
 
@@ -36,8 +38,12 @@ GPTQ_CFG = {'quant': {'method': 'GPTQ', 'weight': {'bit': 4, 'symmetric': False,
                                   'blocksize': 128, 'true_sequential': True},
                       'quant_out': True}}
 
+GPTQ_SG_CFG = copy.deepcopy(GPTQ_CFG)
+GPTQ_SG_CFG['quant']['special']['static_groups'] = True
 
-@pytest.mark.parametrize('cfg', [AWQ_CFG, GPTQ_CFG], ids=['awq', 'gptq'])
+
+@pytest.mark.parametrize('cfg', [AWQ_CFG, GPTQ_CFG, GPTQ_SG_CFG],
+                         ids=['awq', 'gptq', 'gptq_static'])
 def test_pipeline_runs_and_deploys(dev, cfg):
     from lightcompress_amd.pipeline import build_algo
     from lightcompress_amd.utils import load_config
@@ -55,10 +61,10 @@ def test_pipeline_runs_and_deploys(dev, cfg):
     y = y[0] if isinstance(y, tuple) else y
     assert torch.isfinite(y).all()
     # deployed fake-quant weights take at most 16 values per 128-group (groups live in the
-    # act-order permuted column space for GPTQ)
+    # act-order permuted column space for GPTQ, in the original one with static_groups)
     m = model.blocks[0].mlp.down_proj
     w = m.weight.float()
-    if hasattr(m, 'buf_perm'):
+    if hasattr(m, 'buf_perm') and not getattr(algo, 'static_groups', False):
         w = w[:, m.buf_perm]
     w = w.reshape(-1, 128)
     assert max(len(torch.unique(r)) for r in w[:64]) <= 16
@@ -159,17 +165,18 @@ def test_save_quantized_checkpoint(dev, tmp_path, target):
         assert any(k.endswith('q_proj.qzeros') for k in keys)
 
 
-def test_gptq_concatenated_rows_bit_identical(dev):
+@pytest.mark.parametrize('static', [False, True], ids=['dynamic', 'static_groups'])
+def test_gptq_concatenated_rows_bit_identical(dev, static):
     """q/k/v (and gate/up) quantized as one column loop over their concatenated rows give the
     same weights and qparams, bit for bit, as one loop per linear."""
-    import copy
     from lightcompress_amd.gptq import GPTQ
     from lightcompress_amd.pipeline import build_algo
     from lightcompress_amd.utils import load_config
     out = []
     for concat in (True, False):
         model = tiny_model(dev)
-        algo = build_algo(model, load_config(copy.deepcopy(GPTQ_CFG)), calib(model))
+        algo = build_algo(model, load_config(copy.deepcopy(GPTQ_SG_CFG if static else GPTQ_CFG)),
+                          calib(model))
         algo.concat_rows = concat
         algo.run_block_loop()
         st = {}
