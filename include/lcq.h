@@ -95,6 +95,16 @@ int lcq_int_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols,
                          int fq_dtype, void* codes_out, int codes_dtype, void* packed_out,
                          int pack_bits, void* stream);
 
+/* Per-tensor static qparams given as 0-dim tensors on the reference's CPU path
+ * (fake_quant_act_static with register_act_qparams' scale / zero, quant.py:699-743): torch-CPU
+ * takes a 0-dim operand as a scalar of the op's opmath type, so the fp32 scale / zero (device
+ * fp32, one element each; zero NULL = 0) enter every op at full precision while each result is
+ * rounded to ct_dtype. x [rows, cols], cols % 8 == 0. */
+int lcq_int_quant_static_scalar(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                                const void* scale, const void* zero, int ct_dtype, int qmin,
+                                int qmax, void* fq_out, int fq_dtype, void* codes_out,
+                                int codes_dtype, void* stream);
+
 /* Static quant with a column -> group map: element (r, c) uses scales/zeros group
  * r * ngc + col_group[c] (int32 [cols], 16-byte aligned). GPTQ's act-order deploy
  * (gptq.py:411-459 w_qdq: fake_quant_static(W[:, perm])[:, invperm]) with
@@ -317,6 +327,37 @@ int lcq_silu_mul(const void* gate, const void* up, int dtype, int64_t n, void* o
  * row; x, out [rows, H] contiguous, weight [H] (same dtype). */
 int lcq_rmsnorm(const void* x, const void* weight, int dtype, int64_t rows, int64_t H,
                 float eps, void* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Static activation calibration (per-tensor, `act: {static: True}`): register_act_qparams
+ * (base_blockwise_quantization.py:567-588) -> get_batch_tensors_qparams (quant.py:561-586).
+ * ------------------------------------------------------------------------------------- */
+/* Scratch (float2 count) per launch of lcq_minmax_segments: LCQ_MINMAX_SEGS segments at a time,
+ * at most LCQ_MINMAX_PARTS workgroups each. */
+#define LCQ_MINMAX_PARTS 32
+#define LCQ_MINMAX_SEGS 64
+#define LCQ_MINMAX_WORKSPACE (LCQ_MINMAX_PARTS * LCQ_MINMAX_SEGS)
+
+/* torch.min / torch.max of each of nseg device tensors (segs[i]: host array of device pointers,
+ * 16-byte aligned, seg_lens[i] > 0 elements, dtype F32 / F16 / BF16), NaN-propagating like torch:
+ * get_minmax_stats (quant.py:221-251) on per_tensor ranges (quant.py:132-135). minmax: device
+ * fp32 [2 * nseg] = (min, max) per segment, exact. workspace: LCQ_MINMAX_WORKSPACE device
+ * float2. */
+int lcq_minmax_segments(const void* const* segs, const int64_t* seg_lens, int64_t nseg,
+                        int dtype, void* minmax, void* workspace, void* stream);
+
+#define LCQ_CALIB_STATIC_MINMAX 0        /* quant.py:253-262: mean of the per-segment ranges */
+#define LCQ_CALIB_STATIC_MOVING_MINMAX 1 /* quant.py:431-450: EMA (alpha) in the range dtype */
+
+/* Static per-tensor qparams from lcq_minmax_segments' ranges: the range (static_minmax: fp32
+ * means, sum then / nseg; static_moving_minmax: m += alpha * (v - m) with every op rounded to
+ * range_dtype), then get_qparams (quant.py:545-559) with torch's 0-dim type promotion: the
+ * scale (and zero) computed in / rounded to scale_dtype (the caller's promote(range dtype,
+ * qmax [- qmin] dtype)). out: device fp32 [4] = scale, zero, min, max (each exactly
+ * representable in its dtype). */
+int lcq_act_static_qparams(const void* minmax, int64_t nseg, int algo, float alpha,
+                           int range_dtype, int scale_dtype, int sym, float qmin, float qmax,
+                           void* out, void* stream);
 
 #ifdef __cplusplus
 }

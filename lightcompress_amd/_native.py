@@ -39,6 +39,8 @@ SIGNATURES = {
                                _vp, _int, _vp, _int, _vp, _int, _vp, _vp, _vp], _int),
     'lcq_int_quant_static': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _int, _int,
                               _int, _vp, _int, _vp, _int, _vp, _int, _vp], _int),
+    'lcq_int_quant_static_scalar': ([_vp, _int, _i64, _i64, _vp, _vp, _int, _int, _int, _vp,
+                                     _int, _vp, _int, _vp], _int),
     'lcq_int_quant_static_cols': ([_vp, _int, _i64, _i64, _vp, _i64, _vp, _int, _vp, _int,
                                    _int, _int, _int, _vp, _int, _vp, _int, _vp], _int),
     'lcq_attn_fwd_causal': ([_vp, _vp, _vp, _int, _i64, _i64, _int, _int, _int, _vp, _vp, _vp,
@@ -77,6 +79,9 @@ SIGNATURES = {
                                  _vp, _vp, _vp], _int),
     'lcq_fp8_block_to_tensor_many': ([_int, _vp, _i64, _int, _int, _int, _f32, _f32, _int, _vp,
                                       _vp, _vp], _int),
+    'lcq_minmax_segments': ([_vp, _vp, _i64, _int, _vp, _vp, _vp], _int),
+    'lcq_act_static_qparams': ([_vp, _i64, _int, _f32, _int, _int, _int, _f32, _f32, _vp, _vp],
+                               _int),
     'lcq_fp_emul_quant': ([_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int, _vp], _int),
 }
 

@@ -218,8 +218,11 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
             self.aquantizer = self.act_quant_module(**qc['act'])
             self.act_static = qc['act'].get('static', False)
             if self.act_static:
-                raise NotImplementedError('static activation calibration is not on the device '
-                                          'path yet (SURVEY.md §8f rank 3)')
+                assert qc['act']['granularity'] == 'per_tensor', \
+                    'Only support per_tensor static quant'
+            for k in ('quant_attn', 'quant_act_fn'):
+                if qc['act'].get(k, False):
+                    raise NotImplementedError(f'act.{k} (non-linear quant) is out of scope')
         else:
             self.w_only, self.aquantizer, self.act_static = True, None, False
         self.quant_kvcache = 'kvcache' in qc
@@ -397,12 +400,46 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
             else:
                 subset_kwargs = {}
             self.subset_transform(subset, input_feat, subset_kwargs)
+            if self.act_static:
+                self.register_act_qparams(subset['layers'], input_feat[subset['input'][0]])
             if self.true_sequential and index != len(subsets) - 1:
                 nxt = subsets[index + 1]
                 input_feat.update(self.rehook_next_subset(block, subset, nxt))
 
     def subset_transform(self, subset, input_feat, subset_kwargs):
         raise NotImplementedError
+
+    # ---- static activation qparams (:567-588) --------------------------------------------------
+    def _reference_entries(self, feats):
+        """The calibration entries as the reference's hooks hold them: block_forward may run
+        the stored entries as one stacked batch, so its captured input is split back into the
+        entries' batch sizes (the reference calibrates per entry, or per sample when there is
+        a single entry)."""
+        sizes = [x.shape[0] for x in (self.input or {}).get('data', [])]
+        if (len(feats) == 1 and len(sizes) > 1 and torch.is_tensor(feats[0])
+                and feats[0].shape[0] == sum(sizes)):
+            return list(torch.split(feats[0], sizes, dim=0))
+        return list(feats)
+
+    @torch.no_grad()
+    def register_act_qparams(self, layers_dict, act_tensors):
+        """base_blockwise_quantization.py:567-588: per-tensor static activation qparams from
+        the calibration inputs (HBM-resident, not copied), averaged over ranks in the
+        reference's replica mode, registered as buf_act_{scales,zeros,qmin,qmax}_{i}."""
+        entries = self._reference_entries(act_tensors)
+        scales_l, zeros_l, qmin_l, qmax_l = self.aquantizer.get_batch_tensors_qparams(entries)
+        _, ws, _ = world()
+        for i, (scales, zeros, qmin, qmax) in enumerate(zip(scales_l, zeros_l, qmin_l, qmax_l)):
+            if ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate':
+                dist.all_reduce(scales, op=dist.ReduceOp.SUM)
+                scales = scales / ws
+            for name, layer in layers_dict.items():
+                if not isinstance(layer, _LINEAR_TYPES):
+                    continue
+                layer.register_buffer(f'buf_act_scales_{i}', scales)
+                layer.register_buffer(f'buf_act_zeros_{i}', zeros)
+                layer.register_buffer(f'buf_act_qmin_{i}', qmin)
+                layer.register_buffer(f'buf_act_qmax_{i}', qmax)
 
     def rehook_next_subset(self, block, subset, next_subset):
         self.subset_init(next_subset)

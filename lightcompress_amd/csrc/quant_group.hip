@@ -35,6 +35,7 @@ struct QuantArgs {
   int pack_bits;
   void* s_out;
   void* z_out;
+  int qp_scalar;  // static: one fp32 scale / zero used at full precision (0-dim CPU operands)
 };
 
 __device__ __forceinline__ float ld_rt(const void* p, int dt, int64_t i) {
@@ -257,13 +258,17 @@ __global__ void __launch_bounds__(256) k_quant_static(QuantArgs a) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
     const int64_t e0 = t * 8;
-    const int64_t gi = e0 / a.group;
+    const int64_t gi = a.qp_scalar ? 0 : e0 / a.group;
     float w[8];
     ld8<XT>(a.x, e0, w);
 #pragma unroll
     for (int j = 0; j < 8; ++j) w[j] = rnd<CT>(w[j]);  // .to(compute dtype)
-    const float s = rnd<CT>(ld_rt(a.s_in, a.s_dt, gi));
-    const float z = a.z_in ? rnd<CT>(ld_rt(a.z_in, a.z_dt, gi)) : 0.f;
+    float s = ld_rt(a.s_in, a.s_dt, gi);
+    float z = a.z_in ? ld_rt(a.z_in, a.z_dt, gi) : 0.f;
+    if (!a.qp_scalar) {  // tensor operands are converted to the compute dtype
+      s = rnd<CT>(s);
+      z = rnd<CT>(z);
+    }
     float q[8], dq[8];
     qdq8<CT>(w, s, z, a.qmin, a.qmax, q, dq);
     emit<CT>(a, e0, q, dq);
@@ -430,6 +435,30 @@ extern "C" int lcq_int_quant_static(const void* x, int x_dtype, int64_t rows, in
   a.qmin = (float)qmin; a.qmax = (float)qmax; a.sym = zeros == nullptr;
   a.fq = fq_out; a.fq_dt = fq_dtype; a.codes = codes_out; a.codes_dt = codes_dtype;
   a.packed = packed_out; a.pack_bits = pack_bits;
+  hipStream_t st = as_stream(stream);
+  switch (x_dtype) {
+    case LCQ_F32: return launch_static_x<LCQ_F32>(a, ct_dtype, st);
+    case LCQ_BF16: return launch_static_x<LCQ_BF16>(a, ct_dtype, st);
+    default: return launch_static_x<LCQ_F16>(a, ct_dtype, st);
+  }
+}
+
+extern "C" int lcq_int_quant_static_scalar(const void* x, int x_dtype, int64_t rows,
+                                           int64_t cols, const void* scale, const void* zero,
+                                           int ct_dtype, int qmin, int qmax, void* fq_out,
+                                           int fq_dtype, void* codes_out, int codes_dtype,
+                                           void* stream) {
+  int64_t group = cols;
+  int rc = common_checks("lcq_int_quant_static_scalar", x_dtype, rows, cols, group, qmin, qmax,
+                         fq_out, fq_dtype, codes_out, codes_dtype, nullptr, 0);
+  if (rc) return rc;
+  LCQ_REQUIRE(scale != nullptr, "scale required");
+  LCQ_REQUIRE(is_float_dt(ct_dtype), "compute dtype must be float");
+  QuantArgs a{};
+  a.x = x; a.s_in = scale; a.s_dt = LCQ_F32; a.z_in = zero; a.z_dt = LCQ_F32;
+  a.rows = rows; a.cols = cols; a.group = group; a.qp_scalar = 1;
+  a.qmin = (float)qmin; a.qmax = (float)qmax; a.sym = zero == nullptr;
+  a.fq = fq_out; a.fq_dt = fq_dtype; a.codes = codes_out; a.codes_dt = codes_dtype;
   hipStream_t st = as_stream(stream);
   switch (x_dtype) {
     case LCQ_F32: return launch_static_x<LCQ_F32>(a, ct_dtype, st);

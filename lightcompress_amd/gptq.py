@@ -90,6 +90,8 @@ class GPTQ(BaseBlockwiseQuantization):
     def cache_input_hook(self, m, inp, out, name, feat_dict):
         if isinstance(m, _LINEAR_TYPES):
             self.add_batch(m, name, inp[0].data, None if out is None else out.data)
+        if self.act_static:  # gptq.py:250-251: static act qparams need the inputs themselves
+            super().cache_input_hook(m, inp, out, name, feat_dict)
 
     @torch.no_grad()
     def add_batch(self, layer, name, inp, out):

@@ -113,6 +113,30 @@ def int_quant_static(x: torch.Tensor, group: int, scales: torch.Tensor,
     return res
 
 
+def int_quant_static_scalar(x: torch.Tensor, scale: torch.Tensor, zero: torch.Tensor | None,
+                            qmin: int, qmax: int, *, ct_dtype: torch.dtype, fq: bool = True,
+                            codes_dtype: torch.dtype | None = None) -> dict:
+    """Quantize ``x`` [rows, cols] with one fp32 scale / zero kept at full precision (0-dim
+    CPU operands: torch's scalar semantics), every op rounded to ct_dtype."""
+    assert x.dim() == 2
+    x = x.contiguous()
+    rows, cols = x.shape
+    s = scale.reshape(1).to(torch.float32).contiguous()
+    z = None if zero is None else zero.reshape(1).to(torch.float32).contiguous()
+    res = {}
+    fq_t = codes_t = None
+    if fq:
+        fq_t = torch.empty((rows, cols), dtype=ct_dtype, device=x.device)
+        res['fq'] = fq_t
+    if codes_dtype is not None:
+        codes_t = torch.empty((rows, cols), dtype=codes_dtype, device=x.device)
+        res['codes'] = codes_t
+    N.call('lcq_int_quant_static_scalar', N.ptr(x), N.dt(x), rows, cols, N.ptr(s), N.ptr(z),
+           N.dt(ct_dtype), int(qmin), int(qmax), N.ptr(fq_t), N.dt(ct_dtype) if fq else 0,
+           N.ptr(codes_t), N.dt(codes_dtype) if codes_t is not None else 0, N.stream_of(x))
+    return res
+
+
 def int_quant_static_cols(x: torch.Tensor, col_group: torch.Tensor, scales: torch.Tensor,
                           zeros: torch.Tensor | None, qmin: int, qmax: int, *,
                           ct_dtype: torch.dtype, fq_dtype: torch.dtype) -> torch.Tensor:
@@ -595,4 +619,44 @@ def attn_fwd_causal(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
            ctypes.addressof(strides[1]), ctypes.addressof(strides[2]), float(scale), N.ptr(out),
            N.stream_of(q))
     N.note_work('lcq_attn_fwd_causal', 2.0 * B * H * S * (S + 1) * D)  # causal QK^T + PV flops
+    return out
+
+
+# ---- static activation calibration (quant.py:561-586) ---------------------------------------
+MINMAX_WORKSPACE = 32 * 64  # LCQ_MINMAX_WORKSPACE (float2)
+CALIB_ALGOS = {'static_minmax': 0, 'static_moving_minmax': 1}
+
+
+def minmax_segments(segs) -> torch.Tensor:
+    """(torch.min, torch.max) of every tensor in ``segs`` (same dtype, device) as fp32 [n, 2]
+    (get_minmax_stats, quant.py:221-251, per_tensor ranges)."""
+    import ctypes
+    segs = [t if t.is_contiguous() else t.contiguous() for t in segs]
+    if not segs:
+        raise ValueError('no calibration tensors')
+    dev, dt = segs[0].device, segs[0].dtype
+    if any(t.dtype != dt or t.device != dev for t in segs):
+        raise ValueError('calibration tensors must share dtype and device')
+    n = len(segs)
+    ptrs = (ctypes.c_void_p * n)(*[N.ptr(t) for t in segs])
+    lens = (ctypes.c_int64 * n)(*[t.numel() for t in segs])
+    out = torch.empty((n, 2), dtype=torch.float32, device=dev)
+    ws = torch.empty((MINMAX_WORKSPACE, 2), dtype=torch.float32, device=dev)
+    N.call('lcq_minmax_segments', ctypes.cast(ptrs, ctypes.c_void_p),
+           ctypes.cast(lens, ctypes.c_void_p), n, N.dt(dt), N.ptr(out), N.ptr(ws),
+           N.stream_of(out))
+    N.note_work('lcq_minmax_segments', sum(t.numel() * t.element_size() for t in segs))
+    return out
+
+
+def act_static_qparams(minmax: torch.Tensor, algo: str, alpha: float, range_dtype: torch.dtype,
+                       scale_dtype: torch.dtype, sym: bool, qmin: float, qmax: float):
+    """Range (static_minmax / static_moving_minmax) + get_qparams on the device. Returns fp32
+    [4] = scale, zero, min, max."""
+    if algo not in CALIB_ALGOS:
+        raise ValueError(f'Unsupported calibration algorithm: {algo}')
+    out = torch.empty(4, dtype=torch.float32, device=minmax.device)
+    N.call('lcq_act_static_qparams', N.ptr(minmax.contiguous()), minmax.shape[0],
+           CALIB_ALGOS[algo], float(alpha), N.dt(range_dtype), N.dt(scale_dtype), int(bool(sym)),
+           float(qmin), float(qmax), N.ptr(out), N.stream_of(minmax))
     return out

@@ -92,5 +92,22 @@ def broadcast_block(block: torch.nn.Module, owner: int):
     rank, world = dist_world()
     if world == 1:
         return
-    for t in list(block.parameters()) + list(block.buffers()):
+    for t in block.parameters():
         dist.broadcast(t.data, src=owner)
+    # buffers the owner's transform registered (e.g. static act qparams buf_act_*) may not
+    # exist on the other ranks: publish the owner's buffer list first, create what is missing
+    spec = [None]
+    if rank == owner:
+        spec = [[(mn, bn, tuple(b.shape), str(b.dtype).split('.')[-1])
+                 for mn, m in block.named_modules() for bn, b in m.named_buffers(recurse=False)
+                 if b is not None]]
+    dist.broadcast_object_list(spec, src=owner)
+    mods = dict(block.named_modules())
+    dev = next(block.parameters(), next(block.buffers(), None))
+    dev = dev.device if dev is not None else torch.device('cpu')
+    for mn, bn, shape, dt in spec[0]:
+        m = mods[mn]
+        b = m._buffers.get(bn)
+        if b is None or tuple(b.shape) != shape or str(b.dtype).split('.')[-1] != dt:
+            m.register_buffer(bn, torch.empty(shape, dtype=getattr(torch, dt), device=dev))
+        dist.broadcast(m._buffers[bn].data, src=owner)

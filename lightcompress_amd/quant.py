@@ -9,8 +9,9 @@ live on the GPU.
 Supported on the device path (the hot path of SURVEY.md §8a): calib_algo ``minmax``,
 granularity per_group / per_channel / per_token / per_tensor / per_head (+ per_block for FP8),
 round_zp=True, bit 2..8, dynamic and static qparams, fake quant, real quant (+ vLLM / AutoAWQ
-packing in ``module_utils``); FP8 e4m3 / e5m2 (``FloatQuantizer``). Not yet supported (raise NotImplementedError): mse / hqq / learnable / static
-histogram calibration, ``int_indices`` mixed precision, STE rounding, ``rounding`` overrides.
+packing in ``module_utils``); FP8 e4m3 / e5m2 (``FloatQuantizer``); static per-tensor activation
+calibration (static_minmax / static_moving_minmax). Not yet supported (raise
+NotImplementedError): mse / hqq / learnable / static_hist calibration, ``int_indices`` mixed precision, STE rounding, ``rounding`` overrides.
 """
 from __future__ import annotations
 
@@ -35,6 +36,11 @@ def weight_cast_to_fp8(weight, block_size):
     r = ops.fp8_quant_blocks(weight, torch.float8_e4m3fn, 128, qmax=448.0, clamp_min=1e-5,
                              add_zero=True)
     return r['codes'], r['scales']
+
+
+# get_tensor_range (quant.py:122-130) falls back to min/max for the static_* algorithms, which
+# only change get_batch_tensors_qparams
+_MINMAX_LIKE = ('minmax', 'static_minmax', 'static_moving_minmax', 'static_hist')
 
 
 class BaseQuantizer:
@@ -120,7 +126,7 @@ class BaseQuantizer:
         raise NotImplementedError(f'granularity {g} is not on the device path yet')
 
     def _check_supported(self, args):
-        if self.calib_algo not in ('minmax',):
+        if self.calib_algo not in _MINMAX_LIKE:
             raise NotImplementedError(f'calib_algo={self.calib_algo} is not on the device path')
         if not self.round_zp:
             raise NotImplementedError('round_zp=False is not on the device path')
@@ -138,6 +144,57 @@ class BaseQuantizer:
 
     def get_tensor_range(self, tensor, args={}):
         return self.get_minmax_range(tensor)
+
+    # -- static activation calibration (quant.py:103-120, 221-262, 431-450, 561-586) --------
+    def reshape_batch_tensors(self, act_tensors):
+        """quant.py:103-120 without mutating the caller's list: one list of calibration
+        segments per module input (a single entry = one batch of samples, split per sample)."""
+        assert len(act_tensors) > 0, (
+            'Calibration data is insufficient. Please provide more data to ensure '
+            'all experts in the MOE receive an adequate number of tokens.')
+        if isinstance(act_tensors[0], tuple):
+            return [list(torch.stack(ts)) for ts in zip(*act_tensors)]
+        if len(act_tensors) == 1:
+            return [[act_tensors[0][i] for i in range(act_tensors[0].size(0))]]
+        return [list(act_tensors)]
+
+    def _static_scale_dtype(self, range_dtype):
+        qd = self.qmax.dtype if self.sym else torch.promote_types(self.qmax.dtype,
+                                                                  self.qmin.dtype)
+        if not qd.is_floating_point:
+            return range_dtype  # 0-dim float op 0-dim int -> the float dtype
+        return torch.promote_types(range_dtype, qd)
+
+    @torch.no_grad()
+    def get_batch_tensors_qparams(self, act_tensors, alpha=0.01, args={}):
+        """quant.py:561-586 on the device: per-segment torch.min / torch.max in one HBM pass
+        (``lcq_minmax_segments``), the range and get_qparams in one tiny kernel
+        (``lcq_act_static_qparams``). Returns (scales, zeros, qmin, qmax) lists, one entry per
+        module input, as 0-dim tensors with the reference's dtypes."""
+        if self.calib_algo == 'static_hist':
+            assert self.sym is True and self.granularity == 'per_tensor', \
+                'Only support per tensor static symmetric int quantize.'
+            raise NotImplementedError('static_hist calibration is not on the device path yet')
+        if self.calib_algo not in ops.CALIB_ALGOS:
+            raise ValueError(f'Unsupported calibration algorithm: {self.calib_algo}')
+        if self.granularity != 'per_tensor':
+            raise NotImplementedError('static activation qparams are per_tensor '
+                                      '(base_blockwise_quantization.py:181-184)')
+        if not self.round_zp:
+            raise NotImplementedError('round_zp=False is not on the device path')
+        scales_l, zeros_l, qmin_l, qmax_l = [], [], [], []
+        for tensors in self.reshape_batch_tensors(act_tensors):
+            dev = tensors[0].device
+            mm = ops.minmax_segments(tensors)
+            rdt = torch.float32 if self.calib_algo == 'static_minmax' else tensors[0].dtype
+            sdt = self._static_scale_dtype(rdt)
+            r = ops.act_static_qparams(mm, self.calib_algo, alpha, rdt, sdt, self.sym,
+                                       float(self.qmin), float(self.qmax))
+            scales_l.append(r[0].to(sdt))
+            zeros_l.append(torch.tensor(0.0, device=dev) if self.sym else r[1].to(sdt))
+            qmin_l.append(self.qmin.to(dev))
+            qmax_l.append(self.qmax.to(dev))
+        return scales_l, zeros_l, qmin_l, qmax_l
 
 
 class IntegerQuantizer(BaseQuantizer):
@@ -189,6 +246,20 @@ class IntegerQuantizer(BaseQuantizer):
     def _static(self, tensor, scales, zeros, want):
         t2 = tensor.reshape(-1, tensor.shape[-1]).contiguous()
         s = scales.contiguous()
+        if s.dim() == 0 and (not torch.is_tensor(zeros) or zeros.dim() == 0):
+            # per-tensor qparams as 0-dim tensors (static act qparams, per_tensor weights):
+            # torch-CPU uses them as scalars at full precision, results in the tensor's dtype
+            qmin, qmax = self._iq
+            z = None
+            if torch.is_tensor(zeros) and zeros.item() != 0 or (not torch.is_tensor(zeros)
+                                                                  and zeros):
+                z = torch.as_tensor(zeros, dtype=torch.float32, device=t2.device)
+            r = ops.int_quant_static_scalar(t2, s.to(t2.device), z, qmin, qmax,
+                                            ct_dtype=tensor.dtype, fq=want != 'codes',
+                                            codes_dtype=torch.int32 if want == 'codes' else None)
+            if want == 'codes':
+                return r['codes'].to(tensor.dtype).reshape(tensor.shape)
+            return r['fq'].reshape(tensor.shape)
         ng = s.numel()
         if t2.numel() % ng:
             raise ValueError('scales do not tile the tensor')
@@ -201,8 +272,8 @@ class IntegerQuantizer(BaseQuantizer):
         elif torch.is_tensor(zeros) and zeros.item() != 0 or (not torch.is_tensor(zeros) and zeros):
             zz = torch.full_like(s, float(zeros), dtype=s.dtype)
         ct = tensor.dtype if s.dim() == 0 else torch.promote_types(tensor.dtype, s.dtype)
-        if zz is not None and zz.is_floating_point():
-            ct = torch.promote_types(ct, zz.dtype)
+        if zz is not None and zz.is_floating_point() and torch.is_tensor(zeros) and zeros.dim() > 0:
+            ct = torch.promote_types(ct, zz.dtype)  # a 0-dim zero never promotes (torch rule)
         qmin, qmax = self._iq
         if want == 'codes':
             r = ops.int_quant_static(t2, group, s, zz, qmin, qmax, ct_dtype=ct, fq=False,
@@ -362,7 +433,7 @@ class FloatQuantizer(BaseQuantizer):
         return self.fp8_dtype
 
     def _check(self, args):
-        if self.calib_algo not in ('minmax',):
+        if self.calib_algo not in _MINMAX_LIKE:
             raise NotImplementedError(f'calib_algo={self.calib_algo} is not on the device path')
         if 'rounding' in args:
             raise NotImplementedError("args['rounding'] is not on the device path")

@@ -438,6 +438,60 @@ def gen_gptq_static():
 GENERATORS['gptq_static'] = gen_gptq_static
 
 
+def gen_act_static():
+    """Static per-tensor activation qparams (get_batch_tensors_qparams, quant.py:561-586) for
+    the act_tensors lists register_act_qparams passes: a single [n, T, H] entry (calib bs -1,
+    split per sample), n [1, T, H] entries (bs 1) or [b, T, H] entries (bs b). FP8: the
+    use_qtorch qparams (qmax = finfo.max, quant.py:982-996) on a use_qtorch=False object, as
+    in gen_fp8 (qtorch is absent here); int cases also pin fake_quant_act_static."""
+    q = R.quant_module()
+    cases = [
+        # name, quant, bit, sym, algo, n_entries, entry_bs, T, H, dtype
+        ('int8_sym_minmax_bs1', 'int', 8, True, 'static_minmax', 6, 1, 48, 256, torch.bfloat16),
+        ('int8_asym_minmax_single', 'int', 8, False, 'static_minmax', 1, 5, 32, 384,
+         torch.bfloat16),
+        ('int8_sym_moving_bs1', 'int', 8, True, 'static_moving_minmax', 7, 1, 40, 256,
+         torch.bfloat16),
+        ('int8_asym_moving_single', 'int', 8, False, 'static_moving_minmax', 1, 6, 32, 512,
+         torch.bfloat16),
+        ('int4_asym_moving_bs2_f16', 'int', 4, False, 'static_moving_minmax', 4, 2, 24, 256,
+         torch.float16),
+        ('int8_sym_minmax_bs3_f32', 'int', 8, True, 'static_minmax', 3, 3, 16, 128,
+         torch.float32),
+        ('int8_asym_moving_bs1_f32', 'int', 8, False, 'static_moving_minmax', 5, 1, 16, 256,
+         torch.float32),
+        ('fp8e4m3_minmax_bs1', 'e4m3', 8, True, 'static_minmax', 5, 1, 32, 256, torch.bfloat16),
+        ('fp8e4m3_moving_single', 'e4m3', 8, True, 'static_moving_minmax', 1, 6, 32, 256,
+         torch.bfloat16),
+        ('fp8e5m2_moving_bs1', 'e5m2', 8, True, 'static_moving_minmax', 4, 1, 32, 256,
+         torch.bfloat16),
+    ]
+    for i, (name, qt, bit, sym, algo, ne, eb, T, H, dt) in enumerate(cases):
+        g = torch.Generator().manual_seed(900 + i)
+        mag = torch.exp(torch.randn(H, generator=g))
+        shift = 0.3 * torch.randn(H, generator=g)   # asymmetric ranges
+        x = ((torch.randn(ne * eb, T, H, generator=g) + shift) * mag).to(dt)
+        entries = [x] if ne == 1 else [x[j * eb:(j + 1) * eb] for j in range(ne)]
+        if qt == 'int':
+            quant = q.IntegerQuantizer(bit, sym, 'per_tensor', calib_algo=algo)
+        else:
+            quant = q.FloatQuantizer(qt, True, 'per_tensor', calib_algo=algo, use_qtorch=False)
+            fi = torch.finfo(torch.float8_e4m3fn if qt == 'e4m3' else torch.float8_e5m2)
+            quant.qmin, quant.qmax = torch.tensor(fi.min), torch.tensor(fi.max)
+        sc, zc, qmn, qmx = quant.get_batch_tensors_qparams([e.clone() for e in entries])
+        out = dict(x=x, scales=sc[0], zeros=zc[0],
+                   meta=torch.tensor([ne, eb, bit if qt == 'int' else 0, int(sym),
+                                      ['static_minmax', 'static_moving_minmax'].index(algo)]))
+        if qt == 'int':
+            args = dict(scales=sc[0], zeros=zc[0], qmax=qmx[0], qmin=qmn[0])
+            out['fq'] = quant.fake_quant_act_static(entries[0].clone(), args)
+        F.save(f'actstatic_{qt}_{name}' if qt != 'int' else f'actstatic_{name}', **out)
+    print('act static fixtures written')
+
+
+GENERATORS['act_static'] = gen_act_static
+
+
 if __name__ == '__main__':
     which = sys.argv[1] if len(sys.argv) > 1 else 'all'
     R.install()

@@ -152,6 +152,8 @@ def run_reference(name, spec):
     for bi, block in enumerate(model.get_blocks()):
         for ln, lin in model.get_block_linears(block).items():
             out[f'b{bi}__{ln.replace(".", "__")}'] = lin.weight.data.clone()
+            if hasattr(lin, 'buf_act_scales_0'):  # static act qparams (register_act_qparams)
+                out[f'a_b{bi}__{ln.replace(".", "__")}'] = lin.buf_act_scales_0.detach().cpu()
     F.save(f'pipe_{name}', **out)
     print(f'pipe_{name}: {len(out) - 1} deployed linears')
 

@@ -35,6 +35,14 @@ CONFIGS = {
                                             'weight_clip': True, 'clip_sym': False},
                                 'quant_out': True},
                       'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}},
+    # configs/quantization/methods/RTN/rtn_w_a_pertensor_static.yml with calib_algo
+    # static_minmax (static_hist is not on the device path); deployed act scales compared too
+    'rtn_a8_static': {'quant': {'method': 'RTN',
+                                'weight': {'bit': 8, 'symmetric': True,
+                                           'granularity': 'per_channel', 'group_size': -1},
+                                'act': {'bit': 8, 'symmetric': True, 'granularity': 'per_tensor',
+                                        'static': True, 'calib_algo': 'static_minmax'}},
+                      'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}, 'diag': False},
     'rtn': {'quant': {'method': 'RTN',
                       'weight': {'bit': 8, 'symmetric': True, 'granularity': 'per_channel'}},
             'calib': None},

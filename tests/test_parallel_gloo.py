@@ -75,6 +75,18 @@ def _bcast(rank, world):
     return [m.weight.sum().item(), m.bias.sum().item()]
 
 
+def _bcast_owner_buffers(rank, world):
+    # the owner's transform registered static act qparams the other rank does not have
+    blk = torch.nn.Sequential(torch.nn.Linear(4, 2), torch.nn.Linear(2, 2))
+    blk[0].register_buffer('buf_scales', torch.full((2, 1), float(rank)))
+    if rank == 1:
+        blk[0].register_buffer('buf_act_scales_0', torch.tensor(0.125))
+        blk[1].register_buffer('buf_act_zeros_0', torch.tensor(3.0, dtype=torch.bfloat16))
+    P.broadcast_block(blk, owner=1)
+    return [blk[0].buf_scales.sum().item(), blk[0].buf_act_scales_0.item(),
+            str(blk[1].buf_act_zeros_0.dtype), blk[1].buf_act_zeros_0.item()]
+
+
 def test_allreduce_mean():
     res = run2(_mean)
     assert res[0] == res[1] == [1.5, 1.5, 1.5]
@@ -114,3 +126,8 @@ def test_shards_cover_exactly_once(world):
     spans = [P.row_shard(1000, r, world) for r in range(world)]
     assert spans[0][0] == 0 and spans[-1][1] == 1000
     assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+def test_broadcast_block_creates_owner_only_buffers():
+    res = run2(_bcast_owner_buffers)
+    assert res[0] == res[1] == [2.0, 0.125, 'torch.bfloat16', 3.0]

@@ -87,6 +87,8 @@ def run_ours(name, dev, monkeypatch=None):
     for bi, block in enumerate(model.get_blocks()):
         for ln, lin in model.get_block_linears(block).items():
             got[f'b{bi}__{ln.replace(".", "__")}'] = lin.weight.data.detach().cpu()
+            if hasattr(lin, 'buf_act_scales_0'):  # static act qparams
+                diag[f'a_b{bi}__{ln.replace(".", "__")}'] = lin.buf_act_scales_0.detach().cpu()
     return ref, got, diag
 
 
@@ -177,3 +179,24 @@ def test_gptq_static_groups_pipeline_vs_reference(dev):
         assert eq >= 0.7, k
         d = (ref[k].float() - got[k].float()).abs().max().item()
         assert d < 0.05, k
+
+
+def test_rtn_static_act_pipeline_vs_reference(dev):
+    """RTN w8a8 with static per-tensor activation qparams (rtn_w_a_pertensor_static.yml,
+    static_minmax): the reference's block loop registers buf_act_scales_0 on every linear from
+    its calibration inputs. Deployed weights bit-equal (T1); the first subset's inputs are
+    identical, so its act scale equals the reference's (the fp32 mean may differ in its last
+    bit: sum order, T2); later inputs come from GPU vs CPU float forwards (module docstring)."""
+    ref, got, diag = run_ours('rtn_a8_static', dev)
+    assert all(eq == 1.0 for eq in compare(ref, got).values())
+    akeys = sorted(k for k in ref if k.startswith('a_'))
+    assert sorted(diag) == akeys and len(akeys) == 14
+    for k in akeys:
+        r, o = ref[k], diag[k]
+        assert r.dtype == o.dtype and r.shape == o.shape, k
+        rel = abs(o.item() - r.item()) / abs(r.item())
+        print(f'{k:32s} act scale {o.item():.8e} ref {r.item():.8e} rel {rel:.1e}')
+        if k.startswith('a_b0__self_attn') and not k.endswith('o_proj'):
+            assert rel <= 2 ** -23, k
+        else:
+            assert rel < 1e-2, k
