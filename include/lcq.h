@@ -186,16 +186,34 @@ int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, int cnt, in
  * AWQ (awq.py) and auto-clip (auto_clip.py) building blocks. dtype = BF16/F16/F32; each op
  * rounds to dtype like the reference's torch expressions.
  * ------------------------------------------------------------------------------------- */
-/* Awq.get_act_scale (awq.py:74-85): out[c] = mean_t |x[t, c]|. x [n, c]; workspace holds
- * splits*c fp64 partial sums (deterministic two-pass reduction). */
+/* Workspace bytes of lcq_absmean_cols / lcq_awq_weight_scale for a [rows, cols] input. */
+int64_t lcq_colmean_workspace_bytes(int64_t rows, int64_t cols);
+
+/* Awq.get_act_scale (awq.py:74-85): out[c] = mean_t |x[t, c]| (x [n, c], c % 8 == 0), summed in
+ * torch-CPU's exact order (its fp32 4-level cascade over rows, SumKernel.cpp; exact for
+ * c % 64 == 0) and rounded like mean_out (fp32 sum / n -> dtype). */
 int lcq_absmean_cols(const void* x, int dtype, int64_t n, int64_t c, void* out,
-                     void* workspace, int splits, void* stream);
+                     void* workspace, void* stream);
+
+/* Awq.get_weight_scale (awq.py:48-72), one linear of the subset per call (layer = 0 ..
+ * nlayers - 1, in the subset's order): |w| / max|w| per group of `group` columns (rounded to
+ * dtype), mean over rows (same cascade as lcq_absmean_cols), accumulated into total [cols]
+ * (dtype): layer 0 writes, later layers add (rounded), the last divides by nlayers.
+ * group / 8 must be a power of two <= 64. */
+int lcq_awq_weight_scale(const void* w, int dtype, int64_t rows, int64_t cols, int64_t group,
+                         int layer, int nlayers, void* total, void* workspace, void* stream);
 
 /* Awq.get_scales, trans_version v2 (awq.py:87-108): s = pow(x, ratio_dt) (exponent already
  * rounded to dtype by the caller, correctly rounded pow) ; clamp(min=1e-4) ;
  * s / sqrt(max(s) * min(s)). xmean, out [c]. */
 int lcq_awq_scales(const void* xmean, int dtype, int64_t c, float ratio_dt, void* out,
                    void* stream);
+
+/* Awq.get_scales, trans_version v1 (awq.py:87-108): s = pow(x, ratio_dt) / pow(wmax,
+ * wexp_dt) (both exponents rounded to dtype by the caller: ratio and 1 - ratio), then as
+ * lcq_awq_scales. wmax [c] from lcq_awq_weight_scale. */
+int lcq_awq_scales_v1(const void* xmean, const void* wmax, int dtype, int64_t c,
+                      float ratio_dt, float wexp_dt, void* out, void* stream);
 
 /* Broadcast scale: out = x * s (op 0) or x / s (op 1), s per column (axis 0, [cols]) or per
  * row (axis 1, [rows]); in place allowed. Replaces scaling_input / update_input_feat /

@@ -56,7 +56,10 @@ SIGNATURES = {
                              _i64, _vp, _vp, _vp], _int),
     'lcq_chol_inv_tile': ([_vp, _i64, _int, _vp, _i64, _vp, _i64, _vp, _i64, _vp], _int),
     'lcq_gptq_trailing': ([_vp, _i64, _i64, _i64, _int, _i64, _i64, _vp, _vp, _i64, _vp], _int),
-    'lcq_absmean_cols': ([_vp, _int, _i64, _i64, _vp, _vp, _int, _vp], _int),
+    'lcq_colmean_workspace_bytes': ([_i64, _i64], _i64),
+    'lcq_absmean_cols': ([_vp, _int, _i64, _i64, _vp, _vp, _vp], _int),
+    'lcq_awq_weight_scale': ([_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp], _int),
+    'lcq_awq_scales_v1': ([_vp, _vp, _int, _i64, _f32, _f32, _vp, _vp], _int),
     'lcq_awq_scales': ([_vp, _int, _i64, _f32, _vp, _vp], _int),
     'lcq_scale_bcast': ([_vp, _int, _i64, _i64, _vp, _int, _int, _vp, _vp], _int),
     'lcq_sq_diff_mean': ([_vp, _vp, _int, _i64, _vp, _int, _vp, _int, _vp], _int),

@@ -1,4 +1,4 @@
-"""AWQ (drop-in for llmc ``quantization/awq.py``; trans_version v2, clip v1).
+"""AWQ (drop-in for llmc ``quantization/awq.py``; trans_version v1 / v2, clip v1).
 
 Device design of ``search_scale_subset`` (awq.py:178-278):
 * the calibration input, the original module output and the original weights stay in HBM;
@@ -31,9 +31,8 @@ class Awq(BaseBlockwiseQuantization):
         self.save_scale = special.get('save_scale', False)
         self.awq_bs = special.get('awq_bs', None)
         self.save_mem = special.get('save_mem', True)
-        if self.trans_version != 'v2':
-            raise NotImplementedError('trans_version v1 (weight-scale term) is not on the '
-                                      'device path yet')
+        if self.trans_version not in ('v1', 'v2'):
+            raise ValueError(f'trans_version {self.trans_version}')
         self.n_grid = 20
         self.last_search = {}
         self._org_cache = {}
@@ -112,8 +111,18 @@ class Awq(BaseBlockwiseQuantization):
                  for i in range(x.shape[0] // self._bs)]
         return sum(means) / len(means)
 
-    def get_scales(self, prev_op, x_mean, ratio, out=None):
-        return ops.awq_scales(x_mean, ratio, out=out)
+    def get_weight_scale(self, layers_dict):
+        """awq.py:48-72 (trans_version v1): one pass per linear, HBM-resident."""
+        wq = self.wquantizer
+        if wq.granularity != 'per_group':
+            raise NotImplementedError('trans_version v1 supports per_group weights')
+        return ops.awq_weight_scale([m.weight.data for m in layers_dict.values()],
+                                    wq.group_size)
+
+    def get_scales(self, prev_op, x_mean, ratio, out=None, w_max=None):
+        return ops.awq_scales(x_mean, ratio, out=out,
+                              w_max=w_max if getattr(self, 'trans_version', 'v2') == 'v1'
+                              else None)
 
     def inspect_module_forward(self, x, inspect_module, kwargs):
         if self._bs == x.shape[0]:
@@ -146,6 +155,8 @@ class Awq(BaseBlockwiseQuantization):
         self._bs = x.shape[0] if self.awq_bs is None else self.awq_bs
         kwargs = subset_kwargs[0] if isinstance(subset_kwargs, list) else subset_kwargs
         layers = list(layers_dict.values())
+        v1 = getattr(self, 'trans_version', 'v2') == 'v1'
+        w_max = self.get_weight_scale(layers_dict) if v1 else None
         orig_w = [fc.weight.data for fc in layers]
         qbufs = [torch.empty_like(w) for w in orig_w]
         x_tmp = torch.empty_like(x)
@@ -156,7 +167,7 @@ class Awq(BaseBlockwiseQuantization):
         try:
             for n in range(self.n_grid):
                 ratio = n * 1 / self.n_grid
-                s = self.get_scales(prev_op, x_mean, ratio, out=all_scales[n])
+                s = self.get_scales(prev_op, x_mean, ratio, out=all_scales[n], w_max=w_max)
                 for fc, buf in zip(layers, qbufs):
                     fc.weight.data = self.fake_quantize_weight(fc, s, buf)
                 self.scaling_input(x, s, False, out=x_tmp)

@@ -3,7 +3,9 @@
 // Reference: llmc/compression/quantization/awq.py and auto_clip.py. Every op rounds to the
 // weight/activation dtype like the reference's torch-bf16 expressions:
 //   get_act_scale      awq.py:74-85     mean_t |x|                        -> lcq_absmean_cols
+//   get_weight_scale   awq.py:48-72     mean_rows |w| / group max          -> lcq_awq_weight_scale
 //   get_scales (v2)    awq.py:87-108    s = x^r ; clamp 1e-4 ; s/sqrt(max*min) -> lcq_awq_scales
+//   get_scales (v1)    awq.py:87-108    s = x^r / w^(1-r) ; ...            -> lcq_awq_scales_v1
 //   scaling_input / update_input_feat / scale_ln_fcs / scale_fc_fc
 //                      base_blockwise_quantization.py:631-778, 880-897  -> lcq_scale_bcast
 //   calculate_loss     awq.py:134-145   mean((org-out).float()^2)        -> lcq_sq_diff_mean
@@ -14,38 +16,114 @@
 namespace lcq {
 
 // ----------------------------------------------------------------------------------------
-// mean over rows of |x| per column: pass 1 writes fp32 partial sums for row slices,
-// pass 2 sums the slices in fixed order (deterministic), divides by n, rounds to DT.
+// Column means in torch-CPU's exact summation order.
+//
+// x.abs().view(-1, H).mean(0) (get_act_scale, awq.py:74-85) and layer_scale.mean(0)
+// (get_weight_scale, awq.py:48-72) are fp32 sums over rows then / rows (bf16/fp16 inputs:
+// mean_out sums in fp32). torch-CPU's outer-dimension sum (SumKernel.cpp multi_row_sum, per
+// column lane, independent of the SIMD width when cols % 64 == 0) is a 4-level cascade with
+// blocks of LS = 2^lp rows, lp = max(4, ceil_log2(rows) / 4):
+//   acc0 = sequential sum of a block; acc1 += acc0 at every block end; at every LS^2-row
+//   boundary acc2 += acc1 (acc1 = 0); at every LS^3-row boundary acc3 += acc2 (acc2 = 0);
+//   tail rows -> acc0; result = ((acc0 + acc1) + acc2) + acc3.
+// Pass 1: one thread per (8 columns, LS^2-row superblock) -> acc1 of the superblock (and the
+// tail's acc0); pass 2: one thread per column folds the superblocks in the same order.
 // ----------------------------------------------------------------------------------------
-template <int DT>
-__global__ void __launch_bounds__(256) k_absmean_p1(const void* x, int64_t n, int64_t c,
-                                                   int64_t rows_per_split, double* part) {
-  const int64_t c8 = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 8-column chunk
-  if (c8 * 8 >= c) return;
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
-  const int64_t r1 = min(n, r0 + rows_per_split);
-  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t r = r0; r < r1; ++r) {
-    float v[8];
-    ld8<DT>(x, r * c + c8 * 8, v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += (double)fabsf(v[j]);
-  }
-  double* p = part + (int64_t)blockIdx.y * c + c8 * 8;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) p[j] = acc[j];
+__host__ __device__ inline int colsum_lp(int64_t rows) {
+  int cl = 0;
+  while (((int64_t)1 << cl) < rows) ++cl;  // ceil_log2
+  return cl / 4 > 4 ? cl / 4 : 4;
 }
 
-template <int DT>
-__global__ void __launch_bounds__(256) k_absmean_p2(const double* part, int splits, int64_t n,
-                                                   int64_t c, void* out) {
+// MODE 0: value = |x| ; MODE 1: value = rnd(|w| / max|w| over its group of G columns)
+// (get_weight_scale's abs_weights.div_(max_vals)); G / 8 lanes, a power of two <= 64.
+template <int DT, int MODE>
+__global__ void __launch_bounds__(256) k_colsum_l1(const void* x, int64_t rows, int64_t c,
+                                                  int lp, int glanes, float* part,
+                                                  float* tail) {
+  const int64_t c8 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = c8 * 8 < c;
+  const int64_t LS = (int64_t)1 << lp, SB = LS * LS;
+  const int64_t r0 = (int64_t)blockIdx.y * SB;
+  const int64_t r1 = min(rows, r0 + SB);
+  const int64_t nfull = r0 + (r1 - r0) / LS * LS;  // end of the full blocks
+  float acc1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, acc0[8];
+  int64_t r = r0;
+  for (; r < r1; r += LS) {
+    const int64_t re = min(r1, r + LS);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc0[j] = 0.f;
+    for (int64_t rr = r; rr < re; ++rr) {
+      float v[8];
+      if (live) ld8<DT>(x, rr * c + c8 * 8, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fabsf(v[j]);
+      if constexpr (MODE == 1) {
+        float m = v[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) m = fmaxf(m, v[j]);
+        for (int o = 1; o < glanes; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = rnd<DT>(v[j] / m);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc0[j] += v[j];
+    }
+    if (re - r == LS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc1[j] += acc0[j];
+    }
+  }
+  if (!live) return;
+  float* p = part + (int64_t)blockIdx.y * c + c8 * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) p[j] = acc1[j];
+  if (r1 == rows) {  // last superblock: the tail rows' sequential sum (0 if none)
+    const bool has_tail = nfull < rows;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tail[c8 * 8 + j] = has_tail ? acc0[j] : 0.f;
+  }
+}
+
+// fold -> column sum, / rows, rounded to DT. MODE 0: out = mean. MODE 1 (get_weight_scale
+// over the subset's layers): layer 0 out = mean, then out = rnd(out + mean), and after the
+// last layer out = rnd(out / nlayers).
+template <int DT, int MODE>
+__global__ void __launch_bounds__(256) k_colsum_fold(const float* part, const float* tail,
+                                                    int64_t rows, int64_t c, int lp, int layer,
+                                                    int nlayers, void* out) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= c) return;
-  double s = 0.0;
-  for (int i = 0; i < splits; ++i) s += part[(int64_t)i * c + j];
-  // the reference's fp32 sum is an approximation of this (near-)exact sum; its bf16 mean is
-  // the correctly rounded fp32(sum) / n (parity tier T3)
-  st1<DT>(out, j, (float)s / (float)n);
+  const int64_t LS = (int64_t)1 << lp, SB = LS * LS;
+  const int64_t mask = LS - 1;
+  const int64_t nsb = (rows + SB - 1) / SB;
+  const int64_t nfull_sb = rows / SB;
+  float acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+  for (int64_t sb = 0; sb < nfull_sb; ++sb) {
+    const int64_t i = (sb + 1) * SB;
+    acc2 += part[sb * c + j];
+    if ((i & (mask << (2 * lp))) == 0) {
+      acc3 += acc2;
+      acc2 = 0.f;
+    }
+  }
+  if (nsb > nfull_sb) acc1 = part[nfull_sb * c + j];  // the partial superblock's full blocks
+  float acc0 = tail[j];
+  acc0 += acc1;
+  acc0 += acc2;
+  acc0 += acc3;
+  const float mean = rnd<DT>(acc0 / (float)rows);
+  if constexpr (MODE == 0) {
+    st1<DT>(out, j, mean);
+  } else {
+    float t = layer == 0 ? mean : rnd<DT>(ld1<DT>(out, j) + mean);
+    if (layer == nlayers - 1) t = rnd<DT>(t / (float)nlayers);
+    st1<DT>(out, j, t);
+  }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -56,13 +134,17 @@ __global__ void __launch_bounds__(256) k_absmean_p2(const double* part, int spli
 // ----------------------------------------------------------------------------------------
 template <int DT>
 __global__ void __launch_bounds__(1024) k_awq_scales(const void* xmean, int64_t c, float r,
-                                                    void* out) {
+                                                    void* out, const void* wmax, float r1) {
   __shared__ float red[2][16];
   const float lo = rnd<DT>(1e-4f);
   float mx = -INFINITY, mn = INFINITY;
   for (int64_t j = threadIdx.x; j < c; j += blockDim.x) {
     const float xv = ld1<DT>(xmean, j);
     float s = rnd<DT>((float)pow((double)xv, (double)r));
+    if (wmax) {  // v1: x^r / w^(1 - r), the second exponent also rounded to DT by the caller
+      const float wv = rnd<DT>((float)pow((double)ld1<DT>(wmax, j), (double)r1));
+      s = rnd<DT>(s / wv);
+    }
     s = fmaxf(s, lo);
     mx = fmaxf(mx, s);
     mn = fminf(mn, s);
@@ -370,45 +452,83 @@ __global__ void __launch_bounds__(256) k_clip_apply(const void* x, int64_t rows,
 
 using namespace lcq;
 
+extern "C" int64_t lcq_colmean_workspace_bytes(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int lp = colsum_lp(rows);
+  const int64_t SB = (int64_t)1 << (2 * lp);
+  return (((rows + SB - 1) / SB) + 1) * cols * (int64_t)sizeof(float);
+}
+
+template <int DT, int MODE>
+static void launch_colmean(const void* x, int64_t rows, int64_t c, int glanes, int layer,
+                           int nlayers, void* out, void* workspace, hipStream_t st) {
+  const int lp = colsum_lp(rows);
+  const int64_t SB = (int64_t)1 << (2 * lp);
+  const int64_t nsb = (rows + SB - 1) / SB;
+  float* part = reinterpret_cast<float*>(workspace);
+  float* tail = part + nsb * c;
+  dim3 g1((unsigned)((c / 8 + 255) / 256), (unsigned)nsb);
+  hipLaunchKernelGGL((k_colsum_l1<DT, MODE>), g1, 256, 0, st, x, rows, c, lp, glanes, part, tail);
+  hipLaunchKernelGGL((k_colsum_fold<DT, MODE>), dim3((unsigned)((c + 255) / 256)), 256, 0, st,
+                     part, tail, rows, c, lp, layer, nlayers, out);
+}
+
 extern "C" int lcq_absmean_cols(const void* x, int dtype, int64_t n, int64_t c, void* out,
-                                void* workspace, int splits, void* stream) {
+                                void* workspace, void* stream) {
   LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16 || dtype == LCQ_F32, "bad dtype");
   LCQ_REQUIRE(n > 0 && c > 0 && c % 8 == 0, "c must be a positive multiple of 8");
-  LCQ_REQUIRE(splits >= 1 && workspace, "workspace of splits*c fp64 required");
+  LCQ_REQUIRE(workspace, "workspace of lcq_colmean_workspace_bytes(n, c) required");
   hipStream_t st = as_stream(stream);
-  const int64_t rps = (n + splits - 1) / splits;
-  dim3 g1((unsigned)((c / 8 + 255) / 256), (unsigned)splits);
-  double* part = reinterpret_cast<double*>(workspace);
   switch (dtype) {
-    case LCQ_BF16:
-      hipLaunchKernelGGL((k_absmean_p1<LCQ_BF16>), g1, 256, 0, st, x, n, c, rps, part);
-      hipLaunchKernelGGL((k_absmean_p2<LCQ_BF16>), dim3((unsigned)((c + 255) / 256)), 256, 0, st,
-                         part, splits, n, c, out);
-      break;
-    case LCQ_F16:
-      hipLaunchKernelGGL((k_absmean_p1<LCQ_F16>), g1, 256, 0, st, x, n, c, rps, part);
-      hipLaunchKernelGGL((k_absmean_p2<LCQ_F16>), dim3((unsigned)((c + 255) / 256)), 256, 0, st,
-                         part, splits, n, c, out);
-      break;
-    default:
-      hipLaunchKernelGGL((k_absmean_p1<LCQ_F32>), g1, 256, 0, st, x, n, c, rps, part);
-      hipLaunchKernelGGL((k_absmean_p2<LCQ_F32>), dim3((unsigned)((c + 255) / 256)), 256, 0, st,
-                         part, splits, n, c, out);
+    case LCQ_BF16: launch_colmean<LCQ_BF16, 0>(x, n, c, 1, 0, 1, out, workspace, st); break;
+    case LCQ_F16: launch_colmean<LCQ_F16, 0>(x, n, c, 1, 0, 1, out, workspace, st); break;
+    default: launch_colmean<LCQ_F32, 0>(x, n, c, 1, 0, 1, out, workspace, st);
   }
   return check_launch("lcq_absmean_cols");
 }
 
-extern "C" int lcq_awq_scales(const void* xmean, int dtype, int64_t c, float ratio_dt,
-                              void* out, void* stream) {
+extern "C" int lcq_awq_weight_scale(const void* w, int dtype, int64_t rows, int64_t cols,
+                                    int64_t group, int layer, int nlayers, void* total,
+                                    void* workspace, void* stream) {
+  LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16 || dtype == LCQ_F32, "bad dtype");
+  LCQ_REQUIRE(rows > 0 && cols > 0, "empty weight");
+  LCQ_REQUIRE(group >= 8 && group % 8 == 0 && cols % group == 0,
+              "group must be a multiple of 8 dividing cols");
+  const int64_t gl = group / 8;
+  LCQ_REQUIRE(gl <= 64 && (gl & (gl - 1)) == 0, "group / 8 must be a power of two <= 64");
+  LCQ_REQUIRE(layer >= 0 && layer < nlayers, "layer index out of range");
+  LCQ_REQUIRE(workspace && total, "null pointer");
+  hipStream_t st = as_stream(stream);
+  switch (dtype) {
+    case LCQ_BF16: launch_colmean<LCQ_BF16, 1>(w, rows, cols, (int)gl, layer, nlayers, total, workspace, st); break;
+    case LCQ_F16: launch_colmean<LCQ_F16, 1>(w, rows, cols, (int)gl, layer, nlayers, total, workspace, st); break;
+    default: launch_colmean<LCQ_F32, 1>(w, rows, cols, (int)gl, layer, nlayers, total, workspace, st);
+  }
+  return check_launch("lcq_awq_weight_scale");
+}
+
+static int awq_scales_impl(const void* xmean, const void* wmax, int dtype, int64_t c,
+                           float ratio_dt, float wexp_dt, void* out, void* stream) {
   LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16 || dtype == LCQ_F32, "bad dtype");
   LCQ_REQUIRE(c > 0, "empty");
   hipStream_t st = as_stream(stream);
   switch (dtype) {
-    case LCQ_BF16: hipLaunchKernelGGL((k_awq_scales<LCQ_BF16>), 1, 1024, 0, st, xmean, c, ratio_dt, out); break;
-    case LCQ_F16: hipLaunchKernelGGL((k_awq_scales<LCQ_F16>), 1, 1024, 0, st, xmean, c, ratio_dt, out); break;
-    default: hipLaunchKernelGGL((k_awq_scales<LCQ_F32>), 1, 1024, 0, st, xmean, c, ratio_dt, out);
+    case LCQ_BF16: hipLaunchKernelGGL((k_awq_scales<LCQ_BF16>), 1, 1024, 0, st, xmean, c, ratio_dt, out, wmax, wexp_dt); break;
+    case LCQ_F16: hipLaunchKernelGGL((k_awq_scales<LCQ_F16>), 1, 1024, 0, st, xmean, c, ratio_dt, out, wmax, wexp_dt); break;
+    default: hipLaunchKernelGGL((k_awq_scales<LCQ_F32>), 1, 1024, 0, st, xmean, c, ratio_dt, out, wmax, wexp_dt);
   }
   return check_launch("lcq_awq_scales");
+}
+
+extern "C" int lcq_awq_scales(const void* xmean, int dtype, int64_t c, float ratio_dt,
+                              void* out, void* stream) {
+  return awq_scales_impl(xmean, nullptr, dtype, c, ratio_dt, 0.f, out, stream);
+}
+
+extern "C" int lcq_awq_scales_v1(const void* xmean, const void* wmax, int dtype, int64_t c,
+                                 float ratio_dt, float wexp_dt, void* out, void* stream) {
+  LCQ_REQUIRE(wmax != nullptr, "wmax required");
+  return awq_scales_impl(xmean, wmax, dtype, c, ratio_dt, wexp_dt, out, stream);
 }
 
 template <int DT>

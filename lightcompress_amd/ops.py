@@ -11,7 +11,7 @@ import torch
 from . import _native as N
 
 __all__ = ['int_quant_dynamic', 'int_quant_static', 'pack_vllm', 'pack_autoawq_gemm',
-           'hessian_accum', 'gptq_block', 'absmean_cols', 'awq_scales', 'scale_bcast',
+           'hessian_accum', 'gptq_block', 'absmean_cols', 'awq_weight_scale', 'awq_scales', 'scale_bcast',
            'sq_diff_mean', 'auto_clip_search', 'clip_apply']
 
 
@@ -268,19 +268,37 @@ def gptq_trailing(W: torch.Tensor, c0: int, cnt: int, c1: int, err: torch.Tensor
            N.ptr(U), U.shape[1], N.stream_of(W))
 
 
-def absmean_cols(x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
-    """mean over all leading dims of |x| per channel (Awq.get_act_scale, awq.py:74-85)."""
+def _colmean_ws(rows: int, cols: int, device) -> torch.Tensor:
+    nbytes = int(N.load().lcq_colmean_workspace_bytes(rows, cols))
+    return torch.empty((max(nbytes, 4) + 3) // 4, dtype=torch.float32, device=device)
+
+
+def absmean_cols(x: torch.Tensor) -> torch.Tensor:
+    """mean over all leading dims of |x| per channel (Awq.get_act_scale, awq.py:74-85), in
+    torch-CPU's summation order."""
     x2 = x.reshape(-1, x.shape[-1])
     if not x2.is_contiguous():
         x2 = x2.contiguous()
     n, c = x2.shape
-    if splits is None:
-        splits = max(1, min(256, n // 64))
-    ws = torch.empty((splits, c), dtype=torch.float64, device=x.device)
+    ws = _colmean_ws(n, c, x.device)
     out = torch.empty((c,), dtype=x.dtype, device=x.device)
-    N.call('lcq_absmean_cols', N.ptr(x2), N.dt(x2), n, c, N.ptr(out), N.ptr(ws), int(splits),
-           N.stream_of(x2))
+    N.call('lcq_absmean_cols', N.ptr(x2), N.dt(x2), n, c, N.ptr(out), N.ptr(ws), N.stream_of(x2))
     return out
+
+
+def awq_weight_scale(weights, group: int) -> torch.Tensor:
+    """Awq.get_weight_scale (awq.py:48-72) over the subset's linears (same dtype and cols)."""
+    w0 = weights[0]
+    cols = w0.shape[-1]
+    total = torch.empty((cols,), dtype=w0.dtype, device=w0.device)
+    ws = _colmean_ws(max(w.shape[0] for w in weights), cols, w0.device)
+    for i, w in enumerate(weights):
+        w2 = w.reshape(-1, cols).contiguous()
+        if w2.dtype != w0.dtype:
+            raise ValueError('subset weights must share the dtype')
+        N.call('lcq_awq_weight_scale', N.ptr(w2), N.dt(w2), w2.shape[0], cols, int(group), i,
+               len(weights), N.ptr(total), N.ptr(ws), N.stream_of(w2))
+    return total
 
 
 def ratio_in_dtype(ratio: float, dtype: torch.dtype) -> float:
@@ -288,11 +306,19 @@ def ratio_in_dtype(ratio: float, dtype: torch.dtype) -> float:
     return float(torch.tensor(ratio, dtype=torch.float32).to(dtype).item())
 
 
-def awq_scales(xmean: torch.Tensor, ratio: float, out: torch.Tensor | None = None) -> torch.Tensor:
-    """AWQ v2 scales for one grid ratio (awq.py:87-108)."""
+def awq_scales(xmean: torch.Tensor, ratio: float, out: torch.Tensor | None = None,
+               w_max: torch.Tensor | None = None) -> torch.Tensor:
+    """AWQ scales for one grid ratio (awq.py:87-108): v2, or v1 when ``w_max`` is given."""
     out = torch.empty_like(xmean) if out is None else out
-    N.call('lcq_awq_scales', N.ptr(xmean), N.dt(xmean), xmean.numel(),
-           ratio_in_dtype(ratio, xmean.dtype), N.ptr(out), N.stream_of(xmean))
+    if w_max is None:
+        N.call('lcq_awq_scales', N.ptr(xmean), N.dt(xmean), xmean.numel(),
+               ratio_in_dtype(ratio, xmean.dtype), N.ptr(out), N.stream_of(xmean))
+    else:
+        if w_max.dtype != xmean.dtype or w_max.numel() != xmean.numel():
+            raise ValueError('w_max must match x_mean')
+        N.call('lcq_awq_scales_v1', N.ptr(xmean), N.ptr(w_max.contiguous()), N.dt(xmean),
+               xmean.numel(), ratio_in_dtype(ratio, xmean.dtype),
+               ratio_in_dtype(1 - ratio, xmean.dtype), N.ptr(out), N.stream_of(xmean))
     return out
 
 

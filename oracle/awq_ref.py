@@ -1,6 +1,6 @@
 """ORACLE (test infrastructure only) — AWQ scale search and auto-clip, CPU restatement.
 
-Follows llmc/compression/quantization/awq.py (trans_version v2, w_only, awq_bs None) and
+Follows llmc/compression/quantization/awq.py (trans_version v1 / v2, w_only, awq_bs None) and
 auto_clip.py (clip_version v1, w_only) op by op in torch-CPU with the reference's dtypes.
 The inspect module forward (HF Llama attention / MLP / Linear) is the same third-party
 torch module the reference calls.
@@ -23,6 +23,25 @@ def scales_v2(x_mean: torch.Tensor, ratio: float) -> torch.Tensor:
     return s / (s.max() * s.min()).sqrt()
 
 
+def weight_scale(weights: list, group) -> torch.Tensor:
+    """awq.py:48-72 (get_weight_scale, bf16/fp16 weights): per group |w| / max|w| in the weight
+    dtype, mean over rows (torch-CPU: fp32 sum, / rows, back to the dtype), summed over the
+    subset's layers in the dtype, / len(layers)."""
+    total = None
+    for w in weights:
+        a = w.clone().reshape(-1, group).abs() if group else w.clone().abs()
+        mx = a.amax(dim=1, keepdim=True)
+        ls = a.div_(mx).view(w.shape)
+        total = ls.mean(0) if total is None else total.add_(ls.mean(0))
+    return total.div_(len(weights))
+
+
+def scales_v1(x_mean: torch.Tensor, w_max: torch.Tensor, ratio: float) -> torch.Tensor:
+    """awq.py:87-108 (trans_version v1, not GQA)."""
+    s = (x_mean.pow(ratio) / w_max.pow(1 - ratio)).clamp(min=1e-4).view(-1)
+    return s / (s.max() * s.min()).sqrt()
+
+
 def fake_quant_scaled(w: torch.Tensor, s: torch.Tensor, bit, sym, group):
     """awq.py:39-46 + 147-164: W.mul_(s) then fake_quant_weight_dynamic, weight dtype."""
     ws = w.clone().mul_(s.view(1, -1))
@@ -34,18 +53,20 @@ def loss(org_out: torch.Tensor, out: torch.Tensor) -> float:
     return (org_out - out).float().pow(2).mean().item()
 
 
-def search_scale(x: torch.Tensor, weights: list, forward, bit, sym, group, n_grid=20):
+def search_scale(x: torch.Tensor, weights: list, forward, bit, sym, group, n_grid=20,
+                 version='v2'):
     """awq.py:178-278 for one input tensor (len(input)==1, world_size 1).
 
     ``forward(x, qweights)`` runs the inspect module with the given (fake-quantised) weights.
     Returns (losses[n_grid], best_index, best_scales)."""
+    w_max = weight_scale(weights, group) if version == 'v1' else None
     x_mean = act_scale(x)
     org_out = forward(x, None)
     best, best_i, best_s = float('inf'), -1, None
     losses = []
     for n in range(n_grid):
         ratio = n * 1 / n_grid
-        s = scales_v2(x_mean, ratio)
+        s = scales_v1(x_mean, w_max, ratio) if version == 'v1' else scales_v2(x_mean, ratio)
         qw = [fake_quant_scaled(w, s, bit, sym, group) for w in weights]
         out = forward(x / s.view(1, -1), qw)
         lo = loss(org_out, out)

@@ -210,11 +210,11 @@ def tiny_llama(seed=0, hidden=256, inter=512, heads=4, kv=2):
     return cfg, layer, rot
 
 
-def _awq_obj(wq, nsamples):
+def _awq_obj(wq, nsamples, version='v2'):
     import llmc.compression.quantization.awq as am
     obj = am.Awq.__new__(am.Awq)
     obj.wquantizer = wq
-    obj.trans_version, obj.awq_bs, obj.save_mem = 'v2', None, True
+    obj.trans_version, obj.awq_bs, obj.save_mem = version, None, True
     obj.padding_mask, obj.w_only, obj.n_samples = None, True, nsamples
     obj.losses_seen = []
     orig = am.Awq.calculate_loss
@@ -227,7 +227,7 @@ def _awq_obj(wq, nsamples):
     return obj
 
 
-def gen_awq():
+def gen_awq(only_v1=False):
     """Reference Awq.search_scale_subset (+ apply_scale) on the three Llama subsets that AWQ
     transforms (qkv / gate-up / down; o_proj is skipped under GQA) of a tiny bf16 layer."""
     R.init_dist()
@@ -244,9 +244,11 @@ def gen_awq():
     pos = torch.arange(seq).unsqueeze(0)
     cos, sin = rot(hidden, pos)
     kwargs = {'position_embeddings': (cos, sin), 'attention_mask': None, 'position_ids': pos}
-    for sym in (True, False):
+    for sym, version in ((True, 'v2'), (False, 'v2'), (True, 'v1'), (False, 'v1')):
+        if only_v1 and version != 'v1':
+            continue
         wq = q.IntegerQuantizer(4, sym, 'per_group', group_size=128)
-        tag = 'sym' if sym else 'asym'
+        tag = ('sym' if sym else 'asym') + ('' if version == 'v2' else '_v1')
         import copy
         lay = copy.deepcopy(layer)
         with torch.no_grad():
@@ -263,15 +265,23 @@ def gen_awq():
             ('down', lay.mlp.up_proj, {'down': lay.mlp.down_proj}, x_down, lay.mlp.down_proj, {}),
         ]
         for name, prev, layers, x, inspect, kw in subsets:
-            obj = _awq_obj(wq, n)
+            obj = _awq_obj(wq, n, version)
             w_before = {k: m.weight.data.clone() for k, m in layers.items()}
+            w_max = obj.get_weight_scale(layers) if version == 'v1' else None
+            if version == 'v1':
+                # awq.py:199 backs the weights up with `.cpu()`: a copy on the GPU, the SAME
+                # tensors on a CPU-only run, where the in-place W.mul_(s) of the first ratio
+                # (awq.py:40-46) then leaks into every later ratio. v2's first scales are all
+                # 1 (x^0), v1's are not: back up real copies, as the reference's GPU run does.
+                inspect.state_dict = (lambda *a, _m=inspect, **k: {
+                    kk: vv.clone() for kk, vv in type(_m).state_dict(_m, *a, **k).items()})
             prev_before = prev.weight.data.clone()
             best = obj.search_scale_subset(prev, layers, [x.clone()], inspect, False, kw)
             losses = torch.tensor(obj.losses_seen, dtype=torch.float64)
             obj.num_key_value_heads, obj.has_gqa = cfg.num_key_value_heads, True
             obj.apply_scale(best, [prev], list(layers.values()))
             out = dict(x=x, scales=best, losses=losses, prev_w=prev_before,
-                       prev_w_after=prev.weight.data.clone())
+                       prev_w_after=prev.weight.data.clone(), w_max=w_max)
             for k in layers:
                 out[f'w_{k}'] = w_before[k]
                 out[f'w_{k}_after'] = layers[k].weight.data.clone()
@@ -490,6 +500,7 @@ def gen_act_static():
 
 
 GENERATORS['act_static'] = gen_act_static
+GENERATORS['awq_v1'] = lambda: gen_awq(only_v1=True)
 
 
 if __name__ == '__main__':

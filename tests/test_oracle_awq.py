@@ -18,6 +18,19 @@ def test_search_scale_matches_reference(subset, sym):
     assert torch.equal(best_s.view(torch.int16), c['scales'].view(torch.int16))
 
 
+@pytest.mark.parametrize('subset', ['qkv', 'mlp', 'down'])
+@pytest.mark.parametrize('sym', [True, False])
+def test_search_scale_v1_matches_reference(subset, sym):
+    """trans_version v1 (weight-scale term): get_weight_scale and the whole search."""
+    c = F.load(f'awq_{subset}_{"sym" if sym else "asym"}_v1')
+    cfg, layer, kwargs = build_layer()
+    fwd, ws = forward_fn(layer, subset, kwargs)
+    assert torch.equal(A.weight_scale(ws, 128).view(torch.int16), c['w_max'].view(torch.int16))
+    losses, best_i, best_s = A.search_scale(c['x'], ws, fwd, 4, sym, 128, version='v1')
+    assert torch.equal(torch.tensor(losses, dtype=torch.float64), c['losses'])
+    assert torch.equal(best_s.view(torch.int16), c['scales'].view(torch.int16))
+
+
 @pytest.mark.parametrize('name', F.names('clip_'))
 def test_auto_clip_matches_reference(name):
     c = F.load(name)
