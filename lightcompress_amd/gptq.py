@@ -40,12 +40,14 @@ class GPTQ(BaseBlockwiseQuantization):
         self.blocksize = sp['blocksize']
         self.owq = sp.get('owq', False)
         self.chunk_num = sp.get('chunk_num', 1)
-        if self.owq:
-            raise NotImplementedError('OWQ is not on the device path yet (SURVEY.md §8f)')
+        if self.owq:  # gptq.py:44-50
+            self.n_outs = sp['n_outs']
+            self.static_groups = False
+            self.actorder = False
         if self.blocksize != gptq_core.BLOCK:
             raise NotImplementedError('device GPTQ uses blocksize 128')
         self.need_perm = (self.wquantizer.granularity == 'per_group' and not self.static_groups
-                          and self.actorder)
+                          and self.actorder) or self.owq
 
     @torch.no_grad()
     def collect_model_qparams(self):
@@ -110,13 +112,42 @@ class GPTQ(BaseBlockwiseQuantization):
     concat_rows = os.environ.get('LCQ_GPTQ_CONCAT', '1') != '0'
 
     @torch.no_grad()
+    def block_transform(self, block, input_feat=None, block_kwargs=None):
+        if getattr(self, 'owq', False) and not hasattr(self, 'n_out_dict'):  # gptq.py:298-306
+            names = list(self.model.get_block_linears(block).keys())
+            self.n_out_dict = {n: self.n_outs[i] for i, n in enumerate(names)}
+        super().block_transform(block, input_feat, block_kwargs)
+
+    def _n_out(self, name):
+        return self.n_out_dict[name] if getattr(self, 'owq', False) else 0
+
+    def _owq_pad_groups(self, r, layers, rows_total, cols):
+        """OWQ: groups past the last quantized column keep the construction qparams the
+        reference seeded `groups` with (search_group_qparams, gptq.py:383-396; only the
+        searched ones are overwritten) -- merged into buf_scales / buf_zeros in group order."""
+        if r['scales'] is None:
+            return r
+        ng_all = -(-cols // self.wquantizer.group_size)
+        ng_q = r['scales'].shape[0] // rows_total
+        if ng_q >= ng_all:
+            return r
+        for key, buf in (('scales', 'buf_scales'), ('zeros', 'buf_zeros')):
+            if r[key] is None:
+                continue
+            orig = torch.cat([getattr(m, buf).reshape(m.weight.shape[0], ng_all) for m in layers])
+            got = r[key].reshape(rows_total, ng_q)
+            r[key] = torch.cat([got, orig[:, ng_q:].to(got.dtype)], 1).reshape(-1, 1)
+        return r
+
+    @torch.no_grad()
     def subset_transform(self, subset, input_feat, subset_kwargs):
         groups = {}
         for name, layer in subset['layers'].items():
             if not isinstance(layer, _LINEAR_TYPES):
                 continue
             acc = self.layers_cache[name]['acc']
-            groups.setdefault(id(acc), []).append((name, layer))
+            # OWQ's permutation depends on the layer's n_out: share only equal ones
+            groups.setdefault((id(acc), self._n_out(name)), []).append((name, layer))
         for grp in groups.values():
             if len(grp) > 1 and self.concat_rows:
                 self.group_transform(grp)
@@ -126,15 +157,19 @@ class GPTQ(BaseBlockwiseQuantization):
             for name, _ in grp:
                 self.free(name)
 
-    def _prepared(self, acc, replicate, ws):
-        if getattr(acc, 'prepared', None) is None:
+    def _prepared(self, acc, replicate, ws, nout=0):
+        cache = getattr(acc, 'prepared_by', None)
+        if cache is None:
+            cache = acc.prepared_by = {}
+        if nout not in cache:
             H = acc.H.clone()
             if replicate:
                 # one all-reduce of the finished Hessian per distinct input (the reference
                 # reduces after every sample); averaging matches its H /= world_size
                 dist.all_reduce(H, op=dist.ReduceOp.SUM)
                 H /= ws
-            acc.prepared = gptq_core.prepare_hessian(H, self.actorder, self.percdamp)
+            cache[nout] = gptq_core.prepare_hessian(H, self.actorder, self.percdamp, nout)
+        acc.prepared = cache[nout]
         return acc.prepared
 
     @torch.no_grad()
@@ -143,7 +178,8 @@ class GPTQ(BaseBlockwiseQuantization):
         acc = self.layers_cache[grp[0][0]]['acc']
         _, ws, _ = world()
         replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
-        prepared = self._prepared(acc, replicate, ws)
+        nout = self._n_out(grp[0][0])
+        prepared = self._prepared(acc, replicate, ws, nout)
         W = torch.cat([layer.weight.data for _, layer in grp], 0)
         fixed = None
         if self.wquantizer.granularity != 'per_group' or self.static_groups:
@@ -153,7 +189,10 @@ class GPTQ(BaseBlockwiseQuantization):
             fixed = (s, z)
         r = gptq_core.quantize_layer(W, None, self.wquantizer, actorder=self.actorder,
                                      percdamp=self.percdamp, fixed=fixed, shard_rows=replicate,
-                                     prepared=prepared, static_groups=self.static_groups)
+                                     prepared=prepared, static_groups=self.static_groups,
+                                     owq_nout=nout)
+        if getattr(self, 'owq', False):
+            r = self._owq_pad_groups(r, [layer for _, layer in grp], W.shape[0], W.shape[1])
         ng = 1 if r['scales'] is None else r['scales'].shape[0] // W.shape[0]
         o0 = 0
         for _, layer in grp:
@@ -162,6 +201,8 @@ class GPTQ(BaseBlockwiseQuantization):
             if r['perm'] is not None:
                 layer.register_buffer('buf_perm', r['perm'])
                 layer.register_buffer('buf_invperm', r['invperm'])
+            if getattr(self, 'owq', False):
+                layer.register_buffer('buf_n_nonout', torch.tensor(W.shape[1] - nout))
             if r['scales'] is not None:
                 layer.buf_scales = r['scales'][o0 * ng:o1 * ng].clone()
                 if not self.wquantizer.sym:
@@ -173,18 +214,23 @@ class GPTQ(BaseBlockwiseQuantization):
         acc = self.layers_cache[name]['acc']  # shared by the linears fed the same input
         _, ws, _ = world()
         replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
-        self._prepared(acc, replicate, ws)
+        nout = self._n_out(name)
+        prepared = self._prepared(acc, replicate, ws, nout)
         fixed = None
         if self.wquantizer.granularity != 'per_group' or self.static_groups:
             fixed = (layer.buf_scales, getattr(layer, 'buf_zeros', None))
         r = gptq_core.quantize_layer(layer.weight.data, None, self.wquantizer,
                                      actorder=self.actorder, percdamp=self.percdamp,
-                                     fixed=fixed, shard_rows=replicate, prepared=acc.prepared,
-                                     static_groups=self.static_groups)
+                                     fixed=fixed, shard_rows=replicate, prepared=prepared,
+                                     static_groups=self.static_groups, owq_nout=nout)
+        if getattr(self, 'owq', False):
+            r = self._owq_pad_groups(r, [layer], layer.weight.shape[0], layer.weight.shape[1])
         layer.weight.data = r['weight']
         if r['perm'] is not None:
             layer.register_buffer('buf_perm', r['perm'])
             layer.register_buffer('buf_invperm', r['invperm'])
+        if getattr(self, 'owq', False):
+            layer.register_buffer('buf_n_nonout', torch.tensor(layer.weight.shape[1] - nout))
         if r['scales'] is not None:
             layer.buf_scales = r['scales']
             if not self.wquantizer.sym:
@@ -204,6 +250,14 @@ class GPTQ(BaseBlockwiseQuantization):
 
     @torch.no_grad()
     def w_qdq(self, module, wquantizer):
+        if getattr(self, 'owq', False):  # gptq.py:424-452: outlier columns stay in float
+            w = module.weight[:, module.buf_perm].contiguous()
+            nn_ = int(module.buf_n_nonout)
+            args = {'scales': module.buf_scales, 'zeros': getattr(module, 'buf_zeros', None),
+                    'qmax': module.buf_qmax, 'qmin': module.buf_qmin}
+            fq = wquantizer.fake_quant_weight_static(w, args).to(self.model_dtype)
+            fq[:, nn_:] = w[:, nn_:].to(self.model_dtype)
+            return fq[:, module.buf_invperm].contiguous()
         fast = self._w_qdq_cols(module, wquantizer)
         if fast is not None:
             return fast

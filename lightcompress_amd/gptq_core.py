@@ -45,7 +45,7 @@ class HessianAccumulator:
 
 
 @torch.no_grad()
-def prepare_hessian(H: torch.Tensor, actorder: bool, percdamp: float):
+def prepare_hessian(H: torch.Tensor, actorder: bool, percdamp: float, owq_nout: int = 0):
     """Hessian side of gptq.py:58-64, 128-176 (H is consumed): act-order permutation, dead
     columns (diag 0 -> 1), damping, and U = upper Cholesky factor of H^-1.
 
@@ -55,6 +55,13 @@ def prepare_hessian(H: torch.Tensor, actorder: bool, percdamp: float):
     dense factor/inverse steps (2.5x faster on MI355X at IC 14336, same U to ~1e-6). Returns
     (U, perm | None, dead mask)."""
     perm = torch.argsort(torch.diag(H), descending=True, stable=True) if actorder else None
+    if owq_nout:
+        # OWQ (gptq.py:58-83, actorder off): the n_out largest-diag columns (outliers) move to
+        # the end and stay in float; the rest keep their order
+        desc = torch.argsort(torch.diag(H), descending=True, stable=True)
+        keep = torch.ones(H.shape[0], dtype=torch.bool, device=H.device)
+        keep[desc[:owq_nout]] = False
+        perm = torch.cat([torch.arange(H.shape[0], device=H.device)[keep], desc[:owq_nout]])
     dead = torch.diag(H) == 0
     if bool(dead.any()):
         idx = torch.nonzero(dead).flatten()
@@ -247,7 +254,8 @@ def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
 @torch.no_grad()
 def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
                 qmin: int, qmax: int, fixed=None, losses: bool = False,
-                superblock: int | None = None, col_group: torch.Tensor | None = None):
+                superblock: int | None = None, col_group: torch.Tensor | None = None,
+                ncols_q: int | None = None):
     """Blocked OBS loop (gptq.py:198-244) on permuted fp32 W, in place.
 
     Per 128-column block: the HIP kernel runs the in-block sequential loop (bit-exact rank-1
@@ -256,12 +264,14 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     block updates only the rest of its superblock, and the far columns receive the
     superblock's stacked errors in ONE K = superblock update (same terms, grouped differently
     -> T2; every element still has a fixed k order, so row sharding stays bit-identical).
-    fp32 MFMA kernel (``lcq_gptq_trailing``)."""
+    fp32 MFMA kernel (``lcq_gptq_trailing``). ``ncols_q`` (OWQ): only the first ncols_q
+    columns are quantized; every block's error still updates all later columns."""
     rows, cols = W.shape
     dev = W.device
     U = U.contiguous()
+    ncq = cols if ncols_q is None else int(ncols_q)
     static = col_group is not None  # static_groups: fixed qparams of the original groups
-    ng = 0 if (group is None or static) else -(-cols // group)
+    ng = 0 if (group is None or static) else -(-ncq // group)
     s_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng else None
     z_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng and not sym else None
     if superblock is None:
@@ -273,10 +283,10 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     if group is None or static:
         s_in = fixed[0].reshape(-1).float().contiguous()
         z_in = None if sym else fixed[1].reshape(-1).float().contiguous()
-    for sb0 in range(0, cols, SB):
-        sb1 = min(sb0 + SB, cols)
+    for sb0 in range(0, ncq, SB):
+        sb1 = min(sb0 + SB, ncq)
         for i1 in range(sb0, sb1, BLOCK):
-            i2 = min(i1 + BLOCK, cols)
+            i2 = min(i1 + BLOCK, sb1)
             cnt = i2 - i1
             e = errT[i1 - sb0:]
             if static:
@@ -294,7 +304,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
 @torch.no_grad()
 def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder=True,
                    percdamp=0.01, fixed=None, losses=False, shard_rows=False, prepared=None,
-                   static_groups=False):
+                   static_groups=False, owq_nout=0):
     """Full GPTQ transform of one linear. Returns dict(weight fp32 (original column order),
     scales / zeros [rows*ng, 1] fp32 (merge_qparams order, permuted groups), perm, invperm,
     loss). ``prepared`` = prepare_hessian(...) output shared by linears with the same input
@@ -304,10 +314,13 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
     group = wquantizer.group_size if wquantizer.granularity == 'per_group' else None
     if group is not None and not static_groups and group not in (32, 64, 128):
         raise NotImplementedError('device GPTQ supports group_size 32/64/128')
+    if owq_nout and group is None:
+        raise NotImplementedError('OWQ supports per_group weights on the device path')
     if prepared is None:
-        prepared = prepare_hessian(H, actorder, percdamp)
+        prepared = prepare_hessian(H, actorder, percdamp, owq_nout)
     U, perm, dead = prepared
     Wp = prepare_weight(W, perm, dead)
+    ncq = Wp.shape[1] - int(owq_nout)
     col_group = None
     if static_groups and group is not None:
         # gptq.py:224-227: permuted column j quantizes with groups[perm[j] // group_size], the
@@ -325,14 +338,14 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
         fx = None if fixed is None else tuple(
             None if f is None else f.reshape(Wp.shape[0], -1)[r0:r1] for f in fixed)
         s, z, L = column_loop(Wl, U, bit, sym, group, qmin, qmax, fixed=fx, losses=losses,
-                              col_group=col_group)
+                              col_group=col_group, ncols_q=ncq)
         Wp = P.gather_rows(Wl, Wp.shape[0])
         s = None if s is None else P.gather_rows(s, Wp.shape[0])
         z = None if z is None else P.gather_rows(z, Wp.shape[0])
         L = None if L is None else P.gather_rows(L, Wp.shape[0])
     else:
         s, z, L = column_loop(Wp, U, bit, sym, group, qmin, qmax, fixed=fixed, losses=losses,
-                              col_group=col_group)
+                              col_group=col_group, ncols_q=ncq)
     invperm = torch.argsort(perm) if perm is not None else None
     weight = Wp[:, invperm] if invperm is not None else Wp
     return dict(weight=weight, scales=None if s is None else s.reshape(-1, 1),

@@ -53,8 +53,29 @@ def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
     return W, U, perm
 
 
+def prepare_owq(W: torch.Tensor, H: torch.Tensor, nout: int, percdamp: float):
+    """OWQ hessian_sorting (gptq.py:58-83, actorder off) + process_hessian_and_weights."""
+    H = H.clone()
+    desc = torch.argsort(torch.diag(H), descending=True)
+    keep = torch.ones(H.shape[0], dtype=torch.bool)
+    keep[desc[:nout]] = False
+    perm = torch.cat([torch.arange(H.shape[0])[keep], desc[:nout]])
+    W = W.clone().float()
+    dead = torch.diag(H) == 0
+    H[dead, dead] = 1
+    W[:, dead] = 0
+    W = W[:, perm]
+    H = H[perm][:, perm]
+    d = torch.arange(H.shape[0])
+    H[d, d] += percdamp * torch.mean(torch.diag(H))
+    H = torch.linalg.cholesky(H)
+    H = torch.cholesky_inverse(H)
+    U = torch.linalg.cholesky(H, upper=True)
+    return W, U, perm
+
+
 def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
-                blocksize: int = 128, fixed=None, static=None):
+                blocksize: int = 128, fixed=None, static=None, ncols_q: int | None = None):
     """gptq.py:198-244 on permuted fp32 W (modified in place to the compensated weights).
 
     group=None with fixed=(scale[rows,1], zero) -> per-channel fixed qparams.
@@ -63,12 +84,13 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     Returns (tmp, Losses, scales [rows, ng], zeros [rows, ng] | None)."""
     qmin, qmax = Q.int_range(bit, sym)
     rows, cols = W.shape
+    ncq = cols if ncols_q is None else ncols_q  # OWQ: the outlier tail is not quantized
     Losses = torch.zeros_like(W)
     tmp = torch.zeros_like(W)
     groups = {}
     qp = fixed
-    for i1 in range(0, cols, blocksize):
-        i2 = min(i1 + blocksize, cols)
+    for i1 in range(0, ncq, blocksize):
+        i2 = min(i1 + blocksize, ncq)
         W1, U1 = W[:, i1:i2].clone(), U[i1:i2, i1:i2]
         tmp1, Err1, L1 = torch.zeros_like(W1), torch.zeros_like(W1), torch.zeros_like(W1)
         for i in range(i2 - i1):
@@ -78,7 +100,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
                 g = (int(sp[i1 + i]) if sp is not None else i1 + i) // group
                 qp = (ss[:, g:g + 1], torch.tensor(0.0) if zs is None else zs[:, g:g + 1])
             elif group is not None and (i1 + i) % group == 0:
-                ct = W[:, i1 + i:min(i1 + i + group, cols)]
+                ct = W[:, i1 + i:min(i1 + i + group, ncq)]
                 t = Q.group_view(ct, 'per_group', group)
                 mn, mx = Q.minmax(t)
                 s, z = Q.qparams(mn, mx, qmin, qmax, sym)
@@ -93,6 +115,8 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
             Err1[:, i] = err1
         tmp[:, i1:i2], Losses[:, i1:i2] = tmp1, L1
         W[:, i2:] -= Err1.matmul(U[i1:i2, i2:])
+    if ncq < cols:
+        tmp[:, ncq:] = W[:, ncq:]  # gptq.py:187-188
     if group is None or static is not None:
         return tmp, Losses, None, None
     ng = len(groups)
@@ -134,3 +158,24 @@ def deploy_fake(weight, scales, zeros, perm, invperm, bit, sym, group, model_dty
     w = weight[:, perm] if perm is not None else weight
     out = Q.fake_quant_static(w, scales, zeros, bit, sym, 'per_group', group).to(model_dtype)
     return out[:, invperm] if invperm is not None else out
+
+
+def quantize_layer_owq(W: torch.Tensor, H: torch.Tensor, nout: int, bit=4, sym=False, group=128,
+                       percdamp=0.01, blocksize=128):
+    """GPTQ + OWQ layer transform; returns dict like quantize_layer (+ n_nonout)."""
+    Wp, U, perm = prepare_owq(W, H, nout, percdamp)
+    ncq = Wp.shape[1] - nout
+    tmp, Losses, s, z = column_loop(Wp, U, bit, sym, group, blocksize, ncols_q=ncq)
+    invperm = torch.argsort(perm)
+    return dict(weight=tmp[:, invperm], scales=s.reshape(-1, 1),
+                zeros=None if z is None else z.reshape(-1, 1), perm=perm, invperm=invperm, U=U,
+                n_nonout=ncq, loss=Losses.sum().item())
+
+
+def deploy_fake_owq(weight, scales, zeros, perm, invperm, n_nonout, bit, sym, group,
+                    model_dtype):
+    """GPTQ.w_qdq with OWQ (gptq.py:424-452): the float outlier columns are put back."""
+    w = weight[:, perm]
+    out = Q.fake_quant_static(w, scales, zeros, bit, sym, 'per_group', group).to(model_dtype)
+    out[:, n_nonout:] = w[:, n_nonout:].to(model_dtype)
+    return out[:, invperm]

@@ -503,6 +503,64 @@ GENERATORS['act_static'] = gen_act_static
 GENERATORS['awq_v1'] = lambda: gen_awq(only_v1=True)
 
 
+def gen_gptq_owq():
+    """GPTQ with OWQ (gptq.py:44-83, 178-196, 424-452): the n_out largest-diag input columns
+    move to the end of the permutation, stay in float (error-compensated) and are excluded
+    from the quantized groups."""
+    import torch.nn as nn
+    R.init_dist()
+    q = R.quant_module()
+    import llmc.compression.quantization.gptq as gm
+    cases = [
+        # name, oc, ic, bit, sym, group, n_out, dead_cols
+        ('int4_asym_g128_out6', 192, 512, 4, False, 128, 6, False),
+        ('int4_sym_g64_out2_dead', 128, 384, 4, True, 64, 2, True),
+        ('int8_asym_g32_out32', 96, 256, 8, False, 32, 32, False),
+    ]
+    for i, (name, oc, ic, bit, sym, gs, nout, dead) in enumerate(cases):
+        torch.manual_seed(3000 + i)
+        layer = nn.Linear(ic, oc, bias=False)
+        layer.weight.data = weights(oc, ic, torch.bfloat16, 600 + i, edge=False)
+        xs = _acts(3, 48, ic, 700 + i)
+        if dead:
+            for x in xs:
+                x[..., 9] = 0
+        obj = gm.GPTQ.__new__(gm.GPTQ)
+        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_group', group_size=gs)
+        obj.dev = torch.device('cpu')
+        obj.model_dtype = torch.bfloat16
+        obj.owq, obj.actorder, obj.static_groups = True, False, False
+        obj.percdamp, obj.blocksize, obj.chunk_num = 0.01, 128, 1
+        obj.true_sequential = True
+        obj.need_perm = True
+        obj.n_out_dict = {'l': nout}
+        obj.layers_cache = {'l': {}}
+        obj.qparams = {}
+        gm.GPTQ.layer_init(obj, layer, 'l')
+        for x in xs:
+            gm.GPTQ.add_batch(obj, layer, 'l', x, None)
+        H = obj.layers_cache['l']['H'].clone()
+        _, s0, z0, qmax, qmin = obj.wquantizer.get_tensor_qparams(layer.weight.data)
+        layer.register_buffer('buf_scales', s0)
+        layer.register_buffer('buf_zeros', z0)
+        layer.register_buffer('buf_qmax', torch.tensor(qmax))
+        layer.register_buffer('buf_qmin', torch.tensor(qmin))
+        w_in = layer.weight.data.clone()
+        obj.layers_cache['l']['H'] = H.clone()
+        obj.qparams = {}
+        obj.layer_transform(layer, 'l')
+        out = dict(x=torch.cat(xs, 0), w=w_in, H=H, perm=layer.buf_perm,
+                   weight=layer.weight.data.clone(), scales=layer.buf_scales,
+                   zeros=None if sym else layer.buf_zeros,
+                   meta=torch.tensor([bit, int(sym), gs, nout, oc, ic]))
+        out['fq'] = obj.w_qdq(layer, obj.wquantizer)
+        F.save(f'gptqowq_{name}', **out)
+    print('gptq owq fixtures written')
+
+
+GENERATORS['gptq_owq'] = gen_gptq_owq
+
+
 if __name__ == '__main__':
     which = sys.argv[1] if len(sys.argv) > 1 else 'all'
     R.install()

@@ -103,3 +103,30 @@ def test_static_groups_layer_and_deploy(name):
                        torch.bfloat16)
     agree = (fq == c['fq']).float().mean().item()
     assert agree > 0.9999, agree
+
+
+OWQ_CASES = F.names('gptqowq_')
+
+
+def _meta_owq(c):
+    bit, sym, gs, nout, oc, ic = c['meta'].tolist()
+    return bit, bool(sym), gs, nout, oc, ic
+
+
+@pytest.mark.parametrize('name', OWQ_CASES)
+def test_owq_layer_matches_reference(name):
+    """OWQ: permutation (outliers last), compensated weights incl. the float outlier columns,
+    group qparams over the non-outlier columns, and w_qdq with the outliers restored."""
+    c = F.load(name)
+    bit, sym, gs, nout, oc, ic = _meta_owq(c)
+    r = G.quantize_layer_owq(c['w'], c['H'], nout, bit, sym, gs)
+    assert torch.equal(r['perm'], c['perm'])
+    same_w = (r['weight'] == c['weight']).float().mean().item()
+    assert same_w > 0.999, same_w
+    # groups past the quantized columns keep the construction qparams (gptq.py:383-396)
+    ngq = r['scales'].shape[0] // oc
+    torch.testing.assert_close(r['scales'].reshape(oc, ngq),
+                               c['scales'].reshape(oc, -1)[:, :ngq], rtol=1e-5, atol=1e-7)
+    fq = G.deploy_fake_owq(c['weight'], c['scales'], c.get('zeros'), c['perm'],
+                           torch.argsort(c['perm']), ic - nout, bit, sym, gs, torch.bfloat16)
+    assert torch.equal(fq, c['fq'])

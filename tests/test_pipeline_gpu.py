@@ -40,10 +40,14 @@ GPTQ_CFG = {'quant': {'method': 'GPTQ', 'weight': {'bit': 4, 'symmetric': False,
 
 GPTQ_SG_CFG = copy.deepcopy(GPTQ_CFG)
 GPTQ_SG_CFG['quant']['special']['static_groups'] = True
+GPTQ_OWQ_CFG = copy.deepcopy(GPTQ_CFG)  # configs/quantization/methods/GPTQ/gptq_owq_w_only.yml
+GPTQ_OWQ_CFG['quant']['special'].update(owq=True, actorder=False, n_outs=[6, 6, 6, 6, 2, 2, 6])
+AWQ_V1_CFG = copy.deepcopy(AWQ_CFG)  # backend/*/w4a16_combin/step_1_awq.yml
+AWQ_V1_CFG['quant']['special']['trans_version'] = 'v1'
 
 
-@pytest.mark.parametrize('cfg', [AWQ_CFG, GPTQ_CFG, GPTQ_SG_CFG],
-                         ids=['awq', 'gptq', 'gptq_static'])
+@pytest.mark.parametrize('cfg', [AWQ_CFG, GPTQ_CFG, GPTQ_SG_CFG, GPTQ_OWQ_CFG, AWQ_V1_CFG],
+                         ids=['awq', 'gptq', 'gptq_static', 'gptq_owq', 'awq_v1'])
 def test_pipeline_runs_and_deploys(dev, cfg):
     from lightcompress_amd.pipeline import build_algo
     from lightcompress_amd.utils import load_config
@@ -64,7 +68,9 @@ def test_pipeline_runs_and_deploys(dev, cfg):
     # act-order permuted column space for GPTQ, in the original one with static_groups)
     m = model.blocks[0].mlp.down_proj
     w = m.weight.float()
-    if hasattr(m, 'buf_perm') and not getattr(algo, 'static_groups', False):
+    if getattr(algo, 'owq', False):  # outlier columns stay float: check the others
+        w = w[:, m.buf_perm][:, :int(m.buf_n_nonout) // 128 * 128]
+    elif hasattr(m, 'buf_perm') and not getattr(algo, 'static_groups', False):
         w = w[:, m.buf_perm]
     w = w.reshape(-1, 128)
     assert max(len(torch.unique(r)) for r in w[:64]) <= 16
