@@ -377,6 +377,17 @@ int lcq_act_static_qparams(const void* minmax, int64_t nseg, int algo, float alp
                            int range_dtype, int scale_dtype, int sym, float qmin, float qmax,
                            void* out, void* stream);
 
+/* static_hist (quant.py:264-529, get_static_hist_range + get_qparams, sym per-tensor int):
+ * per-segment torch.histc(x.float(), 2048, running min, running max) (exact counts), the
+ * reference's sequential histogram combination (upscale x16 + bucketize + bincount), the
+ * quantile-walk / L2-error threshold search, then scale = max(|min|, |max|) / qmax. segs as
+ * for lcq_minmax_segments; minmax: its output for the same segments; dst_nbins = 2^bit.
+ * out: device fp32 [4] = scale, 0, new_min, new_max. workspace: lcq_act_hist_workspace_bytes. */
+int64_t lcq_act_hist_workspace_bytes(int64_t nseg);
+int lcq_act_static_hist_qparams(const void* const* segs, const int64_t* seg_lens, int64_t nseg,
+                                int dtype, const void* minmax, int dst_nbins, float qmax,
+                                void* out, void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -686,3 +686,21 @@ def act_static_qparams(minmax: torch.Tensor, algo: str, alpha: float, range_dtyp
            CALIB_ALGOS[algo], float(alpha), N.dt(range_dtype), N.dt(scale_dtype), int(bool(sym)),
            float(qmin), float(qmax), N.ptr(out), N.stream_of(minmax))
     return out
+
+
+def act_static_hist_qparams(segs, minmax: torch.Tensor, bit: int, qmax: float) -> torch.Tensor:
+    """static_hist range (histograms, combination, threshold search) + sym get_qparams on the
+    device. Returns fp32 [4] = scale, 0, min, max."""
+    import ctypes
+    segs = [t if t.is_contiguous() else t.contiguous() for t in segs]
+    n = len(segs)
+    dev = segs[0].device
+    ptrs = (ctypes.c_void_p * n)(*[N.ptr(t) for t in segs])
+    lens = (ctypes.c_int64 * n)(*[t.numel() for t in segs])
+    nbytes = int(N.load().lcq_act_hist_workspace_bytes(n))
+    ws = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=dev)
+    out = torch.empty(4, dtype=torch.float32, device=dev)
+    N.call('lcq_act_static_hist_qparams', ctypes.cast(ptrs, ctypes.c_void_p),
+           ctypes.cast(lens, ctypes.c_void_p), n, N.dt(segs[0]), N.ptr(minmax.contiguous()),
+           2 ** int(bit), float(qmax), N.ptr(out), N.ptr(ws), N.stream_of(out))
+    return out

@@ -10,8 +10,8 @@ Supported on the device path (the hot path of SURVEY.md §8a): calib_algo ``minm
 granularity per_group / per_channel / per_token / per_tensor / per_head (+ per_block for FP8),
 round_zp=True, bit 2..8, dynamic and static qparams, fake quant, real quant (+ vLLM / AutoAWQ
 packing in ``module_utils``); FP8 e4m3 / e5m2 (``FloatQuantizer``); static per-tensor activation
-calibration (static_minmax / static_moving_minmax). Not yet supported (raise
-NotImplementedError): mse / hqq / learnable / static_hist calibration, ``int_indices`` mixed precision, STE rounding, ``rounding`` overrides.
+calibration (static_minmax / static_moving_minmax / static_hist). Not yet supported (raise
+NotImplementedError): mse / hqq / learnable calibration, ``int_indices`` mixed precision, STE rounding, ``rounding`` overrides.
 """
 from __future__ import annotations
 
@@ -174,7 +174,18 @@ class BaseQuantizer:
         if self.calib_algo == 'static_hist':
             assert self.sym is True and self.granularity == 'per_tensor', \
                 'Only support per tensor static symmetric int quantize.'
-            raise NotImplementedError('static_hist calibration is not on the device path yet')
+            if not isinstance(self.bit, int):
+                raise NotImplementedError('static_hist is for integer quantizers')
+            scales_l, zeros_l, qmin_l, qmax_l = [], [], [], []
+            for tensors in self.reshape_batch_tensors(act_tensors):
+                dev = tensors[0].device
+                mm = ops.minmax_segments(tensors)
+                r = ops.act_static_hist_qparams(tensors, mm, self.bit, float(self.qmax))
+                scales_l.append(r[0].clone())
+                zeros_l.append(torch.tensor(0.0, device=dev))
+                qmin_l.append(self.qmin.to(dev))
+                qmax_l.append(self.qmax.to(dev))
+            return scales_l, zeros_l, qmin_l, qmax_l
         if self.calib_algo not in ops.CALIB_ALGOS:
             raise ValueError(f'Unsupported calibration algorithm: {self.calib_algo}')
         if self.granularity != 'per_tensor':

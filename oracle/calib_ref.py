@@ -62,3 +62,91 @@ def fake_quant_act_static_int(act, scales, zeros, qmin, qmax):
     """IntegerQuantizer.fake_quant_act_static, per_tensor (quant.py:699-717, 719-743)."""
     q = torch.clamp(torch.round(act / scales) + zeros, qmin, qmax)
     return ((q - zeros) * scales).to(act.dtype)
+
+
+# ---- static_hist (quant.py:264-529) ----------------------------------------------------------
+BINS, UPSAMPLE = 2048, 16
+
+
+def _upscale(hist, lo, hi, new_lo, new_hi):
+    """_upscale_histogram (quant.py:332-366): the old histogram's 16x-refined midpoints,
+    re-binned into the new range with their (1/16) counts."""
+    w = hist.repeat_interleave(UPSAMPLE) / UPSAMPLE
+    step = (hi - lo) / (BINS * UPSAMPLE)
+    mids = torch.linspace(lo, hi, BINS * UPSAMPLE + 1)[:-1] + 0.5 * step
+    edges = torch.linspace(new_lo, new_hi, BINS + 1)
+    idx = (torch.bucketize(mids, edges, right=True) - 1).clamp(0, BINS - 1)
+    return torch.bincount(idx, weights=w, minlength=BINS)
+
+
+def hist_range(tensors):
+    """get_static_hist_range for one module input: (min, max) after the threshold search."""
+    hist, lo, hi = None, None, None
+    for t in tensors:
+        t = t.float()
+        t_lo, t_hi = torch.min(t), torch.max(t)
+        if hist is None:
+            hist = torch.histc(t, BINS, min=t_lo.item(), max=t_hi.item())
+            lo, hi = t_lo, t_hi
+            continue
+        n_lo, n_hi = torch.min(lo, t_lo), torch.max(hi, t_hi)
+        upd = torch.histc(t, BINS, min=n_lo.item(), max=n_hi.item())
+        if n_lo == lo and n_hi == hi:
+            hist = hist + upd
+        elif lo == hi:  # _combine_histograms' single-value branch (quant.py:381-389)
+            hist = torch.histc(lo, BINS, min=n_lo, max=n_hi) * torch.sum(upd) + upd
+        else:
+            hist = upd + _upscale(hist, lo, hi, n_lo, n_hi)
+        lo, hi = n_lo, n_hi
+    return hist_threshold(hist, lo, hi)
+
+
+def _l2(b, e, dens):
+    return dens * ((e * e * e - b * b * b) / 3)
+
+
+def _quant_error(hist, lo, hi, s, e, dst_nbins):
+    """get_quantization_error (quant.py:275-330)."""
+    bw = (hi.item() - lo.item()) / BINS
+    dbw = bw * (e - s + 1) / dst_nbins
+    if dbw == 0.0:
+        return 0.0
+    src = torch.arange(BINS)
+    sb = (src - s) * bw
+    se = sb + bw
+    db = torch.clamp(torch.div(sb, dbw, rounding_mode='floor'), 0, dst_nbins - 1)
+    de = torch.clamp(torch.div(se, dbw, rounding_mode='floor'), 0, dst_nbins - 1)
+    dens = hist / bw
+    norm = torch.zeros(BINS)
+    norm += _l2(sb - (db + 0.5) * dbw, torch.ones(BINS) * (dbw / 2), dens)
+    norm += (de - db - 1) * _l2(torch.tensor(-dbw / 2), torch.tensor(dbw / 2), dens)
+    norm += _l2(torch.tensor(-dbw / 2), se - (de * dbw + dbw / 2), dens)
+    return norm.sum().item()
+
+
+def hist_threshold(hist, lo, hi, dst_nbins=256):
+    """get_hist_threshold (quant.py:403-451): walk the quantile bounds in 1e-8 steps, keep
+    the last bin pair before the L2 error stops decreasing."""
+    bw = (hi - lo) / BINS
+    total = torch.sum(hist).item()
+    csum = torch.cumsum(hist, dim=0)
+    a, b, s, e, best = 0.0, 1.0, 0, BINS - 1, float('inf')
+    while a < b:
+        na, nb = a + 1e-8, b - 1e-8
+        left, right = s, e
+        while left < e and csum[left] < na * total:
+            left += 1
+        while right > s and csum[right] > nb * total:
+            right -= 1
+        ns, ne = s, e
+        if left - s > e - right:
+            ns, a = left, na
+        else:
+            ne, b = right, nb
+        if ns == s and ne == e:
+            continue
+        err = _quant_error(hist, lo, hi, ns, ne, dst_nbins)
+        if err > best:
+            break
+        best, s, e = err, ns, ne
+    return lo + bw * s, lo + bw * (e + 1)

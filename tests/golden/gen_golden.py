@@ -500,6 +500,36 @@ def gen_act_static():
 
 
 GENERATORS['act_static'] = gen_act_static
+
+
+def gen_act_hist():
+    """static_hist (quant.py:264-529): IntegerQuantizer(8, sym, per_tensor) qparams and the
+    thresholded range, for growing ranges (histogram upscaling), shrinking ones (plain adds)
+    and one entry split per sample."""
+    q = R.quant_module()
+    cases = [
+        # name, n_entries, entry_bs, T, H, dtype, growth per entry
+        ('bs1_grow', 6, 1, 48, 256, torch.bfloat16, 1.3),
+        ('bs1_shrink', 5, 1, 40, 256, torch.bfloat16, 0.8),
+        ('single', 1, 5, 32, 384, torch.bfloat16, 1.1),
+        ('bs2_f32', 4, 2, 24, 256, torch.float32, 1.2),
+    ]
+    for i, (name, ne, eb, T, H, dt, grow) in enumerate(cases):
+        g = torch.Generator().manual_seed(1200 + i)
+        mag = torch.exp(torch.randn(H, generator=g))
+        xs = [((torch.randn(eb, T, H, generator=g) + 0.2) * mag * grow ** j).to(dt)
+              for j in range(ne)]
+        x = torch.cat(xs, 0)
+        entries = [x] if ne == 1 else xs
+        quant = q.IntegerQuantizer(8, True, 'per_tensor', calib_algo='static_hist')
+        mn, mx = quant.get_static_hist_range([e.clone() for e in entries])
+        sc, zc, _, _ = quant.get_batch_tensors_qparams([e.clone() for e in entries])
+        F.save(f'acthist_{name}', x=x, scales=sc[0], zeros=zc[0], rmin=mn[0], rmax=mx[0],
+               meta=torch.tensor([ne, eb, 8, 1, 2]))
+    print('act hist fixtures written')
+
+
+GENERATORS['act_hist'] = gen_act_hist
 GENERATORS['awq_v1'] = lambda: gen_awq(only_v1=True)
 
 

@@ -43,6 +43,13 @@ CONFIGS = {
                                 'act': {'bit': 8, 'symmetric': True, 'granularity': 'per_tensor',
                                         'static': True, 'calib_algo': 'static_minmax'}},
                       'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}, 'diag': False},
+    # configs/quantization/methods/RTN/rtn_w_a_pertensor_static.yml as shipped (static_hist)
+    'rtn_a8_hist': {'quant': {'method': 'RTN',
+                              'weight': {'bit': 8, 'symmetric': True,
+                                         'granularity': 'per_channel', 'group_size': -1},
+                              'act': {'bit': 8, 'symmetric': True, 'granularity': 'per_tensor',
+                                      'static': True, 'calib_algo': 'static_hist'}},
+                    'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}, 'diag': False},
     'rtn': {'quant': {'method': 'RTN',
                       'weight': {'bit': 8, 'symmetric': True, 'granularity': 'per_channel'}},
             'calib': None},

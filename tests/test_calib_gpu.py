@@ -109,3 +109,33 @@ def test_large_segment_qparams_oracle(dev):
         assert s[0].dtype == rs.dtype
         assert abs(s[0].cpu().item() - rs.item()) <= torch.finfo(torch.float32).eps * rs.item()
         assert z[0].cpu().float().item() == rz.float().item()
+
+
+@pytest.mark.parametrize('name', F.names('acthist_'))
+def test_static_hist_vs_reference(dev, name):
+    """static_hist (quant.py:264-529) on the device: exact per-segment histograms, the
+    reference's combination and threshold walk -> the same thresholded range and scale.
+    (The reference's fp32 sums of the histogram / error vectors and its vectorised linspace
+    are SIMD-width dependent; ours fix one order: T2, measured equal on every case.)"""
+    from lightcompress_amd.quant import IntegerQuantizer
+    c = F.load(name)
+    q = IntegerQuantizer(8, True, 'per_tensor', calib_algo='static_hist')
+    sc, zc, _, _ = q.get_batch_tensors_qparams(_entries(c, dev))
+    assert sc[0].dtype == torch.float32 and float(zc[0]) == 0.0
+    rs = c['scales'].reshape(())
+    assert torch.equal(sc[0].cpu().reshape(()), rs), (sc[0].item(), rs.item())
+
+
+def test_static_hist_large_vs_oracle(dev):
+    """16 calibration entries of 2048 x 1024 bf16 with growing ranges (every combination
+    upscales) against the oracle."""
+    from lightcompress_amd.quant import IntegerQuantizer
+    g = torch.Generator().manual_seed(11)
+    xs = [((torch.randn(1, 2048, 1024, generator=g) + 0.1) * (1 + 0.05 * i)).to(torch.bfloat16)
+          for i in range(16)]
+    q = IntegerQuantizer(8, True, 'per_tensor', calib_algo='static_hist')
+    sc, _, _, _ = q.get_batch_tensors_qparams([x.to(dev) for x in xs])
+    (tensors,) = C.batch_entries(xs)
+    lo, hi = C.hist_range(tensors)
+    rs, _ = C.qparams(lo, hi, *C.int_range(8, True), True)
+    assert abs(sc[0].item() - rs.item()) <= 1e-3 * rs.item(), (sc[0].item(), rs.item())

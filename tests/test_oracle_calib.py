@@ -39,3 +39,17 @@ def test_oracle_matches_reference(name):
     if 'fq' in c:
         fq = C.fake_quant_act_static_int(case_entries(c)[0], s, z, qmin, qmax)
         assert torch.equal(fq, c['fq'])
+
+
+HIST = F.names('acthist_')
+
+
+@pytest.mark.parametrize('name', HIST)
+def test_hist_oracle_matches_reference(name):
+    c = F.load(name)
+    (tensors,) = C.batch_entries(case_entries(c))
+    lo, hi = C.hist_range(tensors)
+    assert torch.equal(lo.reshape(()), c['rmin'].reshape(())) and \
+        torch.equal(hi.reshape(()), c['rmax'].reshape(()))
+    s, _ = C.qparams(lo, hi, *C.int_range(8, True), True)
+    assert torch.equal(s.reshape(()), c['scales'].reshape(()))

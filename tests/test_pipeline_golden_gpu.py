@@ -181,13 +181,14 @@ def test_gptq_static_groups_pipeline_vs_reference(dev):
         assert d < 0.05, k
 
 
-def test_rtn_static_act_pipeline_vs_reference(dev):
-    """RTN w8a8 with static per-tensor activation qparams (rtn_w_a_pertensor_static.yml,
-    static_minmax): the reference's block loop registers buf_act_scales_0 on every linear from
+@pytest.mark.parametrize('name', ['rtn_a8_static', 'rtn_a8_hist'])
+def test_rtn_static_act_pipeline_vs_reference(dev, name):
+    """RTN w8a8 with static per-tensor activation qparams (rtn_w_a_pertensor_static.yml:
+    static_hist as shipped, and static_minmax): the reference's block loop registers buf_act_scales_0 on every linear from
     its calibration inputs. Deployed weights bit-equal (T1); the first subset's inputs are
     identical, so its act scale equals the reference's (the fp32 mean may differ in its last
     bit: sum order, T2); later inputs come from GPU vs CPU float forwards (module docstring)."""
-    ref, got, diag = run_ours('rtn_a8_static', dev)
+    ref, got, diag = run_ours(name, dev)
     assert all(eq == 1.0 for eq in compare(ref, got).values())
     akeys = sorted(k for k in ref if k.startswith('a_'))
     assert sorted(diag) == akeys and len(akeys) == 14
