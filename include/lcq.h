@@ -186,6 +186,15 @@ int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, int cnt, in
  * AWQ (awq.py) and auto-clip (auto_clip.py) building blocks. dtype = BF16/F16/F32; each op
  * rounds to dtype like the reference's torch expressions.
  * ------------------------------------------------------------------------------------- */
+/* calib_algo 'mse' (quant.py:145-203 get_mse_range, then get_qparams :545-559): per group of
+ * `group` contiguous elements of x (rows groups), the shrink grid p = 1 - i / grid for
+ * i < nsteps (= int(maxshrink * grid)) on the fp32 values, err = sum |qdq(x) - x|^norm, the
+ * first strict minimum kept. Outputs fp32 [rows]: range_min, range_max, scales, zeros (asym;
+ * may be NULL when sym). */
+int lcq_mse_qparams(const void* x, int dtype, int64_t rows, int64_t group, int sym, int qmin,
+                    int qmax, int nsteps, float grid, float norm, void* range_min,
+                    void* range_max, void* scales, void* zeros, void* stream);
+
 /* Workspace bytes of lcq_absmean_cols / lcq_awq_weight_scale for a [rows, cols] input. */
 int64_t lcq_colmean_workspace_bytes(int64_t rows, int64_t cols);
 

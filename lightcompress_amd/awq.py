@@ -138,6 +138,10 @@ class Awq(BaseBlockwiseQuantization):
         """awq.py:147-164: Q(W * s) in the weight dtype, fused in one kernel."""
         wq = self.wquantizer
         w = fc.weight.data
+        if wq.calib_algo == 'mse':  # the range search needs W * s itself
+            ops.scale_bcast(w, scales.to(w.dtype), 'mul', out=out)
+            out.copy_(wq.fake_quant_weight_dynamic(out))
+            return out
         x2, group = wq._kernel_view(w)
         ops.int_quant_dynamic(x2, group, int(wq.qmin.item()), int(wq.qmax.item()), wq.sym,
                               pre_scale=scales.to(w.dtype), qparams=False, out=out)

@@ -704,3 +704,20 @@ def act_static_hist_qparams(segs, minmax: torch.Tensor, bit: int, qmax: float) -
            ctypes.cast(lens, ctypes.c_void_p), n, N.dt(segs[0]), N.ptr(minmax.contiguous()),
            2 ** int(bit), float(qmax), N.ptr(out), N.ptr(ws), N.stream_of(out))
     return out
+
+
+def mse_qparams(x2: torch.Tensor, group: int, sym: bool, qmin: int, qmax: int, nsteps: int,
+                grid: float, norm: float = 2.4):
+    """get_mse_range + get_qparams (quant.py:145-203, 545-559) per group of `group`
+    contiguous elements of x2. Returns fp32 (min, max, scales, zeros | None), one per group."""
+    x2 = x2.contiguous()
+    ng = x2.numel() // group
+    dev = x2.device
+    mn = torch.empty(ng, dtype=torch.float32, device=dev)
+    mx = torch.empty_like(mn)
+    s = torch.empty_like(mn)
+    z = None if sym else torch.empty_like(mn)
+    N.call('lcq_mse_qparams', N.ptr(x2), N.dt(x2), ng, int(group), int(bool(sym)), int(qmin),
+           int(qmax), int(nsteps), float(grid), float(norm), N.ptr(mn), N.ptr(mx), N.ptr(s),
+           N.ptr(z), N.stream_of(x2))
+    return mn, mx, s, z

@@ -126,7 +126,7 @@ class BaseQuantizer:
         raise NotImplementedError(f'granularity {g} is not on the device path yet')
 
     def _check_supported(self, args):
-        if self.calib_algo not in _MINMAX_LIKE:
+        if self.calib_algo not in _MINMAX_LIKE + ('mse',):
             raise NotImplementedError(f'calib_algo={self.calib_algo} is not on the device path')
         if not self.round_zp:
             raise NotImplementedError('round_zp=False is not on the device path')
@@ -143,7 +143,23 @@ class BaseQuantizer:
         return tensor.amin(dim=-1, keepdim=True), tensor.amax(dim=-1, keepdim=True)
 
     def get_tensor_range(self, tensor, args={}):
+        if self.calib_algo == 'mse':
+            return self.get_mse_range(tensor)
         return self.get_minmax_range(tensor)
+
+    def _mse_nsteps(self):
+        return int(self.maxshrink * self.mse_grid)
+
+    def get_mse_range(self, tensor, norm=2.4, bs=256):
+        """quant.py:145-203 on the device (``lcq_mse_qparams``): tensor is the reshaped
+        [groups, group] view; returns fp32 (min, max) [groups, 1]."""
+        assert self.mse_b_num >= 1 and tensor.shape[0] % self.mse_b_num == 0, \
+            'Batch number must be divisible by tensor.shape[0],'
+        t = tensor.reshape(tensor.shape[0], -1)
+        qmin, qmax = self._iq
+        mn, mx, _, _ = ops.mse_qparams(t, t.shape[1], self.sym, qmin, qmax, self._mse_nsteps(),
+                                       float(self.mse_grid), norm)
+        return mn.view(-1, 1), mx.view(-1, 1)
 
     # -- static activation calibration (quant.py:103-120, 221-262, 431-450, 561-586) --------
     def reshape_batch_tensors(self, act_tensors):
@@ -239,9 +255,31 @@ class IntegerQuantizer(BaseQuantizer):
         z = (qmin - torch.round(mn / s)).clamp(qmin, qmax)
         return s, z, qmax, qmin
 
+    def _mse(self, tensor):
+        """(x2, group, scales [ng] fp32, zeros [ng] fp32 | None) from the MSE range search."""
+        if self.granularity not in ('per_group', 'per_channel', 'per_token', 'per_tensor'):
+            raise NotImplementedError(f'mse with {self.granularity}')
+        x2, group = self._kernel_view(tensor.contiguous())
+        if (x2.numel() // group) % self.mse_b_num:
+            raise AssertionError('Batch number must be divisible by tensor.shape[0],')
+        qmin, qmax = self._iq
+        _, _, s, z = ops.mse_qparams(x2, group, self.sym, qmin, qmax, self._mse_nsteps(),
+                                     float(self.mse_grid))
+        return x2, group, s, z
+
     def get_tensor_qparams(self, tensor, args={}):
         """quant.py:690-697: (reshaped tensor, scales, zeros, qmax, qmin)."""
         self._check_supported(args)
+        if self.calib_algo == 'mse':  # fp32 qparams from the search over tensor.float()
+            _, _, s, z = self._mse(tensor)
+            dev = tensor.device
+            zeros = z.view(-1, 1) if not self.sym else torch.tensor(0.0)
+            scales = s.view(-1, 1)
+            if self.granularity == 'per_tensor':
+                scales = scales.reshape(())
+                zeros = zeros.reshape(()) if not self.sym else zeros
+            return (self.reshape_tensor(tensor), scales, zeros, self.qmax.to(dev),
+                    self.qmin.to(dev))
         x2, group = self._kernel_view(tensor.contiguous())
         qmin, qmax = self._iq
         r = ops.int_quant_dynamic(x2, group, qmin, qmax, self.sym, fq=False)
@@ -314,8 +352,13 @@ class IntegerQuantizer(BaseQuantizer):
         tr = self._maybe_t(weight, args)
         w = weight.T if tr else weight
         shape = w.shape
-        x2, group = self._kernel_view(w.contiguous())
         qmin, qmax = self._iq
+        if self.calib_algo == 'mse':  # fp32 scales -> the quant_dequant computes in fp32
+            x2, group, s, z = self._mse(w)
+            fq = ops.int_quant_static(x2, group, s, z, qmin, qmax, ct_dtype=torch.float32,
+                                      fq_dtype=w.dtype)['fq'].reshape(shape)
+            return fq.T if tr else fq
+        x2, group = self._kernel_view(w.contiguous())
         fq = ops.int_quant_dynamic(x2, group, qmin, qmax, self.sym, qparams=False)['fq']
         fq = fq.reshape(shape)
         return fq.T if tr else fq
@@ -341,7 +384,14 @@ class IntegerQuantizer(BaseQuantizer):
         x2, group = self._kernel_view(weight.contiguous())
         qmin, qmax = self._iq
         cd = self._codes_dtype()
-        r = ops.int_quant_dynamic(x2, group, qmin, qmax, self.sym, fq=False, codes_dtype=cd)
+        if self.calib_algo == 'mse':
+            x2, group, s, z = self._mse(weight)
+            r = ops.int_quant_static(x2, group, s, z, qmin, qmax, ct_dtype=torch.float32,
+                                     fq=False, codes_dtype=cd)
+            r['scales'], r['zeros'] = s, (z if z is not None else None)
+        else:
+            r = ops.int_quant_dynamic(x2, group, qmin, qmax, self.sym, fq=False,
+                                      codes_dtype=cd)
         codes = r['codes'].reshape(weight.shape)
         scales = r['scales'] * osf if osf != 1 else r['scales']
         zeros = r['zeros'].to(cd) if not self.sym else None

@@ -175,3 +175,25 @@ def gemm_pack_autoawq(w: torch.Tensor, scales: torch.Tensor, zeros: torch.Tensor
     for i in range(pn):
         qz |= z[:, _AWQ_ORDER[i]::pn] << np.uint32(i * bits)
     return qw.view(np.int32), s16, qz.view(np.int32)
+
+
+def mse_range(t: torch.Tensor, bit: int, sym: bool, maxshrink=0.8, grid=100, norm=2.4):
+    """get_mse_range (quant.py:145-203) on a reshaped [groups, group] tensor: candidates
+    p * (min, max) with p = 1 - i / grid, kept when sum |qdq(x) - x|^norm improves strictly.
+    The reference's best_min_val / best_max_val alias the running min / max (slice views
+    updated in place), so an accepted candidate becomes the base the later p's shrink.
+    Returns fp32 (min, max) [groups, 1]."""
+    qmin, qmax = int_range(bit, sym)
+    x = t.float()
+    mn, mx = x.amin(dim=-1, keepdim=True), x.amax(dim=-1, keepdim=True)
+    best = torch.full([x.shape[0]], float('inf'))
+    for i in range(int(maxshrink * grid)):
+        p = 1 - i / grid
+        lo, hi = p * mn, p * mx
+        s, z = qparams(lo, hi, qmin, qmax, sym)
+        err = (dequant(quant(x, s, z, qmin, qmax), s, z) - x).abs().pow(norm).sum(1)
+        better = err < best
+        best[better] = err[better]
+        mn[better] = lo[better]
+        mx[better] = hi[better]
+    return mn, mx

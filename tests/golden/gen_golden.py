@@ -530,6 +530,36 @@ def gen_act_hist():
 
 
 GENERATORS['act_hist'] = gen_act_hist
+
+
+def gen_mse():
+    """calib_algo 'mse' weight qparams (quant.py:145-203): the searched ranges, get_tensor_qparams
+    scales / zeros, fake_quant_weight_dynamic and real_quant_weight_dynamic outputs."""
+    q = R.quant_module()
+    cases = [
+        # name, bit, sym, granularity, group, rows, cols, mse_b_num
+        ('int4_asym_g128', 4, False, 'per_group', 128, 256, 512, 1),
+        ('int4_sym_g128', 4, True, 'per_group', 128, 128, 512, 2),
+        ('int8_sym_pc', 8, True, 'per_channel', None, 128, 1024, 1),
+        ('int4_asym_pc', 4, False, 'per_channel', None, 96, 768, 1),
+    ]
+    for i, (name, bit, sym, gran, gs, rows, cols, bnum) in enumerate(cases):
+        w = weights(rows, cols, torch.bfloat16, 1500 + i, edge=False)
+        kw = dict(calib_algo='mse', mse_b_num=bnum)
+        if gs:
+            kw['group_size'] = gs
+        quant = q.IntegerQuantizer(bit, sym, gran, **kw)
+        t = quant.reshape_tensor(w.clone())
+        mn, mx = quant.get_mse_range(t)
+        _, s, z, _, _ = quant.get_tensor_qparams(w.clone())
+        fq = quant.fake_quant_weight_dynamic(w.clone())
+        codes, s_rq, z_rq = quant.real_quant_weight_dynamic(w.clone())
+        F.save(f'mse_{name}', w=w, rmin=mn, rmax=mx, scales=s, zeros=None if sym else z, fq=fq,
+               codes=codes, meta=torch.tensor([bit, int(sym), gs or 0, bnum]))
+    print('mse fixtures written')
+
+
+GENERATORS['mse'] = gen_mse
 GENERATORS['awq_v1'] = lambda: gen_awq(only_v1=True)
 
 

@@ -78,3 +78,14 @@ def test_gemm_pack_fixture_exercises_out_of_range_codes():
     g = torch.arange(w.shape[1]) // 128
     iw = torch.round((w + sz[g].t()) / s16[g].t())
     assert ((iw < 0) | (iw > 15)).sum() > 0
+
+
+@pytest.mark.parametrize('name', F.names('mse_'))
+def test_mse_oracle_matches_reference(name):
+    """calib_algo 'mse' range search (quant.py:145-203): the oracle reproduces the reference's
+    searched ranges bit for bit (same torch-CPU ops)."""
+    c = F.load(name)
+    bit, sym, gs, bnum = c['meta'].tolist()
+    t = c['w'].reshape(-1, gs) if gs else c['w']
+    mn, mx = Q.mse_range(t, bit, bool(sym))
+    assert torch.equal(mn, c['rmin']) and torch.equal(mx, c['rmax'])

@@ -161,3 +161,30 @@ def test_every_bf16_value_vs_oracle(dev, bit, sym, gran, g):
     small = small[: (small.numel() // 1024) * 1024].reshape(-1, 1024)
     fq_ref, _, _ = Q.fake_quant_dynamic(small, bit, sym, gran, g)
     assert_bit_equal(wq.fake_quant_weight_dynamic(small.to(dev)), fq_ref, 'fq small')
+
+
+@pytest.mark.parametrize('name', F.names('mse_'))
+def test_mse_qparams_vs_reference(dev, name):
+    """calib_algo 'mse' (quant.py:145-203) on the device: the searched ranges and fp32 qparams
+    equal the reference's for >= 99 % of the groups (the rest are near ties of the error sums,
+    whose order and powf rounding differ: T2), and the fake / real quant outputs follow."""
+    from lightcompress_amd.quant import IntegerQuantizer
+    c = F.load(name)
+    bit, sym, gs, bnum = c['meta'].tolist()
+    gran = 'per_group' if gs else 'per_channel'
+    kw = dict(calib_algo='mse', mse_b_num=bnum)
+    if gs:
+        kw['group_size'] = gs
+    q = IntegerQuantizer(bit, bool(sym), gran, **kw)
+    w = c['w'].to(dev)
+    mn, mx = q.get_mse_range(q.reshape_tensor(w))
+    same = ((mn.cpu() == c['rmin']) & (mx.cpu() == c['rmax'])).float().mean().item()
+    assert same >= 0.99, same
+    _, s, z, _, _ = q.get_tensor_qparams(w)
+    assert s.dtype == torch.float32 and s.shape == c['scales'].shape
+    assert (s.cpu() == c['scales']).float().mean().item() >= 0.99
+    fq = q.fake_quant_weight_dynamic(w).cpu()
+    assert fq.dtype == c['fq'].dtype
+    assert (fq == c['fq']).float().mean().item() >= 0.99
+    codes, _, _ = q.real_quant_weight_dynamic(w)
+    assert (codes.cpu().to(torch.int32) == c['codes'].to(torch.int32)).float().mean().item() >= 0.99
