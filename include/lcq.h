@@ -315,6 +315,15 @@ int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t max_elems, in
                                  int block, int fmt_out, float qmax, float clamp_min,
                                  int add_zero, void* amax_ws, void* scales_out, void* stream);
 
+/* Block-scaled FP8 GEMM (fp8_gemm, kernel.py:141-242, called by block_wise_fp8_forward_func,
+ * module_utils.py:41-46, for LlmcFp8Linear / fp8_forward linears): a [M, K] e4m3 codes with
+ * per-token 128-column scales a_s fp32 [M, K/128] (act_quant); b [N, K] e4m3 codes with
+ * 128x128 block scales b_s fp32 [ceil(N/128), K/128]. c[m, n] = sum_kb (dot_kb(a[m], b[n]) *
+ * a_s[m, kb]) * b_s[n/128, kb], fp32 accumulation, stored as c_dtype (LCQ_F32 / LCQ_BF16).
+ * K % 128 == 0; a / b 16-byte aligned. */
+int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const void* b_s, int64_t M,
+                 int64_t N, int64_t K, void* c, int c_dtype, void* stream);
+
 /* Causal flash-attention forward of the calibration forwards (the sdpa call inside
  * LlamaAttention.forward, reached from awq.py:110-126 inspect forwards and the block forwards
  * of base_blockwise_quantization.py:367-381): out[b, s, h, :] = softmax(q k^T * scale, causal)

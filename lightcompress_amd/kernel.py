@@ -8,7 +8,9 @@ The reference implements these as Triton kernels and picks them on FP8-capable G
 * ``weight_cast_to_fp8`` (kernel.py:57-81): per 128x128 block, same rule, fp32 scales
   ``[ceil(M/128), ceil(N/128)]``;
 * ``weight_cast_to_bf16`` (kernel.py:84-138): y = float(w) * s[block], stored in
-  ``torch.get_default_dtype()`` like the reference (callers then ``.to(torch.bfloat16)``).
+  ``torch.get_default_dtype()`` like the reference (callers then ``.to(torch.bfloat16)``);
+* ``fp8_gemm`` (kernel.py:141-242): block-scaled e4m3 GEMM, per 128-wide K block
+  ``acc += (dot(a, b) * a_s) * b_s`` in fp32 on the fp8 MFMA (csrc/fp8_gemm.hip).
 
 Triton's fp32 ``/`` may be approximate on the reference's hardware; this build divides with
 IEEE round-to-nearest (the torch-CPU result), and casts with c10's RNE rule.
@@ -43,3 +45,7 @@ def weight_cast_to_bf16(x: torch.Tensor, s: torch.Tensor, block_size: int = 128)
     assert x.is_contiguous() and s.is_contiguous(), 'Input tensors must be contiguous'
     assert x.dim() == 2 and s.dim() == 2, 'Input tensors must have 2 dimensions'
     return ops.fp8_dequant_blocks(x, s, block_size, out_dtype=torch.get_default_dtype())
+
+
+def fp8_gemm(a: torch.Tensor, a_s: torch.Tensor, b: torch.Tensor, b_s: torch.Tensor):
+    return ops.fp8_gemm(a, a_s, b, b_s)

@@ -21,6 +21,66 @@ def _fname(fn):
     return fn.func.__name__ if isinstance(fn, partial) else getattr(fn, '__name__', str(fn))
 
 
+# The reference switches between its Triton fp8_gemm and a bf16 round trip on
+# USE_FP8GEMM_TRITON_KERNEL (module_utils.py:14-22); here the HIP fp8 GEMM is always present.
+USE_FP8GEMM_TRITON_KERNEL = True
+
+
+def block_wise_fp8_forward_func(x, w, w_scale, block_size, bias):
+    """module_utils.py:41-46: act_quant of x (1x128 groups), block-scaled fp8 GEMM, bf16."""
+    from .kernel import act_quant, fp8_gemm
+    x, scale = act_quant(x.contiguous(), block_size)
+    y = fp8_gemm(x, scale, w, w_scale).to(torch.bfloat16)
+    if bias is not None:
+        y += bias
+    return y
+
+
+class LlmcFp8Linear(nn.Module):
+    """module_utils.py:223-285: a DeepSeek-V3-style block-fp8 linear (e4m3 weight, 128x128
+    ``weight_scale_inv``) whose forward runs on the fp8 MFMA without a bf16 weight copy."""
+
+    def __init__(self, in_features, out_features, bias, block_size):
+        super().__init__()
+        self.block_size = block_size
+        self.in_features = in_features
+        self.out_features = out_features
+        if bias:
+            self.bias = nn.Parameter(torch.empty(out_features))
+        else:
+            self.register_parameter('bias', None)
+        self.weight = nn.Parameter(
+            torch.empty(out_features, in_features, dtype=torch.float8_e4m3fn),
+            requires_grad=False)
+        so = (out_features + block_size - 1) // block_size
+        si = (in_features + block_size - 1) // block_size
+        self.weight_scale_inv = nn.Parameter(torch.empty(so, si, dtype=torch.float32),
+                                             requires_grad=False)
+
+    def forward(self, x):
+        if self.weight.data.dtype == torch.float8_e4m3fn:
+            if USE_FP8GEMM_TRITON_KERNEL:
+                return block_wise_fp8_forward_func(x, self.weight, self.weight_scale_inv,
+                                                   self.block_size, self.bias)
+            from .kernel import weight_cast_to_bf16
+            self.weight.data = weight_cast_to_bf16(self.weight.data, self.weight_scale_inv.data,
+                                                   self.block_size).to(torch.bfloat16)
+        return F.linear(x, self.weight, self.bias)
+
+    @classmethod
+    @torch.no_grad()
+    def new(cls, module, block_size):
+        return cls(module.in_features, module.out_features, module.bias is not None,
+                   block_size)
+
+    def __repr__(self):
+        return (f'LlmcFp8Linear(in_features={self.in_features}, '
+                f'out_features={self.out_features}, bias={self.bias is not None}, '
+                f'weight_shape={self.weight.shape}, weight_dtype={self.weight.dtype}, '
+                f'block_size={self.block_size}, '
+                f'use_fp8gemm_triton_kernel={USE_FP8GEMM_TRITON_KERNEL})')
+
+
 class FakeQuantLinear(nn.Module):
     """module_utils.py:679-771 — weight fake-quantised lazily on first forward (w_qdq)."""
 

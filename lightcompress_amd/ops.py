@@ -518,6 +518,37 @@ def fp8_dequant_blocks(codes: torch.Tensor, scales: torch.Tensor, block: int = 1
     return out
 
 
+def fp8_gemm(a: torch.Tensor, a_s: torch.Tensor, b: torch.Tensor, b_s: torch.Tensor,
+             out_dtype: torch.dtype | None = None) -> torch.Tensor:
+    """fp8_gemm (kernel.py:216-242): a [..., K] e4m3 with a_s [..., K/128]; b [N, K] e4m3 with
+    b_s [ceil(N/128), K/128]; returns c [..., N] in ``out_dtype`` (default
+    torch.get_default_dtype(), as the reference allocates it)."""
+    assert a.is_contiguous() and b.is_contiguous(), 'Input tensors must be contiguous'
+    assert a_s.is_contiguous() and b_s.is_contiguous(), (
+        'Scaling factor tensors must be contiguous')
+    if a.dtype != torch.float8_e4m3fn or b.dtype != torch.float8_e4m3fn:
+        raise TypeError(f'fp8_gemm takes float8_e4m3fn operands, got {a.dtype} / {b.dtype}')
+    K = a.size(-1)
+    M = a.numel() // K
+    Nn = b.size(0)
+    if b.dim() != 2 or b.size(1) != K:
+        raise ValueError(f'b shape {tuple(b.shape)} does not match K={K}')
+    if K % 128 != 0:
+        raise ValueError(f'K={K} is not a multiple of the 128-column scale block')
+    nkb = K // 128
+    if a_s.numel() != M * nkb or a_s.dtype != torch.float32:
+        raise ValueError(f'a_s must be fp32 with {M}x{nkb} elements')
+    if tuple(b_s.shape) != ((Nn + 127) // 128, nkb) or b_s.dtype != torch.float32:
+        raise ValueError(f'b_s must be fp32 [{(Nn + 127) // 128}, {nkb}]')
+    out_dtype = torch.get_default_dtype() if out_dtype is None else out_dtype
+    c = torch.empty(*a.shape[:-1], Nn, dtype=out_dtype, device=a.device)
+    if M == 0:
+        return c
+    N.call('lcq_fp8_gemm', N.ptr(a), N.ptr(a_s), N.ptr(b), N.ptr(b_s), M, Nn, K, N.ptr(c),
+           N.dt(out_dtype), N.stream_of(a))
+    return c
+
+
 def fp8_block_to_tensor(codes: torch.Tensor, scales_inv: torch.Tensor, block: int = 128,
                         fp8: torch.dtype = torch.float8_e4m3fn, qmax: float | None = None):
     """Block-fp8 weight -> bf16 (weight_cast_to_bf16) -> per-tensor fp8 real quant, fused.

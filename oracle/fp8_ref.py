@@ -9,6 +9,9 @@ torch-CPU ops, keeping the reference's dtype promotion. Pinning (tests/golden, g
   image -> the restatement uses torch's native cast (c10 RNE) there: parity UNPINNED for that
   one step.
 * kernel.py: Triton cannot run without a GPU -> restated from source, unpinned.
+* fp8_gemm (kernel.py:141-214): restated from source, parity unpinned (no Triton here); the
+  restatement is itself checked against an exact float64 dequantized matmul
+  (tests/test_oracle_fp8.py).
 """
 from __future__ import annotations
 
@@ -138,3 +141,22 @@ def weight_cast_to_bf16(y: torch.Tensor, s: torch.Tensor, block: int = 128,
     M, N = y.shape
     se = s.repeat_interleave(block, 0).repeat_interleave(block, 1)[:M, :N]
     return (y.float() * se).to(out_dtype)
+
+
+def fp8_gemm(a: torch.Tensor, a_s: torch.Tensor, b: torch.Tensor, b_s: torch.Tensor):
+    """kernel.py:141-214 (fp8_gemm_kernel): per 128-wide K block kb,
+    acc += (dot(a[:, kb], b[:, kb]^T) * a_s[:, kb, None]) * b_s[n / 128, kb]; fp32 result.
+    The block dot is formed in float64 and rounded once to fp32 (the exact sum the MFMA's fp32
+    accumulation approximates), then scaled and accumulated in fp32 in the kernel's order."""
+    K = a.shape[-1]
+    M = a.numel() // K
+    Nn = b.shape[0]
+    af = a.reshape(M, K).double()
+    bf = b.double()
+    asf = a_s.reshape(M, K // 128).float()
+    bse = b_s.float().repeat_interleave(128, 0)[:Nn]
+    acc = torch.zeros(M, Nn, dtype=torch.float32)
+    for kb in range(K // 128):
+        d = (af[:, kb * 128:(kb + 1) * 128] @ bf[:, kb * 128:(kb + 1) * 128].T).float()
+        acc = acc + (d * asf[:, kb:kb + 1]) * bse[:, kb][None, :]
+    return acc.reshape(*a.shape[:-1], Nn)

@@ -218,3 +218,88 @@ def test_block_fp8_to_tensor_single_vs_oracle(dev, block, shape):
     assert torch.equal(bits(oc), rc.view(torch.uint8)) and os_.item() == rs.item()
     am = ops.absmax(O.weight_cast_to_bf16(c, s, block).to(dev))
     assert am.item() == O.weight_cast_to_bf16(c, s, block).float().abs().max().item()
+
+
+def _gemm_inputs(M, Nn, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(M, K, generator=g) * torch.exp(torch.randn(M, 1, generator=g))
+    w = torch.randn(Nn, K, generator=g) * 0.05
+    a, a_s = O.act_quant(x)
+    b, b_s = O.weight_cast_to_fp8(w)
+    return a, a_s, b, b_s
+
+
+def _abs_gemm(a, a_s, b, b_s):
+    return O.fp8_gemm(a.view(torch.uint8).bitwise_and(0x7F).view(torch.float8_e4m3fn), a_s.abs(),
+                      b.view(torch.uint8).bitwise_and(0x7F).view(torch.float8_e4m3fn), b_s.abs())
+
+
+# ragged M / N tiles, one K block, the DeepSeek-V3 hidden size (K 7168)
+@pytest.mark.parametrize('M,Nn,K', [(1, 128, 128), (37, 200, 384), (256, 512, 1024),
+                                    (130, 2048, 7168)])
+def test_fp8_gemm_vs_oracle(dev, M, Nn, K):
+    """lcq_fp8_gemm vs the fp8_gemm restatement (kernel.py:141-214): same per-block scaling
+    order; only the fp32 accumulation order inside a 128-wide block differs (tolerance 1e-5 of
+    the |a||b| product)."""
+    from lightcompress_amd import ops
+    a, a_s, b, b_s = _gemm_inputs(M, Nn, K, seed=M * 7 + Nn)
+    got = ops.fp8_gemm(a.to(dev), a_s.to(dev), b.to(dev), b_s.to(dev),
+                       out_dtype=torch.float32).cpu()
+    want = O.fp8_gemm(a, a_s, b, b_s)
+    tol = 1e-5 * _abs_gemm(a, a_s, b, b_s) + 1e-30
+    err = (got - want).abs()
+    assert (err <= tol).all(), float((err / tol).max())
+
+
+def test_fp8_gemm_bf16_out_and_leading_dims(dev):
+    from lightcompress_amd import kernel
+    a, a_s, b, b_s = _gemm_inputs(24, 384, 512, seed=11)
+    a3, s3 = a.reshape(2, 12, 512), a_s.reshape(2, 12, 4)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16)
+    try:
+        got = kernel.fp8_gemm(a3.to(dev), s3.to(dev), b.to(dev), b_s.to(dev)).cpu()
+    finally:
+        torch.set_default_dtype(prev)
+    assert got.dtype == torch.bfloat16 and got.shape == (2, 12, 384)
+    want = O.fp8_gemm(a, a_s, b, b_s).reshape(2, 12, 384)
+    tol = 1e-5 * _abs_gemm(a, a_s, b, b_s).reshape(2, 12, 384) + want.abs() * 2.0 ** -8
+    assert ((got.float() - want).abs() <= tol).all()
+
+
+def test_llmc_fp8_linear_forward(dev):
+    """LlmcFp8Linear.forward = block_wise_fp8_forward_func (module_utils.py:41-46, 244-262):
+    act_quant bit-exact, then the fp8 GEMM, bf16, + bias."""
+    import torch.nn as nn
+    from lightcompress_amd.module_utils import LlmcFp8Linear
+    g = torch.Generator().manual_seed(2)
+    lin = nn.Linear(512, 320, bias=True)
+    m = LlmcFp8Linear.new(lin, 128)
+    w = torch.randn(320, 512, generator=g) * 0.05
+    b, b_s = O.weight_cast_to_fp8(w)
+    bias = (torch.randn(320, generator=g) * 0.1).to(torch.bfloat16)
+    m.weight.data = b
+    m.weight_scale_inv.data = b_s
+    m.bias = nn.Parameter(bias, requires_grad=False)
+    m = m.to(dev)
+    x = (torch.randn(3, 5, 512, generator=g)).to(torch.bfloat16)
+    got = m(x.to(dev)).cpu()
+    a, a_s = O.act_quant(x)
+    want = O.fp8_gemm(a, a_s, b, b_s).to(torch.bfloat16) + bias
+    assert got.dtype == torch.bfloat16 and got.shape == (3, 5, 320)
+    assert (got.float() - want.float()).abs().max() <= 2.0 ** -6 * want.float().abs().max()
+    from lightcompress_amd import kernel
+    ya, sa = kernel.act_quant(x.to(dev).contiguous())
+    assert torch.equal(ya.cpu().view(torch.uint8), a.view(torch.uint8))
+    assert torch.equal(sa.cpu(), a_s)
+
+
+def test_fp8_gemm_rejects_bad_shapes(dev):
+    from lightcompress_amd import ops
+    a, a_s, b, b_s = _gemm_inputs(8, 128, 256, seed=1)
+    with pytest.raises(ValueError):
+        ops.fp8_gemm(a.to(dev), a_s.to(dev), b[:, :128].contiguous().to(dev), b_s.to(dev))
+    with pytest.raises(ValueError):
+        ops.fp8_gemm(a.to(dev), a_s[:, :1].contiguous().to(dev), b.to(dev), b_s.to(dev))
+    with pytest.raises(TypeError):
+        ops.fp8_gemm(a.float().to(dev), a_s.to(dev), b.to(dev), b_s.to(dev))

@@ -91,3 +91,44 @@ def test_encoder_model_matches_torch_cast(fmt):
     got = enc_model(x.numpy(), fmt == 'e4m3')
     nan = np.isnan(x.numpy())
     assert np.array_equal(got[~nan], ref[~nan])
+
+
+def _gemm_case(M, Nn, K, seed, batch=None):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(M, K, generator=g) * torch.exp(torch.randn(M, 1, generator=g))
+    w = torch.randn(Nn, K, generator=g) * 0.05
+    a, a_s = O.act_quant(x)
+    b, b_s = O.weight_cast_to_fp8(w)
+    if batch is not None:
+        a = a.reshape(*batch, K)
+        a_s = a_s.reshape(*batch, K // 128)
+    return a, a_s, b, b_s
+
+
+def _dequant_gemm(a, a_s, b, b_s, absolute=False):
+    K = a.shape[-1]
+    ad = a.reshape(-1, K).double() * a_s.reshape(-1, K // 128).double().repeat_interleave(128, 1)
+    bd = b.double() * b_s.double().repeat_interleave(128, 0)[:b.shape[0]].repeat_interleave(128, 1)
+    if absolute:
+        ad, bd = ad.abs(), bd.abs()
+    return (ad @ bd.T).reshape(*a.shape[:-1], b.shape[0])
+
+
+@pytest.mark.parametrize('M,Nn,K', [(1, 128, 128), (37, 200, 384), (64, 256, 1024)])
+def test_fp8_gemm_oracle_vs_exact_dequant_matmul(M, Nn, K):
+    """fp8_gemm restatement (kernel.py:141-214) vs the exact float64 dequantized product:
+    fp32 accumulation error only (tolerance 1e-5 of the |a||b| product)."""
+    a, a_s, b, b_s = _gemm_case(M, Nn, K, seed=M + Nn)
+    got = O.fp8_gemm(a, a_s, b, b_s)
+    assert got.dtype == torch.float32 and got.shape == (M, Nn)
+    exact = _dequant_gemm(a, a_s, b, b_s)
+    tol = 1e-5 * _dequant_gemm(a, a_s, b, b_s, absolute=True) + 1e-30
+    assert ((got.double() - exact).abs() <= tol).all()
+
+
+def test_fp8_gemm_oracle_batched_leading_dims():
+    a, a_s, b, b_s = _gemm_case(6, 130, 256, seed=5, batch=(2, 3))
+    got = O.fp8_gemm(a, a_s, b, b_s)
+    assert got.shape == (2, 3, 130)
+    flat = O.fp8_gemm(a.reshape(6, 256), a_s.reshape(6, 2), b, b_s)
+    assert torch.equal(got.reshape(6, 130), flat)
