@@ -7,17 +7,19 @@
 // A [M, K] e4m3 (act_quant output, per-token 128-column scales a_s [M, K/128]); B [N, K] e4m3
 // with 128x128 block scales b_s [ceil(N/128), K/128]; fp32 accumulation; C fp32 or bf16.
 //
-// Tile 128x128 per workgroup (4 waves, each 64x64 = 2x2 MFMA 32x32x16 fp8 tiles), one K block
-// of 128 per step staged through LDS (16-byte global loads, padded rows); the block's partial
-// dot products are scaled ((dot * a_s) * b_s, the reference's order) and accumulated in fp32.
+// Tile 128x128 (or 64x128 when the grid would be small) per workgroup, 4 waves on gfx950's
+// 32x32x64 f8f6f4 MFMA, one K block of 128 per step double-buffered through LDS (16-byte global
+// loads into registers one block ahead, padded rows); the block's partial dot products are
+// scaled ((dot * a_s) * b_s, the reference's order) and accumulated in fp32.
 #include "lcq_common.h"
 
 namespace lcq {
 namespace {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
+typedef int v8i __attribute__((ext_vector_type(8)));
 
-constexpr int BM = 128, BN = 128, BK = 128;
+constexpr int BN = 128, BK = 128;
 constexpr int LDA = BK + 16;  // padded LDS row (bytes): 16-byte aligned, offsets the banks
 
 struct GemmArgs {
@@ -30,84 +32,129 @@ struct GemmArgs {
   int c_dt;
 };
 
-__global__ __launch_bounds__(256) void k_fp8_gemm(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) uint8_t sa[BM * LDA];
-  __shared__ __attribute__((aligned(16))) uint8_t sb[BN * LDA];
-  __shared__ float sas[BM];
+// BM x 128 output tile per workgroup, 4 waves in a 2 x 2 grid, each (BM/2) x 64 of 32x32 MFMA
+// tiles. K advances one 128-wide scale block at a time through two LDS buffers: the global
+// loads of block kb+1 are issued into registers before block kb's MFMAs and written to the
+// other buffer after them (one barrier per block). The MFMA is gfx950's 32x32x64 f8f6f4 form
+// (e4m3 x e4m3, no block scale: twice the fp8 rate of 32x32x16); each lane feeds 32 consecutive
+// k of its row to both operands, so the k order inside the instruction is the same for A and B.
+template <int BM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_fp8_gemm(GemmArgs g) {
+  constexpr int TI = BM / 64;          // 32-row MFMA tiles per wave
+  constexpr int ACH = BM * 8 / 256;    // 16-byte A chunks per thread per block
+  constexpr int BCH = BN * 8 / 256;
+  __shared__ __attribute__((aligned(16))) uint8_t sa[2][BM * LDA];
+  __shared__ __attribute__((aligned(16))) uint8_t sb[2][BN * LDA];
+  __shared__ float sas[2][BM];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
   const int64_t nkb = g.K / BK;
   const float* bsrow = g.bs + (n0 / 128) * nkb;
-  v16f acc[2][2];
+  const int r_hi = lane >> 5, r_lo = lane & 31;
+
+  uint4 ra[ACH], rb[BCH];
+  float ras = 0.f;
+  auto load = [&](int64_t kb) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int p = 0; p < ACH; ++p) {
+      const int idx = p * 256 + tid, row = idx >> 3, ch = idx & 7;
+      ra[p] = make_uint4(0, 0, 0, 0);
+      if (m0 + row < g.M)
+        ra[p] = *reinterpret_cast<const uint4*>(g.a + (m0 + row) * g.K + kb * BK + ch * 16);
+    }
+#pragma unroll
+    for (int p = 0; p < BCH; ++p) {
+      const int idx = p * 256 + tid, row = idx >> 3, ch = idx & 7;
+      rb[p] = make_uint4(0, 0, 0, 0);
+      if (n0 + row < g.N)
+        rb[p] = *reinterpret_cast<const uint4*>(g.b + (n0 + row) * g.K + kb * BK + ch * 16);
+    }
+    if (tid < BM) ras = (m0 + tid < g.M) ? g.as[(m0 + tid) * nkb + kb] : 0.f;
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < ACH; ++p) {
+      const int idx = p * 256 + tid, row = idx >> 3, ch = idx & 7;
+      *reinterpret_cast<uint4*>(&sa[buf][row * LDA + ch * 16]) = ra[p];
+    }
+#pragma unroll
+    for (int p = 0; p < BCH; ++p) {
+      const int idx = p * 256 + tid, row = idx >> 3, ch = idx & 7;
+      *reinterpret_cast<uint4*>(&sb[buf][row * LDA + ch * 16]) = rb[p];
+    }
+    if (tid < BM) sas[buf][tid] = ras;
+  };
+
+  v16f acc[TI][2];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const int r_hi = lane >> 5, r_lo = lane & 31;
+
+  load(0);
+  store(0);
+  __syncthreads();
   for (int64_t kb = 0; kb < nkb; ++kb) {
-    // stage A / B K-block tiles (128 rows x 128 bytes each; rows past M / N read as zeros)
+    const int buf = (int)(kb & 1);
+    if (kb + 1 < nkb) load(kb + 1);
+    v16f t[TI][2];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int idx = p * 256 + tid;
-      const int row = idx >> 3, ch = idx & 7;
-      uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
-      if (m0 + row < g.M)
-        va = *reinterpret_cast<const uint4*>(g.a + (m0 + row) * g.K + kb * BK + ch * 16);
-      if (n0 + row < g.N)
-        vb = *reinterpret_cast<const uint4*>(g.b + (n0 + row) * g.K + kb * BK + ch * 16);
-      *reinterpret_cast<uint4*>(sa + row * LDA + ch * 16) = va;
-      *reinterpret_cast<uint4*>(sb + row * LDA + ch * 16) = vb;
-    }
-    if (tid < BM) sas[tid] = (m0 + tid < g.M) ? g.as[(m0 + tid) * nkb + kb] : 0.f;
-    __syncthreads();
-    v16f t[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      long fa[2], fb[2];
+    for (int ks = 0; ks < BK / 64; ++ks) {
+      v8i fa[TI], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        fa[i] = *reinterpret_cast<const long*>(sa + (64 * wm + 32 * i + r_lo) * LDA + 16 * ks +
-                                               8 * r_hi);
+      for (int i = 0; i < TI; ++i) {
+        const uint8_t* p = &sa[buf][((BM / 2) * wm + 32 * i + r_lo) * LDA + 64 * ks + 32 * r_hi];
+        const uint4 lo = *reinterpret_cast<const uint4*>(p);
+        const uint4 hi = *reinterpret_cast<const uint4*>(p + 16);
+        fa[i] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w,
+                    (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[j] = *reinterpret_cast<const long*>(sb + (64 * wn + 32 * j + r_lo) * LDA + 16 * ks +
-                                               8 * r_hi);
+      for (int j = 0; j < 2; ++j) {
+        const uint8_t* p = &sb[buf][(64 * wn + 32 * j + r_lo) * LDA + 64 * ks + 32 * r_hi];
+        const uint4 lo = *reinterpret_cast<const uint4*>(p);
+        const uint4 hi = *reinterpret_cast<const uint4*>(p + 16);
+        fb[j] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w,
+                    (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(fa[i], fb[j], t[i][j], 0, 0, 0);
+          t[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[i], fb[j], t[i][j], 0, 0,
+                                                                    0, 0, 0, 0);
     }
     // acc += (dot * a_s[m]) * b_s[n / 128]   (kernel.py: tl.dot(a, b) * a_s[:, None] * b_s)
     const float bsv = bsrow[kb];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float asv = sas[64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * r_hi];
+        const float asv = sas[buf][(BM / 2) * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * r_hi];
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j][r] = acc[i][j][r] + (t[i][j][r] * asv) * bsv;
       }
+    if (kb + 1 < nkb) store(buf ^ 1);
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int64_t n = n0 + 64 * wn + 32 * j + r_lo;
       if (n >= g.N) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * r_hi;
+        const int64_t m = m0 + (BM / 2) * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * r_hi;
         if (m >= g.M) continue;
         if (g.c_dt == LCQ_F32) reinterpret_cast<float*>(g.c)[m * g.N + n] = acc[i][j][r];
         else st1<LCQ_BF16>(g.c, m * g.N + n, acc[i][j][r]);
@@ -132,7 +179,14 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
               "A / B must be 16-byte aligned");
   GemmArgs g{static_cast<const uint8_t*>(a), static_cast<const float*>(a_s),
              static_cast<const uint8_t*>(b), static_cast<const float*>(b_s), c, M, N, K, c_dtype};
-  dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM));
-  k_fp8_gemm<<<grid, 256, 0, as_stream(stream)>>>(g);
+  // 128-row tiles unless that leaves most of the 256 CUs idle (short calibration batches)
+  const int64_t nt = (N + BN - 1) / BN;
+  if (((M + 127) / 128) * nt >= 512) {
+    dim3 grid((unsigned)nt, (unsigned)((M + 127) / 128));
+    k_fp8_gemm<128><<<grid, 256, 0, as_stream(stream)>>>(g);
+  } else {
+    dim3 grid((unsigned)nt, (unsigned)((M + 63) / 64));
+    k_fp8_gemm<64><<<grid, 256, 0, as_stream(stream)>>>(g);
+  }
   return check_launch("lcq_fp8_gemm");
 }
