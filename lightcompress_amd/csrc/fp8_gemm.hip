@@ -48,7 +48,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __shared__ float sas[2][BM];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+  // XCD-aware tile order: workgroup L runs on XCD L % 8, so hand each XCD a contiguous run of
+  // tiles, walked in groups of 8 M-tiles (column-major inside a group) to share A / B in its L2
+  const unsigned nx = gridDim.x, my = gridDim.y, total = nx * my;
+  unsigned L = blockIdx.x + nx * blockIdx.y;
+  if ((total & 7u) == 0) L = (L & 7u) * (total >> 3) + (L >> 3);
+  const unsigned grp = L / (8u * nx), first = grp * 8u;
+  const unsigned gsz = (my - first) < 8u ? (my - first) : 8u;
+  const unsigned in = L - grp * 8u * nx;
+  const int64_t m0 = (int64_t)(first + in % gsz) * BM, n0 = (int64_t)(in / gsz) * BN;
   const int64_t nkb = g.K / BK;
   const float* bsrow = g.bs + (n0 / 128) * nkb;
   const int r_hi = lane >> 5, r_lo = lane & 31;
