@@ -320,9 +320,13 @@ int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t max_elems, in
  * per-token 128-column scales a_s fp32 [M, K/128] (act_quant); b [N, K] e4m3 codes with
  * 128x128 block scales b_s fp32 [ceil(N/128), K/128]. c[m, n] = sum_kb (dot_kb(a[m], b[n]) *
  * a_s[m, kb]) * b_s[n/128, kb], fp32 accumulation, stored as c_dtype (LCQ_F32 / LCQ_BF16).
- * K % 128 == 0; a / b 16-byte aligned. */
+ * K % 128 == 0; a / b 16-byte aligned. Short batches split K across workgroups when
+ * `workspace` holds lcq_fp8_gemm_workspace_bytes(M, N, K) bytes of device memory (fp32
+ * partials summed in split order: deterministic); null / smaller workspace = no split. */
+int64_t lcq_fp8_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const void* b_s, int64_t M,
-                 int64_t N, int64_t K, void* c, int c_dtype, void* stream);
+                 int64_t N, int64_t K, void* c, int c_dtype, void* workspace, int64_t ws_bytes,
+                 void* stream);
 
 /* Causal flash-attention forward of the calibration forwards (the sdpa call inside
  * LlamaAttention.forward, reached from awq.py:110-126 inspect forwards and the block forwards

@@ -10,7 +10,9 @@
 // Tile 128x128 (or 64x128 when the grid would be small) per workgroup, 4 waves on gfx950's
 // 32x32x64 f8f6f4 MFMA, one K block of 128 per step double-buffered through LDS (16-byte global
 // loads into registers one block ahead, padded rows); the block's partial dot products are
-// scaled ((dot * a_s) * b_s, the reference's order) and accumulated in fp32.
+// scaled ((dot * a_s) * b_s, the reference's order) and accumulated in fp32. Grids of fewer
+// than 256 64-row tiles (short MoE / calibration batches) split K over blockIdx.z into fp32
+// partials that a second kernel sums in split order (deterministic).
 #include "lcq_common.h"
 
 namespace lcq {
@@ -28,7 +30,9 @@ struct GemmArgs {
   const uint8_t* b;
   const float* bs;
   void* c;
+  float* ws;  // split-K partials [splits, M, N] fp32, or null (one split, C written directly)
   int64_t M, N, K;
+  int64_t kb_per_split;
   int c_dt;
 };
 
@@ -58,6 +62,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const unsigned in = L - grp * 8u * nx;
   const int64_t m0 = (int64_t)(first + in % gsz) * BM, n0 = (int64_t)(in / gsz) * BN;
   const int64_t nkb = g.K / BK;
+  const int64_t kb_begin = (int64_t)blockIdx.z * g.kb_per_split;
+  const int64_t kb_end = kb_begin + g.kb_per_split < nkb ? kb_begin + g.kb_per_split : nkb;
   const float* bsrow = g.bs + (n0 / 128) * nkb;
   const int r_hi = lane >> 5, r_lo = lane & 31;
 
@@ -102,12 +108,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  load(0);
+  load(kb_begin);
   store(0);
   __syncthreads();
-  for (int64_t kb = 0; kb < nkb; ++kb) {
-    const int buf = (int)(kb & 1);
-    if (kb + 1 < nkb) load(kb + 1);
+  for (int64_t kb = kb_begin; kb < kb_end; ++kb) {
+    const int buf = (int)((kb - kb_begin) & 1);
+    if (kb + 1 < kb_end) load(kb + 1);
     v16f t[TI][2];
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -151,7 +157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j][r] = acc[i][j][r] + (t[i][j][r] * asv) * bsv;
       }
-    if (kb + 1 < nkb) store(buf ^ 1);
+    if (kb + 1 < kb_end) store(buf ^ 1);
     __syncthreads();
   }
 #pragma unroll
@@ -164,10 +170,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int r = 0; r < 16; ++r) {
         const int64_t m = m0 + (BM / 2) * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * r_hi;
         if (m >= g.M) continue;
-        if (g.c_dt == LCQ_F32) reinterpret_cast<float*>(g.c)[m * g.N + n] = acc[i][j][r];
+        if (g.ws) g.ws[((int64_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
+        else if (g.c_dt == LCQ_F32) reinterpret_cast<float*>(g.c)[m * g.N + n] = acc[i][j][r];
         else st1<LCQ_BF16>(g.c, m * g.N + n, acc[i][j][r]);
       }
     }
+}
+
+// Split-K epilogue: c = sum over splits in split order (deterministic), then the C dtype.
+__global__ __launch_bounds__(256) void k_fp8_gemm_reduce(const float* __restrict__ ws,
+                                                         int splits, int64_t mn, void* c,
+                                                         int c_dt) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < mn;
+       i += (int64_t)gridDim.x * 256) {
+    float v = ws[i];
+    for (int z = 1; z < splits; ++z) v += ws[(int64_t)z * mn + i];
+    if (c_dt == LCQ_F32) reinterpret_cast<float*>(c)[i] = v;
+    else st1<LCQ_BF16>(c, i, v);
+  }
+}
+
+// K splits for a short batch: a 64-row grid of fewer than 256 tiles is split along K until
+// ~512 workgroups (two per CU at this kernel's occupancy) are in flight, keeping at least 4 K
+// blocks per split.
+int64_t gemm_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t nt = (N + BN - 1) / BN;
+  if (((M + 127) / 128) * nt >= 512) return 1;
+  const int64_t tiles = ((M + 63) / 64) * nt, nkb = K / BK;
+  if (tiles >= 256) return 1;  // one workgroup per CU already: the partials' traffic costs more
+  int64_t s = (512 + tiles - 1) / tiles;
+  if (s > nkb / 4) s = nkb / 4;
+  if (s < 2) return 1;
+  const int64_t per = (nkb + s - 1) / s;
+  return (nkb + per - 1) / per;  // no empty split
 }
 
 }  // namespace
@@ -175,9 +210,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 using namespace lcq;
 
+extern "C" int64_t lcq_fp8_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0) return 0;
+  const int64_t s = gemm_splits(M, N, K);
+  return s > 1 ? s * M * N * (int64_t)sizeof(float) : 0;
+}
+
 extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const void* b_s,
                             int64_t M, int64_t N, int64_t K, void* c, int c_dtype,
-                            void* stream) {
+                            void* workspace, int64_t ws_bytes, void* stream) {
   LCQ_REQUIRE(a && a_s && b && b_s && c, "null pointer");
   LCQ_REQUIRE(M > 0 && N > 0 && K > 0, "empty GEMM");
   LCQ_REQUIRE(K % 128 == 0, "K must be a multiple of 128 (the scale block)");
@@ -185,16 +226,30 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
   LCQ_REQUIRE((reinterpret_cast<uintptr_t>(a) & 15) == 0 &&
                   (reinterpret_cast<uintptr_t>(b) & 15) == 0,
               "A / B must be 16-byte aligned");
+  const int64_t nkb = K / BK;
+  int64_t splits = gemm_splits(M, N, K);
+  if (!workspace || ws_bytes < splits * M * N * (int64_t)sizeof(float)) splits = 1;
+  const int64_t per = (nkb + splits - 1) / splits;
   GemmArgs g{static_cast<const uint8_t*>(a), static_cast<const float*>(a_s),
-             static_cast<const uint8_t*>(b), static_cast<const float*>(b_s), c, M, N, K, c_dtype};
+             static_cast<const uint8_t*>(b), static_cast<const float*>(b_s), c,
+             splits > 1 ? static_cast<float*>(workspace) : nullptr, M, N, K, per, c_dtype};
   // 128-row tiles unless that leaves most of the 256 CUs idle (short calibration batches)
   const int64_t nt = (N + BN - 1) / BN;
-  if (((M + 127) / 128) * nt >= 512) {
+  if (splits == 1 && ((M + 127) / 128) * nt >= 512) {
     dim3 grid((unsigned)nt, (unsigned)((M + 127) / 128));
     k_fp8_gemm<128><<<grid, 256, 0, as_stream(stream)>>>(g);
   } else {
-    dim3 grid((unsigned)nt, (unsigned)((M + 63) / 64));
+    dim3 grid((unsigned)nt, (unsigned)((M + 63) / 64), (unsigned)splits);
     k_fp8_gemm<64><<<grid, 256, 0, as_stream(stream)>>>(g);
+  }
+  if (splits > 1) {
+    const int rc = check_launch("lcq_fp8_gemm");
+    if (rc) return rc;
+    const int64_t mn = M * N;
+    int64_t blocks = (mn + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    k_fp8_gemm_reduce<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(
+        static_cast<const float*>(workspace), (int)splits, mn, c, c_dtype);
   }
   return check_launch("lcq_fp8_gemm");
 }

@@ -544,8 +544,10 @@ def fp8_gemm(a: torch.Tensor, a_s: torch.Tensor, b: torch.Tensor, b_s: torch.Ten
     c = torch.empty(*a.shape[:-1], Nn, dtype=out_dtype, device=a.device)
     if M == 0:
         return c
+    wsb = int(N.load().lcq_fp8_gemm_workspace_bytes(M, Nn, K))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=a.device)
     N.call('lcq_fp8_gemm', N.ptr(a), N.ptr(a_s), N.ptr(b), N.ptr(b_s), M, Nn, K, N.ptr(c),
-           N.dt(out_dtype), N.stream_of(a))
+           N.dt(out_dtype), N.ptr(ws), wsb, N.stream_of(a))
     return c
 
 
