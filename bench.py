@@ -41,6 +41,7 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+PEAK_FP8_TFLOPS = 5000.0    # MI355X dense fp8 (e4m3) MFMA (MI355X_MICROARCH.md)
 
 LLAMA3_8B = dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
                  num_key_value_heads=8, head_dim=128, rope_theta=500000.0,
@@ -59,6 +60,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--algo', choices=['awq', 'gptq', 'fp8', 'both', 'all'], default='all')
     ap.add_argument('--fp8-experts', type=int, default=32)
+    ap.add_argument('--fp8-tokens', type=int, default=2048,
+                    help='calibration tokens routed to each expert in the fp8 forward leg')
     ap.add_argument('--gptq-steps', type=int, default=2)
     ap.add_argument('--gptq-samples', type=int, default=128)
     ap.add_argument('--gptq-seq-len', type=int, default=2048)
@@ -363,8 +366,51 @@ def bench_fp8(args, rank, world, dev):
                            'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                            'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic,
                            'traffic_source': src, 'avg_launch_ms': round(t['avg_ms'], 4)}
+    out['calib_forward'] = bench_fp8_forward(args, weights[:12], dev)
     del weights
     torch.cuda.empty_cache()
+    return out
+
+
+def bench_fp8_forward(args, weights, dev):
+    """Calibration forward of block-fp8 expert linears (LlmcFp8Linear.forward =
+    block_wise_fp8_forward_func, module_utils.py:41-46, 244-262): act_quant + the block-scaled
+    fp8 GEMM (kernel.py:141-242) for args.fp8_tokens tokens per expert, 4 experts x 3 linears.
+    Roofline: 2*M*N*K flops per lcq_fp8_gemm launch over its HIP-event time vs fp8 dense peak."""
+    from lightcompress_amd import _native
+    from lightcompress_amd.module_utils import block_wise_fp8_forward_func
+    T = args.fp8_tokens
+    g = torch.Generator(device=dev).manual_seed(5)
+    xs = {}
+    for c, _ in weights:
+        K = c.shape[1]
+        if K not in xs:
+            xs[K] = (torch.randn(T, K, device=dev, generator=g)).to(torch.bfloat16)
+
+    def step(_):
+        for c, s in weights:
+            block_wise_fp8_forward_func(xs[c.shape[1]], c, s, 128, None)
+
+    step(0)
+    torch.cuda.synchronize()
+    timer = _native.KernelTimer()
+    with timer:
+        elapsed = timed_blocks(step, 0, args.steps, 1, dev)
+    kern = timer.summary()
+    flops = sum(2.0 * T * c.shape[0] * c.shape[1] for c, _ in weights)
+    out = {'linears_per_s': round(len(weights) * args.steps / elapsed, 1),
+           'ms_per_step': round(elapsed / args.steps * 1e3, 3),
+           'workload': (f'{len(weights)} DSv3 block-fp8 expert linears (2048x7168 / 7168x2048), '
+                        f'{T} bf16 tokens each: act_quant + fp8 GEMM + bf16'),
+           'lcq_kernels': kernel_table(kern, elapsed)}
+    t = kern.get('lcq_fp8_gemm')
+    if t:
+        tf = flops * args.steps / (t['total_ms'] * 1e-3) / 1e12
+        out['roofline'] = {'kernel': 'lcq_fp8_gemm (k_fp8_gemm)', 'bound': 'mfma',
+                           'achieved': round(tf, 1), 'peak': PEAK_FP8_TFLOPS, 'unit': 'TFLOP/s',
+                           'frac': round(tf / PEAK_FP8_TFLOPS, 4), 'traffic': None,
+                           'flops_per_launch': flops / len(weights),
+                           'avg_launch_ms': round(t['avg_ms'], 4)}
     return out
 
 
