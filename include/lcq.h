@@ -410,6 +410,38 @@ int lcq_act_static_hist_qparams(const void* const* segs, const int64_t* seg_lens
                                 int dtype, const void* minmax, int dst_nbins, float qmax,
                                 void* out, void* workspace, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Projection GEMMs of the calibration / AWQ loss-search forwards (awq.py:110-145, 178-278:
+ * the nn.Linear calls inside inspect_module, and calculate_loss) on bf16/fp16 MFMA
+ * (csrc/gemm256.hip). A [m, k] (row stride lda), weights [rows, k] (row stride ldb, the
+ * nn.Linear layout); k % 64 == 0; strides multiples of 8 elements; fp32 accumulation, each
+ * output rounded once to dtype (bias added in fp32 first).
+ *
+ * lcq_gemm: C_s = A . B_s^T (+ bias_s) for nseg (1..3) weight segments B_s [b_rows[s], k]
+ * written to c[s] [m, b_rows[s]] (row stride ldc[s]) -- q / k / v of one input in one launch.
+ * All segments but the last are multiples of 256 rows; bias may be NULL or hold NULLs.
+ * ------------------------------------------------------------------------------------- */
+int lcq_gemm(const void* a, int dtype, int64_t lda, int64_t m, int64_t k, int nseg,
+             const void* const* b, const int64_t* b_rows, int64_t ldb, const void* const* bias,
+             void* const* c, const int64_t* ldc, void* stream);
+
+/* LlamaMLP's act_fn(gate_proj(x)) * up_proj(x) (SiLU) in one GEMM: h [m, n] =
+ * rnd(rnd(silu(rnd(A . gate^T))) * rnd(A . up^T)); gate / up [n, k]; the two [m, n]
+ * projections are never written. */
+int lcq_gemm_silu_mul(const void* a, int dtype, int64_t lda, int64_t m, int64_t k,
+                      const void* gate, const void* up, int64_t ldb, int64_t n, void* h,
+                      int64_t ldh, void* stream);
+
+/* Awq.calculate_loss fused into the last projection of inspect_module: out = rnd(A . B^T +
+ * bias) is not written; out_f32[slot] = fp32(sum((ref - out)_dtype^2)) / (m * n), fp64 partial
+ * per 256x256 tile summed in tile order (deterministic). ref [m, n] (row stride ldr) = the
+ * original module output. workspace >= lcq_gemm_sq_diff_workspace_bytes(m, n). */
+int64_t lcq_gemm_sq_diff_workspace_bytes(int64_t m, int64_t n);
+int lcq_gemm_sq_diff(const void* a, int dtype, int64_t lda, int64_t m, int64_t k,
+                     const void* b, int64_t ldb, int64_t n, const void* bias, const void* ref,
+                     int64_t ldr, void* workspace, int64_t ws_bytes, void* out_f32, int slot,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

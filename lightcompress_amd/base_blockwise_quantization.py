@@ -86,14 +86,24 @@ class BlockwiseOpt:
         for i in range(len(self.blocks)):
             self.block_idx = i
             if mode == 'shard_blocks' and i % world != rank:
-                # not ours: only advance the float activation chain (quant_out False)
+                # not ours: only advance the float activation chain (quant_out False); the
+                # staged forward's memo of this block (stage outputs: GBs at calibration
+                # sizes) is dropped at once, as block_opt does for owned blocks
                 if not self.data_free:
                     self.input['data'] = self.block_forward(self.blocks[i])
+                    self._clear_block_cache(self.blocks[i])
                 continue
             self.block_opt(self.blocks[i])
         if mode == 'shard_blocks':
             for i, block in enumerate(self.blocks):
                 P.broadcast_block(block, owner=i % world)
+                # the broadcast writes weights through .data (no version bump): no memoised
+                # stage may survive it
+                self._clear_block_cache(block)
+
+    def _clear_block_cache(self, block):
+        if hasattr(self.model, 'clear_block_cache'):
+            self.model.clear_block_cache(block)
 
     def cache_input_hook(self, m, x, y, name, feat_dict):
         # device-resident, shared (no copy): see module docstring
@@ -357,8 +367,7 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         self.block_init(block)
         self.run(block, input_feat, handles)
         del input_feat
-        if hasattr(self.model, 'clear_block_cache'):
-            self.model.clear_block_cache(block)
+        self._clear_block_cache(block)
 
     def register_hooks(self, modules, input_feat):
         if self.data_free:

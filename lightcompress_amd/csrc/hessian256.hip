@@ -429,14 +429,11 @@ extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t 
                   : nullptr;
   a.alpha = alpha; a.beta = beta; a.nt = nt; a.ntiles = ntiles; a.ns = ns; a.kt_per_split = ktps;
   a.nslots = n_slots(nt);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)k_syrk256<false>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF_B);
-    hipFuncSetAttribute((const void*)k_syrk256<true>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF_B);
-    attr_set = true;
-  }
+  // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
+  (void)hipFuncSetAttribute((const void*)k_syrk256<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF_B);
+  (void)hipFuncSetAttribute((const void*)k_syrk256<true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF_B);
   if (x_dtype == LCQ_F16)
     hipLaunchKernelGGL(k_syrk256<true>, dim3((unsigned)(a.nslots * ns)), 512, 2 * BUF_B, st, a);
   else

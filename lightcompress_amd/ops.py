@@ -12,7 +12,8 @@ from . import _native as N
 
 __all__ = ['int_quant_dynamic', 'int_quant_static', 'pack_vllm', 'pack_autoawq_gemm',
            'hessian_accum', 'gptq_block', 'absmean_cols', 'awq_weight_scale', 'awq_scales', 'scale_bcast',
-           'sq_diff_mean', 'auto_clip_search', 'clip_apply']
+           'sq_diff_mean', 'auto_clip_search', 'clip_apply', 'linear', 'linear_multi',
+           'linear_silu_mul', 'linear_sq_diff', 'gemm_supported']
 
 
 def _code_dtype(bit: int, qmin: int) -> torch.dtype:
@@ -346,12 +347,116 @@ class LossBuffer:
         self.out = torch.zeros((slots,), dtype=torch.float32, device=device)
         self.ws = torch.empty((nparts,), dtype=torch.float64, device=device)
         self.nparts = nparts
+        self._gws = None
+
+    def gemm_ws(self, m: int, n: int) -> torch.Tensor:
+        """fp64 tile partials of lcq_gemm_sq_diff (grown on demand, reused across ratios)."""
+        need = (N.load().lcq_gemm_sq_diff_workspace_bytes(m, n) + 7) // 8
+        if self._gws is None or self._gws.numel() < need:
+            self._gws = torch.empty((need,), dtype=torch.float64, device=self.out.device)
+        return self._gws
 
     def record(self, a: torch.Tensor, b: torch.Tensor, slot: int):
         a = a.contiguous()
         b = b.contiguous()
         N.call('lcq_sq_diff_mean', N.ptr(a), N.ptr(b), N.dt(a), a.numel(), N.ptr(self.ws),
                self.nparts, N.ptr(self.out), int(slot), N.stream_of(a))
+
+
+# ---- projection GEMMs (csrc/gemm256.hip; awq.py:110-145 inspect forwards + calculate_loss) ----
+def _rows2d(x: torch.Tensor) -> torch.Tensor:
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    if x2.stride(-1) != 1 or x2.stride(0) % 8 != 0 or x2.data_ptr() % 16 != 0:
+        x2 = x2.contiguous()
+    return x2
+
+
+def gemm_supported(x: torch.Tensor, *weights: torch.Tensor) -> bool:
+    """Shapes / dtypes the lcq GEMMs take (others go to the caller's own path)."""
+    K = x.shape[-1]
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and K % 64 == 0
+            and x.numel() > 0 and all(
+                w.is_cuda and w.dtype == x.dtype and w.dim() == 2 and w.shape[1] == K
+                and w.stride(1) == 1 and w.stride(0) % 8 == 0 and w.data_ptr() % 16 == 0
+                and w.shape[0] % 16 == 0 for w in weights))
+
+
+def _wstride(ws):
+    ld = ws[0].stride(0)
+    if any(w.stride(0) != ld for w in ws):
+        raise ValueError('weights must share a row stride')
+    return ld
+
+
+def linear_multi(x: torch.Tensor, weights, biases=None):
+    """[F.linear(x, w_s, b_s) for each weight] from one GEMM launch (x read once)."""
+    import ctypes
+    x2 = _rows2d(x)
+    M, K = x2.shape
+    n = len(weights)
+    if not 1 <= n <= 3:
+        raise ValueError('1..3 weights')
+    for w in weights[:-1]:
+        if w.shape[0] % 256 != 0:
+            raise ValueError('all but the last weight need a multiple of 256 rows')
+    outs = [torch.empty((M, w.shape[0]), dtype=x.dtype, device=x.device) for w in weights]
+    bs = list(biases) if biases is not None else [None] * n
+    for b, w in zip(bs, weights):
+        if b is not None and (b.dtype != x.dtype or b.numel() != w.shape[0] or not b.is_contiguous()):
+            raise ValueError('bias must be contiguous [N] in the input dtype')
+    arr_b = (ctypes.c_void_p * 3)(*[w.data_ptr() for w in weights])
+    arr_r = (ctypes.c_int64 * 3)(*[w.shape[0] for w in weights])
+    arr_bias = (ctypes.c_void_p * 3)(*[None if b is None else b.data_ptr() for b in bs])
+    arr_c = (ctypes.c_void_p * 3)(*[o.data_ptr() for o in outs])
+    arr_ld = (ctypes.c_int64 * 3)(*[o.shape[1] for o in outs])
+    N.call('lcq_gemm', N.ptr_strided(x2), N.dt(x2), x2.stride(0), M, K, n, arr_b, arr_r,
+           _wstride(weights), arr_bias, arr_c, arr_ld, N.stream_of(x2))
+    N.note_work('lcq_gemm', 2.0 * M * K * sum(w.shape[0] for w in weights))
+    return [o.view(*x.shape[:-1], o.shape[1]) for o in outs]
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
+    """F.linear(x, weight, bias) on the lcq GEMM (fp32 accumulation, one rounding)."""
+    return linear_multi(x, [weight], None if bias is None else [bias])[0]
+
+
+def linear_silu_mul(x: torch.Tensor, gate_w: torch.Tensor, up_w: torch.Tensor) -> torch.Tensor:
+    """act_fn(gate_proj(x)) * up_proj(x) (SiLU, no bias) in one GEMM; the [.., I] projections
+    are never materialised."""
+    x2 = _rows2d(x)
+    M, K = x2.shape
+    I = gate_w.shape[0]
+    if tuple(up_w.shape) != tuple(gate_w.shape):
+        raise ValueError('gate / up weights must match')
+    h = torch.empty((M, I), dtype=x.dtype, device=x.device)
+    N.call('lcq_gemm_silu_mul', N.ptr_strided(x2), N.dt(x2), x2.stride(0), M, K,
+           gate_w.data_ptr(), up_w.data_ptr(), _wstride([gate_w, up_w]), I, N.ptr(h), I,
+           N.stream_of(x2))
+    N.note_work('lcq_gemm_silu_mul', 4.0 * M * K * I)
+    return h.view(*x.shape[:-1], I)
+
+
+def linear_sq_diff(x: torch.Tensor, weight: torch.Tensor, ref: torch.Tensor,
+                   losses: 'LossBuffer', slot: int, bias=None):
+    """losses.out[slot] = mean((ref - F.linear(x, weight, bias))^2) (calculate_loss,
+    awq.py:134-145) without writing the linear's output."""
+    x2 = _rows2d(x)
+    M, K = x2.shape
+    Nn = weight.shape[0]
+    r2 = ref.reshape(-1, Nn)
+    if r2.shape[0] != M or r2.dtype != x.dtype:
+        raise ValueError('ref must be [.., N] matching x rows and dtype')
+    if r2.stride(-1) != 1 or r2.stride(0) % 4 != 0:
+        r2 = r2.contiguous()
+    if bias is not None and (bias.dtype != x.dtype or bias.numel() != Nn):
+        raise ValueError('bias must be [N] in the input dtype')
+    ws = losses.gemm_ws(M, Nn)
+    N.call('lcq_gemm_sq_diff', N.ptr_strided(x2), N.dt(x2), x2.stride(0), M, K,
+           weight.data_ptr(), weight.stride(0), Nn, None if bias is None else N.ptr(bias),
+           N.ptr_strided(r2), r2.stride(0), N.ptr(ws), ws.numel() * 8, N.ptr(losses.out),
+           int(slot), N.stream_of(x2))
+    N.note_work('lcq_gemm_sq_diff', 2.0 * M * K * Nn)
 
 
 def sq_diff_mean(a: torch.Tensor, b: torch.Tensor) -> float:
