@@ -93,15 +93,20 @@ class Awq(BaseBlockwiseQuantization):
             handles.append(m.register_forward_hook(hook))
         return handles
 
-    def _org_output(self, x, inspect_module, kwargs):
+    def _org_cached(self, x, inspect_module):
+        """The capture forward's output of inspect_module on x, if still valid, else None."""
         hit = getattr(self, '_org_cache', {}).pop(id(inspect_module), None)
-        if (getattr(self, 'reuse_org', False) and hit is not None and self._bs == x.shape[0] and hit[1] == _mkey(*hit[2])
-                and tuple(hit[0].shape[:-1]) == tuple(x.shape[:-1])):
+        if (getattr(self, 'reuse_org', False) and hit is not None and self._bs == x.shape[0]
+                and hit[1] == _mkey(*hit[2]) and tuple(hit[0].shape[:-1]) == tuple(x.shape[:-1])):
             self.org_reuse_stats['reused'] += 1
             return hit[0]
         if hasattr(self, 'org_reuse_stats'):
             self.org_reuse_stats['recomputed'] += 1
-        return self.inspect_module_forward(x, inspect_module, kwargs)
+        return None
+
+    def _org_output(self, x, inspect_module, kwargs):
+        hit = self._org_cached(x, inspect_module)
+        return hit if hit is not None else self.inspect_module_forward(x, inspect_module, kwargs)
 
     # -- awq.py:74-108 ----------------------------------------------------------------------
     def get_act_scale(self, x):
@@ -147,6 +152,86 @@ class Awq(BaseBlockwiseQuantization):
                               pre_scale=scales.to(w.dtype), qparams=False, out=out)
         return out
 
+    # -- fused inspect forward + loss (awq.py:110-145 on the lcq GEMM epilogues) ------------
+    @staticmethod
+    def _qbufs(weights):
+        """Buffers for the fake-quantized weights; linears of one input (q/k/v, gate/up) get
+        row ranges of ONE buffer, so a fused GEMM reads them as one weight panel."""
+        w0 = weights[0]
+        if len(weights) > 1 and all(w.dim() == 2 and w.shape[1] == w0.shape[1] and w.dtype ==
+                                    w0.dtype and w.device == w0.device for w in weights):
+            cat = torch.empty((sum(w.shape[0] for w in weights), w0.shape[1]), dtype=w0.dtype,
+                              device=w0.device)
+            return list(torch.split(cat, [w.shape[0] for w in weights], dim=0))
+        return [torch.empty_like(w) for w in weights]
+
+    fused_search = True  # class switch for A/B runs (LCQ_GEMM=0 also disables it)
+
+    def _fused_paths(self, inspect_module, layers, qbufs, orig_w, kwargs, x):
+        """`inspect_module(x/s)` + calculate_loss as lcq GEMM launches whose epilogues do the
+        elementwise tail (SiLU product, squared error against org_out), so the module's
+        output is never written. Returns (org_fn(x) -> org_out with the original weights,
+        loss_factory(org_out, losses) -> fn(xin, slot)), or None for any other module or
+        setting (activation quant, awq_bs batching, padding masks: the module forward runs).
+        Same math as the module forward on the lcq GEMM (fp32 accumulation, one rounding per
+        output), so a reused capture-forward org_out and the ratios' outputs stay comparable."""
+        from .module_utils import _GEMM_ON
+        if not (_GEMM_ON and self.fused_search and getattr(self, 'w_only', True)
+                and self._bs == x.shape[0] and not getattr(self, 'padding_mask', None)):
+            return None
+        mods = list(layers)
+        if isinstance(inspect_module, nn.Linear) and mods == [inspect_module]:
+            b = inspect_module.bias
+            if not (ops.gemm_supported(x, *qbufs, *orig_w) and (b is None or b.dtype == x.dtype)):
+                return None
+            qw = qbufs[0]
+            return (lambda xx: ops.linear(xx, orig_w[0], b),
+                    lambda org, losses: (lambda xin, n: ops.linear_sq_diff(xin, qw, org, losses,
+                                                                           n, bias=b)))
+        name = type(inspect_module).__name__
+        if name == 'LlamaMLP' and getattr(inspect_module.config, 'hidden_act', None) == 'silu':
+            gp, up, dp = inspect_module.gate_proj, inspect_module.up_proj, inspect_module.down_proj
+            if not (mods == [gp, up] and gp.bias is None and up.bias is None
+                    and isinstance(dp, nn.Linear) and ops.gemm_supported(x, *qbufs, *orig_w)
+                    and ops.gemm_supported(x.new_empty((1, dp.weight.shape[1])), dp.weight)
+                    and (dp.bias is None or dp.bias.dtype == x.dtype)
+                    and qbufs[0].stride(0) == qbufs[1].stride(0)
+                    and orig_w[0].stride(0) == orig_w[1].stride(0)):
+                return None
+            wd, bd = dp.weight, dp.bias
+
+            def org_fn(xx):
+                return ops.linear(ops.linear_silu_mul(xx, orig_w[0], orig_w[1]), wd, bd)
+
+            def factory(org, losses):
+                return lambda xin, n: ops.linear_sq_diff(
+                    ops.linear_silu_mul(xin, qbufs[0], qbufs[1]), wd, org, losses, n, bias=bd)
+            return org_fn, factory
+        if name == 'LlamaAttention':
+            from .llama import _attn_core
+            a = inspect_module
+            o = a.o_proj
+            kw = dict(kwargs)
+            pe = kw.pop('position_embeddings', None)
+            am = kw.pop('attention_mask', None)
+            kw = {k: v for k, v in kw.items() if k in ('position_ids', 'cache_position')}
+            if not (mods == [a.q_proj, a.k_proj, a.v_proj] and isinstance(o, nn.Linear)
+                    and pe is not None and ops.gemm_supported(x, *qbufs, *orig_w)
+                    and ops.gemm_supported(x.new_empty((1, o.weight.shape[1])), o.weight)
+                    and (o.bias is None or o.bias.dtype == x.dtype)):
+                return None
+
+            def org_fn(xx):
+                return ops.linear(_attn_core(a, xx, pe, am, qkv_weights=orig_w, **kw),
+                                  o.weight, o.bias)
+
+            def factory(org, losses):
+                return lambda xin, n: ops.linear_sq_diff(
+                    _attn_core(a, xin, pe, am, qkv_weights=qbufs, **kw), o.weight, org, losses,
+                    n, bias=o.bias)
+            return org_fn, factory
+        return None
+
     # -- awq.py:178-278 --------------------------------------------------------------------
     @torch.no_grad()
     def search_scale_subset(self, prev_op, layers_dict, input, inspect_module, is_gqa,
@@ -162,12 +247,17 @@ class Awq(BaseBlockwiseQuantization):
         v1 = getattr(self, 'trans_version', 'v2') == 'v1'
         w_max = self.get_weight_scale(layers_dict) if v1 else None
         orig_w = [fc.weight.data for fc in layers]
-        qbufs = [torch.empty_like(w) for w in orig_w]
+        qbufs = self._qbufs(orig_w)
         x_tmp = torch.empty_like(x)
         x_mean = self.get_act_scale(x)
-        org_out = self._org_output(x, inspect_module, kwargs)
-        all_scales = torch.empty((self.n_grid, x.shape[-1]), dtype=x.dtype, device=x.device)
         losses = ops.LossBuffer(self.n_grid, x.device)
+        paths = self._fused_paths(inspect_module, layers, qbufs, orig_w, kwargs, x)
+        org_out = self._org_cached(x, inspect_module)
+        if org_out is None:  # recompute: through the fused kernels when the ratios use them
+            org_out = (paths[0](x) if paths is not None
+                       else self.inspect_module_forward(x, inspect_module, kwargs))
+        fused = paths[1](org_out, losses) if paths is not None else None
+        all_scales = torch.empty((self.n_grid, x.shape[-1]), dtype=x.dtype, device=x.device)
         try:
             for n in range(self.n_grid):
                 ratio = n * 1 / self.n_grid
@@ -178,8 +268,11 @@ class Awq(BaseBlockwiseQuantization):
                 xin = x_tmp
                 if not self.w_only:
                     xin = self.aquantizer.fake_quant_act_dynamic(x_tmp)
-                out = self.inspect_module_forward(xin, inspect_module, kwargs)
-                losses.record(org_out, out, n)
+                if fused is not None:
+                    fused(xin, n)
+                else:
+                    out = self.inspect_module_forward(xin, inspect_module, kwargs)
+                    losses.record(org_out, out, n)
                 for fc, w in zip(layers, orig_w):
                     fc.weight.data = w
         finally:

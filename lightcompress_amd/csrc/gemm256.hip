@@ -389,7 +389,9 @@ __global__ void __launch_bounds__(512, 1) k_gemm256(Args a) {
       double s = 0.0;
 #pragma unroll
       for (int w = 0; w < 8; ++w) s += red[w];
-      a.part[(int64_t)tm * a.n_nt + tn] = s;
+      double* pp = a.part + ((int64_t)tm * a.n_nt + tn) * 4;  // 4 slots per tile (k_gemm16p)
+      pp[0] = s;
+      pp[1] = pp[2] = pp[3] = 0.0;
     }
   }
 }
@@ -702,7 +704,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm4w(Args a) {
     double* red = reinterpret_cast<double*>(lds);
     if (lane == 0) red[w] = dsum;
     __syncthreads();
-    if (tid == 0) a.part[(int64_t)tm * a.n_nt + tn] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (tid < 4) a.part[((int64_t)tm * a.n_nt + tn) * 4 + tid] = red[tid];
   }
 }
 
@@ -848,75 +850,437 @@ __global__ void __launch_bounds__(256, 1) k_gemm16(Args a) {
   for (int64_t t = 0; t < nk; ++t) ktile16<FP16>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 
-  // epilogue as k_gemm256 (swapped 16x16 layout): acc[m][n][j] = token tm*256 + wr*128 +
-  // m*16 + fr, tile column wc*128 + n*16 + fq*4 + j (EPI_SILU: n < 4 gate, n + 4 up of output
-  // column tn*128 + wc*64 + n*16 + fq*4 + j)
+  // epilogue (swapped 16x16 layout): acc[m][n][j] = token tm*256 + wr*128 + m*16 + fr, tile
+  // column wc*128 + n*16 + fq*4 + j (EPI_SILU: n < 4 gate, n + 4 up of output column
+  // tn*128 + wc*64 + n*16 + fq*4 + j). Segment, bias and row pointers are resolved once per
+  // tile / row (a tile never straddles a segment), loads are batched per row.
   const int fr = lane & 15, fq = lane >> 4;
-  double dsum = 0.0;
+  if constexpr (EPI == EPI_SILU) {
+    const int64_t col0 = (int64_t)tn * 128 + wc * 64 + fq * 4;
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
-    if (trow >= a.m) continue;
-    if constexpr (EPI == EPI_SILU) {
+    for (int m = 0; m < 8; ++m) {
+      const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
+      if (trow >= a.m) break;
+      uint16_t* crow = a.c[0] + trow * a.ldc[0] + col0;
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        const int64_t col = (int64_t)tn * 128 + wc * 64 + n * 16 + fq * 4;
-        if (col >= a.n) continue;
+        if (col0 + n * 16 >= a.n) break;
         float o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float g = rnd<DT>(acc[m][n][j]);
+          const float gg = rnd<DT>(acc[m][n][j]);
           const float u = rnd<DT>(acc[m][n + 4][j]);
-          const float sl = rnd<DT>(g / (1.0f + expf(-g)));
+          const float sl = rnd<DT>(gg / (1.0f + expf(-gg)));
           o[j] = rnd<DT>(sl * u);
         }
         uint2 wv;
         wv.x = pack2<DT>(o[0], o[1]);
         wv.y = pack2<DT>(o[2], o[3]);
-        *reinterpret_cast<uint2*>(a.c[0] + trow * a.ldc[0] + col) = wv;
+        *reinterpret_cast<uint2*>(crow + n * 16) = wv;
       }
-    } else {
+    }
+  } else {
+    const int64_t tcol = (int64_t)tn * ST;
+    int s = 0;
+    int64_t base = 0;
+    if (a.nseg > 1 && tcol >= a.bend[0]) { s = 1; base = a.bend[0]; }
+    if (a.nseg > 2 && tcol >= a.bend[1]) { s = 2; base = a.bend[1]; }
+    const int64_t col0 = tcol + wc * 128 + fq * 4;  // + n * 16
+    const int64_t lcol0 = col0 - base;              // column within segment s
+    const bool full_n = tcol + ST <= a.n;
+    // bias (uniform presence): 4 values per n, read once
+    float bias[8][4];
+    const uint16_t* bp = a.bias[s];
+    if (bp != nullptr) {
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
-        const int64_t col = (int64_t)tn * ST + wc * 128 + n * 16 + fq * 4;
-        if (col >= a.n) continue;
-        int s = 0;
-        int64_t base = 0;
-        if (a.nseg > 1 && col >= a.bend[0]) { s = 1; base = a.bend[0]; }
-        if (a.nseg > 2 && col >= a.bend[1]) { s = 2; base = a.bend[1]; }
-        float o[4];
+        if (full_n || col0 + n * 16 < a.n) {
+          float b4[4];
+          unpack4<DT>(*reinterpret_cast<const uint2*>(bp + lcol0 + n * 16), b4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float v = acc[m][n][j];
-          if (a.bias[s] != nullptr) v = __fadd_rn(v, ld_h<DT>(a.bias[s] + (col - base) + j));
-          o[j] = rnd<DT>(v);
-        }
-        if constexpr (EPI == EPI_STORE) {
-          uint2 wv;
-          wv.x = pack2<DT>(o[0], o[1]);
-          wv.y = pack2<DT>(o[2], o[3]);
-          *reinterpret_cast<uint2*>(a.c[s] + trow * a.ldc[s] + (col - base)) = wv;
+          for (int j = 0; j < 4; ++j) bias[n][j] = b4[j];
         } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) bias[n][j] = 0.f;
+        }
+      }
+    }
+    double dsum = 0.0;
+    // EPI_SQDIFF: the reference rows are loaded one row block ahead (16 loads in flight)
+    uint2 rv[2][8];
+    auto load_ref = [&](int m, uint2 (&dst)[8]) {
+      const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
+      const uint16_t* rrow = a.ref + (trow < a.m ? trow : a.m - 1) * a.ldr + col0;
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        dst[n] = (full_n || col0 + n * 16 < a.n) ? *reinterpret_cast<const uint2*>(rrow + n * 16)
+                                                 : make_uint2(0u, 0u);
+    };
+    if constexpr (EPI == EPI_SQDIFF) load_ref(0, rv[0]);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
+      if constexpr (EPI == EPI_SQDIFF) {
+        if (m + 1 < 8) load_ref(m + 1, rv[(m + 1) & 1]);
+      }
+      if (trow >= a.m) continue;
+      float o[8][4];
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[n][j] = rnd<DT>(bp != nullptr ? __fadd_rn(acc[m][n][j], bias[n][j]) : acc[m][n][j]);
+      if constexpr (EPI == EPI_STORE) {
+        uint16_t* crow = a.c[s] + trow * a.ldc[s] + lcol0;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          if (!full_n && col0 + n * 16 >= a.n) break;
+          uint2 wv;
+          wv.x = pack2<DT>(o[n][0], o[n][1]);
+          wv.y = pack2<DT>(o[n][2], o[n][3]);
+          *reinterpret_cast<uint2*>(crow + n * 16) = wv;
+        }
+      } else {
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          if (!full_n && col0 + n * 16 >= a.n) break;
           float r[4];
-          unpack4<DT>(*reinterpret_cast<const uint2*>(a.ref + trow * a.ldr + col), r);
+          unpack4<DT>(rv[m & 1][n], r);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float d = rnd<DT>(r[j] - o[j]);
+            const float d = rnd<DT>(r[j] - o[n][j]);
             dsum += (double)(d * d);
           }
         }
       }
     }
-  }
-  if constexpr (EPI == EPI_SQDIFF) {
+    if constexpr (EPI == EPI_SQDIFF) {
 #pragma unroll
-    for (int msk = 32; msk >= 1; msk >>= 1) dsum += __shfl_xor(dsum, msk, 64);
-    __syncthreads();
-    double* red = reinterpret_cast<double*>(lds);
-    if (lane == 0) red[w] = dsum;
-    __syncthreads();
-    if (tid == 0) a.part[(int64_t)tm * a.n_nt + tn] = (red[0] + red[1]) + (red[2] + red[3]);
+      for (int msk = 32; msk >= 1; msk >>= 1) dsum += __shfl_xor(dsum, msk, 64);
+      __syncthreads();
+      double* red = reinterpret_cast<double*>(lds);
+      if (lane == 0) red[w] = dsum;
+      __syncthreads();
+      if (tid < 4) a.part[((int64_t)tm * a.n_nt + tn) * 4 + tid] = red[tid];
+    }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Persistent form of k_gemm16 (probe, LCQ_GEMM_KERNEL=p). One workgroup per CU walks the tile
+// slots wgid, wgid + G, ... (consecutive wgids share an XCD: each XCD's workgroups take one
+// 4 x 8 tile block per round). The per-lane load offsets are the same for every tile: a tile
+// only changes the three buffer descriptors (panel base + the bytes of valid rows, so rows
+// past M / N / a segment end read as zeros instead of being clamped). The last two K-tiles
+// of a tile load the NEXT tile's first two, so its prologue runs behind this tile's
+// epilogue and the matrix pipe restarts without a memory wait.
+// ---------------------------------------------------------------------------------------
+struct Desc {
+  __amdgpu_buffer_rsrc_t ra, rb0, rb1;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_n(const void* p, int64_t bytes) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)(bytes > 0x7fffffff ? 0x7fffffff : bytes));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo),
+                                           (short)0, nb, 0x00020000);
+}
+
+template <int EPI>
+__device__ __forceinline__ Desc make_desc(const Args& a, int tm, int tn) {
+  Desc d;
+  const int64_t arow0 = (int64_t)tm * ST;
+  int64_t arows = a.m - arow0;
+  if (arows > ST) arows = ST;
+  d.ra = rsrc_n(a.a + arow0 * a.lda, arows * a.lda * 2);
+  if constexpr (EPI == EPI_SILU) {
+    const int64_t brow0 = (int64_t)tn * 128;
+    int64_t brows = a.n - brow0;
+    if (brows > 128) brows = 128;
+    d.rb0 = rsrc_n(a.b[0] + brow0 * a.ldb, brows * a.ldb * 2);
+    d.rb1 = rsrc_n(a.b[1] + brow0 * a.ldb, brows * a.ldb * 2);
+  } else {
+    const int64_t row0 = (int64_t)tn * ST;
+    int s = 0;
+    int64_t segbase = 0;
+    if (a.nseg > 1 && row0 >= a.bend[0]) { s = 1; segbase = a.bend[0]; }
+    if (a.nseg > 2 && row0 >= a.bend[1]) { s = 2; segbase = a.bend[1]; }
+    int64_t brows = a.bend[s] - row0;
+    if (brows > ST) brows = ST;
+    d.rb0 = d.rb1 = rsrc_n(a.b[s] + (row0 - segbase) * a.ldb, brows * a.ldb * 2);
+  }
+  return d;
+}
+
+// B piece j of wave w -> LDS subtile (row block rb, k half kb) = index rb * 2 + kb. Plain:
+// subtile w + 4j. EPI_SILU: waves 0, 1 stage the 16 gate subtiles (row blocks 0-3, 8-11),
+// waves 2, 3 the 16 up subtiles (4-7, 12-15), so every wave reads ONE B descriptor.
+template <int EPI>
+__device__ __forceinline__ int bsub(int w, int j) {
+  if constexpr (EPI == EPI_SILU) {
+    const int g = (w & 1) * 8 + j;
+    const int rbi = g >> 1;
+    const int rb = (rbi < 4 ? rbi : rbi + 4) + (w >= 2 ? 4 : 0);
+    return rb * 2 + (g & 1);
+  } else {
+    return w + 4 * j;
+  }
+}
+
+// tile-independent per-lane offsets of the 8 A and 8 B pieces (16-row subtiles, st_16x32)
+template <int EPI>
+__device__ __forceinline__ void make_offsets(const Args& a, int w, int lane, uint32_t (&aoff)[8],
+                                             uint32_t (&boff)[8]) {
+  const int r = lane >> 2;
+  const int pc = (lane & 3) * 16;
+  const int lc = pc ^ (((r >> 3) & 1) << 5);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int rb = (w >> 1) + 2 * j;
+    aoff[j] = (uint32_t)((int64_t)(rb * 16 + r) * a.lda * 2 + (w & 1) * 64 + lc);
+    const int sb = bsub<EPI>(w, j);
+    const int row = (sb >> 1) * 16 + r;           // tile-local B row
+    int brow = row;
+    if constexpr (EPI == EPI_SILU) brow = (row >> 7) * 64 + (row & 63);  // row in gate / up
+    boff[j] = (uint32_t)((int64_t)brow * a.ldb * 2 + (sb & 1) * 64 + lc);
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void load_piece_d(const Desc& d, const uint32_t (&aoff)[8],
+                                             const uint32_t (&boff)[8], char* lds, int buf,
+                                             int kofs, int wu, int idx) {
+  char* dA = lds + buf * BUF4;
+  if (idx < 8) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        (EPI == EPI_SILU && wu >= 2) ? d.rb1 : d.rb0,
+        (lds_void_t*)(dA + TILE_B + bsub<EPI>(wu, idx) * 1024), 16, boff[idx], kofs, 0, 0);
+  } else {
+    const int q = idx - 8;                       // 0..7 -> A piece 0,4,1,5,2,6,3,7
+    const int j = (q >> 1) + 4 * (q & 1);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(d.ra, (lds_void_t*)(dA + (wu + 4 * j) * 1024), 16,
+                                             aoff[j], kofs, 0, 0);
+  }
+}
+
+template <bool FP16>
+__device__ __forceinline__ void mfma16z(v4f& acc, v8s bfrag, v8s afrag) {  // C = 0
+  if constexpr (FP16)
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc) : "v"(bfrag), "v"(afrag));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(bfrag), "v"(afrag));
+}
+
+// one K-tile of k_gemm16p (schedule of ktile16); FIRST: kb = 0 MFMAs start from C = 0;
+// LAST: no fragment reads of the next K-tile (the next tile's are read after the epilogue,
+// so no fragment registers stay live across it)
+template <bool FP16, bool FIRST, bool LAST, int EPI>
+__device__ __forceinline__ void ktile16p(v4f (&acc)[8][8], v8s (&bf)[8][2], v8s (&af)[2][2][2],
+                                         const Desc& d, const uint32_t (&aoff)[8],
+                                         const uint32_t (&boff)[8], char* lds, int buf,
+                                         int kofs, int w, int wr, int wc, int lane) {
+  const char* At = lds + buf * BUF4;
+  const char* An = lds + (buf ^ 1) * BUF4;
+  const char* Bn = An + TILE_B;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+    for (int mm = 0; mm < 2; ++mm) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const int i = mm * 16 + n * 2 + kb;
+          if (FIRST && kb == 0) mfma16z<FP16>(acc[2 * mb + mm][n], bf[n][kb], af[mb & 1][mm][kb]);
+          else mfma16a<FP16>(acc[2 * mb + mm][n], bf[n][kb], af[mb & 1][mm][kb]);
+          if (i == 7) {
+            if (mb == 0 || mb == 3) wait_barrier<20>();
+            else wait_barrier<28>();
+          }
+          if (mb == 0 && i >= 8 && i < 28 && (i & 1) == 0)
+            load_piece_d<EPI>(d, aoff, boff, lds, buf, kofs, w, (i - 8) >> 1);
+          if (mb > 0 && (i == 8 || i == 20))
+            load_piece_d<EPI>(d, aoff, boff, lds, buf, kofs, w, 8 + 2 * mb + (i == 20));
+          if (i >= 8 && i < 12) {
+            const int q = i - 8, m2 = q >> 1, k2 = q & 1;
+            if (mb < 3) af[(mb + 1) & 1][m2][k2] = read_frag(At, wr * 8 + 2 * (mb + 1) + m2, k2, lane);
+            else if (!LAST) af[0][m2][k2] = read_frag(An, wr * 8 + m2, k2, lane);
+          }
+          if (!LAST && mb == 3 && mm == 1 && kb == 1) {
+#pragma unroll
+            for (int k3 = 0; k3 < 2; ++k3) bf[n][k3] = read_frag(Bn, wc * 8 + n, k3, lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  }
+}
+
+// K-tile fragments a workgroup starts a tile with: all B fragments, A block 0
+__device__ __forceinline__ void first_frags(v8s (&bf)[8][2], v8s (&af)[2][2][2], const char* lds,
+                                            int buf, int wr, int wc, int lane) {
+  const char* A0 = lds + buf * BUF4;
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) bf[n][k] = read_frag(A0 + TILE_B, wc * 8 + n, k, lane);
+#pragma unroll
+  for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) af[0][m2][k] = read_frag(A0, wr * 8 + m2, k, lane);
+}
+
+__device__ __forceinline__ bool next_tile(const Args& a, int& slot, int stride, int& tm, int& tn) {
+  while (slot < a.nslots) {
+    if (slot_tile(a, slot, tm, tn)) return true;
+    slot += stride;
+  }
+  return false;
+}
+
+template <int DT, int EPI>
+__global__ void __launch_bounds__(256, 1) k_gemm16p(Args a) {
+  constexpr bool FP16 = DT == LCQ_F16;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  int tm, tn;
+  if (!next_tile(a, slot, G, tm, tn)) return;
+  const int64_t nk = a.k / SKT;  // >= 2 (host)
+  uint32_t aoff[8], boff[8];
+  make_offsets<EPI>(a, w, lane, aoff, boff);
+  Desc d = make_desc<EPI>(a, tm, tn);
+
+  v4f acc[8][8];
+  v8s af[2][2][2], bf[8][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_piece_d<EPI>(d, aoff, boff, lds, 0, 0, w, i);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_piece_d<EPI>(d, aoff, boff, lds, 1, SKT * 2, w, i);
+  wait_barrier<22>();
+
+  int buf = 0;  // LDS buffer of the current K-tile (parity of K-tiles run so far)
+  for (;;) {
+    int nslot = slot + G, ntm = 0, ntn = 0;
+    const bool has_next = next_tile(a, nslot, G, ntm, ntn);
+    const Desc dn = has_next ? make_desc<EPI>(a, ntm, ntn) : d;
+    first_frags(bf, af, lds, buf, wr, wc, lane);
+    // K-tile 0 (C = 0), K-tiles 1 .. nk-2, K-tile nk-1 (no next-fragment reads); loads of
+    // step t fetch K-tile t+2 of this tile, or K-tile t+2-nk of the next one
+    ktile16p<FP16, true, false, EPI>(acc, bf, af, nk > 2 ? d : dn, aoff, boff, lds, buf,
+                                (int)((nk > 2 ? 2 : (has_next ? 0 : nk - 1)) * (SKT * 2)), w,
+                                wr, wc, lane);
+    buf ^= 1;
+    for (int64_t t = 1; t < nk - 1; ++t) {
+      const bool nx = t + 2 >= nk;
+      const int64_t kl = !nx ? t + 2 : (has_next ? t + 2 - nk : nk - 1);
+      ktile16p<FP16, false, false, EPI>(acc, bf, af, nx ? dn : d, aoff, boff, lds, buf,
+                                   (int)(kl * (SKT * 2)), w, wr, wc, lane);
+      buf ^= 1;
+    }
+    ktile16p<FP16, false, true, EPI>(acc, bf, af, dn, aoff, boff, lds, buf,
+                                (int)((has_next ? 1 : nk - 1) * (SKT * 2)), w, wr, wc, lane);
+    buf ^= 1;
+    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // last MFMA's D -> epilogue reads
+
+    const int fr = lane & 15, fq = lane >> 4;
+    if constexpr (EPI == EPI_SILU) {
+      const int64_t col0 = (int64_t)tn * 128 + wc * 64 + fq * 4;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
+        if (trow >= a.m) break;
+        uint16_t* crow = a.c[0] + trow * a.ldc[0] + col0;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          if (col0 + n * 16 >= a.n) break;
+          float o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float gg = rnd<DT>(acc[m][n][j]);
+            const float u = rnd<DT>(acc[m][n + 4][j]);
+            const float sl = rnd<DT>(gg / (1.0f + expf(-gg)));
+            o[j] = rnd<DT>(sl * u);
+          }
+          uint2 wv;
+          wv.x = pack2<DT>(o[0], o[1]);
+          wv.y = pack2<DT>(o[2], o[3]);
+          *reinterpret_cast<uint2*>(crow + n * 16) = wv;
+        }
+      }
+    } else {
+      const int64_t tcol = (int64_t)tn * ST;
+      int s = 0;
+      int64_t base = 0;
+      if (a.nseg > 1 && tcol >= a.bend[0]) { s = 1; base = a.bend[0]; }
+      if (a.nseg > 2 && tcol >= a.bend[1]) { s = 2; base = a.bend[1]; }
+      const int64_t col0 = tcol + wc * 128 + fq * 4;
+      const int64_t lcol0 = col0 - base;
+      const bool full_n = tcol + ST <= a.n;
+      const uint16_t* bp = a.bias[s];
+      double dsum = 0.0;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
+        if (trow >= a.m) break;
+        uint2 rv[8];
+        if constexpr (EPI == EPI_SQDIFF) {
+          const uint16_t* rrow = a.ref + trow * a.ldr + col0;
+#pragma unroll
+          for (int n = 0; n < 8; ++n)
+            rv[n] = (full_n || col0 + n * 16 < a.n) ? *reinterpret_cast<const uint2*>(rrow + n * 16)
+                                                    : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          if (!full_n && col0 + n * 16 >= a.n) break;
+          float o[4];
+          if (bp != nullptr) {
+            float b4[4];
+            unpack4<DT>(*reinterpret_cast<const uint2*>(bp + lcol0 + n * 16), b4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = rnd<DT>(__fadd_rn(acc[m][n][j], b4[j]));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = rnd<DT>(acc[m][n][j]);
+          }
+          if constexpr (EPI == EPI_STORE) {
+            uint2 wv;
+            wv.x = pack2<DT>(o[0], o[1]);
+            wv.y = pack2<DT>(o[2], o[3]);
+            *reinterpret_cast<uint2*>(a.c[s] + trow * a.ldc[s] + lcol0 + n * 16) = wv;
+          } else {
+            float r[4];
+            unpack4<DT>(rv[n], r);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float dd = rnd<DT>(r[j] - o[j]);
+              dsum += (double)(dd * dd);
+            }
+          }
+        }
+      }
+      if constexpr (EPI == EPI_SQDIFF) {
+        // per-wave partial straight to memory (the LDS holds the next tile's K-tiles)
+#pragma unroll
+        for (int msk = 32; msk >= 1; msk >>= 1) dsum += __shfl_xor(dsum, msk, 64);
+        if (lane == 0) a.part[((int64_t)tm * a.n_nt + tn) * 4 + w] = dsum;
+      }
+    }
+    if (!has_next) break;
+    slot = nslot;
+    tm = ntm;
+    tn = ntn;
+    d = dn;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // tail re-fetches landed
 }
 
 // one wave: lane l sums partials l, l+64, ... in order, then a fixed xor tree (deterministic)
@@ -940,7 +1304,8 @@ static void plan(Args& a, int64_t tile_n) {
 template <int DT, int EPI>
 static int launch(Args& a, hipStream_t st) {
   // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
-  // default: the 4-wave 16x16x32 kernel; LCQ_GEMM_KERNEL=w4x32 | w8 select the probes
+  // default: the 4-wave 16x16x32 kernel, one tile per workgroup; LCQ_GEMM_KERNEL=p
+  // (persistent) | w4x32 | w8 select the probes
   static const char* sel = getenv("LCQ_GEMM_KERNEL");
   if (sel && sel[0] == 'w' && sel[1] == '8') {
     (void)hipFuncSetAttribute((const void*)k_gemm256<DT, EPI>,
@@ -950,10 +1315,18 @@ static int launch(Args& a, hipStream_t st) {
     (void)hipFuncSetAttribute((const void*)k_gemm4w<DT, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
     hipLaunchKernelGGL((k_gemm4w<DT, EPI>), dim3((unsigned)a.nslots), 256, 2 * BUF4, st, a);
-  } else {
+  } else if (!(sel && sel[0] == 'p') || a.k < 2 * SKT) {  // one tile per workgroup
     (void)hipFuncSetAttribute((const void*)k_gemm16<DT, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
     hipLaunchKernelGGL((k_gemm16<DT, EPI>), dim3((unsigned)a.nslots), 256, 2 * BUF4, st, a);
+  } else {  // LCQ_GEMM_KERNEL=p: persistent probe (SGPR pressure still costs it; see DESIGN)
+    (void)hipFuncSetAttribute((const void*)k_gemm16p<DT, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int grid = a.nslots < ncu ? a.nslots : ncu;  // persistent: one workgroup per CU
+    hipLaunchKernelGGL((k_gemm16p<DT, EPI>), dim3((unsigned)grid), 256, 2 * BUF4, st, a);
   }
   return check_launch("lcq_gemm: k_gemm");
 }
@@ -1037,7 +1410,7 @@ extern "C" int lcq_gemm_silu_mul(const void* a, int dtype, int64_t lda, int64_t 
 
 extern "C" int64_t lcq_gemm_sq_diff_workspace_bytes(int64_t m, int64_t n) {
   if (m <= 0 || n <= 0) return 0;
-  return ((m + ST - 1) / ST) * ((n + ST - 1) / ST) * (int64_t)sizeof(double);
+  return ((m + ST - 1) / ST) * ((n + ST - 1) / ST) * 4 * (int64_t)sizeof(double);
 }
 
 extern "C" int lcq_gemm_sq_diff(const void* a, int dtype, int64_t lda, int64_t m, int64_t k,
@@ -1065,7 +1438,7 @@ extern "C" int lcq_gemm_sq_diff(const void* a, int dtype, int64_t lda, int64_t m
   hipStream_t st = as_stream(stream);
   rc = dispatch<EPI_SQDIFF>(dtype, g, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_loss_reduce, 1, 64, 0, st, g.part, (int64_t)g.n_mt * g.n_nt, m * n,
+  hipLaunchKernelGGL(k_loss_reduce, 1, 64, 0, st, g.part, (int64_t)g.n_mt * g.n_nt * 4, m * n,
                      reinterpret_cast<float*>(out_f32), slot);
   return check_launch("lcq_gemm_sq_diff: reduce");
 }

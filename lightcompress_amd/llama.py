@@ -64,18 +64,42 @@ def _lcq_sdpa(module, query, key, value, attention_mask, dropout=0.0, scaling=No
                       scaling=scaling, is_causal=is_causal, **kwargs)
 
 
-def _fused_mlp_forward(self, x):
-    """LlamaMLP.forward with act_fn(gate) * up on one lcq_silu_mul pass; the projections are
-    still called as modules (hooks fire in the original order: gate, up, down)."""
+def _plain_linears(*mods):
+    """Exact nn.Linear modules without hooks: their math may be fused across modules."""
+    return all(type(m) is nn.Linear and not (m._forward_hooks or m._forward_pre_hooks)
+               for m in mods)
+
+
+def _gate_up_silu(mlp, x):
+    """act_fn(gate_proj(x)) * up_proj(x): one lcq GEMM with the SiLU product in its epilogue
+    when both projections are plain (bias-free) linears the GEMM takes; otherwise the
+    projections run as modules (hooks fire in order) and lcq_silu_mul makes the product."""
     from . import ops
-    g = self.gate_proj(x)
-    u = self.up_proj(x)
+    from .module_utils import _GEMM_ON
+    gp, up = mlp.gate_proj, mlp.up_proj
+    if (_GEMM_ON and getattr(mlp.config, 'hidden_act', None) == 'silu'
+            and _plain_linears(gp, up) and gp.bias is None and up.bias is None
+            and ops.gemm_supported(x, gp.weight, up.weight)
+            and gp.weight.stride(0) == up.weight.stride(0)):
+        return ops.linear_silu_mul(x, gp.weight, up.weight)
+    g = gp(x)
+    u = up(x)
     if g.is_cuda and g.dtype in (torch.bfloat16, torch.float16) and g.shape == u.shape \
-            and u.dtype == g.dtype and g.numel() % 8 == 0:
-        h = ops.silu_mul(g, u)
-    else:
-        h = self.act_fn(g) * u
-    return self.down_proj(h)
+            and u.dtype == g.dtype and g.numel() % 8 == 0 \
+            and getattr(mlp.config, 'hidden_act', None) == 'silu':
+        return ops.silu_mul(g, u)
+    return mlp.act_fn(g) * u
+
+
+def _fused_mlp_forward(self, x):
+    """LlamaMLP.forward with act_fn(gate) * up fused (see _gate_up_silu)."""
+    return self.down_proj(_gate_up_silu(self, x))
+
+
+def _linear_forward(self, x):
+    """nn.Linear.forward on the lcq projection GEMM (module_utils.lcq_linear)."""
+    from .module_utils import lcq_linear
+    return lcq_linear(x, self.weight, self.bias)
 
 
 def _fused_rmsnorm_forward(self, hidden_states):
@@ -126,14 +150,34 @@ def _stage(cache, name, key, mods, fn):
     return val
 
 
-def _attn_core(attn, xn, position_embeddings, attention_mask, **kwargs):
+def qkv_proj(attn, xn, weights=None):
+    """q / k / v projections of LlamaAttention: one lcq GEMM launch for the three when they
+    are plain linears the GEMM takes (x read once), else the three modules. `weights`
+    overrides the three weights (the AWQ search's fake-quantized copies)."""
+    from . import ops
+    from .module_utils import _GEMM_ON
+    mods = (attn.q_proj, attn.k_proj, attn.v_proj)
+    ws = list(weights) if weights is not None else [m.weight for m in mods]
+    if (_GEMM_ON and (weights is not None or _plain_linears(*mods))
+            and ops.gemm_supported(xn, *ws) and len({w.stride(0) for w in ws}) == 1
+            and all(w.shape[0] % 256 == 0 for w in ws[:2])
+            and all(m.bias is None or m.bias.dtype == xn.dtype for m in mods)):
+        return ops.linear_multi(xn, ws, [m.bias for m in mods])
+    if weights is not None:
+        from .module_utils import lcq_linear
+        return [lcq_linear(xn, w, m.bias) for w, m in zip(ws, mods)]
+    return [m(xn) for m in mods]
+
+
+def _attn_core(attn, xn, position_embeddings, attention_mask, qkv_weights=None, **kwargs):
     """LlamaAttention.forward up to (not including) o_proj, exactly as transformers runs it."""
     from transformers.models.llama import modeling_llama as ml
     input_shape = xn.shape[:-1]
     hidden_shape = (*input_shape, -1, attn.head_dim)
-    q = attn.q_proj(xn).view(hidden_shape).transpose(1, 2)
-    k = attn.k_proj(xn).view(hidden_shape).transpose(1, 2)
-    v = attn.v_proj(xn).view(hidden_shape).transpose(1, 2)
+    q, k, v = qkv_proj(attn, xn, qkv_weights)
+    q = q.view(hidden_shape).transpose(1, 2)
+    k = k.view(hidden_shape).transpose(1, 2)
+    v = v.view(hidden_shape).transpose(1, 2)
     cos, sin = position_embeddings
     q, k = ml.apply_rotary_pos_emb(q, k, cos, sin)
     iface = ml.ALL_ATTENTION_FUNCTIONS.get_interface(attn.config._attn_implementation,
@@ -180,14 +224,7 @@ def _staged_decoder_forward(self, hidden_states, attention_mask=None, position_i
     key = key + _mkey(self.post_attention_layernorm, mlp.gate_proj, mlp.up_proj)
 
     def _mlp_in():
-        from . import ops
-        hn = self.post_attention_layernorm(h)
-        g = mlp.gate_proj(hn)
-        u = mlp.up_proj(hn)
-        if g.is_cuda and g.dtype in (torch.bfloat16, torch.float16) and g.shape == u.shape \
-                and getattr(mlp.config, 'hidden_act', None) == 'silu' and g.numel() % 8 == 0:
-            return ops.silu_mul(g, u)
-        return mlp.act_fn(g) * u
+        return _gate_up_silu(mlp, self.post_attention_layernorm(h))
 
     m = _stage(cache, 'm', key, (self.post_attention_layernorm, mlp.gate_proj, mlp.up_proj),
                _mlp_in)
@@ -219,7 +256,9 @@ def install_fused_forward(model: nn.Module):
         _STOCK_DECODER_FORWARD = ml.LlamaDecoderLayer.forward
     staged = os.environ.get('LCQ_STAGED_FORWARD', '1') != '0'
     for m in model.modules():
-        if isinstance(m, ml.LlamaMLP) and getattr(m.config, 'hidden_act', None) == 'silu':
+        if type(m) is nn.Linear:
+            m.forward = types.MethodType(_linear_forward, m)
+        elif isinstance(m, ml.LlamaMLP) and getattr(m.config, 'hidden_act', None) == 'silu':
             m.forward = types.MethodType(_fused_mlp_forward, m)
         elif isinstance(m, ml.LlamaRMSNorm):
             m.forward = types.MethodType(_fused_rmsnorm_forward, m)

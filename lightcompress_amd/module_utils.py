@@ -12,7 +12,23 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import os
+
 from . import ops
+
+# F.linear of the calibration forwards on the lcq projection GEMM (csrc/gemm256.hip);
+# LCQ_GEMM=0 hands every linear back to torch (hipBLASLt) for A/B runs
+_GEMM_ON = os.environ.get('LCQ_GEMM', '1') != '0'
+
+
+def lcq_linear(x, weight, bias=None):
+    """F.linear(x, weight, bias) on the lcq GEMM when the operands fit it (bf16 / fp16 on the
+    device, K % 64 == 0, out_features % 16 == 0, bias in the input dtype); other operands
+    (fp32 GPTQ weights, odd shapes) take torch's F.linear."""
+    if (_GEMM_ON and ops.gemm_supported(x, weight)
+            and (bias is None or (bias.dtype == x.dtype and bias.is_contiguous()))):
+        return ops.linear(x, weight, bias)
+    return F.linear(x, weight, bias)
 
 
 def _fname(fn):
@@ -65,7 +81,7 @@ class LlmcFp8Linear(nn.Module):
             from .kernel import weight_cast_to_bf16
             self.weight.data = weight_cast_to_bf16(self.weight.data, self.weight_scale_inv.data,
                                                    self.block_size).to(torch.bfloat16)
-        return F.linear(x, self.weight, self.bias)
+        return lcq_linear(x, self.weight, self.bias)
 
     @classmethod
     @torch.no_grad()
@@ -110,7 +126,7 @@ class FakeQuantLinear(nn.Module):
             self.tmp_bias = self.bias
         elif self.dynamic_quant_tmp_weight:
             self.tmp_weight = self.w_qdq(self)
-        return F.linear(x, self.tmp_weight, self.tmp_bias)
+        return lcq_linear(x, self.tmp_weight, self.tmp_bias)
 
     @classmethod
     @torch.no_grad()
@@ -147,7 +163,7 @@ class EffcientFakeQuantLinear(nn.Module):
     def forward(self, x):
         if self.a_qdq is not None:
             x = self.a_qdq(x, self)
-        return F.linear(x, self.weight, self.bias)
+        return lcq_linear(x, self.weight, self.bias)
 
     @classmethod
     @torch.no_grad()
@@ -177,7 +193,7 @@ class OriginFloatLinear(nn.Module):
 
     @torch.no_grad()
     def forward(self, x):
-        return F.linear(x, self.weight, self.bias)
+        return lcq_linear(x, self.weight, self.bias)
 
     @classmethod
     @torch.no_grad()
