@@ -1,28 +1,34 @@
 """Benchmark: LightCompress per-layer weight-quantization hot path on MI355X.
 
-Workload (BASELINE.json configs[1]): Llama-3-8B AWQ w4a16 g128 (symmetric, weight_clip,
+Headline (BASELINE.json configs[1]): Llama-3-8B AWQ w4a16 g128 (symmetric, weight_clip,
 trans_version v2 -- configs/quantization/methods/Awq/awq_w_only.yml) with 128 calibration
 samples x 512 tokens, deployed to vLLM packed int4 (need_pack). One step = one Llama-3-8B
-decoder block through the reference's block_opt (calibration forward with input capture, AWQ
-scale search on the qkv / gate-up / down subsets -- o_proj is skipped under GQA exactly as the
-reference does -- scale application, auto-clip of v/o/gate/up/down) plus the real-quant + vLLM
-pack of its 7 linears. Random-init weights and synthetic activations of the real shapes
-(no network: no checkpoints / datasets).
+decoder block through the reference's run_block_loop / block_opt (calibration forward with
+input capture, AWQ scale search on the qkv / gate-up / down subsets -- o_proj is skipped under
+GQA exactly as the reference does -- scale application, auto-clip of v/o/gate/up/down) plus
+the real-quant + vLLM pack of its 7 linears. Random-init weights and synthetic activations of
+the real shapes (no network: no checkpoints / datasets).
 
 metric: linear layers quantized per second (whole job, all ranks). Multi-GPU: one process per
-GPU (torchrun); with quant_out=False AWQ blocks are independent given the float activations
-(SURVEY.md §8e), so every rank quantizes its own blocks -- weak scaling, no data-path collective.
+GPU (torchrun); quant_out=False makes AWQ blocks independent given the float activations
+(SURVEY.md §8e), so the timed run is the algorithm's own run_block_loop in shard_blocks mode
+over steps x N blocks: every rank quantizes its blocks, runs the float forward of the others
+(the activation chain) and receives their quantized weights by broadcast -- weak scaling.
 
-GPTQ leg (BASELINE.json configs[2], reported under "gptq"): Llama-3-8B GPTQ w4a16 g128 asym,
-act-order, true_sequential, quant_out (configs/quantization/methods/GPTQ/gptq_w_only.yml),
-128 x 2048 calibration tokens at bs 1 (128 inputs per block, as the reference's Catcher
-stores them); one step = one block through block_opt (Hessians, column loops, fake-quant
-forward of the next block's input). Its roofline is the XᵀX Hessian kernel.
-
-Also reported: the roofline of the dominant kernel (the bf16 projection GEMMs of the AWQ loss
-search, timed live with device events around every linear launch), live timings of every lcq
-HIP kernel family, and a CPU baseline (the oracle = reference algorithm restated on torch-CPU,
-timed on a bounded sample of the same step on the host cores and extrapolated).
+Also in the line:
+* "gptq" (configs[2]): Llama-3-8B GPTQ w4a16 g128 asym, act-order, true_sequential, quant_out,
+  128 x 2048 tokens (bs 1); per-block time; at N > 1 the calibration samples are sharded
+  (shard_tokens: partial Hessians summed, row-sharded column loop); roofline = the XᵀX kernel.
+* "e2e": MEASURED end-to-end wall-clock of the whole 32-block Llama-3-8B (AWQ and GPTQ):
+  run_block_loop + deploy (vllm_quant / fake_quant) -- the reference's llmc_duration_time.
+* "fp8" (configs[4]): DeepSeek-V3 expert linears, block-fp8 -> per-tensor e4m3 deploy, and the
+  block-scaled fp8 GEMM of their calibration forward.
+* roofline: the dominant kernel of the headline step (k_gemm16: the projection GEMMs of the
+  AWQ loss search with their fused epilogues), flops and algorithmic bytes of every launch
+  over its device-event time; traffic = PMC HBM bytes per launch from profiles/.
+* cpu_baseline: the oracle (the reference algorithm restated on torch-CPU, pinned to the
+  reference by tests/golden) on the host cores over a bounded sample, extrapolated; AWQ (the
+  headline) and GPTQ.
 """
 from __future__ import annotations
 
@@ -48,6 +54,7 @@ LLAMA3_8B = dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=
                  max_position_embeddings=8192, rms_norm_eps=1e-5, num_hidden_layers=32,
                  vocab_size=128256)
 N_LINEARS_PER_BLOCK = 7
+GEMM_FAMILY = ('lcq_gemm', 'lcq_gemm_silu_mul', 'lcq_gemm_sq_diff')
 
 
 def parse():
@@ -58,22 +65,24 @@ def parse():
     ap.add_argument('--n-samples', type=int, default=128)
     ap.add_argument('--seq-len', type=int, default=512)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-e2e', action='store_true')
+    ap.add_argument('--e2e-blocks', type=int, default=32)
     ap.add_argument('--algo', choices=['awq', 'gptq', 'fp8', 'both', 'all'], default='all')
     ap.add_argument('--fp8-experts', type=int, default=32)
     ap.add_argument('--fp8-tokens', type=int, default=2048,
                     help='calibration tokens routed to each expert in the fp8 forward leg')
-    ap.add_argument('--gptq-steps', type=int, default=2)
+    ap.add_argument('--gptq-steps', type=int, default=3)
     ap.add_argument('--gptq-samples', type=int, default=128)
     ap.add_argument('--gptq-seq-len', type=int, default=2048)
     ap.add_argument('--cpu-budget-s', type=float, default=20.0)
     return ap.parse_args()
 
 
-def awq_config(seq_len):
+def awq_config(seq_len, n_samples=128):
     from lightcompress_amd.utils import load_config
     return load_config({
         'base': {'seed': 42},
-        'calib': {'name': 'pileval', 'n_samples': 128, 'bs': -1, 'seq_len': seq_len,
+        'calib': {'name': 'pileval', 'n_samples': n_samples, 'bs': -1, 'seq_len': seq_len,
                   'preproc': 'pileval_awq'},
         'quant': {'method': 'Awq',
                   'weight': {'bit': 4, 'symmetric': True, 'granularity': 'per_group',
@@ -101,58 +110,11 @@ def gptq_config(seq_len, n_samples):
 
 def synthetic_hidden(n, seq, hidden, device, seed):
     """Calibration hidden states with log-normal per-channel magnitudes (outlier channels,
-    SURVEY.md §8d), bf16."""
+    SURVEY.md §8d), bf16. The same seed on every rank: one global calibration set."""
     g = torch.Generator(device=device).manual_seed(seed)
     mag = torch.exp(torch.randn(hidden, generator=g, device=device))
     x = torch.randn(n, seq, hidden, generator=g, device=device) * mag
     return x.to(torch.bfloat16)
-
-
-class GemmMeter:
-    """Device events around every nn.Linear forward (one hipBLASLt GEMM each: no bias)."""
-
-    def __init__(self, blocks):
-        self.records = []
-        self.handles = []
-        self.active = False
-        for b in blocks:
-            for m in b.modules():
-                if isinstance(m, torch.nn.Linear):
-                    self.handles.append(m.register_forward_pre_hook(self._pre))
-                    self.handles.append(m.register_forward_hook(self._post))
-
-    def _pre(self, m, inp):
-        if self.active:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record()
-            m._lcq_ev = e
-
-    def _post(self, m, inp, out):
-        if self.active and hasattr(m, '_lcq_ev'):
-            e = torch.cuda.Event(enable_timing=True)
-            e.record()
-            x = inp[0]
-            rows = x.numel() // x.shape[-1]
-            flops = 2.0 * rows * m.in_features * m.out_features
-            nbytes = 2.0 * (rows * m.in_features + m.in_features * m.out_features
-                            + rows * m.out_features)  # bf16 x, W, y once each
-            self.records.append((m._lcq_ev, e, flops, nbytes))
-            del m._lcq_ev
-
-    def summary(self):
-        torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for a, b, _, _ in self.records]
-        fl = [f for _, _, f, _ in self.records]
-        by = [b for _, _, _, b in self.records]
-        if not ms:
-            return None
-        return {'launches': len(ms), 'avg_ms': sum(ms) / len(ms), 'total_ms': sum(ms),
-                'flops_per_launch': sum(fl) / len(fl), 'bytes_per_launch': sum(by) / len(by),
-                'tflops': sum(fl) / (sum(ms) * 1e-3) / 1e12}
-
-    def close(self):
-        for h in self.handles:
-            h.remove()
 
 
 def pmc_traffic(leg, kernel):
@@ -170,19 +132,57 @@ def pmc_traffic(leg, kernel):
     return sum(k['hbm_bytes'] for k in ks), str(files[-1].relative_to(ROOT))
 
 
-def deploy_block(algo, model, block, idx):
-    from lightcompress_amd.module_utils import VllmRealQuantLinear
-    model.replace_module_block(VllmRealQuantLinear, block, idx,
-                               algo.get_replacement_params('vllm_quant', algo.w_only))
+def sync_barrier(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
 
 
-def cpu_baseline(args, budget_s):
-    """Oracle (the reference algorithm restated on torch-CPU, pinned to the reference's
-    outputs by tests/golden) timed on a bounded sample of one AWQ block step on the host
-    cores, then extrapolated linearly to the full step. The sample is sized by wall time
-    (~budget_s): as many calibration samples x (org + one ratio) per subset as fit in ~60% of
-    the budget, auto-clip on as many 64-row chunks of gate_proj as fit in the next ~25%, and
-    the real-quant + vLLM pack of one gate_proj."""
+def max_over_ranks(v, world, dev):
+    if world > 1:
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        v = t.item()
+    return v
+
+
+def kernel_table(kern, elapsed):
+    return {k: {'launches': v['launches'], 'avg_ms': round(v['avg_ms'], 4),
+                'share_of_step': round(v['total_ms'] / (elapsed * 1e3), 4)}
+            for k, v in sorted(kern.items(), key=lambda kv: -kv[1]['total_ms'])}
+
+
+def gemm_roofline(kern, elapsed):
+    """The projection-GEMM family (all k_gemm16 launches: lcq_gemm / _silu_mul / _sq_diff):
+    algorithmic flops and bytes of every launch (noted by ops.py) over the device-event time
+    of those launches."""
+    fam = [kern[n] for n in GEMM_FAMILY if n in kern]
+    if not fam:
+        return None
+    ms = sum(f['total_ms'] for f in fam)
+    n = sum(f['launches'] for f in fam)
+    fl = sum(f.get('flops', 0.0) for f in fam)
+    by = sum(f.get('bytes', 0.0) for f in fam)
+    tf = fl / (ms * 1e-3) / 1e12
+    traffic, src = pmc_traffic('awq', 'k_gemm16')
+    return {'kernel': 'k_gemm16 (csrc/gemm256.hip): bf16 MFMA projection GEMMs of the AWQ loss '
+                      'search + calibration forwards, epilogues fused (q/k/v, SiLU*up, loss)',
+            'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
+            'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4), 'traffic': traffic,
+            'traffic_source': src, 'algorithmic_bytes_per_launch': by / n,
+            'flops_per_launch': fl / n, 'avg_launch_ms': round(ms / n, 4), 'launches': n,
+            'share_of_step': round(ms / (elapsed * 1e3), 3)}
+
+
+# ---------------------------------------------------------------------------------------
+# CPU baselines (oracle = the reference algorithm on torch-CPU; bounded samples, extrapolated)
+# ---------------------------------------------------------------------------------------
+def cpu_baseline_awq(args, budget_s):
+    """One AWQ block step on the host cores: as many calibration samples x (org + one ratio)
+    per subset as fit in ~60% of the budget, auto-clip on as many 64-row chunks of gate_proj
+    as fit in the next ~25%, the real-quant + vLLM pack of one gate_proj; extrapolated
+    linearly to the full step."""
     from transformers import LlamaConfig
     from transformers.models.llama import modeling_llama as ml
     from oracle import awq_ref as A
@@ -243,8 +243,6 @@ def cpu_baseline(args, budget_s):
             per_sample = (sum(org_t[name]) / len(org_t[name])
                           + 20 * sum(ratio_t[name]) / len(ratio_t[name]))
             parts[f'search_{name}'] = per_sample * args.n_samples  # linear in tokens
-        # auto-clip of gate_proj rows in 64-row chunks on the 512 sampled tokens, extrapolated
-        # by OC*IC to every clipped linear (v, o, gate, up, down)
         xs = xm.reshape(-1, cfg.hidden_size)[: seq]
         t_clip, rows = 0.0, 0
         while rows < cfg.intermediate_size:
@@ -258,7 +256,6 @@ def cpu_baseline(args, budget_s):
         clipped = (cfg.num_key_value_heads * cfg.head_dim * cfg.hidden_size
                    + cfg.hidden_size ** 2 + 3 * cfg.intermediate_size * cfg.hidden_size)
         parts['auto_clip'] = t_clip * clipped / (rows * cfg.hidden_size)
-        # deploy: real quant + vLLM pack of one gate_proj, extrapolated to the 7 linears
         t0 = time.perf_counter()
         codes, sc, _ = Q.real_quant_dynamic(layer.mlp.gate_proj.weight.data, 4, True)
         Q.pack_vllm(codes, 4)
@@ -279,33 +276,206 @@ def cpu_baseline(args, budget_s):
             'parts_s': {k: round(v, 1) for k, v in parts.items()}}
 
 
-def timed_blocks(step, warmup, steps, world, dev):
-    """Run `warmup` untimed then `steps` timed steps; barrier + sync on both sides; max over
-    ranks. Returns elapsed seconds."""
-    for i in range(warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+def cpu_baseline_gptq(args, budget_s):
+    """One GPTQ block step on the host cores, the reference's own work per block: 11 Hessians
+    (7 in block_init + 4 recomputed by true_sequential, gptq.py / base_blockwise_quantization
+    .py:498-526) over 128 x 2048 tokens, the Cholesky chain per linear and the column loop of
+    each linear. Sampled: the 4096-wide Hessian over as many 2048-token samples as fit in
+    ~45% of the budget, one Cholesky chain at IC 4096, the column loop of a row slice of a
+    4096^2 linear; extrapolated by IC^2 (Hessian), IC^3 (Cholesky), OC*IC^2 (column loop)."""
+    from oracle import gptq_ref as Gr
+    threads = torch.get_num_threads()
+    H, I = 4096, 14336
+    seq, ns = args.gptq_seq_len, args.gptq_samples
+    t_start = time.perf_counter()
+    samples, t_h = [], 0.0
+    while True:
+        x = synthetic_hidden(1, seq, H, 'cpu', 100 + len(samples))
+        samples.append(x)
+        t0 = time.perf_counter()
+        Hm, _ = Gr.hessian(samples[-1:], H)
+        t_h += time.perf_counter() - t0
+        if time.perf_counter() - t_start > 0.45 * budget_s or len(samples) >= ns:
+            break
+    per_sample_4096 = t_h / len(samples)
+    hess_units = 9 + 2 * (I / H) ** 2          # 9 Hessians at IC 4096, 2 at IC 14336
+    t_hess = per_sample_4096 * ns * hess_units
+    g = torch.Generator().manual_seed(1)
+    W = (torch.randn(H, H, generator=g) * 0.02)
+    Hm = Hm + torch.eye(H)
     t0 = time.perf_counter()
-    for i in range(warmup, warmup + steps):
+    Wp, U, perm = Gr.prepare(W.clone(), Hm.clone(), True, 0.01)
+    t_chol = time.perf_counter() - t0
+    rows = 64
+    t0 = time.perf_counter()
+    while True:
+        Gr.column_loop(Wp[:rows].clone(), U, 4, False, 128)
+        if time.perf_counter() - t_start > 0.9 * budget_s or rows >= H:
+            break
+        rows *= 2
+    t_col_rows = time.perf_counter() - t0
+    # the last call covered `rows` rows (the doublings before it cost as much again)
+    per_row_4096 = t_col_rows / (2 * rows - 64)
+    oc_ic2 = (H * H * H * 2 + 2 * 1024 * H * H + 2 * I * H * H + H * I * I) / (H * H)  # rows x (IC/4096)^2
+    t_col = per_row_4096 * oc_ic2
+    t_chol_all = t_chol * (6 + (I / H) ** 3)   # 6 linears at IC 4096 (q,k,v,o,gate,up), down
+    t_total = t_hess + t_chol_all + t_col
+    wall = time.perf_counter() - t_start
+    return {'value': N_LINEARS_PER_BLOCK / t_total, 'unit': 'linears/s', 'cores': threads,
+            'kind': 'port',
+            'sample': (f'oracle (gptq_ref: gptq.py restated on torch-CPU, pinned by tests/golden) '
+                       f'on Llama-3-8B block shapes: Hessian of {len(samples)} of {ns} 2048-token '
+                       f'samples at IC 4096, one Cholesky chain at IC 4096, column loop of '
+                       f'{rows} rows x 4096; {wall:.1f} s measured, extrapolated to '
+                       f'{t_total:.0f} s per block (11 Hessians, 7 chains, 7 column loops)'),
+            'est_s_per_block': round(t_total, 1),
+            'parts_s': {'hessian': round(t_hess, 1), 'cholesky': round(t_chol_all, 1),
+                        'column_loop': round(t_col, 1)}}
+
+
+# ---------------------------------------------------------------------------------------
+# legs
+# ---------------------------------------------------------------------------------------
+def bench_awq(args, rank, world, dev):
+    """Headline: AWQ block steps through the algorithm's run_block_loop (shard_blocks at N > 1)
+    + the vLLM real-quant deploy of this rank's blocks."""
+    from transformers import LlamaConfig
+    from lightcompress_amd import _native
+    from lightcompress_amd.llama import Llama
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.module_utils import VllmRealQuantLinear
+    cfg = LlamaConfig(**LLAMA3_8B)
+    config = awq_config(args.seq_len, args.n_samples)
+    # warmup on blocks of its own model (no collectives: every rank warms its kernels)
+    if args.warmup:
+        wm = Llama.random(cfg, num_layers=args.warmup, device=dev, seed=999)
+        wx = synthetic_hidden(args.n_samples, args.seq_len, cfg.hidden_size, dev, 5)
+        walgo = build_algo(wm, config, {'data': [wx], 'kwargs': [wm.rotary_kwargs(args.seq_len)]})
+        for i, b in enumerate(wm.get_blocks()):
+            walgo.block_idx = i
+            walgo.block_opt(b)
+            wm.replace_module_block(VllmRealQuantLinear, b, i,
+                                    walgo.get_replacement_params('vllm_quant', walgo.w_only))
+        del walgo, wm, wx
+        torch.cuda.empty_cache()
+    nblk = args.steps * world
+    model = Llama.random(cfg, num_layers=nblk, device=dev, seed=1000)   # same on every rank
+    hidden = synthetic_hidden(args.n_samples, args.seq_len, cfg.hidden_size, dev, 17)
+    algo = build_algo(model, config, {'data': [hidden], 'kwargs': [model.rotary_kwargs(args.seq_len)]})
+    blocks = model.get_blocks()
+    mine = [i for i in range(nblk) if world == 1 or i % world == rank]
+    timer = _native.KernelTimer()
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    with timer:
+        algo.run_block_loop()
+        for i in mine:  # deploy: real-quant + vLLM pack of this rank's blocks
+            model.replace_module_block(VllmRealQuantLinear, blocks[i], i,
+                                       algo.get_replacement_params('vllm_quant', algo.w_only))
+    sync_barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    kern = timer.summary()
+    mode = algo.parallel_mode()
+    del algo, model, hidden
+    torch.cuda.empty_cache()
+    return elapsed, kern, mode
+
+
+def bench_gptq(args, rank, world, dev):
+    """GPTQ leg: per-block wall-clock (block_opt; token-sharded at N > 1) and the Hessian
+    kernel's roofline."""
+    from transformers import LlamaConfig
+    from lightcompress_amd import _native
+    from lightcompress_amd.llama import Llama
+    from lightcompress_amd.pipeline import build_algo
+    cfg = LlamaConfig(**LLAMA3_8B)
+    warm, steps = 1, args.gptq_steps
+    model = Llama.random(cfg, num_layers=warm + steps, device=dev, seed=2000)
+    seq = args.gptq_seq_len
+    hidden = synthetic_hidden(args.gptq_samples, seq, cfg.hidden_size, dev, 31)
+    kw = model.rotary_kwargs(seq)
+    calib = {'data': [hidden[i:i + 1] for i in range(args.gptq_samples)],
+             'kwargs': [kw] * args.gptq_samples}
+    algo = build_algo(model, gptq_config(seq, args.gptq_samples), calib)
+    blocks = model.get_blocks()
+
+    def step(i):
+        algo.block_idx = i
+        algo.block_opt(blocks[i])
+
+    for i in range(warm):
         step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    return elapsed
+    timer = _native.KernelTimer()
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    with timer:
+        for i in range(warm, warm + steps):
+            step(i)
+    sync_barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    kern = timer.summary()
+    ms = elapsed / steps * 1e3
+    out = {'linears_per_s': round(N_LINEARS_PER_BLOCK * steps / elapsed, 3),
+           'parallelism': ('single GPU' if world == 1 else
+                           f'{world} ranks, {algo.parallel_mode()} (calibration samples sharded, '
+                           'partial Hessians summed, row-sharded column loop)'),
+           'ms_per_block': round(ms, 1), 'steps': steps, 'warmup': warm,
+           'workload': (f'Llama-3-8B GPTQ w4a16 g128 asym act-order true_sequential quant_out, '
+                        f'{args.gptq_samples}x{seq} calib tokens (bs 1)'),
+           'lcq_kernels': kernel_table(kern, elapsed)}
+    h = kern.get('lcq_hessian_accum')
+    if h:
+        # algorithmic: symmetric rank-n update n*ic*(ic+1) flops per launch (SURVEY.md §8d)
+        tf = h['flops'] / (h['total_ms'] * 1e-3) / 1e12
+        traffic, src = pmc_traffic('gptq', 'k_syrk256')
+        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_xt_pack + k_syrk256, bf16 MFMA XᵀX)',
+                           'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
+                           'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4),
+                           'traffic': traffic, 'traffic_source': src,
+                           'avg_launch_ms': round(h['avg_ms'], 4),
+                           'flops_per_launch': h['flops'] / h['launches']}
+    del algo, model, hidden, calib
+    torch.cuda.empty_cache()
+    return out
 
 
-def kernel_table(kern, elapsed):
-    return {k: {'launches': v['launches'], 'avg_ms': round(v['avg_ms'], 4),
-                'share_of_step': round(v['total_ms'] / (elapsed * 1e3), 4)}
-            for k, v in sorted(kern.items(), key=lambda kv: -kv[1]['total_ms'])}
+def bench_e2e(args, rank, world, dev, which):
+    """Whole-model wall-clock (MEASURED, not extrapolated): a random-init 32-block Llama-3-8B
+    through build_algo -> run_block_loop -> deploy, the span the reference times as
+    llmc_duration_time (llmc/__main__.py:182, 265-267) minus model loading / dataset / eval."""
+    from transformers import LlamaConfig
+    from lightcompress_amd.llama import Llama
+    from lightcompress_amd.pipeline import build_algo
+    cfg = LlamaConfig(**LLAMA3_8B)
+    nb = args.e2e_blocks
+    model = Llama.random(cfg, num_layers=nb, device=dev, seed=3000 if which == 'awq' else 4000)
+    if which == 'awq':
+        hidden = synthetic_hidden(args.n_samples, args.seq_len, cfg.hidden_size, dev, 41)
+        calib = {'data': [hidden], 'kwargs': [model.rotary_kwargs(args.seq_len)]}
+        config, fmt = awq_config(args.seq_len, args.n_samples), 'vllm_quant'
+    else:
+        seq = args.gptq_seq_len
+        hidden = synthetic_hidden(args.gptq_samples, seq, cfg.hidden_size, dev, 43)
+        kw = model.rotary_kwargs(seq)
+        calib = {'data': [hidden[i:i + 1] for i in range(args.gptq_samples)],
+                 'kwargs': [kw] * args.gptq_samples}
+        config, fmt = gptq_config(seq, args.gptq_samples), 'fake_quant'
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    algo = build_algo(model, config, calib)
+    algo.run_block_loop()
+    t_loop = time.perf_counter() - t0
+    algo.deploy(fmt)
+    sync_barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    t_loop = max_over_ranks(t_loop, world, dev)
+    mode = algo.parallel_mode()
+    del algo, model, hidden, calib
+    torch.cuda.empty_cache()
+    return {'wall_s': round(elapsed, 2), 'block_loop_s': round(t_loop, 2),
+            'blocks': nb, 'linears': N_LINEARS_PER_BLOCK * nb,
+            'linears_per_s': round(N_LINEARS_PER_BLOCK * nb / elapsed, 3),
+            'deploy': fmt, 'parallel_mode': mode}
 
 
 DSV3_EXPERT = dict(hidden=7168, moe_inter=2048, block=128)
@@ -333,24 +503,27 @@ def bench_fp8(args, rank, world, dev):
             weights.append((r['codes'], r['scales']))
         del w
     q = FloatQuantizer('e4m3', True, 'per_tensor', use_qtorch=True)
-
     codes_l = [c for c, _ in weights]
     sinv_l = [s for _, s in weights]
 
-    def step(_):  # one MoE layer slice: all its expert linears in one batched launch pair
+    def step():  # one MoE layer slice: all its expert linears in one batched launch pair
         q.real_quant_weights_from_block_fp8(codes_l, sinv_l, 128)
 
+    step()
     timer = _native.KernelTimer()
-    step(0)
-    torch.cuda.synchronize()
-    steps = args.steps
+    sync_barrier(world)
+    t0 = time.perf_counter()
     with timer:
-        elapsed = timed_blocks(step, 0, steps, world, dev)
+        for _ in range(args.steps):
+            step()
+    sync_barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     kern = timer.summary()
-    units = 3 * E * steps * world
+    units = 3 * E * args.steps * world
     elems = sum(c.numel() for c, _ in weights)
-    out = {'linears_per_s': round(units / elapsed, 1), 'ms_per_step': round(elapsed / steps * 1e3, 3),
-           'steps': steps, 'warmup': 1,
+    out = {'linears_per_s': round(units / elapsed, 1),
+           'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'steps': args.steps,
+           'warmup': 1,
            'workload': (f'DeepSeek-V3 MoE expert linears (gate/up 2048x7168, down 7168x2048), '
                         f'block-fp8 source -> bf16 -> FP8 e4m3 per-tensor real quant; '
                         f'{E} experts x 3 linears per rank per step'),
@@ -358,7 +531,6 @@ def bench_fp8(args, rank, world, dev):
     t = kern.get('lcq_fp8_block_to_tensor_many')
     if t:
         # algorithmic bytes per expert linear: 1 B fp8 read + 1 B fp8 written per element
-        # (+ fp32 block scales); the amax pass re-reads the 1 B codes (counted as overhead)
         gbs = elems * 2.0 * t['launches'] / (t['total_ms'] * 1e-3) / 1e9
         traffic, src = pmc_traffic('fp8', ('k_bmax16_many', 'k_requant16_many'))
         out['roofline'] = {'kernel': 'lcq_fp8_block_to_tensor_many (k_bmax16_many + '
@@ -366,16 +538,18 @@ def bench_fp8(args, rank, world, dev):
                            'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                            'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic,
                            'traffic_source': src, 'avg_launch_ms': round(t['avg_ms'], 4)}
-    out['calib_forward'] = bench_fp8_forward(args, weights[:12], dev)
+    n_fwd = min(4, E) * 3
+    out['calib_forward'] = bench_fp8_forward(args, weights[:n_fwd], dev, world)
     del weights
     torch.cuda.empty_cache()
     return out
 
 
-def bench_fp8_forward(args, weights, dev):
+def bench_fp8_forward(args, weights, dev, world):
     """Calibration forward of block-fp8 expert linears (LlmcFp8Linear.forward =
     block_wise_fp8_forward_func, module_utils.py:41-46, 244-262): act_quant + the block-scaled
-    fp8 GEMM (kernel.py:141-242) for args.fp8_tokens tokens per expert, 4 experts x 3 linears.
+    fp8 GEMM (kernel.py:141-242) for args.fp8_tokens tokens per expert linear. Every rank runs
+    its own experts (weak scaling); linears_per_s is the job total over ranks.
     Roofline: 2*M*N*K flops per lcq_fp8_gemm launch over its HIP-event time vs fp8 dense peak."""
     from lightcompress_amd import _native
     from lightcompress_amd.module_utils import block_wise_fp8_forward_func
@@ -387,21 +561,25 @@ def bench_fp8_forward(args, weights, dev):
         if K not in xs:
             xs[K] = (torch.randn(T, K, device=dev, generator=g)).to(torch.bfloat16)
 
-    def step(_):
+    def step():
         for c, s in weights:
             block_wise_fp8_forward_func(xs[c.shape[1]], c, s, 128, None)
 
-    step(0)
-    torch.cuda.synchronize()
+    step()
     timer = _native.KernelTimer()
+    sync_barrier(world)
+    t0 = time.perf_counter()
     with timer:
-        elapsed = timed_blocks(step, 0, args.steps, 1, dev)
+        for _ in range(args.steps):
+            step()
+    sync_barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     kern = timer.summary()
     flops = sum(2.0 * T * c.shape[0] * c.shape[1] for c, _ in weights)
-    out = {'linears_per_s': round(len(weights) * args.steps / elapsed, 1),
+    out = {'linears_per_s': round(len(weights) * args.steps * world / elapsed, 1),
            'ms_per_step': round(elapsed / args.steps * 1e3, 3),
-           'workload': (f'{len(weights)} DSv3 block-fp8 expert linears (2048x7168 / 7168x2048), '
-                        f'{T} bf16 tokens each: act_quant + fp8 GEMM + bf16'),
+           'workload': (f'{len(weights) // 3} DSv3 block-fp8 experts x 3 linears (2048x7168 / '
+                        f'7168x2048) per rank, {T} bf16 tokens each: act_quant + fp8 GEMM + bf16'),
            'lcq_kernels': kernel_table(kern, elapsed)}
     t = kern.get('lcq_fp8_gemm')
     if t:
@@ -411,64 +589,6 @@ def bench_fp8_forward(args, weights, dev):
                            'frac': round(tf / PEAK_FP8_TFLOPS, 4), 'traffic': None,
                            'flops_per_launch': flops / len(weights),
                            'avg_launch_ms': round(t['avg_ms'], 4)}
-    return out
-
-
-def bench_gptq(args, rank, world, dev):
-    """GPTQ leg: per-block wall-clock and the Hessian kernel's roofline."""
-    from transformers import LlamaConfig
-    from lightcompress_amd import _native
-    from lightcompress_amd.llama import Llama
-    from lightcompress_amd.pipeline import build_algo
-    cfg = LlamaConfig(**LLAMA3_8B)
-    warm, steps = 1, args.gptq_steps
-    model = Llama.random(cfg, num_layers=warm + steps, device=dev, seed=2000 + rank)
-    seq = args.gptq_seq_len
-    hidden = synthetic_hidden(args.gptq_samples, seq, cfg.hidden_size, dev, 31 + rank)
-    kw = model.rotary_kwargs(seq)
-    calib = {'data': [hidden[i:i + 1] for i in range(args.gptq_samples)],
-             'kwargs': [kw] * args.gptq_samples}
-    algo = build_algo(model, gptq_config(seq, args.gptq_samples), calib)
-    blocks = model.get_blocks()
-
-    def step(i):
-        algo.block_idx = i
-        algo.block_opt(blocks[i])
-
-    timer = _native.KernelTimer()
-    for i in range(warm):
-        step(i)
-    torch.cuda.synchronize()
-    with timer:
-        elapsed = timed_blocks(lambda i: step(i + warm), 0, steps, world, dev)
-    kern = timer.summary()
-    ms = elapsed / steps * 1e3
-    # N > 1 runs the reference's data-parallel replica scheme (quant_out makes blocks
-    # sequential, SURVEY.md §8e): every rank holds its own 128 x 2048 calibration tokens, the
-    # Hessians are all-reduced and the column loop is row-sharded, so the job quantizes the
-    # SAME 7 linears per block whatever N is (no x world in the linear count)
-    out = {'linears_per_s': round(N_LINEARS_PER_BLOCK * steps / elapsed, 3),
-           'parallelism': ('single GPU' if world == 1 else
-                           f'{world} replicas (Hessian all-reduce, row-sharded column loop)'),
-           'ms_per_block': round(ms, 1), 'steps': steps, 'warmup': warm,
-           'extrapolated_model_wall_s': round(ms * 32 / 1e3, 2),
-           'workload': (f'Llama-3-8B GPTQ w4a16 g128 asym act-order true_sequential quant_out, '
-                        f'{args.gptq_samples}x{seq} calib tokens (bs 1)'),
-           'lcq_kernels': kernel_table(kern, elapsed)}
-    h = kern.get('lcq_hessian_accum')
-    if h:
-        # algorithmic: symmetric rank-n update n*ic*(ic+1) flops per launch (SURVEY.md §8d);
-        # KernelTimer records the flops each launch was given
-        tf = h['flops'] / (h['total_ms'] * 1e-3) / 1e12
-        traffic, src = pmc_traffic('gptq', 'k_syrk256')
-        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_xt_pack + k_syrk256, bf16 MFMA XᵀX)',
-                           'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
-                           'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4),
-                           'traffic': traffic, 'traffic_source': src,
-                           'avg_launch_ms': round(h['avg_ms'], 4),
-                           'flops_per_launch': h['flops'] / h['launches']}
-    del algo, model, hidden, calib
-    torch.cuda.empty_cache()
     return out
 
 
@@ -491,12 +611,9 @@ def main():
             dist.init_process_group('nccl', device_id=dev)
         else:
             dist.init_process_group(backend)
-    from transformers import LlamaConfig
     from lightcompress_amd import _native
-    from lightcompress_amd.llama import Llama
-    from lightcompress_amd.pipeline import build_algo
-
     _native.load()
+
     fp8 = bench_fp8(args, rank, world, dev) if args.algo in ('fp8', 'all') else None
     if args.algo == 'fp8':
         if rank == 0:
@@ -515,67 +632,24 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    cfg = LlamaConfig(**LLAMA3_8B)
-    nblk = args.warmup + args.steps
-    model = Llama.random(cfg, num_layers=nblk, device=dev, seed=1000 + rank)
-    hidden = synthetic_hidden(args.n_samples, args.seq_len, cfg.hidden_size, dev, 17 + rank)
-    calib = {'data': [hidden], 'kwargs': [model.rotary_kwargs(args.seq_len)]}
-    config = awq_config(args.seq_len)
-    algo = build_algo(model, config, calib)
-    blocks = model.get_blocks()
 
-    def step(i):
-        algo.block_idx = i
-        algo.block_opt(blocks[i])
-        deploy_block(algo, model, blocks[i], i)
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    meter = GemmMeter([blocks[i] for i in range(args.warmup, nblk)])
-    meter.active = True
-    timer = _native.KernelTimer()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with timer:
-        for i in range(args.warmup, nblk):
-            step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    meter.active = False
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    gemm = meter.summary()
-    kern = timer.summary()
-    meter.close()
+    elapsed, kern, mode = bench_awq(args, rank, world, dev)
     linears = N_LINEARS_PER_BLOCK * args.steps * world
     value = linears / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
+    e2e = None
+    if not args.no_e2e and args.algo == 'all':
+        e2e = {'awq': bench_e2e(args, rank, world, dev, 'awq'),
+               'gptq': bench_e2e(args, rank, world, dev, 'gptq')}
+
     if rank == 0:
-        roofline = None
-        if gemm:
-            traffic, src = pmc_traffic('awq', 'hipblaslt_gemm')
-            roofline = {'kernel': 'bf16 projection GEMM of the AWQ loss search (q/k/v/o/gate/up/'
-                                  'down, hipBLASLt via the HF module forward)',
-                        'bound': 'mfma', 'achieved': round(gemm['tflops'], 1),
-                        'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
-                        'frac': round(gemm['tflops'] / PEAK_BF16_TFLOPS, 4),
-                        'traffic': traffic, 'traffic_source': src,
-                        'algorithmic_bytes_per_launch': gemm['bytes_per_launch'],
-                        'avg_launch_ms': round(gemm['avg_ms'], 4),
-                        'flops_per_launch': gemm['flops_per_launch'],
-                        'share_of_step': round(gemm['total_ms'] / (elapsed * 1e3), 3)}
-        kernels = kernel_table(kern, elapsed)
+        roofline = gemm_roofline(kern, elapsed)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-            cpu = cpu_baseline(args, args.cpu_budget_s)
+            cpu = cpu_baseline_awq(args, args.cpu_budget_s)
+            if gptq is not None:
+                gptq['cpu_baseline'] = cpu_baseline_gptq(args, args.cpu_budget_s * 0.75)
         line = {
             'metric': 'linear-layers quantized/sec (Llama-3-8B AWQ w4a16 g128)',
             'value': round(value, 3), 'unit': 'linears/s', 'n_gpus': world,
@@ -584,15 +658,17 @@ def main():
             'data': 'synthetic (random-init Llama-3-8B blocks, log-normal-channel activations)',
             'config': {'workload': 'Llama-3-8B AWQ w4a16 g128 sym, weight_clip, v2, '
                                    f'{args.n_samples}x{args.seq_len} calib tokens, vLLM int4 '
-                                   'pack; 1 step = 1 decoder block (7 linears)',
+                                   'pack; 1 step = 1 decoder block (7 linears) per GPU',
                        'model': 'Llama-3-8B (4096/14336, 32q/8kv heads)',
-                       'global_batch': args.n_samples * world, 'seq_len': args.seq_len,
-                       'parallelism': f'blocks sharded over {world} GPU(s), no collective'},
-            'extrapolated_model_wall_s': round(ms_per_step * 32 / 1e3, 2),
+                       'global_batch': args.n_samples, 'seq_len': args.seq_len,
+                       'parallelism': (f'run_block_loop {mode}: {args.steps} blocks per GPU '
+                                       f'x {world} GPU(s); non-owner float forwards + '
+                                       'owner broadcasts included')},
+            'e2e': e2e,
             'gptq': gptq,
             'fp8': fp8,
             'roofline': roofline,
-            'lcq_kernels': kernels,
+            'lcq_kernels': kernel_table(kern, elapsed),
             'cpu_baseline': cpu,
         }
         print(json.dumps(line))

@@ -172,6 +172,7 @@ class KernelTimer:
     def __init__(self):
         self.events = {}
         self.work = {}
+        self.bytes = {}
 
     def __enter__(self):
         global _timer
@@ -191,6 +192,8 @@ class KernelTimer:
             out[name] = {'launches': len(ms), 'total_ms': sum(ms), 'avg_ms': sum(ms) / len(ms)}
             if name in self.work:
                 out[name]['flops'] = self.work[name]
+            if name in self.bytes:
+                out[name]['bytes'] = self.bytes[name]
         return out
 
 
@@ -201,6 +204,13 @@ def note_work(name: str, units: float):
     """Attribute algorithmic work (flops or bytes) to the last `name` launch while timing."""
     if _timer is not None:
         _timer.work[name] = _timer.work.get(name, 0.0) + float(units)
+
+
+def note_bytes(name: str, nbytes: float):
+    """Attribute algorithmic HBM bytes (operands read once, outputs written once) to the
+    last `name` launch while timing."""
+    if _timer is not None:
+        _timer.bytes[name] = _timer.bytes.get(name, 0.0) + float(nbytes)
 
 
 def call(name: str, *args):

@@ -30,6 +30,7 @@ class AutoClipper:
         self.weight_clips = {}
         self.w_only = w_only
         self.reduce_across_ranks = False  # set by the algorithm in replicate (DP) mode
+        self.shard_rows = False           # shard_search: each rank searches its row range
         if clip_version != 'v1':
             raise NotImplementedError('clip_version v2 (learnable) is not on the device path')
         if not w_only:
@@ -46,6 +47,19 @@ class AutoClipper:
                 continue
             feats = input_feat[n]
             inputs = [torch.cat(feats)] if len(feats) != 1 else feats
+            _, ws, _ = world()
+            if self.shard_rows and ws > 1 and dist.is_initialized():
+                # rows are independent (auto_clip.py:72-76 batches them): search this rank's
+                # share, gather the bounds (bit-identical to one GPU)
+                from .parallel import dist_world, gather_rows, row_shard
+                rank, wsz = dist_world()
+                r0, r1 = row_shard(m.weight.shape[0], rank, wsz)
+                mx, mn = self.auto_clip_layer(block_idx, n, m.weight.data[r0:r1], inputs,
+                                              n_sample_token=n_sample_token)
+                max_val = gather_rows(mx.contiguous(), m.weight.shape[0])
+                min_val = gather_rows(mn.contiguous(), m.weight.shape[0])
+                self.apply_clip(block_idx, m, min_val, max_val, n)
+                continue
             max_val, min_val = self.auto_clip_layer(block_idx, n, m.weight, inputs,
                                                     n_sample_token=n_sample_token)
             _, ws, _ = world()

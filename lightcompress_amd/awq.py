@@ -23,6 +23,11 @@ from .registry import ALGO_REGISTRY
 
 @ALGO_REGISTRY
 class Awq(BaseBlockwiseQuantization):
+    # quant_out at world > 1 (every backend AWQ config): every rank holds the block's
+    # calibration tokens and evaluates its share of the ratio grid and of the clip rows; the
+    # losses and clip bounds are gathered (bit-identical to one GPU)
+    sequential_parallel_mode = 'shard_search'
+
     def __init__(self, model, quant_config, input, padding_mask, config):
         super().__init__(model, quant_config, input, padding_mask, config)
         special = self.quant_config.get('special', {}) or {}
@@ -258,8 +263,14 @@ class Awq(BaseBlockwiseQuantization):
                        else self.inspect_module_forward(x, inspect_module, kwargs))
         fused = paths[1](org_out, losses) if paths is not None else None
         all_scales = torch.empty((self.n_grid, x.shape[-1]), dtype=x.dtype, device=x.device)
+        mine = range(self.n_grid)
+        shard = self.parallel_mode() == 'shard_search'
+        if shard:  # this rank's ratios; the others' loss slots stay 0 for the sum below
+            from .parallel import dist_world
+            rank, world = dist_world()
+            mine = range(rank, self.n_grid, world)
         try:
-            for n in range(self.n_grid):
+            for n in mine:
                 ratio = n * 1 / self.n_grid
                 s = self.get_scales(prev_op, x_mean, ratio, out=all_scales[n], w_max=w_max)
                 for fc, buf in zip(layers, qbufs):
@@ -278,12 +289,18 @@ class Awq(BaseBlockwiseQuantization):
         finally:
             for fc, w in zip(layers, orig_w):
                 fc.weight.data = w
+        if shard:  # gather the grid: each slot has exactly one non-zero contributor (exact)
+            import torch.distributed as dist
+            dist.all_reduce(losses.out, op=dist.ReduceOp.SUM)
         loss_list = losses.out.tolist()  # the one host sync of the search
         best_i, best = -1, float('inf')
         for n, lo in enumerate(loss_list):
             if lo < best:  # strict: the first minimum wins, as the reference's is_best
                 best, best_i = lo, n
         self.last_search = {'losses': loss_list, 'best_index': best_i}
+        if shard and best_i % world != rank:  # the winner's scales, rebuilt locally (same op)
+            self.get_scales(prev_op, x_mean, best_i * 1 / self.n_grid, out=all_scales[best_i],
+                            w_max=w_max)
         best_scales = all_scales[best_i].clone()
         if self.parallel_mode() == 'replicate':
             from .parallel import awq_pick_best
@@ -297,6 +314,7 @@ class Awq(BaseBlockwiseQuantization):
         if self.weight_clip:
             n_tok = self.config.get('calib', {}).get('seq_len', None)
             self.auto_clipper.reduce_across_ranks = self.parallel_mode() == 'replicate'
+            self.auto_clipper.shard_rows = self.parallel_mode() == 'shard_search'
             self.auto_clipper.run(block, self.block_idx, input_feat, n_sample_token=n_tok)
 
     @torch.no_grad()

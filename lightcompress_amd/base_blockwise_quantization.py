@@ -63,22 +63,55 @@ class BlockwiseOpt:
         calib = (config or {}).get('calib', {}) or {}
         self.batch_calib = bool(calib.get('batch_forward', True))
         self._batch_ok = None
+        if self.input and self.parallel_mode() == 'shard_tokens':
+            self._shard_input_tokens()
+
+    # how ranks split a block whose input depends on the previous block's quantization
+    # (quant_out True): 'shard_search' (AWQ: the ratio grid and the clip rows),
+    # 'shard_tokens' (GPTQ: calibration samples, partial Hessians summed), or 'replicate'
+    # (the reference's data-parallel replicas with averaged statistics)
+    sequential_parallel_mode = 'replicate'
 
     def parallel_mode(self) -> str:
-        """'single' | 'shard_blocks' | 'replicate' (reference DP semantics).
+        """'single' | 'shard_blocks' | 'shard_search' | 'shard_tokens' | 'replicate'.
 
         Blocks can be sharded when each block's input does not depend on the quantization of
-        the previous one (quant_out False); otherwise ranks run the reference's
-        data-parallel replica scheme (statistics reconciled by collectives)."""
+        the previous one (quant_out False); otherwise the work inside a block
+        is sharded (sequential_parallel_mode) or ranks run the reference's data-parallel
+        replica scheme (special.parallel: replicate). The sharded modes reproduce the
+        single-GPU result (bit for bit, or to GPTQ's Hessian summation order)."""
         _, world = P.dist_world()
         if world == 1:
             return 'single'
         mode = (self.quant_config.get('special', {}) or {}).get('parallel', None)
         if mode:
             return mode
-        if not self.data_free and not self.quant_config.get('quant_out', False):
+        if self.data_free:
+            return 'replicate'
+        if not self.quant_config.get('quant_out', False):
             return 'shard_blocks'
-        return 'replicate'
+        return self.sequential_parallel_mode
+
+    def _shard_input_tokens(self):
+        """shard_tokens: keep this rank's contiguous share of the calibration samples (the
+        reference's per-rank slicing, base_dataset.py:169-184, of ONE global set), entries
+        and their batch-dim kwargs sliced alike."""
+        rank, world = P.dist_world()
+        data, kws = self.input['data'], self.input['kwargs']
+        total = sum(d.shape[0] for d in data)
+        s, e = P.row_shard(total, rank, world)
+        new_d, new_k, off = [], [], 0
+        for d, kw in zip(data, kws):
+            b = d.shape[0]
+            lo, hi = max(s, off), min(e, off + b)
+            if hi > lo:
+                new_d.append(d[lo - off:hi - off])
+                new_k.append({k: (v[lo - off:hi - off] if torch.is_tensor(v) and v.dim() > 0
+                                  and v.shape[0] == b and b > 1 else v) for k, v in kw.items()})
+            off += b
+        self.input['data'], self.input['kwargs'] = new_d, new_k
+        self.n_samples_global = total
+        self.n_samples = e - s
 
     def run_block_loop(self):
         mode = self.parallel_mode()
@@ -437,6 +470,9 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         """base_blockwise_quantization.py:567-588: per-tensor static activation qparams from
         the calibration inputs (HBM-resident, not copied), averaged over ranks in the
         reference's replica mode, registered as buf_act_{scales,zeros,qmin,qmax}_{i}."""
+        if self.parallel_mode() == 'shard_tokens':
+            raise NotImplementedError('static activation calibration with token-sharded '
+                                      'calibration data: set special.parallel: replicate')
         entries = self._reference_entries(act_tensors)
         scales_l, zeros_l, qmin_l, qmax_l = self.aquantizer.get_batch_tensors_qparams(entries)
         _, ws, _ = world()

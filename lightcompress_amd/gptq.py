@@ -24,6 +24,10 @@ _LINEAR_TYPES = tuple(_LLMC_LINEAR_TYPES_ + _TRANSFORMERS_LINEAR_TYPES_)
 
 @ALGO_REGISTRY
 class GPTQ(BaseBlockwiseQuantization):
+    # quant_out at world > 1: each rank forwards its share of the samples, the partial
+    # Hessians are summed once per distinct input, the column loop is row-sharded
+    sequential_parallel_mode = 'shard_tokens'
+
     def __init__(self, model, quant_config, input, padding_mask, config, modality='language'):
         super().__init__(model, quant_config, input, padding_mask, config)
         self.model_dtype = next(self.model.model.parameters()).dtype
@@ -167,7 +171,15 @@ class GPTQ(BaseBlockwiseQuantization):
             cache = acc.prepared_by = {}
         if nout not in cache:
             H = acc.H.clone()
-            if replicate:
+            if replicate and self.parallel_mode() == 'shard_tokens':
+                # token shards: H = sum_r n_r H_r / N (each H_r the running average over the
+                # rank's n_r samples) -- the single-GPU Hessian up to fp32 summation order
+                n = torch.tensor([float(acc.nsamples)], dtype=torch.float64, device=H.device)
+                H *= float(acc.nsamples)
+                dist.all_reduce(H, op=dist.ReduceOp.SUM)
+                dist.all_reduce(n, op=dist.ReduceOp.SUM)
+                H /= float(n.item())
+            elif replicate:
                 # one all-reduce of the finished Hessian per distinct input (the reference
                 # reduces after every sample); averaging matches its H /= world_size
                 dist.all_reduce(H, op=dist.ReduceOp.SUM)
@@ -181,7 +193,8 @@ class GPTQ(BaseBlockwiseQuantization):
         """layer_transform of several linears sharing one Hessian, as one column loop."""
         acc = self.layers_cache[grp[0][0]]['acc']
         _, ws, _ = world()
-        replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
+        replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() in (
+            'replicate', 'shard_tokens')
         nout = self._n_out(grp[0][0])
         prepared = self._prepared(acc, replicate, ws, nout)
         W = torch.cat([layer.weight.data for _, layer in grp], 0)
@@ -217,7 +230,8 @@ class GPTQ(BaseBlockwiseQuantization):
     def layer_transform(self, layer, name):
         acc = self.layers_cache[name]['acc']  # shared by the linears fed the same input
         _, ws, _ = world()
-        replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate'
+        replicate = ws > 1 and dist.is_initialized() and self.parallel_mode() in (
+            'replicate', 'shard_tokens')
         nout = self._n_out(name)
         prepared = self._prepared(acc, replicate, ws, nout)
         fixed = None

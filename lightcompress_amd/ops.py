@@ -412,7 +412,9 @@ def linear_multi(x: torch.Tensor, weights, biases=None):
     arr_ld = (ctypes.c_int64 * 3)(*[o.shape[1] for o in outs])
     N.call('lcq_gemm', N.ptr_strided(x2), N.dt(x2), x2.stride(0), M, K, n, arr_b, arr_r,
            _wstride(weights), arr_bias, arr_c, arr_ld, N.stream_of(x2))
-    N.note_work('lcq_gemm', 2.0 * M * K * sum(w.shape[0] for w in weights))
+    Ntot = sum(w.shape[0] for w in weights)
+    N.note_work('lcq_gemm', 2.0 * M * K * Ntot)
+    N.note_bytes('lcq_gemm', 2.0 * (M * K + Ntot * K + M * Ntot))
     return [o.view(*x.shape[:-1], o.shape[1]) for o in outs]
 
 
@@ -434,6 +436,7 @@ def linear_silu_mul(x: torch.Tensor, gate_w: torch.Tensor, up_w: torch.Tensor) -
            gate_w.data_ptr(), up_w.data_ptr(), _wstride([gate_w, up_w]), I, N.ptr(h), I,
            N.stream_of(x2))
     N.note_work('lcq_gemm_silu_mul', 4.0 * M * K * I)
+    N.note_bytes('lcq_gemm_silu_mul', 2.0 * (M * K + 2 * I * K + M * I))
     return h.view(*x.shape[:-1], I)
 
 
@@ -457,6 +460,7 @@ def linear_sq_diff(x: torch.Tensor, weight: torch.Tensor, ref: torch.Tensor,
            N.ptr_strided(r2), r2.stride(0), N.ptr(ws), ws.numel() * 8, N.ptr(losses.out),
            int(slot), N.stream_of(x2))
     N.note_work('lcq_gemm_sq_diff', 2.0 * M * K * Nn)
+    N.note_bytes('lcq_gemm_sq_diff', 2.0 * (M * K + Nn * K + M * Nn))
 
 
 def sq_diff_mean(a: torch.Tensor, b: torch.Tensor) -> float:
