@@ -3,13 +3,13 @@
 # line + rocprofv3 kernel-trace stats per leg. Stage B: PMC HBM traffic (separate FETCH_SIZE /
 # WRITE_SIZE passes per leg, MI355X_MICROARCH.md HBM section), summarised per launch.
 set -o pipefail
-TAG=${TAG:-r1s3}
+TAG=${TAG:-r2}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 stage=${1:-A}
 if [ "$stage" = A ]; then
-  timeout -k 10 400 python3 -u bench.py > $OUT/bench_default.log 2>&1 || exit 1
+  timeout -k 10 600 python3 -u bench.py > $OUT/bench_default.log 2>&1 || exit 1
   for leg in awq gptq fp8; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$leg -o run \
       -- python3 bench.py --algo $leg --no-cpu-baseline > $OUT/kt_$leg.log 2>&1 || exit 1
@@ -21,5 +21,8 @@ else
         -- python3 bench.py --algo $leg --no-cpu-baseline --steps 1 --warmup 0 --gptq-steps 1 \
         > $OUT/pmc_${leg}_$c.log 2>&1 || exit 1
     done
+    python3 scripts/pmc_summary.py $OUT/pmc_${leg}_FETCH_SIZE/run_counter_collection.csv \
+      $OUT/pmc_${leg}_WRITE_SIZE/run_counter_collection.csv $OUT/pmc_traffic_$leg.json \
+      > $OUT/pmc_traffic_$leg.txt 2>&1 || exit 1
   done
 fi
