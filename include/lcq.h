@@ -236,13 +236,15 @@ int lcq_scale_bcast(const void* x, int dtype, int64_t rows, int64_t cols, const 
 int lcq_sq_diff_mean(const void* a, const void* b, int dtype, int64_t n, void* workspace,
                      int nparts, void* out_f32, int slot, void* stream);
 
-/* AutoClipper.auto_clip_layer, clip v1 (auto_clip.py:83-191) for bf16 weights:
- * w [oc, ic], x [T, ic] (already token-subsampled), group 128, nsteps shrink steps with
- * factors[nsteps] = fp32(1 - i/n_grid) (device array). best_max / best_min [oc, ic/128] bf16.
- * Exact emulation of the reference's bf16 products and sums (VALU, not MFMA). */
-int lcq_auto_clip_search(const void* w, const void* x, int64_t oc, int64_t ic, int64_t T,
-                         int group, int nsteps, const void* factors, int qmin, int qmax,
-                         int sym, int clip_sym, void* best_max, void* best_min, void* stream);
+/* AutoClipper.auto_clip_layer, clip v1 (auto_clip.py:83-191) for bf16 / fp16 weights:
+ * w [oc, ic], x [T, ic] (already token-subsampled), group 32 / 64 / 128 / 256, nsteps shrink
+ * steps with factors[nsteps] = fp32(1 - i/n_grid) (device array). best_max / best_min
+ * [oc, ic/group] in dtype. Exact emulation of the reference's dtype products and sums (VALU,
+ * not MFMA). */
+int lcq_auto_clip_search(const void* w, const void* x, int dtype, int64_t oc, int64_t ic,
+                         int64_t T, int group, int nsteps, const void* factors, int qmin,
+                         int qmax, int sym, int clip_sym, void* best_max, void* best_min,
+                         void* stream);
 
 /* AutoClipper.apply_clip, v1 (auto_clip.py:193-212): out = clamp(x, cmin, cmax) per group;
  * cmin NULL -> -cmax. In place allowed. */

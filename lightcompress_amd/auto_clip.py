@@ -88,8 +88,10 @@ class AutoClipper:
         group = wq.group_size if wq.granularity == 'per_group' else w.shape[1]
         if len(inputs) != 1:
             raise NotImplementedError('auto-clip over several calibration tensors')
-        if w.dtype != torch.bfloat16:
-            raise NotImplementedError('device auto-clip kernel is bf16')
+        if w.dtype not in (torch.bfloat16, torch.float16):
+            raise NotImplementedError('device auto-clip kernel takes bf16 / fp16 weights')
+        if group not in (32, 64, 128, 256):
+            raise NotImplementedError(f'device auto-clip kernel: group size {group}')
         x = self.sample_tokens(inputs[0], n_sample_token)
         qmin, qmax = int(wq.qmin.item()), int(wq.qmax.item())
         return ops.auto_clip_search(w.data, x, group, int(max_shrink * n_grid), n_grid, qmin,

@@ -138,11 +138,42 @@ class BlockwiseOpt:
         if hasattr(self.model, 'clear_block_cache'):
             self.model.clear_block_cache(block)
 
+    # (entries, tokens per entry) while block_forward runs several calibration entries as one
+    # stacked batch, else None
+    _batch_ctx = None
+
+    def entry_view(self, m, inp):
+        """A linear input captured during a stacked forward, as the reference's per-entry
+        forwards would have seen it. 3-D inputs carry the entries in their batch dim already.
+        A 2-D input (OPT's MLP, routed MoE experts) counts as ONE sample per forward in the
+        reference (cache_input_hook / add_batch unsqueeze it), so here it is split back:
+        a dense one (every token of every entry) is viewed [entries, tokens, C]; a routed
+        one (ExpertList tags each expert's linears with the global token index of every row)
+        becomes the list of its non-empty per-entry row blocks, in entry order, each in the
+        order the reference's single-entry forward produces them. Other inputs pass as is."""
+        ctx = self._batch_ctx
+        if ctx is None or inp.dim() != 2:
+            return inp
+        n, tpe = ctx
+        rows = getattr(m, '_lcq_rows', None)
+        if rows is None or rows.numel() != inp.shape[0]:
+            if inp.shape[0] == n * tpe:
+                return inp.view(n, tpe, inp.shape[-1])
+            return inp
+        ent = torch.div(rows, tpe, rounding_mode='floor')
+        order = torch.argsort(ent, stable=True)
+        counts = torch.bincount(ent, minlength=n).tolist()
+        xs = inp.index_select(0, order)
+        return [t for t in torch.split(xs, counts, dim=0) if t.shape[0] > 0]
+
     def cache_input_hook(self, m, x, y, name, feat_dict):
         # device-resident, shared (no copy): see module docstring
         inputs = [t.detach() for t in x]
         if len(inputs) == 1:
-            inp = inputs[0]
+            inp = self.entry_view(m, inputs[0])
+            if isinstance(inp, list):  # per-entry row blocks of a routed expert
+                feat_dict[name].extend(t.unsqueeze(0) for t in inp)
+                return
             if inp.dim() == 2:
                 inp = inp.unsqueeze(0)
             feat_dict[name].append(inp)
@@ -380,7 +411,12 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
             if xb is None:
                 xb = torch.cat(list(input_data), dim=0)
                 self._cat_cache = (list(input_data), xb)
-            y = self._call_block(block, xb, kwargs[0], stop_after)
+            x0 = input_data[0]
+            self._batch_ctx = (len(input_data), x0.numel() // x0.shape[-1])
+            try:
+                y = self._call_block(block, xb, kwargs[0], stop_after)
+            finally:
+                self._batch_ctx = None
             if y is None:
                 return None
             outs = list(torch.split(y, [x.shape[0] for x in input_data], dim=0))

@@ -241,66 +241,103 @@ __global__ void __launch_bounds__(64) k_sqdiff_p2(const double* part, int nparts
 
 // ----------------------------------------------------------------------------------------
 // auto_clip search (auto_clip.py:83-191). A workgroup = 128 output rows (one per lane, two
-// waves) x one 128-wide group; the group's sampled-token tiles are shared through LDS.
+// waves) x one G-wide group (G = 32 / 64 / 128 / 256); the group's sampled-token tiles are
+// shared through LDS. Model dtype DT = bf16 or fp16 (every rounding below is to DT).
 // For every (row o, group g):
-//   org[t]  = bf16( sum_k bf16(x[t,g,k] * w[o,g,k]) )          (t over the T sampled tokens)
-//   step i: max_i = bf16(org_max * (1 - i/n_grid)), min_i = -max_i | bf16(org_min * (..))
-//           q = fake_quant(clamp(w, min_i, max_i)) (bf16, per-group min/max qparams)
-//           cur[t] = bf16( sum_k bf16(x * q) );  err_i = bf16(mean_t bf16(bf16(cur-org)^2))
-//   keep the first strictly smaller err (min_errs starts at bf16(1e9)).
-// The reference materialises the bf16 broadcast product, so every product is rounded to bf16
+//   org[t]  = DT( sum_k DT(x[t,g,k] * w[o,g,k]) )              (t over the T sampled tokens)
+//   step i: max_i = DT(org_max * (1 - i/n_grid)), min_i = -max_i | DT(org_min * (..))
+//           q = fake_quant(clamp(w, min_i, max_i)) (DT, per-group min/max qparams)
+//           cur[t] = DT( sum_k DT(x * q) );  err_i = DT(mean_t DT(DT(cur-org)^2))
+//   keep the first strictly smaller err (min_errs starts at DT(1e9)).
+// The reference materialises the DT broadcast product, so every product is rounded to DT
 // before the fp32 sum: that rules out MFMA (exact products). VALU design: the candidate
 // weights live unpacked in VGPRs, x tiles are fp32 in LDS and read as wave-uniform broadcasts,
 // products go through v_pk_mul_f32 + v_cvt_pk_bf16_f32 (RNE) and v_pk_add_f32 into 8 partial
 // sums (k mod 8) reduced by a halving tree (torch-CPU's vectorised order), the per-step
 // squared-error sums and the original outputs sit in LDS so the token loop stays rolled.
 // ----------------------------------------------------------------------------------------
-constexpr int CG = 128;        // group size
 constexpr int CROWS = 128;     // rows per workgroup (2 lanes per row -> 256 threads)
 constexpr int CT = 32;         // sampled tokens per LDS tile
 constexpr int CMAXSTEPS = 16;
-constexpr int CH = CG / 2;     // weights per lane: k = 8i + 4h + j, h = lane parity
+constexpr int CGMAX = 256;     // largest group (xs tile = CT x G fp32)
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+typedef _Float16 v2h __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ float bf16r(float f) {  // RNE to bf16 (v_cvt_pk_bf16_f32)
-  const __bf16 h = (__bf16)f;
-  return __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, h) << 16);
+// fp16 RNE (subnormals and overflow to inf included) in integer / fp32 arithmetic. Written
+// out rather than as (float)(_Float16)f: with the conversion pair the compiler re-forms the
+// surrounding fp32 ops into native f16 / mixed-precision instructions (v_mul_f16,
+// v_fma_mixlo_f16), which measured 1.5 % of clip bounds off the reference's on fp16 models.
+__device__ __forceinline__ float f16r_soft(float f) {
+  const uint32_t u = __float_as_uint(f), a = u & 0x7fffffffu, s = u & 0x80000000u;
+  if (a > 0x7f800000u) return f;                                    // NaN
+  if (a >= 0x477ff000u) return __uint_as_float(s | 0x7f800000u);   // >= 65520 -> inf
+  if (a < 0x38800000u) {  // below 2^-14: the fp16 subnormal grid, multiples of 2^-24
+    const float t = rintf(__uint_as_float(a) * 16777216.0f) * 5.9604644775390625e-08f;
+    return __uint_as_float(__float_as_uint(t) | s);
+  }
+  const uint32_t r = a + 0xfffu + ((a >> 13) & 1u);
+  return __uint_as_float((r & 0xffffe000u) | s);
 }
 
-// products of a pair rounded to bf16 and widened back to fp32
-__device__ __forceinline__ v2f bf16r2(v2f p) {
-  const v2bf h = __builtin_convertvector(p, v2bf);
-  const uint32_t u = __builtin_bit_cast(uint32_t, h);
-  v2f r;
-  r.x = __uint_as_float(u << 16);
-  r.y = __uint_as_float(u & 0xffff0000u);
-  return r;
+// RNE to the model dtype DT (bf16: v_cvt_pk_bf16_f32; fp16: f16r_soft) and back to fp32
+template <int DT>
+__device__ __forceinline__ float dtr(float f) {
+  if constexpr (DT == LCQ_BF16) {
+    const __bf16 h = (__bf16)f;
+    return __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, h) << 16);
+  } else {
+    return f16r_soft(f);
+  }
 }
 
-// IEEE quotient a/b given rb = RN(1/b) (Markstein: e = a - b*q0 is exact, one fma rounds)
-__device__ __forceinline__ float div_rn(float a, float b, float rb) {
-  const float q0 = a * rb;
-  const float e = __fmaf_rn(-b, q0, a);
-  return __fmaf_rn(e, rb, q0);
+// products of a pair rounded to DT and widened back to fp32
+template <int DT>
+__device__ __forceinline__ v2f dtr2(v2f p) {
+  if constexpr (DT == LCQ_BF16) {
+    const v2bf h = __builtin_convertvector(p, v2bf);
+    const uint32_t u = __builtin_bit_cast(uint32_t, h);
+    v2f r;
+    r.x = __uint_as_float(u << 16);
+    r.y = __uint_as_float(u & 0xffff0000u);
+    return r;
+  } else {
+    return v2f{f16r_soft(p.x), f16r_soft(p.y)};
+  }
+}
+
+// 4 consecutive DT elements (8 bytes) widened to fp32
+template <int DT>
+__device__ __forceinline__ void widen4(uint2 v, float* q) {
+  if constexpr (DT == LCQ_BF16) {
+    q[0] = __uint_as_float(v.x << 16);
+    q[1] = __uint_as_float(v.x & 0xffff0000u);
+    q[2] = __uint_as_float(v.y << 16);
+    q[3] = __uint_as_float(v.y & 0xffff0000u);
+  } else {
+    const v2h a = __builtin_bit_cast(v2h, v.x), b = __builtin_bit_cast(v2h, v.y);
+    q[0] = (float)a.x; q[1] = (float)a.y; q[2] = (float)b.x; q[3] = (float)b.y;
+  }
 }
 
 __device__ __forceinline__ float xor1(float v) {  // value of the partner lane (lane ^ 1)
   return __shfl_xor(v, 1, 64);
 }
 
-// sum_k bf16(x[k] * q[k]) over one 128-wide group, split over a lane pair: this lane owns
-// k = 8i + 4h + j (j = 0..3) i.e. partial sums acc_{4h+j} of the 8-way (k mod 8) order; the
+// sum_k DT(x[k] * q[k]) over one G-wide group, split over a lane pair: this lane owns
+// k = 8i + 4h + j (j = 0..3) i.e. partial sums acc_{4h+j} of the 8-way (k mod 8) order that
+// torch-CPU's vectorised reduction uses for every group size and for bf16 and fp16 alike; the
 // pair exchange forms l_j = acc_j + acc_{j+4} and both lanes finish the halving tree.
-__device__ __forceinline__ float dot_row(const float* __restrict__ xr, const float (&q)[CH],
+template <int DT, int G>
+__device__ __forceinline__ float dot_row(const float* __restrict__ xr, const float (&q)[G / 2],
                                          int h) {
   v2f a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < CG / 8; ++i) {
+  for (int i = 0; i < G / 8; ++i) {
     const float4 xv = *reinterpret_cast<const float4*>(xr + 8 * i + 4 * h);
-    a0 += bf16r2(v2f{xv.x, xv.y} * v2f{q[4 * i], q[4 * i + 1]});
-    a1 += bf16r2(v2f{xv.z, xv.w} * v2f{q[4 * i + 2], q[4 * i + 3]});
+    a0 += dtr2<DT>(v2f{xv.x, xv.y} * v2f{q[4 * i], q[4 * i + 1]});
+    a1 += dtr2<DT>(v2f{xv.z, xv.w} * v2f{q[4 * i + 2], q[4 * i + 3]});
   }
   // lane h=0 holds acc0..3, h=1 holds acc4..7: l_j = acc_j + acc_{j+4}. The partner values
   // are read in uniform control flow (a cross-lane read inside a divergent branch would see
@@ -310,40 +347,39 @@ __device__ __forceinline__ float dot_row(const float* __restrict__ xr, const flo
   const float l1 = (h ? p1 : a0.y) + (h ? a0.y : p1);
   const float l2 = (h ? p2 : a1.x) + (h ? a1.x : p2);
   const float l3 = (h ? p3 : a1.y) + (h ? a1.y : p3);
-  return bf16r((l0 + l2) + (l1 + l3));
+  return dtr<DT>((l0 + l2) + (l1 + l3));
 }
 
+template <int DT, int G>
 __device__ __forceinline__ void load_half(const uint16_t* __restrict__ wrow, int h,
-                                          float (&q)[CH]) {
+                                          float (&q)[G / 2]) {
 #pragma unroll
-  for (int i = 0; i < CG / 8; ++i) {
-    const uint2 v = *reinterpret_cast<const uint2*>(wrow + 8 * i + 4 * h);
-    q[4 * i] = __uint_as_float(v.x << 16);
-    q[4 * i + 1] = __uint_as_float(v.x & 0xffff0000u);
-    q[4 * i + 2] = __uint_as_float(v.y << 16);
-    q[4 * i + 3] = __uint_as_float(v.y & 0xffff0000u);
-  }
+  for (int i = 0; i < G / 8; ++i)
+    widen4<DT>(*reinterpret_cast<const uint2*>(wrow + 8 * i + 4 * h), &q[4 * i]);
 }
 
-__global__ void __launch_bounds__(2 * CROWS, 2)
+template <int DT, int G>
+__global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 weights/lane
     k_auto_clip(const uint16_t* __restrict__ w, const uint16_t* __restrict__ x, int64_t oc,
                 int64_t ic, int T, int nsteps, const float* __restrict__ factors, float qmin,
                 float qmax, int sym, int clip_sym, uint16_t* best_max, uint16_t* best_min) {
-  __shared__ __attribute__((aligned(16))) float xs[CT * CG];     // 16 KB
+  constexpr int CH = G / 2;    // weights per lane: k = 8i + 4h + j, h = lane parity
+  constexpr int CHUNKS = G / 8;
+  __shared__ __attribute__((aligned(16))) float xs[CT * G];      // <= 32 KB
   __shared__ float orgs[CT * CROWS];                              // 16 KB
   __shared__ float es[CMAXSTEPS * CROWS];                          // 8 KB
   const int tid = threadIdx.x;
   const int r = tid >> 1, h = tid & 1;
   const int64_t o = (int64_t)blockIdx.x * CROWS + r;
   const int64_t g = blockIdx.y;
-  const int64_t ng = ic / CG;
+  const int64_t ng = ic / G;
   const bool live = o < oc;
-  const uint16_t* wrow = w + (live ? o : 0) * ic + g * CG;
+  const uint16_t* wrow = w + (live ? o : 0) * ic + g * G;
 
   float mxs = -INFINITY, mn = INFINITY, amax = 0.f;
   {
     float q[CH];
-    load_half(wrow, h, q);
+    load_half<DT, G>(wrow, h, q);
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       mxs = fmaxf(mxs, q[k]);
@@ -361,54 +397,51 @@ __global__ void __launch_bounds__(2 * CROWS, 2)
 
   for (int t0 = 0; t0 < T; t0 += CT) {
     __syncthreads();  // previous tile fully consumed
-    // stage CT token rows of this group as fp32: 512 chunks of 8 bf16, 2 per thread
-#pragma unroll
-    for (int i = 0; i < (CT * CG / 8) / (2 * CROWS); ++i) {
-      const int idx = i * 2 * CROWS + tid;
-      const int row = idx >> 4, ch = idx & 15;
+    // stage CT token rows of this group as fp32, 8 elements (16 B) per chunk
+    for (int idx = tid; idx < CT * CHUNKS; idx += 2 * CROWS) {
+      const int row = idx / CHUNKS, ch = idx % CHUNKS;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (t0 + row < T)
-        v = *reinterpret_cast<const uint4*>(x + (int64_t)(t0 + row) * ic + g * CG + ch * 8);
-      float4 a, b;
-      a.x = __uint_as_float(v.x << 16); a.y = __uint_as_float(v.x & 0xffff0000u);
-      a.z = __uint_as_float(v.y << 16); a.w = __uint_as_float(v.y & 0xffff0000u);
-      b.x = __uint_as_float(v.z << 16); b.y = __uint_as_float(v.z & 0xffff0000u);
-      b.z = __uint_as_float(v.w << 16); b.w = __uint_as_float(v.w & 0xffff0000u);
-      *reinterpret_cast<float4*>(&xs[row * CG + ch * 8]) = a;
-      *reinterpret_cast<float4*>(&xs[row * CG + ch * 8 + 4]) = b;
+        v = *reinterpret_cast<const uint4*>(x + (int64_t)(t0 + row) * ic + g * G + ch * 8);
+      float a[8];
+      widen4<DT>(make_uint2(v.x, v.y), a);
+      widen4<DT>(make_uint2(v.z, v.w), a + 4);
+      *reinterpret_cast<float4*>(&xs[row * G + ch * 8]) = make_float4(a[0], a[1], a[2], a[3]);
+      *reinterpret_cast<float4*>(&xs[row * G + ch * 8 + 4]) = make_float4(a[4], a[5], a[6], a[7]);
     }
     __syncthreads();
     const int tn = min(CT, T - t0);
     // pass p = 0: original outputs; p = s + 1: shrink step s
     for (int p = 0; p <= nsteps; ++p) {
       float q[CH];
-      load_half(wrow, h, q);
+      load_half<DT, G>(wrow, h, q);
       if (p > 0) {
         const float f = factors[p - 1];
-        const float smax = bf16r(org_max * f);
-        const float smin = clip_sym ? -smax : bf16r(org_min * f);
+        const float smax = dtr<DT>(org_max * f);
+        const float smin = clip_sym ? -smax : dtr<DT>(org_min * f);
         const float cmn = fminf(fmaxf(mn, smin), smax);
         const float cmx = fminf(fmaxf(mxs, smin), smax);
         float qs, qz;
-        qparams_ct<LCQ_BF16>(cmn, cmx, qmin, qmax, sym, qs, qz);
-        const float rs = 1.0f / qs;  // correctly rounded reciprocal (IEEE division)
+        qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
           const float v = fminf(fmaxf(q[k], smin), smax);
-          float tq = rintf(bf16r(div_rn(v, qs, rs)));
-          if (!sym) tq = bf16r(tq + qz);
+          // correctly rounded fp32 quotient (IEEE division; a reciprocal-based quotient can
+          // miss by an ulp, which fp16's extra mantissa bits expose), then rounded to DT
+          float tq = rintf(dtr<DT>(__fdiv_rn(v, qs)));
+          if (!sym) tq = dtr<DT>(tq + qz);
           tq = fminf(fmaxf(tq, qmin), qmax);
-          q[k] = bf16r((sym ? tq : bf16r(tq - qz)) * qs);
+          q[k] = dtr<DT>((sym ? tq : dtr<DT>(tq - qz)) * qs);
         }
       }
       float e = (p > 0) ? es[(p - 1) * CROWS + r] : 0.f;
       for (int t = 0; t < tn; ++t) {
-        const float d = dot_row(&xs[t * CG], q, h);
+        const float d = dot_row<DT, G>(&xs[t * G], q, h);
         if (p == 0) {
           if (h == 0) orgs[t * CROWS + r] = d;
         } else {
-          const float dd = bf16r(d - orgs[t * CROWS + r]);
-          e += bf16r(dd * dd);
+          const float dd = dtr<DT>(d - orgs[t * CROWS + r]);
+          e += dtr<DT>(dd * dd);
         }
       }
       if (p > 0 && h == 0) es[(p - 1) * CROWS + r] = e;
@@ -416,18 +449,23 @@ __global__ void __launch_bounds__(2 * CROWS, 2)
     }
   }
   if (!live || h) return;
-  float bmax = org_max, bmin = org_min, best = bf16r(1e9f);
+  float bmax = org_max, bmin = org_min, best = dtr<DT>(1e9f);
   for (int s = 0; s < nsteps; ++s) {
-    const float em = bf16r(es[s * CROWS + r] / (float)T);
+    const float em = dtr<DT>(es[s * CROWS + r] / (float)T);
     if (em < best) {
       best = em;
       const float f = factors[s];
-      bmax = bf16r(org_max * f);
-      bmin = clip_sym ? -bmax : bf16r(org_min * f);
+      bmax = dtr<DT>(org_max * f);
+      bmin = clip_sym ? -bmax : dtr<DT>(org_min * f);
     }
   }
-  best_max[o * ng + g] = (uint16_t)(__float_as_uint(bmax) >> 16);
-  best_min[o * ng + g] = (uint16_t)(__float_as_uint(bmin) >> 16);
+  if constexpr (DT == LCQ_BF16) {
+    best_max[o * ng + g] = (uint16_t)(__float_as_uint(bmax) >> 16);
+    best_min[o * ng + g] = (uint16_t)(__float_as_uint(bmin) >> 16);
+  } else {
+    best_max[o * ng + g] = __builtin_bit_cast(uint16_t, (_Float16)bmax);
+    best_min[o * ng + g] = __builtin_bit_cast(uint16_t, (_Float16)bmin);
+  }
 }
 
 template <int DT>
@@ -573,21 +611,47 @@ extern "C" int lcq_sq_diff_mean(const void* a, const void* b, int dtype, int64_t
   return check_launch("lcq_sq_diff_mean");
 }
 
-extern "C" int lcq_auto_clip_search(const void* w, const void* x, int64_t oc, int64_t ic,
-                                    int64_t T, int group, int nsteps, const void* factors,
-                                    int qmin, int qmax, int sym, int clip_sym, void* best_max,
-                                    void* best_min, void* stream) {
-  LCQ_REQUIRE(group == CG, "auto-clip kernel supports group_size 128");
-  LCQ_REQUIRE(oc > 0 && ic > 0 && ic % CG == 0, "ic must be a multiple of 128");
-  LCQ_REQUIRE(T > 0 && nsteps >= 1 && nsteps <= CMAXSTEPS, "bad T / nsteps (<= 16)");
-  LCQ_REQUIRE(qmax > qmin, "qmax <= qmin");
-  dim3 grid((unsigned)((oc + CROWS - 1) / CROWS), (unsigned)(ic / CG));
-  hipLaunchKernelGGL(k_auto_clip, grid, 2 * CROWS, 0, as_stream(stream),
+template <int DT, int G>
+static void launch_auto_clip(const void* w, const void* x, int64_t oc, int64_t ic, int64_t T,
+                             int nsteps, const void* factors, int qmin, int qmax, int sym,
+                             int clip_sym, void* best_max, void* best_min, hipStream_t st) {
+  dim3 grid((unsigned)((oc + CROWS - 1) / CROWS), (unsigned)(ic / G));
+  hipLaunchKernelGGL((k_auto_clip<DT, G>), grid, 2 * CROWS, 0, st,
                      reinterpret_cast<const uint16_t*>(w), reinterpret_cast<const uint16_t*>(x),
                      oc, ic, (int)T, nsteps, reinterpret_cast<const float*>(factors),
                      (float)qmin, (float)qmax, sym, clip_sym,
                      reinterpret_cast<uint16_t*>(best_max), reinterpret_cast<uint16_t*>(best_min));
+}
+
+template <int DT>
+static int auto_clip_group(int group, const void* w, const void* x, int64_t oc, int64_t ic,
+                           int64_t T, int nsteps, const void* factors, int qmin, int qmax,
+                           int sym, int clip_sym, void* bmax, void* bmin, hipStream_t st) {
+  switch (group) {
+    case 32: launch_auto_clip<DT, 32>(w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, bmax, bmin, st); break;
+    case 64: launch_auto_clip<DT, 64>(w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, bmax, bmin, st); break;
+    case 128: launch_auto_clip<DT, 128>(w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, bmax, bmin, st); break;
+    default: launch_auto_clip<DT, 256>(w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, bmax, bmin, st);
+  }
   return check_launch("lcq_auto_clip_search");
+}
+
+extern "C" int lcq_auto_clip_search(const void* w, const void* x, int dtype, int64_t oc,
+                                    int64_t ic, int64_t T, int group, int nsteps,
+                                    const void* factors, int qmin, int qmax, int sym,
+                                    int clip_sym, void* best_max, void* best_min, void* stream) {
+  LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16, "auto-clip: bf16 or fp16 model dtype");
+  LCQ_REQUIRE(group == 32 || group == 64 || group == 128 || group == CGMAX,
+              "auto-clip kernel supports group_size 32 / 64 / 128 / 256");
+  LCQ_REQUIRE(oc > 0 && ic > 0 && ic % group == 0, "ic must be a multiple of the group size");
+  LCQ_REQUIRE(T > 0 && nsteps >= 1 && nsteps <= CMAXSTEPS, "bad T / nsteps (<= 16)");
+  LCQ_REQUIRE(qmax > qmin, "qmax <= qmin");
+  hipStream_t st = as_stream(stream);
+  if (dtype == LCQ_BF16)
+    return auto_clip_group<LCQ_BF16>(group, w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym,
+                                     clip_sym, best_max, best_min, st);
+  return auto_clip_group<LCQ_F16>(group, w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym,
+                                  clip_sym, best_max, best_min, st);
 }
 
 extern "C" int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t cols,

@@ -109,7 +109,11 @@ class GPTQ(BaseBlockwiseQuantization):
         entry = self.layers_cache.get(name)
         if entry is None or not entry['owner']:
             return
-        entry['acc'].add_batch(inp)
+        v = self.entry_view(layer, inp)
+        if isinstance(v, list):  # a routed expert: one sample per entry that reached it
+            entry['acc'].add_batch(torch.cat(v, dim=0), samples=len(v))
+        else:
+            entry['acc'].add_batch(v)
 
     # ---- transform (gptq.py:96-244) -------------------------------------------------------------
     # Linears fed the same input (q/k/v, gate/up) share H, perm, damping and U, and GPTQ's

@@ -30,10 +30,12 @@ class HessianAccumulator:
         self.prepared = None  # (U, perm, dead) once the layer transform has factored H
 
     @torch.no_grad()
-    def add_batch(self, inp: torch.Tensor):
+    def add_batch(self, inp: torch.Tensor, samples: int | None = None):
+        """`samples`: how many of the reference's add_batch calls this batch stands for
+        (default: the batch dim of a 3-D input, 1 for a 2-D one)."""
         if inp.dim() == 2:
             inp = inp.unsqueeze(0)
-        b = inp.shape[0]
+        b = inp.shape[0] if samples is None else samples
         x = inp.reshape(-1, inp.shape[-1])
         if x.dtype not in (torch.bfloat16, torch.float16):
             x = x.to(torch.bfloat16)  # fp32 activations: bf16 MFMA path (documented tolerance)

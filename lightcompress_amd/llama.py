@@ -4,18 +4,14 @@ replacement, first-block input capture. The model lives in HBM for the whole run
 """
 from __future__ import annotations
 
-import inspect
 import os
 import types
-from collections import defaultdict
 
 import torch
 import torch.nn as nn
 
-from .module_utils import _LLMC_LINEAR_TYPES_, _TRANSFORMERS_LINEAR_TYPES_
+from .base_model import BaseModel, _linear_forward
 from .registry import MODEL_REGISTRY
-
-_LINEAR_TYPES = tuple(_LLMC_LINEAR_TYPES_ + _TRANSFORMERS_LINEAR_TYPES_)
 
 
 _ORIG_ROTARY = None
@@ -96,10 +92,6 @@ def _fused_mlp_forward(self, x):
     return self.down_proj(_gate_up_silu(self, x))
 
 
-def _linear_forward(self, x):
-    """nn.Linear.forward on the lcq projection GEMM (module_utils.lcq_linear)."""
-    from .module_utils import lcq_linear
-    return lcq_linear(x, self.weight, self.bias)
 
 
 def _fused_rmsnorm_forward(self, hidden_states):
@@ -276,26 +268,25 @@ class _Blocks(nn.Module):
 
 
 @MODEL_REGISTRY
-class Llama:
+class Llama(BaseModel):
+    """llama.py:1-91 on the BaseModel contract, with the Llama calibration-forward fusions."""
     block_name_prefix = 'model.layers'
 
-    def __init__(self, config=None, hf_model=None, device='cuda', dtype=None):
-        if hf_model is None:
-            from transformers import AutoModelForCausalLM
-            path = config['model']['path']
-            td = config['model'].get('torch_dtype', 'auto')
-            dtype = dtype or (torch.bfloat16 if td == 'auto' else getattr(torch, td))
-            hf_model = AutoModelForCausalLM.from_pretrained(path, torch_dtype=dtype,
-                                                            local_files_only=True)
-        self.model = hf_model.to(device).eval()
-        self.model_config = hf_model.config
-        inner = getattr(hf_model, 'model', hf_model)
+    def find_blocks(self):
+        inner = getattr(self.model, 'model', self.model)
         self.blocks = inner.layers
         self.rotary_emb = inner.rotary_emb
-        self.embed_tokens = getattr(inner, 'embed_tokens', None)
-        self.torch_dtype = next(self.model.parameters()).dtype
-        self.mm_model = None
+
+    def find_embed_layers(self):
+        self.embed_tokens = getattr(getattr(self.model, 'model', self.model), 'embed_tokens',
+                                    None)
+
+    def install_fused_forward(self):
         install_fused_forward(self.model)
+
+    def get_layernorms_in_block(self, block):
+        return {'input_layernorm': block.input_layernorm,
+                'post_attention_layernorm': block.post_attention_layernorm}
 
     # -- random-init constructor (synthetic benchmark / tests) --------------------------------
     @classmethod
@@ -331,25 +322,6 @@ class Llama:
         return {'position_embeddings': (cos, sin), 'attention_mask': None, 'position_ids': pos}
 
     # -- BaseModel contract ---------------------------------------------------------------------
-    def skip_layer_name(self):
-        return ['lm_head']
-
-    def get_blocks(self):
-        return self.blocks
-
-    def get_block_linears(self, block):
-        return {n: m for n, m in block.named_modules() if isinstance(m, _LINEAR_TYPES)}
-
-    def get_extra_modules(self, block):
-        return {}
-
-    def clear_block_cache(self, block):
-        """Drop the staged forward's memo of a finished block (its tensors are large)."""
-        clear_stage_cache(block)
-
-    def get_num_attention_heads(self):
-        return self.model_config.num_attention_heads
-
     def get_subsets_in_block(self, block):
         """llama.py:52-91."""
         return [
@@ -369,52 +341,6 @@ class Llama:
              'inspect': block.mlp.down_proj, 'has_kwargs': False, 'is_mlp': True},
         ]
 
-    @staticmethod
-    def _same_fake_quant(m, module, params_dict):
-        """m is already `module` (exact class) built with the same quant callbacks: a new one
-        would re-derive the identical fake-quant weight from the same weight and buffers, so
-        the existing object is kept (the staged forward's memo stays valid)."""
-        if type(m) is not module or not hasattr(m, 'w_qdq'):
-            return False
-
-        def same(a, b):
-            if a is b:
-                return True
-            fa, fb = getattr(a, 'func', None), getattr(b, 'func', None)
-            return (fa is not None and fa == fb and a.args == b.args
-                    and a.keywords.keys() == b.keywords.keys()
-                    and all(a.keywords[k] is b.keywords[k] for k in a.keywords))
-        return (same(m.w_qdq, params_dict.get('w_qdq')) and
-                same(m.a_qdq, params_dict.get('a_qdq')))
-
-    def replace_module_subset(self, module, block, subset, block_idx, params_dict):
-        for name, m in subset['layers'].items():
-            if not isinstance(m, _LINEAR_TYPES) or getattr(m, 'no_quant', False):
-                continue
-            if self._same_fake_quant(m, module, params_dict):
-                continue
-            new = module.new(m, **params_dict)
-            parent_name, _, child = name.rpartition('.')
-            parent = block.get_submodule(parent_name) if parent_name else block
-            setattr(parent, child, new)
-
-    def replace_module_block(self, module, block, block_idx, params_dict):
-        self.replace_module_subset(module, block, {'layers': self.get_block_linears(block)},
-                                   block_idx, params_dict)
-
-    def replace_module_all(self, module, params_dict, keep_device=True):
-        for i, block in enumerate(self.blocks):
-            self.replace_module_block(module, block, i, params_dict)
-
-    def convert_dtype(self, dtype):
-        for block in self.blocks:
-            for m in block.modules():
-                if isinstance(m, nn.Linear) and m.weight.dtype != dtype:
-                    m.weight.data = m.weight.data.to(dtype)
-
-    def set_modality(self, modality):
-        self.modality = modality
-
     def save_pretrained(self, path):
         if hasattr(self.model, 'save_pretrained'):
             self.model.save_pretrained(path)
@@ -427,37 +353,3 @@ class Llama:
               if torch.is_tensor(v)}
         save_file(sd, os.path.join(path, 'model.safetensors'))
         self.model_config.to_json_file(os.path.join(path, 'config.json'))
-
-    # -- calibration capture (base_model.py:174-192, 279-336) -----------------------------------
-    @torch.no_grad()
-    def collect_first_block_input(self, calib_data):
-        first = defaultdict(list)
-        block0 = self.blocks[0]
-        sig = list(inspect.signature(block0.forward).parameters.keys())
-
-        class Catcher(nn.Module):
-            def __init__(self, module):
-                super().__init__()
-                self.module = module
-
-            def forward(self, *args, **kwargs):
-                for i, a in enumerate(args):
-                    if i > 0:
-                        kwargs[sig[i]] = a
-                first['data'].append(args[0])
-                first['kwargs'].append(kwargs)
-                raise ValueError
-
-        self.blocks[0] = Catcher(block0)
-        try:
-            for data in calib_data:
-                data = {k: (v.to(next(self.model.parameters()).device) if torch.is_tensor(v)
-                            else v) for k, v in data.items()}
-                try:
-                    self.model(**data)
-                except ValueError:
-                    pass
-        finally:
-            self.blocks[0] = block0
-        self.first_block_input = first
-        return first

@@ -347,7 +347,8 @@ _REALQUANT_LINEAR_MAP_ = {
     'lightx2v_quant': Lightx2vRealQuantLinear,
 }
 
-_LLMC_LINEAR_TYPES_ = [OriginFloatLinear, FakeQuantLinear, EffcientFakeQuantLinear,
-                       VllmRealQuantLinear, SglRealQuantLinear, AutoawqRealQuantLinear,
-                       MlcllmRealQuantLinear, LightllmRealQuantLinear, Lightx2vRealQuantLinear]
+_LLMC_LINEAR_TYPES_ = [LlmcFp8Linear, OriginFloatLinear, FakeQuantLinear,
+                       EffcientFakeQuantLinear, VllmRealQuantLinear, SglRealQuantLinear,
+                       AutoawqRealQuantLinear, MlcllmRealQuantLinear, LightllmRealQuantLinear,
+                       Lightx2vRealQuantLinear]
 _TRANSFORMERS_LINEAR_TYPES_ = [nn.Linear]

@@ -479,8 +479,10 @@ def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, 
     ng = ic // group
     bmax = torch.empty((oc, ng, 1), dtype=w.dtype, device=w.device)
     bmin = torch.empty((oc, ng, 1), dtype=w.dtype, device=w.device)
-    N.call('lcq_auto_clip_search', N.ptr(w.contiguous()), N.ptr(x.contiguous()), oc, ic, T,
-           int(group), int(nsteps), N.ptr(factors), int(qmin), int(qmax), int(sym),
+    if x.dtype != w.dtype:
+        raise ValueError('auto-clip: x and w must share the model dtype')
+    N.call('lcq_auto_clip_search', N.ptr(w.contiguous()), N.ptr(x.contiguous()), N.dt(w), oc,
+           ic, T, int(group), int(nsteps), N.ptr(factors), int(qmin), int(qmax), int(sym),
            int(clip_sym), N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
     return bmax, bmin
 

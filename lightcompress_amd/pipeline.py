@@ -2,8 +2,14 @@
 from the YAML config, run the block loop, deploy / save."""
 from __future__ import annotations
 
-from .registry import ALGO_REGISTRY
+from .registry import ALGO_REGISTRY, MODEL_REGISTRY
 from . import awq, gptq, rtn  # noqa: F401  (register algorithms)
+from . import deepseekv3, llama, opt  # noqa: F401  (register model adapters)
+
+
+def build_model(config, device='cuda'):
+    """MODEL_REGISTRY[config.model.type](config) (llmc/__main__.py:31)."""
+    return MODEL_REGISTRY[config['model']['type']](config, device=device)
 
 
 def build_algo(model, config, calib_input, padding_mask=None):

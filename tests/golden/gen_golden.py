@@ -295,28 +295,35 @@ def gen_awq(only_v1=False):
 
 
 def gen_clip():
-    """Reference AutoClipper.auto_clip_layer (clip v1) + apply_clip on bf16 layers."""
+    """Reference AutoClipper.auto_clip_layer (clip v1) + apply_clip on bf16 / fp16 layers,
+    group sizes 32 .. 256."""
     R.init_dist()
     q = R.quant_module()
     import llmc.compression.quantization.auto_clip as ac
-    cases = [('sym_s', True, True, 128, 256, 512, 64),
-             ('asym_s', False, False, 128, 256, 512, 64),
-             ('sym_w_asym_clip', True, False, 256, 512, 1024, 128)]
-    for i, (name, sym, clip_sym, oc, ic, ntok, nst) in enumerate(cases):
-        wq = q.IntegerQuantizer(4, sym, 'per_group', group_size=128)
+    bf, hf = torch.bfloat16, torch.float16
+    # (name, sym, clip_sym, oc, ic, tokens, n_sample_token, group, model dtype)
+    cases = [('sym_s', True, True, 128, 256, 512, 64, 128, bf),
+             ('asym_s', False, False, 128, 256, 512, 64, 128, bf),
+             ('sym_w_asym_clip', True, False, 256, 512, 1024, 128, 128, bf),
+             ('asym_g64', False, False, 192, 256, 512, 64, 64, bf),      # DSv3 configs
+             ('sym_g256', True, True, 128, 512, 512, 64, 256, bf),
+             ('asym_g128_f16', False, False, 128, 512, 512, 64, 128, hf),  # OPT (fp16)
+             ('sym_g32_f16', True, True, 64, 256, 512, 64, 32, hf)]
+    for i, (name, sym, clip_sym, oc, ic, ntok, nst, grp, dt) in enumerate(cases):
+        wq = q.IntegerQuantizer(4, sym, 'per_group', group_size=grp)
         clipper = ac.AutoClipper(w_only=True, wquantizer=wq, aquantizer=None,
                                  clip_version='v1', clip_sym=clip_sym, save_clip=False,
                                  padding_mask=None)
-        w = weights(oc, ic, torch.bfloat16, 400 + i, edge=False)
-        x = _acts(1, ntok, ic, 500 + i)[0]
+        w = weights(oc, ic, dt, 400 + i, edge=False)
+        x = _acts(1, ntok, ic, 500 + i, dtype=dt)[0]
         bmax, bmin = clipper.auto_clip_layer(0, 'l', w.clone(), [x.clone()],
                                              n_sample_token=nst)
-        m = torch.nn.Linear(ic, oc, bias=False).to(torch.bfloat16)
+        m = torch.nn.Linear(ic, oc, bias=False).to(dt)
         m.weight.data = w.clone()
         clipper.apply_clip(0, m, bmin.clone(), bmax.clone(), 'l')
         F.save(f'clip_{name}', w=w, x=x, best_max=bmax, best_min=bmin,
                w_clipped=m.weight.data.clone(),
-               meta=torch.tensor([int(sym), int(clip_sym), nst]))
+               meta=torch.tensor([int(sym), int(clip_sym), nst, grp]))
     print('clip fixtures written')
 
 

@@ -1,7 +1,8 @@
 """End-to-end pipeline goldens: the REAL reference's ``run_block_loop`` + ``deploy('fake_quant')``
-on a tiny random Llama (2 decoder layers), CPU, in the build container only.
+on tiny random Llama / OPT / DeepSeek-V3 models (2 decoder layers, tests/golden/tiny_models.py),
+CPU, in the build container only.
 
-    python tests/golden/gen_pipeline.py
+    python tests/golden/gen_pipeline.py [config ...]
 
 Pins what the subset-level fixtures cannot: the block driver (SURVEY.md §8c "Python harness
 counterparts"): block order, subset order and skip rules (o_proj skipped under GQA,
@@ -9,8 +10,8 @@ awq.py:338-351; q/k clip skip, auto_clip.py:56-60), GPTQ's true_sequential rehoo
 from fake-quantized predecessors (base_blockwise_quantization.py:498-526), quant_out
 (:436-462) and AWQ's input-feature rescaling (:891-897).
 
-Writes ``tests/golden/pipeline_llama/`` (HF config + safetensors of the random model, so the
-test loads the very same weights through the Llama adapter) and ``pipe_<algo>.npz`` with the
+Writes ``tests/golden/pipeline_<family>/`` (HF config + safetensors of the random model, so the
+test loads the very same weights through our adapter) and ``pipe_<config>.npz`` with the
 calibration token ids and every deployed linear weight of both blocks. Calibration data are
 token ids fed through the reference's own Catcher (base_model.py:279-336); the embedding table
 has log-normal per-channel magnitudes so that AWQ's scale search has outlier channels to find.
@@ -29,6 +30,7 @@ HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE))
 import _ref_import as R  # noqa: E402
 import fixtures as F  # noqa: E402
+import tiny_models as TM  # noqa: E402
 
 from pipeline_configs import CONFIGS, MODEL_DIR  # noqa: E402
 
@@ -81,10 +83,72 @@ def make_model():
     return cfg
 
 
-def run_reference(name, spec):
+def _adapter(family):
+    """The reference's own adapter class. DeepSeek-V3's (deepseekv3.py:69-167) indexes
+    ``mlp.experts[i]`` as the checkpoint's remote modeling code lays them out; transformers'
+    built-in DeepseekV3 fuses the experts into 3-D tensors, so the loaded model is given the
+    per-expert layout first (lightcompress_amd.deepseekv3.unfuse_experts: same weights)."""
     import llmc.models.base_model as bm
-    from llmc.models.llama import Llama
     bm.BaseModel.build_tokenizer = lambda self: setattr(self, 'tokenizer', None)
+    if family == 'Llama':
+        from llmc.models.llama import Llama
+        return Llama
+    if family == 'Opt':
+        from llmc.models.opt import Opt
+        return Opt
+    from llmc.models.deepseekv3 import DeepseekV3
+    sys.path.insert(0, str(HERE.parent.parent))
+    from lightcompress_amd.deepseekv3 import unfuse_experts
+
+    class DeepseekV3PerExpert(DeepseekV3):
+        def build_model(self):
+            super().build_model()
+            unfuse_experts(self.model)
+    return DeepseekV3PerExpert
+
+
+def subset_structure(model, block):
+    """The adapter's get_subsets_in_block(block) as names (modules resolved inside the block)."""
+    names = {id(m): n for n, m in block.named_modules()}
+    out = []
+    for sub in model.get_subsets_in_block(block):
+        d = {'layers': list(sub['layers']),
+             'prev_op': [None if p is None else names[id(p)] for p in sub['prev_op']],
+             'input': list(sub['input']), 'inspect': names[id(sub['inspect'])]}
+        for k in ('has_kwargs', 'is_mlp', 'do_trans', 'skip_rotate'):
+            if k in sub:
+                d[k] = sub[k]
+        out.append(d)
+    return out
+
+
+def dump_structure(family):
+    """subsets_<family>.json: every block's subset structure from the reference adapter, plus
+    its block linears, extra modules and layer norms (the adapter contract, base_model.py)."""
+    import json
+    cls = _adapter(family)
+    dtype = 'torch.float16' if family == 'Opt' else 'torch.bfloat16'
+    model = cls(ED({'model': {'type': family, 'path': str(TM.MODEL_DIRS[family]),
+                              'torch_dtype': dtype}}))
+    blocks = []
+    for block in model.get_blocks():
+        names = {id(m): n for n, m in block.named_modules()}
+        blocks.append({'subsets': subset_structure(model, block),
+                       'linears': list(model.get_block_linears(block)),
+                       'extra': {k: names[id(v)] for k, v in
+                                 model.get_extra_modules(block).items()},
+                       'layernorms': {k: names[id(v)] for k, v in
+                                      model.get_layernorms_in_block(block).items()}})
+    out = {'family': family, 'block_name_prefix': model.block_name_prefix,
+           'has_bias': model.has_bias(), 'skip_layer_name': model.skip_layer_name(),
+           'blocks': blocks}
+    (HERE / f'subsets_{family}.json').write_text(json.dumps(out, indent=1))
+    print(f'subsets_{family}.json: {sum(len(b["subsets"]) for b in blocks)} subsets')
+
+
+def run_reference(name, spec):
+    family = spec.get('model', 'Llama')
+    model_cls = _adapter(family)
     if spec['quant']['method'] == 'GPTQ':
         import llmc.compression.quantization.gptq as mod
         algo_cls = mod.GPTQ
@@ -94,11 +158,13 @@ def run_reference(name, spec):
     else:
         import llmc.compression.quantization.rtn as mod
         algo_cls = mod.RTN
-    config = ED({'model': {'type': 'Llama', 'path': str(MODEL_DIR), 'torch_dtype': 'torch.bfloat16'},
+    dtype = 'torch.float16' if family == 'Opt' else 'torch.bfloat16'
+    config = ED({'model': {'type': family, 'path': str(TM.MODEL_DIRS[family]),
+                           'torch_dtype': dtype},
                  'quant': dict(copy.deepcopy(spec['quant']), modality='language')})
     if spec['calib']:
         config['calib'] = dict(spec['calib'])
-    model = Llama(config)
+    model = model_cls(config)
     calib = spec['calib']
     ids = None
     if calib is None:
@@ -161,7 +227,12 @@ def run_reference(name, spec):
 if __name__ == '__main__':
     R.install()
     R.init_dist()
-    make_model()
     which = sys.argv[1:] or list(CONFIGS)
+    for fam in sorted({CONFIGS[k].get('model', 'Llama') for k in which}):
+        if fam == 'Llama':
+            make_model()
+        else:
+            TM.save(fam)
+        dump_structure(fam)
     for k in which:
         run_reference(k, CONFIGS[k])

@@ -53,4 +53,47 @@ CONFIGS = {
     'rtn': {'quant': {'method': 'RTN',
                       'weight': {'bit': 8, 'symmetric': True, 'granularity': 'per_channel'}},
             'calib': None},
+    # ---- OPT (opt.py:53-89; fc2 do_trans False), fp16 -------------------------------------
+    # BASELINE config 1: OPT-125M RTN w8a16 per-channel (data-free)
+    'opt_rtn': {'model': 'Opt',
+                'quant': {'method': 'RTN',
+                          'weight': {'bit': 8, 'symmetric': True, 'granularity': 'per_channel'}},
+                'calib': None},
+    'opt_awq': {'model': 'Opt',
+                'quant': {'method': 'Awq',
+                          'weight': {'bit': 4, 'symmetric': True, 'granularity': 'per_group',
+                                     'group_size': 128},
+                          'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True,
+                                      'clip_sym': True}},
+                'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}},
+    'opt_gptq': {'model': 'Opt',
+                 'quant': {'method': 'GPTQ',
+                           'weight': {'bit': 4, 'symmetric': False, 'granularity': 'per_group',
+                                      'group_size': 128},
+                           'special': {'actorder': True, 'static_groups': False,
+                                       'percdamp': 0.01, 'blocksize': 128,
+                                       'true_sequential': True},
+                           'quant_out': True},
+                 'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}},
+    # ---- DeepSeek-V3 (deepseekv3.py:69-167: MLA subsets, MoE + per-expert down subsets) -----
+    # configs/quantization/deepseekv3/awq_w_only_dsv3_bf16.yml, calib shrunk
+    'dsv3_awq': {'model': 'DeepseekV3',
+                 'quant': {'method': 'Awq',
+                           'weight': {'bit': 4, 'symmetric': False, 'granularity': 'per_group',
+                                      'group_size': 64},
+                           'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True,
+                                       'save_mem': False}},
+                 'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}},
+    # static per-tensor activation calibration through the expert subsets (each expert's
+    # act scale from the tokens routed to it). The FP8 form (e4m3 act, sglang/fp8 configs)
+    # needs qtorch in the reference (quant.py:975-978, absent), so the reference runs the
+    # int8 form; tests/test_models_gpu.py checks the FP8 run's scales against these.
+    'dsv3_rtn_a8_static': {'model': 'DeepseekV3',
+                           'quant': {'method': 'RTN',
+                                     'weight': {'bit': 8, 'symmetric': True,
+                                                'granularity': 'per_channel', 'group_size': -1},
+                                     'act': {'bit': 8, 'symmetric': True,
+                                             'granularity': 'per_tensor', 'static': True,
+                                             'calib_algo': 'static_minmax'}},
+                           'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}, 'diag': False},
 }

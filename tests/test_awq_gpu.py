@@ -82,16 +82,17 @@ def test_auto_clip_vs_reference(dev, name):
     from lightcompress_amd import ops
     from lightcompress_amd.auto_clip import AutoClipper
     c = F.load(name)
-    sym, clip_sym, nst = c['meta'].tolist()
+    sym, clip_sym, nst, group = c['meta'].tolist()
     qmin, qmax = (-8, 7) if sym else (0, 15)
     x = AutoClipper.sample_tokens(c['x'].to(dev), nst)
-    bmax, bmin = ops.auto_clip_search(c['w'].to(dev), x, 128, 10, 20, qmin, qmax, bool(sym),
+    bmax, bmin = ops.auto_clip_search(c['w'].to(dev), x, group, 10, 20, qmin, qmax, bool(sym),
                                       bool(clip_sym))
+    assert bmax.dtype == c['w'].dtype
     eq_max = (bits(bmax) == bits(c['best_max'])).float().mean().item()
     eq_min = (bits(bmin) == bits(c['best_min'])).float().mean().item()
     assert eq_max == 1.0 and eq_min == 1.0, (eq_max, eq_min)
     w = c['w'].to(dev).clone()
-    ops.clip_apply(w, 128, bmax.reshape(-1), None if clip_sym else bmin.reshape(-1), out=w)
+    ops.clip_apply(w, group, bmax.reshape(-1), None if clip_sym else bmin.reshape(-1), out=w)
     assert torch.equal(bits(w), bits(c['w_clipped']))
 
 

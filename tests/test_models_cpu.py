@@ -1,0 +1,86 @@
+"""Model adapters on the CPU (no kernels run): each adapter's contract — subsets of every block
+(layers, prev_op, input, inspect, flags), block linears, extra modules, layer norms — equals
+the reference adapter's on the same tiny model (tests/golden/subsets_<family>.json, written
+by gen_pipeline.py from llmc/models/{llama,opt,deepseekv3}.py), and DeepSeek-V3's per-expert
+layout computes what transformers' fused experts compute."""
+import json
+
+import pytest
+import torch
+
+import tiny_models as TM
+
+FAMILIES = ['Llama', 'Opt', 'DeepseekV3']
+
+
+def _adapter(family, hf_model):
+    from lightcompress_amd.pipeline import MODEL_REGISTRY
+    return MODEL_REGISTRY[family](hf_model=hf_model, device='cpu')
+
+
+def _structure(model, block):
+    names = {id(m): n for n, m in block.named_modules()}
+    out = []
+    for sub in model.get_subsets_in_block(block):
+        d = {'layers': list(sub['layers']),
+             'prev_op': [None if p is None else names[id(p)] for p in sub['prev_op']],
+             'input': list(sub['input']), 'inspect': names[id(sub['inspect'])]}
+        for k in ('has_kwargs', 'is_mlp', 'do_trans', 'skip_rotate'):
+            if k in sub:
+                d[k] = sub[k]
+        out.append(d)
+    return out
+
+
+@pytest.mark.parametrize('family', FAMILIES)
+def test_adapter_contract_matches_reference(family):
+    from transformers import AutoModelForCausalLM
+    ref = json.loads((TM.HERE / f'subsets_{family}.json').read_text())
+    hf = AutoModelForCausalLM.from_pretrained(TM.MODEL_DIRS[family], local_files_only=True)
+    model = _adapter(family, hf)
+    assert model.block_name_prefix == ref['block_name_prefix']
+    assert model.has_bias() == ref['has_bias']
+    assert model.skip_layer_name() == ref['skip_layer_name']
+    assert len(model.get_blocks()) == len(ref['blocks'])
+    n_lin = 0
+    for block, rb in zip(model.get_blocks(), ref['blocks']):
+        names = {id(m): n for n, m in block.named_modules()}
+        assert _structure(model, block) == rb['subsets']
+        assert list(model.get_block_linears(block)) == rb['linears']
+        assert {k: names[id(v)] for k, v in model.get_extra_modules(block).items()} == rb['extra']
+        assert {k: names[id(v)] for k, v in
+                model.get_layernorms_in_block(block).items()} == rb['layernorms']
+        n_lin += len(rb['linears'])
+    assert n_lin == TM.N_LINEARS[family]
+
+
+def test_dsv3_per_expert_layout_same_forward():
+    """unfuse_experts: ExpertList of per-expert MLPs vs transformers' DeepseekV3Experts on the
+    same weights (fp32, so the comparison is not hidden by bf16 rounding)."""
+    from lightcompress_amd.deepseekv3 import ExpertList, unfuse_experts
+    fused = TM.build('DeepseekV3').float().eval()
+    ids = torch.randint(0, 128, (2, 64), generator=torch.Generator().manual_seed(3))
+    with torch.no_grad():
+        want = fused(input_ids=ids).logits
+        per = unfuse_experts(fused)
+        moe = per.model.layers[1].mlp
+        assert isinstance(moe.experts, ExpertList) and len(moe.experts) == 4
+        assert moe.experts[2].gate_proj.weight.shape == (128, 256)
+        got = per(input_ids=ids).logits
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)
+
+
+def test_dsv3_moe_subsets_cover_every_expert():
+    """deepseekv3.py:128-167: one MoE subset holding every expert's gate/up, the shared
+    expert's and the router, then one down_proj subset per expert and the shared down."""
+    from transformers import AutoModelForCausalLM
+    hf = AutoModelForCausalLM.from_pretrained(TM.MODEL_DIRS['DeepseekV3'], local_files_only=True)
+    model = _adapter('DeepseekV3', hf)
+    subs = model.get_subsets_in_block(model.get_blocks()[1])
+    moe = [s for s in subs if s['input'] == ['mlp']]
+    assert len(moe) == 1 and moe[0]['inspect'] is model.get_blocks()[1].mlp
+    assert len(moe[0]['layers']) == 2 * 4 + 2 + 1 and 'mlp.gate' in moe[0]['layers']
+    downs = [s for s in subs if list(s['layers'])[0].endswith('down_proj')]
+    assert len(downs) == 5
+    assert model.get_moe_gate(model.get_blocks()[1]) is not None
+    assert model.get_moe_gate(model.get_blocks()[0]) is None

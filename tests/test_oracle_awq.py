@@ -34,8 +34,8 @@ def test_search_scale_v1_matches_reference(subset, sym):
 @pytest.mark.parametrize('name', F.names('clip_'))
 def test_auto_clip_matches_reference(name):
     c = F.load(name)
-    sym, clip_sym, nst = c['meta'].tolist()
-    bmax, bmin = A.clip_layer(c['w'], c['x'], 4, bool(sym), 128, bool(clip_sym),
+    sym, clip_sym, nst, group = c['meta'].tolist()
+    bmax, bmin = A.clip_layer(c['w'], c['x'], 4, bool(sym), group, bool(clip_sym),
                               n_sample_token=nst)
     assert torch.equal(bmax.view(torch.int16), c['best_max'].view(torch.int16))
     assert torch.equal(bmin.view(torch.int16), c['best_min'].view(torch.int16))

@@ -25,84 +25,17 @@ import pytest
 import torch
 
 import fixtures as F
-from pipeline_configs import CONFIGS, MODEL_DIR
+import pipeline_helpers as P
 
 pytestmark = pytest.mark.gpu
 
 
+def compare(ref, got, n=14):
+    return P.compare(ref, got, n)
+
+
 def run_ours(name, dev, monkeypatch=None):
-    from lightcompress_amd.llama import Llama
-    from lightcompress_amd.pipeline import build_algo
-    from lightcompress_amd.utils import load_config
-    spec = CONFIGS[name]
-    ref = F.load(f'pipe_{name}')
-    diag = {}
-    if monkeypatch is not None and spec['quant']['method'] == 'GPTQ':
-        from lightcompress_amd.gptq import GPTQ
-        orig = GPTQ.layer_transform
-
-        def lt(self, layer, lname):
-            diag[f'H_b{self.block_idx}__{lname.replace(".", "__")}'] = \
-                self.layers_cache[lname]['acc'].H.detach().cpu().clone()
-            return orig(self, layer, lname)
-        orig_g = GPTQ.group_transform
-
-        def gt(self, grp):
-            for lname, _ in grp:
-                diag[f'H_b{self.block_idx}__{lname.replace(".", "__")}'] = \
-                    self.layers_cache[lname]['acc'].H.detach().cpu().clone()
-            return orig_g(self, grp)
-        monkeypatch.setattr(GPTQ, 'layer_transform', lt)
-        monkeypatch.setattr(GPTQ, 'group_transform', gt)
-    elif monkeypatch is not None and spec['quant']['method'] == 'Awq':
-        from lightcompress_amd.awq import Awq
-        orig = Awq.search_scale_subset
-
-        def ss(self, *a, **k):
-            best = orig(self, *a, **k)
-            n = len([d for d in diag if d.startswith(f'S_b{self.block_idx}')])
-            diag[f'S_b{self.block_idx}__{n}'] = best.detach().cpu().clone()
-            diag[f'L_b{self.block_idx}__{n}'] = torch.tensor(self.last_search['losses'],
-                                                             dtype=torch.float64)
-            return best
-        monkeypatch.setattr(Awq, 'search_scale_subset', ss)
-    cfg = {'model': {'type': 'Llama', 'path': str(MODEL_DIR), 'torch_dtype': 'bfloat16'},
-           'quant': dict(spec['quant'])}
-    if spec['calib']:
-        cfg['calib'] = dict(spec['calib'])
-    config = load_config(cfg)
-    model = Llama(config, device=dev)
-    calib = spec['calib']
-    if calib is None:
-        first = None
-    else:
-        ids = ref['ids']
-        batches = ([{'input_ids': ids}] if calib['bs'] == -1 else
-                   [{'input_ids': ids[i:i + 1]} for i in range(ids.shape[0])])
-        first = model.collect_first_block_input(batches)
-    algo = build_algo(model, config, first)
-    algo.run_block_loop()
-    algo.deploy('fake_quant')
-    got = {}
-    for bi, block in enumerate(model.get_blocks()):
-        for ln, lin in model.get_block_linears(block).items():
-            got[f'b{bi}__{ln.replace(".", "__")}'] = lin.weight.data.detach().cpu()
-            if hasattr(lin, 'buf_act_scales_0'):  # static act qparams
-                diag[f'a_b{bi}__{ln.replace(".", "__")}'] = lin.buf_act_scales_0.detach().cpu()
-    return ref, got, diag
-
-
-def compare(ref, got):
-    res = {}
-    for k, w in got.items():
-        r = ref[k]
-        assert r.shape == w.shape and r.dtype == w.dtype, k
-        eq = (r.view(torch.int16) == w.view(torch.int16)).float().mean().item()
-        res[k] = eq
-        print(f'{k:32s} equal {eq * 100:8.4f} %  max|dw| '
-              f'{(r.float() - w.float()).abs().max().item():.3e}')
-    assert len(res) == 14
-    return res
+    return P.run_ours(name, dev, monkeypatch)
 
 
 def test_rtn_pipeline_bit_exact(dev):
