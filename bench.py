@@ -21,6 +21,8 @@ Also in the line:
   (shard_tokens: partial Hessians summed, row-sharded column loop); roofline = the XᵀX kernel.
 * "e2e": MEASURED end-to-end wall-clock of the whole 32-block Llama-3-8B (AWQ and GPTQ):
   run_block_loop + deploy (vllm_quant / fake_quant) -- the reference's llmc_duration_time.
+* "l70b" (configs[3] shapes): one Llama-3-70B decoder block through the AWQ and the GPTQ
+  recipes (block_opt + deploy), per-block time and the projection-GEMM roofline at 70B shapes.
 * "fp8" (configs[4]): DeepSeek-V3 expert linears, block-fp8 -> per-tensor e4m3 deploy, and the
   block-scaled fp8 GEMM of their calibration forward.
 * roofline: the dominant kernel of the headline step (k_gemm16: the projection GEMMs of the
@@ -53,6 +55,8 @@ LLAMA3_8B = dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=
                  num_key_value_heads=8, head_dim=128, rope_theta=500000.0,
                  max_position_embeddings=8192, rms_norm_eps=1e-5, num_hidden_layers=32,
                  vocab_size=128256)
+LLAMA3_70B = dict(LLAMA3_8B, hidden_size=8192, intermediate_size=28672,
+                  num_attention_heads=64, num_key_value_heads=8, num_hidden_layers=80)
 N_LINEARS_PER_BLOCK = 7
 GEMM_FAMILY = ('lcq_gemm', 'lcq_gemm_silu_mul', 'lcq_gemm_sq_diff')
 
@@ -75,6 +79,8 @@ def parse():
     ap.add_argument('--gptq-samples', type=int, default=128)
     ap.add_argument('--gptq-seq-len', type=int, default=2048)
     ap.add_argument('--cpu-budget-s', type=float, default=20.0)
+    ap.add_argument('--no-l70b', action='store_true',
+                    help='skip the Llama-3-70B-shaped block leg (BASELINE configs[3])')
     return ap.parse_args()
 
 
@@ -478,6 +484,67 @@ def bench_e2e(args, rank, world, dev, which):
             'deploy': fmt, 'parallel_mode': mode}
 
 
+def bench_l70b(args, rank, world, dev):
+    """Llama-3-70B shapes (BASELINE.json configs[3]: hidden 8192, MLP 28672, 64q/8kv heads):
+    one decoder block through the AWQ headline config (128 x 512 tokens, vLLM int4 deploy) and
+    one through the GPTQ config (128 x 2048 tokens: the IC-28672 down_proj Hessian and column
+    loop), each timed as block_opt + deploy after one warm-up block of the same shapes. The
+    80-block model is 80 such blocks (per-block time x 80 / N GPUs under shard_blocks)."""
+    from transformers import LlamaConfig
+    from lightcompress_amd import _native
+    from lightcompress_amd.llama import Llama
+    from lightcompress_amd.module_utils import VllmRealQuantLinear
+    from lightcompress_amd.pipeline import build_algo
+    cfg = LlamaConfig(**LLAMA3_70B)
+    out = {}
+    for which in ('awq', 'gptq'):
+        model = Llama.random(cfg, num_layers=2, device=dev, seed=5000)
+        if which == 'awq':
+            seq, n = args.seq_len, args.n_samples
+            hidden = synthetic_hidden(n, seq, cfg.hidden_size, dev, 51)
+            calib = {'data': [hidden], 'kwargs': [model.rotary_kwargs(seq)]}
+            config = awq_config(seq, n)
+        else:
+            seq, n = args.gptq_seq_len, args.gptq_samples
+            hidden = synthetic_hidden(n, seq, cfg.hidden_size, dev, 53)
+            kw = model.rotary_kwargs(seq)
+            calib = {'data': [hidden[i:i + 1] for i in range(n)], 'kwargs': [kw] * n}
+            config = gptq_config(seq, n)
+        algo = build_algo(model, config, calib)
+        blocks = model.get_blocks()
+
+        def step(i):
+            algo.block_idx = i
+            algo.block_opt(blocks[i])
+            if which == 'awq':
+                model.replace_module_block(VllmRealQuantLinear, blocks[i], i,
+                                           algo.get_replacement_params('vllm_quant',
+                                                                       algo.w_only))
+        step(0)
+        timer = _native.KernelTimer()
+        sync_barrier(world)
+        t0 = time.perf_counter()
+        with timer:
+            step(1)
+        sync_barrier(world)
+        el = max_over_ranks(time.perf_counter() - t0, world, dev)
+        kern = timer.summary()
+        top = dict(list(kernel_table(kern, el).items())[:6])
+        out[which] = {'ms_per_block': round(el * 1e3, 1),
+                      'linears_per_s': round(N_LINEARS_PER_BLOCK * world / el, 3),
+                      'est_80_blocks_s': round(80 * el / world, 1),
+                      'calib': f'{n}x{seq} tokens' + (' (bs 1)' if which == 'gptq' else ''),
+                      'lcq_kernels': top}
+        if which == 'awq':
+            out[which]['roofline'] = gemm_roofline(kern, el)
+        del algo, model, hidden, calib
+        torch.cuda.empty_cache()
+    out['workload'] = ('Llama-3-70B decoder block (8192 / 28672, 64q/8kv): AWQ w4a16 g128 '
+                       '(configs[1] recipe) and GPTQ w4a16 g128 act-order (configs[2] recipe); '
+                       'per-GPU replicas at N > 1')
+    return out
+
+
 DSV3_EXPERT = dict(hidden=7168, moe_inter=2048, block=128)
 
 
@@ -638,6 +705,10 @@ def main():
     value = linears / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
+    l70b = None
+    if not args.no_l70b and args.algo == 'all':
+        l70b = bench_l70b(args, rank, world, dev)
+
     e2e = None
     if not args.no_e2e and args.algo == 'all':
         e2e = {'awq': bench_e2e(args, rank, world, dev, 'awq'),
@@ -665,6 +736,7 @@ def main():
                                        f'x {world} GPU(s); non-owner float forwards + '
                                        'owner broadcasts included')},
             'e2e': e2e,
+            'l70b': l70b,
             'gptq': gptq,
             'fp8': fp8,
             'roofline': roofline,
