@@ -241,28 +241,31 @@ class Awq(BaseBlockwiseQuantization):
     @torch.no_grad()
     def search_scale_subset(self, prev_op, layers_dict, input, inspect_module, is_gqa,
                             subset_kwargs):
-        if is_gqa:
-            raise NotImplementedError('GQA scale transfer is not on the device path')
         if len(input) != 1:
             raise NotImplementedError('multiple calibration tensors per subset')
         x = input[0]
         self._bs = x.shape[0] if self.awq_bs is None else self.awq_bs
         kwargs = subset_kwargs[0] if isinstance(subset_kwargs, list) else subset_kwargs
         layers = list(layers_dict.values())
-        v1 = getattr(self, 'trans_version', 'v2') == 'v1'
+        # is_gqa (do_gqa_trans, awq.py:88-108 / 40-46): x is v_proj's input; the scales live
+        # on v_proj's outputs (act scale of prev_op(x), v2 formula) and multiply o_proj's
+        # columns / divide x repeated over the query heads of each kv head
+        v1 = getattr(self, 'trans_version', 'v2') == 'v1' and not is_gqa
         w_max = self.get_weight_scale(layers_dict) if v1 else None
         orig_w = [fc.weight.data for fc in layers]
         qbufs = self._qbufs(orig_w)
         x_tmp = torch.empty_like(x)
-        x_mean = self.get_act_scale(x)
+        x_mean = self.get_act_scale(prev_op(x) if is_gqa else x)
         losses = ops.LossBuffer(self.n_grid, x.device)
         paths = self._fused_paths(inspect_module, layers, qbufs, orig_w, kwargs, x)
-        org_out = self._org_cached(x, inspect_module)
+        # the capture forward ran o_proj on the attention output, not on this x
+        org_out = None if is_gqa else self._org_cached(x, inspect_module)
         if org_out is None:  # recompute: through the fused kernels when the ratios use them
             org_out = (paths[0](x) if paths is not None
                        else self.inspect_module_forward(x, inspect_module, kwargs))
         fused = paths[1](org_out, losses) if paths is not None else None
-        all_scales = torch.empty((self.n_grid, x.shape[-1]), dtype=x.dtype, device=x.device)
+        all_scales = torch.empty((self.n_grid, x_mean.shape[-1]), dtype=x.dtype,
+                                 device=x.device)
         mine = range(self.n_grid)
         shard = self.parallel_mode() == 'shard_search'
         if shard:  # this rank's ratios; the others' loss slots stay 0 for the sum below
@@ -273,9 +276,10 @@ class Awq(BaseBlockwiseQuantization):
             for n in mine:
                 ratio = n * 1 / self.n_grid
                 s = self.get_scales(prev_op, x_mean, ratio, out=all_scales[n], w_max=w_max)
+                sw = self.repeat_gqa_scales(s) if is_gqa else s
                 for fc, buf in zip(layers, qbufs):
-                    fc.weight.data = self.fake_quantize_weight(fc, s, buf)
-                self.scaling_input(x, s, False, out=x_tmp)
+                    fc.weight.data = self.fake_quantize_weight(fc, sw, buf)
+                self.scaling_input(x, sw, False, out=x_tmp)
                 xin = x_tmp
                 if not self.w_only:
                     xin = self.aquantizer.fake_quant_act_dynamic(x_tmp)
@@ -331,14 +335,21 @@ class Awq(BaseBlockwiseQuantization):
         layers = list(layers_dict.values())
         if isinstance(prev_op[0], (nn.Linear, FakeQuantLinear)):
             of = prev_op[0].out_features
+            is_gqa = False
             if of not in (layers[0].in_features, 2 * layers[0].in_features,
                           3 * layers[0].in_features):
-                if self.has_gqa and self.do_gqa_trans:
-                    raise NotImplementedError('do_gqa_trans is not on the device path')
-                return  # 'Cannot apply scale. Do not transform this subset.'
+                if not (self.has_gqa and self.do_gqa_trans):
+                    return  # 'Cannot apply scale. Do not transform this subset.'
+                # awq.py:338-351: search on the input of the linear captured before this one
+                # (v_proj: the block's normalized hidden states)
+                is_gqa = True
+                keys = list(input_feat.keys())
+                input_name = keys[keys.index(input_name) - 1]
         elif not is_norm(prev_op[0]):
             return
+        else:
+            is_gqa = False
         scale = self.search_scale_subset(prev_op[0], layers_dict, input_feat[input_name],
-                                         inspect_module, False, subset_kwargs)
+                                         inspect_module, is_gqa, subset_kwargs)
         self.apply_scale(scale, prev_op, layers)
-        self.update_input_feat(scale, input_feat, layers_dict, False)
+        self.update_input_feat(scale, input_feat, layers_dict, is_gqa)

@@ -559,6 +559,19 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         elif fc1.out_features == fc2.in_features * 2:
             half = fc1.weight.data[fc1.weight.data.shape[0] // 2:]
             ops.scale_bcast(half, scales.to(half.dtype), 'div', axis=1, out=half)
+            if getattr(fc1, 'bias', None) is not None:
+                hb = fc1.bias.data[fc1.bias.data.shape[0] // 2:].view(1, -1)
+                ops.scale_bcast(hb, scales.to(hb.dtype), 'div', out=hb)
+        elif self.has_gqa and self.do_gqa_trans:
+            # :678-685: v_proj rows / s, o_proj columns * s repeated over the query heads of
+            # each kv head (an exact transfer through the attention's value path)
+            if getattr(fc1, 'bias', None) is not None:
+                ops.scale_bcast(fc1.bias.data.view(1, -1), scales.to(fc1.bias.dtype), 'div',
+                                out=fc1.bias.data.view(1, -1))
+            ops.scale_bcast(fc1.weight.data, scales.to(fc1.weight.dtype), 'div', axis=1,
+                            out=fc1.weight.data)
+            if fc1.out_features != fc2.in_features:
+                scales = self.repeat_gqa_scales(scales)
         else:
             raise NotImplementedError('fc-fc scaling for this shape is not on the device path')
         ops.scale_bcast(fc2.weight.data, scales.to(fc2.weight.dtype), 'mul', axis=0,
@@ -576,10 +589,17 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
             ops.scale_bcast(fc.weight.data, scales.to(fc.weight.dtype), 'mul', axis=0,
                             out=fc.weight.data)
 
+    def repeat_gqa_scales(self, scales):
+        """:591-595: per-kv-channel scales [kv_heads * head_dim] repeated for the query heads
+        of each kv head (repeat_interleave over heads), flattened to [heads * head_dim]."""
+        s = scales.reshape(1, self.num_key_value_heads, self.head_dim)
+        return torch.repeat_interleave(s, dim=1, repeats=self.num_key_value_groups).reshape(-1)
+
     @torch.no_grad()
     def scaling_input(self, x, scales, is_gqa=False, out=None):
+        """:877-890: x / s (GQA: s repeated over the query heads)."""
         if is_gqa:
-            raise NotImplementedError('GQA scale transfer (do_gqa_trans) is not on the device path')
+            scales = self.repeat_gqa_scales(scales)
         return ops.scale_bcast(x, scales.to(x.dtype), 'div', out=out)
 
     @torch.no_grad()

@@ -810,46 +810,10 @@ __device__ __forceinline__ void ktile16(v4f (&acc)[8][8], v8s (&bf)[8][2], v8s (
   }
 }
 
+// Epilogue of the 4-wave 16x16x32 kernels (swapped layout, see k_gemm16).
 template <int DT, int EPI>
-__global__ void __launch_bounds__(256, 1) k_gemm16(Args a) {
-  constexpr bool FP16 = DT == LCQ_F16;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  int tm, tn;
-  if (!slot_tile(a, wgid, tm, tn)) return;
-  const int64_t nk = a.k / SKT;
-  Stage4 st;
-  make_stage16<EPI>(a, tm, tn, w, lane, st);
-
-  v4f acc[8][8];
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-    for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
-  v8s af[2][2][2], bf[8][2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) load_piece(st, lds, 0, 0, w, i);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) load_piece(st, lds, 1, nk > 1 ? SKT * 2 : 0, w, i);
-  wait_barrier<22>();
-#pragma unroll
-  for (int n = 0; n < 8; ++n)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) bf[n][k] = read_frag(lds + TILE_B, wc * 8 + n, k, lane);
-#pragma unroll
-  for (int m2 = 0; m2 < 2; ++m2)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) af[0][m2][k] = read_frag(lds, wr * 8 + m2, k, lane);
-  asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
-
-  for (int64_t t = 0; t < nk; ++t) ktile16<FP16>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-
+__device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, int tn, int w,
+                                      int wr, int wc, int lane, int tid, char* lds) {
   // epilogue (swapped 16x16 layout): acc[m][n][j] = token tm*256 + wr*128 + m*16 + fr, tile
   // column wc*128 + n*16 + fq*4 + j (EPI_SILU: n < 4 gate, n + 4 up of output column
   // tn*128 + wc*64 + n*16 + fq*4 + j). Segment, bias and row pointers are resolved once per
@@ -964,6 +928,209 @@ __global__ void __launch_bounds__(256, 1) k_gemm16(Args a) {
       if (tid < 4) a.part[((int64_t)tm * a.n_nt + tn) * 4 + tid] = red[tid];
     }
   }
+}
+
+template <int DT, int EPI>
+__global__ void __launch_bounds__(256, 1) k_gemm16(Args a) {
+  constexpr bool FP16 = DT == LCQ_F16;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  int tm, tn;
+  if (!slot_tile(a, wgid, tm, tn)) return;
+  const int64_t nk = a.k / SKT;
+  Stage4 st;
+  make_stage16<EPI>(a, tm, tn, w, lane, st);
+
+  v4f acc[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s af[2][2][2], bf[8][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_piece(st, lds, 0, 0, w, i);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_piece(st, lds, 1, nk > 1 ? SKT * 2 : 0, w, i);
+  wait_barrier<22>();
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) bf[n][k] = read_frag(lds + TILE_B, wc * 8 + n, k, lane);
+#pragma unroll
+  for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) af[0][m2][k] = read_frag(lds, wr * 8 + m2, k, lane);
+  asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
+
+  for (int64_t t = 0; t < nk; ++t) ktile16<FP16>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  epi16<DT, EPI>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
+}
+
+// ---------------------------------------------------------------------------------------
+// Ring-buffer form of k_gemm16 (LCQ_GEMM_KERNEL=r): K-tile 32, NBR = 4 LDS buffers of 32 KB
+// (A 16 KB + B 16 KB, sixteen 16-row x 32-k st_16x32 subtiles each), ONE barrier per K-tile.
+// Iteration t: barrier (tile t+1 landed everywhere: counted vmcnt(16) = the 2 younger tiles'
+// 8 pieces each; every wave is past iteration t-1, so tile t's buffer -- its fragments were
+// read during t-1 -- is free), then 64 MFMAs on tile t's fragments (register set t & 1) with
+// the 16 fragment reads of tile t+1 (other set) and the 8 LDS-DMA pieces of tile t+4 (into
+// tile t's buffer) interleaved. A load is consumed three iterations after issue.
+// ---------------------------------------------------------------------------------------
+constexpr int SKR = 32;                 // K-tile
+constexpr int NBR = 4;                  // ring depth (5: measured no faster)
+constexpr int TILE_R = ST * SKR * 2;    // 16 KB: one operand tile
+constexpr int BUFR = 2 * TILE_R;        // A + B
+
+struct StageR {
+  __amdgpu_buffer_rsrc_t ra;
+  __amdgpu_buffer_rsrc_t rb[2];
+  uint32_t aoff[4];
+  uint32_t boff[4];
+  int bsel;
+};
+
+// piece j (0..3) of wave w = subtile rb = w + 4 j of the A / B tile image
+template <int EPI>
+__device__ __forceinline__ void make_stage_r(const Args& a, int tm, int tn, int w, int lane,
+                                             StageR& st) {
+  const int64_t arow0 = (int64_t)tm * ST;
+  st.ra = panel_rsrc(a.a + arow0 * a.lda);
+  int64_t brow0 = 0, blast = 0;
+  if constexpr (EPI == EPI_SILU) {
+    st.rb[0] = panel_rsrc(a.b[0]);
+    st.rb[1] = panel_rsrc(a.b[1]);
+    blast = a.n - 1;
+    brow0 = (int64_t)tn * 128;
+  } else {
+    const int64_t row0 = (int64_t)tn * ST;
+    int s = 0;
+    int64_t segbase = 0;
+    if (a.nseg > 1 && row0 >= a.bend[0]) { s = 1; segbase = a.bend[0]; }
+    if (a.nseg > 2 && row0 >= a.bend[1]) { s = 2; segbase = a.bend[1]; }
+    brow0 = row0 - segbase;
+    blast = a.bend[s] - segbase - 1;
+    st.rb[0] = st.rb[1] = panel_rsrc(a.b[s] + brow0 * a.ldb);
+  }
+  st.bsel = 0;
+  const int r = lane >> 2;
+  const int pc = (lane & 3) * 16;
+  const int lc = pc ^ (((r >> 3) & 1) << 5);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int rb = w + 4 * j;
+    const int row = rb * 16 + r;
+    int64_t ar = row;
+    if (arow0 + ar > a.m - 1) ar = a.m - 1 - arow0;
+    st.aoff[j] = (uint32_t)(ar * a.lda * 2 + lc);
+    int64_t br;
+    if constexpr (EPI == EPI_SILU) {
+      if (((rb * 16) & 127) >= 64) st.bsel |= 1 << j;  // uniform: whole 16-row subtile
+      br = brow0 + (row >> 7) * 64 + (row & 63);
+      if (br > blast) br = blast;
+    } else {
+      br = row;
+      if (brow0 + br > blast) br = blast - brow0;
+    }
+    st.boff[j] = (uint32_t)(br * a.ldb * 2 + lc);
+  }
+}
+
+// piece idx (0..7) of one K-tile: 0..3 B subtiles, 4..7 A subtiles
+__device__ __forceinline__ void load_r(const StageR& st, char* lds, int buf, int kofs, int w,
+                                       int idx) {
+  char* dA = lds + buf * BUFR;
+  if (idx < 4) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(((st.bsel >> idx) & 1) ? st.rb[1] : st.rb[0],
+                                             (lds_void_t*)(dA + TILE_R + (w + 4 * idx) * 1024),
+                                             16, st.boff[idx], kofs, 0, 0);
+  } else {
+    const int j = idx - 4;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(st.ra, (lds_void_t*)(dA + (w + 4 * j) * 1024), 16,
+                                             st.aoff[j], kofs, 0, 0);
+  }
+}
+
+// 16x32 fragment of subtile rb (st_16x32 swizzle)
+__device__ __forceinline__ v8s frag_r(const char* tile, int rb, int lane) {
+  const int r = lane & 15;
+  const int lc = (lane >> 4) * 16;
+  const int pc = lc ^ (((r >> 3) & 1) << 5);
+  return *reinterpret_cast<const v8s*>(tile + rb * 1024 + r * 64 + pc);
+}
+
+template <bool FP16, int P>
+__device__ __forceinline__ void ring_iter(v4f (&acc)[8][8], v8s (&af)[2][8], v8s (&bf)[2][8],
+                                          const StageR& st, char* lds, int64_t t, int64_t nk,
+                                          int w, int wr, int wc, int lane) {
+  wait_barrier<8 * (NBR - 2)>();
+  const int64_t tl = t + NBR < nk ? t + NBR : nk - 1;  // past the end: re-fetch the last tile
+  const int kofs = (int)(tl * (SKR * 2));
+  const int lbuf = (int)(t % NBR);
+  const char* nA = lds + ((t + 1) % NBR) * BUFR;
+  const char* nB = nA + TILE_R;
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const int m = i >> 3, n = i & 7;
+    mfma16a<FP16>(acc[m][n], bf[P][n], af[P][m]);
+    if ((i & 3) == 1) {
+      const int q = i >> 2;
+      if (q < 8) af[P ^ 1][q] = frag_r(nA, wr * 8 + q, lane);
+      else bf[P ^ 1][q - 8] = frag_r(nB, wc * 8 + q - 8, lane);
+    }
+    if ((i & 7) == 3) load_r(st, lds, lbuf, kofs, w, i >> 3);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int DT, int EPI>
+__global__ void __launch_bounds__(256, 1) k_gemm16r(Args a) {
+  constexpr bool FP16 = DT == LCQ_F16;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  int tm, tn;
+  if (!slot_tile(a, wgid, tm, tn)) return;
+  const int64_t nk = a.k / SKR;  // even: K % 64 == 0
+  StageR st;
+  make_stage_r<EPI>(a, tm, tn, w, lane, st);
+
+  v4f acc[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s af[2][8], bf[2][8];
+#pragma unroll
+  for (int j = 0; j < NBR; ++j) {
+    const int kofs = (int)((j < nk ? j : nk - 1) * (SKR * 2));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) load_r(st, lds, j, kofs, w, i);
+  }
+  wait_barrier<8 * (NBR - 1)>();  // tile 0 landed
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    af[0][q] = frag_r(lds, wr * 8 + q, lane);
+    bf[0][q] = frag_r(lds + TILE_R, wc * 8 + q, lane);
+  }
+  asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
+
+  for (int64_t t = 0; t < nk; t += 2) {
+    ring_iter<FP16, 0>(acc, af, bf, st, lds, t, nk, w, wr, wc, lane);
+    ring_iter<FP16, 1>(acc, af, bf, st, lds, t + 1, nk, w, wr, wc, lane);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  __syncthreads();  // every wave's DMA landed before the epilogue may reuse LDS
+  epi16<DT, EPI>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1315,6 +1482,10 @@ static int launch(Args& a, hipStream_t st) {
     (void)hipFuncSetAttribute((const void*)k_gemm4w<DT, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
     hipLaunchKernelGGL((k_gemm4w<DT, EPI>), dim3((unsigned)a.nslots), 256, 2 * BUF4, st, a);
+  } else if (sel && sel[0] == 'r') {  // ring-buffer probe (K-tile 32, 4 buffers)
+    (void)hipFuncSetAttribute((const void*)k_gemm16r<DT, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, NBR * BUFR);
+    hipLaunchKernelGGL((k_gemm16r<DT, EPI>), dim3((unsigned)a.nslots), 256, NBR * BUFR, st, a);
   } else if (!(sel && sel[0] == 'p') || a.k < 2 * SKT) {  // one tile per workgroup
     (void)hipFuncSetAttribute((const void*)k_gemm16<DT, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);

@@ -48,10 +48,6 @@ class GPTQ(BaseBlockwiseQuantization):
             self.n_outs = sp['n_outs']
             self.static_groups = False
             self.actorder = False
-        if (self.wquantizer.calib_algo == 'mse' and self.wquantizer.granularity == 'per_group'
-                and not self.static_groups):
-            raise NotImplementedError('GPTQ per_group column qparams use min/max on the device '
-                                      'path (calib_algo mse: per_channel or static_groups)')
         if self.blocksize != gptq_core.BLOCK:
             raise NotImplementedError('device GPTQ uses blocksize 128')
         self.need_perm = (self.wquantizer.granularity == 'per_group' and not self.static_groups

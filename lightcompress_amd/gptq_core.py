@@ -257,7 +257,7 @@ def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
 def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
                 qmin: int, qmax: int, fixed=None, losses: bool = False,
                 superblock: int | None = None, col_group: torch.Tensor | None = None,
-                ncols_q: int | None = None):
+                ncols_q: int | None = None, col_qparams=None):
     """Blocked OBS loop (gptq.py:198-244) on permuted fp32 W, in place.
 
     Per 128-column block: the HIP kernel runs the in-block sequential loop (bit-exact rank-1
@@ -267,11 +267,29 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     superblock's stacked errors in ONE K = superblock update (same terms, grouped differently
     -> T2; every element still has a fixed k order, so row sharding stays bit-identical).
     fp32 MFMA kernel (``lcq_gptq_trailing``). ``ncols_q`` (OWQ): only the first ncols_q
-    columns are quantized; every block's error still updates all later columns."""
+    columns are quantized; every block's error still updates all later columns.
+
+    ``col_qparams`` (per_group with a searched range, calib_algo mse): a function of a
+    [rows, width] fp32 column slice returning its per-row (scales, zeros | None). The reference
+    computes a group's qparams when the loop reaches its first column, from the global W,
+    whose columns of the current block are not updated inside the block (gptq.py:213-222,
+    search_column_qparams :359-366): so every group starting in a block gets its qparams from
+    the block-start W, here before the block kernel, which then quantizes with them."""
     rows, cols = W.shape
     dev = W.device
     U = U.contiguous()
     ncq = cols if ncols_q is None else int(ncols_q)
+    searched = col_qparams is not None
+    if searched:
+        if group is None or col_group is not None or not (BLOCK % group == 0
+                                                          or group % BLOCK == 0):
+            raise NotImplementedError('searched column qparams need per_group with a group '
+                                      'size dividing or divisible by 128')
+        ngs = -(-ncq // group)
+        s_srch = torch.empty((rows, ngs), dtype=torch.float32, device=dev)
+        z_srch = None if sym else torch.empty((rows, ngs), dtype=torch.float32, device=dev)
+        col_group = (torch.arange(cols, device=dev) // group).clamp(max=ngs - 1).to(
+            torch.int32).contiguous()
     static = col_group is not None  # static_groups: fixed qparams of the original groups
     ng = 0 if (group is None or static) else -(-ncq // group)
     s_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng else None
@@ -282,7 +300,9 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     errT = torch.empty((SB, rows), dtype=torch.float32, device=dev)  # k-major stacked Err1
     L = torch.zeros_like(W) if losses else None
     s_in = z_in = None
-    if group is None or static:
+    if searched:
+        s_in, z_in = s_srch, z_srch
+    elif group is None or static:
         s_in = fixed[0].reshape(-1).float().contiguous()
         z_in = None if sym else fixed[1].reshape(-1).float().contiguous()
     for sb0 in range(0, ncq, SB):
@@ -291,6 +311,12 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
             i2 = min(i1 + BLOCK, sb1)
             cnt = i2 - i1
             e = errT[i1 - sb0:]
+            if searched:  # groups starting in this block, from the block-start columns
+                for g0 in range(-(-i1 // group) * group, i2, group):
+                    sg, zg = col_qparams(W[:, g0:min(g0 + group, ncq)])
+                    s_srch[:, g0 // group] = sg.reshape(-1)
+                    if z_srch is not None:
+                        z_srch[:, g0 // group] = zg.reshape(-1)
             if static:
                 ops.gptq_block_cols(W, i1, cnt, U, qmin, qmax, s_in, z_in, col_group, e, L)
             else:
@@ -300,6 +326,8 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
                 ops.gptq_trailing(W, i1, cnt, i2, e, U, c2=sb1)
         if sb1 < cols:    # far columns: the whole superblock's errors at once
             ops.gptq_trailing(W, sb0, sb1 - sb0, sb1, errT, U, c2=cols)
+    if searched:
+        return s_srch, z_srch, L
     return s_out, z_out, L
 
 
@@ -307,6 +335,8 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
 def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder=True,
                    percdamp=0.01, fixed=None, losses=False, shard_rows=False, prepared=None,
                    static_groups=False, owq_nout=0):
+    """(calib_algo mse per_group: the column qparams are searched in the loop, see
+    column_loop's col_qparams.)"""
     """Full GPTQ transform of one linear. Returns dict(weight fp32 (original column order),
     scales / zeros [rows*ng, 1] fp32 (merge_qparams order, permuted groups), perm, invperm,
     loss). ``prepared`` = prepare_hessian(...) output shared by linears with the same input
@@ -316,6 +346,15 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
     group = wquantizer.group_size if wquantizer.granularity == 'per_group' else None
     if group is not None and not static_groups and group not in (32, 64, 128):
         raise NotImplementedError('device GPTQ supports group_size 32/64/128')
+    col_qparams = None
+    if (group is not None and not static_groups
+            and getattr(wquantizer, 'calib_algo', 'minmax') == 'mse'):
+        if owq_nout:
+            raise NotImplementedError('OWQ with calib_algo mse')
+
+        def col_qparams(cols_view):
+            _, _, sg, zg = wquantizer._mse(cols_view.contiguous())
+            return sg, zg
     if owq_nout and group is None:
         raise NotImplementedError('OWQ supports per_group weights on the device path')
     if prepared is None:
@@ -340,14 +379,14 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
         fx = None if fixed is None else tuple(
             None if f is None else f.reshape(Wp.shape[0], -1)[r0:r1] for f in fixed)
         s, z, L = column_loop(Wl, U, bit, sym, group, qmin, qmax, fixed=fx, losses=losses,
-                              col_group=col_group, ncols_q=ncq)
+                              col_group=col_group, ncols_q=ncq, col_qparams=col_qparams)
         Wp = P.gather_rows(Wl, Wp.shape[0])
         s = None if s is None else P.gather_rows(s, Wp.shape[0])
         z = None if z is None else P.gather_rows(z, Wp.shape[0])
         L = None if L is None else P.gather_rows(L, Wp.shape[0])
     else:
         s, z, L = column_loop(Wp, U, bit, sym, group, qmin, qmax, fixed=fixed, losses=losses,
-                              col_group=col_group, ncols_q=ncq)
+                              col_group=col_group, ncols_q=ncq, col_qparams=col_qparams)
     invperm = torch.argsort(perm) if perm is not None else None
     weight = Wp[:, invperm] if invperm is not None else Wp
     return dict(weight=weight, scales=None if s is None else s.reshape(-1, 1),

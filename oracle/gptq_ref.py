@@ -75,12 +75,15 @@ def prepare_owq(W: torch.Tensor, H: torch.Tensor, nout: int, percdamp: float):
 
 
 def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
-                blocksize: int = 128, fixed=None, static=None, ncols_q: int | None = None):
+                blocksize: int = 128, fixed=None, static=None, ncols_q: int | None = None,
+                mse: bool = False):
     """gptq.py:198-244 on permuted fp32 W (modified in place to the compensated weights).
 
     group=None with fixed=(scale[rows,1], zero) -> per-channel fixed qparams.
     static=(scales [rows, ng], zeros | None, perm | None): static_groups (gptq.py:224-227,
     split_qparams :333-341) -- permuted column j uses original group perm[j] // group.
+    mse=True: calib_algo mse, the group range from get_mse_range (search_column_qparams
+    :359-366 -> get_tensor_qparams) of the group's columns of the global W.
     Returns (tmp, Losses, scales [rows, ng], zeros [rows, ng] | None)."""
     qmin, qmax = Q.int_range(bit, sym)
     rows, cols = W.shape
@@ -102,7 +105,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
             elif group is not None and (i1 + i) % group == 0:
                 ct = W[:, i1 + i:min(i1 + i + group, ncq)]
                 t = Q.group_view(ct, 'per_group', group)
-                mn, mx = Q.minmax(t)
+                mn, mx = Q.mse_range(t, bit, sym) if mse else Q.minmax(t)
                 s, z = Q.qparams(mn, mx, qmin, qmax, sym)
                 qp = (s, z)
                 groups[(i1 + i) // group] = qp
@@ -128,11 +131,11 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
 
 
 def quantize_layer(W: torch.Tensor, H: torch.Tensor, bit=4, sym=False, group=128,
-                   actorder=True, percdamp=0.01, blocksize=128):
+                   actorder=True, percdamp=0.01, blocksize=128, mse=False):
     """Whole GPTQ layer transform. Returns dict(weight (fp32, original column order),
     scales/zeros [rows*ng, 1] (merge_qparams order), perm, invperm, U, loss)."""
     Wp, U, perm = prepare(W, H, actorder, percdamp)
-    tmp, Losses, s, z = column_loop(Wp, U, bit, sym, group, blocksize)
+    tmp, Losses, s, z = column_loop(Wp, U, bit, sym, group, blocksize, mse=mse)
     invperm = torch.argsort(perm) if perm is not None else None
     weight = tmp[:, invperm] if invperm is not None else tmp
     return dict(weight=weight, scales=s.reshape(-1, 1), zeros=None if z is None else z.reshape(-1, 1),

@@ -132,13 +132,21 @@ def gen_gptq():
     q = R.quant_module()
     import llmc.compression.quantization.gptq as gm
     cases = [
-        # name, oc, ic, bit, sym, group, actorder, dead_cols
+        # name, oc, ic, bit, sym, group, actorder, dead_cols[, calib_algo]
         ('int4_asym_g128_act', 192, 512, 4, False, 128, True, False),
         ('int4_sym_g128_noact', 128, 384, 4, True, 128, False, False),
         ('int4_asym_g64_act_dead', 128, 256, 4, False, 64, True, True),
         ('int8_sym_g128_act', 64, 256, 8, True, 128, True, False),
+        # calib_algo mse: group ranges searched in the loop (gptq_w_only.yml's commented
+        # option); prefix gptqmse_
+        ('mse:int4_asym_g128_act', 192, 512, 4, False, 128, True, False),
+        ('mse:int4_sym_g64_act', 128, 256, 4, True, 64, True, False),
+        ('mse:int3_asym_g128_noact', 64, 384, 3, False, 128, False, False),
     ]
     for i, (name, oc, ic, bit, sym, gs, act, dead) in enumerate(cases):
+        calib = 'minmax'
+        if name.startswith('mse:'):
+            calib, name = 'mse', name[4:]
         torch.manual_seed(1000 + i)
         layer = nn.Linear(ic, oc, bias=False)
         layer.weight.data = weights(oc, ic, torch.bfloat16, 200 + i, edge=False)
@@ -148,7 +156,8 @@ def gen_gptq():
                 x[..., 5] = 0
                 x[..., 77] = 0
         obj = gm.GPTQ.__new__(gm.GPTQ)
-        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_group', group_size=gs)
+        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_group', group_size=gs,
+                                            calib_algo=calib)
         obj.dev = torch.device('cpu')
         obj.model_dtype = torch.bfloat16
         obj.owq, obj.actorder, obj.static_groups = False, act, False
@@ -185,7 +194,7 @@ def gen_gptq():
         if not act:
             codes, s_rq, z_rq = obj.w_q(layer, obj.wquantizer)
             out.update(codes=codes, scales_rq=s_rq, zeros_rq=z_rq)
-        F.save(f'gptq_{name}', **out)
+        F.save(f'gptq{"mse" if calib == "mse" else ""}_{name}', **out)
     print('gptq fixtures written')
 
 
@@ -415,7 +424,8 @@ def gen_gptq_static():
                 x[..., 3] = 0
                 x[..., 101] = 0
         obj = gm.GPTQ.__new__(gm.GPTQ)
-        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_group', group_size=gs)
+        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_group', group_size=gs,
+                                            calib_algo=calib)
         obj.dev = torch.device('cpu')
         obj.model_dtype = torch.bfloat16
         obj.owq, obj.actorder, obj.static_groups = False, act, True
@@ -593,7 +603,8 @@ def gen_gptq_owq():
             for x in xs:
                 x[..., 9] = 0
         obj = gm.GPTQ.__new__(gm.GPTQ)
-        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_group', group_size=gs)
+        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_group', group_size=gs,
+                                            calib_algo=calib)
         obj.dev = torch.device('cpu')
         obj.model_dtype = torch.bfloat16
         obj.owq, obj.actorder, obj.static_groups = True, False, False

@@ -28,6 +28,14 @@ CONFIGS = {
                       'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True,
                                   'clip_sym': True}},
             'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}},
+    # do_gqa_trans (awq.py:338-351, base_blockwise_quantization.py:591-595, 678-685): the
+    # o_proj subset is searched on v_proj's input and its scales move into v_proj's rows
+    'awq_gqa': {'quant': {'method': 'Awq',
+                          'weight': {'bit': 4, 'symmetric': True, 'granularity': 'per_group',
+                                     'group_size': 128},
+                          'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True,
+                                      'clip_sym': True, 'do_gqa_trans': True}},
+                'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}},
     'awq_qout_asym': {'quant': {'method': 'Awq',
                                 'weight': {'bit': 4, 'symmetric': False,
                                            'granularity': 'per_group', 'group_size': 128},

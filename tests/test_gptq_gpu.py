@@ -120,6 +120,67 @@ def test_column_loop_given_reference_U(dev, name):
     assert agree >= 0.999, agree
 
 
+@pytest.mark.parametrize('name', F.names('gptqmse_'))
+def test_mse_column_loop_given_reference_U(dev, name):
+    """calib_algo mse in the loop (gptq.py:213-222): every group's range searched on the
+    block-start columns (lcq_mse_qparams) and quantized by the block kernel with those
+    qparams; given the reference's U only the trailing GEMM's fp32 order differs (T2)."""
+    from lightcompress_amd import gptq_core
+    from lightcompress_amd.quant import IntegerQuantizer
+    c = F.load(name)
+    bit, sym, gs, act, oc, ic = _meta(c)
+    qmin, qmax = Q.int_range(bit, sym)
+    wq = IntegerQuantizer(bit, sym, 'per_group', group_size=gs, calib_algo='mse')
+    W = c['w'].float().clone()
+    if act:
+        W = W[:, c['perm']]
+    Wd = W.contiguous().to(dev)
+
+    def col_qparams(v):
+        _, _, sg, zg = wq._mse(v.contiguous())
+        return sg, zg
+    s, z, _ = gptq_core.column_loop(Wd, c['U'].to(dev), bit, sym, gs, int(qmin), int(qmax),
+                                    col_qparams=col_qparams)
+    w = Wd.cpu()
+    if act:
+        w = w[:, torch.argsort(c['perm'])]
+    torch.testing.assert_close(w, c['weight'], rtol=1e-4, atol=1e-6)
+    same_s = (s.cpu().reshape(-1, 1) == c['scales']).float().mean().item()
+    assert same_s >= 0.99, same_s   # a range search may flip where the columns moved in ulps
+    perm = c['perm'] if act else None
+
+    def codes(wt):
+        wp = wt[:, perm] if perm is not None else wt
+        zz = c['zeros'] if not sym else torch.tensor(0.0)
+        return Q.quant(Q.group_view(wp, 'per_group', gs), c['scales'], zz, qmin, qmax)
+    agree = (codes(w) == codes(c['weight'])).float().mean().item()
+    assert agree >= 0.999, agree
+
+
+@pytest.mark.parametrize('name', F.names('gptqmse_'))
+def test_mse_plugin_layer_vs_reference(dev, name):
+    """quantize_layer with an mse quantizer (the GPTQ plugin's path): deployed fake-quant
+    weights >= 99.9 % bit-equal to the reference's."""
+    from lightcompress_amd import gptq_core
+    from lightcompress_amd.gptq_core import HessianAccumulator
+    from lightcompress_amd.quant import IntegerQuantizer
+    c = F.load(name)
+    bit, sym, gs, act, oc, ic = _meta(c)
+    wq = IntegerQuantizer(bit, sym, 'per_group', group_size=gs, calib_algo='mse')
+    acc = HessianAccumulator(ic, dev)
+    for x in c['x']:
+        acc.add_batch(x.unsqueeze(0).to(dev))
+    r = gptq_core.quantize_layer(c['w'].to(dev), acc.H, wq, actorder=act, percdamp=0.01)
+    perm = r['perm']
+    wp = r['weight'][:, perm] if perm is not None else r['weight']
+    args = {'scales': r['scales'], 'zeros': r['zeros'], 'qmax': wq.qmax, 'qmin': wq.qmin}
+    fq = wq.fake_quant_weight_static(wp.contiguous(), args).to(torch.bfloat16)
+    if perm is not None:
+        fq = fq[:, r['invperm']]
+    same = (fq.cpu() == c['fq']).float().mean().item()
+    assert same >= 0.999, same
+
+
 @pytest.mark.parametrize('name', F.names('gptq_'))
 def test_layer_end_to_end_vs_reference(dev, name):
     """Full device transform (MFMA Hessian + rocSOLVER Cholesky + HIP loop) vs reference:

@@ -130,3 +130,35 @@ def test_owq_layer_matches_reference(name):
     fq = G.deploy_fake_owq(c['weight'], c['scales'], c.get('zeros'), c['perm'],
                            torch.argsort(c['perm']), ic - nout, bit, sym, gs, torch.bfloat16)
     assert torch.equal(fq, c['fq'])
+
+
+MSE_CASES = F.names('gptqmse_')
+
+
+@pytest.mark.parametrize('name', MSE_CASES)
+def test_mse_column_loop_exact_given_reference_U(name):
+    """calib_algo mse: the group ranges searched from the global W at each group's first
+    column (search_column_qparams) -- oracle column loop bit-exact given the reference's U."""
+    c = F.load(name)
+    bit, sym, gs, act, oc, ic = _meta(c)
+    W = c['w'].float().clone()
+    if act:
+        W = W[:, c['perm']]
+    tmp, _, s, z = G.column_loop(W, c['U'], bit, sym, gs, mse=True)
+    if act:
+        tmp = tmp[:, torch.argsort(c['perm'])]
+    assert torch.equal(tmp, c['weight'])
+    assert torch.equal(s.reshape(-1, 1), c['scales'])
+    if not sym:
+        assert torch.equal(z.reshape(-1, 1), c['zeros'])
+
+
+@pytest.mark.parametrize('name', MSE_CASES)
+def test_mse_layer_matches_reference(name):
+    c = F.load(name)
+    bit, sym, gs, act, oc, ic = _meta(c)
+    r = G.quantize_layer(c['w'], c['H'], bit, sym, gs, act, mse=True)
+    fq = G.deploy_fake(r['weight'], r['scales'], r['zeros'], r['perm'], r['invperm'], bit, sym,
+                       gs, torch.bfloat16)
+    agree = (fq == c['fq']).float().mean().item()
+    assert agree > 0.999, agree

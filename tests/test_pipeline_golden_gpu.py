@@ -43,11 +43,17 @@ def test_rtn_pipeline_bit_exact(dev):
     assert all(eq == 1.0 for eq in compare(ref, got).values())
 
 
-@pytest.mark.parametrize('name', ['awq', 'awq_qout_asym'])
+@pytest.mark.parametrize('name', ['awq', 'awq_qout_asym', 'awq_gqa'])
 def test_awq_pipeline_vs_reference(dev, name, monkeypatch):
+    """awq_gqa (do_gqa_trans): the o_proj subset is searched too (on v_proj's input, scales
+    repeated over the query heads) and its scales divide v_proj's rows, so v_proj is no longer
+    a first-subset-only linear."""
+    gqa = name == 'awq_gqa'
     ref, got, diag = run_ours(name, dev, monkeypatch)
     res = compare(ref, got)
-    for k in ('b0__self_attn__q_proj', 'b0__self_attn__k_proj', 'b0__self_attn__v_proj'):
+    first = ('b0__self_attn__q_proj', 'b0__self_attn__k_proj') + (
+        () if gqa else ('b0__self_attn__v_proj',))
+    for k in first:
         assert res[k] == 1.0, k
     rdiag = F.load(f'pipe_{name}_diag')
     lkeys = sorted(k for k in rdiag if k.startswith('L_'))
@@ -68,8 +74,11 @@ def test_awq_pipeline_vs_reference(dev, name, monkeypatch):
             moved.add(k)
     # deployed weights: >= 95 % bit-equal wherever the same ratio was chosen (the rest are
     # clip choices downstream of last-bit input differences)
-    subset_of = {'self_attn__q_proj': 0, 'self_attn__k_proj': 0, 'self_attn__v_proj': 0,
-                 'mlp__gate_proj': 1, 'mlp__up_proj': 1, 'mlp__down_proj': 2}
+    subset_of = ({'self_attn__q_proj': 0, 'self_attn__k_proj': 0, 'self_attn__v_proj': 1,
+                  'self_attn__o_proj': 1, 'mlp__gate_proj': 2, 'mlp__up_proj': 2,
+                  'mlp__down_proj': 3} if gqa else
+                 {'self_attn__q_proj': 0, 'self_attn__k_proj': 0, 'self_attn__v_proj': 0,
+                  'mlp__gate_proj': 1, 'mlp__up_proj': 1, 'mlp__down_proj': 2})
     for k, eq in res.items():
         b, lin = k.split('__', 1)
         sub = subset_of.get(lin)
