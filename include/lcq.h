@@ -240,11 +240,13 @@ int lcq_sq_diff_mean(const void* a, const void* b, int dtype, int64_t n, void* w
  * w [oc, ic], x [T, ic] (already token-subsampled), group 32 / 64 / 128 / 256, nsteps shrink
  * steps with factors[nsteps] = fp32(1 - i/n_grid) (device array). best_max / best_min
  * [oc, ic/group] in dtype. Exact emulation of the reference's dtype products and sums (VALU,
- * not MFMA). */
+ * not MFMA). mse_steps > 0: the weight quantizer's calib_algo is mse -- every step's fake
+ * quant searches its range (quant.py:145-203) with mse_p[mse_steps] = fp32(1 - i/mse_grid)
+ * (device array) and the norm (2.4); mse_steps = 0: min/max qparams. */
 int lcq_auto_clip_search(const void* w, const void* x, int dtype, int64_t oc, int64_t ic,
                          int64_t T, int group, int nsteps, const void* factors, int qmin,
-                         int qmax, int sym, int clip_sym, void* best_max, void* best_min,
-                         void* stream);
+                         int qmax, int sym, int clip_sym, int mse_steps, const void* mse_p,
+                         float norm, void* best_max, void* best_min, void* stream);
 
 /* AutoClipper.apply_clip, v1 (auto_clip.py:193-212): out = clamp(x, cmin, cmax) per group;
  * cmin NULL -> -cmax. In place allowed. */

@@ -94,8 +94,11 @@ class AutoClipper:
             raise NotImplementedError(f'device auto-clip kernel: group size {group}')
         x = self.sample_tokens(inputs[0], n_sample_token)
         qmin, qmax = int(wq.qmin.item()), int(wq.qmax.item())
+        mse = None
+        if wq.calib_algo == 'mse':  # every step's fake quant searches its range
+            mse = (wq._mse_nsteps(), wq.mse_grid, 2.4)
         return ops.auto_clip_search(w.data, x, group, int(max_shrink * n_grid), n_grid, qmin,
-                                    qmax, wq.sym, self.clip_sym)
+                                    qmax, wq.sym, self.clip_sym, mse=mse)
 
     @torch.no_grad()
     def apply_clip(self, block_idx, layer, min_val, max_val, layer_name):

@@ -305,8 +305,6 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         special = qc.get('special', {}) or {}
         self.true_sequential = special.get('true_sequential', False)
         self.weight_clip = special.get('weight_clip', False)
-        if self.weight_clip and self.wquantizer.calib_algo == 'mse':
-            raise NotImplementedError('auto-clip with calib_algo mse is not on the device path')
         if self.weight_clip or special.get('search_clip_init', False):
             from .auto_clip import AutoClipper
             self.save_clip = special.get('save_clip', False)

@@ -358,11 +358,32 @@ __device__ __forceinline__ void load_half(const uint16_t* __restrict__ wrow, int
     widen4<DT>(*reinterpret_cast<const uint2*>(wrow + 8 * i + 4 * h), &q[4 * i]);
 }
 
-template <int DT, int G>
+// get_qparams in fp32 (quant.py:545-559) for the calib_algo mse search
+__device__ __forceinline__ void qparams_f32_mse(float mn, float mx, float qmin, float qmax,
+                                                int sym, float& s, float& z) {
+  if (sym) {
+    float am = fmaxf(fabsf(mx), fabsf(mn));
+    am = am < 1e-5f ? 1e-5f : am;
+    s = am / qmax;
+    z = 0.f;
+  } else {
+    float r = mx - mn;
+    r = r < 1e-5f ? 1e-5f : r;
+    s = r / (qmax - qmin);
+    z = fminf(fmaxf(qmin - rintf(mn / s), qmin), qmax);
+  }
+}
+
+// MSE: the weight quantizer's calib_algo is mse (quant.py:145-203): each shrink step's fake
+// quant searches its range on the clamped group in fp32 (mse_p[i] = fp32(1 - i / grid),
+// |qdq(v) - v|^norm summed, strict improvements shrink the base), then quantizes in fp32 with
+// the fp32 qparams and rounds to DT once (the DT tensor is promoted by the fp32 scales).
+template <int DT, int G, bool MSE>
 __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 weights/lane
     k_auto_clip(const uint16_t* __restrict__ w, const uint16_t* __restrict__ x, int64_t oc,
                 int64_t ic, int T, int nsteps, const float* __restrict__ factors, float qmin,
-                float qmax, int sym, int clip_sym, uint16_t* best_max, uint16_t* best_min) {
+                float qmax, int sym, int clip_sym, uint16_t* best_max, uint16_t* best_min,
+                int mse_steps, const float* __restrict__ mse_p, float norm) {
   constexpr int CH = G / 2;    // weights per lane: k = 8i + 4h + j, h = lane parity
   constexpr int CHUNKS = G / 8;
   __shared__ __attribute__((aligned(16))) float xs[CT * G];      // <= 32 KB
@@ -422,6 +443,37 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 we
         const float cmn = fminf(fmaxf(mn, smin), smax);
         const float cmx = fminf(fmaxf(mxs, smin), smax);
         float qs, qz;
+        if constexpr (MSE) {
+#pragma unroll
+          for (int k = 0; k < CH; ++k) q[k] = fminf(fmaxf(q[k], smin), smax);
+          float rmn = cmn, rmx = cmx, best_e = INFINITY;
+          for (int i = 0; i < mse_steps; ++i) {
+            const float pp = mse_p[i];
+            const float xmn = pp * rmn, xmx = pp * rmx;
+            float s2, z2;
+            qparams_f32_mse(xmn, xmx, qmin, qmax, sym, s2, z2);
+            float err = 0.f;
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+              float qq = rintf(q[k] / s2) + z2;
+              qq = fminf(fmaxf(qq, qmin), qmax);
+              err += powf(fabsf((qq - z2) * s2 - q[k]), norm);
+            }
+            const float pe = xor1(err);
+            err = h ? pe + err : err + pe;  // same operand order on both lanes
+            if (err < best_e) {
+              best_e = err;
+              rmn = xmn;
+              rmx = xmx;
+            }
+          }
+          qparams_f32_mse(rmn, rmx, qmin, qmax, sym, qs, qz);
+#pragma unroll
+          for (int k = 0; k < CH; ++k) {
+            float tq = fminf(fmaxf(rintf(q[k] / qs) + qz, qmin), qmax);
+            q[k] = dtr<DT>((tq - qz) * qs);
+          }
+        } else {
         qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
@@ -432,6 +484,7 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 we
           if (!sym) tq = dtr<DT>(tq + qz);
           tq = fminf(fmaxf(tq, qmin), qmax);
           q[k] = dtr<DT>((sym ? tq : dtr<DT>(tq - qz)) * qs);
+        }
         }
       }
       float e = (p > 0) ? es[(p - 1) * CROWS + r] : 0.f;
@@ -611,47 +664,65 @@ extern "C" int lcq_sq_diff_mean(const void* a, const void* b, int dtype, int64_t
   return check_launch("lcq_sq_diff_mean");
 }
 
-template <int DT, int G>
-static void launch_auto_clip(const void* w, const void* x, int64_t oc, int64_t ic, int64_t T,
-                             int nsteps, const void* factors, int qmin, int qmax, int sym,
-                             int clip_sym, void* best_max, void* best_min, hipStream_t st) {
-  dim3 grid((unsigned)((oc + CROWS - 1) / CROWS), (unsigned)(ic / G));
-  hipLaunchKernelGGL((k_auto_clip<DT, G>), grid, 2 * CROWS, 0, st,
-                     reinterpret_cast<const uint16_t*>(w), reinterpret_cast<const uint16_t*>(x),
-                     oc, ic, (int)T, nsteps, reinterpret_cast<const float*>(factors),
-                     (float)qmin, (float)qmax, sym, clip_sym,
-                     reinterpret_cast<uint16_t*>(best_max), reinterpret_cast<uint16_t*>(best_min));
+struct ClipLaunch {
+  const void* w;
+  const void* x;
+  int64_t oc, ic, T;
+  int nsteps;
+  const void* factors;
+  int qmin, qmax, sym, clip_sym;
+  void* bmax;
+  void* bmin;
+  int mse_steps;
+  const void* mse_p;
+  float norm;
+};
+
+template <int DT, int G, bool MSE>
+static void launch_auto_clip(const ClipLaunch& c, hipStream_t st) {
+  dim3 grid((unsigned)((c.oc + CROWS - 1) / CROWS), (unsigned)(c.ic / G));
+  hipLaunchKernelGGL((k_auto_clip<DT, G, MSE>), grid, 2 * CROWS, 0, st,
+                     reinterpret_cast<const uint16_t*>(c.w), reinterpret_cast<const uint16_t*>(c.x),
+                     c.oc, c.ic, (int)c.T, c.nsteps, reinterpret_cast<const float*>(c.factors),
+                     (float)c.qmin, (float)c.qmax, c.sym, c.clip_sym,
+                     reinterpret_cast<uint16_t*>(c.bmax), reinterpret_cast<uint16_t*>(c.bmin),
+                     c.mse_steps, reinterpret_cast<const float*>(c.mse_p), c.norm);
 }
 
-template <int DT>
-static int auto_clip_group(int group, const void* w, const void* x, int64_t oc, int64_t ic,
-                           int64_t T, int nsteps, const void* factors, int qmin, int qmax,
-                           int sym, int clip_sym, void* bmax, void* bmin, hipStream_t st) {
+template <int DT, bool MSE>
+static void auto_clip_group(int group, const ClipLaunch& c, hipStream_t st) {
   switch (group) {
-    case 32: launch_auto_clip<DT, 32>(w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, bmax, bmin, st); break;
-    case 64: launch_auto_clip<DT, 64>(w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, bmax, bmin, st); break;
-    case 128: launch_auto_clip<DT, 128>(w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, bmax, bmin, st); break;
-    default: launch_auto_clip<DT, 256>(w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, bmax, bmin, st);
+    case 32: launch_auto_clip<DT, 32, MSE>(c, st); break;
+    case 64: launch_auto_clip<DT, 64, MSE>(c, st); break;
+    case 128: launch_auto_clip<DT, 128, MSE>(c, st); break;
+    default: launch_auto_clip<DT, 256, MSE>(c, st);
   }
-  return check_launch("lcq_auto_clip_search");
 }
 
 extern "C" int lcq_auto_clip_search(const void* w, const void* x, int dtype, int64_t oc,
                                     int64_t ic, int64_t T, int group, int nsteps,
                                     const void* factors, int qmin, int qmax, int sym,
-                                    int clip_sym, void* best_max, void* best_min, void* stream) {
+                                    int clip_sym, int mse_steps, const void* mse_p, float norm,
+                                    void* best_max, void* best_min, void* stream) {
   LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16, "auto-clip: bf16 or fp16 model dtype");
   LCQ_REQUIRE(group == 32 || group == 64 || group == 128 || group == CGMAX,
               "auto-clip kernel supports group_size 32 / 64 / 128 / 256");
   LCQ_REQUIRE(oc > 0 && ic > 0 && ic % group == 0, "ic must be a multiple of the group size");
   LCQ_REQUIRE(T > 0 && nsteps >= 1 && nsteps <= CMAXSTEPS, "bad T / nsteps (<= 16)");
   LCQ_REQUIRE(qmax > qmin, "qmax <= qmin");
+  LCQ_REQUIRE(mse_steps == 0 || (mse_steps > 0 && mse_p != nullptr && norm > 0.f),
+              "mse: steps > 0 need the shrink factors and a positive norm");
   hipStream_t st = as_stream(stream);
-  if (dtype == LCQ_BF16)
-    return auto_clip_group<LCQ_BF16>(group, w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym,
-                                     clip_sym, best_max, best_min, st);
-  return auto_clip_group<LCQ_F16>(group, w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym,
-                                  clip_sym, best_max, best_min, st);
+  const ClipLaunch c{w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, best_max,
+                     best_min, mse_steps, mse_p, norm};
+  if (dtype == LCQ_BF16) {
+    if (mse_steps) auto_clip_group<LCQ_BF16, true>(group, c, st);
+    else auto_clip_group<LCQ_BF16, false>(group, c, st);
+  } else {
+    if (mse_steps) auto_clip_group<LCQ_F16, true>(group, c, st);
+    else auto_clip_group<LCQ_F16, false>(group, c, st);
+  }
+  return check_launch("lcq_auto_clip_search");
 }
 
 extern "C" int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t cols,

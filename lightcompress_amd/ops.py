@@ -470,8 +470,9 @@ def sq_diff_mean(a: torch.Tensor, b: torch.Tensor) -> float:
 
 
 def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, n_grid: int,
-                     qmin: int, qmax: int, sym: bool, clip_sym: bool):
-    """AutoClipper.auto_clip_layer (v1) on device: returns (best_max, best_min) [oc, ng, 1]."""
+                     qmin: int, qmax: int, sym: bool, clip_sym: bool, mse=None):
+    """AutoClipper.auto_clip_layer (v1) on device: returns (best_max, best_min) [oc, ng, 1].
+    mse = (steps, grid, norm): the weight quantizer's calib_algo is mse."""
     oc, ic = w.shape
     T = x.shape[0]
     factors = torch.tensor([float(1 - i / n_grid) for i in range(nsteps)], dtype=torch.float32,
@@ -481,9 +482,14 @@ def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, 
     bmin = torch.empty((oc, ng, 1), dtype=w.dtype, device=w.device)
     if x.dtype != w.dtype:
         raise ValueError('auto-clip: x and w must share the model dtype')
+    msteps, mp, norm = 0, None, 0.0
+    if mse is not None:
+        msteps, grid, norm = int(mse[0]), float(mse[1]), float(mse[2])
+        mp = torch.tensor([float(1 - i / grid) for i in range(msteps)], dtype=torch.float32,
+                          device=w.device)
     N.call('lcq_auto_clip_search', N.ptr(w.contiguous()), N.ptr(x.contiguous()), N.dt(w), oc,
            ic, T, int(group), int(nsteps), N.ptr(factors), int(qmin), int(qmax), int(sym),
-           int(clip_sym), N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
+           int(clip_sym), msteps, N.ptr(mp), norm, N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
     return bmax, bmin
 
 

@@ -77,10 +77,22 @@ def search_scale(x: torch.Tensor, weights: list, forward, bit, sym, group, n_gri
     return losses, best_i, best_s
 
 
+def _fq_mse(cur: torch.Tensor, bit, sym, group):
+    """fake_quant_weight_dynamic with calib_algo mse (quant.py:145-203, 690-697, 833-869):
+    fp32 range search, fp32 qparams, quant-dequant in fp32 (bf16 / fp16 tensor promoted by the
+    fp32 scales), back to the weight dtype."""
+    qmin, qmax = Q.int_range(bit, sym)
+    t = cur.reshape(-1, group)
+    mn, mx = Q.mse_range(t, bit, sym)
+    s, z = Q.qparams(mn, mx, qmin, qmax, sym)
+    out = Q.dequant(Q.quant(t.float(), s, z, qmin, qmax), s, z)
+    return out.reshape(cur.shape).to(cur.dtype)
+
+
 def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_grid=20,
-               max_shrink=0.5, n_sample_token=512):
+               max_shrink=0.5, n_sample_token=512, mse=False):
     """auto_clip.py:83-191 (clip v1, w_only, single input). Returns (best_max, best_min)
-    shaped [oc, ng, 1]."""
+    shaped [oc, ng, 1]. mse=True: the weight quantizer's calib_algo is mse."""
     w = w.reshape(w.shape[0], 1, -1, group)
     ocb = 256 if w.shape[0] % 256 == 0 else 64
     x = x.view(-1, x.shape[-1]).reshape(1, -1, x.shape[-1] // group, group)
@@ -98,7 +110,8 @@ def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_gr
             max_val = org_max * (1 - i_s / n_grid)
             min_val = -max_val if clip_sym else org_min * (1 - i_s / n_grid)
             cur = torch.clamp(wb, min_val, max_val)
-            q_w = Q.fake_quant_dynamic(cur, bit, sym, 'per_group', group)[0]
+            q_w = (_fq_mse(cur, bit, sym, group) if mse else
+                   Q.fake_quant_dynamic(cur, bit, sym, 'per_group', group)[0])
             cur_out = (x * q_w).sum(dim=-1)
             err = (cur_out - org_out).pow(2).mean(dim=1).view(min_errs.shape)
             err_mean = 0 + err

@@ -317,9 +317,13 @@ def gen_clip():
              ('asym_g64', False, False, 192, 256, 512, 64, 64, bf),      # DSv3 configs
              ('sym_g256', True, True, 128, 512, 512, 64, 256, bf),
              ('asym_g128_f16', False, False, 128, 512, 512, 64, 128, hf),  # OPT (fp16)
-             ('sym_g32_f16', True, True, 64, 256, 512, 64, 32, hf)]
+             ('sym_g32_f16', True, True, 64, 256, 512, 64, 32, hf),
+             # calib_algo mse: every shrink step's fake quant searches its range
+             ('mse_asym_g128', False, False, 128, 256, 512, 64, 128, bf),
+             ('mse_sym_g64', True, True, 64, 256, 512, 64, 64, bf)]
     for i, (name, sym, clip_sym, oc, ic, ntok, nst, grp, dt) in enumerate(cases):
-        wq = q.IntegerQuantizer(4, sym, 'per_group', group_size=grp)
+        calib = 'mse' if name.startswith('mse_') else 'minmax'
+        wq = q.IntegerQuantizer(4, sym, 'per_group', group_size=grp, calib_algo=calib)
         clipper = ac.AutoClipper(w_only=True, wquantizer=wq, aquantizer=None,
                                  clip_version='v1', clip_sym=clip_sym, save_clip=False,
                                  padding_mask=None)
@@ -332,7 +336,7 @@ def gen_clip():
         clipper.apply_clip(0, m, bmin.clone(), bmax.clone(), 'l')
         F.save(f'clip_{name}', w=w, x=x, best_max=bmax, best_min=bmin,
                w_clipped=m.weight.data.clone(),
-               meta=torch.tensor([int(sym), int(clip_sym), nst, grp]))
+               meta=torch.tensor([int(sym), int(clip_sym), nst, grp, int(calib == 'mse')]))
     print('clip fixtures written')
 
 

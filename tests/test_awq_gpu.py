@@ -82,14 +82,19 @@ def test_auto_clip_vs_reference(dev, name):
     from lightcompress_amd import ops
     from lightcompress_amd.auto_clip import AutoClipper
     c = F.load(name)
-    sym, clip_sym, nst, group = c['meta'].tolist()
+    sym, clip_sym, nst, group, mse = c['meta'].tolist()
     qmin, qmax = (-8, 7) if sym else (0, 15)
     x = AutoClipper.sample_tokens(c['x'].to(dev), nst)
     bmax, bmin = ops.auto_clip_search(c['w'].to(dev), x, group, 10, 20, qmin, qmax, bool(sym),
-                                      bool(clip_sym))
+                                      bool(clip_sym), mse=(80, 100, 2.4) if mse else None)
     assert bmax.dtype == c['w'].dtype
     eq_max = (bits(bmax) == bits(c['best_max'])).float().mean().item()
     eq_min = (bits(bmin) == bits(c['best_min'])).float().mean().item()
+    if mse:
+        # the range search's |d|^2.4 sums: device powf and a fixed pair order vs the
+        # reference's vectorised powf and row-sum order -> near-tie range choices (T2)
+        assert eq_max >= 0.98 and eq_min >= 0.98, (eq_max, eq_min)
+        return
     assert eq_max == 1.0 and eq_min == 1.0, (eq_max, eq_min)
     w = c['w'].to(dev).clone()
     ops.clip_apply(w, group, bmax.reshape(-1), None if clip_sym else bmin.reshape(-1), out=w)

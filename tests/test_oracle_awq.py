@@ -34,9 +34,9 @@ def test_search_scale_v1_matches_reference(subset, sym):
 @pytest.mark.parametrize('name', F.names('clip_'))
 def test_auto_clip_matches_reference(name):
     c = F.load(name)
-    sym, clip_sym, nst, group = c['meta'].tolist()
+    sym, clip_sym, nst, group, mse = c['meta'].tolist()
     bmax, bmin = A.clip_layer(c['w'], c['x'], 4, bool(sym), group, bool(clip_sym),
-                              n_sample_token=nst)
+                              n_sample_token=nst, mse=bool(mse))
     assert torch.equal(bmax.view(torch.int16), c['best_max'].view(torch.int16))
     assert torch.equal(bmin.view(torch.int16), c['best_min'].view(torch.int16))
     wc = A.apply_clip(c['w'], bmax, bmin, bool(clip_sym))
