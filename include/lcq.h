@@ -95,6 +95,33 @@ int lcq_int_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols,
                          int fq_dtype, void* codes_out, int codes_dtype, void* packed_out,
                          int pack_bits, void* stream);
 
+/* lcq_int_quant_static with round_zp False (quant.py:701-707, the HQQ configs):
+ * q = clamp(round(x / s.clamp_min(1e-9) + z), qmin, qmax), x^ = (q - z) * s, every op
+ * rounded to ct_dtype; zeros stay float (real quant keeps them unrounded). */
+int lcq_int_quant_static_nozp(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                              int64_t group, const void* scales, int s_dtype, const void* zeros,
+                              int z_dtype, int ct_dtype, int qmin, int qmax, void* fq_out,
+                              int fq_dtype, void* codes_out, int codes_dtype, void* stream);
+
+/* get_minmax_range + get_qparams (quant.py:132-143, 545-559) of x [ng, gs] (gs % 8 == 0) in
+ * the x dtype, incl. round_zp False (zeros = qmin - min / scales, unrounded, unclamped).
+ * scales / zeros [ng] in the x dtype; zeros may be NULL when sym. */
+int lcq_minmax_qparams(const void* x, int dtype, int64_t ng, int64_t gs, int qmin, int qmax,
+                       int sym, int round_zp, void* scales, void* zeros, void* stream);
+
+/* Workspace bytes of lcq_hqq_proximal for ng groups. */
+int64_t lcq_hqq_workspace_bytes(int64_t ng);
+
+/* optimize_weights_proximal (quant.py:588-610; hqq.py:36-61) on w [ng, gs] fp32 (gs % 8 == 0):
+ * scales / zeros fp32 [ng] in (get_qparams of the same groups) and out (best scales =
+ * 1 / (1 / s), the zeros of the last iteration run). Up to `iters` half-quadratic steps,
+ * shrink_op with lp_norm and the quantizer's beta, stopping at the first step whose mean
+ * |w - w_r| is not below the best so far; enqueued without a host sync. state_out (nullable,
+ * device, 16 B): {float best_error, int stopped, int iters_run, int pad}. */
+int lcq_hqq_proximal(const void* w, int64_t ng, int64_t gs, void* scales, void* zeros, int qmin,
+                     int qmax, float lp_norm, float beta, int iters, void* workspace,
+                     int64_t ws_bytes, void* state_out, void* stream);
+
 /* Per-tensor static qparams given as 0-dim tensors on the reference's CPU path
  * (fake_quant_act_static with register_act_qparams' scale / zero, quant.py:699-743): torch-CPU
  * takes a 0-dim operand as a scalar of the op's opmath type, so the fp32 scale / zero (device
@@ -323,10 +350,12 @@ int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t max_elems, in
  * module_utils.py:41-46, for LlmcFp8Linear / fp8_forward linears): a [M, K] e4m3 codes with
  * per-token 128-column scales a_s fp32 [M, K/128] (act_quant); b [N, K] e4m3 codes with
  * 128x128 block scales b_s fp32 [ceil(N/128), K/128]. c[m, n] = sum_kb (dot_kb(a[m], b[n]) *
- * a_s[m, kb]) * b_s[n/128, kb], fp32 accumulation, stored as c_dtype (LCQ_F32 / LCQ_BF16).
- * K % 128 == 0; a / b 16-byte aligned. Short batches split K across workgroups when
+ * a_s[m, kb]) * b_s[n/128, kb], fp32 accumulation, stored as c_dtype (LCQ_F32 / LCQ_BF16 /
+ * LCQ_F16). K % 128 == 0; a / b 16-byte aligned. Short batches split K across workgroups when
  * `workspace` holds lcq_fp8_gemm_workspace_bytes(M, N, K) bytes of device memory (fp32
- * partials summed in split order: deterministic); null / smaller workspace = no split. */
+ * partials summed in split order: deterministic for a given M; the split count depends on M,
+ * so a row's fp32 sum order -- not its value up to rounding -- can differ between batch
+ * sizes); null / smaller workspace = no split. */
 int64_t lcq_fp8_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const void* b_s, int64_t M,
                  int64_t N, int64_t K, void* c, int c_dtype, void* workspace, int64_t ws_bytes,

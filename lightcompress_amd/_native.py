@@ -39,6 +39,12 @@ SIGNATURES = {
                                _vp, _int, _vp, _int, _vp, _int, _vp, _vp, _vp], _int),
     'lcq_int_quant_static': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _int, _int,
                               _int, _vp, _int, _vp, _int, _vp, _int, _vp], _int),
+    'lcq_int_quant_static_nozp': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _int,
+                                   _int, _int, _vp, _int, _vp, _int, _vp], _int),
+    'lcq_minmax_qparams': ([_vp, _int, _i64, _i64, _int, _int, _int, _int, _vp, _vp, _vp], _int),
+    'lcq_hqq_workspace_bytes': ([_i64], _i64),
+    'lcq_hqq_proximal': ([_vp, _i64, _i64, _vp, _vp, _int, _int, _f32, _f32, _int, _vp, _i64,
+                          _vp, _vp], _int),
     'lcq_int_quant_static_scalar': ([_vp, _int, _i64, _i64, _vp, _vp, _int, _int, _int, _vp,
                                      _int, _vp, _int, _vp], _int),
     'lcq_int_quant_static_cols': ([_vp, _int, _i64, _i64, _vp, _i64, _vp, _int, _vp, _int,

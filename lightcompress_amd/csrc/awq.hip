@@ -12,6 +12,7 @@
 //   auto_clip_layer    auto_clip.py:83-191 (10-step shrink grid)          -> lcq_auto_clip_search
 //   apply_clip (v1)    auto_clip.py:193-212                               -> lcq_clip_apply
 #include "lcq_common.h"
+#include <stdlib.h>
 
 namespace lcq {
 
@@ -292,10 +293,16 @@ __device__ __forceinline__ float dtr(float f) {
   }
 }
 
-// products of a pair rounded to DT and widened back to fp32
-template <int DT>
+// products of a pair rounded to DT and widened back to fp32. bf16, CVT2: one
+// v_cvt_pk_bf16_f32 per product with a zero low half, so the result register IS the widened
+// fp32 value (2 VALU per pair instead of convert + shift + mask: 3)
+template <int DT, bool CVT2 = true>
 __device__ __forceinline__ v2f dtr2(v2f p) {
-  if constexpr (DT == LCQ_BF16) {
+  if constexpr (DT == LCQ_BF16 && CVT2) {
+    const v2bf lo = __builtin_convertvector(v2f{0.f, p.x}, v2bf);
+    const v2bf hi = __builtin_convertvector(v2f{0.f, p.y}, v2bf);
+    return v2f{__builtin_bit_cast(float, lo), __builtin_bit_cast(float, hi)};
+  } else if constexpr (DT == LCQ_BF16) {
     const v2bf h = __builtin_convertvector(p, v2bf);
     const uint32_t u = __builtin_bit_cast(uint32_t, h);
     v2f r;
@@ -329,15 +336,15 @@ __device__ __forceinline__ float xor1(float v) {  // value of the partner lane (
 // k = 8i + 4h + j (j = 0..3) i.e. partial sums acc_{4h+j} of the 8-way (k mod 8) order that
 // torch-CPU's vectorised reduction uses for every group size and for bf16 and fp16 alike; the
 // pair exchange forms l_j = acc_j + acc_{j+4} and both lanes finish the halving tree.
-template <int DT, int G>
+template <int DT, int G, bool CVT2 = true>
 __device__ __forceinline__ float dot_row(const float* __restrict__ xr, const float (&q)[G / 2],
                                          int h) {
   v2f a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < G / 8; ++i) {
     const float4 xv = *reinterpret_cast<const float4*>(xr + 8 * i + 4 * h);
-    a0 += dtr2<DT>(v2f{xv.x, xv.y} * v2f{q[4 * i], q[4 * i + 1]});
-    a1 += dtr2<DT>(v2f{xv.z, xv.w} * v2f{q[4 * i + 2], q[4 * i + 3]});
+    a0 += dtr2<DT, CVT2>(v2f{xv.x, xv.y} * v2f{q[4 * i], q[4 * i + 1]});
+    a1 += dtr2<DT, CVT2>(v2f{xv.z, xv.w} * v2f{q[4 * i + 2], q[4 * i + 3]});
   }
   // lane h=0 holds acc0..3, h=1 holds acc4..7: l_j = acc_j + acc_{j+4}. The partner values
   // are read in uniform control flow (a cross-lane read inside a divergent branch would see
@@ -378,7 +385,7 @@ __device__ __forceinline__ void qparams_f32_mse(float mn, float mx, float qmin, 
 // quant searches its range on the clamped group in fp32 (mse_p[i] = fp32(1 - i / grid),
 // |qdq(v) - v|^norm summed, strict improvements shrink the base), then quantizes in fp32 with
 // the fp32 qparams and rounds to DT once (the DT tensor is promoted by the fp32 scales).
-template <int DT, int G, bool MSE>
+template <int DT, int G, bool MSE, bool CVT2 = true>
 __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 weights/lane
     k_auto_clip(const uint16_t* __restrict__ w, const uint16_t* __restrict__ x, int64_t oc,
                 int64_t ic, int T, int nsteps, const float* __restrict__ factors, float qmin,
@@ -489,7 +496,7 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 we
       }
       float e = (p > 0) ? es[(p - 1) * CROWS + r] : 0.f;
       for (int t = 0; t < tn; ++t) {
-        const float d = dot_row<DT, G>(&xs[t * G], q, h);
+        const float d = dot_row<DT, G, CVT2>(&xs[t * G], q, h);
         if (p == 0) {
           if (h == 0) orgs[t * CROWS + r] = d;
         } else {
@@ -681,7 +688,10 @@ struct ClipLaunch {
 template <int DT, int G, bool MSE>
 static void launch_auto_clip(const ClipLaunch& c, hipStream_t st) {
   dim3 grid((unsigned)((c.oc + CROWS - 1) / CROWS), (unsigned)(c.ic / G));
-  hipLaunchKernelGGL((k_auto_clip<DT, G, MSE>), grid, 2 * CROWS, 0, st,
+  const char* e = getenv("LCQ_CLIP_CVT");  // 0: the convert + shift / mask widening (A/B)
+  auto k = (DT == LCQ_BF16 && e && e[0] == '0') ? k_auto_clip<DT, G, MSE, false>
+                                                : k_auto_clip<DT, G, MSE, true>;
+  hipLaunchKernelGGL(k, grid, 2 * CROWS, 0, st,
                      reinterpret_cast<const uint16_t*>(c.w), reinterpret_cast<const uint16_t*>(c.x),
                      c.oc, c.ic, (int)c.T, c.nsteps, reinterpret_cast<const float*>(c.factors),
                      (float)c.qmin, (float)c.qmax, c.sym, c.clip_sym,

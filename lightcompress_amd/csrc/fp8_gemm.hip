@@ -15,6 +15,8 @@
 // partials that a second kernel sums in split order (deterministic).
 #include "lcq_common.h"
 
+#include <stdlib.h>
+
 namespace lcq {
 namespace {
 
@@ -172,6 +174,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (m >= g.M) continue;
         if (g.ws) g.ws[((int64_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
         else if (g.c_dt == LCQ_F32) reinterpret_cast<float*>(g.c)[m * g.N + n] = acc[i][j][r];
+        else if (g.c_dt == LCQ_F16) st1<LCQ_F16>(g.c, m * g.N + n, acc[i][j][r]);
         else st1<LCQ_BF16>(g.c, m * g.N + n, acc[i][j][r]);
       }
     }
@@ -186,8 +189,216 @@ __global__ __launch_bounds__(256) void k_fp8_gemm_reduce(const float* __restrict
     float v = ws[i];
     for (int z = 1; z < splits; ++z) v += ws[(int64_t)z * mn + i];
     if (c_dt == LCQ_F32) reinterpret_cast<float*>(c)[i] = v;
+    else if (c_dt == LCQ_F16) st1<LCQ_F16>(c, i, v);
     else st1<LCQ_BF16>(c, i, v);
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_fp8_gemm2: 256 x 256 tile, 8 waves (2 per SIMD, 2 (M) x 4 (N), 128 x 64 each), gfx950's
+// 16x16x128 f8f6f4 MFMA: ONE instruction is the whole 128-wide scale block's dot product of a
+// 16 x 16 sub-tile, so the block scaling needs no second accumulator set: dot (4 VGPRs, C = 0)
+// then acc = fma(dot, a_s[m, kb] * b_s[n / 128, kb], acc) (4 FMAs, the lane's 4 values share
+// one row m in the swapped layout). The reference rounds (dot * a_s) * b_s + acc three times;
+// this rounds the scale product and one fma: <= 2 ulp of each block term (tested against the
+// oracle at 1e-5 of |a||b|). 128 accumulator VGPRs per wave, ~200 VGPRs: two waves per SIMD.
+// Operands stream through LDS by LDS-DMA (buffer_load ... lds, 16 B per lane; 8 pieces per wave
+// per K block) into two 64 KB buffers (A 256 x 128 B + B 256 x 128 B, 16-B chunks XOR-swizzled
+// by row & 7), plus the K block's 256 a_s values (kb-major copy made by k_as_transpose; 4 B
+// per lane from waves 0-3: an LDS-DMA lane writes a whole dword). One barrier per K block: after it the next K
+// block's loads go into the buffer every wave finished reading.
+// ---------------------------------------------------------------------------------------
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+constexpr int T2 = 256;                   // output tile (M and N)
+constexpr int OPB = T2 * BK;              // one operand tile: 256 rows x 128 B = 32 KB
+constexpr int STG = 2 * OPB + 1024;       // A + B + 256 fp32 a_s per K block
+constexpr int LDS2 = 2 * STG;             // double buffered: 130 KB
+
+struct Gemm2Args {
+  const uint8_t* a;
+  const uint8_t* b;
+  const float* ast;   // a_s transposed, [nkb][mp] (mp = M rounded up to 256)
+  const float* bs;    // [ceil(N/128), nkb]
+  void* c;
+  float* ws;          // split-K partials or null
+  int64_t M, N, K, mp;
+  int64_t kb_per_split;
+  int c_dt;
+  int nmt, nnt;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane(
+      (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo),
+                                           (short)0, nb, 0x00020000);
+}
+
+// 16-B chunk c (0..7) of row r of an operand tile lives at physical chunk c ^ (r & 7)
+__device__ __forceinline__ v8i frag2(const uint8_t* tile, int row, int q) {
+  const uint8_t* rp = tile + row * BK;
+  const int c0 = (2 * q) ^ (row & 7), c1 = (2 * q + 1) ^ (row & 7);
+  const uint4 lo = *reinterpret_cast<const uint4*>(rp + c0 * 16);
+  const uint4 hi = *reinterpret_cast<const uint4*>(rp + c1 * 16);
+  return v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z,
+             (int)hi.w};
+}
+
+__global__ __launch_bounds__(512, 1) void k_fp8_gemm2(Gemm2Args g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  // XCD-aware order: the 32 workgroups an XCD runs at once take a 4 (M) x 8 (N) block
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int cpb = (g.nnt + 7) / 8;
+  const int chunk = wg >> 5, sl = wg & 31, band = chunk / cpb, cc = chunk - band * cpb;
+  const int tm = band * 4 + (sl >> 3), tn = cc * 8 + (sl & 7);
+  if (tm >= g.nmt || tn >= g.nnt) return;
+  const int64_t m0 = (int64_t)tm * T2, n0 = (int64_t)tn * T2;
+  const int64_t nkb = g.K / BK;
+  const int64_t kb0 = (int64_t)blockIdx.z * g.kb_per_split;
+  int64_t nk = nkb - kb0;
+  if (nk > g.kb_per_split) nk = g.kb_per_split;
+
+  // staging: piece j (0..7) of wave w = 8 rows (w * 8 + j * 64 .. ) of A (j < 4) or B (j >= 4)
+  // 8 rows x 128 B = 64 lanes x 16 B; lane l -> row l / 8, physical chunk l % 8 = logical
+  // chunk (l % 8) ^ (row & 7)
+  const __amdgpu_buffer_rsrc_t ra = rsrc(g.a + m0 * g.K, (g.M - m0) * g.K);
+  const __amdgpu_buffer_rsrc_t rb = rsrc(g.b + n0 * g.K, (g.N - n0) * g.K);
+  const __amdgpu_buffer_rsrc_t rs = rsrc(g.ast + m0, (g.mp * nkb - m0) * 4);
+  uint32_t off[4];
+  int lrow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = j * 64 + w * 8 + (lane >> 3);
+    lrow[j] = row;
+    off[j] = (uint32_t)(row * g.K + (((lane & 7) ^ (row & 7)) * 16));
+  }
+  auto stage = [&](int buf, int64_t kbl) {  // kbl: K block index within the split
+    const int64_t kb = kb0 + (kbl < nk ? kbl : nk - 1);
+    uint8_t* dst = lds + buf * STG;
+    const int kofs = (int)(kb * BK);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(dst + (j * 64 + w * 8) * BK),
+                                               16, off[j], kofs, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(dst + OPB +
+                                                                 (j * 64 + w * 8) * BK),
+                                               16, off[j], kofs, 0, 0);
+    }
+    // a_s of this K block: 256 floats = waves 0-3 x 64 lanes x 4 B (the K loop waits with
+    // vmcnt(0), so the per-wave piece counts need not match)
+    if (w < 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + 2 * OPB + w * 256), 4,
+                                               (uint32_t)(w * 256 + lane * 4),
+                                               (int)(kb * g.mp * 4), 0, 0);
+  };
+  (void)lrow;
+
+  v4f acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const v4f zero = {0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, q = lane >> 4;
+  int64_t nbr = (n0 + wc * 64) >> 7;  // this wave's 128-column scale block (clamped past N)
+  if (nbr > (g.N - 1) >> 7) nbr = (g.N - 1) >> 7;
+  const float* bsrow = g.bs + nbr * nkb + kb0;
+
+  stage(0, 0);
+  for (int64_t t = 0; t < nk; ++t) {
+    const int buf = (int)(t & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this K block's pieces landed
+    __builtin_amdgcn_s_barrier();                     // ... for every wave; buf ^ 1 is free
+    stage(buf ^ 1, t + 1);                            // past the end: re-fetch (unused)
+    const uint8_t* At = lds + buf * STG;
+    const uint8_t* Bt = At + OPB;
+    const float* Sa = reinterpret_cast<const float*>(At + 2 * OPB);
+    const float bsv = bsrow[t];
+    v8i bfr[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) bfr[nb] = frag2(Bt, wc * 64 + nb * 16 + r16, q);
+    float sc[8];
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) sc[mb] = Sa[wr * 128 + mb * 16 + r16] * bsv;
+    v8i afr = frag2(At, wr * 128 + r16, q);
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) {
+      v8i anext = afr;
+      if (mb < 7) anext = frag2(At, wr * 128 + (mb + 1) * 16 + r16, q);
+      v4f d[4];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+        d[nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[nb], afr, zero, 0, 0, 0, 0,
+                                                                  0, 0);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[mb][nb][j] = __builtin_fmaf(d[nb][j], sc[mb], acc[mb][nb][j]);
+      afr = anext;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // acc[mb][nb][j] (swapped layout): C[m0 + wr*128 + mb*16 + r16][n0 + wc*64 + nb*16 + 4q + j]
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) {
+    const int64_t m = m0 + wr * 128 + mb * 16 + r16;
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const int64_t n = n0 + wc * 64 + nb * 16 + 4 * q;
+      if (n >= g.N) continue;
+      const v4f v = acc[mb][nb];
+      if (g.ws) {
+        *reinterpret_cast<float4*>(g.ws + ((int64_t)blockIdx.z * g.M + m) * g.N + n) =
+            make_float4(v[0], v[1], v[2], v[3]);
+      } else if (g.c_dt == LCQ_F32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.c) + m * g.N + n) =
+            make_float4(v[0], v[1], v[2], v[3]);
+      } else if (g.c_dt == LCQ_F16) {
+        uint2 o;
+        o.x = pack2<LCQ_F16>(v[0], v[1]);
+        o.y = pack2<LCQ_F16>(v[2], v[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(g.c) + m * g.N + n) = o;
+      } else {
+        uint2 o;
+        o.x = pack2<LCQ_BF16>(v[0], v[1]);
+        o.y = pack2<LCQ_BF16>(v[2], v[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(g.c) + m * g.N + n) = o;
+      }
+    }
+  }
+}
+
+// a_s [M, nkb] -> [nkb, mp] (rows past M zero)
+__global__ __launch_bounds__(256) void k_as_transpose(const float* __restrict__ as, int64_t M,
+                                                      int64_t nkb, int64_t mp,
+                                                      float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nkb * mp) return;
+  const int64_t kb = i / mp, m = i - kb * mp;
+  out[i] = m < M ? as[m * nkb + kb] : 0.f;
+}
+
+// split count for the 256^2 kernel: grids of fewer than 224 tiles split K (>= 4 K blocks each)
+int64_t gemm2_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((M + T2 - 1) / T2) * ((N + T2 - 1) / T2), nkb = K / BK;
+  if (tiles >= 224) return 1;
+  int64_t s = (256 + tiles - 1) / tiles;
+  if (s > nkb / 4) s = nkb / 4;
+  if (s < 2) return 1;
+  const int64_t per = (nkb + s - 1) / s;
+  return (nkb + per - 1) / per;
 }
 
 // K splits for a short batch: a 64-row grid of fewer than 256 tiles is split along K until
@@ -210,10 +421,19 @@ int64_t gemm_splits(int64_t M, int64_t N, int64_t K) {
 
 using namespace lcq;
 
+// workspace of the 256^2 kernel: the kb-major a_s copy, then the split-K partials
+static int64_t ws2_bytes(int64_t M, int64_t N, int64_t K) {
+  const int64_t mp = (M + T2 - 1) / T2 * T2, nkb = K / BK;
+  const int64_t s = gemm2_splits(M, N, K);
+  return nkb * mp * 4 + (s > 1 ? s * M * N * 4 : 0);
+}
+
 extern "C" int64_t lcq_fp8_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0) return 0;
   const int64_t s = gemm_splits(M, N, K);
-  return s > 1 ? s * M * N * (int64_t)sizeof(float) : 0;
+  const int64_t old = s > 1 ? s * M * N * (int64_t)sizeof(float) : 0;
+  const int64_t w2 = ws2_bytes(M, N, K);
+  return old > w2 ? old : w2;
 }
 
 extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const void* b_s,
@@ -222,11 +442,45 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
   LCQ_REQUIRE(a && a_s && b && b_s && c, "null pointer");
   LCQ_REQUIRE(M > 0 && N > 0 && K > 0, "empty GEMM");
   LCQ_REQUIRE(K % 128 == 0, "K must be a multiple of 128 (the scale block)");
-  LCQ_REQUIRE(c_dtype == LCQ_F32 || c_dtype == LCQ_BF16, "C dtype must be F32 or BF16");
+  LCQ_REQUIRE(c_dtype == LCQ_F32 || c_dtype == LCQ_BF16 || c_dtype == LCQ_F16,
+              "C dtype must be F32, BF16 or F16");
   LCQ_REQUIRE((reinterpret_cast<uintptr_t>(a) & 15) == 0 &&
                   (reinterpret_cast<uintptr_t>(b) & 15) == 0,
               "A / B must be 16-byte aligned");
   const int64_t nkb = K / BK;
+  const char* sel = getenv("LCQ_FP8_GEMM");  // 1: always the 64/128-row 32x32x64 kernel
+  // the 256^2 kernel where its grid fills the chip (>= 128 tiles; measured: 1.46 vs 1.01
+  // PFLOP/s at 2048 x 7168 x 7168, 1.85 vs 1.30 at 8192^3), else the 64/128-row kernel (2x
+  // faster at M 512: the big tile's split-K partials cost more than they save)
+  const int64_t tiles2 = ((M + T2 - 1) / T2) * ((N + T2 - 1) / T2);
+  if (!(sel && sel[0] == '1') && tiles2 >= 128 && workspace && ws_bytes >= ws2_bytes(M, N, K) &&
+      N % 4 == 0 &&
+      M * K < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31)) {
+    hipStream_t st = as_stream(stream);
+    const int64_t mp = (M + T2 - 1) / T2 * T2;
+    const int64_t s2 = gemm2_splits(M, N, K);
+    float* ast = static_cast<float*>(workspace);
+    float* part = s2 > 1 ? ast + nkb * mp : nullptr;
+    hipLaunchKernelGGL(k_as_transpose, dim3((unsigned)((nkb * mp + 255) / 256)), 256, 0, st,
+                       static_cast<const float*>(a_s), M, nkb, mp, ast);
+    Gemm2Args g2{static_cast<const uint8_t*>(a), static_cast<const uint8_t*>(b), ast,
+                 static_cast<const float*>(b_s), c, part, M, N, K, mp,
+                 (nkb + s2 - 1) / s2, c_dtype, (int)((M + T2 - 1) / T2),
+                 (int)((N + T2 - 1) / T2)};
+    const int nslots = 32 * ((g2.nmt + 3) / 4) * ((g2.nnt + 7) / 8);
+    (void)hipFuncSetAttribute((const void*)k_fp8_gemm2,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+    hipLaunchKernelGGL(k_fp8_gemm2, dim3((unsigned)nslots, 1, (unsigned)s2), 512, LDS2, st, g2);
+    if (s2 > 1) {
+      const int rc = check_launch("lcq_fp8_gemm");
+      if (rc) return rc;
+      const int64_t mn = M * N;
+      int64_t blocks = (mn + 255) / 256;
+      if (blocks > 4096) blocks = 4096;
+      k_fp8_gemm_reduce<<<(unsigned)blocks, 256, 0, st>>>(part, (int)s2, mn, c, c_dtype);
+    }
+    return check_launch("lcq_fp8_gemm");
+  }
   int64_t splits = gemm_splits(M, N, K);
   if (!workspace || ws_bytes < splits * M * N * (int64_t)sizeof(float)) splits = 1;
   const int64_t per = (nkb + splits - 1) / splits;

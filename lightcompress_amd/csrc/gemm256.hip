@@ -71,6 +71,8 @@ struct Args {
   double* part;
   int nseg;
   int n_mt, n_nt, cpb, nslots;
+  int order;  // tile order of k_gemm16: 0 = per-XCD bands (slot_tile), 1 = N-band-major (tile_nb)
+  int wide;   // every output pointer 16-B aligned and every ldc % 8 == 0: 16-B epilogue stores
 };
 
 // half-row hr (0..127) of half-tile h -> row of the 256-row operand tile
@@ -87,6 +89,20 @@ __device__ __forceinline__ bool slot_tile(const Args& a, int slot, int& tm, int&
   const int band = chunk / a.cpb, c = chunk - band * a.cpb;
   tm = band * 4 + (s >> 3);
   tn = c * 8 + (s & 7);
+  return tm < a.n_mt && tn < a.n_nt;
+}
+
+// N-band-major order: launch step T = bid >> 8 (the 256 workgroups resident at once, one per
+// CU) covers a region of 32 (M) x 8 (N) tiles; XCD x = bid & 7 takes its 4 x 8 chunk (tile rows
+// 4x..4x+3, 12 operand panels shared in its L2). Regions walk M first inside one band of 8
+// N-tiles, so every XCD streams the same B band while the A panels pass once per band:
+// beyond-L2 reads of B come from the MALL, HBM reads ~ A x (N / 2048) + B once.
+__device__ __forceinline__ bool tile_nb(const Args& a, int bid, int& tm, int& tn) {
+  const int xcd = bid & 7, s = (bid >> 3) & 31, T = bid >> 8;
+  const int mreg = (a.n_mt + 31) >> 5;
+  const int nb = T / mreg, mr = T - nb * mreg;
+  tm = mr * 32 + xcd * 4 + (s >> 3);
+  tn = nb * 8 + (s & 7);
   return tm < a.n_mt && tn < a.n_nt;
 }
 
@@ -768,7 +784,7 @@ __device__ __forceinline__ void make_stage16(const Args& a, int tm, int tn, int 
   }
 }
 
-template <bool FP16>
+template <bool FP16, int DIAG = 0>
 __device__ __forceinline__ void ktile16(v4f (&acc)[8][8], v8s (&bf)[8][2], v8s (&af)[2][2][2],
                                         const Stage4& st, char* lds, int64_t t, int64_t nk,
                                         int w, int wr, int wc, int lane) {
@@ -789,8 +805,13 @@ __device__ __forceinline__ void ktile16(v4f (&acc)[8][8], v8s (&bf)[8][2], v8s (
           const int i = mm * 16 + n * 2 + kb;  // MFMA index within the block (0..31)
           mfma16a<FP16>(acc[2 * mb + mm][n], bf[n][kb], af[mb & 1][mm][kb]);
           if (i == 7) {
-            if (mb == 0 || mb == 3) wait_barrier<20>();
-            else wait_barrier<28>();
+            if constexpr (DIAG & 2) {  // diagnostic: the counted waits without the barrier
+              if (mb == 0 || mb == 3) asm volatile("s_waitcnt vmcnt(20) lgkmcnt(0)" ::: "memory");
+              else asm volatile("s_waitcnt vmcnt(28) lgkmcnt(0)" ::: "memory");
+            } else {
+              if (mb == 0 || mb == 3) wait_barrier<20>();
+              else wait_barrier<28>();
+            }
           }
           if (mb == 0 && i >= 8 && i < 28 && (i & 1) == 0) load_piece(st, lds, cur, kofs, w, (i - 8) >> 1);
           if (mb > 0 && (i == 8 || i == 20)) load_piece(st, lds, cur, kofs, w, 8 + 2 * mb + (i == 20));
@@ -810,6 +831,71 @@ __device__ __forceinline__ void ktile16(v4f (&acc)[8][8], v8s (&bf)[8][2], v8s (
   }
 }
 
+// k_gemm16 with the B fragments double-buffered in registers (LCQ_GEMM_KERNEL=b): the B
+// fragments of K-tile t+1 are read during blocks 1 and 2 of K-tile t (8 per block, one per MFMA
+// gap after that block's 4 A-fragment reads) into the other register set, instead of 16 reads
+// in the last 16 MFMA gaps whose lgkmcnt the next K-tile's first MFMAs wait on. Block 1's
+// barrier therefore retires K-tile t+1's B pieces (vmcnt 18: the 8 A pieces of K-tile t+1 and
+// the 10 pieces of K-tile t+2 issued in block 0 are younger), ~1.3 K-tiles after their issue.
+// P = register set of K-tile t (t & 1).
+template <bool FP16, int P, int DIAG = 0>
+__device__ __forceinline__ void ktile16b(v4f (&acc)[8][8], v8s (&bf)[2][8][2],
+                                         v8s (&af)[2][2][2], const Stage4& st, char* lds,
+                                         int64_t t, int64_t nk, int w, int wr, int wc,
+                                         int lane) {
+  const int cur = (int)(t & 1);
+  const char* At = lds + cur * BUF4;
+  const char* An = lds + (cur ^ 1) * BUF4;
+  const char* Bn = An + TILE_B;
+  const int64_t kt2 = t + 2 < nk ? t + 2 : nk - 1;
+  const int kofs = (int)(kt2 * (SKT * 2));
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+    for (int mm = 0; mm < 2; ++mm) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const int i = mm * 16 + n * 2 + kb;
+          mfma16a<FP16>(acc[2 * mb + mm][n], bf[P][n][kb], af[mb & 1][mm][kb]);
+          if (i == 7) {
+            if constexpr (DIAG & 2) {
+              if (mb == 1) asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)" ::: "memory");
+              else asm volatile("s_waitcnt vmcnt(20) lgkmcnt(0)" ::: "memory");
+            } else {
+              if (mb == 1) wait_barrier<18>();
+              else wait_barrier<20>();
+            }
+          }
+          if (mb == 0 && i >= 8 && i < 28 && (i & 1) == 0) load_piece(st, lds, cur, kofs, w, (i - 8) >> 1);
+          if (mb > 0 && (i == 8 || i == 20)) load_piece(st, lds, cur, kofs, w, 8 + 2 * mb + (i == 20));
+          if (i >= 8 && i < 12) {
+            const int q = i - 8, m2 = q >> 1, k2 = q & 1;
+            if (mb < 3) af[(mb + 1) & 1][m2][k2] = read_frag(At, wr * 8 + 2 * (mb + 1) + m2, k2, lane);
+            else af[0][m2][k2] = read_frag(An, wr * 8 + m2, k2, lane);  // K-tile t+1, block 0
+          }
+          if ((mb == 1 || mb == 2) && i >= 12 && i < 20) {  // B fragments of K-tile t+1
+            const int f = (mb - 1) * 8 + (i - 12), nn = f >> 1, k3 = f & 1;
+            bf[P ^ 1][nn][k3] = read_frag(Bn, wc * 8 + nn, k3, lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  }
+}
+
+// Two column groups of one row (this lane's packed x4 of group n: cols n*16 + fq*4.., and of
+// group n+1) -> 8 contiguous columns per lane for ONE 16-B store (T21 for the 16x16 swapped
+// layout): v_permlane16_swap exchanges lanes 16-31 of `a` with lanes 0-15 of `b` (and 48-63
+// with 32-47), so lane fq holds columns (fq & 1) * 16 + (fq >> 1) * 8 + 0..7 of the pair.
+__device__ __forceinline__ uint4 pair16(uint2 a, uint2 b) {
+  const auto rx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto ry = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  return make_uint4(rx[0], ry[0], rx[1], ry[1]);
+}
+
 // Epilogue of the 4-wave 16x16x32 kernels (swapped layout, see k_gemm16).
 template <int DT, int EPI>
 __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, int tn, int w,
@@ -819,13 +905,36 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
   // tn*128 + wc*64 + n*16 + fq*4 + j). Segment, bias and row pointers are resolved once per
   // tile / row (a tile never straddles a segment), loads are batched per row.
   const int fr = lane & 15, fq = lane >> 4;
+  const int poff = (fq & 1) * 16 + (fq >> 1) * 8;  // pair16 column offset of this lane
   if constexpr (EPI == EPI_SILU) {
     const int64_t col0 = (int64_t)tn * 128 + wc * 64 + fq * 4;
+    const bool wide = a.wide && (int64_t)tn * 128 + 128 <= a.n;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
       if (trow >= a.m) break;
       uint16_t* crow = a.c[0] + trow * a.ldc[0] + col0;
+      if (wide) {  // partner lanes (lane ^ 16) share the row: same branch
+        uint2 wv[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          float o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float gg = rnd<DT>(acc[m][n][j]);
+            const float u = rnd<DT>(acc[m][n + 4][j]);
+            const float sl = rnd<DT>(gg / (1.0f + expf(-gg)));
+            o[j] = rnd<DT>(sl * u);
+          }
+          wv[n].x = pack2<DT>(o[0], o[1]);
+          wv[n].y = pack2<DT>(o[2], o[3]);
+        }
+        uint16_t* cpair = crow - fq * 4 + poff;
+#pragma unroll
+        for (int n = 0; n < 4; n += 2)
+          *reinterpret_cast<uint4*>(cpair + n * 16) = pair16(wv[n], wv[n + 1]);
+        continue;
+      }
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         if (col0 + n * 16 >= a.n) break;
@@ -896,6 +1005,19 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
           o[n][j] = rnd<DT>(bp != nullptr ? __fadd_rn(acc[m][n][j], bias[n][j]) : acc[m][n][j]);
       if constexpr (EPI == EPI_STORE) {
         uint16_t* crow = a.c[s] + trow * a.ldc[s] + lcol0;
+        if (a.wide && full_n) {
+          uint16_t* cpair = crow - fq * 4 + poff;
+#pragma unroll
+          for (int n = 0; n < 8; n += 2) {
+            uint2 w0, w1;
+            w0.x = pack2<DT>(o[n][0], o[n][1]);
+            w0.y = pack2<DT>(o[n][2], o[n][3]);
+            w1.x = pack2<DT>(o[n + 1][0], o[n + 1][1]);
+            w1.y = pack2<DT>(o[n + 1][2], o[n + 1][3]);
+            *reinterpret_cast<uint4*>(cpair + n * 16) = pair16(w0, w1);
+          }
+          continue;
+        }
 #pragma unroll
         for (int n = 0; n < 8; ++n) {
           if (!full_n && col0 + n * 16 >= a.n) break;
@@ -930,7 +1052,10 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
   }
 }
 
-template <int DT, int EPI>
+// DIAG (timing-only builds, LCQ_GEMM_DIAG; outputs wrong): bit 0 = operand descriptors with
+// zero records (every LDS-DMA load dropped: no memory traffic, same instruction stream), bit 1
+// = no s_barrier in the K loop (the counted waits stay)
+template <int DT, int EPI, int DIAG = 0>
 __global__ void __launch_bounds__(256, 1) k_gemm16(Args a) {
   constexpr bool FP16 = DT == LCQ_F16;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -938,13 +1063,21 @@ __global__ void __launch_bounds__(256, 1) k_gemm16(Args a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1;
   const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   int tm, tn;
-  if (!slot_tile(a, wgid, tm, tn)) return;
+  if (a.order == 1) {
+    if (!tile_nb(a, bid, tm, tn)) return;
+  } else {
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    if (!slot_tile(a, wgid, tm, tn)) return;
+  }
   const int64_t nk = a.k / SKT;
   Stage4 st;
   make_stage16<EPI>(a, tm, tn, w, lane, st);
+  if constexpr (DIAG & 1) {
+    st.ra = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, (short)0, 0, 0x00020000);
+    st.rb[0] = st.rb[1] = st.ra;
+  }
 
   v4f acc[8][8];
 #pragma unroll
@@ -967,7 +1100,64 @@ __global__ void __launch_bounds__(256, 1) k_gemm16(Args a) {
     for (int k = 0; k < 2; ++k) af[0][m2][k] = read_frag(lds, wr * 8 + m2, k, lane);
   asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
 
-  for (int64_t t = 0; t < nk; ++t) ktile16<FP16>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
+  for (int64_t t = 0; t < nk; ++t)
+    ktile16<FP16, DIAG>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  epi16<DT, EPI>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
+}
+
+template <int DT, int EPI, int DIAG = 0>
+__global__ void __launch_bounds__(256, 1) k_gemm16b(Args a) {
+  constexpr bool FP16 = DT == LCQ_F16;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  int tm, tn;
+  if (a.order == 1) {
+    if (!tile_nb(a, bid, tm, tn)) return;
+  } else {
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    if (!slot_tile(a, wgid, tm, tn)) return;
+  }
+  const int64_t nk = a.k / SKT;
+  Stage4 st;
+  make_stage16<EPI>(a, tm, tn, w, lane, st);
+  if constexpr (DIAG & 1) {
+    st.ra = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, (short)0, 0, 0x00020000);
+    st.rb[0] = st.rb[1] = st.ra;
+  }
+
+  v4f acc[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s af[2][2][2], bf[2][8][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_piece(st, lds, 0, 0, w, i);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_piece(st, lds, 1, nk > 1 ? SKT * 2 : 0, w, i);
+  wait_barrier<22>();
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) bf[0][n][k] = read_frag(lds + TILE_B, wc * 8 + n, k, lane);
+#pragma unroll
+  for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) af[0][m2][k] = read_frag(lds, wr * 8 + m2, k, lane);
+  asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
+
+  int64_t t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile16b<FP16, 0, DIAG>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
+    ktile16b<FP16, 1, DIAG>(acc, bf, af, st, lds, t + 1, nk, w, wr, wc, lane);
+  }
+  if (t < nk) ktile16b<FP16, 0, DIAG>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 
   epi16<DT, EPI>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
@@ -1466,14 +1656,19 @@ static void plan(Args& a, int64_t tile_n) {
   a.cpb = (a.n_nt + 7) / 8;
   const int bands = (a.n_mt + 3) / 4;
   a.nslots = 32 * bands * a.cpb;
+  // N-band-major order when the M extent fills whole 32-tile regions (every XCD busy);
+  // LCQ_GEMM_ORDER=0/1 forces one (read per launch: A/B probes flip it between calls)
+  const char* e = getenv("LCQ_GEMM_ORDER");
+  a.order = e ? (e[0] == '1') : 0;
+  if (a.order == 1) a.nslots = 256 * ((a.n_mt + 31) / 32) * a.cpb;
 }
 
 template <int DT, int EPI>
 static int launch(Args& a, hipStream_t st) {
   // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
-  // default: the 4-wave 16x16x32 kernel, one tile per workgroup; LCQ_GEMM_KERNEL=p
-  // (persistent) | w4x32 | w8 select the probes
-  static const char* sel = getenv("LCQ_GEMM_KERNEL");
+  // default: k_gemm16b (4-wave 16x16x32, B fragments double-buffered, one tile per
+  // workgroup); LCQ_GEMM_KERNEL=a (k_gemm16) | p (persistent) | r (ring) | w4 | w8 select probes
+  const char* sel = getenv("LCQ_GEMM_KERNEL");  // per launch: A/B probes flip it
   if (sel && sel[0] == 'w' && sel[1] == '8') {
     (void)hipFuncSetAttribute((const void*)k_gemm256<DT, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF_B);
@@ -1486,7 +1681,23 @@ static int launch(Args& a, hipStream_t st) {
     (void)hipFuncSetAttribute((const void*)k_gemm16r<DT, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, NBR * BUFR);
     hipLaunchKernelGGL((k_gemm16r<DT, EPI>), dim3((unsigned)a.nslots), 256, NBR * BUFR, st, a);
-  } else if (!(sel && sel[0] == 'p') || a.k < 2 * SKT) {  // one tile per workgroup
+  } else if (const char* dg = (EPI == EPI_STORE && DT == LCQ_BF16) ? getenv("LCQ_GEMM_DIAG")
+                                                                   : nullptr) {
+    const int d = dg[0] - '0';  // timing-only diagnostic builds (outputs wrong)
+    const bool b = !(sel && sel[0] == 'a');
+    auto k = d == 1 ? (b ? k_gemm16b<DT, EPI, 1> : k_gemm16<DT, EPI, 1>)
+           : d == 2 ? (b ? k_gemm16b<DT, EPI, 2> : k_gemm16<DT, EPI, 2>)
+           : d == 3 ? (b ? k_gemm16b<DT, EPI, 3> : k_gemm16<DT, EPI, 3>)
+                    : (b ? k_gemm16b<DT, EPI, 0> : k_gemm16<DT, EPI, 0>);
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * BUF4);
+    hipLaunchKernelGGL(k, dim3((unsigned)a.nslots), 256, 2 * BUF4, st, a);
+  } else if (!sel || sel[0] == 'b' || (sel[0] == 'p' && a.k < 2 * SKT)) {
+    // the default: B fragments double-buffered in registers, one tile per workgroup
+    (void)hipFuncSetAttribute((const void*)k_gemm16b<DT, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
+    hipLaunchKernelGGL((k_gemm16b<DT, EPI>), dim3((unsigned)a.nslots), 256, 2 * BUF4, st, a);
+  } else if (sel[0] != 'p') {  // LCQ_GEMM_KERNEL=a: single B register set (previous default)
     (void)hipFuncSetAttribute((const void*)k_gemm16<DT, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
     hipLaunchKernelGGL((k_gemm16<DT, EPI>), dim3((unsigned)a.nslots), 256, 2 * BUF4, st, a);
@@ -1524,7 +1735,167 @@ static int check_common(int dtype, const void* x, int64_t lda, int64_t m, int64_
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// GPTQ Hessian SYRK on the k_gemm16b core (hessian256.hip's lcq_hessian_accum, LCQ_SYRK=16):
+// H = beta*H + alpha * X^T X over the upper-triangle 256^2 tiles of the transposed, zero
+// padded X^T panels (A = B = XT rows, k-contiguous), split-K over `ns` slabs when the
+// triangle has few tiles. Tile order: slot -> (ti, tj) in chunks of 4 x 8 tiles walked band
+// by band (12 panels per 32 tiles of one XCD), as k_syrk256.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool syrk_slot_tile(int slot, int nt, int& ti, int& tj) {
+  int b = 0, rem = slot >> 5;
+  while (true) {
+    const int nch = (nt - 4 * b + 7) / 8;
+    if (rem < nch) break;
+    rem -= nch;
+    ++b;
+  }
+  const int s = slot & 31;
+  ti = 4 * b + (s >> 3);
+  tj = 4 * b + rem * 8 + (s & 7);
+  return ti < nt && tj < nt && tj >= ti;
+}
+
+struct SyrkArgs16 {
+  const uint16_t* xt;
+  int64_t kp, ic, icp;
+  float* H;
+  float* part;
+  float alpha, beta;
+  int nt, ns, nslots;
+  int64_t ktps;
+};
+
+template <bool FP16>
+__global__ void __launch_bounds__(256, 1) k_syrk16(SyrkArgs16 s) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int slot = wgid % s.nslots, split = wgid / s.nslots;
+  int ti, tj;
+  if (!syrk_slot_tile(slot, s.nt, ti, tj)) return;
+  const int64_t kt0 = (int64_t)split * s.ktps;
+  int64_t nk = s.kp / SKT - kt0;
+  if (nk > s.ktps) nk = s.ktps;
+  Args a{};  // the GEMM view of this split: A = B = XT (k from column kt0 * 64 on)
+  a.a = s.xt + kt0 * SKT;
+  a.lda = s.kp;
+  a.m = s.icp;
+  a.k = nk * SKT;
+  a.b[0] = a.a;
+  a.bend[0] = s.icp;
+  a.ldb = s.kp;
+  a.n = s.icp;
+  a.nseg = 1;
+  Stage4 st;
+  make_stage16<EPI_STORE>(a, ti, tj, w, lane, st);
+
+  v4f acc[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s af[2][2][2], bf[2][8][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_piece(st, lds, 0, 0, w, i);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_piece(st, lds, 1, nk > 1 ? SKT * 2 : 0, w, i);
+  wait_barrier<22>();
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) bf[0][n][k] = read_frag(lds + TILE_B, wc * 8 + n, k, lane);
+#pragma unroll
+  for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) af[0][m2][k] = read_frag(lds, wr * 8 + m2, k, lane);
+  asm volatile("s_nop 4" ::: "memory");
+
+  int64_t t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile16b<FP16, 0>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
+    ktile16b<FP16, 1>(acc, bf, af, st, lds, t + 1, nk, w, wr, wc, lane);
+  }
+  if (t < nk) ktile16b<FP16, 0>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  // acc[m][n][jj] (swapped layout): H row i = ti*256 + wr*128 + m*16 + fr, columns
+  // tj*256 + wc*128 + n*16 + fq*4 + jj
+  const int fr = lane & 15, fq = lane >> 4;
+  const int64_t i0 = (int64_t)ti * ST + wr * 128 + fr;
+  const int64_t j0 = (int64_t)tj * ST + wc * 128 + fq * 4;
+  if (s.ns > 1) {
+    float* P = s.part + (int64_t)split * s.icp * s.icp;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        *reinterpret_cast<float4*>(P + (i0 + m * 16) * s.icp + j0 + n * 16) =
+            make_float4(acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]);
+    return;
+  }
+  const bool diag = ti == tj;
+  const bool vec = (s.ic & 3) == 0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int64_t i = i0 + m * 16;
+    if (i >= s.ic) break;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int64_t j = j0 + n * 16;
+      if (j >= s.ic) break;
+      float o[4];
+      const bool full = vec && j + 3 < s.ic;
+      float h[4] = {0.f, 0.f, 0.f, 0.f};
+      if (s.beta != 0.f) {
+        if (full) {
+          const float4 hv = *reinterpret_cast<const float4*>(s.H + i * s.ic + j);
+          h[0] = hv.x; h[1] = hv.y; h[2] = hv.z; h[3] = hv.w;
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            if (j + jj < s.ic) h[jj] = s.H[i * s.ic + j + jj];
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        float v = __fmul_rn(s.alpha, acc[m][n][jj]);
+        if (s.beta != 0.f) v = __fadd_rn(__fmul_rn(s.beta, h[jj]), v);
+        o[jj] = v;
+      }
+      if (full) {
+        *reinterpret_cast<float4*>(s.H + i * s.ic + j) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (j + jj < s.ic) s.H[i * s.ic + j + jj] = o[jj];
+      }
+      if (!diag) {  // mirror H[j + jj][i]
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (j + jj < s.ic) s.H[(j + jj) * s.ic + i] = o[jj];
+      }
+    }
+  }
+}
+
 }  // namespace g256
+
+// host launcher used by lcq_hessian_accum (hessian256.hip) for LCQ_SYRK=16
+int syrk16_launch(const uint16_t* xt, int64_t kp, int64_t ic, int64_t icp, float* H,
+                  float* part, float alpha, float beta, int nt, int ns, int nslots,
+                  int64_t ktps, bool fp16, hipStream_t st) {
+  g256::SyrkArgs16 s{xt, kp, ic, icp, H, part, alpha, beta, nt, ns, nslots, ktps};
+  auto k = fp16 ? g256::k_syrk16<true> : g256::k_syrk16<false>;
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            2 * g256::BUF4);
+  hipLaunchKernelGGL(k, dim3((unsigned)(nslots * ns)), 256, 2 * g256::BUF4, st, s);
+  return check_launch("lcq_hessian_accum: syrk16");
+}
 }  // namespace lcq
 
 using namespace lcq;
@@ -1555,6 +1926,9 @@ extern "C" int lcq_gemm(const void* a, int dtype, int64_t lda, int64_t m, int64_
     g.ldc[s] = ldc[s];
   }
   g.n = end;
+  g.wide = 1;
+  for (int s = 0; s < nseg; ++s)
+    if (!aligned16(c[s]) || ldc[s] % 8 != 0) g.wide = 0;
   plan(g, ST);
   return dispatch<EPI_STORE>(dtype, g, as_stream(stream));
 }
@@ -1575,6 +1949,7 @@ extern "C" int lcq_gemm_silu_mul(const void* a, int dtype, int64_t lda, int64_t 
   g.b[1] = reinterpret_cast<const uint16_t*>(up);
   g.c[0] = reinterpret_cast<uint16_t*>(h);
   g.ldc[0] = ldh;
+  g.wide = aligned16(h) && ldh % 8 == 0;
   plan(g, 128);
   return dispatch<EPI_SILU>(dtype, g, as_stream(stream));
 }

@@ -24,6 +24,8 @@
 //    in a fixed order by k_syrk_reduce (deterministic: no float atomics).
 #include "lcq_common.h"
 
+#include <stdlib.h>
+
 namespace lcq {
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -429,6 +431,18 @@ extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t 
                   : nullptr;
   a.alpha = alpha; a.beta = beta; a.nt = nt; a.ntiles = ntiles; a.ns = ns; a.kt_per_split = ktps;
   a.nslots = n_slots(nt);
+  const char* sk = getenv("LCQ_SYRK");  // 256: the 8-wave k_syrk256 (previous default)
+  if (!(sk && sk[0] == '2')) {
+    // default: the 4-wave projection-GEMM core (gemm256.hip k_gemm16b schedule)
+    rc = syrk16_launch(xt, kp, ic, icp, a.H, a.part, alpha, beta, nt, ns, a.nslots, ktps,
+                       x_dtype == LCQ_F16, st);
+    if (rc) return rc;
+    if (ns > 1) {
+      hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)ntiles, ST), 256, 0, st, a);
+      rc = check_launch("lcq_hessian_accum: reduce");
+    }
+    return rc;
+  }
   // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
   (void)hipFuncSetAttribute((const void*)k_syrk256<false>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF_B);

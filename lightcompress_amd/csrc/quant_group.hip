@@ -36,6 +36,7 @@ struct QuantArgs {
   void* s_out;
   void* z_out;
   int qp_scalar;  // static: one fp32 scale / zero used at full precision (0-dim CPU operands)
+  int nozp;       // static: round_zp False (quant.py:701-707): round(x / s.clamp_min(1e-9) + z)
 };
 
 __device__ __forceinline__ float ld_rt(const void* p, int dt, int64_t i) {
@@ -86,6 +87,12 @@ __device__ __forceinline__ void qdq8_mk(const float (&w)[8], float s, float rs, 
     q[j] = t;
     dq[j] = rnd<CT>(rnd<CT>(t - z) * s);
   }
+}
+
+__device__ __forceinline__ float round_dt(float v, int dt) {
+  if (dt == LCQ_BF16) return rnd<LCQ_BF16>(v);
+  if (dt == LCQ_F16) return rnd<LCQ_F16>(v);
+  return v;
 }
 
 __device__ __forceinline__ void store_fq8(void* fq, int dt, int64_t e0, const float (&v)[8]) {
@@ -270,7 +277,20 @@ __global__ void __launch_bounds__(256) k_quant_static(QuantArgs a) {
       z = rnd<CT>(z);
     }
     float q[8], dq[8];
-    qdq8<CT>(w, s, z, a.qmin, a.qmax, q, dq);
+    if (a.nozp) {
+      // scales.clamp_min(1e-9) in the scales' dtype, then the quotient + zeros rounded once
+      // more before torch.round; dequant is the same (q - z) * s
+      const float sc = rnd<CT>(round_dt(fmaxf(s, 1e-9f), a.s_dt));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = rintf(rnd<CT>(rnd<CT>(w[j] / sc) + z));
+        t = fminf(fmaxf(t, a.qmin), a.qmax);
+        q[j] = t;
+        dq[j] = rnd<CT>(rnd<CT>(t - z) * s);
+      }
+    } else {
+      qdq8<CT>(w, s, z, a.qmin, a.qmax, q, dq);
+    }
     emit<CT>(a, e0, q, dq);
   }
 }
@@ -415,13 +435,12 @@ extern "C" int lcq_int_quant_dynamic(const void* x, int x_dtype, int64_t rows, i
   }
 }
 
-extern "C" int lcq_int_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols,
-                                    int64_t group, const void* scales, int s_dtype,
-                                    const void* zeros, int z_dtype, int ct_dtype, int qmin,
-                                    int qmax, void* fq_out, int fq_dtype, void* codes_out,
-                                    int codes_dtype, void* packed_out, int pack_bits,
-                                    void* stream) {
-  int rc = common_checks("lcq_int_quant_static", x_dtype, rows, cols, group, qmin, qmax,
+static int int_quant_static(const char* fn, int nozp, const void* x, int x_dtype, int64_t rows,
+                            int64_t cols, int64_t group, const void* scales, int s_dtype,
+                            const void* zeros, int z_dtype, int ct_dtype, int qmin, int qmax,
+                            void* fq_out, int fq_dtype, void* codes_out, int codes_dtype,
+                            void* packed_out, int pack_bits, void* stream) {
+  int rc = common_checks(fn, x_dtype, rows, cols, group, qmin, qmax,
                          fq_out, fq_dtype, codes_out, codes_dtype, packed_out, pack_bits);
   if (rc) return rc;
   LCQ_REQUIRE(scales != nullptr, "scales required");
@@ -434,13 +453,34 @@ extern "C" int lcq_int_quant_static(const void* x, int x_dtype, int64_t rows, in
   a.rows = rows; a.cols = cols; a.group = group;
   a.qmin = (float)qmin; a.qmax = (float)qmax; a.sym = zeros == nullptr;
   a.fq = fq_out; a.fq_dt = fq_dtype; a.codes = codes_out; a.codes_dt = codes_dtype;
-  a.packed = packed_out; a.pack_bits = pack_bits;
+  a.packed = packed_out; a.pack_bits = pack_bits; a.nozp = nozp;
   hipStream_t st = as_stream(stream);
   switch (x_dtype) {
     case LCQ_F32: return launch_static_x<LCQ_F32>(a, ct_dtype, st);
     case LCQ_BF16: return launch_static_x<LCQ_BF16>(a, ct_dtype, st);
     default: return launch_static_x<LCQ_F16>(a, ct_dtype, st);
   }
+}
+
+extern "C" int lcq_int_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                                    int64_t group, const void* scales, int s_dtype,
+                                    const void* zeros, int z_dtype, int ct_dtype, int qmin,
+                                    int qmax, void* fq_out, int fq_dtype, void* codes_out,
+                                    int codes_dtype, void* packed_out, int pack_bits,
+                                    void* stream) {
+  return int_quant_static("lcq_int_quant_static", 0, x, x_dtype, rows, cols, group, scales,
+                          s_dtype, zeros, z_dtype, ct_dtype, qmin, qmax, fq_out, fq_dtype,
+                          codes_out, codes_dtype, packed_out, pack_bits, stream);
+}
+
+extern "C" int lcq_int_quant_static_nozp(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                                         int64_t group, const void* scales, int s_dtype,
+                                         const void* zeros, int z_dtype, int ct_dtype, int qmin,
+                                         int qmax, void* fq_out, int fq_dtype, void* codes_out,
+                                         int codes_dtype, void* stream) {
+  return int_quant_static("lcq_int_quant_static_nozp", 1, x, x_dtype, rows, cols, group, scales,
+                          s_dtype, zeros, z_dtype, ct_dtype, qmin, qmax, fq_out, fq_dtype,
+                          codes_out, codes_dtype, nullptr, 0, stream);
 }
 
 extern "C" int lcq_int_quant_static_scalar(const void* x, int x_dtype, int64_t rows,

@@ -133,7 +133,7 @@ class GPTQ(BaseBlockwiseQuantization):
         """OWQ: groups past the last quantized column keep the construction qparams the
         reference seeded `groups` with (search_group_qparams, gptq.py:383-396; only the
         searched ones are overwritten) -- merged into buf_scales / buf_zeros in group order."""
-        if r['scales'] is None:
+        if r['scales'] is None or self.wquantizer.granularity != 'per_group':
             return r
         ng_all = -(-cols // self.wquantizer.group_size)
         ng_q = r['scales'].shape[0] // rows_total

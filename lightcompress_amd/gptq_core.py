@@ -355,13 +355,21 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
         def col_qparams(cols_view):
             _, _, sg, zg = wquantizer._mse(cols_view.contiguous())
             return sg, zg
-    if owq_nout and group is None:
-        raise NotImplementedError('OWQ supports per_group weights on the device path')
     if prepared is None:
         prepared = prepare_hessian(H, actorder, percdamp, owq_nout)
     U, perm, dead = prepared
     Wp = prepare_weight(W, perm, dead)
     ncq = Wp.shape[1] - int(owq_nout)
+    owq_fixed = None
+    if owq_nout and group is None:
+        # gptq.py:157-166: OWQ per_channel takes its qparams from the permuted, dead-zeroed
+        # fp32 non-outlier columns (they replace buf_scales / buf_zeros)
+        Wn = Wp[:, :ncq]
+        pad = (-ncq) % 8  # the grouped kernel reads 8-column chunks: repeat a column (same
+        if pad:           # row min / max) up to the next multiple of 8
+            Wn = torch.cat([Wn, Wn[:, :1].expand(-1, pad)], 1)
+        _, fs, fz, _, _ = wquantizer.get_tensor_qparams(Wn.contiguous())
+        owq_fixed = fixed = (fs, None if sym else fz)
     col_group = None
     if static_groups and group is not None:
         # gptq.py:224-227: permuted column j quantizes with groups[perm[j] // group_size], the
@@ -389,6 +397,8 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
                               col_group=col_group, ncols_q=ncq, col_qparams=col_qparams)
     invperm = torch.argsort(perm) if perm is not None else None
     weight = Wp[:, invperm] if invperm is not None else Wp
+    if owq_fixed is not None:
+        s, z = owq_fixed
     return dict(weight=weight, scales=None if s is None else s.reshape(-1, 1),
                 zeros=None if z is None else z.reshape(-1, 1), perm=perm, invperm=invperm,
                 loss=None if L is None else L.sum())

@@ -79,8 +79,9 @@ def int_quant_static(x: torch.Tensor, group: int, scales: torch.Tensor,
                      ct_dtype: torch.dtype, fq: bool = True,
                      fq_dtype: torch.dtype | None = None,
                      codes_dtype: torch.dtype | None = None,
-                     pack_bits: int | None = None) -> dict:
-    """Quantize ``x`` [rows, cols] with given per-group scales/zeros (flat group order)."""
+                     pack_bits: int | None = None, round_zp: bool = True) -> dict:
+    """Quantize ``x`` [rows, cols] with given per-group scales/zeros (flat group order).
+    ``round_zp=False``: quant.py:701-707 (``round(x / s.clamp_min(1e-9) + z)``)."""
     assert x.dim() == 2
     rows, cols = x.shape
     group = cols if group in (0, None) else int(group)
@@ -105,6 +106,15 @@ def int_quant_static(x: torch.Tensor, group: int, scales: torch.Tensor,
         pf = 32 // pack_bits
         packed_t = torch.empty((rows, (cols + pf - 1) // pf), dtype=torch.int32, device=x.device)
         res['packed'] = packed_t
+    if not round_zp:
+        if pack_bits:
+            raise ValueError('round_zp=False codes are not packed')
+        N.call('lcq_int_quant_static_nozp', N.ptr(x), N.dt(x), rows, cols, group,
+               N.ptr(scales), N.dt(scales), N.ptr(zeros),
+               N.dt(zeros) if zeros is not None else 0, N.dt(ct_dtype), int(qmin), int(qmax),
+               N.ptr(fq_t), N.dt(fq_dtype) if fq else 0,
+               N.ptr(codes_t), N.dt(codes_dtype) if codes_t is not None else 0, N.stream_of(x))
+        return res
     N.call('lcq_int_quant_static', N.ptr(x), N.dt(x), rows, cols, group,
            N.ptr(scales), N.dt(scales), N.ptr(zeros), N.dt(zeros) if zeros is not None else 0,
            N.dt(ct_dtype), int(qmin), int(qmax),
@@ -871,3 +881,37 @@ def mse_qparams(x2: torch.Tensor, group: int, sym: bool, qmin: int, qmax: int, n
            int(qmax), int(nsteps), float(grid), float(norm), N.ptr(mn), N.ptr(mx), N.ptr(s),
            N.ptr(z), N.stream_of(x2))
     return mn, mx, s, z
+
+
+def minmax_qparams(x2: torch.Tensor, group: int, qmin: int, qmax: int, sym: bool,
+                   round_zp: bool = True):
+    """get_minmax_range + get_qparams (quant.py:132-143, 545-559) per group of `group`
+    contiguous elements, every op in x2's dtype (incl. round_zp False). Returns (scales,
+    zeros | None) [ng] in x2's dtype."""
+    x2 = x2.contiguous()
+    ng = x2.numel() // group
+    s = torch.empty(ng, dtype=x2.dtype, device=x2.device)
+    z = None if sym else torch.empty_like(s)
+    N.call('lcq_minmax_qparams', N.ptr(x2), N.dt(x2), ng, int(group), int(qmin), int(qmax),
+           int(bool(sym)), int(bool(round_zp)), N.ptr(s), N.ptr(z), N.stream_of(x2))
+    return s, z
+
+
+def hqq_proximal(w2: torch.Tensor, group: int, scales: torch.Tensor, zeros: torch.Tensor,
+                 qmin: int, qmax: int, lp_norm: float, beta: float, iters: int):
+    """optimize_weights_proximal (quant.py:588-610, hqq.py:36-61) on fp32 groups of w2.
+    scales / zeros: fp32 [ng] starting qparams. Returns (best scales, zeros, state) where
+    state = device int32 [4] view of {best error (float bits), stopped, iters run, pad}."""
+    if w2.dtype != torch.float32:
+        raise ValueError('hqq works on tensor.float()')
+    w2 = w2.contiguous()
+    ng = w2.numel() // group
+    s = scales.to(torch.float32).reshape(ng).clone()
+    z = zeros.to(torch.float32).reshape(ng).clone() if zeros.numel() == ng else \
+        torch.full((ng,), float(zeros), dtype=torch.float32, device=w2.device)
+    ws = torch.empty(int(N.load().lcq_hqq_workspace_bytes(ng)), dtype=torch.uint8, device=w2.device)
+    state = torch.zeros(4, dtype=torch.int32, device=w2.device)
+    N.call('lcq_hqq_proximal', N.ptr(w2), ng, int(group), N.ptr(s), N.ptr(z), int(qmin),
+           int(qmax), float(lp_norm), float(beta), int(iters), N.ptr(ws), ws.numel(),
+           N.ptr(state), N.stream_of(w2))
+    return s, z, state

@@ -3,7 +3,7 @@ from the YAML config, run the block loop, deploy / save."""
 from __future__ import annotations
 
 from .registry import ALGO_REGISTRY, MODEL_REGISTRY
-from . import awq, gptq, rtn  # noqa: F401  (register algorithms)
+from . import awq, gptq, hqq, rtn  # noqa: F401  (register algorithms)
 from . import deepseekv3, llama, opt  # noqa: F401  (register model adapters)
 
 

@@ -11,7 +11,9 @@ granularity per_group / per_channel / per_token / per_tensor / per_head (+ per_b
 round_zp=True, bit 2..8, dynamic and static qparams, fake quant, real quant (+ vLLM / AutoAWQ
 packing in ``module_utils``); FP8 e4m3 / e5m2 (``FloatQuantizer``); static per-tensor activation
 calibration (static_minmax / static_moving_minmax / static_hist). Not yet supported (raise
-NotImplementedError): mse / hqq / learnable calibration, ``int_indices`` mixed precision, STE rounding, ``rounding`` overrides.
+NotImplementedError): learnable calibration, ``int_indices`` mixed precision, STE rounding,
+``rounding`` overrides. calib_algo mse and hqq (the proximal search, ``lcq_hqq_proximal``) and
+round_zp False run on the device.
 """
 from __future__ import annotations
 
@@ -66,6 +68,11 @@ class BaseQuantizer:
         self.mse_b_num = kwargs.get('mse_b_num', 1)
         self.maxshrink = kwargs.get('maxshrink', 0.8)
         self.mse_grid = kwargs.get('mse_grid', 100)
+        # hqq config (quant.py:87-101)
+        self.lp_norm = kwargs.get('lp_norm', 0.7)
+        self.beta = kwargs.get('beta', 10)
+        self.kappa = kwargs.get('kappa', 1.01)
+        self.iters = kwargs.get('iters', 20)
 
     # -- layout helpers (quant.py:612-658) --------------------------------------------------
     def reshape_tensor(self, tensor, allow_padding=False):
@@ -126,10 +133,10 @@ class BaseQuantizer:
         raise NotImplementedError(f'granularity {g} is not on the device path yet')
 
     def _check_supported(self, args):
-        if self.calib_algo not in _MINMAX_LIKE + ('mse',):
+        if self.calib_algo not in _MINMAX_LIKE + ('mse', 'hqq'):
             raise NotImplementedError(f'calib_algo={self.calib_algo} is not on the device path')
-        if not self.round_zp:
-            raise NotImplementedError('round_zp=False is not on the device path')
+        if not self.round_zp and self.calib_algo == 'mse':
+            raise NotImplementedError('round_zp=False with mse is not on the device path')
         for k in ('int_indices', 'rounding'):
             if k in args:
                 raise NotImplementedError(f'args[{k!r}] is not on the device path')
@@ -252,8 +259,30 @@ class IntegerQuantizer(BaseQuantizer):
             am = torch.max(mx.abs(), mn.abs()).clamp(min=1e-5)
             return am / qmax, torch.tensor(0.0), qmax, qmin
         s = (mx - mn).clamp(min=1e-5) / (qmax - qmin)
+        if not self.round_zp:
+            return s, qmin - (mn / s), qmax, qmin
         z = (qmin - torch.round(mn / s)).clamp(qmin, qmax)
         return s, z, qmax, qmin
+
+    def _hqq_or_nozp(self, tensor):
+        """qparams of the two paths the lane kernel does not fuse: calib_algo hqq
+        (get_hqq_qparams, quant.py:680-689: tensor.float(), minmax qparams, the proximal
+        search on the device) and minmax with round_zp False. Returns (x2, group, scales [ng],
+        zeros [ng] | None, compute dtype)."""
+        if self.granularity not in ('per_group', 'per_channel', 'per_token', 'per_head'):
+            raise NotImplementedError(f'{self.calib_algo} / round_zp with {self.granularity}')
+        qmin, qmax = self._iq
+        if self.calib_algo == 'hqq':
+            x2, group = self._kernel_view(tensor.float().contiguous())
+            s, z = ops.minmax_qparams(x2, group, qmin, qmax, self.sym, self.round_zp)
+            if z is None:  # sym: zeros = torch.tensor(0.0) until the first update
+                z = torch.zeros_like(s)
+            s, z, _ = ops.hqq_proximal(x2, group, s, z, qmin, qmax, self.lp_norm, self.beta,
+                                       self.iters)
+            return x2, group, s, z, torch.float32
+        x2, group = self._kernel_view(tensor.contiguous())
+        s, z = ops.minmax_qparams(x2, group, qmin, qmax, self.sym, round_zp=False)
+        return x2, group, s, z, tensor.dtype
 
     def _mse(self, tensor):
         """(x2, group, scales [ng] fp32, zeros [ng] fp32 | None) from the MSE range search."""
@@ -267,9 +296,24 @@ class IntegerQuantizer(BaseQuantizer):
                                      float(self.mse_grid))
         return x2, group, s, z
 
+    def get_hqq_qparams(self, tensor, args={}):
+        """quant.py:680-689: (reshaped tensor.float(), best scales, zeros, qmax, qmin)."""
+        _, _, s, z, _ = self._hqq_or_nozp(tensor)
+        dev = tensor.device
+        return (self.reshape_tensor(tensor.float()), s.view(-1, 1), z.view(-1, 1),
+                self.qmax.to(dev), self.qmin.to(dev))
+
     def get_tensor_qparams(self, tensor, args={}):
         """quant.py:690-697: (reshaped tensor, scales, zeros, qmax, qmin)."""
         self._check_supported(args)
+        if self.calib_algo == 'hqq':
+            return self.get_hqq_qparams(tensor, args)
+        if not self.round_zp and self.calib_algo != 'mse':
+            _, _, s, z, _ = self._hqq_or_nozp(tensor)
+            dev = tensor.device
+            zeros = z.view(-1, 1) if not self.sym else torch.tensor(0.0)
+            return (self.reshape_tensor(tensor), s.view(-1, 1), zeros, self.qmax.to(dev),
+                    self.qmin.to(dev))
         if self.calib_algo == 'mse':  # fp32 qparams from the search over tensor.float()
             _, _, s, z = self._mse(tensor)
             dev = tensor.device
@@ -296,6 +340,8 @@ class IntegerQuantizer(BaseQuantizer):
         t2 = tensor.reshape(-1, tensor.shape[-1]).contiguous()
         s = scales.contiguous()
         if s.dim() == 0 and (not torch.is_tensor(zeros) or zeros.dim() == 0):
+            if not self.round_zp:
+                raise NotImplementedError('round_zp=False with 0-dim qparams')
             # per-tensor qparams as 0-dim tensors (static act qparams, per_tensor weights):
             # torch-CPU uses them as scalars at full precision, results in the tensor's dtype
             qmin, qmax = self._iq
@@ -326,9 +372,10 @@ class IntegerQuantizer(BaseQuantizer):
         qmin, qmax = self._iq
         if want == 'codes':
             r = ops.int_quant_static(t2, group, s, zz, qmin, qmax, ct_dtype=ct, fq=False,
-                                     codes_dtype=torch.int32)
+                                     codes_dtype=torch.int32, round_zp=self.round_zp)
             return r['codes'].to(ct).reshape(tensor.shape)
-        r = ops.int_quant_static(t2, group, s, zz, qmin, qmax, ct_dtype=ct, fq=True)
+        r = ops.int_quant_static(t2, group, s, zz, qmin, qmax, ct_dtype=ct, fq=True,
+                                 round_zp=self.round_zp)
         return r['fq'].reshape(tensor.shape)
 
     def quant(self, tensor, scales, zeros, qmax, qmin):
@@ -357,6 +404,12 @@ class IntegerQuantizer(BaseQuantizer):
             x2, group, s, z = self._mse(w)
             fq = ops.int_quant_static(x2, group, s, z, qmin, qmax, ct_dtype=torch.float32,
                                       fq_dtype=w.dtype)['fq'].reshape(shape)
+            return fq.T if tr else fq
+        if self.calib_algo == 'hqq' or not self.round_zp:
+            # hqq: quant_dequant of tensor.float() with fp32 qparams, then .to(weight dtype)
+            x2, group, s, z, ct = self._hqq_or_nozp(w)
+            fq = ops.int_quant_static(x2, group, s, z, qmin, qmax, ct_dtype=ct, fq_dtype=w.dtype,
+                                      round_zp=self.round_zp)['fq'].reshape(shape)
             return fq.T if tr else fq
         x2, group = self._kernel_view(w.contiguous())
         fq = ops.int_quant_dynamic(x2, group, qmin, qmax, self.sym, qparams=False)['fq']
@@ -389,12 +442,19 @@ class IntegerQuantizer(BaseQuantizer):
             r = ops.int_quant_static(x2, group, s, z, qmin, qmax, ct_dtype=torch.float32,
                                      fq=False, codes_dtype=cd)
             r['scales'], r['zeros'] = s, (z if z is not None else None)
+        elif self.calib_algo == 'hqq' or not self.round_zp:
+            x2, group, s, z, ct = self._hqq_or_nozp(weight)
+            r = ops.int_quant_static(x2, group, s, z, qmin, qmax, ct_dtype=ct, fq=False,
+                                     codes_dtype=cd, round_zp=self.round_zp)
+            r['scales'], r['zeros'] = s, z
         else:
             r = ops.int_quant_dynamic(x2, group, qmin, qmax, self.sym, fq=False,
                                       codes_dtype=cd)
         codes = r['codes'].reshape(weight.shape)
         scales = r['scales'] * osf if osf != 1 else r['scales']
-        zeros = r['zeros'].to(cd) if not self.sym else None
+        zeros = None
+        if not self.sym:  # quant.py:938-941: float zeros kept when round_zp is False
+            zeros = r['zeros'].to(cd) if self.round_zp else r['zeros']
         qshape = 1 if self.granularity == 'per_tensor' else (codes.shape[0], -1)
         if zeros is not None:
             zeros = zeros.view(qshape)

@@ -165,9 +165,20 @@ def deploy_fake(weight, scales, zeros, perm, invperm, bit, sym, group, model_dty
 
 def quantize_layer_owq(W: torch.Tensor, H: torch.Tensor, nout: int, bit=4, sym=False, group=128,
                        percdamp=0.01, blocksize=128):
-    """GPTQ + OWQ layer transform; returns dict like quantize_layer (+ n_nonout)."""
+    """GPTQ + OWQ layer transform; returns dict like quantize_layer (+ n_nonout).
+    group=None: per_channel -- the qparams of the permuted non-outlier columns
+    (gptq.py:157-166, get_tensor_qparams(W[:, :n_nonout]) on the fp32 weights)."""
     Wp, U, perm = prepare_owq(W, H, nout, percdamp)
     ncq = Wp.shape[1] - nout
+    if group is None:
+        qmin, qmax = Q.int_range(bit, sym)
+        mn, mx = Q.minmax(Wp[:, :ncq], 'per_channel')
+        fs, fz = Q.qparams(mn, mx, qmin, qmax, sym)
+        tmp, Losses, _, _ = column_loop(Wp, U, bit, sym, None, blocksize, fixed=(fs, fz),
+                                        ncols_q=ncq)
+        invperm = torch.argsort(perm)
+        return dict(weight=tmp[:, invperm], scales=fs, zeros=None if sym else fz, perm=perm,
+                    invperm=invperm, U=U, n_nonout=ncq, loss=Losses.sum().item())
     tmp, Losses, s, z = column_loop(Wp, U, bit, sym, group, blocksize, ncols_q=ncq)
     invperm = torch.argsort(perm)
     return dict(weight=tmp[:, invperm], scales=s.reshape(-1, 1),
@@ -179,6 +190,7 @@ def deploy_fake_owq(weight, scales, zeros, perm, invperm, n_nonout, bit, sym, gr
                     model_dtype):
     """GPTQ.w_qdq with OWQ (gptq.py:424-452): the float outlier columns are put back."""
     w = weight[:, perm]
-    out = Q.fake_quant_static(w, scales, zeros, bit, sym, 'per_group', group).to(model_dtype)
+    gran = 'per_group' if group else 'per_channel'
+    out = Q.fake_quant_static(w, scales, zeros, bit, sym, gran, group).to(model_dtype)
     out[:, n_nonout:] = w[:, n_nonout:].to(model_dtype)
     return out[:, invperm]

@@ -197,3 +197,69 @@ def mse_range(t: torch.Tensor, bit: int, sym: bool, maxshrink=0.8, grid=100, nor
         mn[better] = lo[better]
         mx[better] = hi[better]
     return mn, mx
+
+
+def qparams_nozp(mn, mx, qmin, qmax, sym: bool):
+    """quant.py:545-559 with round_zp False: zeros = qmin - min / scales (no round, no clamp)."""
+    if sym:
+        return qparams(mn, mx, qmin, qmax, sym)
+    s = (mx - mn).clamp(min=1e-5) / (qmax - qmin)
+    return s, qmin - (mn / s)
+
+
+def quant_nozp(t, s, z, qmin, qmax):
+    """quant.py:703-707 (round_zp False)."""
+    return torch.clamp(torch.round(t / s.clamp_min(1e-9) + z), qmin, qmax)
+
+
+def hqq_proximal(t: torch.Tensor, s, z, qmin, qmax, lp_norm=0.7, beta=10, iters=20):
+    """optimize_weights_proximal (quant.py:588-610) on fp32 groups t [ng, gs]. shrink_op
+    (quant.py:92-101) uses the quantizer's own beta (the lambda reads self.beta), so the
+    kappa schedule never reaches it. The zeros of the stopping iteration are kept."""
+    if lp_norm == 1:
+        def shrink(x):
+            return torch.sign(x) * torch.nn.functional.relu(torch.abs(x) - 1.0 / beta)
+    else:
+        def shrink(x):
+            return torch.sign(x) * torch.nn.functional.relu(
+                torch.abs(x) - (1.0 / beta) * torch.pow(torch.abs(x), lp_norm - 1))
+    best = 1e4
+    s = 1 / s
+    for _ in range(iters):
+        wq = torch.round(t * s + z).clamp(qmin, qmax)
+        wr = (wq - z) / s
+        we = shrink(t - wr)
+        z = torch.mean(wq - (t - we) * s, axis=-1, keepdim=True)
+        err = float(torch.abs(t - wr).mean())
+        if err < best:
+            best = err
+        else:
+            break
+    return 1 / s, z
+
+
+def hqq_qparams(w, bit, sym, granularity='per_group', group=128, round_zp=True, lp_norm=0.7,
+                beta=10, iters=20):
+    """get_hqq_qparams (quant.py:680-689): (fp32 groups, scales, zeros, qmin, qmax)."""
+    qmin, qmax = int_range(bit, sym)
+    t = group_view(w.float(), granularity, group)
+    mn, mx = minmax(t, granularity)
+    s, z = (qparams if round_zp else qparams_nozp)(mn, mx, qmin, qmax, sym)
+    s, z = hqq_proximal(t, s, z, qmin, qmax, lp_norm, beta, iters)
+    return t, s, z, qmin, qmax
+
+
+def fake_quant_hqq(w, bit, sym, granularity='per_group', group=128, round_zp=True, **kw):
+    """fake_quant_weight_dynamic with calib_algo hqq: quant_dequant of tensor.float()."""
+    t, s, z, qmin, qmax = hqq_qparams(w, bit, sym, granularity, group, round_zp, **kw)
+    q = quant(t, s, z, qmin, qmax) if round_zp else quant_nozp(t, s, z, qmin, qmax)
+    return dequant(q, s, z).reshape(w.shape).to(w.dtype), s, z
+
+
+def fake_quant_nozp(w, bit, sym, granularity='per_group', group=128):
+    """fake_quant_weight_dynamic with calib_algo minmax and round_zp False (dtype of w)."""
+    qmin, qmax = int_range(bit, sym)
+    t = group_view(w, granularity, group)
+    mn, mx = minmax(t, granularity)
+    s, z = qparams_nozp(mn, mx, qmin, qmax, sym)
+    return dequant(quant_nozp(t, s, z, qmin, qmax), s, z).reshape(w.shape).to(w.dtype), s, z

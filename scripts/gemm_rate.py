@@ -6,6 +6,7 @@ rounds in one process (rule 24), median of rounds.
 usage: python scripts/gemm_rate.py [--m 65536] [--rounds 5] [--iters 10]
 """
 import argparse
+import os
 import statistics
 import sys
 from pathlib import Path
@@ -28,6 +29,20 @@ def timeit(fn, iters):
     return e0.elapsed_time(e1) / iters
 
 
+_SET = set()
+
+
+def setenv(v):
+    for k in list(_SET):
+        os.environ.pop(k, None)
+    _SET.clear()
+    if v != '-':
+        for kv in v.split('+'):
+            k, val = kv.split('=')
+            os.environ[k] = val
+            _SET.add(k)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--m', type=int, default=65536)
@@ -36,7 +51,11 @@ def main():
     ap.add_argument('--hidden', type=int, default=4096)
     ap.add_argument('--inter', type=int, default=14336)
     ap.add_argument('--kv', type=int, default=1024)
+    ap.add_argument('--variants', default='-',
+                    help="comma list of env settings to A/B, e.g. '-,LCQ_GEMM_KERNEL=b' "
+                         "('-' = defaults)")
     args = ap.parse_args()
+    orders = args.variants.split(',')
     dev = 'cuda'
     M, H, I, KV = args.m, args.hidden, args.inter, args.kv
     g = torch.Generator(device=dev).manual_seed(0)
@@ -68,20 +87,26 @@ def main():
             2.0 * M * I * H, lambda: ops.linear_sq_diff(xi, wd, org, lb, 0),
             lambda: lb.record(org, F.linear(xi, wd), 0)),
     }
-    res = {k: ([], []) for k in cases}
+    res = {k: ({o: [] for o in orders}, []) for k in cases}
     for name, (fl, f_lcq, f_ref) in cases.items():  # warm up (kernels, allocator)
-        f_lcq(); f_ref()
+        for o in orders:
+            setenv(o)
+            f_lcq()
+        f_ref()
     torch.cuda.synchronize()
     for _ in range(args.rounds):
         for name, (fl, f_lcq, f_ref) in cases.items():
-            res[name][0].append(timeit(f_lcq, args.iters))
+            for o in orders:
+                setenv(o)
+                res[name][0][o].append(timeit(f_lcq, args.iters))
             res[name][1].append(timeit(f_ref, args.iters))
     print(f'M = {M} tokens, median of {args.rounds} rounds x {args.iters} calls (ms, TFLOP/s)')
     for name, (fl, _, _) in cases.items():
-        a = statistics.median(res[name][0])
         b = statistics.median(res[name][1])
-        print(f'{name:34s} lcq {a:8.3f} ms {fl / a / 1e9:7.1f} TF/s | torch {b:8.3f} ms '
-              f'{fl / b / 1e9:7.1f} TF/s | lcq/torch time {a / b:5.3f}')
+        for o in orders:
+            a = statistics.median(res[name][0][o])
+            print(f'{name:30s} lcq[{o}] {a:8.3f} ms {fl / a / 1e9:7.1f} TF/s | torch '
+                  f'{b:8.3f} ms {fl / b / 1e9:7.1f} TF/s | lcq/torch time {a / b:5.3f}')
 
 
 if __name__ == '__main__':

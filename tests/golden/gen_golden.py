@@ -643,6 +643,98 @@ def gen_gptq_owq():
 GENERATORS['gptq_owq'] = gen_gptq_owq
 
 
+def gen_gptq_owq_pc():
+    """GPTQ OWQ with per_channel weights (gptq.py:157-166): the per-channel qparams are taken
+    from the permuted, dead-zeroed fp32 non-outlier columns and replace buf_scales / buf_zeros."""
+    import torch.nn as nn
+    R.init_dist()
+    q = R.quant_module()
+    import llmc.compression.quantization.gptq as gm
+    cases = [
+        # name, oc, ic, bit, sym, n_out, dead_cols
+        ('int4_asym_pc_out6', 160, 384, 4, False, 6, False),
+        ('int8_sym_pc_out16_dead', 96, 256, 8, True, 16, True),
+    ]
+    for i, (name, oc, ic, bit, sym, nout, dead) in enumerate(cases):
+        torch.manual_seed(3100 + i)
+        layer = nn.Linear(ic, oc, bias=False)
+        layer.weight.data = weights(oc, ic, torch.bfloat16, 650 + i, edge=False)
+        xs = _acts(3, 48, ic, 750 + i)
+        if dead:
+            for x in xs:
+                x[..., 5] = 0
+        obj = gm.GPTQ.__new__(gm.GPTQ)
+        obj.wquantizer = q.IntegerQuantizer(bit, sym, 'per_channel')
+        obj.dev = torch.device('cpu')
+        obj.model_dtype = torch.bfloat16
+        obj.owq, obj.actorder, obj.static_groups = True, False, False
+        obj.percdamp, obj.blocksize, obj.chunk_num = 0.01, 128, 1
+        obj.true_sequential = True
+        obj.need_perm = True
+        obj.n_out_dict = {'l': nout}
+        obj.layers_cache = {'l': {}}
+        obj.qparams = {}
+        gm.GPTQ.layer_init(obj, layer, 'l')
+        for x in xs:
+            gm.GPTQ.add_batch(obj, layer, 'l', x, None)
+        H = obj.layers_cache['l']['H'].clone()
+        _, s0, z0, qmax, qmin = obj.wquantizer.get_tensor_qparams(layer.weight.data)
+        layer.register_buffer('buf_scales', s0)
+        layer.register_buffer('buf_zeros', z0)
+        layer.register_buffer('buf_qmax', torch.tensor(qmax))
+        layer.register_buffer('buf_qmin', torch.tensor(qmin))
+        w_in = layer.weight.data.clone()
+        obj.layers_cache['l']['H'] = H.clone()
+        obj.layer_transform(layer, 'l')
+        out = dict(x=torch.cat(xs, 0), w=w_in, H=H, perm=layer.buf_perm,
+                   weight=layer.weight.data.clone(), scales=layer.buf_scales,
+                   zeros=None if sym else layer.buf_zeros,
+                   meta=torch.tensor([bit, int(sym), 0, nout, oc, ic]))
+        out['fq'] = obj.w_qdq(layer, obj.wquantizer)
+        F.save(f'gptqowqpc_{name}', **out)
+    print('gptq owq per_channel fixtures written')
+
+
+GENERATORS['gptq_owq_pc'] = gen_gptq_owq_pc
+
+
+def gen_hqq():
+    """calib_algo hqq (quant.py:588-610, 680-697) and round_zp False (quant.py:545-559,
+    699-707): get_tensor_qparams, fake_quant_weight_dynamic, real_quant_weight_dynamic."""
+    q = R.quant_module()
+    cases = [
+        # name, bit, sym, granularity, group, rows, cols, calib, round_zp, extra kwargs
+        ('hqq_int4_asym_g128_nozp', 4, False, 'per_group', 128, 256, 512, 'hqq', False, {}),
+        ('hqq_int4_asym_g64_rzp', 4, False, 'per_group', 64, 128, 512, 'hqq', True, {}),
+        ('hqq_int3_sym_g128', 3, True, 'per_group', 128, 128, 384, 'hqq', True, {}),
+        ('hqq_int4_asym_pc_l1', 4, False, 'per_channel', None, 96, 768, 'hqq', False,
+         dict(lp_norm=1, beta=20, iters=8)),
+        ('nozp_int4_asym_g128_bf16', 4, False, 'per_group', 128, 256, 512, 'minmax', False, {}),
+        ('nozp_int8_asym_pc_bf16', 8, False, 'per_channel', None, 64, 1024, 'minmax', False, {}),
+        ('nozp_int4_asym_g128_f32', 4, False, 'per_group', 128, 64, 256, 'minmax', False, {}),
+    ]
+    for i, (name, bit, sym, gran, gs, rows, cols, calib, rzp, kw) in enumerate(cases):
+        dt = torch.float32 if name.endswith('f32') else torch.bfloat16
+        w = weights(rows, cols, dt, 1700 + i, edge=False)
+        kwa = dict(calib_algo=calib, round_zp=rzp, **kw)
+        if gs:
+            kwa['group_size'] = gs
+        quant = q.IntegerQuantizer(bit, sym, gran, **kwa)
+        _, s, z, _, _ = quant.get_tensor_qparams(w.clone())
+        fq = quant.fake_quant_weight_dynamic(w.clone())
+        codes, s_rq, z_rq = quant.real_quant_weight_dynamic(w.clone())
+        lp, beta, iters = kw.get('lp_norm', 0.7), kw.get('beta', 10), kw.get('iters', 20)
+        F.save(name, w=w, scales=s, zeros=z if torch.is_tensor(z) and z.dim() else None,
+               fq=fq, codes=codes, zeros_rq=z_rq,
+               meta=torch.tensor([bit, int(sym), gs or 0, int(rzp), int(calib == 'hqq'),
+                                  iters]),
+               hqq=torch.tensor([float(lp), float(beta)]))
+    print('hqq / round_zp fixtures written')
+
+
+GENERATORS['hqq'] = gen_hqq
+
+
 if __name__ == '__main__':
     which = sys.argv[1] if len(sys.argv) > 1 else 'all'
     R.install()

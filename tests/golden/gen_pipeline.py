@@ -155,6 +155,9 @@ def run_reference(name, spec):
     elif spec['quant']['method'] == 'Awq':
         import llmc.compression.quantization.awq as mod
         algo_cls = mod.Awq
+    elif spec['quant']['method'] == 'HQQ':
+        import llmc.compression.quantization.hqq as mod
+        algo_cls = mod.HQQ
     else:
         import llmc.compression.quantization.rtn as mod
         algo_cls = mod.RTN

@@ -58,6 +58,13 @@ CONFIGS = {
                               'act': {'bit': 8, 'symmetric': True, 'granularity': 'per_tensor',
                                       'static': True, 'calib_algo': 'static_hist'}},
                     'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}, 'diag': False},
+    # configs/quantization/methods/HQQ/hqq_w_only.yml (data-free; axis 0: groups along OC)
+    'hqq': {'quant': {'method': 'HQQ',
+                      'weight': {'bit': 4, 'symmetric': False, 'granularity': 'per_group',
+                                 'group_size': 128, 'round_zp': False},
+                      'special': {'axis': 0, 'lp_norm': 0.7, 'beta': 10, 'kappa': 1.01,
+                                  'iters': 20}},
+            'calib': None},
     'rtn': {'quant': {'method': 'RTN',
                       'weight': {'bit': 8, 'symmetric': True, 'granularity': 'per_channel'}},
             'calib': None},

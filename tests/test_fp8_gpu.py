@@ -325,3 +325,21 @@ def test_fp8_gemm_split_k_matches_unsplit_and_is_deterministic(dev):
     tol = 1e-5 * _abs_gemm(a, a_s, b, b_s) + 1e-30
     assert ((split1.cpu() - want).abs() <= tol).all()
     assert ((one.cpu() - want).abs() <= tol).all()
+
+
+def test_fp8_gemm_f16_default_dtype(dev):
+    """out_dtype follows torch.get_default_dtype() as in the reference's Triton kernel: with an
+    fp16 default the GEMM stores fp16 (split and unsplit paths)."""
+    from lightcompress_amd import kernel
+    for M in (24, 96):
+        a, a_s, b, b_s = _gemm_inputs(M, 384, 1024 if M == 24 else 7168, seed=12 + M)
+        prev = torch.get_default_dtype()
+        torch.set_default_dtype(torch.float16)
+        try:
+            got = kernel.fp8_gemm(a.to(dev), a_s.to(dev), b.to(dev), b_s.to(dev)).cpu()
+        finally:
+            torch.set_default_dtype(prev)
+        assert got.dtype == torch.float16 and got.shape == (M, 384)
+        want = O.fp8_gemm(a, a_s, b, b_s)
+        tol = 1e-5 * _abs_gemm(a, a_s, b, b_s) + want.abs() * 2.0 ** -11
+        assert ((got.float() - want).abs() <= tol).all()

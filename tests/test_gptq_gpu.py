@@ -476,3 +476,45 @@ def test_owq_plugin_layer_vs_reference(dev, name):
     outl = c['perm'][ic - nout:]
     torch.testing.assert_close(fq[:, outl].float(), c['fq'][:, outl].float(), rtol=2e-2,
                                atol=1e-3)
+
+
+@pytest.mark.parametrize('name', F.names('gptqowqpc_'))
+def test_owq_per_channel_plugin_layer_vs_reference(dev, name):
+    """GPTQ plugin layer_transform with OWQ and per_channel weights (gptq.py:157-166): the
+    per-channel qparams come from the permuted non-outlier fp32 columns (bit-exact), deployed
+    weights >= 99.9 % bit-equal (T2)."""
+    from lightcompress_amd.gptq import GPTQ
+    from lightcompress_amd.gptq_core import HessianAccumulator
+    from lightcompress_amd.quant import IntegerQuantizer
+    c = F.load(name)
+    bit, sym, _, nout, oc, ic = c['meta'].tolist()
+    sym = bool(sym)
+    wq = IntegerQuantizer(bit, sym, 'per_channel')
+    layer = torch.nn.Linear(ic, oc, bias=False, device=dev, dtype=torch.bfloat16)
+    layer.weight.data = c['w'].to(dev)
+    _, s0, z0, _, _ = wq.get_tensor_qparams(layer.weight.data)
+    layer.register_buffer('buf_scales', s0)
+    if not sym:
+        layer.register_buffer('buf_zeros', z0)
+    layer.register_buffer('buf_qmax', wq.qmax.clone().to(dev))
+    layer.register_buffer('buf_qmin', wq.qmin.clone().to(dev))
+    obj = GPTQ.__new__(GPTQ)
+    obj.wquantizer = wq
+    obj.actorder, obj.static_groups, obj.percdamp, obj.owq = False, False, 0.01, True
+    obj.need_perm = True
+    obj.n_out_dict = {'l': nout}
+    obj.model_dtype = torch.bfloat16
+    acc = HessianAccumulator(ic, dev)
+    for x in c['x']:
+        acc.add_batch(x.unsqueeze(0).to(dev))
+    obj.layers_cache = {'l': {'acc': acc, 'owner': True, 'columns': ic}}
+    obj.parallel_mode = lambda: 'single'
+    obj.layer_transform(layer, 'l')
+    assert torch.equal(layer.buf_perm.cpu(), c['perm'])
+    assert layer.buf_scales.dtype == torch.float32
+    torch.testing.assert_close(layer.buf_scales.cpu(), c['scales'], rtol=1e-6, atol=0)
+    if not sym:
+        torch.testing.assert_close(layer.buf_zeros.cpu(), c['zeros'], rtol=0, atol=0)
+    fq = obj.w_qdq(layer, wq).cpu()
+    same = (fq == c['fq']).float().mean().item()
+    assert same >= 0.999, same

@@ -162,3 +162,19 @@ def test_mse_layer_matches_reference(name):
                        gs, torch.bfloat16)
     agree = (fq == c['fq']).float().mean().item()
     assert agree > 0.999, agree
+
+
+@pytest.mark.parametrize('name', F.names('gptqowqpc_'))
+def test_owq_per_channel_matches_reference(name):
+    """OWQ per_channel (gptq.py:157-166): per-channel qparams of the permuted non-outlier
+    columns, column loop with them, w_qdq with the outliers restored."""
+    c = F.load(name)
+    bit, sym, _, nout, oc, ic = _meta_owq(c)
+    r = G.quantize_layer_owq(c['w'], c['H'], nout, bit, sym, None)
+    assert torch.equal(r['perm'], c['perm'])
+    torch.testing.assert_close(r['scales'], c['scales'], rtol=1e-6, atol=0)
+    same_w = (r['weight'] == c['weight']).float().mean().item()
+    assert same_w > 0.999, same_w
+    fq = G.deploy_fake_owq(c['weight'], c['scales'], c.get('zeros'), c['perm'],
+                           torch.argsort(c['perm']), ic - nout, bit, sym, None, torch.bfloat16)
+    assert torch.equal(fq, c['fq'])

@@ -89,3 +89,30 @@ def test_mse_oracle_matches_reference(name):
     t = c['w'].reshape(-1, gs) if gs else c['w']
     mn, mx = Q.mse_range(t, bit, bool(sym))
     assert torch.equal(mn, c['rmin']) and torch.equal(mx, c['rmax'])
+
+
+HQQ_CASES = F.names('hqq_') + F.names('nozp_')
+
+
+def _hqq_meta(c):
+    bit, sym, gs, rzp, hqq, iters = c['meta'].tolist()
+    lp, beta = c['hqq'].tolist()
+    return bit, bool(sym), gs or None, bool(rzp), bool(hqq), iters, lp, beta
+
+
+@pytest.mark.parametrize('name', HQQ_CASES)
+def test_hqq_and_nozp_oracle_matches_reference(name):
+    """calib_algo hqq (quant.py:588-610, 680-689) and round_zp False (quant.py:545-559,
+    701-707): qparams and fake quant of the oracle equal the reference's."""
+    c = F.load(name)
+    bit, sym, gs, rzp, hqq, iters, lp, beta = _hqq_meta(c)
+    gran = 'per_group' if gs else 'per_channel'
+    if hqq:
+        fq, s, z = Q.fake_quant_hqq(c['w'], bit, sym, gran, gs, round_zp=rzp, lp_norm=lp,
+                                    beta=beta, iters=iters)
+    else:
+        fq, s, z = Q.fake_quant_nozp(c['w'], bit, sym, gran, gs)
+    assert torch.equal(s, c['scales'])
+    if 'zeros' in c:
+        assert torch.equal(z, c['zeros'])
+    assert torch.equal(fq, c['fq'])

@@ -188,3 +188,81 @@ def test_mse_qparams_vs_reference(dev, name):
     assert (fq == c['fq']).float().mean().item() >= 0.99
     codes, _, _ = q.real_quant_weight_dynamic(w)
     assert (codes.cpu().to(torch.int32) == c['codes'].to(torch.int32)).float().mean().item() >= 0.99
+
+
+def _hqq_quantizer(c):
+    from lightcompress_amd.quant import IntegerQuantizer
+    bit, sym, gs, rzp, hqq, iters = c['meta'].tolist()
+    lp, beta = c['hqq'].tolist()
+    kw = dict(calib_algo='hqq' if hqq else 'minmax', round_zp=bool(rzp))
+    if hqq:
+        kw.update(lp_norm=lp, beta=beta, iters=iters)
+    if gs:
+        kw['group_size'] = gs
+    return IntegerQuantizer(bit, bool(sym), 'per_group' if gs else 'per_channel', **kw), bool(hqq)
+
+
+@pytest.mark.parametrize('name', F.names('nozp_'))
+def test_round_zp_false_vs_reference(dev, name):
+    """round_zp False (quant.py:545-559, 701-707, 937-941): float zeros qmin - min / s,
+    quant round(x / s.clamp_min(1e-9) + z): qparams, fake quant and codes bit-exact, zeros of
+    the real quant kept float."""
+    c = F.load(name)
+    q, _ = _hqq_quantizer(c)
+    w = c['w'].to(dev)
+    _, s, z, _, _ = q.get_tensor_qparams(w)
+    assert_bit_equal(s.cpu(), c['scales'], 'scales')
+    assert_bit_equal(z.cpu(), c['zeros'], 'zeros')
+    assert_bit_equal(q.fake_quant_weight_dynamic(w).cpu(), c['fq'], 'fq')
+    codes, _, zr = q.real_quant_weight_dynamic(w)
+    assert torch.equal(codes.cpu().to(torch.int32), c['codes'].to(torch.int32))
+    assert_bit_equal(zr.cpu(), c['zeros_rq'], 'real-quant zeros')
+
+
+@pytest.mark.parametrize('name', F.names('hqq_'))
+def test_hqq_vs_reference(dev, name):
+    """calib_algo hqq (optimize_weights_proximal, quant.py:588-610) on the device: scales
+    (1 / (1 / s) of the minmax qparams) bit-exact, zeros (per-group means of the last step)
+    within fp32 summation-order noise for >= 97 % of the groups (a code flipped at a tie moves
+    a mean by 1 / group), fake quant and codes >= 99 % equal (T2: the group means and the global error
+    mean sum in a different order than torch-CPU)."""
+    c = F.load(name)
+    q, _ = _hqq_quantizer(c)
+    w = c['w'].to(dev)
+    _, s, z, _, _ = q.get_tensor_qparams(w)
+    assert_bit_equal(s.cpu(), c['scales'], 'scales')
+    # a zero is a mean over the group: one code flipped at a rounding tie (the running zero
+    # differs in its last bits) moves it by 1 / group -- allowed for a few groups
+    zc, zr = z.cpu().reshape(-1), c['zeros'].reshape(-1)
+    gsz = w.numel() // zr.numel()
+    close = ((zc - zr).abs() <= 1e-5 + 1e-5 * zr.abs()).float().mean().item()
+    assert close >= 0.97, close
+    assert (zc - zr).abs().max().item() <= 2.0 / gsz + 1e-5
+    # elements of a group whose zero moved may round the other way: >= 99 % equal overall
+    # (per_channel cases have ~100 groups, so one moved zero is ~1 % of the tensor)
+    fq = q.fake_quant_weight_dynamic(w).cpu()
+    assert fq.dtype == c['fq'].dtype
+    assert (fq == c['fq']).float().mean().item() >= 0.99
+    codes, _, _ = q.real_quant_weight_dynamic(w)
+    assert (codes.cpu().to(torch.int32) == c['codes'].to(torch.int32)).float().mean().item() \
+        >= 0.99
+
+
+def test_hqq_state_and_early_stop(dev):
+    """The device loop stops where the oracle's does: iteration count and best error."""
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(5)
+    w = (torch.randn(512, 256, generator=g) * 0.02)
+    t = w.reshape(-1, 128)
+    qmin, qmax = Q.int_range(4, False)
+    mn, mx = Q.minmax(t)
+    s0, z0 = Q.qparams(mn, mx, qmin, qmax, False)
+    for iters in (0, 1, 3, 20):
+        s_ref, z_ref = Q.hqq_proximal(t.clone(), s0, z0, qmin, qmax, iters=iters)
+        s, z, st = ops.hqq_proximal(t.to(dev), 128, s0.to(dev), z0.to(dev), 0, 15, 0.7, 10.0,
+                                    iters)
+        assert torch.equal(s.cpu(), s_ref.reshape(-1))
+        d = (z.cpu() - z_ref.reshape(-1)).abs()
+        assert (d <= 1e-6 + 1e-5 * z_ref.abs().reshape(-1)).float().mean().item() >= 0.99
+        assert d.max().item() <= 2.0 / 128 + 1e-6  # a code flipped at a tie: 1 / group
+        assert int(st[2]) <= iters
