@@ -172,7 +172,7 @@ def gemm_roofline(kern, elapsed):
     by = sum(f.get('bytes', 0.0) for f in fam)
     tf = fl / (ms * 1e-3) / 1e12
     traffic, src = pmc_traffic('awq', 'k_gemm16')
-    return {'kernel': 'k_gemm16 (csrc/gemm256.hip): bf16 MFMA projection GEMMs of the AWQ loss '
+    return {'kernel': 'k_gemm16b (csrc/gemm256.hip): bf16 MFMA projection GEMMs of the AWQ loss '
                       'search + calibration forwards, epilogues fused (q/k/v, SiLU*up, loss)',
             'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
             'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4), 'traffic': traffic,
@@ -433,8 +433,8 @@ def bench_gptq(args, rank, world, dev):
     if h:
         # algorithmic: symmetric rank-n update n*ic*(ic+1) flops per launch
         tf = h['flops'] / (h['total_ms'] * 1e-3) / 1e12
-        traffic, src = pmc_traffic('gptq', 'k_syrk256')
-        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_xt_pack + k_syrk256, bf16 MFMA XᵀX)',
+        traffic, src = pmc_traffic('gptq', ('k_xt_pack', 'k_syrk16'))
+        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_xt_pack + k_syrk16, bf16 MFMA XᵀX)',
                            'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
                            'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4),
                            'traffic': traffic, 'traffic_source': src,
@@ -651,7 +651,8 @@ def bench_fp8_forward(args, weights, dev, world):
     t = kern.get('lcq_fp8_gemm')
     if t:
         tf = flops * args.steps / (t['total_ms'] * 1e-3) / 1e12
-        out['roofline'] = {'kernel': 'lcq_fp8_gemm (k_fp8_gemm)', 'bound': 'mfma',
+        out['roofline'] = {'kernel': 'lcq_fp8_gemm (k_fp8_gemm2 on grids of >= 128 256x256 tiles, '
+                                     'else k_fp8_gemm)', 'bound': 'mfma',
                            'achieved': round(tf, 1), 'peak': PEAK_FP8_TFLOPS, 'unit': 'TFLOP/s',
                            'frac': round(tf / PEAK_FP8_TFLOPS, 4), 'traffic': None,
                            'flops_per_launch': flops / len(weights),

@@ -634,8 +634,8 @@ static void launch_scale(const void* x, int64_t rows, int64_t cols, const void* 
                          int axis, void* out, hipStream_t st) {
   const unsigned grid = stream_grid(rows * cols / 8, 256);
   if (op == 0 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 0, 0>), grid, 256, 0, st, x, rows, cols, s, out);
-  if (op == 0 && axis == 1) hipLaunchKernelGGL((k_scale_bcast<DT, 0, 1>), grid, 256, 0, st, x, rows, cols, s, out);
   if (op == 1 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 1, 0>), grid, 256, 0, st, x, rows, cols, s, out);
+  if (op == 0 && axis == 1) hipLaunchKernelGGL((k_scale_bcast<DT, 0, 1>), grid, 256, 0, st, x, rows, cols, s, out);
   if (op == 1 && axis == 1) hipLaunchKernelGGL((k_scale_bcast<DT, 1, 1>), grid, 256, 0, st, x, rows, cols, s, out);
 }
 

@@ -5,8 +5,10 @@
 // called by block_wise_fp8_forward_func (module_utils.py:41-46):
 //   C[m, n] = sum_kb ( sum_{k in block kb} A[m, k] B[n, k] ) * a_s[m, kb] * b_s[n / 128, kb]
 // A [M, K] e4m3 (act_quant output, per-token 128-column scales a_s [M, K/128]); B [N, K] e4m3
-// with 128x128 block scales b_s [ceil(N/128), K/128]; fp32 accumulation; C fp32 or bf16.
+// with 128x128 block scales b_s [ceil(N/128), K/128]; fp32 accumulation; C fp32 / bf16 / fp16.
 //
+// Two kernels: k_fp8_gemm2 (below, 256x256 tiles on the 16x16x128 MFMA) for grids of >= 64
+// tiles, and k_fp8_gemm for short batches:
 // Tile 128x128 (or 64x128 when the grid would be small) per workgroup, 4 waves on gfx950's
 // 32x32x64 f8f6f4 MFMA, one K block of 128 per step double-buffered through LDS (16-byte global
 // loads into registers one block ahead, padded rows); the block's partial dot products are
@@ -448,12 +450,13 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
                   (reinterpret_cast<uintptr_t>(b) & 15) == 0,
               "A / B must be 16-byte aligned");
   const int64_t nkb = K / BK;
-  const char* sel = getenv("LCQ_FP8_GEMM");  // 1: always the 64/128-row 32x32x64 kernel
-  // the 256^2 kernel where its grid fills the chip (>= 128 tiles; measured: 1.46 vs 1.01
-  // PFLOP/s at 2048 x 7168 x 7168, 1.85 vs 1.30 at 8192^3), else the 64/128-row kernel (2x
-  // faster at M 512: the big tile's split-K partials cost more than they save)
+  const char* sel = getenv("LCQ_FP8_GEMM");  // 1 / 2: force the 64/128-row / the 256^2 kernel
+  // the 256^2 kernel on grids of >= 64 tiles (measured: 1.46 vs 1.01 PFLOP/s at 2048 x 7168 x
+  // 7168, 1.85 vs 1.30 at 8192^3, 65 vs 78 us at 2048 x 2048 x 7168 with 4 K splits), else the
+  // 64/128-row kernel (2x faster at M 512: the big tile's split-K partials cost more there)
   const int64_t tiles2 = ((M + T2 - 1) / T2) * ((N + T2 - 1) / T2);
-  if (!(sel && sel[0] == '1') && tiles2 >= 128 && workspace && ws_bytes >= ws2_bytes(M, N, K) &&
+  if (!(sel && sel[0] == '1') && (tiles2 >= 64 || (sel && sel[0] == '2')) && workspace &&
+      ws_bytes >= ws2_bytes(M, N, K) &&
       N % 4 == 0 &&
       M * K < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31)) {
     hipStream_t st = as_stream(stream);

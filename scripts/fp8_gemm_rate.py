@@ -11,8 +11,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from lightcompress_amd import kernel, ops  # noqa: E402
 
 dev = torch.device('cuda:0')
-shapes = [(512, 7168, 2048), (512, 2048, 7168), (2048, 7168, 7168), (4096, 4096, 4096),
-          (8192, 8192, 8192)]
+shapes = [(512, 7168, 2048), (512, 2048, 7168), (2048, 2048, 7168), (2048, 7168, 2048),
+          (2048, 7168, 7168), (4096, 4096, 4096), (8192, 8192, 8192)]
 
 
 def timeit(fn, it=20):
