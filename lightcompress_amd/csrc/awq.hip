@@ -198,6 +198,68 @@ __global__ void __launch_bounds__(256) k_scale_bcast(const void* x, int64_t rows
   }
 }
 
+// Per-column fast path (axis 0): a thread keeps its 8 columns' s (and RN(1/s) for op div)
+// in registers and walks rows, 4 rows in flight, so the hot loop has no 64-bit index
+// division and the quotient is div_mk (3 VALU, Markstein: the IEEE quotient) instead of the
+// ~10-op IEEE sequence. Elements outside the proven range (|x| < 2^-96, |x / s| outside
+// [2^-100, 2^100], zeros, inf / NaN) take the IEEE division, so every output equals
+// round_dt(x / s) of the generic kernel. Block = TPR threads per row x (256 / TPR) rows.
+template <int DT, int OP>
+__global__ void __launch_bounds__(256) k_scale_cols(const void* x, int64_t rows, int64_t cols,
+                                                   const void* s, void* out, int tpr) {
+  const int c8n = (int)(cols >> 3);
+  const int rsub = threadIdx.x / tpr, rpb = 256 / tpr;
+  const int c8 = blockIdx.x * tpr + (int)(threadIdx.x % tpr);
+  if (c8 >= c8n) return;
+  float sv[8], rv[8];
+  ld8<DT>(s, (int64_t)c8 * 8, sv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {  // RN(1/s) must be a normal number for Markstein: else NaN
+    const float as = fabsf(sv[j]);  // (every quotient of the column then takes a / s)
+    rv[j] = (as >= 0x1p-100f && as <= 0x1p100f) ? 1.0f / sv[j] : __builtin_nanf("");
+  }
+  const int64_t rstep = (int64_t)gridDim.y * rpb;
+  int64_t r = (int64_t)blockIdx.y * rpb + rsub;
+  for (; r + 3 * rstep < rows; r += 4 * rstep) {
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ld8<DT>(x, (r + u * rstep) * cols + c8 * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (OP == 0) {
+          v[u][j] = v[u][j] * sv[j];
+        } else {
+          const float a = v[u][j];
+          float q = div_mk(a, sv[j], rv[j]);
+          const float aq = fabsf(q);
+          if (!(fabsf(a) >= 0x1p-96f && aq >= 0x1p-100f && aq <= 0x1p100f)) q = a / sv[j];
+          v[u][j] = q;
+        }
+      }
+      st8<DT>(out, (r + u * rstep) * cols + c8 * 8, v[u]);
+    }
+  }
+  for (; r < rows; r += rstep) {
+    float v[8];
+    ld8<DT>(x, r * cols + c8 * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (OP == 0) {
+        v[j] = v[j] * sv[j];
+      } else {
+        const float a = v[j];
+        float q = div_mk(a, sv[j], rv[j]);
+        const float aq = fabsf(q);
+        if (!(fabsf(a) >= 0x1p-96f && aq >= 0x1p-100f && aq <= 0x1p100f)) q = a / sv[j];
+        v[j] = q;
+      }
+    }
+    st8<DT>(out, r * cols + c8 * 8, v);
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // loss = mean(((a - b) in DT).float()^2): fp64 partial sums per block, fixed-order final sum,
 // result stored as fp32(sum) / n (the reference's fp32 mean) into out[slot].
@@ -632,6 +694,19 @@ extern "C" int lcq_awq_scales_v1(const void* xmean, const void* wmax, int dtype,
 template <int DT>
 static void launch_scale(const void* x, int64_t rows, int64_t cols, const void* s, int op,
                          int axis, void* out, hipStream_t st) {
+  const int64_t c8n = cols / 8;
+  if (axis == 0 && (c8n % 256 == 0 || 256 % c8n == 0) && !getenv("LCQ_SCALE_GENERIC")) {
+    const int tpr = c8n >= 256 ? 256 : (int)c8n;
+    const int64_t bx = (c8n + tpr - 1) / tpr, rpb = 256 / tpr;
+    int64_t by = (2048 + bx - 1) / bx;  // ~8 workgroups per CU
+    const int64_t need = (rows + rpb - 1) / rpb;
+    if (by > need) by = need;
+    if (by > 65535) by = 65535;
+    const dim3 g((unsigned)bx, (unsigned)by);
+    if (op == 0) hipLaunchKernelGGL((k_scale_cols<DT, 0>), g, 256, 0, st, x, rows, cols, s, out, tpr);
+    else hipLaunchKernelGGL((k_scale_cols<DT, 1>), g, 256, 0, st, x, rows, cols, s, out, tpr);
+    return;
+  }
   const unsigned grid = stream_grid(rows * cols / 8, 256);
   if (op == 0 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 0, 0>), grid, 256, 0, st, x, rows, cols, s, out);
   if (op == 1 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 1, 0>), grid, 256, 0, st, x, rows, cols, s, out);

@@ -1756,13 +1756,38 @@ __device__ __forceinline__ bool syrk_slot_tile(int slot, int nt, int& ti, int& t
   return ti < nt && tj < nt && tj >= ti;
 }
 
+// v-th upper-triangle tile in the same 4 x 8 chunk order, counting valid tiles only: the grid
+// is exactly ntiles x ns workgroups, so every XCD's contiguous wgid range holds the same number
+// of live tiles (+-1) and the last round is as full as the tile count allows (no exiting slots
+// that leave one XCD a round longer than the others)
+__device__ __forceinline__ void syrk_valid_tile(int v, int nt, int& ti, int& tj) {
+  for (int b = 0; 4 * b < nt; ++b) {
+    const int nch = (nt - 4 * b + 7) / 8;
+    for (int rem = 0; rem < nch; ++rem) {
+      const int c0 = 4 * b + rem * 8, c1 = min(nt - 1, c0 + 7);
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * b + r;
+        if (i >= nt) break;
+        const int lo = max(i, c0), cnt = c1 >= lo ? c1 - lo + 1 : 0;
+        if (v < cnt) {
+          ti = i;
+          tj = lo + v;
+          return;
+        }
+        v -= cnt;
+      }
+    }
+  }
+  ti = tj = 0;  // not reached for v < nt (nt + 1) / 2
+}
+
 struct SyrkArgs16 {
   const uint16_t* xt;
   int64_t kp, ic, icp;
   float* H;
   float* part;
   float alpha, beta;
-  int nt, ns, nslots;
+  int nt, ns, ntiles;
   int64_t ktps;
 };
 
@@ -1775,9 +1800,9 @@ __global__ void __launch_bounds__(256, 1) k_syrk16(SyrkArgs16 s) {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int slot = wgid % s.nslots, split = wgid / s.nslots;
+  const int split = wgid / s.ntiles;
   int ti, tj;
-  if (!syrk_slot_tile(slot, s.nt, ti, tj)) return;
+  syrk_valid_tile(wgid - split * s.ntiles, s.nt, ti, tj);
   const int64_t kt0 = (int64_t)split * s.ktps;
   int64_t nk = s.kp / SKT - kt0;
   if (nk > s.ktps) nk = s.ktps;
@@ -1887,13 +1912,13 @@ __global__ void __launch_bounds__(256, 1) k_syrk16(SyrkArgs16 s) {
 
 // host launcher used by lcq_hessian_accum (hessian256.hip) for LCQ_SYRK=16
 int syrk16_launch(const uint16_t* xt, int64_t kp, int64_t ic, int64_t icp, float* H,
-                  float* part, float alpha, float beta, int nt, int ns, int nslots,
+                  float* part, float alpha, float beta, int nt, int ns, int ntiles,
                   int64_t ktps, bool fp16, hipStream_t st) {
-  g256::SyrkArgs16 s{xt, kp, ic, icp, H, part, alpha, beta, nt, ns, nslots, ktps};
+  g256::SyrkArgs16 s{xt, kp, ic, icp, H, part, alpha, beta, nt, ns, ntiles, ktps};
   auto k = fp16 ? g256::k_syrk16<true> : g256::k_syrk16<false>;
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                             2 * g256::BUF4);
-  hipLaunchKernelGGL(k, dim3((unsigned)(nslots * ns)), 256, 2 * g256::BUF4, st, s);
+  hipLaunchKernelGGL(k, dim3((unsigned)(ntiles * ns)), 256, 2 * g256::BUF4, st, s);
   return check_launch("lcq_hessian_accum: syrk16");
 }
 }  // namespace lcq

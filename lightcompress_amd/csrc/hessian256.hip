@@ -20,8 +20,8 @@
 //    raw s_barrier, never vmcnt(0) in the loop.
 //  * Tile order is XCD-aware: each XCD's 32 concurrent workgroups take a 4x8 block of tiles
 //    (bijective blockIdx remap + slot_tile), so 12 operand panels feed 32 tiles from L2.
-//  * Few tiles (ic 4096: 136) -> split-K over `ns` slabs written to the workspace and combined
-//    in a fixed order by k_syrk_reduce (deterministic: no float atomics).
+//  * Split-K over `ns` slabs (count from a round-filling cost model, plan()) written to the
+//    workspace and combined in a fixed order by k_syrk_reduce (deterministic: no float atomics).
 #include "lcq_common.h"
 
 #include <stdlib.h>
@@ -377,6 +377,15 @@ __global__ void __launch_bounds__(256) k_syrk_reduce(SyrkArgs a) {
 
 static int64_t ceil_to(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
+// Split-K count. The k_syrk16 grid is ntiles x ns workgroups, one per CU (128 KB LDS), in
+// contiguous wgid ranges per XCD (8 XCDs x 32 CUs), so a launch takes
+// rounds = ceil(ceil(ntiles * ns / 8) / 32) waves of workgroups, each ~(ktps + 6) K-tile
+// times long (6 ~ prologue + the 256 KB fp32 tile store); every split adds a 256 KB partial
+// tile written and re-read by k_syrk_reduce (~0.034 K-tile times at HBM rate). Pick the ns
+// with the least modelled time: at n = 262144 ic 4096 (136 tiles) ns 15 fills 8 rounds to
+// 99.6 % where ns 8 left a 5th round a quarter full; ic 8192 (528 tiles) ns 8 instead of 1.
+// At least 8 K-tiles per split; partial slabs capped at 8 GiB. LCQ_SYRK_NS forces a count
+// (A/B probes: scripts/probes/syrk_ns_sweep.py).
 static void plan(int64_t n, int64_t ic, int& nt, int& ntiles, int& ns, int64_t& ktps,
                  int64_t& kp, int64_t& icp) {
   icp = ceil_to(ic, ST);
@@ -384,14 +393,26 @@ static void plan(int64_t n, int64_t ic, int& nt, int& ntiles, int& ns, int64_t& 
   nt = (int)(icp / ST);
   ntiles = nt * (nt + 1) / 2;
   const int64_t nkt = kp / SKT;
-  ns = 1;
-  if (ntiles < 512) {
-    int64_t want = (1024 + ntiles - 1) / ntiles;
-    int64_t cap = nkt / 8 > 0 ? nkt / 8 : 1;
-    ns = (int)(want < cap ? want : cap);
-    if (ns < 1) ns = 1;
+  const char* force = getenv("LCQ_SYRK_NS");
+  int64_t best_ns = 1;
+  if (force && atoi(force) > 0) {
+    best_ns = atoi(force);
+  } else {
+    double best = 1e300;
+    for (int64_t c = 1; c <= 256; ++c) {
+      if (c > 1 && (nkt / c < 8 || c * icp * icp * 4 > (int64_t(8) << 30))) break;
+      const int64_t per = (nkt + c - 1) / c, cc = (nkt + per - 1) / per;
+      const int64_t per_xcd = (ntiles * cc + 7) / 8, rounds = (per_xcd + 31) / 32;
+      const double cost = (double)rounds * (double)(per + 6) +
+                          (cc > 1 ? 0.034 * (double)(cc * ntiles) + 0.07 * ntiles : 0.0);
+      if (cost < best * 0.995) {
+        best = cost;
+        best_ns = cc;
+      }
+    }
   }
-  ktps = (nkt + ns - 1) / ns;
+  if (best_ns > nkt) best_ns = nkt;
+  ktps = (nkt + best_ns - 1) / best_ns;
   ns = (int)((nkt + ktps - 1) / ktps);
 }
 
@@ -434,7 +455,7 @@ extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t 
   const char* sk = getenv("LCQ_SYRK");  // 256: the 8-wave k_syrk256 (previous default)
   if (!(sk && sk[0] == '2')) {
     // default: the 4-wave projection-GEMM core (gemm256.hip k_gemm16b schedule)
-    rc = syrk16_launch(xt, kp, ic, icp, a.H, a.part, alpha, beta, nt, ns, a.nslots, ktps,
+    rc = syrk16_launch(xt, kp, ic, icp, a.H, a.part, alpha, beta, nt, ns, ntiles, ktps,
                        x_dtype == LCQ_F16, st);
     if (rc) return rc;
     if (ns > 1) {

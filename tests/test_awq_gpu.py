@@ -162,3 +162,36 @@ def test_awq_weight_scale_vs_oracle(dev, rows, cols, group, nl):
     ws = [(torch.randn(rows, cols, generator=g) * 0.02).to(torch.bfloat16) for _ in range(nl)]
     got = ops.awq_weight_scale([w.to(dev) for w in ws], group).cpu()
     assert torch.equal(bits(got), bits(A.weight_scale(ws, group)))
+
+
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
+def test_scale_bcast_cols_every_x_every_scale(dev, dt):
+    """The per-column fast path (k_scale_cols: Markstein quotient from RN(1/s), IEEE division
+    outside its proven range): every finite bf16 x in every column against 1024 scales
+    covering every bf16 mantissa across exponents -16..15 (plus tiny / huge / near-1 scales),
+    bit-equal to torch-CPU's x / s and x * s."""
+    from lightcompress_amd import ops
+    allb = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    fin = allb[torch.isfinite(allb.float())]
+    mant = torch.arange(128, dtype=torch.int32)
+    exps = torch.arange(127 - 16, 127 + 16, dtype=torch.int32)
+    sb = ((exps.view(-1, 1) << 7) | mant.view(1, -1)).reshape(-1)[::4]  # 1024 positive bf16
+    s = sb.to(torch.int16).view(torch.bfloat16)
+    s[:4] = torch.tensor([1e-35, 3e-30, 1e30, 3e35]).to(torch.bfloat16)
+    s = s.to(dt)
+    s = torch.where(torch.isfinite(s.float()) & (s.float() != 0), s, torch.ones_like(s))
+    nc = s.numel()
+    idx = (torch.arange(fin.numel()).view(-1, 1) + torch.arange(nc).view(1, -1) * 37) % fin.numel()
+    x = fin[idx].to(dt)
+    ib = torch.int16
+    for op, ref in (('div', x / s.view(1, -1)), ('mul', x * s.view(1, -1))):
+        got = ops.scale_bcast(x.to(dev), s.to(dev), op).cpu()
+        same = got.view(ib) == ref.view(ib)
+        same |= got.isnan() & ref.isnan()
+        assert bool(same.all()), (op, int((~same).sum()))
+    # a 4096-wide layout (512 threads' worth of columns per row: two workgroups per row span)
+    x4 = x[:4096].reshape(-1, 4096)[:, :4096].contiguous()
+    s4 = s.repeat(4)
+    ref = x4 / s4.view(1, -1)
+    got = ops.scale_bcast(x4.to(dev), s4.to(dev), 'div').cpu()
+    assert torch.equal(got.view(ib), ref.view(ib))
