@@ -275,6 +275,28 @@ int lcq_auto_clip_search(const void* w, const void* x, int dtype, int64_t oc, in
                          int qmax, int sym, int clip_sym, int mse_steps, const void* mse_p,
                          float norm, void* best_max, void* best_min, void* stream);
 
+/* lcq_auto_clip_search with activation fake-quant (w_only False: auto_clip.py:176-177,
+ * fake_quantize_input at :269-274): the shrink steps multiply the weights with qx [T, ic] (the
+ * aquantizer's fake_quant_act_dynamic of x viewed [1, T, ic/group, group]), the original
+ * outputs with x. qx NULL == lcq_auto_clip_search. */
+int lcq_auto_clip_search_act(const void* w, const void* x, const void* qx, int dtype, int64_t oc,
+                             int64_t ic, int64_t T, int group, int nsteps, const void* factors,
+                             int qmin, int qmax, int sym, int clip_sym, int mse_steps,
+                             const void* mse_p, float norm, void* best_max, void* best_min,
+                             void* stream);
+
+/* AutoClipper.auto_clip_layer for per_channel integer weights (group = ic, auto_clip.py:96-99;
+ * awq_w8a8.yml): w [oc, ic] (ic % 128 == 0), x [T, ic] sampled tokens, qx [T, ic] their
+ * activation fake-quant or NULL (weight-only), nsteps <= 10 with factors[nsteps] =
+ * fp32(1 - i/n_grid) on device; best_max / best_min [oc] in dtype. Products rounded to dtype
+ * like the reference's broadcast product; the ic-long fp32 sum runs in k order (parity tier
+ * T2). workspace >= lcq_auto_clip_pc_workspace_bytes(oc, T, nsteps). */
+int64_t lcq_auto_clip_pc_workspace_bytes(int64_t oc, int64_t T, int nsteps);
+int lcq_auto_clip_search_pc(const void* w, const void* x, const void* qx, int dtype, int64_t oc,
+                            int64_t ic, int64_t T, int nsteps, const void* factors, int qmin,
+                            int qmax, int sym, int clip_sym, void* workspace, int64_t ws_bytes,
+                            void* best_max, void* best_min, void* stream);
+
 /* AutoClipper.apply_clip, v1 (auto_clip.py:193-212): out = clamp(x, cmin, cmax) per group;
  * cmin NULL -> -cmax. In place allowed. */
 int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t cols, int64_t group,

@@ -71,6 +71,11 @@ SIGNATURES = {
     'lcq_sq_diff_mean': ([_vp, _vp, _int, _i64, _vp, _int, _vp, _int, _vp], _int),
     'lcq_auto_clip_search': ([_vp, _vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int, _int,
                               _int, _int, _int, _vp, _f32, _vp, _vp, _vp], _int),
+    'lcq_auto_clip_search_act': ([_vp, _vp, _vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int,
+                                  _int, _int, _int, _int, _vp, _f32, _vp, _vp, _vp], _int),
+    'lcq_auto_clip_pc_workspace_bytes': ([_i64, _i64, _int], _i64),
+    'lcq_auto_clip_search_pc': ([_vp, _vp, _vp, _int, _i64, _i64, _i64, _int, _vp, _int, _int,
+                                 _int, _int, _vp, _i64, _vp, _vp, _vp], _int),
     'lcq_clip_apply': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _vp, _vp], _int),
     'lcq_absmax': ([_vp, _int, _i64, _vp, _vp, _vp], _int),
     'lcq_fp8_quant': ([_vp, _int, _i64, _i64, _i64, _int, _int, _f32, _f32, _int, _vp, _vp, _vp,

@@ -3,6 +3,8 @@
 ``auto_clip_layer`` is one HIP launch per linear (``lcq_auto_clip_search``): the reference
 materialises a [256, T, ng, 128] bf16 broadcast product per shrink step and batch of rows
 (1 GiB at ng=32); the kernel keeps weights in VGPRs and streams token tiles through LDS.
+per_channel weights (group = ic, the w8a8 AWQ configs) take ``lcq_auto_clip_search_pc``;
+w_only False feeds the shrink steps the activation fake-quant (``fake_quantize_input``).
 """
 from __future__ import annotations
 
@@ -33,9 +35,6 @@ class AutoClipper:
         self.shard_rows = False           # shard_search: each rank searches its row range
         if clip_version != 'v1':
             raise NotImplementedError('clip_version v2 (learnable) is not on the device path')
-        if not w_only:
-            raise NotImplementedError('auto-clip with activation fake-quant is not on the '
-                                      'device path yet')
 
     @torch.no_grad()
     def run(self, block, block_idx, input_feat, n_sample_token):
@@ -90,15 +89,27 @@ class AutoClipper:
             raise NotImplementedError('auto-clip over several calibration tensors')
         if w.dtype not in (torch.bfloat16, torch.float16):
             raise NotImplementedError('device auto-clip kernel takes bf16 / fp16 weights')
-        if group not in (32, 64, 128, 256):
+        per_channel = wq.granularity == 'per_channel'
+        if not per_channel and group not in (32, 64, 128, 256):
             raise NotImplementedError(f'device auto-clip kernel: group size {group}')
+        if per_channel and (w.shape[1] % 128 or wq.calib_algo == 'mse'):
+            raise NotImplementedError('per_channel auto-clip: ic % 128 == 0, minmax qparams')
+        if getattr(wq, 'quant_type', 'int-quant') != 'int-quant':
+            raise NotImplementedError('auto-clip of float-quant weights is not on the device '
+                                      'path')
         x = self.sample_tokens(inputs[0], n_sample_token)
+        qx = None
+        if not self.w_only:
+            # fake_quantize_input (auto_clip.py:269-274) sees x as [1, T, ic/group, group]:
+            # per_token act quant then runs per (token, group) (reshape_tensor is a no-op)
+            qx = self.aquantizer.fake_quant_act_dynamic(
+                x.reshape(1, x.shape[0], -1, group)).reshape(x.shape)
         qmin, qmax = int(wq.qmin.item()), int(wq.qmax.item())
         mse = None
         if wq.calib_algo == 'mse':  # every step's fake quant searches its range
             mse = (wq._mse_nsteps(), wq.mse_grid, 2.4)
         return ops.auto_clip_search(w.data, x, group, int(max_shrink * n_grid), n_grid, qmin,
-                                    qmax, wq.sym, self.clip_sym, mse=mse)
+                                    qmax, wq.sym, self.clip_sym, mse=mse, qx=qx)
 
     @torch.no_grad()
     def apply_clip(self, block_idx, layer, min_val, max_val, layer_name):

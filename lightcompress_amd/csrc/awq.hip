@@ -198,68 +198,6 @@ __global__ void __launch_bounds__(256) k_scale_bcast(const void* x, int64_t rows
   }
 }
 
-// Per-column fast path (axis 0): a thread keeps its 8 columns' s (and RN(1/s) for op div)
-// in registers and walks rows, 4 rows in flight, so the hot loop has no 64-bit index
-// division and the quotient is div_mk (3 VALU, Markstein: the IEEE quotient) instead of the
-// ~10-op IEEE sequence. Elements outside the proven range (|x| < 2^-96, |x / s| outside
-// [2^-100, 2^100], zeros, inf / NaN) take the IEEE division, so every output equals
-// round_dt(x / s) of the generic kernel. Block = TPR threads per row x (256 / TPR) rows.
-template <int DT, int OP>
-__global__ void __launch_bounds__(256) k_scale_cols(const void* x, int64_t rows, int64_t cols,
-                                                   const void* s, void* out, int tpr) {
-  const int c8n = (int)(cols >> 3);
-  const int rsub = threadIdx.x / tpr, rpb = 256 / tpr;
-  const int c8 = blockIdx.x * tpr + (int)(threadIdx.x % tpr);
-  if (c8 >= c8n) return;
-  float sv[8], rv[8];
-  ld8<DT>(s, (int64_t)c8 * 8, sv);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {  // RN(1/s) must be a normal number for Markstein: else NaN
-    const float as = fabsf(sv[j]);  // (every quotient of the column then takes a / s)
-    rv[j] = (as >= 0x1p-100f && as <= 0x1p100f) ? 1.0f / sv[j] : __builtin_nanf("");
-  }
-  const int64_t rstep = (int64_t)gridDim.y * rpb;
-  int64_t r = (int64_t)blockIdx.y * rpb + rsub;
-  for (; r + 3 * rstep < rows; r += 4 * rstep) {
-    float v[4][8];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) ld8<DT>(x, (r + u * rstep) * cols + c8 * 8, v[u]);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if constexpr (OP == 0) {
-          v[u][j] = v[u][j] * sv[j];
-        } else {
-          const float a = v[u][j];
-          float q = div_mk(a, sv[j], rv[j]);
-          const float aq = fabsf(q);
-          if (!(fabsf(a) >= 0x1p-96f && aq >= 0x1p-100f && aq <= 0x1p100f)) q = a / sv[j];
-          v[u][j] = q;
-        }
-      }
-      st8<DT>(out, (r + u * rstep) * cols + c8 * 8, v[u]);
-    }
-  }
-  for (; r < rows; r += rstep) {
-    float v[8];
-    ld8<DT>(x, r * cols + c8 * 8, v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if constexpr (OP == 0) {
-        v[j] = v[j] * sv[j];
-      } else {
-        const float a = v[j];
-        float q = div_mk(a, sv[j], rv[j]);
-        const float aq = fabsf(q);
-        if (!(fabsf(a) >= 0x1p-96f && aq >= 0x1p-100f && aq <= 0x1p100f)) q = a / sv[j];
-        v[j] = q;
-      }
-    }
-    st8<DT>(out, r * cols + c8 * 8, v);
-  }
-}
-
 // ----------------------------------------------------------------------------------------
 // loss = mean(((a - b) in DT).float()^2): fp64 partial sums per block, fixed-order final sum,
 // result stored as fp32(sum) / n (the reference's fp32 mean) into out[slot].
@@ -452,7 +390,8 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 we
     k_auto_clip(const uint16_t* __restrict__ w, const uint16_t* __restrict__ x, int64_t oc,
                 int64_t ic, int T, int nsteps, const float* __restrict__ factors, float qmin,
                 float qmax, int sym, int clip_sym, uint16_t* best_max, uint16_t* best_min,
-                int mse_steps, const float* __restrict__ mse_p, float norm) {
+                int mse_steps, const float* __restrict__ mse_p, float norm,
+                const uint16_t* __restrict__ qx) {
   constexpr int CH = G / 2;    // weights per lane: k = 8i + 4h + j, h = lane parity
   constexpr int CHUNKS = G / 8;
   __shared__ __attribute__((aligned(16))) float xs[CT * G];      // <= 32 KB
@@ -485,24 +424,32 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 we
   if (h == 0)
     for (int s = 0; s < nsteps; ++s) es[s * CROWS + r] = 0.f;
 
-  for (int t0 = 0; t0 < T; t0 += CT) {
-    __syncthreads();  // previous tile fully consumed
-    // stage CT token rows of this group as fp32, 8 elements (16 B) per chunk
+  // stage CT token rows of this group as fp32, 8 elements (16 B) per chunk
+  auto stage = [&](const uint16_t* __restrict__ src, int t0) {
     for (int idx = tid; idx < CT * CHUNKS; idx += 2 * CROWS) {
       const int row = idx / CHUNKS, ch = idx % CHUNKS;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (t0 + row < T)
-        v = *reinterpret_cast<const uint4*>(x + (int64_t)(t0 + row) * ic + g * G + ch * 8);
+        v = *reinterpret_cast<const uint4*>(src + (int64_t)(t0 + row) * ic + g * G + ch * 8);
       float a[8];
       widen4<DT>(make_uint2(v.x, v.y), a);
       widen4<DT>(make_uint2(v.z, v.w), a + 4);
       *reinterpret_cast<float4*>(&xs[row * G + ch * 8]) = make_float4(a[0], a[1], a[2], a[3]);
       *reinterpret_cast<float4*>(&xs[row * G + ch * 8 + 4]) = make_float4(a[4], a[5], a[6], a[7]);
     }
+  };
+  for (int t0 = 0; t0 < T; t0 += CT) {
+    __syncthreads();  // previous tile fully consumed
+    stage(x, t0);
     __syncthreads();
     const int tn = min(CT, T - t0);
     // pass p = 0: original outputs; p = s + 1: shrink step s
     for (int p = 0; p <= nsteps; ++p) {
+      if (qx != nullptr && p == 1) {  // w8a8: shrink steps see fake-quantized activations
+        __syncthreads();              // (auto_clip.py:177, fake_quantize_input)
+        stage(qx, t0);
+        __syncthreads();
+      }
       float q[CH];
       load_half<DT, G>(wrow, h, q);
       if (p > 0) {
@@ -694,19 +641,6 @@ extern "C" int lcq_awq_scales_v1(const void* xmean, const void* wmax, int dtype,
 template <int DT>
 static void launch_scale(const void* x, int64_t rows, int64_t cols, const void* s, int op,
                          int axis, void* out, hipStream_t st) {
-  const int64_t c8n = cols / 8;
-  if (axis == 0 && (c8n % 256 == 0 || 256 % c8n == 0) && !getenv("LCQ_SCALE_GENERIC")) {
-    const int tpr = c8n >= 256 ? 256 : (int)c8n;
-    const int64_t bx = (c8n + tpr - 1) / tpr, rpb = 256 / tpr;
-    int64_t by = (2048 + bx - 1) / bx;  // ~8 workgroups per CU
-    const int64_t need = (rows + rpb - 1) / rpb;
-    if (by > need) by = need;
-    if (by > 65535) by = 65535;
-    const dim3 g((unsigned)bx, (unsigned)by);
-    if (op == 0) hipLaunchKernelGGL((k_scale_cols<DT, 0>), g, 256, 0, st, x, rows, cols, s, out, tpr);
-    else hipLaunchKernelGGL((k_scale_cols<DT, 1>), g, 256, 0, st, x, rows, cols, s, out, tpr);
-    return;
-  }
   const unsigned grid = stream_grid(rows * cols / 8, 256);
   if (op == 0 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 0, 0>), grid, 256, 0, st, x, rows, cols, s, out);
   if (op == 1 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 1, 0>), grid, 256, 0, st, x, rows, cols, s, out);
@@ -758,6 +692,7 @@ struct ClipLaunch {
   int mse_steps;
   const void* mse_p;
   float norm;
+  const void* qx;
 };
 
 template <int DT, int G, bool MSE>
@@ -771,7 +706,8 @@ static void launch_auto_clip(const ClipLaunch& c, hipStream_t st) {
                      c.oc, c.ic, (int)c.T, c.nsteps, reinterpret_cast<const float*>(c.factors),
                      (float)c.qmin, (float)c.qmax, c.sym, c.clip_sym,
                      reinterpret_cast<uint16_t*>(c.bmax), reinterpret_cast<uint16_t*>(c.bmin),
-                     c.mse_steps, reinterpret_cast<const float*>(c.mse_p), c.norm);
+                     c.mse_steps, reinterpret_cast<const float*>(c.mse_p), c.norm,
+                     reinterpret_cast<const uint16_t*>(c.qx));
 }
 
 template <int DT, bool MSE>
@@ -789,6 +725,17 @@ extern "C" int lcq_auto_clip_search(const void* w, const void* x, int dtype, int
                                     const void* factors, int qmin, int qmax, int sym,
                                     int clip_sym, int mse_steps, const void* mse_p, float norm,
                                     void* best_max, void* best_min, void* stream) {
+  return lcq_auto_clip_search_act(w, x, nullptr, dtype, oc, ic, T, group, nsteps, factors, qmin,
+                                  qmax, sym, clip_sym, mse_steps, mse_p, norm, best_max,
+                                  best_min, stream);
+}
+
+extern "C" int lcq_auto_clip_search_act(const void* w, const void* x, const void* qx, int dtype,
+                                        int64_t oc, int64_t ic, int64_t T, int group,
+                                        int nsteps, const void* factors, int qmin, int qmax,
+                                        int sym, int clip_sym, int mse_steps, const void* mse_p,
+                                        float norm, void* best_max, void* best_min,
+                                        void* stream) {
   LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16, "auto-clip: bf16 or fp16 model dtype");
   LCQ_REQUIRE(group == 32 || group == 64 || group == 128 || group == CGMAX,
               "auto-clip kernel supports group_size 32 / 64 / 128 / 256");
@@ -799,7 +746,7 @@ extern "C" int lcq_auto_clip_search(const void* w, const void* x, int dtype, int
               "mse: steps > 0 need the shrink factors and a positive norm");
   hipStream_t st = as_stream(stream);
   const ClipLaunch c{w, x, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym, best_max,
-                     best_min, mse_steps, mse_p, norm};
+                     best_min, mse_steps, mse_p, norm, qx};
   if (dtype == LCQ_BF16) {
     if (mse_steps) auto_clip_group<LCQ_BF16, true>(group, c, st);
     else auto_clip_group<LCQ_BF16, false>(group, c, st);
@@ -824,4 +771,276 @@ extern "C" int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t co
     default: hipLaunchKernelGGL((k_clip_apply<LCQ_F32>), grid, 256, 0, st, x, rows, cols, group, cmax, cmin, out);
   }
   return check_launch("lcq_clip_apply");
+}
+
+// ----------------------------------------------------------------------------------------
+// auto_clip search for per_channel weights (group = the whole row, auto_clip.py:96-99; the
+// w8a8 vLLM / SGLang AWQ configs, awq_w8a8.yml). The per-group kernel's lane-pair-per-row
+// layout cannot hold an IC-long row, so:
+//  * k_clip_pc_stats: one wave per row -> org max / min and every shrink step's clamp bounds
+//    and min/max qparams (the reference's fake_quant_weight_dynamic of the clamped row).
+//  * k_auto_clip_pc: a workgroup = 256 rows (lane = row) x PC_TT sampled tokens, k walked in
+//    PC_KC-wide chunks whose x / fake-quantized x tiles sit transposed in LDS (wave-uniform
+//    broadcast reads); each k regenerates the 10 candidate weights in registers (Markstein
+//    quotient, as the quant kernels) and accumulates the DT-rounded products of the original
+//    output (x) and of every step (qx, = x for weight-only) in fp32. Partial squared-error
+//    sums per token tile go to a workspace [ntt][nsteps][oc].
+//  * k_clip_pc_pick: fixed-order sum of the tiles, DT mean, first strict minimum.
+// Products are rounded to DT exactly as the reference's materialised broadcast product; the
+// IC-long fp32 sum runs in k order, not torch-CPU's vectorised cascade, so a sum can round
+// to a neighbouring DT value -> parity tier T2 (tests/test_awq_gpu.py: bounds equal on
+// >= 98 % of rows, chosen errors within a few DT ulps).
+// ----------------------------------------------------------------------------------------
+constexpr int PC_TT = 16;       // sampled tokens per workgroup
+constexpr int PC_KC = 128;      // k per LDS chunk
+constexpr int PC_NS = 10;       // shrink steps (max_shrink 0.5 x n_grid 20)
+constexpr int PC_QP = 5;        // per step: smin, smax, s, 1/s, z
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_clip_pc_stats(const uint16_t* __restrict__ w,
+                                                      int64_t oc, int64_t ic, int nsteps,
+                                                      const float* __restrict__ factors,
+                                                      float qmin, float qmax, int sym,
+                                                      int clip_sym, float* __restrict__ qp,
+                                                      float* __restrict__ orgmm) {
+  const int lane = threadIdx.x & 63;
+  const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (o >= oc) return;
+  float mx = -INFINITY, mn = INFINITY, am = 0.f;
+  for (int64_t k = (int64_t)lane * 8; k < ic; k += 64 * 8) {
+    float v[8];
+    ld8<DT>(w, o * ic + k, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mx = fmaxf(mx, v[j]);
+      mn = fminf(mn, v[j]);
+      am = fmaxf(am, fabsf(v[j]));
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+    mn = fminf(mn, __shfl_xor(mn, m, 64));
+    am = fmaxf(am, __shfl_xor(am, m, 64));
+  }
+  const float org_max = clip_sym ? am : mx, org_min = mn;
+  if (lane == 0) {
+    orgmm[2 * o] = org_max;
+    orgmm[2 * o + 1] = org_min;
+  }
+  if (lane < nsteps) {
+    const float f = factors[lane];
+    const float smax = dtr<DT>(org_max * f);
+    const float smin = clip_sym ? -smax : dtr<DT>(org_min * f);
+    const float cmn = fminf(fmaxf(mn, smin), smax), cmx = fminf(fmaxf(mx, smin), smax);
+    float qs, qz;
+    qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
+    float* d = qp + ((int64_t)o * PC_NS + lane) * PC_QP;
+    d[0] = smin;
+    d[1] = smax;
+    d[2] = qs;
+    d[3] = 1.0f / qs;
+    d[4] = qz;
+  }
+}
+
+// fake_quant of one clamped weight with step qparams (the per-group kernel's sequence, with
+// the quotient from RN(1/s): |v / s| <= qmax-ish, so it is normal or rounds to zero either way)
+template <int DT, bool SYM>
+__device__ __forceinline__ float fq_pc(float v, float smin, float smax, float qs, float rs,
+                                       float qz, float qmin, float qmax) {
+  v = fminf(fmaxf(v, smin), smax);
+  float tq = rintf(dtr<DT>(div_mk(v, qs, rs)));
+  if constexpr (!SYM) tq = dtr<DT>(tq + qz);
+  tq = fminf(fmaxf(tq, qmin), qmax);
+  return dtr<DT>((SYM ? tq : dtr<DT>(tq - qz)) * qs);
+}
+
+template <int DT, bool SYM>
+__global__ void __launch_bounds__(256, 1) k_auto_clip_pc(const uint16_t* __restrict__ w,
+                                                        const uint16_t* __restrict__ x,
+                                                        const uint16_t* __restrict__ qx,
+                                                        int64_t oc, int64_t ic, int T,
+                                                        int nsteps, const float* __restrict__ qp,
+                                                        float qmin, float qmax,
+                                                        float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float xs[PC_KC * PC_TT];   // [k][t], 8 KB
+  __shared__ __attribute__((aligned(16))) float qxs[PC_KC * PC_TT];  // 8 KB
+  const int tid = threadIdx.x;
+  const int64_t o = (int64_t)blockIdx.x * 256 + tid;
+  const bool live = o < oc;
+  const int t0 = blockIdx.y * PC_TT;
+  const int tn = min(PC_TT, T - t0);
+  const uint16_t* wrow = w + (live ? o : 0) * ic;
+  float q[PC_NS][PC_QP];
+#pragma unroll
+  for (int i = 0; i < PC_NS; ++i)
+#pragma unroll
+    for (int j = 0; j < PC_QP; ++j)
+      q[i][j] = (live && i < nsteps) ? qp[((int64_t)o * PC_NS + i) * PC_QP + j] : 1.f;
+  v2f org[PC_TT / 2], cur[PC_NS][PC_TT / 2];
+#pragma unroll
+  for (int t = 0; t < PC_TT / 2; ++t) {
+    org[t] = v2f{0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < PC_NS; ++i) cur[i][t] = v2f{0.f, 0.f};
+  }
+  const uint16_t* qsrc = qx ? qx : x;
+  for (int64_t k0 = 0; k0 < ic; k0 += PC_KC) {
+    __syncthreads();
+    // stage PC_TT tokens x PC_KC k of x and qx transposed: thread -> (token, 8 k)
+    {
+      const int t = tid / (PC_KC / 8), c8 = (tid % (PC_KC / 8)) * 8;
+      float a[8], b[8];
+      if (t < tn) {
+        const uint4 v = *reinterpret_cast<const uint4*>(x + (int64_t)(t0 + t) * ic + k0 + c8);
+        const uint4 u = *reinterpret_cast<const uint4*>(qsrc + (int64_t)(t0 + t) * ic + k0 + c8);
+        widen4<DT>(make_uint2(v.x, v.y), a);
+        widen4<DT>(make_uint2(v.z, v.w), a + 4);
+        widen4<DT>(make_uint2(u.x, u.y), b);
+        widen4<DT>(make_uint2(u.z, u.w), b + 4);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xs[(c8 + j) * PC_TT + t] = a[j];
+        qxs[(c8 + j) * PC_TT + t] = b[j];
+      }
+    }
+    __syncthreads();
+    for (int kk = 0; kk < PC_KC; kk += 8) {
+      float wv[8];
+      widen4<DT>(*reinterpret_cast<const uint2*>(wrow + k0 + kk), wv);
+      widen4<DT>(*reinterpret_cast<const uint2*>(wrow + k0 + kk + 4), wv + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float* xk = &xs[(kk + j) * PC_TT];
+        const float* qk = &qxs[(kk + j) * PC_TT];
+        const v2f wp = {wv[j], wv[j]};
+#pragma unroll
+        for (int t = 0; t < PC_TT / 4; ++t) {
+          const float4 xv = *reinterpret_cast<const float4*>(xk + 4 * t);
+          org[2 * t] += dtr2<DT>(v2f{xv.x, xv.y} * wp);
+          org[2 * t + 1] += dtr2<DT>(v2f{xv.z, xv.w} * wp);
+        }
+        float qv[PC_TT];
+#pragma unroll
+        for (int t = 0; t < PC_TT / 4; ++t) {
+          const float4 v = *reinterpret_cast<const float4*>(qk + 4 * t);
+          qv[4 * t] = v.x; qv[4 * t + 1] = v.y; qv[4 * t + 2] = v.z; qv[4 * t + 3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < PC_NS; ++i) {
+          const float c = fq_pc<DT, SYM>(wv[j], q[i][0], q[i][1], q[i][2], q[i][3], q[i][4],
+                                         qmin, qmax);
+          const v2f cp = {c, c};
+#pragma unroll
+          for (int t = 0; t < PC_TT / 2; ++t)
+            cur[i][t] += dtr2<DT>(v2f{qv[2 * t], qv[2 * t + 1]} * cp);
+        }
+      }
+    }
+  }
+  if (!live) return;
+  float og[PC_TT];
+#pragma unroll
+  for (int t = 0; t < PC_TT / 2; ++t) {
+    og[2 * t] = dtr<DT>(org[t].x);
+    og[2 * t + 1] = dtr<DT>(org[t].y);
+  }
+  // static indices only (a dynamic one would move the accumulators to scratch)
+#pragma unroll
+  for (int i = 0; i < PC_NS; ++i) {
+    float e = 0.f;
+#pragma unroll
+    for (int t = 0; t < PC_TT; ++t) {
+      const float cu = dtr<DT>((t & 1) ? cur[i][t >> 1].y : cur[i][t >> 1].x);
+      const float dd = dtr<DT>(cu - og[t]);
+      if (t < tn) e += dtr<DT>(dd * dd);
+    }
+    if (i < nsteps) part[((int64_t)blockIdx.y * nsteps + i) * oc + o] = e;
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_clip_pc_pick(const float* __restrict__ part, int ntt,
+                                                     int64_t oc, int T, int nsteps,
+                                                     const float* __restrict__ factors,
+                                                     int clip_sym,
+                                                     const float* __restrict__ orgmm,
+                                                     uint16_t* best_max, uint16_t* best_min) {
+  const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (o >= oc) return;
+  const float org_max = orgmm[2 * o], org_min = orgmm[2 * o + 1];
+  float bmax = org_max, bmin = org_min, best = dtr<DT>(1e9f);
+  for (int i = 0; i < nsteps; ++i) {
+    float e = 0.f;
+    for (int y = 0; y < ntt; ++y) e += part[((int64_t)y * nsteps + i) * oc + o];
+    const float em = dtr<DT>(e / (float)T);
+    if (em < best) {
+      best = em;
+      bmax = dtr<DT>(org_max * factors[i]);
+      bmin = clip_sym ? -bmax : dtr<DT>(org_min * factors[i]);
+    }
+  }
+  if constexpr (DT == LCQ_BF16) {
+    best_max[o] = (uint16_t)(__float_as_uint(bmax) >> 16);
+    best_min[o] = (uint16_t)(__float_as_uint(bmin) >> 16);
+  } else {
+    best_max[o] = __builtin_bit_cast(uint16_t, (_Float16)bmax);
+    best_min[o] = __builtin_bit_cast(uint16_t, (_Float16)bmin);
+  }
+}
+
+extern "C" int64_t lcq_auto_clip_pc_workspace_bytes(int64_t oc, int64_t T, int nsteps) {
+  const int64_t ntt = (T + PC_TT - 1) / PC_TT;
+  return oc * PC_NS * PC_QP * 4 + oc * 2 * 4 + ntt * nsteps * oc * 4;
+}
+
+template <int DT>
+static void launch_clip_pc(const void* w, const void* x, const void* qx, int64_t oc, int64_t ic,
+                           int64_t T, int nsteps, const void* factors, int qmin, int qmax,
+                           int sym, int clip_sym, char* ws, void* best_max, void* best_min,
+                           hipStream_t st) {
+  float* qp = reinterpret_cast<float*>(ws);
+  float* orgmm = qp + oc * PC_NS * PC_QP;
+  float* part = orgmm + oc * 2;
+  const int ntt = (int)((T + PC_TT - 1) / PC_TT);
+  const auto* wp = reinterpret_cast<const uint16_t*>(w);
+  const auto* fp = reinterpret_cast<const float*>(factors);
+  hipLaunchKernelGGL(k_clip_pc_stats<DT>, dim3((unsigned)((oc + 3) / 4)), 256, 0, st, wp, oc,
+                     ic, nsteps, fp, (float)qmin, (float)qmax, sym, clip_sym, qp, orgmm);
+  const dim3 g((unsigned)((oc + 255) / 256), (unsigned)ntt);
+  auto k = sym ? k_auto_clip_pc<DT, true> : k_auto_clip_pc<DT, false>;
+  hipLaunchKernelGGL(k, g, 256, 0, st, wp, reinterpret_cast<const uint16_t*>(x),
+                     reinterpret_cast<const uint16_t*>(qx), oc, ic, (int)T, nsteps, qp,
+                     (float)qmin, (float)qmax, part);
+  hipLaunchKernelGGL(k_clip_pc_pick<DT>, dim3((unsigned)((oc + 255) / 256)), 256, 0, st, part,
+                     ntt, oc, (int)T, nsteps, fp, clip_sym, orgmm,
+                     reinterpret_cast<uint16_t*>(best_max), reinterpret_cast<uint16_t*>(best_min));
+}
+
+extern "C" int lcq_auto_clip_search_pc(const void* w, const void* x, const void* qx, int dtype,
+                                       int64_t oc, int64_t ic, int64_t T, int nsteps,
+                                       const void* factors, int qmin, int qmax, int sym,
+                                       int clip_sym, void* workspace, int64_t ws_bytes,
+                                       void* best_max, void* best_min, void* stream) {
+  LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16, "auto-clip: bf16 or fp16 model dtype");
+  LCQ_REQUIRE(oc > 0 && ic > 0 && ic % PC_KC == 0, "per-channel auto-clip: ic % 128 == 0");
+  LCQ_REQUIRE(T > 0 && nsteps >= 1 && nsteps <= PC_NS, "bad T / nsteps (<= 10)");
+  LCQ_REQUIRE(qmax > qmin, "qmax <= qmin");
+  LCQ_REQUIRE(workspace != nullptr &&
+                  ws_bytes >= lcq_auto_clip_pc_workspace_bytes(oc, T, nsteps),
+              "workspace smaller than lcq_auto_clip_pc_workspace_bytes");
+  hipStream_t st = as_stream(stream);
+  char* ws = reinterpret_cast<char*>(workspace);
+  if (dtype == LCQ_BF16)
+    launch_clip_pc<LCQ_BF16>(w, x, qx, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym,
+                             ws, best_max, best_min, st);
+  else
+    launch_clip_pc<LCQ_F16>(w, x, qx, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym,
+                            ws, best_max, best_min, st);
+  return check_launch("lcq_auto_clip_search_pc");
 }

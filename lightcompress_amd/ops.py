@@ -480,10 +480,19 @@ def sq_diff_mean(a: torch.Tensor, b: torch.Tensor) -> float:
 
 
 def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, n_grid: int,
-                     qmin: int, qmax: int, sym: bool, clip_sym: bool, mse=None):
+                     qmin: int, qmax: int, sym: bool, clip_sym: bool, mse=None,
+                     qx: torch.Tensor | None = None):
     """AutoClipper.auto_clip_layer (v1) on device: returns (best_max, best_min) [oc, ng, 1].
-    mse = (steps, grid, norm): the weight quantizer's calib_algo is mse."""
+    mse = (steps, grid, norm): the weight quantizer's calib_algo is mse. qx: the activation
+    fake-quant of x (w_only False) that the shrink steps multiply with. group == ic takes the
+    per_channel kernel (lcq_auto_clip_search_pc)."""
     oc, ic = w.shape
+    if qx is not None and (qx.shape != x.shape or qx.dtype != x.dtype):
+        raise ValueError('auto-clip: qx must match x in shape and dtype')
+    if group == ic and group not in (32, 64, 128, 256):
+        if mse is not None:
+            raise NotImplementedError('per_channel auto-clip with calib_algo mse')
+        return _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym)
     T = x.shape[0]
     factors = torch.tensor([float(1 - i / n_grid) for i in range(nsteps)], dtype=torch.float32,
                            device=w.device)
@@ -497,9 +506,29 @@ def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, 
         msteps, grid, norm = int(mse[0]), float(mse[1]), float(mse[2])
         mp = torch.tensor([float(1 - i / grid) for i in range(msteps)], dtype=torch.float32,
                           device=w.device)
-    N.call('lcq_auto_clip_search', N.ptr(w.contiguous()), N.ptr(x.contiguous()), N.dt(w), oc,
-           ic, T, int(group), int(nsteps), N.ptr(factors), int(qmin), int(qmax), int(sym),
-           int(clip_sym), msteps, N.ptr(mp), norm, N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
+    N.call('lcq_auto_clip_search_act', N.ptr(w.contiguous()), N.ptr(x.contiguous()),
+           N.ptr(qx.contiguous() if qx is not None else None), N.dt(w), oc, ic, T, int(group),
+           int(nsteps), N.ptr(factors), int(qmin), int(qmax), int(sym), int(clip_sym), msteps,
+           N.ptr(mp), norm, N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
+    return bmax, bmin
+
+
+def _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym):
+    """per_channel weights: best bounds [oc, 1, 1] (auto_clip.py:96-99, group = ic)."""
+    oc, ic = w.shape
+    T = x.shape[0]
+    if x.dtype != w.dtype:
+        raise ValueError('auto-clip: x and w must share the model dtype')
+    factors = torch.tensor([float(1 - i / n_grid) for i in range(nsteps)], dtype=torch.float32,
+                           device=w.device)
+    bmax = torch.empty((oc, 1, 1), dtype=w.dtype, device=w.device)
+    bmin = torch.empty((oc, 1, 1), dtype=w.dtype, device=w.device)
+    wsb = N.load().lcq_auto_clip_pc_workspace_bytes(oc, T, int(nsteps))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=w.device)
+    N.call('lcq_auto_clip_search_pc', N.ptr(w.contiguous()), N.ptr(x.contiguous()),
+           N.ptr(qx.contiguous() if qx is not None else None), N.dt(w), oc, ic, T, int(nsteps),
+           N.ptr(factors), int(qmin), int(qmax), int(sym), int(clip_sym), N.ptr(ws), wsb,
+           N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
     return bmax, bmin
 
 

@@ -90,9 +90,12 @@ def _fq_mse(cur: torch.Tensor, bit, sym, group):
 
 
 def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_grid=20,
-               max_shrink=0.5, n_sample_token=512, mse=False):
-    """auto_clip.py:83-191 (clip v1, w_only, single input). Returns (best_max, best_min)
-    shaped [oc, ng, 1]. mse=True: the weight quantizer's calib_algo is mse."""
+               max_shrink=0.5, n_sample_token=512, mse=False, act=None):
+    """auto_clip.py:83-191 (clip v1, single input). Returns (best_max, best_min) shaped
+    [oc, ng, 1]. mse=True: the weight quantizer's calib_algo is mse. group = ic is the
+    per_channel case (auto_clip.py:96-99). act = (bits, sym): w_only False, the shrink steps
+    see fake_quantize_input(x) = per_token fake quant of the [1, T, ng, group] view
+    (auto_clip.py:176-177, 269-274; quant.py:754-771 with reshape_tensor's per_token no-op)."""
     w = w.reshape(w.shape[0], 1, -1, group)
     ocb = 256 if w.shape[0] % 256 == 0 else 64
     x = x.view(-1, x.shape[-1]).reshape(1, -1, x.shape[-1] // group, group)
@@ -106,13 +109,14 @@ def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_gr
         best_max, best_min = org_max.clone(), org_min.clone()
         min_errs = torch.ones_like(org_max) * 1e9
         org_out = (x * wb).sum(dim=-1)
+        qx = x if act is None else Q.fake_quant_dynamic(x, act[0], act[1], 'per_token')[0]
         for i_s in range(int(max_shrink * n_grid)):
             max_val = org_max * (1 - i_s / n_grid)
             min_val = -max_val if clip_sym else org_min * (1 - i_s / n_grid)
             cur = torch.clamp(wb, min_val, max_val)
             q_w = (_fq_mse(cur, bit, sym, group) if mse else
                    Q.fake_quant_dynamic(cur, bit, sym, 'per_group', group)[0])
-            cur_out = (x * q_w).sum(dim=-1)
+            cur_out = (qx * q_w).sum(dim=-1)
             err = (cur_out - org_out).pow(2).mean(dim=1).view(min_errs.shape)
             err_mean = 0 + err
             err_mean /= 1

@@ -340,7 +340,38 @@ def gen_clip():
     print('clip fixtures written')
 
 
-GENERATORS = {'quant': gen_quant, 'gptq': gen_gptq, 'awq': gen_awq, 'clip': gen_clip}
+def gen_clip_act():
+    """Reference AutoClipper.auto_clip_layer for per_channel weights (group = ic) and with
+    activation fake-quant (w_only False: awq_w8a8.yml's int8 per_token act), bf16 / fp16."""
+    R.init_dist()
+    q = R.quant_module()
+    import llmc.compression.quantization.auto_clip as ac
+    bf, hf = torch.bfloat16, torch.float16
+    # (name, wbit, sym, clip_sym, granularity, group, act (bit, sym) or None, oc, ic, dtype)
+    cases = [('pc_w8a8', 8, True, True, 'per_channel', -1, (8, True), 256, 512, bf),
+             ('pc_w8_wonly', 8, True, True, 'per_channel', -1, None, 256, 512, bf),
+             ('pc_w4_asym', 4, False, False, 'per_channel', -1, None, 128, 1024, bf),
+             ('pc_w8a8_asym_f16', 8, False, False, 'per_channel', -1, (8, False), 128, 512, hf),
+             ('pg_w4a8', 4, False, False, 'per_group', 128, (8, True), 128, 512, bf)]
+    for i, (name, wb, sym, clip_sym, gran, grp, act, oc, ic, dt) in enumerate(cases):
+        kw = {'group_size': grp} if gran == 'per_group' else {}
+        wq = q.IntegerQuantizer(wb, sym, gran, **kw)
+        aq = q.IntegerQuantizer(act[0], act[1], 'per_token') if act else None
+        clipper = ac.AutoClipper(w_only=act is None, wquantizer=wq, aquantizer=aq,
+                                 clip_version='v1', clip_sym=clip_sym, save_clip=False,
+                                 padding_mask=None)
+        w = weights(oc, ic, dt, 700 + i, edge=False)
+        x = _acts(1, 512, ic, 800 + i, dtype=dt)[0]
+        bmax, bmin = clipper.auto_clip_layer(0, 'l', w.clone(), [x.clone()],
+                                             n_sample_token=64)
+        F.save(f'clipact_{name}', w=w, x=x, best_max=bmax, best_min=bmin,
+               meta=torch.tensor([wb, int(sym), int(clip_sym), 64, grp,
+                                  act[0] if act else 0, int(act[1]) if act else 0]))
+    print('clip act / per-channel fixtures written')
+
+
+GENERATORS = {'quant': gen_quant, 'gptq': gen_gptq, 'awq': gen_awq, 'clip': gen_clip,
+              'clip_act': gen_clip_act}
 
 
 def gen_fp8():

@@ -43,6 +43,17 @@ CONFIGS = {
                                             'weight_clip': True, 'clip_sym': False},
                                 'quant_out': True},
                       'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}},
+    # configs/quantization/backend/vllm/awq_w8a8.yml: int8 per_channel weights, int8 dynamic
+    # per_token activations (the search and the clip see fake-quantized inputs), per-channel
+    # auto-clip, quant_out
+    'awq_w8a8': {'quant': {'method': 'Awq',
+                           'weight': {'bit': 8, 'symmetric': True, 'granularity': 'per_channel',
+                                      'group_size': -1},
+                           'act': {'bit': 8, 'symmetric': True, 'granularity': 'per_token'},
+                           'special': {'trans': True, 'trans_version': 'v2',
+                                       'weight_clip': True},
+                           'quant_out': True},
+                 'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}},
     # configs/quantization/methods/RTN/rtn_w_a_pertensor_static.yml with calib_algo
     # static_minmax (static_hist is not on the device path); deployed act scales compared too
     'rtn_a8_static': {'quant': {'method': 'RTN',

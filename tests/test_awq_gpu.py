@@ -166,10 +166,9 @@ def test_awq_weight_scale_vs_oracle(dev, rows, cols, group, nl):
 
 @pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
 def test_scale_bcast_cols_every_x_every_scale(dev, dt):
-    """The per-column fast path (k_scale_cols: Markstein quotient from RN(1/s), IEEE division
-    outside its proven range): every finite bf16 x in every column against 1024 scales
-    covering every bf16 mantissa across exponents -16..15 (plus tiny / huge / near-1 scales),
-    bit-equal to torch-CPU's x / s and x * s."""
+    """x / s and x * s per column at an AWQ-like width: every finite bf16 x in every column
+    against 1024 scales covering every bf16 mantissa across exponents -16..15 (plus tiny and
+    huge scales), bit-equal to torch-CPU's x / s and x * s."""
     from lightcompress_amd import ops
     allb = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
     fin = allb[torch.isfinite(allb.float())]
@@ -195,3 +194,56 @@ def test_scale_bcast_cols_every_x_every_scale(dev, dt):
     ref = x4 / s4.view(1, -1)
     got = ops.scale_bcast(x4.to(dev), s4.to(dev), 'div').cpu()
     assert torch.equal(got.view(ib), ref.view(ib))
+
+
+@pytest.mark.parametrize('name', F.names('clipact_'))
+def test_auto_clip_pc_act_vs_reference(dev, name):
+    """AutoClipper.auto_clip_layer through the plugin class for per_channel weights
+    (lcq_auto_clip_search_pc) and with activation fake-quant (w_only False), against the
+    reference's own bounds. Per-group with act: exact emulation, bit-equal. Per-channel: the
+    ic-long fp32 sums run in k order instead of torch-CPU's cascade, so a cur/org output can
+    round to the neighbouring bf16 value and move a near-tie step choice (T2)."""
+    from lightcompress_amd.auto_clip import AutoClipper
+    from lightcompress_amd.quant import IntegerQuantizer
+    c = F.load(name)
+    wb, sym, clip_sym, nst, grp, abit, asym = c['meta'].tolist()
+    gran = 'per_channel' if grp == -1 else 'per_group'
+    kw = {'group_size': grp} if grp != -1 else {}
+    wq = IntegerQuantizer(wb, bool(sym), gran, **kw)
+    aq = IntegerQuantizer(abit, bool(asym), 'per_token') if abit else None
+    clipper = AutoClipper(w_only=not abit, wquantizer=wq, aquantizer=aq, clip_version='v1',
+                          clip_sym=bool(clip_sym), save_clip=False, padding_mask=None)
+    bmax, bmin = clipper.auto_clip_layer(0, 'l', c['w'].to(dev), [c['x'].to(dev)],
+                                         n_sample_token=nst)
+    assert bmax.shape == c['best_max'].shape
+    eq_max = (bits(bmax.cpu()) == bits(c['best_max'])).float().mean().item()
+    eq_min = (bits(bmin.cpu()) == bits(c['best_min'])).float().mean().item()
+    if grp != -1:
+        assert eq_max == 1.0 and eq_min == 1.0, (eq_max, eq_min)
+    else:
+        assert eq_max >= 0.97 and eq_min >= 0.97, (eq_max, eq_min)
+
+
+def test_auto_clip_pc_llama_shape(dev):
+    """per_channel w8a8 clip at a Llama-3-8B o_proj shape (4096 x 4096, 512 sampled tokens)
+    against the oracle on 64 rows: bounds equal on >= 97 % of the rows, and every chosen
+    bound is one of the shrink grid's values of its row."""
+    from lightcompress_amd import ops
+    from oracle import awq_ref as A
+    from oracle import quant_ref as Q
+    g = torch.Generator().manual_seed(11)
+    oc, ic, T = 4096, 4096, 512
+    w = (torch.randn(oc, ic, generator=g) * 0.02).to(torch.bfloat16)
+    mag = torch.exp(torch.randn(ic, generator=g))
+    x = (torch.randn(T, ic, generator=g) * mag).to(torch.bfloat16)
+    qx = Q.fake_quant_dynamic(x, 8, True, 'per_token')[0]
+    bmax, bmin = ops.auto_clip_search(w.to(dev), x.to(dev), ic, 10, 20, -128, 127, True, True,
+                                      qx=qx.to(dev))
+    rows = torch.arange(0, oc, oc // 64)
+    emax, emin = A.clip_layer(w[rows], x, 8, True, ic, True, n_sample_token=T, act=(8, True))
+    eq = (bits(bmax.cpu()[rows]) == bits(emax)).float().mean().item()
+    assert eq >= 0.97, eq
+    am = w.float().abs().amax(dim=1)
+    grid = torch.stack([(am * (1 - i / 20)).to(torch.bfloat16).float() for i in range(10)], 1)
+    assert bool((grid == bmax.cpu().float().view(-1, 1)).any(dim=1).all())
+    assert torch.equal(bits(bmin), bits(-bmax))

@@ -41,3 +41,16 @@ def test_auto_clip_matches_reference(name):
     assert torch.equal(bmin.view(torch.int16), c['best_min'].view(torch.int16))
     wc = A.apply_clip(c['w'], bmax, bmin, bool(clip_sym))
     assert torch.equal(wc.view(torch.int16), c['w_clipped'].view(torch.int16))
+
+
+@pytest.mark.parametrize('name', F.names('clipact_'))
+def test_auto_clip_pc_act_matches_reference(name):
+    """per_channel weights (group = ic) and activation fake-quant (w_only False): the oracle
+    restatement against the reference's own auto_clip_layer, bit-equal."""
+    c = F.load(name)
+    wb, sym, clip_sym, nst, grp, abit, asym = c['meta'].tolist()
+    group = c['w'].shape[1] if grp == -1 else grp
+    bmax, bmin = A.clip_layer(c['w'], c['x'], wb, bool(sym), group, bool(clip_sym),
+                              n_sample_token=nst, act=(abit, bool(asym)) if abit else None)
+    assert torch.equal(bmax.view(torch.int16), c['best_max'].view(torch.int16))
+    assert torch.equal(bmin.view(torch.int16), c['best_min'].view(torch.int16))

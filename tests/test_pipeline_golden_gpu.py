@@ -99,6 +99,37 @@ def test_awq_pipeline_vs_reference(dev, name, monkeypatch):
         assert eq >= 0.95, k
 
 
+def test_awq_w8a8_pipeline_vs_reference(dev, monkeypatch):
+    """configs/quantization/backend/vllm/awq_w8a8.yml (int8 per_channel weights, int8 dynamic
+    per_token activations in the search and the clip, per-channel auto-clip, quant_out):
+    block 0's q/k projections deploy bit-equal (no clip there, identical inputs), every block-0
+    loss curve within 3e-3 with the same argmin, later curves near-tie (T3 as above). Clipped
+    linears: the per-channel clip sums ic-long rows in k order (T2), so a row whose
+    bound choice sits on a near tie may take the neighbouring bound -> >= 90 % bit-equal."""
+    ref, got, diag = run_ours('awq_w8a8', dev, monkeypatch)
+    res = compare(ref, got)
+    print(res)
+    for k in ('b0__self_attn__q_proj', 'b0__self_attn__k_proj'):
+        assert res[k] == 1.0, k
+    rdiag = F.load('pipe_awq_w8a8_diag')
+    lkeys = sorted(k for k in rdiag if k.startswith('L_'))
+    assert lkeys == sorted(k for k in diag if k.startswith('L_'))
+    for k in lkeys:
+        r, o = rdiag[k], diag[k]
+        rel = ((o - r).abs() / r.abs()).max().item()
+        ri, oi = int(r.argmin()), int(o.argmin())
+        print(f'{k}: max rel loss diff {rel:.2e}, argmin ref {ri} ours {oi}')
+        if k.startswith('L_b0'):
+            # the per_token int8 fake quant of each GEMM's input turns a last-bit difference
+            # of the CPU vs GPU forward into a whole int8 step now and then: 1.4e-3 measured
+            assert rel < 3e-3 and ri == oi, k
+        else:
+            assert rel < 1e-2, k
+            assert ri == oi or r[oi].item() <= r[ri].item() * 1.002, k
+    for k, eq in res.items():
+        assert eq >= 0.9, (k, eq)
+
+
 def test_gptq_pipeline_vs_reference(dev, monkeypatch):
     ref, got, diag = run_ours('gptq', dev, monkeypatch)
     res = compare(ref, got)
