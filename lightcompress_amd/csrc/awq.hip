@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(64) k_sqdiff_p2(const double* part, int nparts
 // squared-error sums and the original outputs sit in LDS so the token loop stays rolled.
 // ----------------------------------------------------------------------------------------
 constexpr int CROWS = 128;     // rows per workgroup (2 lanes per row -> 256 threads)
-constexpr int CT = 32;         // sampled tokens per LDS tile
+constexpr int CT = 32;         // sampled tokens per LDS tile (64 measured 5 % slower)
 constexpr int CMAXSTEPS = 16;
 constexpr int CGMAX = 256;     // largest group (xs tile = CT x G fp32)
 
@@ -391,7 +391,7 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 we
                 int64_t ic, int T, int nsteps, const float* __restrict__ factors, float qmin,
                 float qmax, int sym, int clip_sym, uint16_t* best_max, uint16_t* best_min,
                 int mse_steps, const float* __restrict__ mse_p, float norm,
-                const uint16_t* __restrict__ qx) {
+                const uint16_t* __restrict__ qx, int mkdiv) {
   constexpr int CH = G / 2;    // weights per lane: k = 8i + 4h + j, h = lane parity
   constexpr int CHUNKS = G / 8;
   __shared__ __attribute__((aligned(16))) float xs[CT * G];      // <= 32 KB
@@ -491,12 +491,15 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 we
           }
         } else {
         qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
+        const float rqs = 1.0f / qs;  // RN(1/s): qs >= DT(1e-5) / qmax, so it is normal
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
           const float v = fminf(fmaxf(q[k], smin), smax);
-          // correctly rounded fp32 quotient (IEEE division; a reciprocal-based quotient can
-          // miss by an ulp, which fp16's extra mantissa bits expose), then rounded to DT
-          float tq = rintf(dtr<DT>(__fdiv_rn(v, qs)));
+          // correctly rounded fp32 quotient, then rounded to DT: Markstein's from RN(1/s) (3
+          // VALU; |v / s| <= qmax + 1, normal or rounding to zero either way, as mk_safe in
+          // quant_group.hip) or the IEEE division (mkdiv 0, ~10 VALU). A plain v * RN(1/s)
+          // can miss by an ulp, which fp16's extra mantissa bits expose.
+          float tq = rintf(dtr<DT>(mkdiv ? div_mk(v, qs, rqs) : __fdiv_rn(v, qs)));
           if (!sym) tq = dtr<DT>(tq + qz);
           tq = fminf(fmaxf(tq, qmin), qmax);
           q[k] = dtr<DT>((sym ? tq : dtr<DT>(tq - qz)) * qs);
@@ -699,6 +702,8 @@ template <int DT, int G, bool MSE>
 static void launch_auto_clip(const ClipLaunch& c, hipStream_t st) {
   dim3 grid((unsigned)((c.oc + CROWS - 1) / CROWS), (unsigned)(c.ic / G));
   const char* e = getenv("LCQ_CLIP_CVT");  // 0: the convert + shift / mask widening (A/B)
+  const char* dv = getenv("LCQ_CLIP_DIV");  // ieee: the IEEE division sequence (A/B)
+  const int mkdiv = !(dv && dv[0] == 'i');
   auto k = (DT == LCQ_BF16 && e && e[0] == '0') ? k_auto_clip<DT, G, MSE, false>
                                                 : k_auto_clip<DT, G, MSE, true>;
   hipLaunchKernelGGL(k, grid, 2 * CROWS, 0, st,
@@ -707,7 +712,7 @@ static void launch_auto_clip(const ClipLaunch& c, hipStream_t st) {
                      (float)c.qmin, (float)c.qmax, c.sym, c.clip_sym,
                      reinterpret_cast<uint16_t*>(c.bmax), reinterpret_cast<uint16_t*>(c.bmin),
                      c.mse_steps, reinterpret_cast<const float*>(c.mse_p), c.norm,
-                     reinterpret_cast<const uint16_t*>(c.qx));
+                     reinterpret_cast<const uint16_t*>(c.qx), mkdiv);
 }
 
 template <int DT, bool MSE>
