@@ -358,21 +358,36 @@ __global__ void __launch_bounds__(512, 1) k_syrk256(SyrkArgs a) {
     }
 }
 
-// split-K combine: H = beta*H + alpha * sum_s P[s] (fixed order), upper tiles + mirror
+// split-K combine: H = beta*H + alpha * sum_s P[s] (fixed order), upper tiles + mirror. A
+// workgroup = one 64 x 64 piece of an upper tile: the row-major store and the mirrored store
+// both go out coalesced (the mirror through an LDS transpose)
 __global__ void __launch_bounds__(256) k_syrk_reduce(SyrkArgs a) {
+  __shared__ float tp[64][65];
   int ti, tj;
   tri_tile(blockIdx.x, a.nt, ti, tj);
   const bool diag = ti == tj;
-  const int64_t r = (int64_t)ti * ST + blockIdx.y;  // one tile row per block.y
-  if (r >= a.ic) return;
-  const int64_t c = (int64_t)tj * ST + threadIdx.x;
-  if (c >= a.ic) return;
-  float s = 0.f;
-  for (int k = 0; k < a.ns; ++k) s = __fadd_rn(s, a.part[(int64_t)k * a.icp * a.icp + r * a.icp + c]);
-  float v = __fmul_rn(a.alpha, s);
-  if (a.beta != 0.f) v = __fadd_rn(__fmul_rn(a.beta, a.H[r * a.ic + c]), v);
-  a.H[r * a.ic + c] = v;
-  if (!diag) a.H[c * a.ic + r] = v;
+  const int pr = blockIdx.y >> 2, pc = blockIdx.y & 3;  // 4 x 4 pieces of the 256^2 tile
+  const int64_t r0 = (int64_t)ti * ST + pr * 64, c0 = (int64_t)tj * ST + pc * 64;
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  for (int rr = ry; rr < 64; rr += 4) {
+    const int64_t r = r0 + rr, c = c0 + cx;
+    float v = 0.f;
+    if (r < a.ic && c < a.ic) {
+      float s = 0.f;
+      for (int k = 0; k < a.ns; ++k)
+        s = __fadd_rn(s, a.part[(int64_t)k * a.icp * a.icp + r * a.icp + c]);
+      v = __fmul_rn(a.alpha, s);
+      if (a.beta != 0.f) v = __fadd_rn(__fmul_rn(a.beta, a.H[r * a.ic + c]), v);
+      a.H[r * a.ic + c] = v;
+    }
+    tp[rr][cx] = v;
+  }
+  if (diag) return;  // a diagonal tile's mirror is its own transpose: written above
+  __syncthreads();
+  for (int cc = ry; cc < 64; cc += 4) {  // H[c0 + cc][r0 + cx] = tile[cx][cc]
+    const int64_t c = c0 + cc, r = r0 + cx;
+    if (r < a.ic && c < a.ic) a.H[c * a.ic + r] = tp[cx][cc];
+  }
 }
 
 static int64_t ceil_to(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
@@ -459,7 +474,7 @@ extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t 
                        x_dtype == LCQ_F16, st);
     if (rc) return rc;
     if (ns > 1) {
-      hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)ntiles, ST), 256, 0, st, a);
+      hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)ntiles, 16), 256, 0, st, a);
       rc = check_launch("lcq_hessian_accum: reduce");
     }
     return rc;
@@ -476,7 +491,7 @@ extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t 
   rc = check_launch("lcq_hessian_accum: syrk");
   if (rc) return rc;
   if (ns > 1) {
-    hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)ntiles, ST), 256, 0, st, a);
+    hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)ntiles, 16), 256, 0, st, a);
     rc = check_launch("lcq_hessian_accum: reduce");
   }
   return rc;

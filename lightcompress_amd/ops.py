@@ -6,6 +6,8 @@ through ``_native``. There is no CPU path: CPU tensors raise ``LcqError``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as N
@@ -741,10 +743,32 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
         if Nn % 8:
             raise ValueError('N must be a multiple of 8')
         rec += [N.ptr(c), N.ptr(s), N.ptr(o), M, Nn]
-    descs = torch.tensor(rec, dtype=torch.int64).to(dev, non_blocking=False)
-    ws = torch.empty(n * FP8_PARTIALS, dtype=torch.float32, device=dev)
     sc = torch.empty(n, dtype=torch.float32, device=dev)
     qmax = fp8_max(fp8) if qmax is None else float(qmax)
+    if block == 128 and os.environ.get('LCQ_FP8_DEPLOY') != 'pair' and all(
+            c.shape[1] % 16 == 0 and c.numel() < (1 << 28) and N.ptr(c) % 16 == 0 and
+            N.ptr(o) % 16 == 0 for c, o in zip(codes, outs)):
+        # one persistent launch (lcq_fp8_block_to_tensor_stream): the work-item plan is the
+        # prefix over P1(0) P1(1) P2(0) P1(2) P2(1) ... P2(n-1), items of 65536 codes
+        items = [-(-c.numel() // 65536) for c in codes]
+        seg = [items[0]]
+        for L in range(1, n):
+            seg += [items[L], items[L - 1]]
+        seg.append(items[n - 1])
+        plan = [0]
+        for v in seg:
+            plan.append(plan[-1] + v)
+        host = torch.tensor(rec + plan, dtype=torch.int64)
+        dbuf = host.to(dev)
+        descs = dbuf[:5 * n]
+        plan_d = dbuf[5 * n:].to(torch.int32)
+        ws = torch.empty(2 * n + 1, dtype=torch.int32, device=dev)
+        N.call('lcq_fp8_block_to_tensor_stream', n, N.ptr(descs), N.ptr(plan_d),
+               N.dt(codes[0].dtype), N.dt(fp8), qmax, 1e-5, 1, N.ptr(ws), N.ptr(sc),
+               N.stream_of(codes[0]))
+        return outs, sc
+    descs = torch.tensor(rec, dtype=torch.int64).to(dev, non_blocking=False)
+    ws = torch.empty(n * FP8_PARTIALS, dtype=torch.float32, device=dev)
     N.call('lcq_fp8_block_to_tensor_many', n, N.ptr(descs), max(c.numel() for c in codes),
            N.dt(codes[0].dtype), block, N.dt(fp8), qmax, 1e-5, 1, N.ptr(ws), N.ptr(sc),
            N.stream_of(codes[0]))

@@ -19,7 +19,8 @@ KEYS = {'k_syrk16': 'k_syrk16', 'k_fp8_gemm2': 'k_fp8_gemm2', 'k_fp8_gemm': 'k_f
         'k_gptq_trailing': 'k_gptq_trailing', 'k_xt_pack': 'k_xt_pack',
         'k_requant_blockfp8_many': 'k_requant_blockfp8_many',
         'k_absmax_blockfp8_many': 'k_absmax_blockfp8_many',
-        'k_bmax16_many': 'k_bmax16_many', 'k_requant16_many': 'k_requant16_many'}
+        'k_bmax16_many': 'k_bmax16_many', 'k_requant16_many': 'k_requant16_many',
+        'k_b2t_stream': 'k_b2t_stream'}
 
 
 def load(path):
