@@ -611,14 +611,15 @@ __global__ void __launch_bounds__(256) k_requant16_many(const Fp8Desc* d, Fp8Des
 // ---- one-launch streaming form of the batched deploy (block 128, fast16 tensors) ---------
 // The two-pass pair above reads every code twice from HBM (pass 2 starts after pass 1 has
 // swept all tensors, far beyond the 256 MB MALL): 3 B of traffic per element. Here one
-// persistent grid walks a single work list in the order P1(0) P1(1) P2(0) P1(2) P2(1) ...
-// P2(n-1) (P1 = amax items, P2 = requant items, B2T_ITEM 16-byte chunks each); workgroup b
-// takes items b, b + G, ... in order. A P1 item folds its byte-max amax into amax[L] (device
-// atomic max of the float bits) and then bumps done[L] (release); a P2 item of tensor L waits
-// for done[L] == #P1 items of L (acquire), so it re-reads codes that were streamed one tensor
+// persistent grid walks a single work list P1(0) .. P1(D-1) P1(D) P2(0) P1(D+1) P2(1) ...
+// P2(n-1) (P1 = amax items, P2 = requant items, B2T_ITEM 16-byte chunks each; the host picks
+// the lag D so that >= 1.25 grids of items separate P1(L) from P2(L): the requant items
+// rarely wait); workgroup b takes items b, b + G, ... in order. A P1 item folds its byte-max amax into amax[L] (device
+// atomic max of the float bits) and then bumps done[L]; a P2 item of tensor L waits
+// for done[L] == #P1 items of L, so it re-reads codes that were streamed one tensor
 // earlier (~15-30 MB back: MALL, not HBM) -> 2 B of HBM traffic per element. Every dependency
 // points to a smaller item index and workgroups take their items in increasing order, so with
-// the whole grid resident (G = 2 per CU) the smallest unfinished item can always run; the spin
+// the whole grid resident (G = 4 per CU) the smallest unfinished item can always run; the spin
 // is bounded anyway (err flag, no hang). Codes equal the two-pass path's bit for bit (same
 // per-chunk arithmetic; max is order-independent).
 constexpr int B2T_ITEM = 4096;  // 16-byte chunks per work item (64 KB of codes)
@@ -634,27 +635,13 @@ __global__ void __launch_bounds__(256) k_b2t_stream(const Fp8Desc* __restrict__ 
   uint32_t* done = ws + n;
   uint32_t* err = ws + 2 * n;
   const int nseg = 2 * n, nitems = plan[nseg];
+  const int* segc = plan + nseg + 1;  // segment code: tensor * 2 + (1 for a requant segment)
+  const int* p1s = segc + nseg;       // index of tensor L's amax segment
+  int g = 0;                          // items only grow: walk the segments forward
   for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
-    int lo = 0, hi = nseg - 1;  // segment g: the last with plan[g] <= it
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (plan[mid] <= it) lo = mid;
-      else hi = mid - 1;
-    }
-    const int g = lo;
-    int L;
-    bool p1;
-    if (g == 0) {
-      L = 0;
-      p1 = true;
-    } else if (g & 1) {
-      L = (g + 1) >> 1;
-      p1 = L <= n - 1;
-      if (!p1) L = n - 1;
-    } else {
-      L = (g >> 1) - 1;
-      p1 = false;
-    }
+    while (plan[g + 1] <= it) ++g;
+    const int L = segc[g] >> 1;
+    const bool p1 = (segc[g] & 1) == 0;
     const Fp8Desc t = d[L];
     const int nc = (int)(t.N >> 4), nbc = (int)((t.N + 127) >> 7);
     const int nk = (int)(t.M * t.N >> 4);
@@ -686,15 +673,21 @@ __global__ void __launch_bounds__(256) k_b2t_stream(const Fp8Desc* __restrict__ 
       __syncthreads();
       if (threadIdx.x == 0) {
         const uint32_t m = max(max(red[0], red[1]), max(red[2], red[3]));
-        __hip_atomic_fetch_max(&amax[L], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&done[L], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        // relaxed device-scope RMWs (performed past the per-XCD L2s); the returning max
+        // completes before the count is bumped. No release / acquire fences: at agent scope
+        // they write back / invalidate the whole L2, and the only data handed over is these
+        // two words
+        const uint32_t prev =
+            __hip_atomic_fetch_max(&amax[L], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+        __hip_atomic_fetch_add(&done[L], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     } else {
       if (threadIdx.x == 0) {
-        const int gp = L == 0 ? 0 : 2 * L - 1;
+        const int gp = p1s[L];
         const uint32_t need = (uint32_t)(plan[gp + 1] - plan[gp]);
         int spins = 0;
-        while (__hip_atomic_load(&done[L], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        while (__hip_atomic_load(&done[L], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
           __builtin_amdgcn_s_sleep(8);
           if (++spins > (1 << 22)) {  // never expected: report, do not hang the device
             __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -702,7 +695,7 @@ __global__ void __launch_bounds__(256) k_b2t_stream(const Fp8Desc* __restrict__ 
           }
         }
         const float am = __uint_as_float(
-            __hip_atomic_load(&amax[L], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
+            __hip_atomic_load(&amax[L], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         sc_sh = fp8_scale<LCQ_BF16, LCQ_F32>(am, qmax, clamp_min, ADD_ZERO);
       }
       __syncthreads();
@@ -1148,7 +1141,7 @@ extern "C" int lcq_fp8_block_to_tensor_stream(int n, const void* descs, const vo
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const dim3 grid((unsigned)(2 * cus));  // 2 per CU: the whole grid is resident
+  const dim3 grid((unsigned)(4 * cus));  // 4 per CU (tiny kernel): the whole grid is resident
   const auto* d = reinterpret_cast<const Fp8Desc*>(descs);
   const auto* pl = reinterpret_cast<const int*>(plan);
   auto* w = reinterpret_cast<uint32_t*>(ws);

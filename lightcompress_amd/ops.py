@@ -745,20 +745,28 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
         rec += [N.ptr(c), N.ptr(s), N.ptr(o), M, Nn]
     sc = torch.empty(n, dtype=torch.float32, device=dev)
     qmax = fp8_max(fp8) if qmax is None else float(qmax)
-    if block == 128 and os.environ.get('LCQ_FP8_DEPLOY') != 'pair' and all(
+    if block == 128 and os.environ.get('LCQ_FP8_DEPLOY') == 'stream' and all(
             c.shape[1] % 16 == 0 and c.numel() < (1 << 28) and N.ptr(c) % 16 == 0 and
             N.ptr(o) % 16 == 0 for c, o in zip(codes, outs)):
-        # one persistent launch (lcq_fp8_block_to_tensor_stream): the work-item plan is the
-        # prefix over P1(0) P1(1) P2(0) P1(2) P2(1) ... P2(n-1), items of 65536 codes
+        # opt-in: one persistent launch (lcq_fp8_block_to_tensor_stream; bit-identical, but
+        # measured 2.2 ms vs the pair's 0.99 ms over 96 DSv3 expert linears,
+        # profiles/r2s4_fp8_deploy_ab.txt). Work items of 65536 codes, P2(L) lagging P1(L)
         items = [-(-c.numel() // 65536) for c in codes]
-        seg = [items[0]]
-        for L in range(1, n):
-            seg += [items[L], items[L - 1]]
-        seg.append(items[n - 1])
-        plan = [0]
-        for v in seg:
-            plan.append(plan[-1] + v)
-        host = torch.tensor(rec + plan, dtype=torch.int64)
+        grid = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+        codes_seq, lag, p1_items, L2 = [], 0, 0, 0
+        for L in range(n):  # P2(L2) follows once >= 1.25 grids of items lie after P1(L2)
+            codes_seq.append(2 * L)
+            p1_items += items[L]
+            while L2 < L and p1_items - sum(items[:L2 + 1]) >= 1.25 * grid:
+                codes_seq.append(2 * L2 + 1)
+                L2 += 1
+        codes_seq += [2 * L + 1 for L in range(L2, n)]
+        plan, p1s = [0], [0] * n
+        for gi, sc_ in enumerate(codes_seq):
+            plan.append(plan[-1] + items[sc_ >> 1])
+            if sc_ % 2 == 0:
+                p1s[sc_ >> 1] = gi
+        host = torch.tensor(rec + plan + codes_seq + p1s, dtype=torch.int64)
         dbuf = host.to(dev)
         descs = dbuf[:5 * n]
         plan_d = dbuf[5 * n:].to(torch.int32)

@@ -1,6 +1,6 @@
 """A/B of the block-fp8 -> per-tensor fp8 deploy over 96 DSv3 expert linears (32 experts x
-gate/up 2048x7168 + down 7168x2048): the one-launch streaming kernel (default) vs the two-pass
-pair (LCQ_FP8_DEPLOY=pair), interleaved rounds, kernel time from HIP events around the launch.
+gate/up 2048x7168 + down 7168x2048): the one-launch streaming kernel (LCQ_FP8_DEPLOY=stream)
+vs the two-pass pair (default), interleaved rounds, kernel time from HIP events around the launch.
 Algorithmic traffic 2 B per element."""
 import os
 import statistics

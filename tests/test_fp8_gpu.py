@@ -361,7 +361,7 @@ def test_block_fp8_to_tensor_stream_equals_pair(dev, fin, fout, monkeypatch):
         c_l, s_l = [cs[i] for i in lst], [ss[i] for i in lst]
         monkeypatch.setenv('LCQ_FP8_DEPLOY', 'stream')
         o1, sc1 = ops.fp8_block_to_tensor_many(c_l, s_l, 128, fout)
-        monkeypatch.setenv('LCQ_FP8_DEPLOY', 'pair')
+        monkeypatch.delenv('LCQ_FP8_DEPLOY')
         o2, sc2 = ops.fp8_block_to_tensor_many(c_l, s_l, 128, fout)
         torch.cuda.synchronize()
         for a, b in zip(o1, o2):
