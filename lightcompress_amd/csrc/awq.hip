@@ -784,7 +784,8 @@ extern "C" int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t co
 // layout cannot hold an IC-long row, so:
 //  * k_clip_pc_stats: one wave per row -> org max / min and every shrink step's clamp bounds
 //    and min/max qparams (the reference's fake_quant_weight_dynamic of the clamped row).
-//  * k_auto_clip_pc: a workgroup = 256 rows (lane = row) x PC_TT sampled tokens, k walked in
+//  * k_auto_clip_pc: a workgroup = 256 rows (lane = row) x PC_TT sampled tokens (16; 8 for
+//    fp16 asym), k walked in
 //    PC_KC-wide chunks whose x / fake-quantized x tiles sit transposed in LDS (wave-uniform
 //    broadcast reads); each k regenerates the 10 candidate weights in registers (Markstein
 //    quotient, as the quant kernels) and accumulates the DT-rounded products of the original
@@ -796,7 +797,8 @@ extern "C" int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t co
 // to a neighbouring DT value -> parity tier T2 (tests/test_awq_gpu.py: bounds equal on
 // >= 98 % of rows, chosen errors within a few DT ulps).
 // ----------------------------------------------------------------------------------------
-constexpr int PC_TT = 16;       // sampled tokens per workgroup
+constexpr int PC_TT_BF16 = 16;  // sampled tokens per workgroup (bf16: no VGPR spill)
+constexpr int PC_TT_MIN = 8;    // fp16 asym (the software RNE needs registers): 8 tokens
 constexpr int PC_KC = 128;      // k per LDS chunk
 constexpr int PC_NS = 10;       // shrink steps (max_shrink 0.5 x n_grid 20)
 constexpr int PC_QP = 5;        // per step: smin, smax, s, 1/s, z
@@ -861,7 +863,7 @@ __device__ __forceinline__ float fq_pc(float v, float smin, float smax, float qs
   return dtr<DT>((SYM ? tq : dtr<DT>(tq - qz)) * qs);
 }
 
-template <int DT, bool SYM>
+template <int DT, bool SYM, int PC_TT>
 __global__ void __launch_bounds__(256, 1) k_auto_clip_pc(const uint16_t* __restrict__ w,
                                                         const uint16_t* __restrict__ x,
                                                         const uint16_t* __restrict__ qx,
@@ -893,8 +895,10 @@ __global__ void __launch_bounds__(256, 1) k_auto_clip_pc(const uint16_t* __restr
   const uint16_t* qsrc = qx ? qx : x;
   for (int64_t k0 = 0; k0 < ic; k0 += PC_KC) {
     __syncthreads();
-    // stage PC_TT tokens x PC_KC k of x and qx transposed: thread -> (token, 8 k)
-    {
+    // stage PC_TT tokens x PC_KC k of x and qx transposed: thread -> (token, 8 k); 256
+    // threads cover 16 tokens, so with PC_TT 8 the upper half idles
+    static_assert(PC_TT * (PC_KC / 8) <= 256, "staging covers at most 256 threads");
+    if (tid < PC_TT * (PC_KC / 8)) {
       const int t = tid / (PC_KC / 8), c8 = (tid % (PC_KC / 8)) * 8;
       float a[8], b[8];
       if (t < tn) {
@@ -1000,7 +1004,7 @@ __global__ void __launch_bounds__(256) k_clip_pc_pick(const float* __restrict__ 
 }
 
 extern "C" int64_t lcq_auto_clip_pc_workspace_bytes(int64_t oc, int64_t T, int nsteps) {
-  const int64_t ntt = (T + PC_TT - 1) / PC_TT;
+  const int64_t ntt = (T + PC_TT_MIN - 1) / PC_TT_MIN;  // the larger tile count (fp16)
   return oc * PC_NS * PC_QP * 4 + oc * 2 * 4 + ntt * nsteps * oc * 4;
 }
 
@@ -1012,13 +1016,17 @@ static void launch_clip_pc(const void* w, const void* x, const void* qx, int64_t
   float* qp = reinterpret_cast<float*>(ws);
   float* orgmm = qp + oc * PC_NS * PC_QP;
   float* part = orgmm + oc * 2;
-  const int ntt = (int)((T + PC_TT - 1) / PC_TT);
+  // fp16: asym spills nothing at 8 tokens (200 spilled VGPRs at 16), sym spills less at 16
+  const int TT = (DT == LCQ_BF16 || sym) ? PC_TT_BF16 : PC_TT_MIN;
+  const int ntt = (int)((T + TT - 1) / TT);
   const auto* wp = reinterpret_cast<const uint16_t*>(w);
   const auto* fp = reinterpret_cast<const float*>(factors);
   hipLaunchKernelGGL(k_clip_pc_stats<DT>, dim3((unsigned)((oc + 3) / 4)), 256, 0, st, wp, oc,
                      ic, nsteps, fp, (float)qmin, (float)qmax, sym, clip_sym, qp, orgmm);
   const dim3 g((unsigned)((oc + 255) / 256), (unsigned)ntt);
-  auto k = sym ? k_auto_clip_pc<DT, true> : k_auto_clip_pc<DT, false>;
+  auto k = sym ? k_auto_clip_pc<DT, true, PC_TT_BF16>
+                : (DT == LCQ_BF16 ? k_auto_clip_pc<DT, false, PC_TT_BF16>
+                                  : k_auto_clip_pc<DT, false, PC_TT_MIN>);
   hipLaunchKernelGGL(k, g, 256, 0, st, wp, reinterpret_cast<const uint16_t*>(x),
                      reinterpret_cast<const uint16_t*>(qx), oc, ic, (int)T, nsteps, qp,
                      (float)qmin, (float)qmax, part);

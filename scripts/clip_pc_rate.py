@@ -24,4 +24,4 @@ for oc, ic in ((4096, 4096), (14336, 4096), (4096, 14336), (1024, 4096)):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 3
-    print(f'{oc}x{ic}: {ms:.2f} ms  {11 * T * oc * ic / ms / 1e9:.1f} G products/s', flush=True)
+    print(f'{oc}x{ic}: {ms:.2f} ms  {11 * T * oc * ic / ms / 1e9:.1f} T products/s', flush=True)
