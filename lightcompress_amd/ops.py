@@ -753,11 +753,13 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
         # profiles/r2s4_fp8_deploy_ab.txt). Work items of 65536 codes, P2(L) lagging P1(L)
         items = [-(-c.numel() // 65536) for c in codes]
         grid = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-        codes_seq, lag, p1_items, L2 = [], 0, 0, 0
+        cum = [0]
+        for v in items:
+            cum.append(cum[-1] + v)
+        codes_seq, L2 = [], 0
         for L in range(n):  # P2(L2) follows once >= 1.25 grids of items lie after P1(L2)
             codes_seq.append(2 * L)
-            p1_items += items[L]
-            while L2 < L and p1_items - sum(items[:L2 + 1]) >= 1.25 * grid:
+            while L2 < L and cum[L + 1] - cum[L2 + 1] >= 1.25 * grid:
                 codes_seq.append(2 * L2 + 1)
                 L2 += 1
         codes_seq += [2 * L + 1 for L in range(L2, n)]

@@ -23,6 +23,8 @@ for e in range(32):
         cs.append(r['codes'])
         ss.append(r['scales'])
 elems = sum(c.numel() for c in cs)
+from lightcompress_amd import _native  # noqa: E402
+ktime = {'stream': [], 'pair': []}
 res = {'stream': [], 'pair': []}
 outs = {}
 for r in range(5):
@@ -31,17 +33,22 @@ for r in range(5):
         ops.fp8_block_to_tensor_many(cs, ss, 128)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        timer = _native.KernelTimer()
         e0.record()
-        for _ in range(5):
-            o = ops.fp8_block_to_tensor_many(cs, ss, 128)
+        with timer:
+            for _ in range(5):
+                o = ops.fp8_block_to_tensor_many(cs, ss, 128)
         e1.record()
         torch.cuda.synchronize()
         res[v].append(e0.elapsed_time(e1) / 5)
+        ktime[v].append(sum(t['avg_ms'] for t in timer.summary().values()))
         outs[v] = o
 same = all(torch.equal(a.view(torch.uint8), b.view(torch.uint8))
            for a, b in zip(outs['stream'][0], outs['pair'][0])) and \
     torch.equal(outs['stream'][1], outs['pair'][1])
 for v in res:
     ms = statistics.median(res[v])
-    print(f'{v}: {ms:.3f} ms per call (incl. descriptor copy)  {2 * elems / ms / 1e6:.0f} GB/s  '
-          f'identical: {same}', flush=True)
+    km = statistics.median(ktime[v])
+    print(f'{v}: {ms:.3f} ms per call (incl. host plan + descriptor copy); launch (HIP events '
+          f'around the C call) {km:.3f} ms = {2 * elems / km / 1e6:.0f} GB/s; identical: {same}',
+          flush=True)
