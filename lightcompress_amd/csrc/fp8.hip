@@ -622,7 +622,7 @@ __global__ void __launch_bounds__(256) k_requant16_many(const Fp8Desc* d, Fp8Des
 // the whole grid resident (G = 4 per CU) the smallest unfinished item can always run; the spin
 // is bounded anyway (err flag, no hang). Codes equal the two-pass path's bit for bit (same
 // per-chunk arithmetic; max is order-independent).
-constexpr int B2T_ITEM = 4096;  // 16-byte chunks per work item (64 KB of codes)
+constexpr int B2T_ITEM = 32768;  // 16-byte chunks per work item (512 KB of codes)
 
 template <int FIN, int FOUT, bool ADD_ZERO>
 __global__ void __launch_bounds__(256) k_b2t_stream(const Fp8Desc* __restrict__ d,

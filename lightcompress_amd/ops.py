@@ -749,9 +749,9 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
             c.shape[1] % 16 == 0 and c.numel() < (1 << 28) and N.ptr(c) % 16 == 0 and
             N.ptr(o) % 16 == 0 for c, o in zip(codes, outs)):
         # opt-in: one persistent launch (lcq_fp8_block_to_tensor_stream; bit-identical, but
-        # measured 2.2 ms vs the pair's 0.99 ms over 96 DSv3 expert linears,
-        # profiles/r2s4_fp8_deploy_ab.txt). Work items of 65536 codes, P2(L) lagging P1(L)
-        items = [-(-c.numel() // 65536) for c in codes]
+        # measured 0.98 ms vs the pair's 0.86 ms over 96 DSv3 expert linears,
+        # profiles/r2s4_fp8_deploy_ab.txt). Work items of 524288 codes, P2(L) lagging P1(L)
+        items = [-(-c.numel() // 524288) for c in codes]
         grid = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         cum = [0]
         for v in items:
