@@ -47,41 +47,51 @@ enum { H_ALO = 0, H_AHI = 1, H_BLO = 2, H_BHI = 3 };
 __global__ void __launch_bounds__(256) k_xt_pack(const uint16_t* __restrict__ X, int64_t n,
                                                  int64_t ic, uint16_t* __restrict__ XT,
                                                  int64_t icp, int64_t kp) {
-  __shared__ uint16_t t[64][64 + 2];
-  const int64_t k0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+  // 64 tokens x 128 channels through LDS with a 65-dword row stride: the load phase stores 16 B
+  // per chunk as 4 dwords, the store phase reads one dword = 2 channels of a token, so a lane
+  // builds 8 tokens of 2 channels (two 16-B row pieces) from 8 dword reads; lanes (k8 = lane
+  // & 7, channel pair = lane >> 3) hit 64 distinct banks and 8 lanes write 128 contiguous
+  // bytes of an XT row (was: 16-bit reads, 16 per 16-B piece)
+  __shared__ uint32_t t[64][65];
+  const int64_t k0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 128;
   const int tid = threadIdx.x;
-  // load 64 tokens x 64 channels: 4 threads per... each thread 16 elements (2 x 8)
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int idx = it * 256 + tid;     // 0..511
-    const int r = idx >> 3, c8 = (idx & 7) * 8;
+  for (int it = 0; it < 4; ++it) {
+    const int idx = it * 256 + tid;     // 0..1023: token r, channels c8 .. c8 + 7
+    const int r = idx >> 4, c8 = (idx & 15) * 8;
     const int64_t k = k0 + r, c = c0 + c8;
-    uint16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint4 q = make_uint4(0, 0, 0, 0);
     if (k < n) {
       if (c + 7 < ic && (ic & 7) == 0) {
-        const uint4 q = *reinterpret_cast<const uint4*>(X + k * ic + c);
-        v[0] = q.x & 0xffff; v[1] = q.x >> 16; v[2] = q.y & 0xffff; v[3] = q.y >> 16;
-        v[4] = q.z & 0xffff; v[5] = q.z >> 16; v[6] = q.w & 0xffff; v[7] = q.w >> 16;
+        q = *reinterpret_cast<const uint4*>(X + k * ic + c);
       } else {
+        uint16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (c + j < ic) v[j] = X[k * ic + c + j];
+        q.x = v[0] | ((uint32_t)v[1] << 16); q.y = v[2] | ((uint32_t)v[3] << 16);
+        q.z = v[4] | ((uint32_t)v[5] << 16); q.w = v[6] | ((uint32_t)v[7] << 16);
       }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[r][c8 + j] = v[j];
+    t[r][c8 / 2 + 0] = q.x;
+    t[r][c8 / 2 + 1] = q.y;
+    t[r][c8 / 2 + 2] = q.z;
+    t[r][c8 / 2 + 3] = q.w;
   }
   __syncthreads();
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int idx = it * 256 + tid;
-    const int c = idx >> 3, k8 = (idx & 7) * 8;
-    uint4 q;
-    q.x = (uint32_t)t[k8 + 0][c] | ((uint32_t)t[k8 + 1][c] << 16);
-    q.y = (uint32_t)t[k8 + 2][c] | ((uint32_t)t[k8 + 3][c] << 16);
-    q.z = (uint32_t)t[k8 + 4][c] | ((uint32_t)t[k8 + 5][c] << 16);
-    q.w = (uint32_t)t[k8 + 6][c] | ((uint32_t)t[k8 + 7][c] << 16);
-    *reinterpret_cast<uint4*>(XT + (c0 + c) * kp + k0 + k8) = q;
+  for (int h = 0; h < 2; ++h) {
+    const int k8 = (tid & 7) * 8, cp = (tid >> 3) + 32 * h;  // channels 2cp, 2cp + 1
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = t[k8 + j][cp];
+    uint4 lo, hi;
+    lo.x = (w[0] & 0xffffu) | (w[1] << 16); hi.x = (w[0] >> 16) | (w[1] & 0xffff0000u);
+    lo.y = (w[2] & 0xffffu) | (w[3] << 16); hi.y = (w[2] >> 16) | (w[3] & 0xffff0000u);
+    lo.z = (w[4] & 0xffffu) | (w[5] << 16); hi.z = (w[4] >> 16) | (w[5] & 0xffff0000u);
+    lo.w = (w[6] & 0xffffu) | (w[7] << 16); hi.w = (w[6] >> 16) | (w[7] & 0xffff0000u);
+    *reinterpret_cast<uint4*>(XT + (c0 + 2 * cp) * kp + k0 + k8) = lo;
+    *reinterpret_cast<uint4*>(XT + (c0 + 2 * cp + 1) * kp + k0 + k8) = hi;
   }
 }
 
@@ -457,7 +467,7 @@ extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t 
   plan(n, ic, nt, ntiles, ns, ktps, kp, icp);
   hipStream_t st = as_stream(stream);
   uint16_t* xt = reinterpret_cast<uint16_t*>(workspace);
-  hipLaunchKernelGGL(k_xt_pack, dim3((unsigned)(kp / 64), (unsigned)(icp / 64)), 256, 0, st,
+  hipLaunchKernelGGL(k_xt_pack, dim3((unsigned)(kp / 64), (unsigned)(icp / 128)), 256, 0, st,
                      reinterpret_cast<const uint16_t*>(x), n, ic, xt, icp, kp);
   int rc = check_launch("lcq_hessian_accum: transpose");
   if (rc) return rc;
