@@ -179,11 +179,15 @@ int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t ic, void* H
  * qparams from the block-start weights written to s_out/z_out [rows, ng_total] (fp32);
  * group == 0: fixed per-row qparams s_in/z_in [rows] (per-channel).
  * losses optional [rows, ld] fp32: (w-q)^2 / (2 d^2).
+ * fmt 0: IntegerQuantizer qdq (quant.py:699-717). fmt LCQ_FP8E4M3 / LCQ_FP8E5M2: FloatQuantizer
+ * (use_qtorch, quant.py:1061-1080): q = float_quantize(w / s + 0) * s in fp32 with the
+ * saturating native cast, symmetric qparams with qmax = finfo.max (qmin, qmax,
+ * sym, z_in, z_out are ignored); the per-channel form is gptq_fp8.yml's column loop.
  * ------------------------------------------------------------------------------------- */
 int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, const void* U,
-                   int64_t ldu, int64_t group, int qmin, int qmax, int sym, const void* s_in,
-                   const void* z_in, void* s_out, void* z_out, int64_t ng_total, void* err,
-                   void* losses, void* stream);
+                   int64_t ldu, int64_t group, int qmin, int qmax, int sym, int fmt,
+                   const void* s_in, const void* z_in, void* s_out, void* z_out,
+                   int64_t ng_total, void* err, void* losses, void* stream);
 
 /* GPTQ static groups (gptq.py:224-227, static_groups: True): the same block loop with fixed
  * qparams per (row, ORIGINAL group): permuted column c uses s_in / z_in [rows, ngc] at group
@@ -290,12 +294,19 @@ int lcq_auto_clip_search_act(const void* w, const void* x, const void* qx, int d
  * activation fake-quant or NULL (weight-only), nsteps <= 10 with factors[nsteps] =
  * fp32(1 - i/n_grid) on device; best_max / best_min [oc] in dtype. Products rounded to dtype
  * like the reference's broadcast product; the ic-long fp32 sum runs in k order (parity tier
- * T2). workspace >= lcq_auto_clip_pc_workspace_bytes(oc, T, nsteps). */
+ * T2). workspace >= lcq_auto_clip_pc_workspace_bytes(oc, T, nsteps).
+ * fmt 0: integer weights. fmt LCQ_FP8E4M3 / LCQ_FP8E5M2: FloatQuantizer weights (use_qtorch;
+ * awq_fp8.yml / awq_fp8_static.yml): the candidates are fake_quant_weight_dynamic of the
+ * clamped weights with the saturating float_quantize stand-in (quant.py:545-553, 1061-1080;
+ * qmin / qmax / sym ignored). tensor_batch 0: per_channel scales (one per row); > 0:
+ * per_tensor scale over each batch of tensor_batch rows, the reference's oc_batch_size
+ * (auto_clip.py:108). */
 int64_t lcq_auto_clip_pc_workspace_bytes(int64_t oc, int64_t T, int nsteps);
 int lcq_auto_clip_search_pc(const void* w, const void* x, const void* qx, int dtype, int64_t oc,
                             int64_t ic, int64_t T, int nsteps, const void* factors, int qmin,
-                            int qmax, int sym, int clip_sym, void* workspace, int64_t ws_bytes,
-                            void* best_max, void* best_min, void* stream);
+                            int qmax, int sym, int clip_sym, int fmt, int tensor_batch,
+                            void* workspace, int64_t ws_bytes, void* best_max, void* best_min,
+                            void* stream);
 
 /* AutoClipper.apply_clip, v1 (auto_clip.py:193-212): out = clamp(x, cmin, cmax) per group;
  * cmin NULL -> -cmax. In place allowed. */
@@ -332,10 +343,14 @@ int lcq_fp8_quant(const void* x, int x_dtype, int64_t rows, int64_t cols, int64_
 
 /* FP8 quant with given scales (fake/real_quant_*_static, quant.py:1061-1076, 1119-1159):
  * s = rnd_ct(scales[e / group]) (0 -> 1); same cast / fake-quant rules as lcq_fp8_quant.
- * ct_dtype = torch.promote_types(x, scales). */
+ * ct_dtype = torch.promote_types(x, scales). saturate != 0 clamps the quotient to
+ * +-finfo.max before the cast (FloatQuantizer's float_quantize stand-in: with given scales a
+ * quotient can leave the format's range -- GPTQ's error-compensated columns, static act
+ * scales -- where c10's cast would give NaN); 0 = torch's `.to()` exactly. */
 int lcq_fp8_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols, int64_t group,
                          int fmt, int ct_dtype, const void* scales, int s_dtype, int add_zero,
-                         void* codes_out, void* fq_out, int fq_dtype, void* stream);
+                         int saturate, void* codes_out, void* fq_out, int fq_dtype,
+                         void* stream);
 
 /* 128x128-block FP8 quant of x [M, N] (N % 8 == 0): per_block FloatQuantizer (clamp_min 1e-5,
  * add_zero 1; quant.py:132-143, 636-641) and weight_cast_to_fp8 (kernel.py:57-81: clamp 0,

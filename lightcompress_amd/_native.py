@@ -56,8 +56,8 @@ SIGNATURES = {
                                _vp, _vp], _int),
     'lcq_hessian_workspace_bytes': ([_i64, _i64], _i64),
     'lcq_hessian_accum': ([_vp, _int, _i64, _i64, _vp, _f32, _f32, _vp, _i64, _vp], _int),
-    'lcq_gptq_block': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _int, _int, _int, _vp,
-                        _vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
+    'lcq_gptq_block': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _int, _int, _int, _int,
+                        _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
     'lcq_gptq_block_cols': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _int, _int, _vp, _vp, _vp,
                              _i64, _vp, _vp, _vp], _int),
     'lcq_chol_inv_tile': ([_vp, _i64, _int, _vp, _i64, _vp, _i64, _vp, _i64, _vp], _int),
@@ -75,13 +75,13 @@ SIGNATURES = {
                                   _int, _int, _int, _int, _vp, _f32, _vp, _vp, _vp], _int),
     'lcq_auto_clip_pc_workspace_bytes': ([_i64, _i64, _int], _i64),
     'lcq_auto_clip_search_pc': ([_vp, _vp, _vp, _int, _i64, _i64, _i64, _int, _vp, _int, _int,
-                                 _int, _int, _vp, _i64, _vp, _vp, _vp], _int),
+                                 _int, _int, _int, _int, _vp, _i64, _vp, _vp, _vp], _int),
     'lcq_clip_apply': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _vp, _vp], _int),
     'lcq_absmax': ([_vp, _int, _i64, _vp, _vp, _vp], _int),
     'lcq_fp8_quant': ([_vp, _int, _i64, _i64, _i64, _int, _int, _f32, _f32, _int, _vp, _vp, _vp,
                        _int, _vp, _vp], _int),
-    'lcq_fp8_quant_static': ([_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int, _int, _vp,
-                              _vp, _int, _vp], _int),
+    'lcq_fp8_quant_static': ([_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int, _int, _int,
+                              _vp, _vp, _int, _vp], _int),
     'lcq_fp8_quant_blocks': ([_vp, _int, _i64, _i64, _int, _int, _f32, _f32, _int, _vp, _vp,
                               _int, _vp, _vp], _int),
     'lcq_fp8_dequant_blocks': ([_vp, _int, _i64, _i64, _int, _vp, _vp, _int, _vp], _int),

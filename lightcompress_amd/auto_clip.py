@@ -52,11 +52,13 @@ class AutoClipper:
                 # share, gather the bounds (bit-identical to one GPU)
                 from .parallel import dist_world, gather_rows, row_shard
                 rank, wsz = dist_world()
-                r0, r1 = row_shard(m.weight.shape[0], rank, wsz)
+                align = self._float_quant(m.weight)[1] or 1  # per-tensor fp8: whole batches
+                r0, r1 = row_shard(m.weight.shape[0], rank, wsz, align)
                 mx, mn = self.auto_clip_layer(block_idx, n, m.weight.data[r0:r1], inputs,
-                                              n_sample_token=n_sample_token)
-                max_val = gather_rows(mx.contiguous(), m.weight.shape[0])
-                min_val = gather_rows(mn.contiguous(), m.weight.shape[0])
+                                              n_sample_token=n_sample_token,
+                                              tensor_batch=align if align > 1 else None)
+                max_val = gather_rows(mx.contiguous(), m.weight.shape[0], align)
+                min_val = gather_rows(mn.contiguous(), m.weight.shape[0], align)
                 self.apply_clip(block_idx, m, min_val, max_val, n)
                 continue
             max_val, min_val = self.auto_clip_layer(block_idx, n, m.weight, inputs,
@@ -80,8 +82,10 @@ class AutoClipper:
 
     @torch.no_grad()
     def auto_clip_layer(self, block_idx, layer_name, w, inputs, n_grid=20, max_shrink=0.5,
-                        n_sample_token=512, eps=0.0):
-        """Returns (best_max_val, best_min_val) shaped [oc, ng, 1] like the reference."""
+                        n_sample_token=512, eps=0.0, tensor_batch=None):
+        """Returns (best_max_val, best_min_val) shaped [oc, ng, 1] like the reference.
+        tensor_batch: the per-tensor FP8 batch rows of the whole layer when ``w`` is a row
+        shard of it (the shard's own row count would pick a different batch size)."""
         assert w.dim() == 2
         wq = self.wquantizer
         group = wq.group_size if wq.granularity == 'per_group' else w.shape[1]
@@ -89,14 +93,20 @@ class AutoClipper:
             raise NotImplementedError('auto-clip over several calibration tensors')
         if w.dtype not in (torch.bfloat16, torch.float16):
             raise NotImplementedError('device auto-clip kernel takes bf16 / fp16 weights')
-        per_channel = wq.granularity == 'per_channel'
+        fp8, tb = self._float_quant(w)
+        tensor_batch = tb if (tensor_batch is None or not tb) else tensor_batch
+        per_channel = wq.granularity in ('per_channel', 'per_tensor')
         if not per_channel and group not in (32, 64, 128, 256):
             raise NotImplementedError(f'device auto-clip kernel: group size {group}')
         if per_channel and (w.shape[1] % 128 or wq.calib_algo == 'mse'):
             raise NotImplementedError('per_channel auto-clip: ic % 128 == 0, minmax qparams')
-        if getattr(wq, 'quant_type', 'int-quant') != 'int-quant':
-            raise NotImplementedError('auto-clip of float-quant weights is not on the device '
-                                      'path')
+        if wq.granularity == 'per_tensor' and fp8 is None:
+            raise NotImplementedError('per_tensor integer auto-clip is not on the device path')
+        if (getattr(wq, 'quant_type', 'int-quant') == 'int-quant'
+                and (not getattr(wq, 'round_zp', True) or wq.calib_algo == 'hqq')):
+            # the kernels form round_zp / minmax (or mse) qparams of every candidate
+            raise NotImplementedError('auto-clip with round_zp False / calib_algo hqq is not '
+                                      'on the device path')
         x = self.sample_tokens(inputs[0], n_sample_token)
         qx = None
         if not self.w_only:
@@ -109,7 +119,24 @@ class AutoClipper:
         if wq.calib_algo == 'mse':  # every step's fake quant searches its range
             mse = (wq._mse_nsteps(), wq.mse_grid, 2.4)
         return ops.auto_clip_search(w.data, x, group, int(max_shrink * n_grid), n_grid, qmin,
-                                    qmax, wq.sym, self.clip_sym, mse=mse, qx=qx)
+                                    qmax, wq.sym, self.clip_sym, mse=mse, qx=qx, fp8=fp8,
+                                    tensor_batch=tensor_batch)
+
+    def _float_quant(self, w):
+        """(fp8 dtype, per-tensor batch rows) for FloatQuantizer weights, (None, 0) for
+        integer ones. The reference fake-quantizes 256 (else 64) rows at a time
+        (auto_clip.py:108-114), so a per_tensor scale is one per such batch of clamped rows."""
+        wq = self.wquantizer
+        if getattr(wq, 'quant_type', 'int-quant') == 'int-quant':
+            return None, 0
+        if (not getattr(wq, 'use_qtorch', False) or getattr(wq, 'fp8_dtype', None) is None
+                or 'float_range' in getattr(wq, 'kwargs', {}) or wq.calib_algo != 'minmax'
+                or wq.granularity not in ('per_channel', 'per_tensor')):
+            raise NotImplementedError('float-quant auto-clip: use_qtorch e4m3 / e5m2, minmax, '
+                                      'per_channel or per_tensor weights')
+        if wq.granularity == 'per_tensor':
+            return wq.fp8_dtype, (256 if w.shape[0] % 256 == 0 else 64)
+        return wq.fp8_dtype, 0
 
     @torch.no_grad()
     def apply_clip(self, block_idx, layer, min_val, max_val, layer_name):

@@ -145,10 +145,13 @@ class Awq(BaseBlockwiseQuantization):
         return torch.cat(outs, dim=0)
 
     def fake_quantize_weight(self, fc, scales, out):
-        """awq.py:147-164: Q(W * s) in the weight dtype, fused in one kernel."""
+        """awq.py:147-164: Q(W * s) in the weight dtype, fused in one kernel for integer
+        minmax quantizers; W * s then the quantizer's own fake_quant_weight_dynamic otherwise
+        (calib_algo mse / hqq, round_zp False, FloatQuantizer weights: awq_fp8*.yml)."""
         wq = self.wquantizer
         w = fc.weight.data
-        if wq.calib_algo == 'mse':  # the range search needs W * s itself
+        if (wq.calib_algo in ('mse', 'hqq') or getattr(wq, 'quant_type', 'int-quant') != 'int-quant'
+                or not getattr(wq, 'round_zp', True)):
             ops.scale_bcast(w, scales.to(w.dtype), 'mul', out=out)
             out.copy_(wq.fake_quant_weight_dynamic(out))
             return out

@@ -12,6 +12,7 @@
 //   auto_clip_layer    auto_clip.py:83-191 (10-step shrink grid)          -> lcq_auto_clip_search
 //   apply_clip (v1)    auto_clip.py:193-212                               -> lcq_clip_apply
 #include "lcq_common.h"
+#include "lcq_fp8.h"
 #include <stdlib.h>
 
 namespace lcq {
@@ -803,7 +804,12 @@ constexpr int PC_KC = 128;      // k per LDS chunk
 constexpr int PC_NS = 10;       // shrink steps (max_shrink 0.5 x n_grid 20)
 constexpr int PC_QP = 5;        // per step: smin, smax, s, 1/s, z
 
-template <int DT>
+// FQ (float-quant weights, FloatQuantizer use_qtorch, quant.py:545-553 / 1061-1080):
+//   0 integer; 1 FP8 per_channel: s = rnd_DT(max(|cmax|, |cmin|).clamp(1e-5) / qmax) per row;
+//   2 FP8 per_tensor: the clamped row's max(|cmax|, |cmin|) is left in slot 2 for
+//     k_clip_pc_tensor_qp, which forms the scale of the whole 256 (or 64)-row batch the
+//     reference fake-quantizes at once (auto_clip.py:108-114, 161-163).
+template <int DT, int FQ>
 __global__ void __launch_bounds__(256) k_clip_pc_stats(const uint16_t* __restrict__ w,
                                                       int64_t oc, int64_t ic, int nsteps,
                                                       const float* __restrict__ factors,
@@ -841,7 +847,13 @@ __global__ void __launch_bounds__(256) k_clip_pc_stats(const uint16_t* __restric
     const float smin = clip_sym ? -smax : dtr<DT>(org_min * f);
     const float cmn = fminf(fmaxf(mn, smin), smax), cmx = fminf(fmaxf(mx, smin), smax);
     float qs, qz;
-    qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
+    if constexpr (FQ == 0) {
+      qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
+    } else {
+      const float am = fmaxf(fmaxf(fabsf(cmx), fabsf(cmn)), dtr<DT>(1e-5f));  // .clamp(1e-5)
+      qs = FQ == 1 ? dtr<DT>(am / qmax) : am;
+      qz = 0.f;
+    }
     float* d = qp + ((int64_t)o * PC_NS + lane) * PC_QP;
     d[0] = smin;
     d[1] = smax;
@@ -863,7 +875,41 @@ __device__ __forceinline__ float fq_pc(float v, float smin, float smax, float qs
   return dtr<DT>((SYM ? tq : dtr<DT>(tq - qz)) * qs);
 }
 
-template <int DT, bool SYM, int PC_TT>
+// FP8 per_tensor: every step's scale over the rows of one reference batch (get_minmax_range
+// of the whole clamped [rows, 1, 1, ic] batch -> 0-dim DT values; their clamp stays DT; the
+// division by the 0-dim fp32 qmax promotes to fp32, so the batch scale is fp32).
+__global__ void __launch_bounds__(256) k_clip_pc_tensor_qp(float* __restrict__ qp, int64_t oc,
+                                                          int nsteps, int batch, float qmax) {
+  __shared__ float red[4];
+  const int64_t o = (int64_t)blockIdx.x * batch + threadIdx.x;
+  const bool live = threadIdx.x < batch && o < oc;
+  for (int i = 0; i < nsteps; ++i) {
+    float am = live ? qp[((int64_t)o * PC_NS + i) * PC_QP + 2] : 0.f;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) am = fmaxf(am, __shfl_xor(am, m, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+    __syncthreads();
+    const float s = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) / qmax;
+    __syncthreads();
+    if (live) {
+      float* d = qp + ((int64_t)o * PC_NS + i) * PC_QP;
+      d[2] = s;
+      d[3] = 1.0f / s;
+    }
+  }
+}
+
+// FloatQuantizer fake quant of one clamped weight (quant.py:1061-1080 through
+// fake_quant_weight_dynamic): DT quotient (a per-tensor fp32 scale is a CPU scalar to torch:
+// full precision), `+ zeros`, float_quantize (saturating native cast), fp32 (q - 0) * s, DT.
+template <int DT, int FMT>
+__device__ __forceinline__ float fq_pc_fp8(float v, float smin, float smax, float qs) {
+  v = fminf(fmaxf(v, smin), smax);
+  const float t = dtr<DT>(dtr<DT>(v / qs) + 0.0f);
+  return dtr<DT>(fp8_round<FMT>(t) * qs);
+}
+
+template <int DT, bool SYM, int PC_TT, int FMT = 0>
 __global__ void __launch_bounds__(256, 1) k_auto_clip_pc(const uint16_t* __restrict__ w,
                                                         const uint16_t* __restrict__ x,
                                                         const uint16_t* __restrict__ qx,
@@ -942,8 +988,11 @@ __global__ void __launch_bounds__(256, 1) k_auto_clip_pc(const uint16_t* __restr
         }
 #pragma unroll
         for (int i = 0; i < PC_NS; ++i) {
-          const float c = fq_pc<DT, SYM>(wv[j], q[i][0], q[i][1], q[i][2], q[i][3], q[i][4],
-                                         qmin, qmax);
+          float c;
+          if constexpr (FMT == 0)
+            c = fq_pc<DT, SYM>(wv[j], q[i][0], q[i][1], q[i][2], q[i][3], q[i][4], qmin, qmax);
+          else
+            c = fq_pc_fp8<DT, FMT>(wv[j], q[i][0], q[i][1], q[i][2]);
           const v2f cp = {c, c};
 #pragma unroll
           for (int t = 0; t < PC_TT / 2; ++t)
@@ -1011,22 +1060,35 @@ extern "C" int64_t lcq_auto_clip_pc_workspace_bytes(int64_t oc, int64_t T, int n
 template <int DT>
 static void launch_clip_pc(const void* w, const void* x, const void* qx, int64_t oc, int64_t ic,
                            int64_t T, int nsteps, const void* factors, int qmin, int qmax,
-                           int sym, int clip_sym, char* ws, void* best_max, void* best_min,
-                           hipStream_t st) {
+                           int sym, int clip_sym, int fmt, int tensor_batch, char* ws,
+                           void* best_max, void* best_min, hipStream_t st) {
   float* qp = reinterpret_cast<float*>(ws);
   float* orgmm = qp + oc * PC_NS * PC_QP;
   float* part = orgmm + oc * 2;
   // fp16: asym spills nothing at 8 tokens (200 spilled VGPRs at 16), sym spills less at 16
-  const int TT = (DT == LCQ_BF16 || sym) ? PC_TT_BF16 : PC_TT_MIN;
+  const int TT = (DT == LCQ_BF16 || sym || fmt != 0) ? PC_TT_BF16 : PC_TT_MIN;
   const int ntt = (int)((T + TT - 1) / TT);
   const auto* wp = reinterpret_cast<const uint16_t*>(w);
   const auto* fp = reinterpret_cast<const float*>(factors);
-  hipLaunchKernelGGL(k_clip_pc_stats<DT>, dim3((unsigned)((oc + 3) / 4)), 256, 0, st, wp, oc,
-                     ic, nsteps, fp, (float)qmin, (float)qmax, sym, clip_sym, qp, orgmm);
+  const dim3 gs((unsigned)((oc + 3) / 4));
+  if (fmt == 0)
+    hipLaunchKernelGGL((k_clip_pc_stats<DT, 0>), gs, 256, 0, st, wp, oc, ic, nsteps, fp,
+                       (float)qmin, (float)qmax, sym, clip_sym, qp, orgmm);
+  else if (tensor_batch == 0)
+    hipLaunchKernelGGL((k_clip_pc_stats<DT, 1>), gs, 256, 0, st, wp, oc, ic, nsteps, fp,
+                       (float)qmin, (float)qmax, sym, clip_sym, qp, orgmm);
+  else {
+    hipLaunchKernelGGL((k_clip_pc_stats<DT, 2>), gs, 256, 0, st, wp, oc, ic, nsteps, fp,
+                       (float)qmin, (float)qmax, sym, clip_sym, qp, orgmm);
+    hipLaunchKernelGGL(k_clip_pc_tensor_qp, dim3((unsigned)((oc + tensor_batch - 1) / tensor_batch)),
+                       256, 0, st, qp, oc, nsteps, tensor_batch, (float)qmax);
+  }
   const dim3 g((unsigned)((oc + 255) / 256), (unsigned)ntt);
-  auto k = sym ? k_auto_clip_pc<DT, true, PC_TT_BF16>
-                : (DT == LCQ_BF16 ? k_auto_clip_pc<DT, false, PC_TT_BF16>
-                                  : k_auto_clip_pc<DT, false, PC_TT_MIN>);
+  auto k = fmt == LCQ_FP8E4M3 ? k_auto_clip_pc<DT, true, PC_TT_BF16, LCQ_FP8E4M3>
+         : fmt == LCQ_FP8E5M2 ? k_auto_clip_pc<DT, true, PC_TT_BF16, LCQ_FP8E5M2>
+         : sym ? k_auto_clip_pc<DT, true, PC_TT_BF16>
+               : (DT == LCQ_BF16 ? k_auto_clip_pc<DT, false, PC_TT_BF16>
+                                 : k_auto_clip_pc<DT, false, PC_TT_MIN>);
   hipLaunchKernelGGL(k, g, 256, 0, st, wp, reinterpret_cast<const uint16_t*>(x),
                      reinterpret_cast<const uint16_t*>(qx), oc, ic, (int)T, nsteps, qp,
                      (float)qmin, (float)qmax, part);
@@ -1038,11 +1100,21 @@ static void launch_clip_pc(const void* w, const void* x, const void* qx, int64_t
 extern "C" int lcq_auto_clip_search_pc(const void* w, const void* x, const void* qx, int dtype,
                                        int64_t oc, int64_t ic, int64_t T, int nsteps,
                                        const void* factors, int qmin, int qmax, int sym,
-                                       int clip_sym, void* workspace, int64_t ws_bytes,
-                                       void* best_max, void* best_min, void* stream) {
+                                       int clip_sym, int fmt, int tensor_batch, void* workspace,
+                                       int64_t ws_bytes, void* best_max, void* best_min,
+                                       void* stream) {
   LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16, "auto-clip: bf16 or fp16 model dtype");
   LCQ_REQUIRE(oc > 0 && ic > 0 && ic % PC_KC == 0, "per-channel auto-clip: ic % 128 == 0");
   LCQ_REQUIRE(T > 0 && nsteps >= 1 && nsteps <= PC_NS, "bad T / nsteps (<= 10)");
+  LCQ_REQUIRE(fmt == 0 || fmt == LCQ_FP8E4M3 || fmt == LCQ_FP8E5M2,
+              "fmt must be 0 (integer) or an fp8 format");
+  LCQ_REQUIRE(tensor_batch == 0 || (fmt != 0 && tensor_batch > 0 && tensor_batch <= 256),
+              "tensor_batch (per-tensor fp8 scale rows) must be 1..256, fp8 only");
+  if (fmt != 0) {  // FloatQuantizer: symmetric, qmax = finfo.max
+    qmax = fmt == LCQ_FP8E4M3 ? 448 : 57344;
+    qmin = -qmax;
+    sym = 1;
+  }
   LCQ_REQUIRE(qmax > qmin, "qmax <= qmin");
   LCQ_REQUIRE(workspace != nullptr &&
                   ws_bytes >= lcq_auto_clip_pc_workspace_bytes(oc, T, nsteps),
@@ -1051,9 +1123,9 @@ extern "C" int lcq_auto_clip_search_pc(const void* w, const void* x, const void*
   char* ws = reinterpret_cast<char*>(workspace);
   if (dtype == LCQ_BF16)
     launch_clip_pc<LCQ_BF16>(w, x, qx, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym,
-                             ws, best_max, best_min, st);
+                             fmt, tensor_batch, ws, best_max, best_min, st);
   else
     launch_clip_pc<LCQ_F16>(w, x, qx, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym,
-                            ws, best_max, best_min, st);
+                            fmt, tensor_batch, ws, best_max, best_min, st);
   return check_launch("lcq_auto_clip_search_pc");
 }

@@ -18,72 +18,9 @@
 // the amax and the cast (one HBM read). No MFMA: this is byte work, not a GEMM.
 #define LCQ_BF16_HW 1  // bf16 rounding on v_cvt_pk_bf16_f32 (see lcq_common.h)
 #include "lcq_common.h"
+#include "lcq_fp8.h"
 
 namespace lcq {
-
-// ---------------------------------------------------------------------------------------
-// fp32 -> fp8 encoders with c10's exact rounding, and exact decoders
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t enc_e4m3(float f) {
-  uint32_t b = __float_as_uint(f);
-  const uint32_t sign = b & 0x80000000u;
-  b ^= sign;
-  uint32_t r;
-  if (b >= (1087u << 20)) {
-    r = 0x7f;
-  } else if (b < (121u << 23)) {
-    const float t = __uint_as_float(b) + __uint_as_float(141u << 23);
-    r = (__float_as_uint(t) - (141u << 23)) & 0xffu;
-  } else {
-    const uint32_t odd = (b >> 20) & 1u;
-    b += ((uint32_t)(7 - 127) << 23) + 0x7ffffu;
-    b += odd;
-    r = (b >> 20) & 0xffu;
-  }
-  return r | (sign >> 24);
-}
-
-__device__ __forceinline__ uint32_t enc_e5m2(float f) {
-  uint32_t b = __float_as_uint(f);
-  const uint32_t sign = b & 0x80000000u;
-  b ^= sign;
-  uint32_t r;
-  if (b >= (143u << 23)) {
-    r = b > 0x7f800000u ? 0x7fu : 0x7cu;
-  } else if (b < (113u << 23)) {
-    const float t = __uint_as_float(b) + __uint_as_float(134u << 23);
-    r = (__float_as_uint(t) - (134u << 23)) & 0xffu;
-  } else {
-    const uint32_t odd = (b >> 21) & 1u;
-    b += ((uint32_t)(15 - 127) << 23) + 0xfffffu;
-    b += odd;
-    r = (b >> 21) & 0xffu;
-  }
-  return r | (sign >> 24);
-}
-
-__device__ __forceinline__ float dec_e4m3(uint32_t u) {
-  const uint32_t sign = (u & 0x80u) << 24;
-  const uint32_t e = (u >> 3) & 15u, m = u & 7u;
-  if (e == 15u && m == 7u) return __uint_as_float(0x7fc00000u | sign);
-  if (e == 0u) return __uint_as_float(__float_as_uint((float)m * 0.001953125f) | sign);
-  return __uint_as_float(sign | ((e + 120u) << 23) | (m << 20));
-}
-
-__device__ __forceinline__ float dec_e5m2(uint32_t u) {
-  return (float)__builtin_bit_cast(_Float16, (uint16_t)(u << 8));
-}
-
-template <int FMT>
-__device__ __forceinline__ uint32_t enc(float f) {
-  if constexpr (FMT == LCQ_FP8E4M3) return enc_e4m3(f);
-  else return enc_e5m2(f);
-}
-template <int FMT>
-__device__ __forceinline__ float dec(uint32_t u) {
-  if constexpr (FMT == LCQ_FP8E4M3) return dec_e4m3(u);
-  else return dec_e5m2(u);
-}
 
 __device__ __forceinline__ void st_codes8(void* p, int64_t e0, const uint32_t (&c)[8]) {
   const uint32_t lo = c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24);
@@ -105,6 +42,7 @@ struct Fp8Args {
   int64_t rows, cols, group;
   float qmax, clamp_min;
   int add_zero;              // quant.py quant(): scales 0 -> 1, `+ zeros` (0.0) after the division
+  int saturate;              // float_quantize stand-in: clamp to +-finfo.max before the cast
   const float* tensor_amax;  // per-tensor mode: device scalar from lcq_absmax
   void* codes;
   void* fq;
@@ -128,11 +66,12 @@ __device__ __forceinline__ float fp8_scale(float amax, float qmax, float clamp_m
 // x -> code / fake-quant for 8 elements sharing scale s
 template <int CT, int FMT>
 __device__ __forceinline__ void fp8_qdq8(const float (&w)[8], float s, int add_zero,
-                                         uint32_t (&c)[8], float (&dq)[8]) {
+                                         int saturate, uint32_t (&c)[8], float (&dq)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     float v = rnd<CT>(w[j] / s);
     if (add_zero) v = rnd<CT>(v + 0.0f);  // `+ zeros`: -0 -> +0
+    if (saturate) v = fp8_sat<FMT>(v);
     c[j] = enc<FMT>(v);
     dq[j] = dec<FMT>(c[j]) * s;  // fp32 q times the scale (promotes to fp32), exact
   }
@@ -143,7 +82,7 @@ __device__ __forceinline__ void fp8_emit(const Fp8Args& a, int64_t e0, const flo
                                          float s) {
   uint32_t c[8];
   float dq[8];
-  fp8_qdq8<CT, FMT>(w, s, a.add_zero, c, dq);
+  fp8_qdq8<CT, FMT>(w, s, a.add_zero, a.saturate, c, dq);
   if (a.codes) st_codes8(a.codes, e0, c);
   if (a.fq) st_any8(a.fq, a.fq_dt, e0, dq);
 }
@@ -390,7 +329,7 @@ __global__ void __launch_bounds__(256) k_requant_blockfp8_many(const Fp8Desc* d,
     float w[8], dq[8];
     uint32_t cc[8];
     deq8_row<FIN>(t.codes + r * t.N, t.s_inv[rb_ * nb_ + cbk_], c, w);
-    fp8_qdq8<LCQ_BF16, FOUT>(w, sc, add_zero, cc, dq);
+    fp8_qdq8<LCQ_BF16, FOUT>(w, sc, add_zero, 0, cc, dq);
     st_codes8(t.out, r * t.N + c, cc);
   LCQ_ROWS_END
   if (blockIdx.x == 0 && threadIdx.x == 0) s_out[blockIdx.y] = sc;
@@ -930,8 +869,8 @@ extern "C" int lcq_fp8_quant(const void* x, int x_dtype, int64_t rows, int64_t c
 
 extern "C" int lcq_fp8_quant_static(const void* x, int x_dtype, int64_t rows, int64_t cols,
                                     int64_t group, int fmt, int ct_dtype, const void* scales,
-                                    int s_dtype, int add_zero, void* codes_out, void* fq_out,
-                                    int fq_dtype, void* stream) {
+                                    int s_dtype, int add_zero, int saturate, void* codes_out,
+                                    void* fq_out, int fq_dtype, void* stream) {
   LCQ_REQUIRE(is_float_dt(x_dtype) && is_float_dt(ct_dtype) && is_float_dt(s_dtype),
               "x / compute / scale dtypes must be f32/f16/bf16");
   LCQ_REQUIRE(fmt == LCQ_FP8E4M3 || fmt == LCQ_FP8E5M2, "fmt must be e4m3fn or e5m2");
@@ -941,7 +880,7 @@ extern "C" int lcq_fp8_quant_static(const void* x, int x_dtype, int64_t rows, in
   LCQ_REQUIRE(fq_out == nullptr || is_float_dt(fq_dtype), "bad fq dtype");
   Fp8Args a{};
   a.x = x; a.rows = rows; a.cols = cols; a.group = group;
-  a.add_zero = add_zero;
+  a.add_zero = add_zero; a.saturate = saturate;
   a.codes = codes_out; a.fq = fq_out; a.fq_dt = fq_dtype;
   const unsigned grid = stream_grid(rows * cols / 8, 256);
   hipStream_t st = as_stream(stream);

@@ -13,6 +13,7 @@
 // is bit-exact given the same block-start W and U. The trailing update
 // W[:, i2:] -= Err @ U[i1:i2, i2:] is a GEMM done by the caller.
 #include "lcq_common.h"
+#include "lcq_fp8.h"
 
 namespace lcq {
 
@@ -44,7 +45,10 @@ struct GptqArgs {
 // contiguous bytes). err is written k-major ([128][rows]) for the trailing GEMM's staging.
 constexpr int LPR = 8, CPL = GB / LPR;
 
-template <int GS>
+// FMT = 0: IntegerQuantizer (quant.py:699-717); FMT = LCQ_FP8E4M3 / LCQ_FP8E5M2: FloatQuantizer
+// use_qtorch (quant.py:1061-1080): q = float_quantize(w / s + 0) * s in fp32, sym qparams with
+// qmax = finfo.max (per-group: the same fp32 formula as the int sym case).
+template <int GS, int FMT>
 __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
   __shared__ float u[GB * GB];
   const int tid = threadIdx.x;
@@ -128,10 +132,15 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
       const float d = u[c * GB + c];
       const float wc = w[jl];
       const float cs = (GS < 0) ? qsk[jl] : qs, cz = (GS < 0) ? qzk[jl] : qz;
-      float t = rintf(wc / cs);
-      t = t + cz;
-      t = fminf(fmaxf(t, a.qmin), a.qmax);
-      const float q = (t - cz) * cs;
+      float q;
+      if constexpr (FMT == 0) {
+        float t = rintf(wc / cs);
+        t = t + cz;
+        t = fminf(fmaxf(t, a.qmin), a.qmax);
+        q = (t - cz) * cs;
+      } else {
+        q = fp8_round<FMT>(wc / cs + 0.0f) * cs;
+      }
       const float diff = wc - q;
       const float e = __shfl(diff / d, rowlane | owner, 64);
       if (sub == owner) {
@@ -191,15 +200,34 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
 
 using namespace lcq;
 
+template <int FMT>
+static void launch_gptq_block(const GptqArgs& a, int64_t group, dim3 grid, hipStream_t st) {
+  switch (group) {
+    case 32: hipLaunchKernelGGL((k_gptq_block<32, FMT>), grid, 256, 0, st, a); break;
+    case 64: hipLaunchKernelGGL((k_gptq_block<64, FMT>), grid, 256, 0, st, a); break;
+    case 128: hipLaunchKernelGGL((k_gptq_block<128, FMT>), grid, 256, 0, st, a); break;
+    default: hipLaunchKernelGGL((k_gptq_block<0, FMT>), grid, 256, 0, st, a); break;
+  }
+}
+
 extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count,
                               const void* U, int64_t ldu, int64_t group, int qmin, int qmax,
-                              int sym, const void* s_in, const void* z_in, void* s_out,
+                              int sym, int fmt, const void* s_in, const void* z_in, void* s_out,
                               void* z_out, int64_t ng_total, void* err, void* losses,
                               void* stream) {
   LCQ_REQUIRE(rows > 0 && ld > 0 && count > 0 && count <= GB, "bad block shape");
   LCQ_REQUIRE(col0 >= 0 && col0 + count <= ld && col0 + count <= ldu, "block out of range");
   LCQ_REQUIRE(col0 % GB == 0, "col0 must be a multiple of the 128-column blocksize");
   LCQ_REQUIRE(ld % 4 == 0 && ldu % 4 == 0, "row lengths must be multiples of 4 (16-B rows)");
+  LCQ_REQUIRE(fmt == 0 || fmt == LCQ_FP8E4M3 || fmt == LCQ_FP8E5M2,
+              "fmt must be 0 (integer) or an fp8 format");
+  if (fmt != 0) {  // FloatQuantizer: symmetric, qmax = finfo.max, no zero point
+    qmin = fmt == LCQ_FP8E4M3 ? -448 : -57344;
+    qmax = -qmin;
+    sym = 1;
+    z_in = nullptr;
+    z_out = nullptr;
+  }
   LCQ_REQUIRE(qmax > qmin, "qmax <= qmin");
   GptqArgs a{};
   a.W = reinterpret_cast<float*>(W);
@@ -215,18 +243,12 @@ extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, i
   a.losses = reinterpret_cast<float*>(losses);
   LCQ_REQUIRE(group == 0 || group == 32 || group == 64 || group == 128,
               "group must be 0 (per-row qparams), 32, 64 or 128");
+  LCQ_REQUIRE(group != 0 || s_in != nullptr, "fixed-qparams mode needs s_in");
   const dim3 grid((unsigned)((rows + (256 / LPR) - 1) / (256 / LPR)));
   hipStream_t st = as_stream(stream);
-  switch (group) {
-    case 32: hipLaunchKernelGGL((k_gptq_block<32>), grid, 256, 0, st, a); break;
-    case 64: hipLaunchKernelGGL((k_gptq_block<64>), grid, 256, 0, st, a); break;
-    case 128: hipLaunchKernelGGL((k_gptq_block<128>), grid, 256, 0, st, a); break;
-    case 0:
-      LCQ_REQUIRE(s_in != nullptr, "fixed-qparams mode needs s_in");
-      hipLaunchKernelGGL((k_gptq_block<0>), grid, 256, 0, st, a);
-      break;
-    default: return fail(LCQ_EUNSUP, "lcq_gptq_block: group size must be 32, 64 or 128");
-  }
+  if (fmt == LCQ_FP8E4M3) launch_gptq_block<LCQ_FP8E4M3>(a, group, grid, st);
+  else if (fmt == LCQ_FP8E5M2) launch_gptq_block<LCQ_FP8E5M2>(a, group, grid, st);
+  else launch_gptq_block<0>(a, group, grid, st);
   return check_launch("lcq_gptq_block");
 }
 
@@ -388,7 +410,7 @@ extern "C" int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t co
   a.err = reinterpret_cast<float*>(err);
   a.losses = reinterpret_cast<float*>(losses);
   const dim3 grid((unsigned)((rows + (256 / LPR) - 1) / (256 / LPR)));
-  hipLaunchKernelGGL((k_gptq_block<-1>), grid, 256, 0, as_stream(stream), a);
+  hipLaunchKernelGGL((k_gptq_block<-1, 0>), grid, 256, 0, as_stream(stream), a);
   return check_launch("lcq_gptq_block_cols");
 }
 

@@ -257,7 +257,7 @@ def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
 def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
                 qmin: int, qmax: int, fixed=None, losses: bool = False,
                 superblock: int | None = None, col_group: torch.Tensor | None = None,
-                ncols_q: int | None = None, col_qparams=None):
+                ncols_q: int | None = None, col_qparams=None, fp8=None):
     """Blocked OBS loop (gptq.py:198-244) on permuted fp32 W, in place.
 
     Per 128-column block: the HIP kernel runs the in-block sequential loop (bit-exact rank-1
@@ -274,7 +274,10 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     computes a group's qparams when the loop reaches its first column, from the global W,
     whose columns of the current block are not updated inside the block (gptq.py:213-222,
     search_column_qparams :359-366): so every group starting in a block gets its qparams from
-    the block-start W, here before the block kernel, which then quantizes with them."""
+    the block-start W, here before the block kernel, which then quantizes with them.
+
+    ``fp8`` (a torch float8 dtype): FloatQuantizer weights (gptq_fp8.yml) -- the in-block
+    quant_dequant is float_quantize(w / s) * s (quant.py:1061-1080), symmetric."""
     rows, cols = W.shape
     dev = W.device
     U = U.contiguous()
@@ -321,7 +324,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
                 ops.gptq_block_cols(W, i1, cnt, U, qmin, qmax, s_in, z_in, col_group, e, L)
             else:
                 ops.gptq_block(W, i1, cnt, U, group or 0, qmin, qmax, sym, s_out, z_out, e, L,
-                               s_in, z_in)
+                               s_in, z_in, fp8=fp8)
             if i2 < sb1:  # near columns: the rest of this superblock
                 ops.gptq_trailing(W, i1, cnt, i2, e, U, c2=sb1)
         if sb1 < cols:    # far columns: the whole superblock's errors at once
@@ -331,17 +334,50 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     return s_out, z_out, L
 
 
+def check_quantizer(wquantizer, static_groups=False, owq_nout=0):
+    """The quantizer settings the device column loop implements; anything else raises
+    instead of running a different quantizer. Returns the fp8 dtype for FloatQuantizer
+    weights, else None."""
+    qt = getattr(wquantizer, 'quant_type', 'int-quant')
+    algo = getattr(wquantizer, 'calib_algo', 'minmax')
+    if qt == 'int-quant':
+        if algo not in ('minmax', 'mse'):
+            raise NotImplementedError(f'GPTQ with calib_algo {algo} is not on the device path')
+        if not getattr(wquantizer, 'round_zp', True):
+            # the reference computes round(w / s + z) with a float zero (quant.py:699-705);
+            # the column kernel's integer-zero form would differ silently
+            raise NotImplementedError('GPTQ with round_zp False is not on the device path')
+        return None
+    if qt != 'float-quant':
+        raise NotImplementedError(f'GPTQ with quant_type {qt}')
+    if not getattr(wquantizer, 'use_qtorch', False):
+        # use_qtorch False keeps per-element scales from get_float_qparams, which the
+        # reference's column loop cannot broadcast against one column (gptq.py:229-238)
+        raise NotImplementedError('GPTQ float-quant needs use_qtorch (the reference\'s '
+                                  'get_float_qparams scales are per element)')
+    if getattr(wquantizer, 'fp8_dtype', None) is None:
+        raise NotImplementedError(f'GPTQ float-quant {wquantizer.bit}: only e4m3 / e5m2')
+    if 'float_range' in getattr(wquantizer, 'kwargs', {}):
+        raise NotImplementedError('GPTQ float-quant with a custom float_range')
+    if algo != 'minmax' or static_groups or owq_nout:
+        raise NotImplementedError('GPTQ float-quant: minmax qparams, no static_groups / OWQ')
+    if wquantizer.granularity not in ('per_channel', 'per_group'):
+        raise NotImplementedError(f'GPTQ float-quant with {wquantizer.granularity}')
+    return wquantizer.fp8_dtype
+
+
 @torch.no_grad()
 def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder=True,
                    percdamp=0.01, fixed=None, losses=False, shard_rows=False, prepared=None,
                    static_groups=False, owq_nout=0):
-    """(calib_algo mse per_group: the column qparams are searched in the loop, see
-    column_loop's col_qparams.)"""
     """Full GPTQ transform of one linear. Returns dict(weight fp32 (original column order),
     scales / zeros [rows*ng, 1] fp32 (merge_qparams order, permuted groups), perm, invperm,
     loss). ``prepared`` = prepare_hessian(...) output shared by linears with the same input
-    (q/k/v, gate/up): their H -- hence perm, damping and U -- are identical."""
+    (q/k/v, gate/up): their H -- hence perm, damping and U -- are identical. calib_algo mse
+    per_group: the column qparams are searched in the loop (column_loop's col_qparams).
+    FloatQuantizer weights (use_qtorch, e4m3 / e5m2): the float-quant column loop."""
     bit, sym = wquantizer.bit, wquantizer.sym
+    fp8 = check_quantizer(wquantizer, static_groups, owq_nout)
     qmin, qmax = int(wquantizer.qmin.item()), int(wquantizer.qmax.item())
     group = wquantizer.group_size if wquantizer.granularity == 'per_group' else None
     if group is not None and not static_groups and group not in (32, 64, 128):
@@ -387,14 +423,16 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
         fx = None if fixed is None else tuple(
             None if f is None else f.reshape(Wp.shape[0], -1)[r0:r1] for f in fixed)
         s, z, L = column_loop(Wl, U, bit, sym, group, qmin, qmax, fixed=fx, losses=losses,
-                              col_group=col_group, ncols_q=ncq, col_qparams=col_qparams)
+                              col_group=col_group, ncols_q=ncq, col_qparams=col_qparams,
+                              fp8=fp8)
         Wp = P.gather_rows(Wl, Wp.shape[0])
         s = None if s is None else P.gather_rows(s, Wp.shape[0])
         z = None if z is None else P.gather_rows(z, Wp.shape[0])
         L = None if L is None else P.gather_rows(L, Wp.shape[0])
     else:
         s, z, L = column_loop(Wp, U, bit, sym, group, qmin, qmax, fixed=fixed, losses=losses,
-                              col_group=col_group, ncols_q=ncq, col_qparams=col_qparams)
+                              col_group=col_group, ncols_q=ncq, col_qparams=col_qparams,
+                              fp8=fp8)
     invperm = torch.argsort(perm) if perm is not None else None
     weight = Wp[:, invperm] if invperm is not None else Wp
     if owq_fixed is not None:

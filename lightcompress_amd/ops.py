@@ -224,13 +224,15 @@ def hessian_accum(x: torch.Tensor, H: torch.Tensor, alpha: float, beta: float) -
 
 def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: int,
                qmin: int, qmax: int, sym: bool, s_out, z_out, err: torch.Tensor,
-               losses=None, s_in=None, z_in=None):
+               losses=None, s_in=None, z_in=None, fp8=None):
     """One 128-column GPTQ block in place on fp32 W (see include/lcq.h lcq_gptq_block);
-    err is k-major [128, rows]."""
+    err is k-major [128, rows]. fp8 (torch.float8_e4m3fn / float8_e5m2): FloatQuantizer's
+    quant_dequant instead of the integer one (qmin / qmax / sym / zeros ignored)."""
     rows, ld = W.shape
     ng_total = s_out.shape[1] if s_out is not None else 0
+    fmt = 0 if fp8 is None else N.dt(fp8)
     N.call('lcq_gptq_block', N.ptr(W), rows, ld, int(col0), int(count), N.ptr(U), U.shape[1],
-           int(group), int(qmin), int(qmax), int(sym), N.ptr(s_in), N.ptr(z_in), N.ptr(s_out),
+           int(group), int(qmin), int(qmax), int(sym), fmt, N.ptr(s_in), N.ptr(z_in), N.ptr(s_out),
            N.ptr(z_out), int(ng_total), N.ptr(err), N.ptr(losses), N.stream_of(W))
 
 
@@ -483,18 +485,22 @@ def sq_diff_mean(a: torch.Tensor, b: torch.Tensor) -> float:
 
 def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, n_grid: int,
                      qmin: int, qmax: int, sym: bool, clip_sym: bool, mse=None,
-                     qx: torch.Tensor | None = None):
+                     qx: torch.Tensor | None = None, fp8=None, tensor_batch: int = 0):
     """AutoClipper.auto_clip_layer (v1) on device: returns (best_max, best_min) [oc, ng, 1].
     mse = (steps, grid, norm): the weight quantizer's calib_algo is mse. qx: the activation
     fake-quant of x (w_only False) that the shrink steps multiply with. group == ic takes the
-    per_channel kernel (lcq_auto_clip_search_pc)."""
+    per_channel kernel (lcq_auto_clip_search_pc). fp8 (a float8 dtype): FloatQuantizer weights,
+    per_channel (tensor_batch 0) or per_tensor over batches of tensor_batch rows (group == ic)."""
     oc, ic = w.shape
     if qx is not None and (qx.shape != x.shape or qx.dtype != x.dtype):
         raise ValueError('auto-clip: qx must match x in shape and dtype')
-    if group == ic and group not in (32, 64, 128, 256):
+    if fp8 is not None and (group != ic or mse is not None):
+        raise NotImplementedError('float-quant auto-clip: per_channel / per_tensor, minmax')
+    if group == ic and (group not in (32, 64, 128, 256) or fp8 is not None):
         if mse is not None:
             raise NotImplementedError('per_channel auto-clip with calib_algo mse')
-        return _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym)
+        return _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym,
+                                    fp8=fp8, tensor_batch=tensor_batch)
     T = x.shape[0]
     factors = torch.tensor([float(1 - i / n_grid) for i in range(nsteps)], dtype=torch.float32,
                            device=w.device)
@@ -515,7 +521,8 @@ def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, 
     return bmax, bmin
 
 
-def _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym):
+def _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym, fp8=None,
+                         tensor_batch=0):
     """per_channel weights: best bounds [oc, 1, 1] (auto_clip.py:96-99, group = ic)."""
     oc, ic = w.shape
     T = x.shape[0]
@@ -529,7 +536,8 @@ def _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym):
     ws = torch.empty(wsb, dtype=torch.uint8, device=w.device)
     N.call('lcq_auto_clip_search_pc', N.ptr(w.contiguous()), N.ptr(x.contiguous()),
            N.ptr(qx.contiguous() if qx is not None else None), N.dt(w), oc, ic, T, int(nsteps),
-           N.ptr(factors), int(qmin), int(qmax), int(sym), int(clip_sym), N.ptr(ws), wsb,
+           N.ptr(factors), int(qmin), int(qmax), int(sym), int(clip_sym),
+           0 if fp8 is None else N.dt(fp8), int(tensor_batch), N.ptr(ws), wsb,
            N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
     return bmax, bmin
 
@@ -613,9 +621,11 @@ def fp8_quant(x: torch.Tensor, group: int, fp8: torch.dtype, *, ct_dtype=None,
 
 def fp8_quant_static(x: torch.Tensor, scales: torch.Tensor, fp8: torch.dtype, *,
                      ct_dtype=None, add_zero: bool = True, codes: bool = True,
-                     fq: bool = False, fq_dtype=None) -> dict:
+                     fq: bool = False, fq_dtype=None, saturate: bool = False) -> dict:
     """FP8 quant of ``x`` with given scales; one scale per ``x.numel() / scales.numel()``
-    consecutive elements (per tensor / per row / per group layouts)."""
+    consecutive elements (per tensor / per row / per group layouts). saturate clamps the
+    quotient to +-finfo.max first (FloatQuantizer's float_quantize stand-in); without it the
+    cast is torch's ``.to()`` (out-of-range quotients -> NaN / inf)."""
     x = x.contiguous()
     s = scales.contiguous()
     if x.numel() % s.numel():
@@ -626,7 +636,8 @@ def fp8_quant_static(x: torch.Tensor, scales: torch.Tensor, fp8: torch.dtype, *,
     f = torch.empty(x.shape, dtype=fq_dtype or x.dtype, device=x.device) if fq else None
     rows = x.shape[0] if x.dim() > 1 else 1
     N.call('lcq_fp8_quant_static', N.ptr(x), N.dt(x.dtype), rows, x.numel() // rows, group,
-           N.dt(fp8), N.dt(ct), N.ptr(s), N.dt(s.dtype), int(add_zero), N.ptr(c), N.ptr(f),
+           N.dt(fp8), N.dt(ct), N.ptr(s), N.dt(s.dtype), int(add_zero), int(saturate),
+           N.ptr(c), N.ptr(f),
            N.dt(f.dtype) if f is not None else 0, N.stream_of(x))
     res = {}
     if codes:

@@ -39,11 +39,14 @@ def lpt_shard(costs: list[float], world: int) -> list[list[int]]:
     return [sorted(o) for o in out]
 
 
-def row_shard(rows: int, rank: int, world: int) -> tuple[int, int]:
-    """Contiguous [start, end) row range of this rank (balanced)."""
-    base, rem = divmod(rows, world)
+def row_shard(rows: int, rank: int, world: int, align: int = 1) -> tuple[int, int]:
+    """Contiguous [start, end) row range of this rank (balanced), in units of ``align`` rows
+    (a per-tensor FP8 clip scale spans one 256- or 64-row batch, auto_clip.py:108)."""
+    units = -(-rows // align)
+    base, rem = divmod(units, world)
     start = rank * base + min(rank, rem)
-    return start, start + base + (1 if rank < rem else 0)
+    end = start + base + (1 if rank < rem else 0)
+    return min(start * align, rows), min(end * align, rows)
 
 
 def allreduce_mean_(t: torch.Tensor) -> torch.Tensor:
@@ -73,12 +76,12 @@ def awq_pick_best(best_error: float, best_scales: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def gather_rows(local: torch.Tensor, rows: int) -> torch.Tensor:
+def gather_rows(local: torch.Tensor, rows: int, align: int = 1) -> torch.Tensor:
     """Reassemble a row-sharded matrix (row_shard layout) on every rank."""
     rank, world = dist_world()
     if world == 1:
         return local
-    sizes = [row_shard(rows, r, world) for r in range(world)]
+    sizes = [row_shard(rows, r, world, align) for r in range(world)]
     maxr = max(e - s for s, e in sizes)
     pad = torch.zeros((maxr,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local

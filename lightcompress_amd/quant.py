@@ -651,7 +651,8 @@ class FloatQuantizer(BaseQuantizer):
         ct = tensor.dtype if s.dim() == 0 else torch.promote_types(tensor.dtype, s.dtype)
         r = ops.fp8_quant_static(tensor.reshape(tensor.shape[0] if tensor.dim() else 1, -1),
                                  s.reshape(-1), fp8, ct_dtype=ct, add_zero=True,
-                                 codes=want == 'codes', fq=want == 'fq', fq_dtype=fq_dtype)
+                                 codes=want == 'codes', fq=want == 'fq', fq_dtype=fq_dtype,
+                                 saturate=True)
         return r[want].reshape(tensor.shape)
 
     def quant(self, tensor, scales, zeros, qmax, qmin):

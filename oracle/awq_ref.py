@@ -89,13 +89,29 @@ def _fq_mse(cur: torch.Tensor, bit, sym, group):
     return out.reshape(cur.shape).to(cur.dtype)
 
 
+def _fq_fp8(cur: torch.Tensor, fmt: str, per_tensor: bool):
+    """FloatQuantizer(use_qtorch).fake_quant_weight_dynamic of a clamped [rows, 1, 1, ic]
+    batch (quant.py:1142-1159): per_channel scales in the weight dtype, per_tensor scale of
+    the whole batch in fp32 (0-dim / 0-dim promotion); q fp32, (q - 0) * s, weight dtype."""
+    from . import fp8_ref as P
+    qmax = P.qmax_of(fmt)
+    if per_tensor:
+        mn, mx = torch.min(cur), torch.max(cur)
+    else:
+        mn, mx = cur.amin(dim=-1, keepdim=True), cur.amax(dim=-1, keepdim=True)
+    s = P.sym_scales(mn, mx, qmax)
+    return P.qdq_given(cur, s, fmt).to(cur.dtype)
+
+
 def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_grid=20,
-               max_shrink=0.5, n_sample_token=512, mse=False, act=None):
+               max_shrink=0.5, n_sample_token=512, mse=False, act=None, fp8=None):
     """auto_clip.py:83-191 (clip v1, single input). Returns (best_max, best_min) shaped
     [oc, ng, 1]. mse=True: the weight quantizer's calib_algo is mse. group = ic is the
     per_channel case (auto_clip.py:96-99). act = (bits, sym): w_only False, the shrink steps
     see fake_quantize_input(x) = per_token fake quant of the [1, T, ng, group] view
-    (auto_clip.py:176-177, 269-274; quant.py:754-771 with reshape_tensor's per_token no-op)."""
+    (auto_clip.py:176-177, 269-274; quant.py:754-771 with reshape_tensor's per_token no-op).
+    fp8 = (fmt, per_tensor, act_quant | None): FloatQuantizer weights (group = ic); act_quant is
+    a function giving fake_quantize_input(x) for w_only False."""
     w = w.reshape(w.shape[0], 1, -1, group)
     ocb = 256 if w.shape[0] % 256 == 0 else 64
     x = x.view(-1, x.shape[-1]).reshape(1, -1, x.shape[-1] // group, group)
@@ -110,12 +126,17 @@ def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_gr
         min_errs = torch.ones_like(org_max) * 1e9
         org_out = (x * wb).sum(dim=-1)
         qx = x if act is None else Q.fake_quant_dynamic(x, act[0], act[1], 'per_token')[0]
+        if fp8 is not None and fp8[2] is not None:
+            qx = fp8[2](x)
         for i_s in range(int(max_shrink * n_grid)):
             max_val = org_max * (1 - i_s / n_grid)
             min_val = -max_val if clip_sym else org_min * (1 - i_s / n_grid)
             cur = torch.clamp(wb, min_val, max_val)
-            q_w = (_fq_mse(cur, bit, sym, group) if mse else
-                   Q.fake_quant_dynamic(cur, bit, sym, 'per_group', group)[0])
+            if fp8 is not None:
+                q_w = _fq_fp8(cur, fp8[0], fp8[1])
+            else:
+                q_w = (_fq_mse(cur, bit, sym, group) if mse else
+                       Q.fake_quant_dynamic(cur, bit, sym, 'per_group', group)[0])
             cur_out = (qx * q_w).sum(dim=-1)
             err = (cur_out - org_out).pow(2).mean(dim=1).view(min_errs.shape)
             err_mean = 0 + err

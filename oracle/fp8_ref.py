@@ -53,6 +53,27 @@ def sym_scales(mn, mx, qmax):
     return torch.max(mx.abs(), mn.abs()).clamp(min=1e-5) / qmax
 
 
+def float_quantize(x: torch.Tensor, bit: str) -> torch.Tensor:
+    """The stand-in for qtorch's float_quantize(x, e, m, 'nearest') (absent from this image):
+    saturate at +-finfo.max (NaN kept), then the native OCP RNE cast, as fp32. Equal to the
+    plain cast wherever |x| < the format's overflow band, which every dynamic scale guarantees;
+    differs only for static scales. Pins: tests/golden clipfp8_ / gptqfp8_ /
+    pipe_*fp8 were made by the reference with this very function as its float_quantize."""
+    dt = FP8[bit]
+    m = torch.finfo(dt).max
+    x = x.float()
+    return torch.where(x.isnan(), x, x.clamp(-m, m)).to(dt).float()
+
+
+def qdq_given(x: torch.Tensor, s: torch.Tensor, bit: str) -> torch.Tensor:
+    """FloatQuantizer(use_qtorch).quant_dequant with given scales and zeros = 0.0
+    (quant.py:1061-1080): float_quantize(x / s + 0) then (q - 0) * s, torch dtype promotion."""
+    s = s.clone()
+    s[s == 0] = 1
+    zeros = torch.tensor(0.0)
+    return (float_quantize(x / s + zeros, bit) - zeros) * s
+
+
 def fp8_qdq(x: torch.Tensor, bit: str, granularity: str, group: int | None = None,
             block: int = 128):
     """FloatQuantizer(use_qtorch=True) fake + real quant, native cast for float_quantize.

@@ -74,9 +74,9 @@ def prepare_owq(W: torch.Tensor, H: torch.Tensor, nout: int, percdamp: float):
     return W, U, perm
 
 
-def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
+def column_loop(W: torch.Tensor, U: torch.Tensor, bit, sym: bool, group: int | None,
                 blocksize: int = 128, fixed=None, static=None, ncols_q: int | None = None,
-                mse: bool = False):
+                mse: bool = False, fp8: str | None = None):
     """gptq.py:198-244 on permuted fp32 W (modified in place to the compensated weights).
 
     group=None with fixed=(scale[rows,1], zero) -> per-channel fixed qparams.
@@ -84,8 +84,16 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     split_qparams :333-341) -- permuted column j uses original group perm[j] // group.
     mse=True: calib_algo mse, the group range from get_mse_range (search_column_qparams
     :359-366 -> get_tensor_qparams) of the group's columns of the global W.
+    fp8='e4m3' / 'e5m2': FloatQuantizer(use_qtorch) weights (gptq_fp8.yml): group qparams
+    max(|min|, |max|).clamp(1e-5) / finfo.max (quant.py:545-553 on the fp32 columns) and
+    quant_dequant = float_quantize(w / s + 0) * s (quant.py:1061-1080, fp8_ref stand-in).
     Returns (tmp, Losses, scales [rows, ng], zeros [rows, ng] | None)."""
-    qmin, qmax = Q.int_range(bit, sym)
+    if fp8 is not None:
+        from . import fp8_ref
+        qmax = fp8_ref.qmax_of(fp8)
+        qmin = -qmax
+    else:
+        qmin, qmax = Q.int_range(bit, sym)
     rows, cols = W.shape
     ncq = cols if ncols_q is None else ncols_q  # OWQ: the outlier tail is not quantized
     Losses = torch.zeros_like(W)
@@ -106,11 +114,19 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
                 ct = W[:, i1 + i:min(i1 + i + group, ncq)]
                 t = Q.group_view(ct, 'per_group', group)
                 mn, mx = Q.mse_range(t, bit, sym) if mse else Q.minmax(t)
-                s, z = Q.qparams(mn, mx, qmin, qmax, sym)
-                qp = (s, z)
+                if fp8 is not None:
+                    from . import fp8_ref
+                    qp = (fp8_ref.sym_scales(mn, mx, qmax), torch.tensor(0.0))
+                else:
+                    s, z = Q.qparams(mn, mx, qmin, qmax, sym)
+                    qp = (s, z)
                 groups[(i1 + i) // group] = qp
             s, z = qp
-            q = Q.dequant(Q.quant(w.unsqueeze(1), s, z, qmin, qmax), s, z).squeeze(1)
+            if fp8 is not None:
+                from . import fp8_ref
+                q = fp8_ref.qdq_given(w.unsqueeze(1), s, fp8).squeeze(1)
+            else:
+                q = Q.dequant(Q.quant(w.unsqueeze(1), s, z, qmin, qmax), s, z).squeeze(1)
             tmp1[:, i] = w
             L1[:, i] = ((w - q) ** 2) / (2 * d ** 2)
             err1 = (w - q) / d
@@ -125,7 +141,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     ng = len(groups)
     scales = torch.stack([groups[g][0] for g in range(ng)], dim=1).reshape(rows, ng)
     zeros = None
-    if not sym:
+    if not sym and fp8 is None:
         zeros = torch.stack([groups[g][1] for g in range(ng)], dim=1).reshape(rows, ng)
     return tmp, Losses, scales, zeros
 

@@ -128,3 +128,23 @@ def module_utils():
     install()
     import llmc.compression.quantization.module_utils as mu
     return mu
+
+
+def native_float_quantize():
+    """qtorch is absent: give the reference's quant module a ``float_quantize``
+    that is the native OCP Float8 RNE cast, saturating at +-finfo.max (NaN kept) -- the
+    rounding lightcompress_amd's FloatQuantizer documents for use_qtorch=True.
+    Everything around that one step stays the reference's own, so fixtures made this way pin
+    the scales, the algorithms' control flow and every other op; the rounding step itself is
+    parity-unpinned against qtorch."""
+    import torch
+    q = quant_module()
+    fmts = {(4, 3): torch.float8_e4m3fn, (5, 2): torch.float8_e5m2}
+
+    def float_quantize(x, exp, man, rounding='stochastic'):
+        assert rounding == 'nearest', rounding
+        dt = fmts[(int(exp), int(man))]
+        m = torch.finfo(dt).max
+        x = x.float()
+        return torch.where(x.isnan(), x, x.clamp(-m, m)).to(dt).float()
+    q.float_quantize = float_quantize

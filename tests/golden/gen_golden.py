@@ -766,6 +766,93 @@ def gen_hqq():
 GENERATORS['hqq'] = gen_hqq
 
 
+def gen_fp8_algos():
+    """Float-quant (FP8) weights inside auto-clip and the GPTQ column loop (the
+    backend/{vllm,sglang}/fp8 awq_fp8*.yml / gptq_fp8.yml recipes): the reference's own
+    AutoClipper.auto_clip_layer and GPTQ layer methods with FloatQuantizer(use_qtorch=True),
+    qtorch's float_quantize replaced by the saturating native cast (R.native_float_quantize,
+    DESIGN.md §5). Prefixes clipfp8_ / gptqfp8_."""
+    import torch.nn as nn
+    R.init_dist()
+    q = R.quant_module()
+    R.native_float_quantize()
+    import llmc.compression.quantization.auto_clip as ac
+    import llmc.compression.quantization.gptq as gm
+    bf, hf = torch.bfloat16, torch.float16
+    # (name, fmt, granularity, act granularity or None, oc, ic, dtype)
+    cases = [('pc_e4m3', 'e4m3', 'per_channel', None, 256, 512, bf),
+             ('pc_e4m3_a8', 'e4m3', 'per_channel', 'per_token', 256, 512, bf),
+             ('pt_e4m3_b64', 'e4m3', 'per_tensor', 'per_tensor', 384, 512, bf),   # 64-row batches
+             ('pt_e4m3_b256', 'e4m3', 'per_tensor', None, 512, 256, bf),
+             ('pc_e4m3_f16', 'e4m3', 'per_channel', None, 128, 512, hf),
+             ('pc_e5m2', 'e5m2', 'per_channel', None, 128, 384, bf)]
+    for i, (name, fmt, gran, agran, oc, ic, dt) in enumerate(cases):
+        wq = q.FloatQuantizer(fmt, True, gran, use_qtorch=True)
+        aq = q.FloatQuantizer(fmt, True, agran, use_qtorch=True) if agran else None
+        clipper = ac.AutoClipper(w_only=aq is None, wquantizer=wq, aquantizer=aq,
+                                 clip_version='v1', clip_sym=True, save_clip=False,
+                                 padding_mask=None)
+        w = weights(oc, ic, dt, 1700 + i, edge=False)
+        w[3, 5] = 0.4  # a row outlier: the clip has something to cut
+        x = _acts(1, 512, ic, 1800 + i, dtype=dt)[0]
+        bmax, bmin = clipper.auto_clip_layer(0, 'l', w.clone(), [x.clone()],
+                                             n_sample_token=64)
+        F.save(f'clipfp8_{name}', w=w, x=x, best_max=bmax, best_min=bmin,
+               meta=torch.tensor([4 if fmt == 'e4m3' else 5, int(gran == 'per_tensor'),
+                                  {None: 0, 'per_token': 1, 'per_tensor': 2}[agran], 64]))
+    gcases = [  # name, fmt, granularity, group, actorder, oc, ic
+        ('pc_e4m3_act', 'e4m3', 'per_channel', None, True, 192, 512),
+        ('pc_e4m3_noact', 'e4m3', 'per_channel', None, False, 128, 384),
+        ('pg_e4m3_g128_act', 'e4m3', 'per_group', 128, True, 128, 512),
+        ('pc_e5m2_act', 'e5m2', 'per_channel', None, True, 128, 256)]
+    for i, (name, fmt, gran, gs, act, oc, ic) in enumerate(gcases):
+        torch.manual_seed(2000 + i)
+        layer = nn.Linear(ic, oc, bias=False)
+        layer.weight.data = weights(oc, ic, torch.bfloat16, 2100 + i, edge=False)
+        xs = _acts(3, 48, ic, 2200 + i)
+        obj = gm.GPTQ.__new__(gm.GPTQ)
+        kw = {'group_size': gs} if gs else {}
+        obj.wquantizer = q.FloatQuantizer(fmt, True, gran, use_qtorch=True, **kw)
+        obj.dev = torch.device('cpu')
+        obj.model_dtype = torch.bfloat16
+        obj.owq, obj.actorder, obj.static_groups = False, act, False
+        obj.percdamp, obj.blocksize, obj.chunk_num = 0.01, 128, 1
+        obj.true_sequential = True
+        obj.need_perm = act and gran == 'per_group'
+        obj.layers_cache = {'l': {}}
+        obj.qparams = {}
+        gm.GPTQ.layer_init(obj, layer, 'l')
+        for x in xs:
+            gm.GPTQ.add_batch(obj, layer, 'l', x, None)
+        H = obj.layers_cache['l']['H'].clone()
+        _, s0, z0, qmax, qmin = obj.wquantizer.get_tensor_qparams(layer.weight.data)
+        layer.register_buffer('buf_scales', s0)
+        layer.register_buffer('buf_zeros', z0)
+        layer.register_buffer('buf_qmax', torch.tensor(qmax))
+        layer.register_buffer('buf_qmin', torch.tensor(qmin))
+        w_in = layer.weight.data.clone()
+        obj.layers_cache['l']['H'] = H.clone()
+        obj.initialize_qparams_and_prepare_weights(layer, 'l')
+        Wp, U = obj.process_hessian_and_weights(layer, 'l')
+        obj.layers_cache['l']['H'] = H.clone()
+        obj.qparams = {}
+        layer.weight.data = w_in.clone()
+        obj.layer_transform(layer, 'l')
+        out = dict(x=torch.cat(xs, 0), w=w_in, H=H, U=U,
+                   perm=getattr(layer, 'buf_perm', None), weight=layer.weight.data.clone(),
+                   scales=layer.buf_scales,
+                   meta=torch.tensor([4 if fmt == 'e4m3' else 5, gs or 0, int(act), oc, ic]))
+        out['fq'] = obj.w_qdq(layer, obj.wquantizer)
+        if not obj.need_perm:
+            codes, s_rq, _ = obj.w_q(layer, obj.wquantizer)
+            out.update(codes=codes, scales_rq=s_rq)
+        F.save(f'gptqfp8_{name}', **out)
+    print('fp8 clip / gptq fixtures written')
+
+
+GENERATORS['fp8_algos'] = gen_fp8_algos
+
+
 if __name__ == '__main__':
     which = sys.argv[1] if len(sys.argv) > 1 else 'all'
     R.install()

@@ -148,6 +148,8 @@ def dump_structure(family):
 
 def run_reference(name, spec):
     family = spec.get('model', 'Llama')
+    if spec.get('qtorch_native'):
+        R.native_float_quantize()
     model_cls = _adapter(family)
     if spec['quant']['method'] == 'GPTQ':
         import llmc.compression.quantization.gptq as mod

@@ -122,4 +122,47 @@ CONFIGS = {
                                              'granularity': 'per_tensor', 'static': True,
                                              'calib_algo': 'static_minmax'}},
                            'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}, 'diag': False},
+    # ---- float-quant (FP8 e4m3) weights through AWQ / GPTQ (configs/quantization/backend/
+    # vllm/fp8/*.yml). These need qtorch in the reference (quant.py:975-978, absent), so the
+    # generator gives the reference's quant module a float_quantize that is the native
+    # Float8_e4m3fn RNE cast (the rounding our FloatQuantizer documents); every other op of the
+    # search, the clip, the column loop and the deploy is the reference's own ('qtorch_native').
+    # awq_fp8_static.yml as shipped omits the act calib_algo, which get_batch_tensors_qparams
+    # rejects (quant.py:564-574); static_minmax is the minmax-like choice it needs. Its
+    # quant_out forward feeds o_proj / down inputs beyond the act range calibrated on the float
+    # inputs (and GPTQ's error-compensated columns exceed their static scales): c10's plain cast
+    # maps |x / s| >= 464 to NaN there, hence the saturating stand-in.
+    'awq_fp8_static': {'quant': {'method': 'Awq',
+                                 'weight': {'quant_type': 'float-quant', 'bit': 'e4m3',
+                                            'symmetric': True, 'granularity': 'per_tensor',
+                                            'use_qtorch': True},
+                                 'act': {'quant_type': 'float-quant', 'bit': 'e4m3',
+                                         'symmetric': True, 'granularity': 'per_tensor',
+                                         'use_qtorch': True, 'static': True,
+                                         'calib_algo': 'static_minmax'},
+                                 'special': {'trans': True, 'trans_version': 'v2',
+                                             'weight_clip': True},
+                                 'quant_out': True},
+                       'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128},
+                       'qtorch_native': True},
+    'awq_fp8': {'quant': {'method': 'Awq',
+                          'weight': {'quant_type': 'float-quant', 'bit': 'e4m3',
+                                     'symmetric': True, 'granularity': 'per_channel',
+                                     'use_qtorch': True},
+                          'act': {'quant_type': 'float-quant', 'bit': 'e4m3', 'symmetric': True,
+                                  'granularity': 'per_token', 'use_qtorch': True},
+                          'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True},
+                          'quant_out': True},
+                'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}, 'qtorch_native': True},
+    'gptq_fp8': {'quant': {'method': 'GPTQ',
+                           'weight': {'quant_type': 'float-quant', 'bit': 'e4m3',
+                                      'symmetric': True, 'granularity': 'per_channel',
+                                      'use_qtorch': True},
+                           'act': {'quant_type': 'float-quant', 'bit': 'e4m3', 'symmetric': True,
+                                   'granularity': 'per_token', 'use_qtorch': True},
+                           'special': {'actorder': True, 'static_groups': False,
+                                       'percdamp': 0.01, 'blocksize': 128,
+                                       'true_sequential': True},
+                           'quant_out': True},
+                 'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}, 'qtorch_native': True},
 }
