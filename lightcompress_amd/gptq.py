@@ -178,7 +178,8 @@ class GPTQ(BaseBlockwiseQuantization):
                 H *= float(acc.nsamples)
                 dist.all_reduce(H, op=dist.ReduceOp.SUM)
                 dist.all_reduce(n, op=dist.ReduceOp.SUM)
-                H /= float(n.item())
+                if n.item() > 0:  # no sample on any rank (an expert no token reached): H
+                    H /= float(n.item())  # stays 0 as on one GPU -> dead-column path
             elif replicate:
                 # one all-reduce of the finished Hessian per distinct input (the reference
                 # reduces after every sample); averaging matches its H /= world_size
