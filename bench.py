@@ -664,11 +664,52 @@ def bench_fp8_forward(args, weights, dev, world):
     return out
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1 rendezvous) and wait. This
+    process never touches the GPU (children are fresh interpreters, no exec of a GPU process);
+    rank 0 prints the JSON line. Returns the first non-zero child exit code (others killed)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__),
+                                       *sys.argv[1:]], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for q in procs:
+            q.kill()
+    return rc
+
+
 def main():
     args = parse()
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args.gpus))
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    if world != args.gpus:
+        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun '
+                         f'--nproc-per-node {args.gpus}, or without a launcher (bench.py starts '
+                         'the ranks itself)')
     # one process per GPU (RCCL). LCQ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
     # (ranks then share devices round-robin); the driver's runs use the default.
     backend = os.environ.get('LCQ_DIST_BACKEND', 'nccl')

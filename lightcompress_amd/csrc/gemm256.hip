@@ -568,192 +568,8 @@ static int check_common(int dtype, const void* x, int64_t lda, int64_t m, int64_
   return 0;
 }
 
-// ---------------------------------------------------------------------------------------
-// GPTQ Hessian SYRK on the k_gemm16b core (hessian256.hip's lcq_hessian_accum, LCQ_SYRK=16):
-// H = beta*H + alpha * X^T X over the upper-triangle 256^2 tiles of the transposed, zero
-// padded X^T panels (A = B = XT rows, k-contiguous), split-K over `ns` slabs when the
-// triangle has few tiles. Tile order: slot -> (ti, tj) in chunks of 4 x 8 tiles walked band
-// by band (12 panels per 32 tiles of one XCD), as k_syrk256.
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ bool syrk_slot_tile(int slot, int nt, int& ti, int& tj) {
-  int b = 0, rem = slot >> 5;
-  while (true) {
-    const int nch = (nt - 4 * b + 7) / 8;
-    if (rem < nch) break;
-    rem -= nch;
-    ++b;
-  }
-  const int s = slot & 31;
-  ti = 4 * b + (s >> 3);
-  tj = 4 * b + rem * 8 + (s & 7);
-  return ti < nt && tj < nt && tj >= ti;
-}
-
-// v-th upper-triangle tile in the same 4 x 8 chunk order, counting valid tiles only: the grid
-// is exactly ntiles x ns workgroups, so every XCD's contiguous wgid range holds the same number
-// of live tiles (+-1) and the last round is as full as the tile count allows (no exiting slots
-// that leave one XCD a round longer than the others)
-__device__ __forceinline__ void syrk_valid_tile(int v, int nt, int& ti, int& tj) {
-  for (int b = 0; 4 * b < nt; ++b) {
-    const int nch = (nt - 4 * b + 7) / 8;
-    for (int rem = 0; rem < nch; ++rem) {
-      const int c0 = 4 * b + rem * 8, c1 = min(nt - 1, c0 + 7);
-      for (int r = 0; r < 4; ++r) {
-        const int i = 4 * b + r;
-        if (i >= nt) break;
-        const int lo = max(i, c0), cnt = c1 >= lo ? c1 - lo + 1 : 0;
-        if (v < cnt) {
-          ti = i;
-          tj = lo + v;
-          return;
-        }
-        v -= cnt;
-      }
-    }
-  }
-  ti = tj = 0;  // not reached for v < nt (nt + 1) / 2
-}
-
-struct SyrkArgs16 {
-  const uint16_t* xt;
-  int64_t kp, ic, icp;
-  float* H;
-  float* part;
-  float alpha, beta;
-  int nt, ns, ntiles;
-  int64_t ktps;
-};
-
-template <bool FP16>
-__global__ void __launch_bounds__(256, 1) k_syrk16(SyrkArgs16 s) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int split = wgid / s.ntiles;
-  int ti, tj;
-  syrk_valid_tile(wgid - split * s.ntiles, s.nt, ti, tj);
-  const int64_t kt0 = (int64_t)split * s.ktps;
-  int64_t nk = s.kp / SKT - kt0;
-  if (nk > s.ktps) nk = s.ktps;
-  Args a{};  // the GEMM view of this split: A = B = XT (k from column kt0 * 64 on)
-  a.a = s.xt + kt0 * SKT;
-  a.lda = s.kp;
-  a.m = s.icp;
-  a.k = nk * SKT;
-  a.b[0] = a.a;
-  a.bend[0] = s.icp;
-  a.ldb = s.kp;
-  a.n = s.icp;
-  a.nseg = 1;
-  Stage4 st;
-  make_stage16<EPI_STORE>(a, ti, tj, w, lane, st);
-
-  v4f acc[8][8];
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-    for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
-  v8s af[2][2][2], bf[2][8][2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) load_piece(st, lds, 0, 0, w, i);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) load_piece(st, lds, 1, nk > 1 ? SKT * 2 : 0, w, i);
-  wait_barrier<22>();
-#pragma unroll
-  for (int n = 0; n < 8; ++n)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) bf[0][n][k] = read_frag(lds + TILE_B, wc * 8 + n, k, lane);
-#pragma unroll
-  for (int m2 = 0; m2 < 2; ++m2)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) af[0][m2][k] = read_frag(lds, wr * 8 + m2, k, lane);
-  asm volatile("s_nop 4" ::: "memory");
-
-  int64_t t = 0;
-  for (; t + 1 < nk; t += 2) {
-    ktile16b<FP16, 0>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
-    ktile16b<FP16, 1>(acc, bf, af, st, lds, t + 1, nk, w, wr, wc, lane);
-  }
-  if (t < nk) ktile16b<FP16, 0>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-
-  // acc[m][n][jj] (swapped layout): H row i = ti*256 + wr*128 + m*16 + fr, columns
-  // tj*256 + wc*128 + n*16 + fq*4 + jj
-  const int fr = lane & 15, fq = lane >> 4;
-  const int64_t i0 = (int64_t)ti * ST + wr * 128 + fr;
-  const int64_t j0 = (int64_t)tj * ST + wc * 128 + fq * 4;
-  if (s.ns > 1) {
-    float* P = s.part + (int64_t)split * s.icp * s.icp;
-#pragma unroll
-    for (int m = 0; m < 8; ++m)
-#pragma unroll
-      for (int n = 0; n < 8; ++n)
-        *reinterpret_cast<float4*>(P + (i0 + m * 16) * s.icp + j0 + n * 16) =
-            make_float4(acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]);
-    return;
-  }
-  const bool diag = ti == tj;
-  const bool vec = (s.ic & 3) == 0;
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const int64_t i = i0 + m * 16;
-    if (i >= s.ic) break;
-#pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      const int64_t j = j0 + n * 16;
-      if (j >= s.ic) break;
-      float o[4];
-      const bool full = vec && j + 3 < s.ic;
-      float h[4] = {0.f, 0.f, 0.f, 0.f};
-      if (s.beta != 0.f) {
-        if (full) {
-          const float4 hv = *reinterpret_cast<const float4*>(s.H + i * s.ic + j);
-          h[0] = hv.x; h[1] = hv.y; h[2] = hv.z; h[3] = hv.w;
-        } else {
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-            if (j + jj < s.ic) h[jj] = s.H[i * s.ic + j + jj];
-        }
-      }
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        float v = __fmul_rn(s.alpha, acc[m][n][jj]);
-        if (s.beta != 0.f) v = __fadd_rn(__fmul_rn(s.beta, h[jj]), v);
-        o[jj] = v;
-      }
-      if (full) {
-        *reinterpret_cast<float4*>(s.H + i * s.ic + j) = make_float4(o[0], o[1], o[2], o[3]);
-      } else {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          if (j + jj < s.ic) s.H[i * s.ic + j + jj] = o[jj];
-      }
-      if (!diag) {  // mirror H[j + jj][i]
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          if (j + jj < s.ic) s.H[(j + jj) * s.ic + i] = o[jj];
-      }
-    }
-  }
-}
-
 }  // namespace g256
 
-// host launcher used by lcq_hessian_accum (hessian256.hip) for LCQ_SYRK=16
-int syrk16_launch(const uint16_t* xt, int64_t kp, int64_t ic, int64_t icp, float* H,
-                  float* part, float alpha, float beta, int nt, int ns, int ntiles,
-                  int64_t ktps, bool fp16, hipStream_t st) {
-  g256::SyrkArgs16 s{xt, kp, ic, icp, H, part, alpha, beta, nt, ns, ntiles, ktps};
-  auto k = fp16 ? g256::k_syrk16<true> : g256::k_syrk16<false>;
-  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            2 * g256::BUF4);
-  hipLaunchKernelGGL(k, dim3((unsigned)(ntiles * ns)), 256, 2 * g256::BUF4, st, s);
-  return check_launch("lcq_hessian_accum: syrk16");
-}
 }  // namespace lcq
 
 using namespace lcq;

