@@ -162,12 +162,21 @@ int lcq_pack_autoawq_gemm(const void* w, int w_dtype, int64_t oc, int64_t ic, in
  * x [n, ic] BF16/F16 token-major activations; H [ic, ic] fp32 (kept symmetric).
  * The reference's per-sample running average maps to beta = n/(n+b),
  * alpha = fp32(sqrt(2/(n+b)))^2. 256x256-tile MFMA SYRK (bf16/fp16 products, fp32
- * accumulation) over the upper triangle, mirrored. workspace >= lcq_hessian_workspace_bytes
- * (a zero-padded X^T copy + split-K slabs when ic is small); caller-owned, device memory.
+ * accumulation) over the upper triangle, mirrored, read from x as it is (transposed LDS
+ * reads; ic % 8 == 0). workspace >= lcq_hessian_workspace_bytes (a zero-padded copy of the
+ * last partial 64-token tile + split-K slabs when ic is small); caller-owned, device memory.
  * ------------------------------------------------------------------------------------- */
 int64_t lcq_hessian_workspace_bytes(int64_t n, int64_t ic);
 int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t ic, void* H, float alpha,
                       float beta, void* workspace, int64_t ws_bytes, void* stream);
+
+/* Deterministic reduction of Hessian partials (the grouped GPTQ Hessian: the calibration
+ * samples of add_batch, gptq.py:253-295, cut into 8 fixed groups, so that token-sharded ranks
+ * and one GPU sum them in the same order): out[i] = alpha * tree(parts[0..np)[i]) with the
+ * fixed pairwise tree ((p0 + p1) + (p2 + p3)) + ...; parts is a HOST array of np in {1, 2, 4, 8}
+ * device pointers to fp32 [n] (n % 4 == 0, 16-byte aligned); out may alias none of them. */
+int lcq_tree_sum(const void* const* parts, int np, int64_t n, float alpha, void* out,
+                 void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * GPTQ in-block column loop for one 128-column block (GPTQ.weight_transform, gptq.py:198-244,

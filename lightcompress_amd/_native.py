@@ -56,6 +56,7 @@ SIGNATURES = {
                                _vp, _vp], _int),
     'lcq_hessian_workspace_bytes': ([_i64, _i64], _i64),
     'lcq_hessian_accum': ([_vp, _int, _i64, _i64, _vp, _f32, _f32, _vp, _i64, _vp], _int),
+    'lcq_tree_sum': ([_vp, _int, _i64, _f32, _vp, _vp], _int),
     'lcq_gptq_block': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _int, _int, _int, _int,
                         _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
     'lcq_gptq_block_cols': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _int, _int, _vp, _vp, _vp,

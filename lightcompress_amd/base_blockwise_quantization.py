@@ -99,7 +99,7 @@ class BlockwiseOpt:
         rank, world = P.dist_world()
         data, kws = self.input['data'], self.input['kwargs']
         total = sum(d.shape[0] for d in data)
-        s, e = P.row_shard(total, rank, world)
+        s, e = self.sample_shard(total, rank, world)
         new_d, new_k, off = [], [], 0
         for d, kw in zip(data, kws):
             b = d.shape[0]
@@ -112,6 +112,10 @@ class BlockwiseOpt:
         self.input['data'], self.input['kwargs'] = new_d, new_k
         self.n_samples_global = total
         self.n_samples = e - s
+
+    def sample_shard(self, total: int, rank: int, world: int) -> tuple[int, int]:
+        """[start, end) of this rank's calibration samples under shard_tokens."""
+        return P.row_shard(total, rank, world)
 
     def run_block_loop(self):
         mode = self.parallel_mode()

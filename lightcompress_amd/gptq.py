@@ -59,6 +59,30 @@ class GPTQ(BaseBlockwiseQuantization):
             self.collect_block_qparams(block)
 
     # ---- Hessian collection (gptq.py:246-322) -------------------------------------------------
+    def sample_shard(self, total, rank, world):
+        """Token shards on the grouped Hessian's group boundaries (world | 8): rank r takes
+        groups [8r/N, 8(r+1)/N), samples [ceil(r n / N), ceil((r + 1) n / N))."""
+        if gptq_core.HESSIAN_GROUPS % world == 0:
+            return (-(-rank * total // world), -(-(rank + 1) * total // world))
+        return super().sample_shard(total, rank, world)
+
+    def _hessian_plan(self):
+        """The grouped-Hessian plan of this process (gptq_core.GroupPlan), or None where the
+        running average is kept: the reference's data-parallel replicas, or a world that does
+        not divide the group count."""
+        if self.data_free:
+            return None
+        mode = self.parallel_mode()
+        if mode in ('single', 'shard_blocks'):
+            return gptq_core.GroupPlan(self.n_samples)
+        if mode == 'shard_tokens':
+            from .parallel import dist_world
+            rank, wsz = dist_world()
+            if gptq_core.HESSIAN_GROUPS % wsz == 0:
+                return gptq_core.GroupPlan(getattr(self, 'n_samples_global', self.n_samples),
+                                           rank, wsz)
+        return None
+
     # The reference keeps one Hessian per linear, each fed by that linear's own hook. Linears of
     # one subset read the same tensor (q/k/v, gate/up), so their Hessians are identical: here the
     # subset's input layer (subset['input'][0]) owns one accumulator that its members share.
@@ -68,7 +92,8 @@ class GPTQ(BaseBlockwiseQuantization):
         acc = None
         for name, m in layers.items():
             if acc is None:
-                acc = gptq_core.HessianAccumulator(m.weight.shape[1], m.weight.device)
+                acc = gptq_core.HessianAccumulator(m.weight.shape[1], m.weight.device,
+                                                   plan=self._hessian_plan())
             self.layers_cache[name] = {'acc': acc, 'owner': name == owner,
                                        'columns': m.weight.shape[1]}
 
@@ -170,8 +195,23 @@ class GPTQ(BaseBlockwiseQuantization):
         if cache is None:
             cache = acc.prepared_by = {}
         if nout not in cache:
-            H = acc.H.clone()
+            grouped = acc.ready_grouped()
             if replicate and self.parallel_mode() == 'shard_tokens':
+                # every rank must take the same road: grouped only if all ranks are
+                flag = torch.tensor([int(grouped)], dtype=torch.int32, device=acc.H.device)
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+                if grouped and not int(flag.item()):
+                    acc.fallback()
+                    grouped = False
+            if grouped:
+                # the fixed group tree, finished across the token shards (bit-identical to
+                # one GPU); nothing else to reduce
+                H = acc.finalize().clone()
+            else:
+                H = acc.H.clone()
+            if grouped:
+                pass
+            elif replicate and self.parallel_mode() == 'shard_tokens':
                 # token shards: H = sum_r n_r H_r / N (each H_r the running average over the
                 # rank's n_r samples) -- the single-GPU Hessian up to fp32 summation order
                 n = torch.tensor([float(acc.nsamples)], dtype=torch.float64, device=H.device)

@@ -15,19 +15,67 @@ from . import ops
 BLOCK = 128
 
 
+HESSIAN_GROUPS = 8  # fixed calibration-sample groups of the grouped Hessian (see below)
+
+
+def _alpha(n: int) -> float:
+    """fp32(sqrt(2 / n))^2: the reference's per-sample scale x <- sqrt(2/n) x, squared."""
+    c = torch.tensor(math.sqrt(2 / n), dtype=torch.float32).item()
+    return float(torch.tensor(c * c, dtype=torch.float32).item())
+
+
+def group_bounds(n: int, groups: int = HESSIAN_GROUPS) -> list[tuple[int, int]]:
+    """Sample range of every Hessian group: group g = samples s with floor(s * G / n) == g,
+    i.e. [ceil(g n / G), ceil((g + 1) n / G)). Ranks of a world that divides G take
+    contiguous blocks of G / world groups, which is also a balanced sample split."""
+    return [(-(-g * n // groups), -(-(g + 1) * n // groups)) for g in range(groups)]
+
+
+class GroupPlan:
+    """Where this process's calibration samples sit in the grouped Hessian: the global sample
+    count, and the local groups as (group, first local sample, end local sample)."""
+
+    def __init__(self, n_global: int, rank: int = 0, world: int = 1,
+                 groups: int = HESSIAN_GROUPS):
+        if groups % world:
+            raise ValueError('world size must divide the Hessian group count')
+        self.n_global, self.rank, self.world, self.groups = n_global, rank, world, groups
+        per = groups // world
+        b = group_bounds(n_global, groups)
+        self.first = b[rank * per][0]
+        self.local = [(g, b[g][0] - self.first, b[g][1] - self.first)
+                      for g in range(rank * per, (rank + 1) * per)]
+        self.n_local = b[(rank + 1) * per - 1][1] - self.first
+
+
 class HessianAccumulator:
     """Running-average Hessian of one linear input (GPTQ.add_batch, gptq.py:253-295).
 
     ``H_n = H_{n-1} * n_{prev}/n + (2/n) x^T x`` per calibration batch, with the product on
-    MFMA (``lcq_hessian_accum``). Multiple-GPU sample sharding is reconciled by the caller
-    (``gptq.GPTQ``) with one all-reduce per layer instead of one per sample.
+    MFMA (``lcq_hessian_accum``).
+
+    Grouped form (``plan`` set and the whole calibration set of this process arrives in ONE
+    batch, as the stacked calibration forward delivers it): the samples are cut into
+    HESSIAN_GROUPS fixed groups, each group's x^T x is one MFMA pass into its own fp32
+    partial, and H = alpha(n) * ((P0 + P1) + (P2 + P3)) + ((P4 + P5) + (P6 + P7)) -- one
+    fixed binary tree (``lcq_tree_sum``). A rank of a token-sharded world keeps only its
+    contiguous subtree; ``finalize`` exchanges the subtrees and finishes the same tree, so
+    every rank ends with the single-GPU H bit for bit. Any other arrival
+    pattern (several batches) falls back to the running average, and sharded ranks then
+    combine by a weighted all-reduce (T2: the fp32 summation order differs).
     """
 
-    def __init__(self, ic: int, device):
+    def __init__(self, ic: int, device, plan: GroupPlan | None = None):
         self.H = torch.zeros((ic, ic), dtype=torch.float32, device=device)
         self.nsamples = 0
         self.ic = ic
         self.prepared = None  # (U, perm, dead) once the layer transform has factored H
+        self.plan = plan
+        self.subtree = None   # grouped: this process's unscaled tree over its local groups
+
+    @property
+    def grouped(self) -> bool:
+        return self.subtree is not None
 
     @torch.no_grad()
     def add_batch(self, inp: torch.Tensor, samples: int | None = None):
@@ -39,11 +87,89 @@ class HessianAccumulator:
         x = inp.reshape(-1, inp.shape[-1])
         if x.dtype not in (torch.bfloat16, torch.float16):
             x = x.to(torch.bfloat16)  # fp32 activations: bf16 MFMA path (documented tolerance)
+        if (self.plan is not None and self.nsamples == 0 and not self.grouped
+                and b == self.plan.n_local and inp.dim() == 3 and inp.shape[0] == b
+                and b > 0):
+            self._add_grouped(x, inp.shape[1])
+            self.nsamples = b
+            return
+        if self.grouped:  # a second batch: continue as the running average of the local set
+            self._materialize_local()
         beta = self.nsamples / (self.nsamples + b)
         self.nsamples += b
-        c = torch.tensor(math.sqrt(2 / self.nsamples), dtype=torch.float32).item()
-        alpha = float(torch.tensor(c * c, dtype=torch.float32).item())
-        ops.hessian_accum(x, self.H, alpha, beta)
+        ops.hessian_accum(x, self.H, _alpha(self.nsamples), beta)
+
+    def _add_grouped(self, x: torch.Tensor, tpe: int):
+        parts = []
+        for _, s0, s1 in self.plan.local:
+            P = torch.zeros((self.ic, self.ic), dtype=torch.float32, device=x.device)
+            if s1 > s0:
+                ops.hessian_accum(x[s0 * tpe:s1 * tpe], P, 1.0, 0.0)
+            parts.append(P)
+        if self.plan.world == 1:  # the whole tree here: H = alpha * tree
+            ops.tree_sum(parts, _alpha(self.plan.n_global), out=self.H)
+            self.subtree = self.H
+            self.finalized = True
+        else:
+            self.subtree = ops.tree_sum(parts, 1.0)
+            self.finalized = False
+        del parts
+
+    def ready_grouped(self) -> bool:
+        """Grouped and waiting for (or done with) the cross-rank tree. A rank whose share of
+        the samples is empty never sees a batch: its subtree is zero."""
+        if (not self.grouped and self.plan is not None and self.plan.n_local == 0
+                and self.nsamples == 0):
+            self.subtree = torch.zeros_like(self.H)
+            self.finalized = self.plan.world == 1
+        return self.grouped
+
+    def fallback(self):
+        """Leave the grouped form (the ranks disagree): H = the local running average."""
+        if self.grouped:
+            self._materialize_local()
+
+    def _materialize_local(self):
+        """grouped -> running average over the local samples (the fallback)."""
+        if not getattr(self, 'finalized', False):
+            if self.plan.n_local:
+                ops.tree_sum([self.subtree], _alpha(self.plan.n_local), out=self.H)
+            else:
+                self.H.zero_()
+        self.subtree = None
+        self.plan = None
+
+    @torch.no_grad()
+    def finalize(self):
+        """Grouped and token-sharded: finish the tree across ranks (every rank gets H).
+        RCCL: all_to_all of the subtrees' row slices, the upper tree levels on this rank's
+        slice, all_gather of the slices; gloo (CPU-side tests): all_gather of whole subtrees."""
+        if not self.grouped or self.finalized:
+            return self.H
+        import torch.distributed as dist
+        world = self.plan.world
+        flat = self.subtree.reshape(-1)
+        n = flat.numel()
+        alpha = _alpha(self.plan.n_global)
+        if dist.get_backend() == 'nccl':
+            chunk = -(-n // (4 * world)) * 4
+            src = torch.zeros(chunk * world, dtype=torch.float32, device=flat.device)
+            src[:n] = flat
+            got = torch.empty_like(src)
+            dist.all_to_all_single(got, src)
+            mine = torch.empty(chunk, dtype=torch.float32, device=flat.device)
+            ops.tree_sum([got[r * chunk:(r + 1) * chunk] for r in range(world)], alpha,
+                         out=mine)
+            full = torch.empty_like(src)
+            dist.all_gather_into_tensor(full, mine)
+            self.H.reshape(-1).copy_(full[:n])
+        else:
+            subs = [torch.empty_like(self.subtree) for _ in range(world)]
+            dist.all_gather(subs, self.subtree.contiguous())
+            ops.tree_sum(subs, alpha, out=self.H)
+        self.subtree = self.H
+        self.finalized = True
+        return self.H
 
 
 @torch.no_grad()

@@ -222,6 +222,23 @@ def hessian_accum(x: torch.Tensor, H: torch.Tensor, alpha: float, beta: float) -
     return H
 
 
+def tree_sum(parts, alpha: float = 1.0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out = alpha * the fixed pairwise tree sum of 1 / 2 / 4 / 8 equal fp32 tensors
+    (lcq_tree_sum; deterministic, the grouped Hessian's reduction order)."""
+    import ctypes
+    p0 = parts[0]
+    for p in parts:
+        if p.dtype != torch.float32 or p.shape != p0.shape or not p.is_contiguous():
+            raise ValueError('tree_sum: contiguous fp32 tensors of one shape')
+    if out is None:
+        out = torch.empty_like(p0)
+    if out.numel() % 4:
+        raise ValueError('tree_sum: numel must be a multiple of 4')
+    N.call('lcq_tree_sum', (ctypes.c_void_p * len(parts))(*[N.ptr(p) for p in parts]),
+           len(parts), out.numel(), float(alpha), N.ptr(out), N.stream_of(out))
+    return out
+
+
 def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: int,
                qmin: int, qmax: int, sym: bool, s_out, z_out, err: torch.Tensor,
                losses=None, s_in=None, z_in=None, fp8=None):

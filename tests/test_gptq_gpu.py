@@ -518,3 +518,36 @@ def test_owq_per_channel_plugin_layer_vs_reference(dev, name):
     fq = obj.w_qdq(layer, wq).cpu()
     same = (fq == c['fq']).float().mean().item()
     assert same >= 0.999, same
+
+
+@pytest.mark.parametrize('n,tpe,ic', [(128, 64, 512), (5, 100, 264), (16, 2048, 4096)])
+def test_grouped_hessian_world_independent(dev, n, tpe, ic):
+    """The grouped Hessian of one process equals the subtrees of 2 / 4 / 8 token shards
+    finished by the same tree, bit for bit; and it is the running-average Hessian up to fp32
+    summation order (<= 1e-6 of sum |x_i x_j| against fp64)."""
+    from lightcompress_amd import gptq_core, ops
+    g = torch.Generator().manual_seed(n + ic)
+    x = (torch.randn(n, tpe, ic, generator=g) *
+         torch.exp(torch.randn(ic, generator=g))).to(torch.bfloat16).to(dev)
+    one = gptq_core.HessianAccumulator(ic, dev, plan=gptq_core.GroupPlan(n))
+    one.add_batch(x)
+    assert one.grouped
+    H1 = one.finalize().clone()
+    for world in (2, 4, 8):
+        subs = []
+        for r in range(world):
+            plan = gptq_core.GroupPlan(n, r, world)
+            acc = gptq_core.HessianAccumulator(ic, dev, plan=plan)
+            xs = x[plan.first:plan.first + plan.n_local]
+            if plan.n_local:
+                acc.add_batch(xs)
+            assert acc.ready_grouped()
+            subs.append(acc.subtree)
+        H = ops.tree_sum(subs, gptq_core._alpha(n))
+        assert torch.equal(H, H1), world
+    xd = x.reshape(-1, ic).double()
+    ref = (2 / n) * xd.t() @ xd
+    bound = (2 / n) * xd.abs().t() @ xd.abs()
+    err = (H1.double() - ref).abs()
+    assert (err <= 2e-6 * bound + 1e-30).all().item(), (err / bound).max().item()
+    assert torch.equal(H1, H1.t())

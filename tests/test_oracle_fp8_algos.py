@@ -109,3 +109,20 @@ def test_row_shard_alignment():
         for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
             assert a1 == b0
         assert all(s0 % align == 0 for s0, _ in spans)
+
+
+def test_hessian_group_plan():
+    """gptq_core.GroupPlan: 8 groups covering every sample once; a world dividing 8 takes
+    contiguous power-of-two blocks of them, balanced (the shard GPTQ.sample_shard cuts)."""
+    from lightcompress_amd.gptq_core import GroupPlan, group_bounds
+    for n in (4, 5, 16, 128, 131):
+        b = group_bounds(n)
+        assert b[0][0] == 0 and b[-1][1] == n
+        assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
+        for world in (1, 2, 4, 8):
+            plans = [GroupPlan(n, r, world) for r in range(world)]
+            assert sum(p.n_local for p in plans) == n
+            for r, p in enumerate(plans):
+                assert p.first == -(-r * n // world)
+                assert len(p.local) == 8 // world
+                assert p.local[0][1] == 0 and p.local[-1][2] == p.n_local
