@@ -502,7 +502,14 @@ __global__ void __launch_bounds__(256, 1) k_gemm16b(Args a) {
     ktile16b<FP16, 1>(acc, bf, af, st, lds, t + 1, nk, w, wr, wc, lane);
   }
   if (t < nk) ktile16b<FP16, 0>(acc, bf, af, st, lds, t, nk, w, wr, wc, lane);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  // The nops carry the last block's accumulators as operands: an epilogue read of them cannot
+  // be scheduled above the wait (the asm MFMAs are opaque to the hazard recognizer; the earlier
+  // blocks' results are >= 16 MFMAs old by now)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 7"
+               : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]),
+                 "+a"(acc[7][4]), "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7])
+               :
+               : "memory");
 
   epi16<DT, EPI>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
 }

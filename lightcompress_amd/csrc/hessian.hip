@@ -153,8 +153,21 @@ __device__ __forceinline__ void wait_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-__device__ __forceinline__ v4s tr_read(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)p);
+// The transposed reads are issued as inline asm: with the builtin, the waitcnt pass cannot
+// tell them apart from the in-flight LDS-DMA stores and drains vmcnt(0) before each one (the
+// whole load pipeline, 14 drains per K-tile pair measured in the ISA). As asm their completion
+// is ours to wait for: every block starts with lgkmcnt(0) (block_wait below), and a fragment
+// is always read at least one block before the MFMA that consumes it; the data they read is
+// ordered by the counted vmcnt barriers, as for the projection GEMM.
+template <int OFF>
+__device__ __forceinline__ v4s tr_read(uint32_t addr) {
+  v4s v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+
+__device__ __forceinline__ void block_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // Per-lane part of a fragment read: MFMA 16x16x32 operand lane l = channel row l & 15, tokens
@@ -168,18 +181,46 @@ __device__ __forceinline__ uint32_t frag_lane_off(int lane, int rbodd, int h) {
   return (uint32_t)((g >> 1) * 1024 + r * 64 + pc * 16 + (p & 1) * 8);
 }
 
+// LDS byte addresses of this lane's fragment reads: [operand A / B][parity of the 16-channel
+// row block], for the wave's 128-channel half (wave row wr for A, wave column wc for B) of
+// buffer 0, h = 0 (h = 1 is 4 token rows = 256 B further)
 struct FragOff {
-  uint32_t o[2];  // [rb & 1], h = 0 (h = 1 is 4 token rows = 256 B further)
+  uint32_t o[2][2][2];  // [buffer][A / B][parity]: offsets within a buffer fit 16 bits
 };
 
-// fragment (16 channels rb * 16.., 32 tokens kb * 32..) of the operand image at byte `tile`
-// of the LDS allocation (a compile-time constant at every call: one address VGPR per rb parity,
-// everything else in the instruction's offset field)
-__device__ __forceinline__ v8s read_frag(char* lds, int tile, const FragOff& fo, int rb, int kb) {
-  const char* base = lds + fo.o[rb & 1] + tile + ((rb >> 1) * 4 + kb * 2) * 1024;
-  const v4s lo = tr_read(base);
-  const v4s hi = tr_read(base + 256);
+// fragment X (16 channels, X = 0..7 within the wave's 128) x k block KB (32 tokens) of the
+// operand image at byte TILE of a buffer: everything but the lane base in the offset field
+template <int TILE, int X, int KB>
+__device__ __forceinline__ v8s read_frag(const uint32_t (&base)[2]) {
+  constexpr int off = TILE + ((X >> 1) * 4 + KB * 2) * 1024;
+  const v4s lo = tr_read<off>(base[X & 1]);
+  const v4s hi = tr_read<off + 256>(base[X & 1]);
   return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int TILE>
+__device__ __forceinline__ v8s frag_at(const FragOff& fo, int op, int x, int kb) {
+  const uint32_t (&base)[2] = fo.o[TILE / BUF][op];
+  constexpr int T = TILE % BUF;
+  // x, kb are constants after unrolling: the switch folds to one read pair
+  switch (x * 2 + kb) {
+    case 0: return read_frag<T, 0, 0>(base);
+    case 1: return read_frag<T, 0, 1>(base);
+    case 2: return read_frag<T, 1, 0>(base);
+    case 3: return read_frag<T, 1, 1>(base);
+    case 4: return read_frag<T, 2, 0>(base);
+    case 5: return read_frag<T, 2, 1>(base);
+    case 6: return read_frag<T, 3, 0>(base);
+    case 7: return read_frag<T, 3, 1>(base);
+    case 8: return read_frag<T, 4, 0>(base);
+    case 9: return read_frag<T, 4, 1>(base);
+    case 10: return read_frag<T, 5, 0>(base);
+    case 11: return read_frag<T, 5, 1>(base);
+    case 12: return read_frag<T, 6, 0>(base);
+    case 13: return read_frag<T, 6, 1>(base);
+    case 14: return read_frag<T, 7, 0>(base);
+    default: return read_frag<T, 7, 1>(base);
+  }
 }
 
 template <bool FP16>
@@ -205,6 +246,8 @@ __device__ __forceinline__ void ktile(v4f (&acc)[8][8], v8s (&bf)[2][8][2], v8s 
   constexpr int At = cur * BUF;
   constexpr int An = (cur ^ 1) * BUF;
   constexpr int Bn = An + TILE_B;
+  (void)wr;
+  (void)wc;
   const int64_t t2 = t + 2 < nk ? t + 2 : nk - 1;
   const __amdgpu_buffer_rsrc_t rs = ktile_rsrc(a, kt0 + t2);
 #pragma unroll
@@ -216,6 +259,7 @@ __device__ __forceinline__ void ktile(v4f (&acc)[8][8], v8s (&bf)[2][8][2], v8s 
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
           const int i = mm * 16 + n * 2 + kb;
+          if (i == 0) block_wait();  // the fragments read during the previous block
           mfma16a<FP16>(acc[2 * mb + mm][n], bf[P][n][kb], af[mb & 1][mm][kb]);
           if (i == 7) {
             if (mb == 1) wait_barrier<18>();
@@ -225,12 +269,12 @@ __device__ __forceinline__ void ktile(v4f (&acc)[8][8], v8s (&bf)[2][8][2], v8s 
           if (mb > 0 && (i == 8 || i == 20)) load_piece(st, rs, lds, cur, w, 8 + 2 * mb + (i == 20));
           if (i >= 8 && i < 12) {
             const int q = i - 8, m2 = q >> 1, k2 = q & 1;
-            if (mb < 3) af[(mb + 1) & 1][m2][k2] = read_frag(lds, At, fo, wr * 8 + 2 * (mb + 1) + m2, k2);
-            else af[0][m2][k2] = read_frag(lds, An, fo, wr * 8 + m2, k2);  // K-tile t+1, block 0
+            if (mb < 3) af[(mb + 1) & 1][m2][k2] = frag_at<At>(fo, 0, 2 * (mb + 1) + m2, k2);
+            else af[0][m2][k2] = frag_at<An>(fo, 0, m2, k2);  // K-tile t+1, block 0
           }
           if ((mb == 1 || mb == 2) && i >= 12 && i < 20) {  // B fragments of K-tile t+1
             const int f = (mb - 1) * 8 + (i - 12), nn = f >> 1, k3 = f & 1;
-            bf[P ^ 1][nn][k3] = read_frag(lds, Bn, fo, wc * 8 + nn, k3);
+            bf[P ^ 1][nn][k3] = frag_at<Bn>(fo, 1, nn, k3);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -257,8 +301,16 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a) {
   Stage st;
   make_stage(a, ti, tj, w, lane, st);
   FragOff fo;
-  fo.o[0] = frag_lane_off(lane, 0, 0);
-  fo.o[1] = frag_lane_off(lane, 1, 0);
+  {
+    const uint32_t l0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        fo.o[b][0][par] = l0 + b * BUF + wr * 16384 + frag_lane_off(lane, par, 0);  // A: 128 wr..
+        fo.o[b][1][par] = l0 + b * BUF + wc * 16384 + frag_lane_off(lane, par, 0);  // B: 128 wc..
+      }
+  }
 
   v4f acc[8][8];
 #pragma unroll
@@ -278,11 +330,11 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a) {
 #pragma unroll
   for (int n = 0; n < 8; ++n)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) bf[0][n][k] = read_frag(lds, TILE_B, fo, wc * 8 + n, k);
+    for (int k = 0; k < 2; ++k) bf[0][n][k] = frag_at<TILE_B>(fo, 1, n, k);
 #pragma unroll
   for (int m2 = 0; m2 < 2; ++m2)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) af[0][m2][k] = read_frag(lds, 0, fo, wr * 8 + m2, k);
+    for (int k = 0; k < 2; ++k) af[0][m2][k] = frag_at<0>(fo, 0, m2, k);
   asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
 
   int64_t t = 0;
@@ -291,7 +343,16 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a) {
     ktile<FP16, 1>(acc, bf, af, st, fo, a, lds, kt0, t + 1, nk, w, wr, wc);
   }
   if (t < nk) ktile<FP16, 0>(acc, bf, af, st, fo, a, lds, kt0, t, nk, w, wr, wc);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  // drain, and cover the last MFMA's result latency before the accumulators are read (the asm
+  // MFMA is opaque to the hazard recognizer: 16x16x32 = 8 passes -> 4 * 8 + 2 wait states)
+  // The nops carry the last block's accumulators as operands: an epilogue read of them cannot
+  // be scheduled above the wait (the asm MFMAs are opaque to the hazard recognizer; the earlier
+  // blocks' results are >= 16 MFMAs old by now)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 7"
+               : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]),
+                 "+a"(acc[7][4]), "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7])
+               :
+               : "memory");
 
   // acc[m][n][jj] (swapped layout): H row i = ti*256 + wr*128 + m*16 + fr, columns
   // tj*256 + wc*128 + n*16 + fq*4 + jj. 32-bit element offsets (ic, icp <= 46336: checked

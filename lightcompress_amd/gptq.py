@@ -73,7 +73,9 @@ class GPTQ(BaseBlockwiseQuantization):
         if self.data_free:
             return None
         mode = self.parallel_mode()
-        if mode in ('single', 'shard_blocks'):
+        if mode in ('single', 'shard_blocks', 'replicate'):
+            # replicas: every rank's own full tree (the averaging all-reduce of identical
+            # replicas is then exact, as on one GPU)
             return gptq_core.GroupPlan(self.n_samples)
         if mode == 'shard_tokens':
             from .parallel import dist_world
@@ -196,22 +198,20 @@ class GPTQ(BaseBlockwiseQuantization):
             cache = acc.prepared_by = {}
         if nout not in cache:
             grouped = acc.ready_grouped()
-            if replicate and self.parallel_mode() == 'shard_tokens':
+            shard = replicate and self.parallel_mode() == 'shard_tokens'
+            if shard:
                 # every rank must take the same road: grouped only if all ranks are
                 flag = torch.tensor([int(grouped)], dtype=torch.int32, device=acc.H.device)
                 dist.all_reduce(flag, op=dist.ReduceOp.MIN)
                 if grouped and not int(flag.item()):
                     acc.fallback()
                     grouped = False
-            if grouped:
-                # the fixed group tree, finished across the token shards (bit-identical to
-                # one GPU); nothing else to reduce
-                H = acc.finalize().clone()
-            else:
-                H = acc.H.clone()
-            if grouped:
+            # grouped: the fixed group tree (finished across the token shards when sharded:
+            # bit-identical to one GPU, nothing else to reduce)
+            H = (acc.finalize() if grouped else acc.H).clone()
+            if shard and grouped:
                 pass
-            elif replicate and self.parallel_mode() == 'shard_tokens':
+            elif shard:
                 # token shards: H = sum_r n_r H_r / N (each H_r the running average over the
                 # rank's n_r samples) -- the single-GPU Hessian up to fp32 summation order
                 n = torch.tensor([float(acc.nsamples)], dtype=torch.float64, device=H.device)
