@@ -514,14 +514,23 @@ __global__ void __launch_bounds__(256, 1) k_gemm16b(Args a) {
   epi16<DT, EPI>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
 }
 
-// one wave: lane l sums partials l, l+64, ... in order, then a fixed xor tree (deterministic)
-__global__ void __launch_bounds__(64) k_loss_reduce(const double* part, int64_t nparts,
-                                                    int64_t numel, float* out, int slot) {
+// one 1024-thread workgroup: thread l sums partials l, l + 1024, ... in order, then a fixed
+// xor tree per wave and the 16 wave sums in wave order (deterministic; 16 K partials at the
+// down_proj shape: one wave took ~0.1 ms, 240 launches per AWQ block step)
+__global__ void __launch_bounds__(1024) k_loss_reduce(const double* part, int64_t nparts,
+                                                      int64_t numel, float* out, int slot) {
+  __shared__ double ws[16];
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < nparts; i += 64) s += part[i];
+  for (int64_t i = threadIdx.x; i < nparts; i += 1024) s += part[i];
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
-  if (threadIdx.x == 0) out[slot] = (float)s / (float)numel;
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += ws[w];
+    out[slot] = (float)t / (float)numel;
+  }
 }
 
 // tile order: 0 = per-XCD 4 x 8 chunks (slot_tile, the default), 1 = N-band-major (tile_nb,
@@ -665,7 +674,7 @@ extern "C" int lcq_gemm_sq_diff(const void* a, int dtype, int64_t lda, int64_t m
   hipStream_t st = as_stream(stream);
   rc = dispatch<EPI_SQDIFF>(dtype, g, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_loss_reduce, 1, 64, 0, st, g.part, (int64_t)g.n_mt * g.n_nt * 4, m * n,
+  hipLaunchKernelGGL(k_loss_reduce, 1, 1024, 0, st, g.part, (int64_t)g.n_mt * g.n_nt * 4, m * n,
                      reinterpret_cast<float*>(out_f32), slot);
   return check_launch("lcq_gemm_sq_diff: reduce");
 }

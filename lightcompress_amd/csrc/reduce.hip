@@ -20,24 +20,26 @@ struct TreeArgs {
   float* out;
 };
 
-// sum of p[lo .. hi) in the tree order (hi - lo a power of two), elementwise on float4
-__device__ __forceinline__ float4 tree4(const float4 (&v)[TREE_MAX], int lo, int hi) {
-  if (hi - lo == 1) return v[lo];
-  const int mid = (lo + hi) >> 1;
-  const float4 a = tree4(v, lo, mid), b = tree4(v, mid, hi);
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y), __fadd_rn(a.z, b.z),
                      __fadd_rn(a.w, b.w));
 }
 
+// the tree order of NP (1, 2, 4, 8) values, level by level (no recursion: a recursive helper
+// is not inlined and spills v[] to scratch)
 template <int NP>
 __global__ void __launch_bounds__(256) k_tree_sum(TreeArgs a) {
   const int64_t n4 = a.n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 v[TREE_MAX];
+    float4 v[NP];
 #pragma unroll
     for (int k = 0; k < NP; ++k) v[k] = reinterpret_cast<const float4*>(a.p[k])[i];
-    float4 s = tree4(v, 0, NP);
+#pragma unroll
+    for (int w = 1; w < NP; w *= 2)
+#pragma unroll
+      for (int k = 0; k < NP; k += 2 * w) v[k] = add4(v[k], v[k + w]);
+    float4 s = v[0];
     if (a.alpha != 1.0f)
       s = make_float4(__fmul_rn(a.alpha, s.x), __fmul_rn(a.alpha, s.y),
                       __fmul_rn(a.alpha, s.z), __fmul_rn(a.alpha, s.w));

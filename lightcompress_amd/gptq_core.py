@@ -102,9 +102,11 @@ class HessianAccumulator:
     def _add_grouped(self, x: torch.Tensor, tpe: int):
         parts = []
         for _, s0, s1 in self.plan.local:
-            P = torch.zeros((self.ic, self.ic), dtype=torch.float32, device=x.device)
-            if s1 > s0:
+            if s1 > s0:  # beta 0: the kernel never reads P
+                P = torch.empty((self.ic, self.ic), dtype=torch.float32, device=x.device)
                 ops.hessian_accum(x[s0 * tpe:s1 * tpe], P, 1.0, 0.0)
+            else:
+                P = torch.zeros((self.ic, self.ic), dtype=torch.float32, device=x.device)
             parts.append(P)
         if self.plan.world == 1:  # the whole tree here: H = alpha * tree
             ops.tree_sum(parts, _alpha(self.plan.n_global), out=self.H)
