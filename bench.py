@@ -433,8 +433,10 @@ def bench_gptq(args, rank, world, dev):
     if h:
         # algorithmic: symmetric rank-n update n*ic*(ic+1) flops per launch
         tf = h['flops'] / (h['total_ms'] * 1e-3) / 1e12
-        traffic, src = pmc_traffic('gptq', ('k_xt_pack', 'k_syrk16'))
-        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_xt_pack + k_syrk16, bf16 MFMA XᵀX)',
+        traffic, src = pmc_traffic('gptq', ('k_syrk_x',))
+        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_syrk_x: bf16 MFMA XᵀX read from '
+                                     'token-major X through transposed LDS reads; one launch '
+                                     'per calibration-sample group)',
                            'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
                            'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4),
                            'traffic': traffic, 'traffic_source': src,
