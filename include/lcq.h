@@ -81,6 +81,17 @@ int lcq_int_quant_dynamic(const void* x, int x_dtype, int64_t rows, int64_t cols
                           void* packed_out, int pack_bits, void* scales_out, void* zeros_out,
                           void* stream);
 
+/* lcq_int_quant_dynamic with calib_algo learnable and clip factors (v2 clip buffers
+ * buf_upbound_factor / buf_lowbound_factor, passed by BaseBlockwiseQuantization.w_qdq,
+ * base_blockwise_quantization.py:46-66): each group's min / max becomes
+ * get_learnable_range(group, low, up) (quant.py:205-219) before get_qparams. up / low:
+ * [rows*cols/group] in x_dtype (f16 / bf16); sym uses up only; asym with low NULL leaves the
+ * range alone, as the reference does. */
+int lcq_int_quant_learnable(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                            int64_t group, const void* up, const void* low, int qmin, int qmax,
+                            int sym, void* fq_out, int fq_dtype, void* codes_out,
+                            int codes_dtype, void* scales_out, void* zeros_out, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Grouped integer quantization with GIVEN qparams.
  * Replaces IntegerQuantizer.fake_quant_weight_static / real_quant_weight_static
@@ -309,18 +320,31 @@ int lcq_auto_clip_search_act(const void* w, const void* x, const void* qx, int d
  * clamped weights with the saturating float_quantize stand-in (quant.py:545-553, 1061-1080;
  * qmin / qmax / sym ignored). tensor_batch 0: per_channel scales (one per row); > 0:
  * per_tensor scale over each batch of tensor_batch rows, the reference's oc_batch_size
- * (auto_clip.py:108). */
+ * (auto_clip.py:108). version 1: clip_version v1 (the candidate is the clamped weight's
+ * dynamic fake quant); 2 (integer only; awq_comb_omni w6a6 / w8a8 step_1_awq.yml, calib_algo
+ * learnable): the candidate is the unclamped weight's static fake quant with the qparams of
+ * get_learnable_range(w, logit(min_val / org_min), logit(max_val / org_max))
+ * (auto_clip.py:258-267, quant.py:205-219). The returned bounds are the same kind in both. */
 int64_t lcq_auto_clip_pc_workspace_bytes(int64_t oc, int64_t T, int nsteps);
 int lcq_auto_clip_search_pc(const void* w, const void* x, const void* qx, int dtype, int64_t oc,
                             int64_t ic, int64_t T, int nsteps, const void* factors, int qmin,
                             int qmax, int sym, int clip_sym, int fmt, int tensor_batch,
-                            void* workspace, int64_t ws_bytes, void* best_max, void* best_min,
-                            void* stream);
+                            int version, void* workspace, int64_t ws_bytes, void* best_max,
+                            void* best_min, void* stream);
 
 /* AutoClipper.apply_clip, v1 (auto_clip.py:193-212): out = clamp(x, cmin, cmax) per group;
  * cmin NULL -> -cmax. In place allowed. */
 int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t cols, int64_t group,
                    const void* cmax, const void* cmin, void* out, void* stream);
+
+/* AutoClipper.get_clip_factor, v2 (auto_clip.py:213-256): per group of x [rows, cols] (group
+ * | cols, group % 8 == 0) the logit factors of the searched bounds against the group's own
+ * range, in dtype: clip_sym: up = logit(cmax / max(|max|, |min|).clamp(1e-5)), low not
+ * written (the reference stores None); else up = logit(cmax / max), low = logit(cmin / min).
+ * cmax / cmin / up / low: [rows * cols / group] in dtype (bf16 / fp16). */
+int lcq_clip_factors(const void* x, int dtype, int64_t rows, int64_t cols, int64_t group,
+                     const void* cmax, const void* cmin, int clip_sym, void* up_out,
+                     void* low_out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * FP8 (FloatQuantizer, quant.py:963-1229; kernel.py:7-138; quant.py:18-43).

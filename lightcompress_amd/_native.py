@@ -37,6 +37,8 @@ SIGNATURES = {
     'lcq_last_error': ([], ctypes.c_char_p),
     'lcq_int_quant_dynamic': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _vp, _int, _int, _int,
                                _vp, _int, _vp, _int, _vp, _int, _vp, _vp, _vp], _int),
+    'lcq_int_quant_learnable': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _int, _int, _int, _vp,
+                                 _int, _vp, _int, _vp, _vp, _vp], _int),
     'lcq_int_quant_static': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _int, _int,
                               _int, _vp, _int, _vp, _int, _vp, _int, _vp], _int),
     'lcq_int_quant_static_nozp': ([_vp, _int, _i64, _i64, _i64, _vp, _int, _vp, _int, _int,
@@ -76,8 +78,9 @@ SIGNATURES = {
                                   _int, _int, _int, _int, _vp, _f32, _vp, _vp, _vp], _int),
     'lcq_auto_clip_pc_workspace_bytes': ([_i64, _i64, _int], _i64),
     'lcq_auto_clip_search_pc': ([_vp, _vp, _vp, _int, _i64, _i64, _i64, _int, _vp, _int, _int,
-                                 _int, _int, _int, _int, _vp, _i64, _vp, _vp, _vp], _int),
+                                 _int, _int, _int, _int, _int, _vp, _i64, _vp, _vp, _vp], _int),
     'lcq_clip_apply': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _vp, _vp], _int),
+    'lcq_clip_factors': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _int, _vp, _vp, _vp], _int),
     'lcq_absmax': ([_vp, _int, _i64, _vp, _vp, _vp], _int),
     'lcq_fp8_quant': ([_vp, _int, _i64, _i64, _i64, _int, _int, _f32, _f32, _int, _vp, _vp, _vp,
                        _int, _vp, _vp], _int),

@@ -1,10 +1,13 @@
-"""AWQ weight clipping (drop-in for llmc ``quantization/auto_clip.py``, clip_version v1).
+"""AWQ weight clipping (drop-in for llmc ``quantization/auto_clip.py``, clip_version v1 / v2).
 
 ``auto_clip_layer`` is one HIP launch per linear (``lcq_auto_clip_search``): the reference
 materialises a [256, T, ng, 128] bf16 broadcast product per shrink step and batch of rows
 (1 GiB at ng=32); the kernel keeps weights in VGPRs and streams token tiles through LDS.
 per_channel weights (group = ic, the w8a8 AWQ configs) take ``lcq_auto_clip_search_pc``;
 w_only False feeds the shrink steps the activation fake-quant (``fake_quantize_input``).
+clip_version v2 (calib_algo learnable; awq_comb_omni w6a6 / w8a8 step_1_awq.yml) searches the
+same bounds with learnable-range candidates (unclamped weight) and stores them as logit factors
+(``buf_upbound_factor`` / ``buf_lowbound_factor``) that the deploy fake quant applies.
 """
 from __future__ import annotations
 
@@ -33,8 +36,8 @@ class AutoClipper:
         self.w_only = w_only
         self.reduce_across_ranks = False  # set by the algorithm in replicate (DP) mode
         self.shard_rows = False           # shard_search: each rank searches its row range
-        if clip_version != 'v1':
-            raise NotImplementedError('clip_version v2 (learnable) is not on the device path')
+        if clip_version not in ('v1', 'v2'):
+            raise Exception('Not support other clip version')
 
     @torch.no_grad()
     def run(self, block, block_idx, input_feat, n_sample_token):
@@ -100,6 +103,9 @@ class AutoClipper:
             raise NotImplementedError(f'device auto-clip kernel: group size {group}')
         if per_channel and (w.shape[1] % 128 or wq.calib_algo == 'mse'):
             raise NotImplementedError('per_channel auto-clip: ic % 128 == 0, minmax qparams')
+        if self.clip_version == 'v2' and (fp8 is not None or wq.granularity != 'per_channel'):
+            # every reference v2 config (awq_comb_omni w6a6 / w8a8) is integer per_channel
+            raise NotImplementedError('clip_version v2: integer per_channel weights')
         if wq.granularity == 'per_tensor' and fp8 is None:
             raise NotImplementedError('per_tensor integer auto-clip is not on the device path')
         if (getattr(wq, 'quant_type', 'int-quant') == 'int-quant'
@@ -120,7 +126,8 @@ class AutoClipper:
             mse = (wq._mse_nsteps(), wq.mse_grid, 2.4)
         return ops.auto_clip_search(w.data, x, group, int(max_shrink * n_grid), n_grid, qmin,
                                     qmax, wq.sym, self.clip_sym, mse=mse, qx=qx, fp8=fp8,
-                                    tensor_batch=tensor_batch)
+                                    tensor_batch=tensor_batch,
+                                    version=2 if self.clip_version == 'v2' else 1)
 
     def _float_quant(self, w):
         """(fp8 dtype, per-tensor batch rows) for FloatQuantizer weights, (None, 0) for
@@ -140,12 +147,30 @@ class AutoClipper:
 
     @torch.no_grad()
     def apply_clip(self, block_idx, layer, min_val, max_val, layer_name):
-        """auto_clip.py:193-212 (v1): clamp the weight per group in place."""
+        """auto_clip.py:193-233. v1: clamp the weight per group in place. v2: keep the weight,
+        register the logit factors of the bounds (get_clip_factor) as buffers."""
+        w = layer.weight.data
+        group = w.shape[1] // max_val.shape[1]
+        if self.clip_version == 'v2':
+            up, low = self.get_clip_factor(block_idx, layer, min_val, max_val, layer_name)
+            layer.register_buffer('buf_upbound_factor', up)
+            layer.register_buffer('buf_lowbound_factor', low)
+            if self.save_clip:
+                n = f'{layer_name}.weight_quantizer.'
+                d = self.weight_clips.setdefault(block_idx, {})
+                d[n + 'upbound_factor'] = up.cpu()
+                d[n + 'lowbound_factor'] = low.cpu() if low is not None else None
+            return
+        cmax = max_val.reshape(-1).to(w.dtype)
+        cmin = None if self.clip_sym else min_val.reshape(-1).to(w.dtype)
+        ops.clip_apply(w, group, cmax, cmin, out=w)
+        # v1 stores nothing under save_clip (only v2 saves clip factors, auto_clip.py:218-233)
+
+    def get_clip_factor(self, block_idx, layer, min_val, max_val, layer_name):
+        """auto_clip.py:235-256 (one HIP launch, lcq_clip_factors): (up, low | None) shaped
+        like get_minmax_range of the reshaped weight, [groups, 1], in the weight dtype."""
         w = layer.weight.data
         group = w.shape[1] // max_val.shape[1]
         cmax = max_val.reshape(-1).to(w.dtype)
         cmin = None if self.clip_sym else min_val.reshape(-1).to(w.dtype)
-        ops.clip_apply(w, group, cmax, cmin, out=w)
-        if self.save_clip:
-            self.weight_clips.setdefault(block_idx, {})[f'{layer_name}.weight_quantizer.'
-                                                        'upbound_factor'] = max_val.cpu()
+        return ops.clip_factors(w, group, cmax, cmin, self.clip_sym)

@@ -33,7 +33,6 @@ class Awq(BaseBlockwiseQuantization):
         special = self.quant_config.get('special', {}) or {}
         self.trans = special.get('trans', True)
         self.trans_version = special.get('trans_version', 'v2')
-        self.save_scale = special.get('save_scale', False)
         self.awq_bs = special.get('awq_bs', None)
         self.save_mem = special.get('save_mem', True)
         if self.trans_version not in ('v1', 'v2'):
@@ -356,3 +355,7 @@ class Awq(BaseBlockwiseQuantization):
                                          inspect_module, is_gqa, subset_kwargs)
         self.apply_scale(scale, prev_op, layers)
         self.update_input_feat(scale, input_feat, layers_dict, is_gqa)
+        if self.save_scale:  # awq.py:367-370
+            for n in layers_dict:
+                name = f'{self.model.block_name_prefix}.{self.block_idx}.{n}'
+                self.act_scales[name] = scale.clone()

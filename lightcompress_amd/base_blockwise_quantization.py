@@ -137,6 +137,39 @@ class BlockwiseOpt:
                 # the broadcast writes weights through .data (no version bump): no memoised
                 # stage may survive it
                 self._clear_block_cache(block)
+        self.save_transforms()
+
+    def save_transforms(self):
+        """blockwise_optimization.py:40-52: the AWQ scales (save_scale) and v2 clip factors
+        (save_clip) as scales.pth / clips.pth, the files OmniQuant's LET / LWC load. Under
+        shard_blocks every rank holds its own blocks' entries: they are merged on rank 0,
+        which alone writes."""
+        import os
+        want_s = getattr(self, 'save_scale', False) and hasattr(self, 'act_scales')
+        want_c = getattr(self, 'save_clip', False) and hasattr(self, 'auto_clipper')
+        if not (want_s or want_c):
+            return
+        rank, world = P.dist_world()
+        scales = dict(getattr(self, 'act_scales', {}))
+        clips = dict(self.auto_clipper.weight_clips) if want_c else {}
+        if world > 1 and self.parallel_mode() == 'shard_blocks':
+            got = [None] * world
+            dist.all_gather_object(got, ({k: v.cpu() for k, v in scales.items()}, clips))
+            scales, clips = {}, {}
+            for sc, cl in got:
+                scales.update(sc)
+                clips.update(cl)
+            clips = dict(sorted(clips.items()))
+        if rank != 0:
+            return
+        if want_s:
+            os.makedirs(self.scale_path, exist_ok=True)
+            torch.save(scales, os.path.join(self.scale_path, 'scales.pth'))
+            if getattr(self, 'act_shifts', None):
+                torch.save(self.act_shifts, os.path.join(self.scale_path, 'shifts.pth'))
+        if want_c:
+            os.makedirs(self.clip_path, exist_ok=True)
+            torch.save(clips, os.path.join(self.clip_path, 'clips.pth'))
 
     def _clear_block_cache(self, block):
         if hasattr(self.model, 'clear_block_cache'):
@@ -312,7 +345,11 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         if self.weight_clip or special.get('search_clip_init', False):
             from .auto_clip import AutoClipper
             self.save_clip = special.get('save_clip', False)
+            if self.save_clip:
+                self.clip_path = special['clip_path']
             self.clip_version = special.get('clip_version', 'v1')
+            if self.clip_version == 'v2':
+                assert self.wquantizer.calib_algo == 'learnable'
             clip_sym = special.get('clip_sym', self.wquantizer.sym)
             self.auto_clipper = AutoClipper(w_only=self.w_only, wquantizer=self.wquantizer,
                                             aquantizer=self.aquantizer,
@@ -320,6 +357,9 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                                             save_clip=self.save_clip,
                                             padding_mask=self.padding_mask)
         self.save_scale = special.get('save_scale', False)
+        if self.save_scale:
+            self.scale_path = special['scale_path']
+            self.act_scales = {}
         self.online_rotate = special.get('online_rotate', False)
         if self.online_rotate:
             raise NotImplementedError('online rotation (QuaRot) is out of scope')

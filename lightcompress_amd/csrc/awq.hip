@@ -779,6 +779,68 @@ extern "C" int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t co
   return check_launch("lcq_clip_apply");
 }
 
+// get_clip_factor (auto_clip.py:213-256): one wave per group -> the group's min / max
+// (get_minmax_range of the reshaped weight), then the logit of the bound ratios in DT.
+template <int DT>
+__global__ void __launch_bounds__(256) k_clip_factors(const uint16_t* __restrict__ x,
+                                                     int64_t ng, int64_t group,
+                                                     const uint16_t* __restrict__ cmax,
+                                                     const uint16_t* __restrict__ cmin,
+                                                     int clip_sym, uint16_t* __restrict__ up,
+                                                     uint16_t* __restrict__ low) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= ng) return;
+  float mx = -INFINITY, mn = INFINITY;
+  for (int64_t k = (int64_t)lane * 8; k < group; k += 64 * 8) {
+    float v[8];
+    ld8<DT>(x, g * group + k, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mx = fmaxf(mx, v[j]);
+      mn = fminf(mn, v[j]);
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+    mn = fminf(mn, __shfl_xor(mn, m, 64));
+  }
+  if (lane != 0) return;
+  const float bmax = ld1<DT>(cmax, g);
+  if (clip_sym) {
+    const float am = fmaxf(fmaxf(fabsf(mx), fabsf(mn)), dtr<DT>(1e-5f));
+    st1<DT>(up, g, logit_ct<DT>(dtr<DT>(bmax / am)));
+  } else {
+    st1<DT>(up, g, logit_ct<DT>(dtr<DT>(bmax / mx)));
+    st1<DT>(low, g, logit_ct<DT>(dtr<DT>(ld1<DT>(cmin, g) / mn)));
+  }
+}
+
+extern "C" int lcq_clip_factors(const void* x, int dtype, int64_t rows, int64_t cols,
+                                int64_t group, const void* cmax, const void* cmin, int clip_sym,
+                                void* up_out, void* low_out, void* stream) {
+  LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16, "clip factors: bf16 / fp16");
+  LCQ_REQUIRE(rows > 0 && cols > 0 && group > 0 && cols % group == 0 && group % 8 == 0,
+              "group must divide cols and be a multiple of 8");
+  LCQ_REQUIRE(x && cmax && up_out && (clip_sym || (cmin && low_out)), "null pointers");
+  const int64_t ng = rows * cols / group;
+  const dim3 grid((unsigned)((ng + 3) / 4));
+  hipStream_t st = as_stream(stream);
+  auto* xp = reinterpret_cast<const uint16_t*>(x);
+  auto* mxp = reinterpret_cast<const uint16_t*>(cmax);
+  auto* mnp = reinterpret_cast<const uint16_t*>(cmin);
+  auto* up = reinterpret_cast<uint16_t*>(up_out);
+  auto* lo = reinterpret_cast<uint16_t*>(low_out);
+  if (dtype == LCQ_BF16)
+    hipLaunchKernelGGL(k_clip_factors<LCQ_BF16>, grid, 256, 0, st, xp, ng, group, mxp, mnp,
+                       clip_sym, up, lo);
+  else
+    hipLaunchKernelGGL(k_clip_factors<LCQ_F16>, grid, 256, 0, st, xp, ng, group, mxp, mnp,
+                       clip_sym, up, lo);
+  return check_launch("lcq_clip_factors");
+}
+
 // ----------------------------------------------------------------------------------------
 // auto_clip search for per_channel weights (group = the whole row, auto_clip.py:96-99; the
 // w8a8 vLLM / SGLang AWQ configs, awq_w8a8.yml). The per-group kernel's lane-pair-per-row
@@ -809,6 +871,10 @@ constexpr int PC_QP = 5;        // per step: smin, smax, s, 1/s, z
 //   2 FP8 per_tensor: the clamped row's max(|cmax|, |cmin|) is left in slot 2 for
 //     k_clip_pc_tensor_qp, which forms the scale of the whole 256 (or 64)-row batch the
 //     reference fake-quantizes at once (auto_clip.py:108-114, 161-163).
+//   3 integer, clip_version v2 (auto_clip.py:258-267): no clamp of the weight; the step's
+//     bounds become logit factors of the row's own min / max and the qparams come from
+//     get_learnable_range of the unclamped row (slots 0 / 1 = -inf / +inf: fq_pc's clamp is
+//     the identity).
 template <int DT, int FQ>
 __global__ void __launch_bounds__(256) k_clip_pc_stats(const uint16_t* __restrict__ w,
                                                       int64_t oc, int64_t ic, int nsteps,
@@ -849,14 +915,20 @@ __global__ void __launch_bounds__(256) k_clip_pc_stats(const uint16_t* __restric
     float qs, qz;
     if constexpr (FQ == 0) {
       qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
+    } else if constexpr (FQ == 3) {
+      const float low = logit_ct<DT>(dtr<DT>(smin / org_min));  // logit(min_val / org_min)
+      const float up = logit_ct<DT>(dtr<DT>(smax / org_max));
+      float lmn = mn, lmx = mx;  // get_learnable_range(w, ...): the unclamped row's range
+      learnable_range<DT>(lmn, lmx, up, low, true, sym);
+      qparams_ct<DT>(lmn, lmx, qmin, qmax, sym, qs, qz);
     } else {
       const float am = fmaxf(fmaxf(fabsf(cmx), fabsf(cmn)), dtr<DT>(1e-5f));  // .clamp(1e-5)
       qs = FQ == 1 ? dtr<DT>(am / qmax) : am;
       qz = 0.f;
     }
     float* d = qp + ((int64_t)o * PC_NS + lane) * PC_QP;
-    d[0] = smin;
-    d[1] = smax;
+    d[0] = FQ == 3 ? -INFINITY : smin;
+    d[1] = FQ == 3 ? INFINITY : smax;
     d[2] = qs;
     d[3] = 1.0f / qs;
     d[4] = qz;
@@ -1060,8 +1132,8 @@ extern "C" int64_t lcq_auto_clip_pc_workspace_bytes(int64_t oc, int64_t T, int n
 template <int DT>
 static void launch_clip_pc(const void* w, const void* x, const void* qx, int64_t oc, int64_t ic,
                            int64_t T, int nsteps, const void* factors, int qmin, int qmax,
-                           int sym, int clip_sym, int fmt, int tensor_batch, char* ws,
-                           void* best_max, void* best_min, hipStream_t st) {
+                           int sym, int clip_sym, int fmt, int tensor_batch, int version,
+                           char* ws, void* best_max, void* best_min, hipStream_t st) {
   float* qp = reinterpret_cast<float*>(ws);
   float* orgmm = qp + oc * PC_NS * PC_QP;
   float* part = orgmm + oc * 2;
@@ -1071,7 +1143,10 @@ static void launch_clip_pc(const void* w, const void* x, const void* qx, int64_t
   const auto* wp = reinterpret_cast<const uint16_t*>(w);
   const auto* fp = reinterpret_cast<const float*>(factors);
   const dim3 gs((unsigned)((oc + 3) / 4));
-  if (fmt == 0)
+  if (fmt == 0 && version == 2)
+    hipLaunchKernelGGL((k_clip_pc_stats<DT, 3>), gs, 256, 0, st, wp, oc, ic, nsteps, fp,
+                       (float)qmin, (float)qmax, sym, clip_sym, qp, orgmm);
+  else if (fmt == 0)
     hipLaunchKernelGGL((k_clip_pc_stats<DT, 0>), gs, 256, 0, st, wp, oc, ic, nsteps, fp,
                        (float)qmin, (float)qmax, sym, clip_sym, qp, orgmm);
   else if (tensor_batch == 0)
@@ -1100,9 +1175,9 @@ static void launch_clip_pc(const void* w, const void* x, const void* qx, int64_t
 extern "C" int lcq_auto_clip_search_pc(const void* w, const void* x, const void* qx, int dtype,
                                        int64_t oc, int64_t ic, int64_t T, int nsteps,
                                        const void* factors, int qmin, int qmax, int sym,
-                                       int clip_sym, int fmt, int tensor_batch, void* workspace,
-                                       int64_t ws_bytes, void* best_max, void* best_min,
-                                       void* stream) {
+                                       int clip_sym, int fmt, int tensor_batch, int version,
+                                       void* workspace, int64_t ws_bytes, void* best_max,
+                                       void* best_min, void* stream) {
   LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16, "auto-clip: bf16 or fp16 model dtype");
   LCQ_REQUIRE(oc > 0 && ic > 0 && ic % PC_KC == 0, "per-channel auto-clip: ic % 128 == 0");
   LCQ_REQUIRE(T > 0 && nsteps >= 1 && nsteps <= PC_NS, "bad T / nsteps (<= 10)");
@@ -1110,6 +1185,8 @@ extern "C" int lcq_auto_clip_search_pc(const void* w, const void* x, const void*
               "fmt must be 0 (integer) or an fp8 format");
   LCQ_REQUIRE(tensor_batch == 0 || (fmt != 0 && tensor_batch > 0 && tensor_batch <= 256),
               "tensor_batch (per-tensor fp8 scale rows) must be 1..256, fp8 only");
+  LCQ_REQUIRE(version == 1 || (version == 2 && fmt == 0),
+              "version must be 1, or 2 (learnable clip factors) for integer weights");
   if (fmt != 0) {  // FloatQuantizer: symmetric, qmax = finfo.max
     qmax = fmt == LCQ_FP8E4M3 ? 448 : 57344;
     qmin = -qmax;
@@ -1123,9 +1200,9 @@ extern "C" int lcq_auto_clip_search_pc(const void* w, const void* x, const void*
   char* ws = reinterpret_cast<char*>(workspace);
   if (dtype == LCQ_BF16)
     launch_clip_pc<LCQ_BF16>(w, x, qx, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym,
-                             fmt, tensor_batch, ws, best_max, best_min, st);
+                             fmt, tensor_batch, version, ws, best_max, best_min, st);
   else
     launch_clip_pc<LCQ_F16>(w, x, qx, oc, ic, T, nsteps, factors, qmin, qmax, sym, clip_sym,
-                            fmt, tensor_batch, ws, best_max, best_min, st);
+                            fmt, tensor_batch, version, ws, best_max, best_min, st);
   return check_launch("lcq_auto_clip_search_pc");
 }

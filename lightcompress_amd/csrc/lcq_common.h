@@ -108,6 +108,35 @@ __device__ __forceinline__ void qparams_f32(float mn, float mx, float qmin, floa
   qparams_ct<LCQ_F32>(mn, mx, qmin, qmax, sym, s, z);
 }
 
+// Learnable clip range (clip_version v2): torch.nn.Sigmoid, auto_clip.py:41 logit
+// log(x / (1 - x)) and quant.py:205-219 get_learnable_range, every tensor op rounded to CT as
+// the reference's CT tensors are. Sigmoid and log evaluate in fp32 and round once, like
+// torch-CPU's reduced-float kernels; expf / logf and torch-CPU's vectorised exp / log may
+// differ in the last fp32 ulp, which moves the CT result only at a rounding tie.
+template <int CT>
+__device__ __forceinline__ float sigmoid_ct(float f) {
+  return rnd<CT>(1.0f / (1.0f + expf(-f)));
+}
+template <int CT>
+__device__ __forceinline__ float logit_ct(float x) {
+  return rnd<CT>(logf(rnd<CT>(x / rnd<CT>(1.0f - x))));
+}
+// (mn, mx): the group's min / max on entry, the learnable range on exit. sym: only the upper
+// factor is used; asym: both, and the range is left alone without a lower factor.
+template <int CT>
+__device__ __forceinline__ void learnable_range(float& mn, float& mx, float up, float low,
+                                                bool has_low, int sym) {
+  if (sym) {
+    float am = fmaxf(fmaxf(fabsf(mx), fabsf(mn)), rnd<CT>(1e-5f));  // .clamp(min=1e-5)
+    am = rnd<CT>(sigmoid_ct<CT>(up) * am);
+    mn = -am;
+    mx = am;
+  } else if (has_low) {
+    mn = rnd<CT>(sigmoid_ct<CT>(low) * mn);
+    mx = rnd<CT>(sigmoid_ct<CT>(up) * mx);
+  }
+}
+
 // load/store one element of dtype DT as float
 template <int DT>
 __device__ __forceinline__ float ld1(const void* p, int64_t i) {

@@ -37,7 +37,17 @@ struct QuantArgs {
   void* z_out;
   int qp_scalar;  // static: one fp32 scale / zero used at full precision (0-dim CPU operands)
   int nozp;       // static: round_zp False (quant.py:701-707): round(x / s.clamp_min(1e-9) + z)
+  const void* up;   // dynamic, calib_algo learnable: [ngroups] clip factors (x dtype)
+  const void* low;  // nullable
 };
+
+// calib_algo learnable: the group's range through get_learnable_range (quant.py:205-219)
+template <int CT>
+__device__ __forceinline__ void learnable(const QuantArgs& a, int64_t gi, float& mn, float& mx) {
+  if (a.up)
+    learnable_range<CT>(mn, mx, ld1<CT>(a.up, gi), a.low ? ld1<CT>(a.low, gi) : 0.f,
+                        a.low != nullptr, a.sym);
+}
 
 __device__ __forceinline__ float ld_rt(const void* p, int dt, int64_t i) {
   switch (dt) {
@@ -193,11 +203,13 @@ __global__ void __launch_bounds__(256) k_quant_dyn_lanes(QuantArgs a) {
       mn = fminf(mn, __shfl_xor(mn, m, 64));
       mx = fmaxf(mx, __shfl_xor(mx, m, 64));
     }
+    const float gmn = mn, gmx = mx;  // the group's values lie in [gmn, gmx] (mk_safe)
+    learnable<CT>(a, gi, mn, mx);
     float s, z;
     qparams_ct<CT>(mn, mx, a.qmin, a.qmax, a.sym, s, z);
     float q[8], dq[8];
     const float rs = 1.0f / s;
-    if (mk_safe(mn, mx, s, rs)) qdq8_mk<CT>(w, s, rs, z, a.qmin, a.qmax, q, dq);
+    if (mk_safe(gmn, gmx, s, rs)) qdq8_mk<CT>(w, s, rs, z, a.qmin, a.qmax, q, dq);
     else qdq8<CT>(w, s, z, a.qmin, a.qmax, q, dq);
     emit<CT>(a, e0, q, dq);
     if ((t & (L - 1)) == 0) {
@@ -239,10 +251,12 @@ __global__ void __launch_bounds__(256) k_quant_dyn_rows(QuantArgs a) {
   __syncthreads();
   mn = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
   mx = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  const float gmn = mn, gmx = mx;
+  learnable<CT>(a, gi, mn, mx);
   float s, z;
   qparams_ct<CT>(mn, mx, a.qmin, a.qmax, a.sym, s, z);
   const float rs = 1.0f / s;
-  const bool fin = mk_safe(mn, mx, s, rs);
+  const bool fin = mk_safe(gmn, gmx, s, rs);
   for (int64_t c = threadIdx.x; c < n8; c += blockDim.x) {
     float w[8], q[8], dq[8];
     load_pre_clip<CT>(a, base + c * 8, gi, w);
@@ -433,6 +447,26 @@ extern "C" int lcq_int_quant_dynamic(const void* x, int x_dtype, int64_t rows, i
     case LCQ_BF16: return launch_dyn<LCQ_BF16>(a, st);
     default: return launch_dyn<LCQ_F16>(a, st);
   }
+}
+
+extern "C" int lcq_int_quant_learnable(const void* x, int x_dtype, int64_t rows, int64_t cols,
+                                       int64_t group, const void* up, const void* low, int qmin,
+                                       int qmax, int sym, void* fq_out, int fq_dtype,
+                                       void* codes_out, int codes_dtype, void* scales_out,
+                                       void* zeros_out, void* stream) {
+  int rc = common_checks("lcq_int_quant_learnable", x_dtype, rows, cols, group, qmin, qmax,
+                         fq_out, fq_dtype, codes_out, codes_dtype, nullptr, 0);
+  if (rc) return rc;
+  LCQ_REQUIRE(x_dtype == LCQ_BF16 || x_dtype == LCQ_F16, "learnable: bf16 / fp16 tensors");
+  LCQ_REQUIRE(up != nullptr, "up factors required");
+  QuantArgs a{};
+  a.x = x; a.up = up; a.low = sym ? nullptr : low;
+  a.rows = rows; a.cols = cols; a.group = group;
+  a.qmin = (float)qmin; a.qmax = (float)qmax; a.sym = sym;
+  a.fq = fq_out; a.fq_dt = fq_dtype; a.codes = codes_out; a.codes_dt = codes_dtype;
+  a.s_out = scales_out; a.z_out = zeros_out;
+  hipStream_t st = as_stream(stream);
+  return x_dtype == LCQ_BF16 ? launch_dyn<LCQ_BF16>(a, st) : launch_dyn<LCQ_F16>(a, st);
 }
 
 static int int_quant_static(const char* fn, int nozp, const void* x, int x_dtype, int64_t rows,

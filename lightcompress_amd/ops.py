@@ -502,13 +502,18 @@ def sq_diff_mean(a: torch.Tensor, b: torch.Tensor) -> float:
 
 def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, n_grid: int,
                      qmin: int, qmax: int, sym: bool, clip_sym: bool, mse=None,
-                     qx: torch.Tensor | None = None, fp8=None, tensor_batch: int = 0):
-    """AutoClipper.auto_clip_layer (v1) on device: returns (best_max, best_min) [oc, ng, 1].
+                     qx: torch.Tensor | None = None, fp8=None, tensor_batch: int = 0,
+                     version: int = 1):
+    """AutoClipper.auto_clip_layer on device: returns (best_max, best_min) [oc, ng, 1].
     mse = (steps, grid, norm): the weight quantizer's calib_algo is mse. qx: the activation
     fake-quant of x (w_only False) that the shrink steps multiply with. group == ic takes the
     per_channel kernel (lcq_auto_clip_search_pc). fp8 (a float8 dtype): FloatQuantizer weights,
-    per_channel (tensor_batch 0) or per_tensor over batches of tensor_batch rows (group == ic)."""
+    per_channel (tensor_batch 0) or per_tensor over batches of tensor_batch rows (group == ic).
+    version 2: clip_version v2 candidates (learnable range of the unclamped weight), integer
+    per_channel weights only."""
     oc, ic = w.shape
+    if version == 2 and (group != ic or fp8 is not None or mse is not None):
+        raise NotImplementedError('clip_version v2 on the device: integer per_channel, minmax')
     if qx is not None and (qx.shape != x.shape or qx.dtype != x.dtype):
         raise ValueError('auto-clip: qx must match x in shape and dtype')
     if fp8 is not None and (group != ic or mse is not None):
@@ -517,7 +522,10 @@ def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, 
         if mse is not None:
             raise NotImplementedError('per_channel auto-clip with calib_algo mse')
         return _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym,
-                                    fp8=fp8, tensor_batch=tensor_batch)
+                                    fp8=fp8, tensor_batch=tensor_batch, version=version)
+    if version == 2:
+        return _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym,
+                                    version=2)
     T = x.shape[0]
     factors = torch.tensor([float(1 - i / n_grid) for i in range(nsteps)], dtype=torch.float32,
                            device=w.device)
@@ -539,7 +547,7 @@ def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, 
 
 
 def _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym, fp8=None,
-                         tensor_batch=0):
+                         tensor_batch=0, version=1):
     """per_channel weights: best bounds [oc, 1, 1] (auto_clip.py:96-99, group = ic)."""
     oc, ic = w.shape
     T = x.shape[0]
@@ -554,7 +562,7 @@ def _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym, fp
     N.call('lcq_auto_clip_search_pc', N.ptr(w.contiguous()), N.ptr(x.contiguous()),
            N.ptr(qx.contiguous() if qx is not None else None), N.dt(w), oc, ic, T, int(nsteps),
            N.ptr(factors), int(qmin), int(qmax), int(sym), int(clip_sym),
-           0 if fp8 is None else N.dt(fp8), int(tensor_batch), N.ptr(ws), wsb,
+           0 if fp8 is None else N.dt(fp8), int(tensor_batch), int(version), N.ptr(ws), wsb,
            N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
     return bmax, bmin
 
@@ -566,6 +574,46 @@ def clip_apply(w: torch.Tensor, group: int, cmax: torch.Tensor, cmin: torch.Tens
     N.call('lcq_clip_apply', N.ptr(w), N.dt(w), rows, cols, int(group), N.ptr(cmax.contiguous()),
            N.ptr(cmin.contiguous() if cmin is not None else None), N.ptr(o), N.stream_of(w))
     return o
+
+
+def clip_factors(w: torch.Tensor, group: int, cmax: torch.Tensor, cmin: torch.Tensor | None,
+                 clip_sym: bool):
+    """AutoClipper.get_clip_factor (auto_clip.py:235-256): (up, low | None), [groups, 1] in
+    the weight dtype, from the searched bounds and each group's own min / max."""
+    rows, cols = w.shape
+    ng = rows * cols // group
+    up = torch.empty((ng, 1), dtype=w.dtype, device=w.device)
+    low = None if clip_sym else torch.empty((ng, 1), dtype=w.dtype, device=w.device)
+    for t in (cmax, cmin):
+        if t is not None and (t.dtype != w.dtype or t.numel() != ng):
+            raise ValueError('clip bounds: one per group, in the weight dtype')
+    N.call('lcq_clip_factors', N.ptr(w.contiguous()), N.dt(w), rows, cols, int(group),
+           N.ptr(cmax.contiguous()), N.ptr(cmin.contiguous() if cmin is not None else None),
+           int(clip_sym), N.ptr(up), N.ptr(low), N.stream_of(w))
+    return up, low
+
+
+def int_quant_learnable(x: torch.Tensor, group: int, up: torch.Tensor, low: torch.Tensor | None,
+                        qmin: int, qmax: int, sym: bool, *, fq_dtype=None, qparams=False):
+    """Dynamic fake quant with calib_algo learnable and clip factors (quant.py:205-219):
+    returns {'fq', ['scales', 'zeros']} like int_quant_dynamic."""
+    rows, cols = x.shape
+    ng = rows * cols // group
+    for t in (up, low):
+        if t is not None and (t.dtype != x.dtype or t.numel() != ng):
+            raise ValueError('clip factors: one per group, in the tensor dtype')
+    fq_dtype = fq_dtype or x.dtype
+    res = {'fq': torch.empty((rows, cols), dtype=fq_dtype, device=x.device)}
+    s_t = z_t = None
+    if qparams:
+        s_t = res['scales'] = torch.empty((ng, 1), dtype=x.dtype, device=x.device)
+        if not sym:
+            z_t = res['zeros'] = torch.empty((ng, 1), dtype=x.dtype, device=x.device)
+    N.call('lcq_int_quant_learnable', N.ptr(x), N.dt(x), rows, cols, int(group),
+           N.ptr(up.contiguous()), N.ptr(low.contiguous() if low is not None else None),
+           int(qmin), int(qmax), int(sym), N.ptr(res['fq']), N.dt(fq_dtype), None, 0,
+           N.ptr(s_t), N.ptr(z_t), N.stream_of(x))
+    return res
 
 
 code_dtype = _code_dtype

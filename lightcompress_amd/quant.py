@@ -11,9 +11,10 @@ granularity per_group / per_channel / per_token / per_tensor / per_head (+ per_b
 round_zp=True, bit 2..8, dynamic and static qparams, fake quant, real quant (+ vLLM / AutoAWQ
 packing in ``module_utils``); FP8 e4m3 / e5m2 (``FloatQuantizer``); static per-tensor activation
 calibration (static_minmax / static_moving_minmax / static_hist). Not yet supported (raise
-NotImplementedError): learnable calibration, ``int_indices`` mixed precision, STE rounding,
-``rounding`` overrides. calib_algo mse and hqq (the proximal search, ``lcq_hqq_proximal``) and
-round_zp False run on the device.
+NotImplementedError): ``int_indices`` mixed precision, STE rounding, ``rounding`` overrides.
+calib_algo mse and hqq (the proximal search, ``lcq_hqq_proximal``), round_zp False and
+learnable (min/max without clip factors; with the v2 clip factors of AutoClipper the range of
+get_learnable_range, ``lcq_int_quant_learnable``) run on the device.
 """
 from __future__ import annotations
 
@@ -41,8 +42,8 @@ def weight_cast_to_fp8(weight, block_size):
 
 
 # get_tensor_range (quant.py:122-130) falls back to min/max for the static_* algorithms, which
-# only change get_batch_tensors_qparams
-_MINMAX_LIKE = ('minmax', 'static_minmax', 'static_moving_minmax', 'static_hist')
+# only change get_batch_tensors_qparams, and learnable is min/max until clip factors are given
+_MINMAX_LIKE = ('minmax', 'static_minmax', 'static_moving_minmax', 'static_hist', 'learnable')
 
 
 class BaseQuantizer:
@@ -140,8 +141,20 @@ class BaseQuantizer:
         for k in ('int_indices', 'rounding'):
             if k in args:
                 raise NotImplementedError(f'args[{k!r}] is not on the device path')
-        if args.get('lowbound_factor') is not None or args.get('upbound_factor') is not None:
-            raise NotImplementedError('learnable clip factors (clip v2) are not on the device path')
+        if self._factors(args) is not None and (
+                getattr(self, 'quant_type', 'int-quant') != 'int-quant' or not self.round_zp):
+            raise NotImplementedError('learnable clip factors: integer quantizers, round_zp')
+
+    def _factors(self, args):
+        """(up, low | None): the clip factors get_learnable_range applies (quant.py:127-128,
+        205-219), or None. Only calib_algo learnable reads them; sym needs the upper factor,
+        asym both (one missing leaves the min/max range)."""
+        if self.calib_algo != 'learnable' or not args:
+            return None
+        up, low = args.get('upbound_factor'), args.get('lowbound_factor')
+        if up is None or (not self.sym and low is None):
+            return None
+        return up, (None if self.sym else low)
 
     # -- API helpers kept for signature parity (quant.py:132-143, 545-559) -----------------
     def get_minmax_range(self, tensor):
@@ -152,7 +165,23 @@ class BaseQuantizer:
     def get_tensor_range(self, tensor, args={}):
         if self.calib_algo == 'mse':
             return self.get_mse_range(tensor)
+        if self.calib_algo == 'learnable':
+            return self.get_learnable_range(tensor, **args)
         return self.get_minmax_range(tensor)
+
+    def get_learnable_range(self, tensor, lowbound_factor=None, upbound_factor=None):
+        """quant.py:205-219 (tiny tensors; kept for API parity -- the fake quant fuses it in
+        lcq_int_quant_learnable)."""
+        mn, mx = self.get_minmax_range(tensor)
+        if self.sym:
+            if upbound_factor is not None:
+                am = torch.max(mx.abs(), mn.abs()).clamp(min=1e-5)
+                am = torch.sigmoid(upbound_factor) * am
+                mn, mx = -am, am
+        elif upbound_factor is not None and lowbound_factor is not None:
+            mn = torch.sigmoid(lowbound_factor) * mn
+            mx = torch.sigmoid(upbound_factor) * mx
+        return mn, mx
 
     def _mse_nsteps(self):
         return int(self.maxshrink * self.mse_grid)
@@ -306,6 +335,14 @@ class IntegerQuantizer(BaseQuantizer):
     def get_tensor_qparams(self, tensor, args={}):
         """quant.py:690-697: (reshaped tensor, scales, zeros, qmax, qmin)."""
         self._check_supported(args)
+        f = self._factors(args)
+        if f is not None:
+            x2, group = self._kernel_view(tensor.contiguous())
+            r = self._learnable(x2, group, f, tensor.dtype, qparams=True)
+            dev = tensor.device
+            zeros = r['zeros'] if not self.sym else torch.tensor(0.0)
+            return (self.reshape_tensor(tensor), r['scales'], zeros, self.qmax.to(dev),
+                    self.qmin.to(dev))
         if self.calib_algo == 'hqq':
             return self.get_hqq_qparams(tensor, args)
         if not self.round_zp and self.calib_algo != 'mse':
@@ -334,6 +371,15 @@ class IntegerQuantizer(BaseQuantizer):
             scales = scales.reshape(())
             zeros = zeros.reshape(()) if not self.sym else zeros
         return (self.reshape_tensor(tensor), scales, zeros, self.qmax.to(dev), self.qmin.to(dev))
+
+    def _learnable(self, x2, group, f, dtype, qparams=False):
+        up, low = f
+        for t in (up, low):
+            if t is not None and t.dtype != x2.dtype:
+                raise NotImplementedError('clip factors in a dtype other than the weight\'s')
+        qmin, qmax = self._iq
+        return ops.int_quant_learnable(x2, group, up, low, qmin, qmax, self.sym, fq_dtype=dtype,
+                                       qparams=qparams)
 
     # -- elementwise ops with given qparams (quant.py:699-717) ------------------------------
     def _static(self, tensor, scales, zeros, want):
@@ -400,6 +446,11 @@ class IntegerQuantizer(BaseQuantizer):
         w = weight.T if tr else weight
         shape = w.shape
         qmin, qmax = self._iq
+        f = self._factors(args)
+        if f is not None:  # calib_algo learnable with the v2 clip factors (w_qdq)
+            x2, group = self._kernel_view(w.contiguous())
+            fq = self._learnable(x2, group, f, w.dtype)['fq'].reshape(shape)
+            return fq.T if tr else fq
         if self.calib_algo == 'mse':  # fp32 scales -> the quant_dequant computes in fp32
             x2, group, s, z = self._mse(w)
             fq = ops.int_quant_static(x2, group, s, z, qmin, qmax, ct_dtype=torch.float32,
