@@ -103,15 +103,32 @@ def _fq_fp8(cur: torch.Tensor, fmt: str, per_tensor: bool):
     return P.qdq_given(cur, s, fmt).to(cur.dtype)
 
 
+def logit(x):
+    """auto_clip.py:41."""
+    return torch.log(x / (1 - x))
+
+
+def _fq_v2(wb, min_val, max_val, org_min, org_max, bit, sym):
+    """auto_clip.py:258-267 (clip_version v2): the unclamped weights' static fake quant with
+    the qparams of get_learnable_range(w, logit(min/org_min), logit(max/org_max))."""
+    low = logit(min_val / org_min)
+    up = logit(max_val / org_max)
+    mn, mx = Q.learnable_range(wb, low, up, sym)
+    qmin, qmax = Q.int_range(bit, sym)
+    s, z = Q.qparams(mn, mx, qmin, qmax, sym)
+    return Q.dequant(Q.quant(wb, s, z, qmin, qmax), s, z).to(wb.dtype)
+
+
 def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_grid=20,
-               max_shrink=0.5, n_sample_token=512, mse=False, act=None, fp8=None):
+               max_shrink=0.5, n_sample_token=512, mse=False, act=None, fp8=None, version=1):
     """auto_clip.py:83-191 (clip v1, single input). Returns (best_max, best_min) shaped
     [oc, ng, 1]. mse=True: the weight quantizer's calib_algo is mse. group = ic is the
     per_channel case (auto_clip.py:96-99). act = (bits, sym): w_only False, the shrink steps
     see fake_quantize_input(x) = per_token fake quant of the [1, T, ng, group] view
     (auto_clip.py:176-177, 269-274; quant.py:754-771 with reshape_tensor's per_token no-op).
     fp8 = (fmt, per_tensor, act_quant | None): FloatQuantizer weights (group = ic); act_quant is
-    a function giving fake_quantize_input(x) for w_only False."""
+    a function giving fake_quantize_input(x) for w_only False. version 2: clip_version v2
+    candidates (_fq_v2, integer weights)."""
     w = w.reshape(w.shape[0], 1, -1, group)
     ocb = 256 if w.shape[0] % 256 == 0 else 64
     x = x.view(-1, x.shape[-1]).reshape(1, -1, x.shape[-1] // group, group)
@@ -132,7 +149,9 @@ def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_gr
             max_val = org_max * (1 - i_s / n_grid)
             min_val = -max_val if clip_sym else org_min * (1 - i_s / n_grid)
             cur = torch.clamp(wb, min_val, max_val)
-            if fp8 is not None:
+            if version == 2:
+                q_w = _fq_v2(wb, min_val, max_val, org_min, org_max, bit, sym)
+            elif fp8 is not None:
                 q_w = _fq_fp8(cur, fp8[0], fp8[1])
             else:
                 q_w = (_fq_mse(cur, bit, sym, group) if mse else
@@ -148,6 +167,18 @@ def clip_layer(w: torch.Tensor, x: torch.Tensor, bit, sym, group, clip_sym, n_gr
         bmx_all.append(best_max)
         bmn_all.append(best_min)
     return torch.cat(bmx_all, 0).squeeze(1), torch.cat(bmn_all, 0).squeeze(1)
+
+
+def clip_factors(w: torch.Tensor, max_val, min_val, clip_sym, group):
+    """auto_clip.py:235-256 get_clip_factor: (up, low | None) [groups, 1]."""
+    mn, mx = Q.minmax(Q.group_view(w, 'per_group', group))
+    shape = mx.shape
+    if clip_sym:
+        am = torch.max(mx.abs(), mn.abs()).clamp(min=1e-5).reshape(*max_val.shape[:2], -1)
+        return logit(max_val / am).reshape(shape), None
+    up = logit(max_val / mx.reshape(*max_val.shape[:2], -1)).reshape(shape)
+    low = logit(min_val / mn.reshape(*min_val.shape[:2], -1)).reshape(shape)
+    return up, low
 
 
 def apply_clip(w: torch.Tensor, max_val, min_val, clip_sym):

@@ -85,6 +85,31 @@ def fake_quant_dynamic(w, bit, sym, granularity='per_group', group=128, pre_scal
     return out.reshape(shape).to(dtype), s, z
 
 
+def learnable_range(t, low, up, sym: bool):
+    """quant.py:205-219 get_learnable_range (torch.nn.Sigmoid factors of the group range)."""
+    mn, mx = minmax(t)
+    if sym:
+        if up is not None:
+            am = torch.max(mx.abs(), mn.abs()).clamp(min=1e-5)
+            am = torch.sigmoid(up) * am
+            mn, mx = -am, am
+    elif up is not None and low is not None:
+        mn = torch.sigmoid(low) * mn
+        mx = torch.sigmoid(up) * mx
+    return mn, mx
+
+
+def fake_quant_learnable(w, bit, sym, granularity='per_group', group=128, low=None, up=None):
+    """fake_quant_weight_dynamic with calib_algo learnable and clip factors (quant.py:127-128,
+    205-219, 833-869): the group ranges of get_learnable_range."""
+    qmin, qmax = int_range(bit, sym)
+    shape, dtype = w.shape, w.dtype
+    t = group_view(w, granularity, group)
+    mn, mx = learnable_range(t, low, up, sym)
+    s, z = qparams(mn, mx, qmin, qmax, sym)
+    return dequant(quant(t, s, z, qmin, qmax), s, z).reshape(shape).to(dtype)
+
+
 def code_dtype(bit, qmin):
     """quant.py:890-896."""
     if bit == 8:

@@ -853,6 +853,52 @@ def gen_fp8_algos():
 GENERATORS['fp8_algos'] = gen_fp8_algos
 
 
+def gen_clip_v2():
+    """clip_version v2 (awq_comb_omni w6a6 / w8a8 step_1_awq.yml): the reference's
+    AutoClipper.auto_clip_layer with learnable-range candidates, apply_clip's logit factors
+    (get_clip_factor) and the deploy fake quant with those factors
+    (fake_quant_weight_dynamic with calib_algo learnable). Prefix clipv2_."""
+    R.init_dist()
+    q = R.quant_module()
+    import llmc.compression.quantization.auto_clip as ac
+    bf, hf = torch.bfloat16, torch.float16
+    # (name, wbit, wsym, clip_sym, act (bit, sym) or None, oc, ic, dtype)
+    cases = [('w8a8_asym', 8, False, False, (8, False), 256, 512, bf),
+             ('w6a6_asym', 6, False, False, (6, False), 256, 384, bf),
+             ('w4_asym_wonly', 4, False, False, None, 128, 256, bf),
+             ('w4_sym', 4, True, True, None, 128, 512, bf),
+             ('w6a6_asym_clipsym', 6, False, True, (6, False), 128, 256, bf),
+             ('w6a8_sym_asymclip', 6, True, False, (8, True), 128, 256, bf),
+             ('w8a8_asym_f16', 8, False, False, (8, False), 128, 512, hf)]
+    for i, (name, wb, sym, clip_sym, act, oc, ic, dt) in enumerate(cases):
+        wq = q.IntegerQuantizer(wb, sym, 'per_channel', calib_algo='learnable')
+        aq = q.IntegerQuantizer(act[0], act[1], 'per_token') if act else None
+        clipper = ac.AutoClipper(w_only=act is None, wquantizer=wq, aquantizer=aq,
+                                 clip_version='v2', clip_sym=clip_sym, save_clip=True,
+                                 padding_mask=None)
+        w = weights(oc, ic, dt, 2500 + i, edge=False)
+        w[3, 5] = 0.4   # row outliers: the clip has something to cut
+        w[7, 9] = -0.3
+        x = _acts(1, 512, ic, 2600 + i, dtype=dt)[0]
+        bmax, bmin = clipper.auto_clip_layer(0, 'l', w.clone(), [x.clone()],
+                                             n_sample_token=64)
+        m = torch.nn.Linear(ic, oc, bias=False).to(dt)
+        m.weight.data = w.clone()
+        clipper.apply_clip(0, m, bmin.clone(), bmax.clone(), 'l')
+        out = dict(w=w, x=x, best_max=bmax, best_min=bmin, up=m.buf_upbound_factor.clone(),
+                   meta=torch.tensor([wb, int(sym), int(clip_sym), 64,
+                                      act[0] if act else 0, int(act[1]) if act else 0]))
+        args = {'lowbound_factor': m.buf_lowbound_factor, 'upbound_factor': m.buf_upbound_factor}
+        if m.buf_lowbound_factor is not None:
+            out['low'] = m.buf_lowbound_factor.clone()
+        out['fq'] = wq.fake_quant_weight_dynamic(w.clone(), args)
+        F.save(f'clipv2_{name}', **out)
+    print('clip v2 fixtures written')
+
+
+GENERATORS['clip_v2'] = gen_clip_v2
+
+
 if __name__ == '__main__':
     which = sys.argv[1] if len(sys.argv) > 1 else 'all'
     R.install()

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import copy
 import shutil
+import tempfile
 import sys
 import types
 from pathlib import Path
@@ -164,9 +165,16 @@ def run_reference(name, spec):
         import llmc.compression.quantization.rtn as mod
         algo_cls = mod.RTN
     dtype = 'torch.float16' if family == 'Opt' else 'torch.bfloat16'
+    quant = copy.deepcopy(spec['quant'])
+    sp = quant.get('special', {})
+    tmp = tempfile.mkdtemp()
+    if sp.get('save_scale'):
+        sp['scale_path'] = f'{tmp}/scale'
+    if sp.get('save_clip'):
+        sp['clip_path'] = f'{tmp}/clip'
     config = ED({'model': {'type': family, 'path': str(TM.MODEL_DIRS[family]),
                            'torch_dtype': dtype},
-                 'quant': dict(copy.deepcopy(spec['quant']), modality='language')})
+                 'quant': dict(quant, modality='language')})
     if spec['calib']:
         config['calib'] = dict(spec['calib'])
     model = model_cls(config)
@@ -216,10 +224,25 @@ def run_reference(name, spec):
         algo.search_scale_subset = types.MethodType(snap, algo)
         algo.calculate_loss = types.MethodType(rec, algo)
     algo.run_block_loop()
+    out = {}
+    for bi, block in enumerate(model.get_blocks()):  # v2 clip factors (before the deploy)
+        for ln, lin in model.get_block_linears(block).items():
+            for k in ('upbound', 'lowbound'):
+                f = getattr(lin, f'buf_{k}_factor', None)
+                if f is not None:
+                    out[f'{k[:2]}_b{bi}__{ln.replace(".", "__")}'] = f.detach().cpu().clone()
+    if sp.get('save_scale'):  # files our own run wrote: plain tensors, weights_only loads
+        for k, v in torch.load(f'{tmp}/scale/scales.pth', weights_only=True).items():
+            out[f'sc__{k.replace(".", "__")}'] = v.cpu()
+    if sp.get('save_clip'):
+        for bi, d in torch.load(f'{tmp}/clip/clips.pth', weights_only=True).items():
+            for k, v in d.items():
+                if v is not None:
+                    out[f'cl{bi}__{k.replace(".", "__")}'] = v
     algo.deploy('fake_quant')
     if diag:
         F.save(f'pipe_{name}_diag', **diag)
-    out = {'ids': ids if ids is not None else torch.zeros(0, dtype=torch.int64)}
+    out['ids'] = ids if ids is not None else torch.zeros(0, dtype=torch.int64)
     for bi, block in enumerate(model.get_blocks()):
         for ln, lin in model.get_block_linears(block).items():
             out[f'b{bi}__{ln.replace(".", "__")}'] = lin.weight.data.clone()

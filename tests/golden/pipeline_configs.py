@@ -165,4 +165,30 @@ CONFIGS = {
                                        'true_sequential': True},
                            'quant_out': True},
                  'calib': {'bs': 1, 'n_samples': 16, 'seq_len': 128}, 'qtorch_native': True},
+    # ---- clip_version v2 (learnable clip factors) -------------------------------------------
+    # configs/quantization/combination/awq_comb_omni/{w8a8,w6a6}/step_1_awq.yml: asym
+    # per_channel weights with calib_algo learnable, asym per_token activations, the clip
+    # searched with learnable-range candidates and kept as logit factors (buf_*bound_factor)
+    # that the deploy fake quant applies; scales.pth / clips.pth written (paths filled in by
+    # the generator and the test)
+    'awq_omni_w8a8': {'quant': {'method': 'Awq',
+                                'weight': {'bit': 8, 'symmetric': False,
+                                           'granularity': 'per_channel', 'group_size': -1,
+                                           'calib_algo': 'learnable'},
+                                'act': {'bit': 8, 'symmetric': False,
+                                        'granularity': 'per_token', 'calib_algo': 'minmax'},
+                                'special': {'trans': True, 'trans_version': 'v2',
+                                            'weight_clip': True, 'clip_version': 'v2',
+                                            'save_scale': True, 'save_clip': True}},
+                      'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}},
+    'awq_omni_w6a6': {'quant': {'method': 'Awq',
+                                'weight': {'bit': 6, 'symmetric': False,
+                                           'granularity': 'per_channel', 'group_size': -1,
+                                           'calib_algo': 'learnable'},
+                                'act': {'bit': 6, 'symmetric': False,
+                                        'granularity': 'per_token', 'calib_algo': 'minmax'},
+                                'special': {'trans': True, 'trans_version': 'v2',
+                                            'weight_clip': True, 'clip_version': 'v2',
+                                            'save_scale': True, 'save_clip': True}},
+                      'calib': {'bs': -1, 'n_samples': 16, 'seq_len': 128}},
 }

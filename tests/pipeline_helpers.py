@@ -2,7 +2,12 @@
 tests/golden/gen_pipeline.py ran the reference's: the same tiny model files, the same
 calibration token ids through our Catcher, run_block_loop + deploy('fake_quant'). Returns the
 reference's fixture, our deployed weights and our diagnostics (GPTQ Hessians, AWQ loss curves
-and chosen scales, static act scales) under the fixture's key names."""
+and chosen scales, static act scales, v2 clip factors, saved scales.pth / clips.pth) under the
+fixture's key names."""
+import copy
+import shutil
+import tempfile
+
 import torch
 
 import fixtures as F
@@ -47,9 +52,15 @@ def run_ours(name, dev, monkeypatch=None, config_override=None):
             return best
         monkeypatch.setattr(Awq, 'search_scale_subset', ss)
     dtype = 'float16' if family == 'Opt' else 'bfloat16'
-    quant = dict(spec['quant'])
+    quant = copy.deepcopy(spec['quant'])
     if config_override:
         quant = config_override(quant)
+    sp = quant.get('special', {})
+    tmp = tempfile.mkdtemp()
+    if sp.get('save_scale'):
+        sp['scale_path'] = f'{tmp}/scale'
+    if sp.get('save_clip'):
+        sp['clip_path'] = f'{tmp}/clip'
     cfg = {'model': {'type': family, 'path': str(TM.MODEL_DIRS[family]), 'torch_dtype': dtype},
            'quant': quant}
     if spec['calib']:
@@ -66,6 +77,21 @@ def run_ours(name, dev, monkeypatch=None, config_override=None):
         first = model.collect_first_block_input(batches)
     algo = build_algo(model, config, first)
     algo.run_block_loop()
+    for bi, block in enumerate(model.get_blocks()):  # v2 clip factors, before the deploy
+        for ln, lin in model.get_block_linears(block).items():
+            for k in ('upbound', 'lowbound'):
+                f = getattr(lin, f'buf_{k}_factor', None)
+                if f is not None:
+                    diag[f'{k[:2]}_b{bi}__{ln.replace(".", "__")}'] = f.detach().cpu().clone()
+    if sp.get('save_scale'):
+        for k, v in torch.load(f'{tmp}/scale/scales.pth', weights_only=True).items():
+            diag[f'sc__{k.replace(".", "__")}'] = v.cpu()
+    if sp.get('save_clip'):
+        for bi, d in torch.load(f'{tmp}/clip/clips.pth', weights_only=True).items():
+            for k, v in d.items():
+                if v is not None:
+                    diag[f'cl{bi}__{k.replace(".", "__")}'] = v
+    shutil.rmtree(tmp, ignore_errors=True)
     algo.deploy('fake_quant')
     got = {}
     for bi, block in enumerate(model.get_blocks()):

@@ -257,3 +257,56 @@ def test_gptq_fp8_pipeline_vs_reference(dev, monkeypatch):
             assert rel < 5e-2, k
     for k, eq in res.items():
         assert eq >= 0.7, (k, eq)
+
+
+@pytest.mark.parametrize('name', ['awq_omni_w8a8', 'awq_omni_w6a6'])
+def test_awq_clip_v2_pipeline_vs_reference(dev, name, monkeypatch):
+    """combination/awq_comb_omni/{w8a8,w6a6}/step_1_awq.yml (asym per_channel weights with
+    calib_algo learnable, asym per_token acts, clip_version v2, save_scale / save_clip): the
+    clip keeps the weights and registers logit factors that the deployed fake quant applies
+    (get_learnable_range). Block 0's q / k projections deploy bit-equal (identical inputs, no
+    clip); block-0 loss curves within 3e-3 with the same argmin (the per_token act quant turns
+    a last-bit forward difference into a whole step now and then), later curves near-tie only.
+    Clip factors: the per-channel clip sums ic-long rows in k order (T2), so a row on a near
+    tie may take the neighbouring bound, and every clipped linear's input already went through
+    a GPU forward (attention, SiLU * up) -> factors equal on >= 93 % of the rows of every
+    linear (measured >= 95.7 %), deployed weights >= 90 % bit-equal. scales.pth holds the
+    chosen scales of every searched linear under the reference's names (block 0's equal to
+    the bit), clips.pth exactly the registered factors."""
+    ref, got, diag = run_ours(name, dev, monkeypatch)
+    res = compare(ref, got)
+    for k in ('b0__self_attn__q_proj', 'b0__self_attn__k_proj'):
+        assert res[k] == 1.0, k
+    rdiag = F.load(f'pipe_{name}_diag')
+    for k in sorted(k for k in rdiag if k.startswith('L_')):
+        r, o = rdiag[k], diag[k]
+        rel = ((o - r).abs() / r.abs()).max().item()
+        ri, oi = int(r.argmin()), int(o.argmin())
+        print(f'{k}: max rel loss diff {rel:.2e}, argmin ref {ri} ours {oi}')
+        if k.startswith('L_b0'):
+            assert rel < 3e-3 and ri == oi, k
+        else:
+            assert rel < 1e-2, k
+            assert ri == oi or r[oi].item() <= r[ri].item() * 1.002, k
+    for k, eq in res.items():
+        assert eq >= 0.9, (k, eq)
+    fkeys = sorted(k for k in ref if k[:3] in ('up_', 'lo_'))
+    assert fkeys and fkeys == sorted(k for k in diag if k[:3] in ('up_', 'lo_'))
+    for k in fkeys:
+        r, o = ref[k], diag[k]
+        assert r.dtype == o.dtype and r.shape == o.shape, k
+        eq = (r.view(torch.int16) == o.view(torch.int16)).float().mean().item()
+        print(f'{k:32s} factors equal {eq * 100:.2f} %')
+        assert eq >= 0.93, (k, eq)
+    skeys = sorted(k for k in ref if k.startswith('sc__'))
+    assert skeys and skeys == sorted(k for k in diag if k.startswith('sc__'))
+    for k in skeys:
+        if '__0__' in k:
+            assert torch.equal(ref[k].view(torch.int16), diag[k].view(torch.int16)), k
+    ckeys = sorted(k for k in ref if k.startswith('cl'))
+    assert ckeys == sorted(k for k in diag if k.startswith('cl'))
+    for k in ckeys:  # clips.pth: the registered buffers themselves
+        b, rest = k[2:].split('__', 1)
+        lin, kind = rest.split('__weight_quantizer__')
+        fk = f'{kind[:2]}_b{b}__{lin}'
+        assert torch.equal(diag[k].view(torch.int16), diag[fk].view(torch.int16)), k
