@@ -484,13 +484,19 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         if self.data_free:
             return []
         self._hooked_names = list(modules)
-        handles = [m.register_forward_hook(functools.partial(self._capture_hook, name=n,
-                                                             feat_dict=input_feat))
-                   for n, m in modules.items()]
+        hooks = {n: functools.partial(self._capture_hook, name=n, feat_dict=input_feat)
+                 for n in modules}
+        pre = {}
         if not self.hook_needs_output:
-            handles += [m.register_forward_pre_hook(functools.partial(
-                self._capture_pre_hook, name=n, feat_dict=input_feat))
-                for n, m in modules.items()]
+            pre = {n: functools.partial(self._capture_pre_hook, name=n, feat_dict=input_feat)
+                   for n in modules}
+            # the capture reads only the module inputs: a fused forward may fire these hooks
+            # itself with out=None and skip materialising the module outputs
+            # (llama._gate_up_silu: the GPTQ calibration forward's gate / up projections)
+            for h in (*hooks.values(), *pre.values()):
+                h._lcq_input_only = True
+        handles = [m.register_forward_hook(hooks[n]) for n, m in modules.items()]
+        handles += [m.register_forward_pre_hook(pre[n]) for n, m in modules.items() if n in pre]
         return handles
 
     def run(self, block, input_feat, handles):

@@ -258,8 +258,7 @@ __global__ void __launch_bounds__(64) k_sqdiff_p2(const double* part, int nparts
 // sums (k mod 8) reduced by a halving tree (torch-CPU's vectorised order), the per-step
 // squared-error sums and the original outputs sit in LDS so the token loop stays rolled.
 // ----------------------------------------------------------------------------------------
-constexpr int CROWS = 128;     // rows per workgroup (2 lanes per row -> 256 threads)
-constexpr int CT = 32;         // sampled tokens per LDS tile (64 measured 5 % slower)
+constexpr int CROWS = 128;     // lane pairs per workgroup (2 lanes per row -> 256 threads)
 constexpr int CMAXSTEPS = 16;
 constexpr int CGMAX = 256;     // largest group (xs tile = CT x G fp32)
 
@@ -294,9 +293,9 @@ __device__ __forceinline__ float dtr(float f) {
   }
 }
 
-// products of a pair rounded to DT and widened back to fp32. bf16, CVT2: one
-// v_cvt_pk_bf16_f32 per product with a zero low half, so the result register IS the widened
-// fp32 value (2 VALU per pair instead of convert + shift + mask: 3)
+// products of a pair rounded to DT and widened back to fp32. bf16: one v_cvt_pk_bf16_f32 per
+// product with a zero low half, so the result register IS the widened fp32 value (2 VALU per
+// pair instead of convert + shift + mask: 3)
 template <int DT, bool CVT2 = true>
 __device__ __forceinline__ v2f dtr2(v2f p) {
   if constexpr (DT == LCQ_BF16 && CVT2) {
@@ -330,32 +329,48 @@ __device__ __forceinline__ void widen4(uint2 v, float* q) {
 }
 
 __device__ __forceinline__ float xor1(float v) {  // value of the partner lane (lane ^ 1)
-  return __shfl_xor(v, 1, 64);
+  // DPP quad_perm [1, 0, 3, 2]: a VALU operand modifier, no LDS round trip (ds_bpermute)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0xB1, 0xF, 0xF, true));
 }
 
-// sum_k DT(x[k] * q[k]) over one G-wide group, split over a lane pair: this lane owns
-// k = 8i + 4h + j (j = 0..3) i.e. partial sums acc_{4h+j} of the 8-way (k mod 8) order that
-// torch-CPU's vectorised reduction uses for every group size and for bf16 and fp16 alike; the
-// pair exchange forms l_j = acc_j + acc_{j+4} and both lanes finish the halving tree.
-template <int DT, int G, bool CVT2 = true>
-__device__ __forceinline__ float dot_row(const float* __restrict__ xr, const float (&q)[G / 2],
-                                         int h) {
-  v2f a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+// sum_k DT(x[k] * q[k]) over one G-wide group for each of this lane's R rows, split over a
+// lane pair: this lane owns k = 8i + 4h + j (j = 0..3) i.e. partial sums acc_{4h+j} of the
+// 8-way (k mod 8) order that torch-CPU's vectorised reduction uses for every group size and for
+// bf16 and fp16 alike; the pair exchange forms l_j = acc_j + acc_{j+4} and both lanes finish
+// the halving tree. One broadcast LDS read of x feeds R rows (R = 2: the ds_read_b128 per 8
+// products of R = 1 kept the LDS array busy every cycle; at 2 it is half busy, VALU-bound).
+template <int DT, int G, int R>
+__device__ __forceinline__ void dot_rows(const float* __restrict__ xr,
+                                         const float (&q)[R][G / 2], int h, float (&out)[R]) {
+  // packed fp32 products and sums (v_pk_mul_f32 / v_pk_add_f32): measured 1.26x faster than
+  // the same work as scalar v_mul_f32 / v_add_f32 (49 % more instructions)
+  v2f a0[R], a1[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) a0[j] = a1[j] = v2f{0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < G / 8; ++i) {
     const float4 xv = *reinterpret_cast<const float4*>(xr + 8 * i + 4 * h);
-    a0 += dtr2<DT, CVT2>(v2f{xv.x, xv.y} * v2f{q[4 * i], q[4 * i + 1]});
-    a1 += dtr2<DT, CVT2>(v2f{xv.z, xv.w} * v2f{q[4 * i + 2], q[4 * i + 3]});
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      a0[j] += dtr2<DT>(v2f{xv.x, xv.y} * v2f{q[j][4 * i], q[j][4 * i + 1]});
+      a1[j] += dtr2<DT>(v2f{xv.z, xv.w} * v2f{q[j][4 * i + 2], q[j][4 * i + 3]});
+    }
   }
-  // lane h=0 holds acc0..3, h=1 holds acc4..7: l_j = acc_j + acc_{j+4}. The partner values
-  // are read in uniform control flow (a cross-lane read inside a divergent branch would see
-  // inactive lanes); the operand order is then fixed with selects so both lanes agree.
-  const float p0 = xor1(a0.x), p1 = xor1(a0.y), p2 = xor1(a1.x), p3 = xor1(a1.y);
-  const float l0 = (h ? p0 : a0.x) + (h ? a0.x : p0);
-  const float l1 = (h ? p1 : a0.y) + (h ? a0.y : p1);
-  const float l2 = (h ? p2 : a1.x) + (h ? a1.x : p2);
-  const float l3 = (h ? p3 : a1.y) + (h ? a1.y : p3);
-  return dtr<DT>((l0 + l2) + (l1 + l3));
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    // lane h=0 holds acc0..3, h=1 holds acc4..7: l_j = acc_j + acc_{j+4}. The partner values
+    // are read in uniform control flow (a cross-lane read inside a divergent branch would see
+    // inactive lanes); the operand order is then fixed with selects so both lanes agree.
+    const float c[4] = {a0[j].x, a0[j].y, a1[j].x, a1[j].y};
+    float l[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float pm = xor1(c[m]);
+      l[m] = (h ? pm : c[m]) + (h ? c[m] : pm);
+    }
+    out[j] = dtr<DT>((l[0] + l[2]) + (l[1] + l[3]));
+  }
 }
 
 template <int DT, int G>
@@ -386,44 +401,76 @@ __device__ __forceinline__ void qparams_f32_mse(float mn, float mx, float qmin, 
 // quant searches its range on the clamped group in fp32 (mse_p[i] = fp32(1 - i / grid),
 // |qdq(v) - v|^norm summed, strict improvements shrink the base), then quantizes in fp32 with
 // the fp32 qparams and rounds to DT once (the DT tensor is promoted by the fp32 scales).
-template <int DT, int G, bool MSE, bool CVT2 = true>
-__global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 weights/lane
+// R rows per lane pair (R = 2 for G <= 128 without mse: 256 rows per workgroup; R = 1 for
+// G = 256, whose 128 weights per lane per row leave no room for a second row, and for mse).
+// LDS of one workgroup: x tile [CT][G] fp32, original outputs [CT][rows] as DT bits (they are
+// DT values), per-step error sums [CMAXSTEPS][rows] fp32
+template <int G, int R>
+struct ClipTile {
+  static constexpr int CT = R == 2 ? 64 : 32;  // sampled tokens per x tile
+  static constexpr int RW = CROWS * R;
+  static constexpr int bytes = CT * G * 4 + CT * RW * 2 + CMAXSTEPS * RW * 4;
+};
+
+template <int DT>
+__device__ __forceinline__ uint16_t dt_bits(float v) {  // v is a DT value
+  if constexpr (DT == LCQ_BF16) return (uint16_t)(__float_as_uint(v) >> 16);
+  else return __builtin_bit_cast(uint16_t, (_Float16)v);
+}
+template <int DT>
+__device__ __forceinline__ float dt_val(uint16_t b) {
+  if constexpr (DT == LCQ_BF16) return __uint_as_float((uint32_t)b << 16);
+  else return (float)__builtin_bit_cast(_Float16, b);
+}
+
+template <int DT, int G, int R, bool MSE>
+__global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)
     k_auto_clip(const uint16_t* __restrict__ w, const uint16_t* __restrict__ x, int64_t oc,
                 int64_t ic, int T, int nsteps, const float* __restrict__ factors, float qmin,
                 float qmax, int sym, int clip_sym, uint16_t* best_max, uint16_t* best_min,
                 int mse_steps, const float* __restrict__ mse_p, float norm,
-                const uint16_t* __restrict__ qx, int mkdiv) {
-  constexpr int CH = G / 2;    // weights per lane: k = 8i + 4h + j, h = lane parity
+                const uint16_t* __restrict__ qx) {
+  static_assert(!MSE || R == 1, "the mse search keeps one row per lane pair");
+  constexpr int CH = G / 2;    // weights per lane per row: k = 8i + 4h + j, h = lane parity
   constexpr int CHUNKS = G / 8;
-  __shared__ __attribute__((aligned(16))) float xs[CT * G];      // <= 32 KB
-  __shared__ float orgs[CT * CROWS];                              // 16 KB
-  __shared__ float es[CMAXSTEPS * CROWS];                          // 8 KB
+  constexpr int RW = CROWS * R;  // rows per workgroup
+  constexpr int CT = ClipTile<G, R>::CT;
+  extern __shared__ __attribute__((aligned(16))) float clip_lds[];
+  float* xs = clip_lds;                                                    // [CT][G]
+  uint16_t* orgs = reinterpret_cast<uint16_t*>(clip_lds + CT * G);         // [CT][RW]
+  float* es = reinterpret_cast<float*>(orgs + CT * RW);                    // [steps][RW]
   const int tid = threadIdx.x;
   const int r = tid >> 1, h = tid & 1;
-  const int64_t o = (int64_t)blockIdx.x * CROWS + r;
   const int64_t g = blockIdx.y;
   const int64_t ng = ic / G;
-  const bool live = o < oc;
-  const uint16_t* wrow = w + (live ? o : 0) * ic + g * G;
-
-  float mxs = -INFINITY, mn = INFINITY, amax = 0.f;
-  {
+  int64_t o[R];
+  bool live[R];
+  const uint16_t* wrow[R];
+  float mxs[R], mn[R], org_max[R], org_min[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    o[j] = (int64_t)blockIdx.x * RW + j * CROWS + r;
+    live[j] = o[j] < oc;
+    wrow[j] = w + (live[j] ? o[j] : 0) * ic + g * G;
     float q[CH];
-    load_half<DT, G>(wrow, h, q);
+    load_half<DT, G>(wrow[j], h, q);
+    float mx = -INFINITY, mi = INFINITY, am = 0.f;
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
-      mxs = fmaxf(mxs, q[k]);
-      mn = fminf(mn, q[k]);
-      amax = fmaxf(amax, fabsf(q[k]));
+      mx = fmaxf(mx, q[k]);
+      mi = fminf(mi, q[k]);
+      am = fmaxf(am, fabsf(q[k]));
     }
-    mxs = fmaxf(mxs, xor1(mxs));
-    mn = fminf(mn, xor1(mn));
-    amax = fmaxf(amax, xor1(amax));
+    mxs[j] = fmaxf(mx, xor1(mx));
+    mn[j] = fminf(mi, xor1(mi));
+    am = fmaxf(am, xor1(am));
+    org_max[j] = clip_sym ? am : mxs[j];
+    org_min[j] = mn[j];
   }
-  const float org_max = clip_sym ? amax : mxs;
-  const float org_min = mn;
   if (h == 0)
-    for (int s = 0; s < nsteps; ++s) es[s * CROWS + r] = 0.f;
+    for (int s = 0; s < nsteps; ++s)
+#pragma unroll
+      for (int j = 0; j < R; ++j) es[s * RW + j * CROWS + r] = 0.f;
 
   // stage CT token rows of this group as fp32, 8 elements (16 B) per chunk
   auto stage = [&](const uint16_t* __restrict__ src, int t0) {
@@ -451,93 +498,110 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)  // G 256: 128 we
         stage(qx, t0);
         __syncthreads();
       }
-      float q[CH];
-      load_half<DT, G>(wrow, h, q);
+      float q[R][CH];
+#pragma unroll
+      for (int j = 0; j < R; ++j) load_half<DT, G>(wrow[j], h, q[j]);
       if (p > 0) {
         const float f = factors[p - 1];
-        const float smax = dtr<DT>(org_max * f);
-        const float smin = clip_sym ? -smax : dtr<DT>(org_min * f);
-        const float cmn = fminf(fmaxf(mn, smin), smax);
-        const float cmx = fminf(fmaxf(mxs, smin), smax);
-        float qs, qz;
-        if constexpr (MSE) {
 #pragma unroll
-          for (int k = 0; k < CH; ++k) q[k] = fminf(fmaxf(q[k], smin), smax);
-          float rmn = cmn, rmx = cmx, best_e = INFINITY;
-          for (int i = 0; i < mse_steps; ++i) {
-            const float pp = mse_p[i];
-            const float xmn = pp * rmn, xmx = pp * rmx;
-            float s2, z2;
-            qparams_f32_mse(xmn, xmx, qmin, qmax, sym, s2, z2);
-            float err = 0.f;
+        for (int j = 0; j < R; ++j) {
+          const float smax = dtr<DT>(org_max[j] * f);
+          const float smin = clip_sym ? -smax : dtr<DT>(org_min[j] * f);
+          const float cmn = fminf(fmaxf(mn[j], smin), smax);
+          const float cmx = fminf(fmaxf(mxs[j], smin), smax);
+          float qs, qz;
+          if constexpr (MSE) {
+#pragma unroll
+            for (int k = 0; k < CH; ++k) q[j][k] = fminf(fmaxf(q[j][k], smin), smax);
+            float rmn = cmn, rmx = cmx, best_e = INFINITY;
+            for (int i = 0; i < mse_steps; ++i) {
+              const float pp = mse_p[i];
+              const float xmn = pp * rmn, xmx = pp * rmx;
+              float s2, z2;
+              qparams_f32_mse(xmn, xmx, qmin, qmax, sym, s2, z2);
+              float err = 0.f;
+#pragma unroll
+              for (int k = 0; k < CH; ++k) {
+                float qq = rintf(q[j][k] / s2) + z2;
+                qq = fminf(fmaxf(qq, qmin), qmax);
+                err += powf(fabsf((qq - z2) * s2 - q[j][k]), norm);
+              }
+              const float pe = xor1(err);
+              err = h ? pe + err : err + pe;  // same operand order on both lanes
+              if (err < best_e) {
+                best_e = err;
+                rmn = xmn;
+                rmx = xmx;
+              }
+            }
+            qparams_f32_mse(rmn, rmx, qmin, qmax, sym, qs, qz);
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
-              float qq = rintf(q[k] / s2) + z2;
-              qq = fminf(fmaxf(qq, qmin), qmax);
-              err += powf(fabsf((qq - z2) * s2 - q[k]), norm);
+              float tq = fminf(fmaxf(rintf(q[j][k] / qs) + qz, qmin), qmax);
+              q[j][k] = dtr<DT>((tq - qz) * qs);
             }
-            const float pe = xor1(err);
-            err = h ? pe + err : err + pe;  // same operand order on both lanes
-            if (err < best_e) {
-              best_e = err;
-              rmn = xmn;
-              rmx = xmx;
+          } else {
+            qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
+            const float rqs = 1.0f / qs;  // RN(1/s): qs >= DT(1e-5) / qmax, so it is normal
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+              const float v = fminf(fmaxf(q[j][k], smin), smax);
+              // correctly rounded fp32 quotient (Markstein's from RN(1/s), 3 VALU: |v / s| <=
+              // qmax + 1, normal or rounding to zero either way, as mk_safe in
+              // quant_group.hip), then rounded to DT. A plain v * RN(1/s) can miss by an ulp,
+              // which fp16's extra mantissa bits expose.
+              float tq = rintf(dtr<DT>(div_mk(v, qs, rqs)));
+              if (!sym) tq = dtr<DT>(tq + qz);
+              tq = fminf(fmaxf(tq, qmin), qmax);
+              q[j][k] = dtr<DT>((sym ? tq : dtr<DT>(tq - qz)) * qs);
             }
           }
-          qparams_f32_mse(rmn, rmx, qmin, qmax, sym, qs, qz);
-#pragma unroll
-          for (int k = 0; k < CH; ++k) {
-            float tq = fminf(fmaxf(rintf(q[k] / qs) + qz, qmin), qmax);
-            q[k] = dtr<DT>((tq - qz) * qs);
-          }
-        } else {
-        qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
-        const float rqs = 1.0f / qs;  // RN(1/s): qs >= DT(1e-5) / qmax, so it is normal
-#pragma unroll
-        for (int k = 0; k < CH; ++k) {
-          const float v = fminf(fmaxf(q[k], smin), smax);
-          // correctly rounded fp32 quotient, then rounded to DT: Markstein's from RN(1/s) (3
-          // VALU; |v / s| <= qmax + 1, normal or rounding to zero either way, as mk_safe in
-          // quant_group.hip) or the IEEE division (mkdiv 0, ~10 VALU). A plain v * RN(1/s)
-          // can miss by an ulp, which fp16's extra mantissa bits expose.
-          float tq = rintf(dtr<DT>(mkdiv ? div_mk(v, qs, rqs) : __fdiv_rn(v, qs)));
-          if (!sym) tq = dtr<DT>(tq + qz);
-          tq = fminf(fmaxf(tq, qmin), qmax);
-          q[k] = dtr<DT>((sym ? tq : dtr<DT>(tq - qz)) * qs);
-        }
         }
       }
-      float e = (p > 0) ? es[(p - 1) * CROWS + r] : 0.f;
+      float e[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) e[j] = (p > 0) ? es[(p - 1) * RW + j * CROWS + r] : 0.f;
       for (int t = 0; t < tn; ++t) {
-        const float d = dot_row<DT, G, CVT2>(&xs[t * G], q, h);
-        if (p == 0) {
-          if (h == 0) orgs[t * CROWS + r] = d;
-        } else {
-          const float dd = dtr<DT>(d - orgs[t * CROWS + r]);
-          e += dtr<DT>(dd * dd);
+        float d[R];
+        dot_rows<DT, G, R>(&xs[t * G], q, h, d);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          if (p == 0) {
+            if (h == 0) orgs[t * RW + j * CROWS + r] = dt_bits<DT>(d[j]);
+          } else {
+            const float dd = dtr<DT>(d[j] - dt_val<DT>(orgs[t * RW + j * CROWS + r]));
+            e[j] += dtr<DT>(dd * dd);
+          }
         }
       }
-      if (p > 0 && h == 0) es[(p - 1) * CROWS + r] = e;
+      if (p > 0 && h == 0)
+#pragma unroll
+        for (int j = 0; j < R; ++j) es[(p - 1) * RW + j * CROWS + r] = e[j];
       if (p == 0) __syncthreads();  // orgs written by the even lanes, read by both
     }
   }
-  if (!live || h) return;
-  float bmax = org_max, bmin = org_min, best = dtr<DT>(1e9f);
-  for (int s = 0; s < nsteps; ++s) {
-    const float em = dtr<DT>(es[s * CROWS + r] / (float)T);
-    if (em < best) {
-      best = em;
-      const float f = factors[s];
-      bmax = dtr<DT>(org_max * f);
-      bmin = clip_sym ? -bmax : dtr<DT>(org_min * f);
+  if (h) return;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if (!live[j]) continue;
+    float bmax = org_max[j], bmin = org_min[j], best = dtr<DT>(1e9f);
+    for (int s = 0; s < nsteps; ++s) {
+      const float em = dtr<DT>(es[s * RW + j * CROWS + r] / (float)T);
+      if (em < best) {
+        best = em;
+        const float f = factors[s];
+        bmax = dtr<DT>(org_max[j] * f);
+        bmin = clip_sym ? -bmax : dtr<DT>(org_min[j] * f);
+      }
     }
-  }
-  if constexpr (DT == LCQ_BF16) {
-    best_max[o * ng + g] = (uint16_t)(__float_as_uint(bmax) >> 16);
-    best_min[o * ng + g] = (uint16_t)(__float_as_uint(bmin) >> 16);
-  } else {
-    best_max[o * ng + g] = __builtin_bit_cast(uint16_t, (_Float16)bmax);
-    best_min[o * ng + g] = __builtin_bit_cast(uint16_t, (_Float16)bmin);
+    const int64_t oi = o[j] * ng + g;
+    if constexpr (DT == LCQ_BF16) {
+      best_max[oi] = (uint16_t)(__float_as_uint(bmax) >> 16);
+      best_min[oi] = (uint16_t)(__float_as_uint(bmin) >> 16);
+    } else {
+      best_max[oi] = __builtin_bit_cast(uint16_t, (_Float16)bmax);
+      best_min[oi] = __builtin_bit_cast(uint16_t, (_Float16)bmin);
+    }
   }
 }
 
@@ -699,21 +763,31 @@ struct ClipLaunch {
   const void* qx;
 };
 
-template <int DT, int G, bool MSE>
-static void launch_auto_clip(const ClipLaunch& c, hipStream_t st) {
-  dim3 grid((unsigned)((c.oc + CROWS - 1) / CROWS), (unsigned)(c.ic / G));
-  const char* e = getenv("LCQ_CLIP_CVT");  // 0: the convert + shift / mask widening (A/B)
-  const char* dv = getenv("LCQ_CLIP_DIV");  // ieee: the IEEE division sequence (A/B)
-  const int mkdiv = !(dv && dv[0] == 'i');
-  auto k = (DT == LCQ_BF16 && e && e[0] == '0') ? k_auto_clip<DT, G, MSE, false>
-                                                : k_auto_clip<DT, G, MSE, true>;
-  hipLaunchKernelGGL(k, grid, 2 * CROWS, 0, st,
+template <int DT, int G, int R, bool MSE>
+static void launch_auto_clip_r(const ClipLaunch& c, hipStream_t st) {
+  constexpr int lds = ClipTile<G, R>::bytes;
+  auto k = k_auto_clip<DT, G, R, MSE>;
+  // dynamic LDS beyond 64 KB needs the attribute (per device: set on every launch, cheap)
+  hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  dim3 grid((unsigned)((c.oc + CROWS * R - 1) / (CROWS * R)), (unsigned)(c.ic / G));
+  hipLaunchKernelGGL(k, grid, 2 * CROWS, lds, st,
                      reinterpret_cast<const uint16_t*>(c.w), reinterpret_cast<const uint16_t*>(c.x),
                      c.oc, c.ic, (int)c.T, c.nsteps, reinterpret_cast<const float*>(c.factors),
                      (float)c.qmin, (float)c.qmax, c.sym, c.clip_sym,
                      reinterpret_cast<uint16_t*>(c.bmax), reinterpret_cast<uint16_t*>(c.bmin),
                      c.mse_steps, reinterpret_cast<const float*>(c.mse_p), c.norm,
-                     reinterpret_cast<const uint16_t*>(c.qx), mkdiv);
+                     reinterpret_cast<const uint16_t*>(c.qx));
+}
+
+// two rows per lane pair where the grid still fills the chip twice over (512 workgroups at
+// 2 per CU); below that (v_proj 1024 x 4096: 128 workgroups) one row per lane pair
+template <int DT, int G, bool MSE>
+static void launch_auto_clip(const ClipLaunch& c, hipStream_t st) {
+  constexpr bool two = G <= 128 && !MSE;
+  const int64_t wg2 = (c.oc + 2 * CROWS - 1) / (2 * CROWS) * (c.ic / G);
+  if (two && wg2 >= 512) launch_auto_clip_r<DT, G, two ? 2 : 1, MSE>(c, st);
+  else launch_auto_clip_r<DT, G, 1, MSE>(c, st);
 }
 
 template <int DT, bool MSE>

@@ -60,23 +60,40 @@ def _lcq_sdpa(module, query, key, value, attention_mask, dropout=0.0, scaling=No
                       scaling=scaling, is_causal=is_causal, **kwargs)
 
 
-def _plain_linears(*mods):
-    """Exact nn.Linear modules without hooks: their math may be fused across modules."""
-    return all(type(m) is nn.Linear and not (m._forward_hooks or m._forward_pre_hooks)
-               for m in mods)
+def _input_only_hooked(*mods):
+    """nn.Linear modules whose hooks (if any) all read only the module inputs (the capture
+    hooks of algorithms whose add_batch ignores the output, marked `_lcq_input_only` by
+    BaseBlockwiseQuantization.register_hooks)."""
+    return all(type(m) is nn.Linear and all(
+        getattr(h, '_lcq_input_only', False)
+        for h in (*m._forward_pre_hooks.values(), *m._forward_hooks.values()))
+        for m in mods)
+
+
+def _fire_input_hooks(m, x):
+    """The hooks a module call would fire, in the same order (pre, then forward), with the
+    output None: only for input-only hooks (_input_only_hooked)."""
+    for h in m._forward_pre_hooks.values():
+        h(m, (x,))
+    for h in m._forward_hooks.values():
+        h(m, (x,), None)
 
 
 def _gate_up_silu(mlp, x):
     """act_fn(gate_proj(x)) * up_proj(x): one lcq GEMM with the SiLU product in its epilogue
-    when both projections are plain (bias-free) linears the GEMM takes; otherwise the
-    projections run as modules (hooks fire in order) and lcq_silu_mul makes the product."""
+    when both projections are bias-free linears the GEMM takes and carry no hooks, or only
+    input-capture hooks (GPTQ's calibration forward: the hooks fire first, in module order,
+    and the two [M, I] projections are never written); otherwise the projections run as
+    modules (hooks fire in order) and lcq_silu_mul makes the product."""
     from . import ops
     from .module_utils import _GEMM_ON
     gp, up = mlp.gate_proj, mlp.up_proj
     if (_GEMM_ON and getattr(mlp.config, 'hidden_act', None) == 'silu'
-            and _plain_linears(gp, up) and gp.bias is None and up.bias is None
+            and _input_only_hooked(gp, up) and gp.bias is None and up.bias is None
             and ops.gemm_supported(x, gp.weight, up.weight)
             and gp.weight.stride(0) == up.weight.stride(0)):
+        _fire_input_hooks(gp, x)
+        _fire_input_hooks(up, x)
         return ops.linear_silu_mul(x, gp.weight, up.weight)
     g = gp(x)
     u = up(x)
@@ -144,16 +161,20 @@ def _stage(cache, name, key, mods, fn):
 
 def qkv_proj(attn, xn, weights=None):
     """q / k / v projections of LlamaAttention: one lcq GEMM launch for the three when they
-    are plain linears the GEMM takes (x read once), else the three modules. `weights`
-    overrides the three weights (the AWQ search's fake-quantized copies)."""
+    are linears the GEMM takes with no hooks or only input-capture hooks (x read once), else
+    the three modules. `weights` overrides the three weights (the AWQ search's
+    fake-quantized copies; their modules' hooks are not fired)."""
     from . import ops
     from .module_utils import _GEMM_ON
     mods = (attn.q_proj, attn.k_proj, attn.v_proj)
     ws = list(weights) if weights is not None else [m.weight for m in mods]
-    if (_GEMM_ON and (weights is not None or _plain_linears(*mods))
+    if (_GEMM_ON and (weights is not None or _input_only_hooked(*mods))
             and ops.gemm_supported(xn, *ws) and len({w.stride(0) for w in ws}) == 1
             and all(w.shape[0] % 256 == 0 for w in ws[:2])
             and all(m.bias is None or m.bias.dtype == xn.dtype for m in mods)):
+        if weights is None:  # input-capture hooks fire first, in module order
+            for m in mods:
+                _fire_input_hooks(m, xn)
         return ops.linear_multi(xn, ws, [m.bias for m in mods])
     if weights is not None:
         from .module_utils import lcq_linear
