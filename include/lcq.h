@@ -217,6 +217,15 @@ int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t col0, int cou
                         const void* z_in, const int32_t* col_group, int64_t ngc, void* err,
                         void* losses, void* stream);
 
+/* C = beta C + alpha A op(B) on row-major fp32 views (the fp32 updates of the recursive
+ * factorisation behind U, gptq_core._chol_inv_rec: `addmm_` of the reference-equivalent
+ * cholesky -> cholesky_inverse -> cholesky chain, gptq.py:161-170). A [M, K] (lda), B [K, N]
+ * (bt 0) or its transpose stored [N, K] (bt 1; ldb), C [M, N] (ldc); beta 0 never reads C.
+ * fp32 MFMA (32x32x2), 128x128 tiles. */
+int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
+                 const void* B, int64_t ldb, int bt, float beta, void* C, int64_t ldc,
+                 void* stream);
+
 /* Diagonal tile of the recursive fp32 factorisation behind U = chol(H^-1, upper)
  * (gptq.py:169-174): for SPD A (n x n, n <= 128, row-major fp32, leading dim lda), X <- L^-1
  * and, if L is not NULL, L <- the lower Cholesky factor (upper parts zeroed). A is only read.

@@ -345,3 +345,193 @@ extern "C" int lcq_chol_inv_tile(const void* A, int64_t lda, int n, void* L, int
                      reinterpret_cast<float*>(X), ldx, reinterpret_cast<int*>(info), row0, vec);
   return check_launch("lcq_chol_inv_tile");
 }
+
+// ---------------------------------------------------------------------------------------
+// fp32 GEMM for the recursion's updates (gptq_core._mm_lowT / _mm_low_right / _mm_low_left /
+// _syrk_lower; torch `out.addmm_(A, B, beta=, alpha=)` in the reference-equivalent chain of
+// gptq.py:161-170): C = beta C + alpha A B, all row-major strided views; A [M, K] (k
+// contiguous), B [K, N] (bt 0) or given as its transpose [N, K] (bt 1). beta 0 never reads C
+// (the recursion's outputs start uninitialised). fp32 MFMA v_mfma_f32_32x32x2_f32 (the
+// trailing-update core of gptq.hip): 128x128 output tile per 256-thread workgroup (2x2 waves
+// of 64x64), K in 32-deep chunks double-buffered through LDS with register staging. Operands
+// whose k runs along the row (A, B^T) are transposed into [k][row] LDS panels while staged
+// (pitch 129: the 8 rows x 8 k-quads a wave writes land <= 2 per bank); B [K, N] copies
+// straight into [k][col] (pitch 128, 16-byte writes).
+// ---------------------------------------------------------------------------------------
+namespace lcq {
+namespace f32g {
+
+typedef float v16f __attribute__((ext_vector_type(16)));
+constexpr int T = 128;   // output tile
+constexpr int KC = 32;   // K chunk
+constexpr int PT = 129;  // pitch of a transposed [k][row] panel
+constexpr int PK = 128;  // pitch of a k-major [k][col] panel
+
+struct Args {
+  const float* A;
+  const float* B;
+  float* C;
+  int64_t M, N, K, lda, ldb, ldc;
+  float alpha, beta;
+  int vec;  // every row start 16-byte aligned: float4 loads
+};
+
+// a k-contiguous operand tile: rows r0.., k0..k0+31 -> 4 float4 slots per thread
+__device__ __forceinline__ void load_kc(const float* __restrict__ P, int64_t rows, int64_t K,
+                                        int64_t ld, int64_t r0, int64_t k0, int tid, int vec,
+                                        float4 (&v)[4]) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = it * 256 + tid;
+    const int64_t r = r0 + idx / 8, k = k0 + (idx % 8) * 4;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < rows) {
+      const float* p = P + r * ld + k;
+      if (vec && k + 3 < K) {
+        x = *reinterpret_cast<const float4*>(p);
+      } else {
+        if (k + 0 < K) x.x = p[0];
+        if (k + 1 < K) x.y = p[1];
+        if (k + 2 < K) x.z = p[2];
+        if (k + 3 < K) x.w = p[3];
+      }
+    }
+    v[it] = x;
+  }
+}
+__device__ __forceinline__ void store_kc(float* __restrict__ S, int tid, const float4 (&v)[4]) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = it * 256 + tid;
+    const int r = idx / 8, k = (idx % 8) * 4;
+    S[(k + 0) * PT + r] = v[it].x;
+    S[(k + 1) * PT + r] = v[it].y;
+    S[(k + 2) * PT + r] = v[it].z;
+    S[(k + 3) * PT + r] = v[it].w;
+  }
+}
+// a k-major operand tile (B [K, N]): k0..k0+31, cols c0..c0+127
+__device__ __forceinline__ void load_km(const float* __restrict__ P, int64_t K, int64_t cols,
+                                        int64_t ld, int64_t k0, int64_t c0, int tid, int vec,
+                                        float4 (&v)[4]) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = it * 256 + tid;
+    const int64_t k = k0 + idx / 32, c = c0 + (idx % 32) * 4;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (k < K) {
+      const float* p = P + k * ld + c;
+      if (vec && c + 3 < cols) {
+        x = *reinterpret_cast<const float4*>(p);
+      } else {
+        if (c + 0 < cols) x.x = p[0];
+        if (c + 1 < cols) x.y = p[1];
+        if (c + 2 < cols) x.z = p[2];
+        if (c + 3 < cols) x.w = p[3];
+      }
+    }
+    v[it] = x;
+  }
+}
+__device__ __forceinline__ void store_km(float* __restrict__ S, int tid, const float4 (&v)[4]) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = it * 256 + tid;
+    *reinterpret_cast<float4*>(&S[(idx / 32) * PK + (idx % 32) * 4]) = v[it];
+  }
+}
+
+template <int BT>
+__global__ void __launch_bounds__(256, 2) k_gemm_f32(Args a) {
+  constexpr int PB = BT ? PT : PK;
+  __shared__ __attribute__((aligned(16))) float As[2][KC * PT];
+  __shared__ __attribute__((aligned(16))) float Bs[2][KC * PB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t r0 = (int64_t)blockIdx.y * T, c0 = (int64_t)blockIdx.x * T;
+  v16f acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[x][y][i] = 0.f;
+  float4 ra[4], rb[4];
+  auto load = [&](int64_t k0) {
+    load_kc(a.A, a.M, a.K, a.lda, r0, k0, tid, a.vec, ra);
+    if constexpr (BT) load_kc(a.B, a.N, a.K, a.ldb, c0, k0, tid, a.vec, rb);
+    else load_km(a.B, a.K, a.N, a.ldb, k0, c0, tid, a.vec, rb);
+  };
+  auto store = [&](int buf) {
+    store_kc(As[buf], tid, ra);
+    if constexpr (BT) store_kc(Bs[buf], tid, rb);
+    else store_km(Bs[buf], tid, rb);
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  const int64_t nch = (a.K + KC - 1) / KC;
+  for (int64_t ch = 0; ch < nch; ++ch) {
+    const int cur = (int)(ch & 1);
+    if (ch + 1 < nch) load((ch + 1) * KC);
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 2) {
+      const int k = kk + (lane >> 5);
+      float av[2], bv[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        av[t] = As[cur][k * PT + wr * 64 + t * 32 + (lane & 31)];
+        bv[t] = Bs[cur][k * PB + wc * 64 + t * 32 + (lane & 31)];
+      }
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x], bv[y], acc[x][y], 0, 0, 0);
+    }
+    if (ch + 1 < nch) store(cur ^ 1);
+    __syncthreads();
+  }
+  // C layout of a 32x32 MFMA tile: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int64_t r = r0 + wr * 64 + x * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+        const int64_t c = c0 + wc * 64 + y * 32 + (lane & 31);
+        if (r < a.M && c < a.N) {
+          float* p = a.C + r * a.ldc + c;
+          const float v = a.alpha * acc[x][y][reg];
+          *p = a.beta == 0.f ? v : __fmaf_rn(a.beta, *p, v);
+        }
+      }
+}
+
+}  // namespace f32g
+}  // namespace lcq
+
+extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
+                            int64_t lda, const void* B, int64_t ldb, int bt, float beta, void* C,
+                            int64_t ldc, void* stream) {
+  LCQ_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
+  if (M == 0 || N == 0) return LCQ_OK;
+  LCQ_REQUIRE(A != nullptr && B != nullptr && C != nullptr, "null pointers");
+  LCQ_REQUIRE(lda >= K && ldc >= N && ldb >= (bt ? K : N), "leading dimensions too small");
+  LCQ_REQUIRE(M / f32g::T < 65535, "M too large");
+  const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  f32g::Args a{};
+  a.A = reinterpret_cast<const float*>(A);
+  a.B = reinterpret_cast<const float*>(B);
+  a.C = reinterpret_cast<float*>(C);
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.alpha = alpha; a.beta = beta;
+  a.vec = al(A) && al(B) && lda % 4 == 0 && ldb % 4 == 0;
+  if (K == 0) a.alpha = 0.f;  // C = beta C
+  const dim3 grid((unsigned)((N + f32g::T - 1) / f32g::T), (unsigned)((M + f32g::T - 1) / f32g::T));
+  hipStream_t st = as_stream(stream);
+  if (bt) hipLaunchKernelGGL(f32g::k_gemm_f32<1>, grid, 256, 0, st, a);
+  else hipLaunchKernelGGL(f32g::k_gemm_f32<0>, grid, 256, 0, st, a);
+  return check_launch("lcq_gemm_f32");
+}

@@ -236,32 +236,6 @@ class _linalg_backend:
             torch.backends.cuda.preferred_linalg_library(self.prev)
 
 
-class _blas_backend:
-    """Scoped torch BLAS library for the recursion's fp32 GEMMs (env LCQ_CHOL_BLAS = cublas
-    (rocBLAS on ROCm; default) | cublaslt (hipBLASLt) | default). Measured on MI355X: the
-    Cholesky-inverse recursion takes 33.6 ms (n 14336) / 3.5 ms (n 4096) on rocBLAS vs
-    42.1 / 5.8 ms on hipBLASLt, whose kernel choices for the many <= 256 and strided
-    mid-size products are slow. Restores the caller's choice on exit."""
-
-    def __enter__(self):
-        import os
-        self.want = os.environ.get('LCQ_CHOL_BLAS', 'cublas')
-        self.prev = None
-        if self.want != 'default' and torch.cuda.is_available():
-            import warnings
-            with warnings.catch_warnings():
-                warnings.simplefilter('ignore')
-                self.prev = torch.backends.cuda.preferred_blas_library()
-                torch.backends.cuda.preferred_blas_library(self.want)
-
-    def __exit__(self, *exc):
-        if self.prev is not None:
-            import warnings
-            with warnings.catch_warnings():
-                warnings.simplefilter('ignore')
-                torch.backends.cuda.preferred_blas_library(self.prev)
-
-
 _TILE = 128
 _TRI_MIN = 1024  # triangular / symmetric products split while both halves stay >= this
 
@@ -275,23 +249,23 @@ def _mm_lowT(A, Xl, out, alpha, beta):
     -- the zero block skipped, 3/4 of the flops per split level."""
     k = Xl.shape[0]
     if k < 2 * _TRI_MIN:
-        out.addmm_(A, Xl.t(), beta=beta, alpha=alpha)
+        ops.gemm_f32(A, Xl, out, alpha, beta, b_trans=True)
         return
     h = _split(k)
     _mm_lowT(A[:, :h], Xl[:h, :h], out[:, :h], alpha, beta)
     _mm_lowT(A[:, h:], Xl[h:, h:], out[:, h:], alpha, beta)
-    out[:, h:].addmm_(A[:, :h], Xl[h:, :h].t(), alpha=alpha)
+    ops.gemm_f32(A[:, :h], Xl[h:, :h], out[:, h:], alpha, 1.0, b_trans=True)
 
 
 def _mm_low_right(A, Xl, out, alpha, beta):
     """out = beta out + alpha A Xl, Xl lower: A Xl = [A1 X11 + A2 X21, A2 X22]."""
     k = Xl.shape[0]
     if k < 2 * _TRI_MIN:
-        out.addmm_(A, Xl, beta=beta, alpha=alpha)
+        ops.gemm_f32(A, Xl, out, alpha, beta)
         return
     h = _split(k)
     _mm_low_right(A[:, :h], Xl[:h, :h], out[:, :h], alpha, beta)
-    out[:, :h].addmm_(A[:, h:], Xl[h:, :h], alpha=alpha)
+    ops.gemm_f32(A[:, h:], Xl[h:, :h], out[:, :h], alpha, 1.0)
     _mm_low_right(A[:, h:], Xl[h:, h:], out[:, h:], alpha, beta)
 
 
@@ -299,12 +273,12 @@ def _mm_low_left(Xl, B, out, alpha, beta):
     """out = beta out + alpha Xl B, Xl lower: Xl B = [X11 B1; X21 B1 + X22 B2]."""
     k = Xl.shape[0]
     if k < 2 * _TRI_MIN:
-        out.addmm_(Xl, B, beta=beta, alpha=alpha)
+        ops.gemm_f32(Xl, B, out, alpha, beta)
         return
     h = _split(k)
     _mm_low_left(Xl[:h, :h], B[:h], out[:h], alpha, beta)
     _mm_low_left(Xl[h:, h:], B[h:], out[h:], alpha, beta)
-    out[h:].addmm_(Xl[h:, :h], B[:h], alpha=alpha)
+    ops.gemm_f32(Xl[h:, :h], B[:h], out[h:], alpha, 1.0)
 
 
 def _syrk_lower(L, C, alpha):
@@ -312,11 +286,11 @@ def _syrk_lower(L, C, alpha):
     diagonal blocks are updated whole)."""
     m = C.shape[0]
     if m < 2 * _TRI_MIN:
-        C.addmm_(L, L.t(), alpha=alpha)
+        ops.gemm_f32(L, L, C, alpha, 1.0, b_trans=True)
         return
     h = _split(m)
     _syrk_lower(L[:h], C[:h, :h], alpha)
-    C[h:, :h].addmm_(L[h:], L[:h].t(), alpha=alpha)
+    ops.gemm_f32(L[h:], L[:h], C[h:, :h], alpha, 1.0, b_trans=True)
     _syrk_lower(L[h:], C[h:, h:], alpha)
 
 
@@ -326,9 +300,11 @@ def _chol_inv_rec(A: torch.Tensor, X: torch.Tensor, info: torch.Tensor, row0: in
 
     [[A11, .], [A21, A22]]: X11 = chol(A11)^-1 (recursion); L21 = A21 X11^T; A22 -= L21 L21^T;
     X22 = chol(A22)^-1 (recursion); X21 = -X22 (L21 X11). Tiles of <= 128 are factored and
-    inverted in one workgroup (lcq_chol_inv_tile); everything else is fp32 GEMM on hipBLASLt
-    (127-145 TF/s at these shapes), written in place through strided views, with the
-    triangular / symmetric structure skipped block-wise (_mm_* / _syrk_lower)."""
+    inverted in one workgroup (lcq_chol_inv_tile); everything else is fp32 MFMA GEMM
+    (lcq_gemm_f32), written in place through strided views, with the triangular / symmetric
+    structure skipped block-wise (_mm_* / _syrk_lower). Under true_sequential the block's
+    Hessians (q/k/v, o, gate/up, down) are built one after another from the previous subsets'
+    quantized outputs, so their chains cannot overlap."""
     n = A.shape[0]
     if n <= _TILE:
         ops.chol_inv_tile(A, info, row0, out=X)
@@ -353,8 +329,7 @@ def inverse_cholesky_upper(H: torch.Tensor) -> torch.Tensor:
     del H
     info = torch.zeros(1, dtype=torch.int32, device=Hr.device)
     X = torch.zeros_like(Hr)
-    with _blas_backend():
-        _chol_inv_rec(Hr, X, info)
+    _chol_inv_rec(Hr, X, info)
     del Hr
     bad = int(info.item())
     if bad:

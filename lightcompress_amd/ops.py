@@ -271,6 +271,22 @@ def _ld(t: torch.Tensor) -> int:
     return t.stride(0)
 
 
+def gemm_f32(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, alpha: float = 1.0,
+             beta: float = 0.0, b_trans: bool = False) -> torch.Tensor:
+    """out = beta * out + alpha * A @ (B.T if b_trans else B) on row-major fp32 views (the
+    Cholesky recursion's `addmm_`, lcq_gemm_f32); beta 0 never reads out."""
+    M, K = A.shape
+    n_ = out.shape[1]
+    ok = B.shape == ((n_, K) if b_trans else (K, n_))
+    if not ok or out.shape[0] != M:
+        raise ValueError('gemm_f32: shape mismatch')
+    if any(t.dtype != torch.float32 for t in (A, B, out)):
+        raise ValueError('gemm_f32: fp32 operands')
+    N.call('lcq_gemm_f32', M, n_, K, float(alpha), A.data_ptr(), _ld(A), B.data_ptr(), _ld(B),
+           int(b_trans), float(beta), out.data_ptr(), _ld(out), N.stream_of(A))
+    return out
+
+
 def chol_inv_tile(A: torch.Tensor, info: torch.Tensor, row0: int = 0,
                   L: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """Returns L^-1 for the lower Cholesky factor L of A (<= 128 x 128 fp32 view, unit column

@@ -237,6 +237,36 @@ def test_trailing_update(dev, rows, ic, c0, K, c2):
     assert torch.equal(part, out[h:])
 
 
+@pytest.mark.parametrize('M,N,K', [(1, 1, 1), (130, 77, 33), (256, 384, 128), (1000, 700, 517),
+                                   (2048, 1536, 2048)])
+@pytest.mark.parametrize('bt', [False, True])
+def test_gemm_f32(dev, M, N, K, bt):
+    """lcq_gemm_f32 (the recursion's addmm_): C = beta C + alpha A op(B) on strided fp32 views
+    (sub-views of larger matrices, unaligned row starts), against fp64; beta 0 ignores a
+    NaN-filled C."""
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    big_a = torch.randn(M + 3, K + 5, generator=g)
+    big_b = torch.randn((N + 2, K + 3) if bt else (K + 2, N + 3), generator=g)
+    A = big_a[1:M + 1, 1:K + 1]
+    B = big_b[:N, 2:K + 2] if bt else big_b[2:K + 2, :N]
+    C0 = torch.randn(M, N, generator=g)
+    ref_p = A.double() @ (B.double().t() if bt else B.double())
+    for alpha, beta in ((1.0, 0.0), (-1.0, 1.0), (0.5, 2.0)):
+        Cd = C0.to(dev).clone()
+        if beta == 0.0:
+            Cd.fill_(float('nan'))
+        Ad = big_a.to(dev)[1:M + 1, 1:K + 1]
+        Bd = big_b.to(dev)[:N, 2:K + 2] if bt else big_b.to(dev)[2:K + 2, :N]
+        ops.gemm_f32(Ad, Bd, Cd, alpha, beta, b_trans=bt)
+        ref = alpha * ref_p + (beta * C0.double() if beta else 0)
+        bound = (abs(alpha) * (A.double().abs() @ (B.double().abs().t() if bt else
+                                                      B.double().abs()))
+                 + abs(beta) * C0.double().abs())
+        err = ((Cd.cpu().double() - ref).abs() / (bound + 1e-30)).max().item()
+        assert err < 2e-6, (alpha, beta, err)
+
+
 @pytest.mark.parametrize('n', [100, 128, 300, 1000, 4096, 4500])
 def test_inverse_cholesky_upper(dev, n):
     """Recursive lcq factorisation: U^T U = H^-1 with U upper (fp64 check), equal to the
