@@ -368,16 +368,14 @@ def bench_awq(args, rank, world, dev):
     model = Llama.random(cfg, num_layers=nblk, device=dev, seed=1000)   # same on every rank
     hidden = synthetic_hidden(args.n_samples, args.seq_len, cfg.hidden_size, dev, 17)
     algo = build_algo(model, config, {'data': [hidden], 'kwargs': [model.rotary_kwargs(args.seq_len)]})
-    blocks = model.get_blocks()
-    mine = [i for i in range(nblk) if world == 1 or i % world == rank]
     timer = _native.KernelTimer()
     sync_barrier(world)
     t0 = time.perf_counter()
     with timer:
         algo.run_block_loop()
-        for i in mine:  # deploy: real-quant + vLLM pack of this rank's blocks
-            model.replace_module_block(VllmRealQuantLinear, blocks[i], i,
-                                       algo.get_replacement_params('vllm_quant', algo.w_only))
+        # deploy: real-quant + vLLM pack; under shard_blocks each rank packs its own blocks and
+        # the packed shards are gathered, so every rank ends with the whole deployed model
+        algo.deploy('vllm_quant')
     sync_barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     kern = timer.summary()
@@ -788,7 +786,7 @@ def main():
                        'global_batch': args.n_samples, 'seq_len': args.seq_len,
                        'parallelism': (f'run_block_loop {mode}: {args.steps} blocks per GPU '
                                        f'x {world} GPU(s); non-owner float forwards + '
-                                       'owner broadcasts included')},
+                                       'packed-shard gather included')},
             'e2e': e2e,
             'l70b': l70b,
             'gptq': gptq,

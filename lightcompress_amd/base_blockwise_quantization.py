@@ -132,12 +132,64 @@ class BlockwiseOpt:
                 continue
             self.block_opt(self.blocks[i])
         if mode == 'shard_blocks':
-            for i, block in enumerate(self.blocks):
-                P.broadcast_block(block, owner=i % world)
-                # the broadcast writes weights through .data (no version bump): no memoised
-                # stage may survive it
-                self._clear_block_cache(block)
+            # blocks stay on their owners until it is known what the other ranks need: a
+            # real-quant deploy gathers the quantized shards only (packed codes + scales,
+            # _publish_deployed), anything else the transformed float blocks (materialize)
+            self._pending_owner = {i: i % world for i in range(len(self.blocks))}
         self.save_transforms()
+
+    def materialize_blocks(self):
+        """shard_blocks: publish every transformed float block from its owner (the state one
+        GPU would hold after run_block_loop); a no-op otherwise or once done."""
+        pending = getattr(self, '_pending_owner', None)
+        if not pending:
+            return
+        for i, block in enumerate(self.blocks):
+            P.broadcast_block(block, owner=pending[i])
+            # the broadcast writes weights through .data (no version bump): no memoised
+            # stage may survive it
+            self._clear_block_cache(block)
+        self._pending_owner = None
+
+    @torch.no_grad()
+    def _publish_deployed(self, block, owner):
+        """After the owner replaced this block's linears by real-quant modules: the other
+        ranks build empty modules of the same class, buffer shapes and plain attributes
+        (their float linears are dropped unread), then every parameter and buffer of the
+        block -- norms in float, linears as packed codes + scales -- comes from the owner."""
+        import importlib
+        rank, _ = P.dist_world()
+        lins = self.model.get_block_linears(block)
+        spec = [None]
+        if rank == owner:
+            spec = [[(n, type(m).__module__, type(m).__qualname__,
+                      {k: v for k, v in m.__dict__.items()
+                       if not k.startswith('_') and k != 'training'
+                       and isinstance(v, (int, float, str, bool, tuple, torch.Size,
+                                          torch.dtype, type(None)))},
+                      [(bn, None if b is None else tuple(b.shape),
+                        None if b is None else str(b.dtype).split('.')[-1])
+                       for bn, b in m._buffers.items()])
+                     for n, m in lins.items()]]
+        dist.broadcast_object_list(spec, src=owner)
+        if rank != owner:
+            dev = next(block.parameters(), next(block.buffers(), None)).device
+            for n, modname, qual, attrs, bufs in spec[0]:
+                cls = importlib.import_module(modname)
+                for part in qual.split('.'):
+                    cls = getattr(cls, part)
+                m = cls.__new__(cls)
+                nn.Module.__init__(m)
+                for bn, shape, dt in bufs:
+                    m.register_buffer(bn, None if shape is None else
+                                      torch.empty(shape, dtype=getattr(torch, dt), device=dev))
+                for k, v in attrs.items():
+                    setattr(m, k, v)
+                parent_name, _, child = n.rpartition('.')
+                parent = block.get_submodule(parent_name) if parent_name else block
+                setattr(parent, child, m)
+        P.broadcast_block(block, owner=owner)
+        self._clear_block_cache(block)
 
     def save_transforms(self):
         """blockwise_optimization.py:40-52: the AWQ scales (save_scale) and v2 clip factors
@@ -667,13 +719,28 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                    'fake_quant_wo_kv': EffcientFakeQuantLinear, **_REALQUANT_LINEAR_MAP_}
         if quant_format not in mapping:
             raise NotImplementedError(f"Quant format '{quant_format}' is not implemented.")
+        pending = getattr(self, '_pending_owner', None)
+        if pending and quant_format in _REALQUANT_LINEAR_MAP_:
+            # shard_blocks: every rank packs its own blocks, then the quantized shards are
+            # gathered (a quarter of the float bytes at int4), never the float weights
+            rank, _ = P.dist_world()
+            self._prequant_fp8_blocks(only={i for i, o in pending.items() if o == rank})
+            params = self.get_replacement_params(quant_format, self.w_only)
+            for i, block in enumerate(self.blocks):
+                if pending[i] == rank:
+                    self.model.replace_module_block(mapping[quant_format], block, i, params)
+            for i, block in enumerate(self.blocks):
+                self._publish_deployed(block, pending[i])
+            self._pending_owner = None
+            return
+        self.materialize_blocks()
         if quant_format in _REALQUANT_LINEAR_MAP_:
             self._prequant_fp8_blocks()
         self.model.replace_module_all(mapping[quant_format],
                                       self.get_replacement_params(quant_format, self.w_only))
 
     @torch.no_grad()
-    def _prequant_fp8_blocks(self):
+    def _prequant_fp8_blocks(self, only=None):
         """Block-fp8 checkpoint linears (DeepSeek-V3 experts) headed for a per-tensor FP8
         real-quant format: requantize every such linear of a block in ONE batched launch
         (lcq_fp8_block_to_tensor_many) instead of one dequant + quant chain per linear;
@@ -685,7 +752,9 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         if self.quant_config['weight'].get('need_pack', False):
             return
         from . import ops
-        for block in self.blocks:
+        for bi, block in enumerate(self.blocks):
+            if only is not None and bi not in only:
+                continue
             mods = [m for m in self.model.get_block_linears(block).values()
                     if getattr(m, 'weight', None) is not None
                     and m.weight.dtype == torch.float8_e4m3fn and hasattr(m, 'weight_scale_inv')]
@@ -700,6 +769,7 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
 
     @torch.no_grad()
     def save_model(self, path):
+        self.materialize_blocks()
         rank, _, _ = world()
         if rank != 0:
             return

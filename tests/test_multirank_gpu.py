@@ -1,5 +1,6 @@
 """Two ranks on one GPU (gloo over device tensors), SURVEY.md §8e: block-sharded AWQ
-(quant_out False), ratio-grid + clip-row sharded AWQ (quant_out True) and replica GPTQ with a
+(quant_out False; deployed to vLLM int4, the other ranks receive the packed shards only),
+ratio-grid + clip-row sharded AWQ (quant_out True) and replica GPTQ with a
 row-sharded column loop reproduce the single-process result bit for bit (the per-unit math is
 identical, only the placement changes); token-sharded GPTQ too (the grouped Hessian sums its
 partials in one fixed tree on any world size dividing 8)."""
@@ -72,6 +73,12 @@ def _run(cfg_dict, layers):
     algo.run_block_loop()
     if cfg_dict.get('deploy'):
         algo.deploy(cfg_dict['deploy'])
+    else:  # shard_blocks publishes the transformed float blocks on demand
+        algo.materialize_blocks()
+    if cfg_dict.get('deploy') == 'vllm_quant':  # every buffer of every block (codes, scales,
+        return {f'{i}.{n}': t.detach().cpu()   # norms) as the rank holds it after the gather
+                for i, b in enumerate(model.blocks)
+                for n, t in [*b.named_parameters(), *b.named_buffers()]}
     return {f'{i}.{n}': m.weight.detach().float().cpu()
             for i, b in enumerate(model.blocks) for n, m in model.get_block_linears(b).items()}
 
@@ -103,7 +110,11 @@ def _two_ranks(cfg, layers, tmp_path):
     return torch.load(path, weights_only=True)
 
 
+AWQ_VLLM = dict(AWQ, deploy='vllm_quant')
+
+
 @pytest.mark.parametrize('name,cfg,layers', [('awq_shard_blocks', AWQ, 4),
+                                             ('awq_shard_blocks_vllm', AWQ_VLLM, 4),
                                              ('awq_shard_search', AWQ_OUT, 2),
                                              ('gptq_replicate_rows', GPTQ, 2)])
 def test_two_ranks_match_single(dev, name, cfg, layers, tmp_path):
@@ -113,6 +124,7 @@ def test_two_ranks_match_single(dev, name, cfg, layers, tmp_path):
     multi = _two_ranks(cfg, layers, tmp_path)
     assert single.keys() == multi.keys()
     for k in single:
+        assert single[k].dtype == multi[k].dtype, k
         assert torch.equal(single[k], multi[k]), k
 
 
