@@ -236,6 +236,11 @@ class _linalg_backend:
             torch.backends.cuda.preferred_linalg_library(self.prev)
 
 
+def _gemm(A, B, out, alpha, beta, b_trans=False):
+    """out = beta out + alpha A op(B): the recursion's products (lcq_gemm_f32)."""
+    return ops.gemm_f32(A, B, out, alpha, beta, b_trans=b_trans)
+
+
 _TILE = 128
 _TRI_MIN = 1024  # triangular / symmetric products split while both halves stay >= this
 
@@ -249,23 +254,23 @@ def _mm_lowT(A, Xl, out, alpha, beta):
     -- the zero block skipped, 3/4 of the flops per split level."""
     k = Xl.shape[0]
     if k < 2 * _TRI_MIN:
-        ops.gemm_f32(A, Xl, out, alpha, beta, b_trans=True)
+        _gemm(A, Xl, out, alpha, beta, b_trans=True)
         return
     h = _split(k)
     _mm_lowT(A[:, :h], Xl[:h, :h], out[:, :h], alpha, beta)
     _mm_lowT(A[:, h:], Xl[h:, h:], out[:, h:], alpha, beta)
-    ops.gemm_f32(A[:, :h], Xl[h:, :h], out[:, h:], alpha, 1.0, b_trans=True)
+    _gemm(A[:, :h], Xl[h:, :h], out[:, h:], alpha, 1.0, b_trans=True)
 
 
 def _mm_low_right(A, Xl, out, alpha, beta):
     """out = beta out + alpha A Xl, Xl lower: A Xl = [A1 X11 + A2 X21, A2 X22]."""
     k = Xl.shape[0]
     if k < 2 * _TRI_MIN:
-        ops.gemm_f32(A, Xl, out, alpha, beta)
+        _gemm(A, Xl, out, alpha, beta)
         return
     h = _split(k)
     _mm_low_right(A[:, :h], Xl[:h, :h], out[:, :h], alpha, beta)
-    ops.gemm_f32(A[:, h:], Xl[h:, :h], out[:, :h], alpha, 1.0)
+    _gemm(A[:, h:], Xl[h:, :h], out[:, :h], alpha, 1.0)
     _mm_low_right(A[:, h:], Xl[h:, h:], out[:, h:], alpha, beta)
 
 
@@ -273,12 +278,12 @@ def _mm_low_left(Xl, B, out, alpha, beta):
     """out = beta out + alpha Xl B, Xl lower: Xl B = [X11 B1; X21 B1 + X22 B2]."""
     k = Xl.shape[0]
     if k < 2 * _TRI_MIN:
-        ops.gemm_f32(Xl, B, out, alpha, beta)
+        _gemm(Xl, B, out, alpha, beta)
         return
     h = _split(k)
     _mm_low_left(Xl[:h, :h], B[:h], out[:h], alpha, beta)
     _mm_low_left(Xl[h:, h:], B[h:], out[h:], alpha, beta)
-    ops.gemm_f32(Xl[h:, :h], B[:h], out[h:], alpha, 1.0)
+    _gemm(Xl[h:, :h], B[:h], out[h:], alpha, 1.0)
 
 
 def _syrk_lower(L, C, alpha):
@@ -286,11 +291,11 @@ def _syrk_lower(L, C, alpha):
     diagonal blocks are updated whole)."""
     m = C.shape[0]
     if m < 2 * _TRI_MIN:
-        ops.gemm_f32(L, L, C, alpha, 1.0, b_trans=True)
+        _gemm(L, L, C, alpha, 1.0, b_trans=True)
         return
     h = _split(m)
     _syrk_lower(L[:h], C[:h, :h], alpha)
-    ops.gemm_f32(L[h:], L[:h], C[h:, :h], alpha, 1.0, b_trans=True)
+    _gemm(L[h:], L[:h], C[h:, :h], alpha, 1.0, b_trans=True)
     _syrk_lower(L[h:], C[h:, h:], alpha)
 
 

@@ -7,10 +7,16 @@ import torch
 from lightcompress_amd import gptq_core as g
 
 
+def _torch_gemm(A, B, out, alpha, beta, b_trans=False):
+    """CPU stand-in for lcq_gemm_f32 (the split logic is what is under test here)."""
+    return out.addmm_(A, B.t() if b_trans else B, beta=beta, alpha=alpha)
+
+
 @pytest.fixture
 def small_splits(monkeypatch):
     monkeypatch.setattr(g, '_TRI_MIN', 8)
     monkeypatch.setattr(g, '_TILE', 4)
+    monkeypatch.setattr(g, '_gemm', _torch_gemm)
 
 
 @pytest.mark.parametrize('k', [7, 16, 40, 64])
