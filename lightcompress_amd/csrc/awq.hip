@@ -176,25 +176,47 @@ __global__ void __launch_bounds__(1024) k_awq_scales(const void* xmean, int64_t 
 // ----------------------------------------------------------------------------------------
 // out[r, c] = round_dt(x[r, c] (op) s[axis index]), op 0 = mul, 1 = div; axis 0 = per column
 // (s has cols entries), 1 = per row (s has rows entries). In place allowed.
+// 2-D grid: a thread owns one 8-column chunk and walks rb (>= SB_ROWS) rows, so a column scale and its
+// reciprocal are loaded / formed once (no per-element index arithmetic). The division is the
+// correctly rounded quotient: Markstein's from RN(1/s) (3 VALU), which equals x / s whenever the
+// quotient is a finite normal number; anything else (zero, subnormal, inf, NaN) takes the IEEE
+// division.
 // ----------------------------------------------------------------------------------------
+constexpr int SB_ROWS = 32;
+
+__device__ __forceinline__ float div_exact(float x, float s, float rs) {
+  const float q = div_mk(x, s, rs);
+  const float a = fabsf(q);
+  return (a >= 1.17549435e-38f && a <= 3.40282347e38f) ? q : __fdiv_rn(x, s);
+}
+
 template <int DT, int OP, int AXIS>
 __global__ void __launch_bounds__(256) k_scale_bcast(const void* x, int64_t rows, int64_t cols,
-                                                    const void* s, void* out) {
-  const int64_t n8 = rows * cols / 8;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
-    const int64_t e0 = t * 8;
-    float v[8], sv[8];
-    ld8<DT>(x, e0, v);
-    if constexpr (AXIS == 0) {
-      ld8<DT>(s, e0 % cols, sv);
-    } else {
-      const float r = ld1<DT>(s, e0 / cols);
+                                                    const void* s, void* out, int64_t rb) {
+  const int64_t c8 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c8 * 8 >= cols) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rb;
+  const int64_t r1 = r0 + rb < rows ? r0 + rb : rows;
+  float sv[8], rs[8];
+  if constexpr (AXIS == 0) {
+    ld8<DT>(s, c8 * 8, sv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sv[j] = r;
+    for (int j = 0; j < 8; ++j) rs[j] = 1.0f / sv[j];
+  }
+  for (int64_t r = r0; r < r1; ++r) {
+    if constexpr (AXIS == 1) {
+      const float v = ld1<DT>(s, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sv[j] = v;
+        rs[j] = 1.0f / v;
+      }
     }
+    const int64_t e0 = r * cols + c8 * 8;
+    float v[8];
+    ld8<DT>(x, e0, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (OP == 0) ? v[j] * sv[j] : v[j] / sv[j];
+    for (int j = 0; j < 8; ++j) v[j] = (OP == 0) ? v[j] * sv[j] : div_exact(v[j], sv[j], rs[j]);
     st8<DT>(out, e0, v);
   }
 }
@@ -709,11 +731,13 @@ extern "C" int lcq_awq_scales_v1(const void* xmean, const void* wmax, int dtype,
 template <int DT>
 static void launch_scale(const void* x, int64_t rows, int64_t cols, const void* s, int op,
                          int axis, void* out, hipStream_t st) {
-  const unsigned grid = stream_grid(rows * cols / 8, 256);
-  if (op == 0 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 0, 0>), grid, 256, 0, st, x, rows, cols, s, out);
-  if (op == 1 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 1, 0>), grid, 256, 0, st, x, rows, cols, s, out);
-  if (op == 0 && axis == 1) hipLaunchKernelGGL((k_scale_bcast<DT, 0, 1>), grid, 256, 0, st, x, rows, cols, s, out);
-  if (op == 1 && axis == 1) hipLaunchKernelGGL((k_scale_bcast<DT, 1, 1>), grid, 256, 0, st, x, rows, cols, s, out);
+  int64_t rb = SB_ROWS;
+  if ((rows + rb - 1) / rb > 65535) rb = (rows + 65534) / 65535;
+  const dim3 grid((unsigned)((cols / 8 + 255) / 256), (unsigned)((rows + rb - 1) / rb));
+  if (op == 0 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 0, 0>), grid, 256, 0, st, x, rows, cols, s, out, rb);
+  if (op == 1 && axis == 0) hipLaunchKernelGGL((k_scale_bcast<DT, 1, 0>), grid, 256, 0, st, x, rows, cols, s, out, rb);
+  if (op == 0 && axis == 1) hipLaunchKernelGGL((k_scale_bcast<DT, 0, 1>), grid, 256, 0, st, x, rows, cols, s, out, rb);
+  if (op == 1 && axis == 1) hipLaunchKernelGGL((k_scale_bcast<DT, 1, 1>), grid, 256, 0, st, x, rows, cols, s, out, rb);
 }
 
 extern "C" int lcq_scale_bcast(const void* x, int dtype, int64_t rows, int64_t cols,

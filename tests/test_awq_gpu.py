@@ -67,6 +67,31 @@ def test_scale_bcast(dev):
     assert torch.equal(bits(y), bits(x * sc.view(1, -1)))
 
 
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16, torch.float32])
+def test_scale_bcast_every_value(dev, dt):
+    """The division's fast path (Markstein quotient from RN(1/s), IEEE fallback off the normal
+    range) equals torch's x / s on every bf16 value (incl. subnormals, +-inf, NaN, +-0)
+    against scales from 1e-30 to 1e30, rows not a multiple of the 32-row block."""
+    from lightcompress_amd import ops
+    allb = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    x = allb.to(dt).reshape(-1, 512)[:100]
+    g = torch.Generator().manual_seed(5)
+    sc = torch.exp(torch.randn(512, generator=g) * 6)
+    sc[:4] = torch.tensor([1e-30, 1e30, 3e-39, 1.0])
+    sc = sc.to(dt)
+    sc = torch.where(sc == 0, torch.ones_like(sc), sc)
+    got = ops.scale_bcast(x.to(dev), sc.to(dev), 'div').cpu()
+    ref = x / sc.view(1, -1)
+    assert torch.equal(got.isnan(), ref.isnan())
+    ok = ~ref.isnan()
+    assert torch.equal(got[ok], ref[ok])
+    sr = sc[:100]
+    got = ops.scale_bcast(x.to(dev), sr.to(dev), 'div', axis=1).cpu()
+    ref = x / sr.view(-1, 1)
+    ok = ~ref.isnan()
+    assert torch.equal(got[ok], ref[ok]) and torch.equal(got.isnan(), ref.isnan())
+
+
 def test_sq_diff_mean(dev):
     from lightcompress_amd import ops
     g = torch.Generator().manual_seed(4)
