@@ -178,16 +178,17 @@ __global__ void __launch_bounds__(1024) k_awq_scales(const void* xmean, int64_t 
 // (s has cols entries), 1 = per row (s has rows entries). In place allowed.
 // 2-D grid: a thread owns one 8-column chunk and walks rb (>= SB_ROWS) rows, so a column scale and its
 // reciprocal are loaded / formed once (no per-element index arithmetic). The division is the
-// correctly rounded quotient: Markstein's from RN(1/s) (3 VALU), which equals x / s whenever the
-// quotient is a finite normal number; anything else (zero, subnormal, inf, NaN) takes the IEEE
-// division.
+// correctly rounded quotient: Markstein's from RN(1/s) (3 VALU), which equals x / s while the
+// residual x - s q0 and the correction r / s stay clear of the subnormal range (|x| and |q| >=
+// 2^-100) and q is finite; anything else (zero, tiny, inf, NaN) takes the IEEE division.
 // ----------------------------------------------------------------------------------------
 constexpr int SB_ROWS = 32;
 
 __device__ __forceinline__ float div_exact(float x, float s, float rs) {
   const float q = div_mk(x, s, rs);
   const float a = fabsf(q);
-  return (a >= 1.17549435e-38f && a <= 3.40282347e38f) ? q : __fdiv_rn(x, s);
+  return (a >= 0x1p-100f && a <= 3.40282347e38f && fabsf(x) >= 0x1p-100f) ? q
+                                                                         : __fdiv_rn(x, s);
 }
 
 template <int DT, int OP, int AXIS>

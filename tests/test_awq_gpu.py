@@ -68,10 +68,11 @@ def test_scale_bcast(dev):
 
 
 @pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16, torch.float32])
-def test_scale_bcast_every_value(dev, dt):
+def test_scale_bcast_rows_every_value(dev, dt):
     """The division's fast path (Markstein quotient from RN(1/s), IEEE fallback off the normal
     range) equals torch's x / s on every bf16 value (incl. subnormals, +-inf, NaN, +-0)
-    against scales from 1e-30 to 1e30, rows not a multiple of the 32-row block."""
+    against scales from 1e-30 to 1e30, per row (axis 1) and per column, 100 rows (not a
+    multiple of the 32-row block)."""
     from lightcompress_amd import ops
     allb = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
     x = allb.to(dt).reshape(-1, 512)[:100]
