@@ -785,7 +785,7 @@ def main():
                        'model': 'Llama-3-8B (4096/14336, 32q/8kv heads)',
                        'global_batch': args.n_samples, 'seq_len': args.seq_len,
                        'parallelism': (f'run_block_loop {mode}: {args.steps} blocks per GPU '
-                                       f'x {world} GPU(s); non-owner float forwards + '
+                                       f'x {world} GPU(s); ring hand-off of block activations + '
                                        'packed-shard gather included')},
             'e2e': e2e,
             'l70b': l70b,

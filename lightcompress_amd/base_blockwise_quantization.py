@@ -120,6 +120,9 @@ class BlockwiseOpt:
     def run_block_loop(self):
         mode = self.parallel_mode()
         rank, world = P.dist_world()
+        if mode == 'shard_blocks' and not self.data_free and self._handoff_ok():
+            self._run_block_loop_ring(rank, world)
+            return
         for i in range(len(self.blocks)):
             self.block_idx = i
             if mode == 'shard_blocks' and i % world != rank:
@@ -137,6 +140,41 @@ class BlockwiseOpt:
             # _publish_deployed), anything else the transformed float blocks (materialize)
             self._pending_owner = {i: i % world for i in range(len(self.blocks))}
         self.save_transforms()
+
+    def _handoff_ok(self):
+        """The ring hand-off passes self.input['data'] as a list of tensors whose shapes every
+        rank already knows (block outputs have their inputs' shapes)."""
+        data = self.input.get('data') if isinstance(self.input, dict) else None
+        return (bool(data) and all(torch.is_tensor(t) for t in data)
+                and type(self).block_opt is BaseBlockwiseQuantization.block_opt)
+
+    def _run_block_loop_ring(self, rank, world):
+        """shard_blocks as a ring pipeline: the owner of block i forwards it first (the float
+        output is the next block's input, quant_out False), hands that output to the owner of
+        block i + 1 over the ring edge, and only then runs the long transform. A rank touches
+        only its own blocks: no rank replays the float chain of the blocks before its own."""
+        groups = P.ring_groups(world)
+        n = len(self.blocks)
+        for i in range(rank, n, world):
+            if i > 0:  # this block's input: the float output of block i - 1
+                src = (i - 1) % world
+                self.input['data'] = [torch.empty_like(t) for t in self.input['data']]
+                P.pass_tensors(self.input['data'], src, groups[src])
+            self.block_idx = i
+            self._handoff = (rank, groups[rank]) if i + 1 < n else None
+            self.block_opt(self.blocks[i])
+            # every owner of a non-last block hands its output on exactly once (run() does it
+            # right after the forward; a path that did not forward must not leave the next
+            # owner waiting)
+            self._send_handoff()
+        self._pending_owner = {i: i % world for i in range(n)}
+        self.save_transforms()
+
+    def _send_handoff(self):
+        h = getattr(self, '_handoff', None)
+        if h is not None:
+            P.pass_tensors(self.input['data'], h[0], h[1])
+            self._handoff = None
 
     def materialize_blocks(self):
         """shard_blocks: publish every transformed float block from its owner (the state one
@@ -557,6 +595,7 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                 self.block_forward(block, stop_after=self.capture_names(self._hooked_names))
             else:
                 self.input['data'] = self.block_forward(block)
+                self._send_handoff()  # ring shard_blocks: the next owner starts now
             for h in handles:
                 h.remove()
             self.block_transform(block, input_feat, self.input['kwargs'])

@@ -114,3 +114,19 @@ def broadcast_block(block: torch.nn.Module, owner: int):
         if b is None or tuple(b.shape) != shape or str(b.dtype).split('.')[-1] != dt:
             m.register_buffer(bn, torch.empty(shape, dtype=getattr(torch, dt), device=dev))
         dist.broadcast(m._buffers[bn].data, src=owner)
+
+
+def ring_groups(world: int):
+    """One process group per ring edge (r, r + 1 mod world), created on every rank in the same
+    order (group creation is collective): the block hand-off of the pipelined shard_blocks
+    loop uses edge r to pass block activations from rank r to rank r + 1."""
+    return [dist.new_group([r, (r + 1) % world]) for r in range(world)]
+
+
+def pass_tensors(tensors, src: int, group):
+    """Hand a list of device tensors from `src` to the other rank of a ring-edge group (a
+    broadcast within the pair: P2P over xGMI under RCCL, and valid on gloo as well). On the
+    receiving rank `tensors` are buffers of the right shapes and dtypes, filled in place."""
+    for t in tensors:
+        dist.broadcast(t, src=src, group=group)
+
