@@ -204,21 +204,28 @@ __global__ void __launch_bounds__(256) k_scale_bcast(const void* x, int64_t rows
 #pragma unroll
     for (int j = 0; j < 8; ++j) rs[j] = 1.0f / sv[j];
   }
-  for (int64_t r = r0; r < r1; ++r) {
-    if constexpr (AXIS == 1) {
-      const float v = ld1<DT>(s, r);
+  // 4 rows per step: their loads are issued together (memory-level parallelism per thread)
+  for (int64_t rb4 = r0; rb4 < r1; rb4 += 4) {
+    float v[4][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sv[j] = v;
-        rs[j] = 1.0f / v;
+    for (int u = 0; u < 4; ++u)
+      if (rb4 + u < r1) ld8<DT>(x, (rb4 + u) * cols + c8 * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rb4 + u >= r1) break;
+      if constexpr (AXIS == 1) {
+        const float q = ld1<DT>(s, rb4 + u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sv[j] = q;
+          rs[j] = 1.0f / q;
+        }
       }
-    }
-    const int64_t e0 = r * cols + c8 * 8;
-    float v[8];
-    ld8<DT>(x, e0, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (OP == 0) ? v[j] * sv[j] : div_exact(v[j], sv[j], rs[j]);
-    st8<DT>(out, e0, v);
+      for (int j = 0; j < 8; ++j)
+        v[u][j] = (OP == 0) ? v[u][j] * sv[j] : div_exact(v[u][j], sv[j], rs[j]);
+      st8<DT>(out, (rb4 + u) * cols + c8 * 8, v[u]);
+    }
   }
 }
 

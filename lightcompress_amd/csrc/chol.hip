@@ -362,10 +362,7 @@ namespace lcq {
 namespace f32g {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
-constexpr int T = 128;   // output tile
 constexpr int KC = 32;   // K chunk
-constexpr int PT = 129;  // pitch of a transposed [k][row] panel
-constexpr int PK = 128;  // pitch of a k-major [k][col] panel
 
 struct Args {
   const float* A;
@@ -376,12 +373,24 @@ struct Args {
   int vec;  // every row start 16-byte aligned: float4 loads
 };
 
-// a k-contiguous operand tile: rows r0.., k0..k0+31 -> 4 float4 slots per thread
+// T x T output tile per 256-thread workgroup, 2 x 2 waves of (T/2)^2 = (T/64)^2 MFMA 32x32
+// tiles each; T = 128 for grids that fill the chip, 64 below that (the recursion's many
+// mid-size products: a 1024^2 output is 64 tiles of 128 but 256 of 64).
+template <int T>
+struct Tile {
+  static constexpr int PT = T + 1;      // pitch of a transposed [k][row] panel
+  static constexpr int PK = T;          // pitch of a k-major [k][col] panel
+  static constexpr int SLOTS = T * KC / 4 / 256;  // float4 slots per thread per operand chunk
+  static constexpr int MT = T / 64;     // MFMA tiles per wave side
+};
+
+// a k-contiguous operand tile: rows r0.., k0..k0+31
+template <int T>
 __device__ __forceinline__ void load_kc(const float* __restrict__ P, int64_t rows, int64_t K,
                                         int64_t ld, int64_t r0, int64_t k0, int tid, int vec,
-                                        float4 (&v)[4]) {
+                                        float4 (&v)[Tile<T>::SLOTS]) {
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < Tile<T>::SLOTS; ++it) {
     const int idx = it * 256 + tid;
     const int64_t r = r0 + idx / 8, k = k0 + (idx % 8) * 4;
     float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -399,9 +408,12 @@ __device__ __forceinline__ void load_kc(const float* __restrict__ P, int64_t row
     v[it] = x;
   }
 }
-__device__ __forceinline__ void store_kc(float* __restrict__ S, int tid, const float4 (&v)[4]) {
+template <int T>
+__device__ __forceinline__ void store_kc(float* __restrict__ S, int tid,
+                                         const float4 (&v)[Tile<T>::SLOTS]) {
+  constexpr int PT = Tile<T>::PT;
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < Tile<T>::SLOTS; ++it) {
     const int idx = it * 256 + tid;
     const int r = idx / 8, k = (idx % 8) * 4;
     S[(k + 0) * PT + r] = v[it].x;
@@ -410,14 +422,15 @@ __device__ __forceinline__ void store_kc(float* __restrict__ S, int tid, const f
     S[(k + 3) * PT + r] = v[it].w;
   }
 }
-// a k-major operand tile (B [K, N]): k0..k0+31, cols c0..c0+127
+// a k-major operand tile (B [K, N]): k0..k0+31, cols c0..c0+T-1
+template <int T>
 __device__ __forceinline__ void load_km(const float* __restrict__ P, int64_t K, int64_t cols,
                                         int64_t ld, int64_t k0, int64_t c0, int tid, int vec,
-                                        float4 (&v)[4]) {
+                                        float4 (&v)[Tile<T>::SLOTS]) {
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < Tile<T>::SLOTS; ++it) {
     const int idx = it * 256 + tid;
-    const int64_t k = k0 + idx / 32, c = c0 + (idx % 32) * 4;
+    const int64_t k = k0 + idx / (T / 4), c = c0 + (idx % (T / 4)) * 4;
     float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
     if (k < K) {
       const float* p = P + k * ld + c;
@@ -433,39 +446,42 @@ __device__ __forceinline__ void load_km(const float* __restrict__ P, int64_t K, 
     v[it] = x;
   }
 }
-__device__ __forceinline__ void store_km(float* __restrict__ S, int tid, const float4 (&v)[4]) {
+template <int T>
+__device__ __forceinline__ void store_km(float* __restrict__ S, int tid,
+                                         const float4 (&v)[Tile<T>::SLOTS]) {
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < Tile<T>::SLOTS; ++it) {
     const int idx = it * 256 + tid;
-    *reinterpret_cast<float4*>(&S[(idx / 32) * PK + (idx % 32) * 4]) = v[it];
+    *reinterpret_cast<float4*>(&S[(idx / (T / 4)) * Tile<T>::PK + (idx % (T / 4)) * 4]) = v[it];
   }
 }
 
-template <int BT>
+template <int BT, int T>
 __global__ void __launch_bounds__(256, 2) k_gemm_f32(Args a) {
-  constexpr int PB = BT ? PT : PK;
+  using TL = Tile<T>;
+  constexpr int PT = TL::PT, PB = BT ? TL::PT : TL::PK, MT = TL::MT, HW = T / 2;
   __shared__ __attribute__((aligned(16))) float As[2][KC * PT];
   __shared__ __attribute__((aligned(16))) float Bs[2][KC * PB];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int64_t r0 = (int64_t)blockIdx.y * T, c0 = (int64_t)blockIdx.x * T;
-  v16f acc[2][2];
+  v16f acc[MT][MT];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < MT; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y)
+    for (int y = 0; y < MT; ++y)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[x][y][i] = 0.f;
-  float4 ra[4], rb[4];
+  float4 ra[TL::SLOTS], rb[TL::SLOTS];
   auto load = [&](int64_t k0) {
-    load_kc(a.A, a.M, a.K, a.lda, r0, k0, tid, a.vec, ra);
-    if constexpr (BT) load_kc(a.B, a.N, a.K, a.ldb, c0, k0, tid, a.vec, rb);
-    else load_km(a.B, a.K, a.N, a.ldb, k0, c0, tid, a.vec, rb);
+    load_kc<T>(a.A, a.M, a.K, a.lda, r0, k0, tid, a.vec, ra);
+    if constexpr (BT) load_kc<T>(a.B, a.N, a.K, a.ldb, c0, k0, tid, a.vec, rb);
+    else load_km<T>(a.B, a.K, a.N, a.ldb, k0, c0, tid, a.vec, rb);
   };
   auto store = [&](int buf) {
-    store_kc(As[buf], tid, ra);
-    if constexpr (BT) store_kc(Bs[buf], tid, rb);
-    else store_km(Bs[buf], tid, rb);
+    store_kc<T>(As[buf], tid, ra);
+    if constexpr (BT) store_kc<T>(Bs[buf], tid, rb);
+    else store_km<T>(Bs[buf], tid, rb);
   };
   load(0);
   store(0);
@@ -474,33 +490,37 @@ __global__ void __launch_bounds__(256, 2) k_gemm_f32(Args a) {
   for (int64_t ch = 0; ch < nch; ++ch) {
     const int cur = (int)(ch & 1);
     if (ch + 1 < nch) load((ch + 1) * KC);
+    // all of this chunk's operand values first (the reads overlap the MFMAs that follow)
+    float av[KC / 2][MT], bv[KC / 2][MT];
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 2) {
       const int k = kk + (lane >> 5);
-      float av[2], bv[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        av[t] = As[cur][k * PT + wr * 64 + t * 32 + (lane & 31)];
-        bv[t] = Bs[cur][k * PB + wc * 64 + t * 32 + (lane & 31)];
+      for (int t = 0; t < MT; ++t) {
+        av[kk / 2][t] = As[cur][k * PT + wr * HW + t * 32 + (lane & 31)];
+        bv[kk / 2][t] = Bs[cur][k * PB + wc * HW + t * 32 + (lane & 31)];
       }
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x], bv[y], acc[x][y], 0, 0, 0);
     }
+#pragma unroll
+    for (int kk = 0; kk < KC / 2; ++kk)
+#pragma unroll
+      for (int x = 0; x < MT; ++x)
+#pragma unroll
+        for (int y = 0; y < MT; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk][x], bv[kk][y], acc[x][y], 0,
+                                                           0, 0);
     if (ch + 1 < nch) store(cur ^ 1);
     __syncthreads();
   }
   // C layout of a 32x32 MFMA tile: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < MT; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y)
+    for (int y = 0; y < MT; ++y)
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
-        const int64_t r = r0 + wr * 64 + x * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-        const int64_t c = c0 + wc * 64 + y * 32 + (lane & 31);
+        const int64_t r = r0 + wr * HW + x * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+        const int64_t c = c0 + wc * HW + y * 32 + (lane & 31);
         if (r < a.M && c < a.N) {
           float* p = a.C + r * a.ldc + c;
           const float v = a.alpha * acc[x][y][reg];
@@ -519,7 +539,7 @@ extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const 
   if (M == 0 || N == 0) return LCQ_OK;
   LCQ_REQUIRE(A != nullptr && B != nullptr && C != nullptr, "null pointers");
   LCQ_REQUIRE(lda >= K && ldc >= N && ldb >= (bt ? K : N), "leading dimensions too small");
-  LCQ_REQUIRE(M / f32g::T < 65535, "M too large");
+  LCQ_REQUIRE(M / 64 < 65535, "M too large");
   const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   f32g::Args a{};
   a.A = reinterpret_cast<const float*>(A);
@@ -529,9 +549,17 @@ extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const 
   a.alpha = alpha; a.beta = beta;
   a.vec = al(A) && al(B) && lda % 4 == 0 && ldb % 4 == 0;
   if (K == 0) a.alpha = 0.f;  // C = beta C
-  const dim3 grid((unsigned)((N + f32g::T - 1) / f32g::T), (unsigned)((M + f32g::T - 1) / f32g::T));
   hipStream_t st = as_stream(stream);
-  if (bt) hipLaunchKernelGGL(f32g::k_gemm_f32<1>, grid, 256, 0, st, a);
-  else hipLaunchKernelGGL(f32g::k_gemm_f32<0>, grid, 256, 0, st, a);
+  // 128^2 tiles where they fill the chip, 64^2 below (4x the workgroups)
+  const int64_t t128 = ((N + 127) / 128) * ((M + 127) / 128);
+  if (t128 >= 256) {
+    const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128));
+    if (bt) hipLaunchKernelGGL((f32g::k_gemm_f32<1, 128>), grid, 256, 0, st, a);
+    else hipLaunchKernelGGL((f32g::k_gemm_f32<0, 128>), grid, 256, 0, st, a);
+  } else {
+    const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64));
+    if (bt) hipLaunchKernelGGL((f32g::k_gemm_f32<1, 64>), grid, 256, 0, st, a);
+    else hipLaunchKernelGGL((f32g::k_gemm_f32<0, 64>), grid, 256, 0, st, a);
+  }
   return check_launch("lcq_gemm_f32");
 }

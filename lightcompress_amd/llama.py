@@ -60,11 +60,30 @@ def _lcq_sdpa(module, query, key, value, attention_mask, dropout=0.0, scaling=No
                       scaling=scaling, is_causal=is_causal, **kwargs)
 
 
+def _linear_wb(m):
+    """(weight, bias) of a module whose forward is exactly x W^T + b through lcq_linear: an
+    nn.Linear, or a weight-only fake-quant linear (its fake-quantised weight, materialised the
+    way its own first forward would); None for anything else."""
+    from .module_utils import EffcientFakeQuantLinear, FakeQuantLinear
+    t = type(m)
+    if t is nn.Linear:
+        return m.weight, m.bias
+    if t is EffcientFakeQuantLinear and m.a_qdq is None:
+        return m.weight, m.bias
+    if (t is FakeQuantLinear and m.a_qdq is None and not m.dynamic_quant_weight
+            and not m.dynamic_quant_tmp_weight):
+        if not hasattr(m, 'tmp_weight'):  # FakeQuantLinear.forward's first call
+            m.register_buffer('tmp_weight', m.w_qdq(m), persistent=False)
+            m.tmp_bias = m.bias
+        return m.tmp_weight, m.tmp_bias
+    return None
+
+
 def _input_only_hooked(*mods):
-    """nn.Linear modules whose hooks (if any) all read only the module inputs (the capture
-    hooks of algorithms whose add_batch ignores the output, marked `_lcq_input_only` by
-    BaseBlockwiseQuantization.register_hooks)."""
-    return all(type(m) is nn.Linear and all(
+    """Linear-like modules (_linear_wb) whose hooks (if any) all read only the module inputs
+    (the capture hooks of algorithms whose add_batch ignores the output, marked
+    `_lcq_input_only` by BaseBlockwiseQuantization.register_hooks)."""
+    return all(_linear_wb(m) is not None and all(
         getattr(h, '_lcq_input_only', False)
         for h in (*m._forward_pre_hooks.values(), *m._forward_hooks.values()))
         for m in mods)
@@ -89,12 +108,13 @@ def _gate_up_silu(mlp, x):
     from .module_utils import _GEMM_ON
     gp, up = mlp.gate_proj, mlp.up_proj
     if (_GEMM_ON and getattr(mlp.config, 'hidden_act', None) == 'silu'
-            and _input_only_hooked(gp, up) and gp.bias is None and up.bias is None
-            and ops.gemm_supported(x, gp.weight, up.weight)
-            and gp.weight.stride(0) == up.weight.stride(0)):
-        _fire_input_hooks(gp, x)
-        _fire_input_hooks(up, x)
-        return ops.linear_silu_mul(x, gp.weight, up.weight)
+            and _input_only_hooked(gp, up)):
+        (gw, gb), (uw, ub) = _linear_wb(gp), _linear_wb(up)
+        if (gb is None and ub is None and ops.gemm_supported(x, gw, uw)
+                and gw.stride(0) == uw.stride(0)):
+            _fire_input_hooks(gp, x)
+            _fire_input_hooks(up, x)
+            return ops.linear_silu_mul(x, gw, uw)
     g = gp(x)
     u = up(x)
     if g.is_cuda and g.dtype in (torch.bfloat16, torch.float16) and g.shape == u.shape \
@@ -167,15 +187,20 @@ def qkv_proj(attn, xn, weights=None):
     from . import ops
     from .module_utils import _GEMM_ON
     mods = (attn.q_proj, attn.k_proj, attn.v_proj)
-    ws = list(weights) if weights is not None else [m.weight for m in mods]
-    if (_GEMM_ON and (weights is not None or _input_only_hooked(*mods))
-            and ops.gemm_supported(xn, *ws) and len({w.stride(0) for w in ws}) == 1
+    fused = weights is not None or _input_only_hooked(*mods)
+    if weights is not None:
+        ws, bs = list(weights), [m.bias for m in mods]
+    elif fused:
+        wb = [_linear_wb(m) for m in mods]
+        ws, bs = [w for w, _ in wb], [b for _, b in wb]
+    if (_GEMM_ON and fused and ops.gemm_supported(xn, *ws)
+            and len({w.stride(0) for w in ws}) == 1
             and all(w.shape[0] % 256 == 0 for w in ws[:2])
-            and all(m.bias is None or m.bias.dtype == xn.dtype for m in mods)):
+            and all(b is None or b.dtype == xn.dtype for b in bs)):
         if weights is None:  # input-capture hooks fire first, in module order
             for m in mods:
                 _fire_input_hooks(m, xn)
-        return ops.linear_multi(xn, ws, [m.bias for m in mods])
+        return ops.linear_multi(xn, ws, bs)
     if weights is not None:
         from .module_utils import lcq_linear
         return [lcq_linear(xn, w, m.bias) for w, m in zip(ws, mods)]
