@@ -595,17 +595,13 @@ def bench_fp8(args, rank, world, dev):
                         f'block-fp8 source -> bf16 -> FP8 e4m3 per-tensor real quant; '
                         f'{E} experts x 3 linears per rank per step'),
            'lcq_kernels': kernel_table(kern, elapsed)}
-    stream = 'lcq_fp8_block_to_tensor_stream' in kern
-    t = kern.get('lcq_fp8_block_to_tensor_stream') or kern.get('lcq_fp8_block_to_tensor_many')
+    t = kern.get('lcq_fp8_block_to_tensor_many')
     if t:
         # algorithmic bytes per expert linear: 1 B fp8 read + 1 B fp8 written per element
         gbs = elems * 2.0 * t['launches'] / (t['total_ms'] * 1e-3) / 1e9
-        traffic, src = pmc_traffic('fp8', ('k_b2t_stream',) if stream else
-                                   ('k_bmax16_many', 'k_requant16_many'))
-        out['roofline'] = {'kernel': ('lcq_fp8_block_to_tensor_stream (k_b2t_stream: one '
-                                      'persistent launch, amax / requant items interleaved)'
-                                      if stream else 'lcq_fp8_block_to_tensor_many '
-                                      '(k_bmax16_many + k_requant16_many)'), 'bound': 'hbm',
+        traffic, src = pmc_traffic('fp8', ('k_bmax16_many', 'k_requant16_many'))
+        out['roofline'] = {'kernel': 'lcq_fp8_block_to_tensor_many (k_bmax16_many + '
+                                     'k_requant16_many)', 'bound': 'hbm',
                            'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                            'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic,
                            'traffic_source': src, 'avg_launch_ms': round(t['avg_ms'], 4)}

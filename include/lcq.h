@@ -425,21 +425,6 @@ int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t max_elems, in
                                  int block, int fmt_out, float qmax, float clamp_min,
                                  int add_zero, void* amax_ws, void* scales_out, void* stream);
 
-/* lcq_fp8_block_to_tensor_many in one persistent launch (same codes and scales, bit for bit)
- * for block 128 and tensors with N % 16 == 0, 16-byte aligned codes / outputs and
- * M * N < 2^28: the amax and requant passes of consecutive tensors interleave, so the
- * re-read comes from the Infinity Cache (2 B of HBM traffic per element instead of 3).
- * plan: device int32 [2n + 1 + 2n + n]: the exclusive prefix of work items (32768 16-byte
- * chunks each) over 2n segments, plan[2n] = total; then each segment's code (2 L for the amax
- * items P1(L), 2 L + 1 for the requant items P2(L); P1(L) precedes P2(L), every tensor's
- * segments hold ceil(M_L * N_L / 524288) items); then, per tensor, the index of its P1
- * segment. The grid is 4 workgroups per CU; order the segments so that P2(L) starts >= 1.25
- * grids of items after P1(L) ends (ops.fp8_block_to_tensor_many). ws: >= 2n + 1 uint32
- * (zeroed here on the stream). */
-int lcq_fp8_block_to_tensor_stream(int n, const void* descs, const void* plan, int fmt_in,
-                                   int fmt_out, float qmax, float clamp_min, int add_zero,
-                                   void* ws, void* scales_out, void* stream);
-
 /* Block-scaled FP8 GEMM (fp8_gemm, kernel.py:141-242, called by block_wise_fp8_forward_func,
  * module_utils.py:41-46, for LlmcFp8Linear / fp8_forward linears): a [M, K] e4m3 codes with
  * per-token 128-column scales a_s fp32 [M, K/128] (act_quant); b [N, K] e4m3 codes with

@@ -102,8 +102,6 @@ SIGNATURES = {
                                  _vp, _vp, _vp], _int),
     'lcq_fp8_block_to_tensor_many': ([_int, _vp, _i64, _int, _int, _int, _f32, _f32, _int, _vp,
                                       _vp, _vp], _int),
-    'lcq_fp8_block_to_tensor_stream': ([_int, _vp, _vp, _int, _int, _f32, _f32, _int, _vp, _vp,
-                                        _vp], _int),
     'lcq_minmax_segments': ([_vp, _vp, _i64, _int, _vp, _vp, _vp], _int),
     'lcq_act_static_qparams': ([_vp, _i64, _int, _f32, _int, _int, _int, _f32, _f32, _vp, _vp],
                                _int),

@@ -265,8 +265,9 @@ class BlockwiseOpt:
         if hasattr(self.model, 'clear_block_cache'):
             self.model.clear_block_cache(block)
 
-    # (entries, tokens per entry) while block_forward runs several calibration entries as one
-    # stacked batch, else None
+    # rows (tokens) of each calibration entry while block_forward runs several entries as one
+    # stacked batch, else None; entries may differ in batch size (a token shard can cut an
+    # entry part-way, _shard_input_tokens)
     _batch_ctx = None
 
     def entry_view(self, m, inp):
@@ -278,16 +279,19 @@ class BlockwiseOpt:
         one (ExpertList tags each expert's linears with the global token index of every row)
         becomes the list of its non-empty per-entry row blocks, in entry order, each in the
         order the reference's single-entry forward produces them. Other inputs pass as is."""
-        ctx = self._batch_ctx
-        if ctx is None or inp.dim() != 2:
+        counts = self._batch_ctx
+        if counts is None or inp.dim() != 2:
             return inp
-        n, tpe = ctx
+        n = len(counts)
         rows = getattr(m, '_lcq_rows', None)
         if rows is None or rows.numel() != inp.shape[0]:
-            if inp.shape[0] == n * tpe:
-                return inp.view(n, tpe, inp.shape[-1])
-            return inp
-        ent = torch.div(rows, tpe, rounding_mode='floor')
+            if inp.shape[0] != sum(counts):
+                return inp
+            if all(c == counts[0] for c in counts):
+                return inp.view(n, counts[0], inp.shape[-1])
+            return list(torch.split(inp, counts, dim=0))
+        bounds = torch.tensor(counts, device=rows.device).cumsum(0)[:-1]
+        ent = torch.bucketize(rows, bounds, right=True)
         order = torch.argsort(ent, stable=True)
         counts = torch.bincount(ent, minlength=n).tolist()
         xs = inp.index_select(0, order)
@@ -543,8 +547,7 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
             if xb is None:
                 xb = torch.cat(list(input_data), dim=0)
                 self._cat_cache = (list(input_data), xb)
-            x0 = input_data[0]
-            self._batch_ctx = (len(input_data), x0.numel() // x0.shape[-1])
+            self._batch_ctx = [x.numel() // x.shape[-1] for x in input_data]
             try:
                 y = self._call_block(block, xb, kwargs[0], stop_after)
             finally:

@@ -547,149 +547,6 @@ __global__ void __launch_bounds__(256) k_requant16_many(const Fp8Desc* d, Fp8Des
   }
 }
 
-// ---- one-launch streaming form of the batched deploy (block 128, fast16 tensors) ---------
-// The two-pass pair above reads every code twice from HBM (pass 2 starts after pass 1 has
-// swept all tensors, far beyond the 256 MB MALL): 3 B of traffic per element. Here one
-// persistent grid walks a single work list P1(0) .. P1(D-1) P1(D) P2(0) P1(D+1) P2(1) ...
-// P2(n-1) (P1 = amax items, P2 = requant items, B2T_ITEM 16-byte chunks each; the host picks
-// the lag D so that >= 1.25 grids of items separate P1(L) from P2(L): the requant items
-// rarely wait); workgroup b takes items b, b + G, ... in order. A P1 item folds its byte-max amax into amax[L] (device
-// atomic max of the float bits) and then bumps done[L]; a P2 item of tensor L waits
-// for done[L] == #P1 items of L, so it re-reads codes that were streamed one tensor
-// earlier (~15-30 MB back: MALL, not HBM) -> 2 B of HBM traffic per element. Every dependency
-// points to a smaller item index and workgroups take their items in increasing order, so with
-// the whole grid resident (G = 4 per CU) the smallest unfinished item can always run; the spin
-// is bounded anyway (err flag, no hang). Codes equal the two-pass path's bit for bit (same
-// per-chunk arithmetic; max is order-independent).
-constexpr int B2T_ITEM = 32768;  // 16-byte chunks per work item (512 KB of codes)
-
-template <int FIN, int FOUT, bool ADD_ZERO>
-__global__ void __launch_bounds__(256) k_b2t_stream(const Fp8Desc* __restrict__ d,
-                                                    const int* __restrict__ plan, int n,
-                                                    uint32_t* ws, float qmax, float clamp_min,
-                                                    float* s_out) {
-  __shared__ uint32_t red[4];
-  __shared__ float sc_sh;
-  uint32_t* amax = ws;
-  uint32_t* done = ws + n;
-  uint32_t* err = ws + 2 * n;
-  const int nseg = 2 * n, nitems = plan[nseg];
-  const int* segc = plan + nseg + 1;  // segment code: tensor * 2 + (1 for a requant segment)
-  const int* p1s = segc + nseg;       // index of tensor L's amax segment
-  int g = 0;                          // items only grow: walk the segments forward
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
-    while (plan[g + 1] <= it) ++g;
-    const int L = segc[g] >> 1;
-    const bool p1 = (segc[g] & 1) == 0;
-    const Fp8Desc t = d[L];
-    const int nc = (int)(t.N >> 4), nbc = (int)((t.N + 127) >> 7);
-    const int nk = (int)(t.M * t.N >> 4);
-    const float fr = 1.0f / (float)nc;
-    const int k0 = (it - plan[g]) * B2T_ITEM;
-    const int k1 = min(nk, k0 + B2T_ITEM);
-    if (p1) {
-      uint32_t am = 0;
-      for (int kb = k0 + (int)threadIdx.x; kb < k1; kb += 256 * 4) {
-        uint4 u[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (kb + j * 256 < k1) u[j] = reinterpret_cast<const uint4*>(t.codes)[kb + j * 256];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = kb + j * 256;
-          if (k < k1) {
-            int row, c16;
-            chunk_rc(k, nc, fr, row, c16);
-            const float sc = fabsf(t.s_inv[(row >> 7) * nbc + (c16 >> 3)]);
-            const float w = bf16_rne(dec<FIN>(absbyte_max16(u[j])) * sc);
-            am = max(am, __float_as_uint(w) & 0x7fffffffu);
-          }
-        }
-      }
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, m, 64));
-      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const uint32_t m = max(max(red[0], red[1]), max(red[2], red[3]));
-        // relaxed device-scope RMWs (performed past the per-XCD L2s); the returning max
-        // completes before the count is bumped. No release / acquire fences: at agent scope
-        // they write back / invalidate the whole L2, and the only data handed over is these
-        // two words
-        const uint32_t prev =
-            __hip_atomic_fetch_max(&amax[L], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
-        __hip_atomic_fetch_add(&done[L], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else {
-      if (threadIdx.x == 0) {
-        const int gp = p1s[L];
-        const uint32_t need = (uint32_t)(plan[gp + 1] - plan[gp]);
-        int spins = 0;
-        while (__hip_atomic_load(&done[L], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-          __builtin_amdgcn_s_sleep(8);
-          if (++spins > (1 << 22)) {  // never expected: report, do not hang the device
-            __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-        const float am = __uint_as_float(
-            __hip_atomic_load(&amax[L], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        sc_sh = fp8_scale<LCQ_BF16, LCQ_F32>(am, qmax, clamp_min, ADD_ZERO);
-      }
-      __syncthreads();
-      const float sc = sc_sh;
-      const float rs = 1.0f / sc;  // RN(1/s): Markstein's reciprocal
-      const v2f_t s2 = {sc, sc}, r2 = {rs, rs};
-      if (it == plan[g] && threadIdx.x == 0) s_out[L] = sc;
-      for (int kb = k0 + (int)threadIdx.x; kb < k1; kb += 256 * 4) {
-        uint4 u[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (kb + j * 256 < k1) u[j] = reinterpret_cast<const uint4*>(t.codes)[kb + j * 256];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = kb + j * 256;
-          if (k >= k1) continue;
-          int row, c16;
-          chunk_rc(k, nc, fr, row, c16);
-          const float si = t.s_inv[(row >> 7) * nbc + (c16 >> 3)];
-          const v2f_t si2 = {si, si};
-          const uint32_t in[4] = {u[j].x, u[j].y, u[j].z, u[j].w};
-          v2f_t q[8];
-          uint32_t big = 0;
-#pragma unroll
-          for (int p = 0; p < 8; ++p) {
-            const v2f_t d2 =
-                (p & 1) ? hw_dec2<FIN, true>(in[p >> 1]) : hw_dec2<FIN, false>(in[p >> 1]);
-            const v2f_t w = bf16r_pk(d2 * si2);
-            const v2f_t q0 = w * r2;
-            const v2f_t e = __builtin_elementwise_fma(-s2, q0, w);
-            v2f_t v = bf16r_pk(__builtin_elementwise_fma(e, r2, q0));
-            if constexpr (ADD_ZERO) v = v + (v2f_t){0.0f, 0.0f};
-            q[p] = v;
-            big = max(big, max(__float_as_uint(v.x) & 0x7fffffffu,
-                               __float_as_uint(v.y) & 0x7fffffffu));
-          }
-          uint4 o;
-          uint32_t* op = reinterpret_cast<uint32_t*>(&o);
-          if (big <= enc_hw_limit<FOUT>()) {
-#pragma unroll
-            for (int p = 0; p < 4; ++p) op[p] = hw_enc4<FOUT>(q[2 * p], q[2 * p + 1]);
-          } else {
-#pragma unroll
-            for (int p = 0; p < 4; ++p)
-              op[p] = enc<FOUT>(q[2 * p].x) | (enc<FOUT>(q[2 * p].y) << 8) |
-                      (enc<FOUT>(q[2 * p + 1].x) << 16) | (enc<FOUT>(q[2 * p + 1].y) << 24);
-          }
-          reinterpret_cast<uint4*>(t.out)[k] = o;
-        }
-      }
-    }
-    __syncthreads();  // red / sc_sh reused by the next item
-  }
-}
-
 // ---- block dequant: out = rnd_out(float(code) * s[block])  (weight_cast_to_bf16) --------
 template <int FMT, int OT>
 __global__ void __launch_bounds__(256) k_fp8_dequant_blocks(const uint8_t* codes,
@@ -1065,44 +922,6 @@ extern "C" int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t ma
   return block_to_tensor(n, reinterpret_cast<const Fp8Desc*>(descs), Fp8Desc{}, max_elems,
                          fmt_in, block, fmt_out, qmax, clamp_min, add_zero, amax_ws,
                          reinterpret_cast<float*>(scales_out), as_stream(stream));
-}
-
-extern "C" int lcq_fp8_block_to_tensor_stream(int n, const void* descs, const void* plan,
-                                              int fmt_in, int fmt_out, float qmax,
-                                              float clamp_min, int add_zero, void* ws,
-                                              void* scales_out, void* stream) {
-  LCQ_REQUIRE(n > 0 && descs && plan && ws && scales_out && qmax > 0.f, "bad batch");
-  LCQ_REQUIRE(fmt_in == LCQ_FP8E4M3 || fmt_in == LCQ_FP8E5M2, "bad input format");
-  LCQ_REQUIRE(fmt_out == LCQ_FP8E4M3 || fmt_out == LCQ_FP8E5M2, "bad output format");
-  hipStream_t st = as_stream(stream);
-  if (hipMemsetAsync(ws, 0, (size_t)(2 * n + 1) * 4, st) != hipSuccess)
-    return check_launch("lcq_fp8_block_to_tensor_stream: counters");
-  int dev = 0, cus = 256;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const dim3 grid((unsigned)(4 * cus));  // 4 per CU (tiny kernel): the whole grid is resident
-  const auto* d = reinterpret_cast<const Fp8Desc*>(descs);
-  const auto* pl = reinterpret_cast<const int*>(plan);
-  auto* w = reinterpret_cast<uint32_t*>(ws);
-  auto* so = reinterpret_cast<float*>(scales_out);
-#define LCQ_B2T(FI, FO)                                                                     \
-  do {                                                                                       \
-    if (add_zero)                                                                            \
-      hipLaunchKernelGGL((k_b2t_stream<FI, FO, true>), grid, 256, 0, st, d, pl, n, w, qmax,  \
-                         clamp_min, so);                                                     \
-    else                                                                                     \
-      hipLaunchKernelGGL((k_b2t_stream<FI, FO, false>), grid, 256, 0, st, d, pl, n, w, qmax, \
-                         clamp_min, so);                                                     \
-  } while (0)
-  if (fmt_in == LCQ_FP8E4M3) {
-    if (fmt_out == LCQ_FP8E4M3) LCQ_B2T(LCQ_FP8E4M3, LCQ_FP8E4M3);
-    else LCQ_B2T(LCQ_FP8E4M3, LCQ_FP8E5M2);
-  } else {
-    if (fmt_out == LCQ_FP8E4M3) LCQ_B2T(LCQ_FP8E5M2, LCQ_FP8E4M3);
-    else LCQ_B2T(LCQ_FP8E5M2, LCQ_FP8E5M2);
-  }
-#undef LCQ_B2T
-  return check_launch("lcq_fp8_block_to_tensor_stream");
 }
 
 extern "C" int lcq_fp_emul_quant(const void* x, int x_dtype, int64_t rows, int64_t cols,

@@ -6,7 +6,6 @@ through ``_native``. There is no CPU path: CPU tensors raise ``LcqError``.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -837,38 +836,6 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
         rec += [N.ptr(c), N.ptr(s), N.ptr(o), M, Nn]
     sc = torch.empty(n, dtype=torch.float32, device=dev)
     qmax = fp8_max(fp8) if qmax is None else float(qmax)
-    if block == 128 and os.environ.get('LCQ_FP8_DEPLOY') == 'stream' and all(
-            c.shape[1] % 16 == 0 and c.numel() < (1 << 28) and N.ptr(c) % 16 == 0 and
-            N.ptr(o) % 16 == 0 for c, o in zip(codes, outs)):
-        # opt-in: one persistent launch (lcq_fp8_block_to_tensor_stream; bit-identical, but
-        # measured 0.98 ms vs the pair's 0.86 ms over 96 DSv3 expert linears,
-        # profiles/r2s4_fp8_deploy_ab.txt). Work items of 524288 codes, P2(L) lagging P1(L)
-        items = [-(-c.numel() // 524288) for c in codes]
-        grid = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-        cum = [0]
-        for v in items:
-            cum.append(cum[-1] + v)
-        codes_seq, L2 = [], 0
-        for L in range(n):  # P2(L2) follows once >= 1.25 grids of items lie after P1(L2)
-            codes_seq.append(2 * L)
-            while L2 < L and cum[L + 1] - cum[L2 + 1] >= 1.25 * grid:
-                codes_seq.append(2 * L2 + 1)
-                L2 += 1
-        codes_seq += [2 * L + 1 for L in range(L2, n)]
-        plan, p1s = [0], [0] * n
-        for gi, sc_ in enumerate(codes_seq):
-            plan.append(plan[-1] + items[sc_ >> 1])
-            if sc_ % 2 == 0:
-                p1s[sc_ >> 1] = gi
-        host = torch.tensor(rec + plan + codes_seq + p1s, dtype=torch.int64)
-        dbuf = host.to(dev)
-        descs = dbuf[:5 * n]
-        plan_d = dbuf[5 * n:].to(torch.int32)
-        ws = torch.empty(2 * n + 1, dtype=torch.int32, device=dev)
-        N.call('lcq_fp8_block_to_tensor_stream', n, N.ptr(descs), N.ptr(plan_d),
-               N.dt(codes[0].dtype), N.dt(fp8), qmax, 1e-5, 1, N.ptr(ws), N.ptr(sc),
-               N.stream_of(codes[0]))
-        return outs, sc
     descs = torch.tensor(rec, dtype=torch.int64).to(dev, non_blocking=False)
     ws = torch.empty(n * FP8_PARTIALS, dtype=torch.float32, device=dev)
     N.call('lcq_fp8_block_to_tensor_many', n, N.ptr(descs), max(c.numel() for c in codes),

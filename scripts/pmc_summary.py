@@ -19,8 +19,7 @@ KEYS = {'k_syrk_x': 'k_syrk_x', 'k_tree_sum': 'k_tree_sum', 'k_syrk16': 'k_syrk1
         'k_gptq_trailing': 'k_gptq_trailing', 'k_xt_pack': 'k_xt_pack',
         'k_requant_blockfp8_many': 'k_requant_blockfp8_many',
         'k_absmax_blockfp8_many': 'k_absmax_blockfp8_many',
-        'k_bmax16_many': 'k_bmax16_many', 'k_requant16_many': 'k_requant16_many',
-        'k_b2t_stream': 'k_b2t_stream'}
+        'k_bmax16_many': 'k_bmax16_many', 'k_requant16_many': 'k_requant16_many'}
 
 
 def load(path):

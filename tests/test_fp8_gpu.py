@@ -343,27 +343,3 @@ def test_fp8_gemm_f16_default_dtype(dev):
         want = O.fp8_gemm(a, a_s, b, b_s)
         tol = 1e-5 * _abs_gemm(a, a_s, b, b_s) + want.abs() * 2.0 ** -11
         assert ((got.float() - want).abs() <= tol).all()
-
-
-@pytest.mark.parametrize('fin,fout', [(torch.float8_e4m3fn, torch.float8_e4m3fn),
-                                      (torch.float8_e5m2, torch.float8_e4m3fn),
-                                      (torch.float8_e4m3fn, torch.float8_e5m2)])
-def test_block_fp8_to_tensor_stream_equals_pair(dev, fin, fout, monkeypatch):
-    """The one-launch streaming deploy (lcq_fp8_block_to_tensor_stream: amax and requant items
-    of consecutive tensors interleaved, device-scope completion counters) gives the two-pass
-    pair's codes and scales bit for bit, over a list of 13 expert-shaped / small tensors with
-    every finite input code (tensor 0 alone, tensors of one item and of many)."""
-    from lightcompress_amd import ops
-    shapes = [(2048, 7168), (7168, 2048), (128, 128), (2048, 7168), (256, 512)] * 2 + \
-        [(384, 144), (16, 4096), (7168, 2048)]
-    cs, ss = zip(*[_random_block_fp8(sh, fin, 70 + i, dev) for i, sh in enumerate(shapes)])
-    for lst in (list(range(len(shapes))), [0], [2, 4]):
-        c_l, s_l = [cs[i] for i in lst], [ss[i] for i in lst]
-        monkeypatch.setenv('LCQ_FP8_DEPLOY', 'stream')
-        o1, sc1 = ops.fp8_block_to_tensor_many(c_l, s_l, 128, fout)
-        monkeypatch.delenv('LCQ_FP8_DEPLOY')
-        o2, sc2 = ops.fp8_block_to_tensor_many(c_l, s_l, 128, fout)
-        torch.cuda.synchronize()
-        for a, b in zip(o1, o2):
-            assert torch.equal(bits(a), bits(b))
-        assert torch.equal(sc1, sc2)

@@ -84,3 +84,30 @@ def test_dsv3_moe_subsets_cover_every_expert():
     assert len(downs) == 5
     assert model.get_moe_gate(model.get_blocks()[1]) is not None
     assert model.get_moe_gate(model.get_blocks()[0]) is None
+
+
+def test_entry_view_unequal_entries():
+    """A token shard can cut a calibration entry part-way (_shard_input_tokens), so the
+    entries of one stacked forward may differ in batch size: 2-D linear inputs are split back
+    per entry by their own row counts (dense: contiguous blocks; routed: by global row index)."""
+    from types import SimpleNamespace
+    from lightcompress_amd.base_blockwise_quantization import BaseBlockwiseQuantization as B
+    counts = [3 * 4, 1 * 4, 2 * 4]  # entries of batch 3, 1, 2 at 4 tokens each
+    ctx = SimpleNamespace(_batch_ctx=counts)
+    x = torch.arange(sum(counts) * 2, dtype=torch.float32).view(-1, 2)
+    dense = B.entry_view(ctx, SimpleNamespace(), x)
+    assert [t.shape[0] for t in dense] == counts
+    assert torch.equal(torch.cat(dense), x)
+    # equal entries keep the [entries, tokens, C] view
+    ctx._batch_ctx = [4, 4, 4]
+    assert B.entry_view(ctx, SimpleNamespace(), x[:12]).shape == (3, 4, 2)
+    # routed rows: global token indices 0..23 over entries [0,12), [12,16), [16,24)
+    ctx._batch_ctx = counts
+    rows = torch.tensor([20, 1, 13, 11, 15, 23])
+    m = SimpleNamespace(_lcq_rows=rows)
+    xr = torch.arange(6, dtype=torch.float32).view(6, 1)
+    got = B.entry_view(ctx, m, xr)
+    assert [t.flatten().tolist() for t in got] == [[1.0, 3.0], [2.0, 4.0], [0.0, 5.0]]
+    # no stacked forward: inputs pass unchanged
+    ctx._batch_ctx = None
+    assert B.entry_view(ctx, m, xr) is xr
