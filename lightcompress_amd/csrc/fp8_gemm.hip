@@ -7,8 +7,9 @@
 // A [M, K] e4m3 (act_quant output, per-token 128-column scales a_s [M, K/128]); B [N, K] e4m3
 // with 128x128 block scales b_s [ceil(N/128), K/128]; fp32 accumulation; C fp32 / bf16 / fp16.
 //
-// Two kernels: k_fp8_gemm2 (below, 256x256 tiles on the 16x16x128 MFMA) for grids of >= 64
-// tiles, and k_fp8_gemm for short batches:
+// Three kernels: k_fp8_gemm2 (256x256 tiles) and k_fp8_gemm2_128 (128x128 tiles, split-K on
+// small grids) on the 16x16x128 MFMA for batches of more than 64 rows (gemm2_plan picks the
+// tile), and k_fp8_gemm for batches of <= 64 rows:
 // Tile 128x128 (or 64x128 when the grid would be small) per workgroup, 4 waves on gfx950's
 // 32x32x64 f8f6f4 MFMA, one K block of 128 per step double-buffered through LDS (16-byte global
 // loads into registers one block ahead, padded rows); the block's partial dot products are
@@ -197,25 +198,30 @@ __global__ __launch_bounds__(256) void k_fp8_gemm_reduce(const float* __restrict
 }
 
 // ---------------------------------------------------------------------------------------
-// k_fp8_gemm2: 256 x 256 tile, 8 waves (2 per SIMD, 2 (M) x 4 (N), 128 x 64 each), gfx950's
+// gemm2_body<TM, WR, WC>: TM x TM tile, WR x WC waves of (TM/WR) x (TM/WC) each, gfx950's
 // 16x16x128 f8f6f4 MFMA: ONE instruction is the whole 128-wide scale block's dot product of a
 // 16 x 16 sub-tile, so the block scaling needs no second accumulator set: dot (4 VGPRs, C = 0)
 // then acc = fma(dot, a_s[m, kb] * b_s[n / 128, kb], acc) (4 FMAs, the lane's 4 values share
 // one row m in the swapped layout). The reference rounds (dot * a_s) * b_s + acc three times;
 // this rounds the scale product and one fma: <= 2 ulp of each block term (tested against the
-// oracle at 1e-5 of |a||b|). 128 accumulator VGPRs per wave, ~200 VGPRs: two waves per SIMD.
-// Operands stream through LDS by LDS-DMA (buffer_load ... lds, 16 B per lane; 8 pieces per wave
-// per K block) into two 64 KB buffers (A 256 x 128 B + B 256 x 128 B, 16-B chunks XOR-swizzled
-// by row & 7), plus the K block's 256 a_s values (kb-major copy made by k_as_transpose; 4 B
-// per lane from waves 0-3: an LDS-DMA lane writes a whole dword). One barrier per K block: after it the next K
-// block's loads go into the buffer every wave finished reading.
+// oracle at 1e-5 of |a||b|).
+//   256^2, 8 waves (2 per SIMD, 2 (M) x 4 (N), 128 x 64 each): 128 accumulator VGPRs per wave,
+//     ~200 VGPRs; for grids that fill the chip.
+//   128^2, 4 waves (one per SIMD, 64 x 64 each): 4x the tiles of the same problem, so a
+//     2048 x 2048 output (DSv3 expert gate / up at 2048 calibration tokens) is 256 workgroups
+//     instead of 64; smaller grids split K on top (fp32 partials summed in split order).
+// Operands stream through LDS by LDS-DMA (buffer_load ... lds, 16 B per lane; 8 rows of 128 B
+// per wave-instruction, 4 A and 4 B pieces per wave per K block in both instances) into two
+// stage buffers (A TM x 128 B + B TM x 128 B, 16-B chunks XOR-swizzled by row & 7), plus the K
+// block's TM a_s values (kb-major copy made by k_as_transpose; 4 B per lane from the first
+// TM / 64 waves: an LDS-DMA lane writes a whole dword). One barrier per K block: after it the
+// next K block's loads go into the buffer every wave finished reading.
 // ---------------------------------------------------------------------------------------
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
-constexpr int T2 = 256;                   // output tile (M and N)
-constexpr int OPB = T2 * BK;              // one operand tile: 256 rows x 128 B = 32 KB
-constexpr int STG = 2 * OPB + 1024;       // A + B + 256 fp32 a_s per K block
-constexpr int LDS2 = 2 * STG;             // double buffered: 130 KB
+
+template <int TM>
+constexpr int stage_bytes() { return 2 * TM * BK + TM * 4; }  // A + B + TM fp32 a_s
 
 struct Gemm2Args {
   const uint8_t* a;
@@ -250,11 +256,19 @@ __device__ __forceinline__ v8i frag2(const uint8_t* tile, int row, int q) {
              (int)hi.w};
 }
 
-__global__ __launch_bounds__(512, 1) void k_fp8_gemm2(Gemm2Args g) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+template <int TM, int WR, int WC, int NS>
+__device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds) {
+  constexpr int NW = WR * WC;                 // waves
+  constexpr int OPB = TM * BK;                // one operand tile
+  constexpr int STG = stage_bytes<TM>();
+  constexpr int WM = TM / WR, WN = TM / WC;   // wave tile
+  constexpr int MB = WM / 16, NB = WN / 16;
+  constexpr int PIECES = TM / (8 * NW);       // 8-row pieces per wave and operand
+  constexpr int LPS = 2 * PIECES + 1;         // loads per wave per stage (vmcnt units)
+  static_assert(PIECES * 8 * NW == TM && WN <= 128 && TM % 64 == 0, "tile shape");
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 2, wc = w & 3;
+  const int wr = w / WC, wc = w % WC;
   // XCD-aware order: the 32 workgroups an XCD runs at once take a 4 (M) x 8 (N) block
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -263,24 +277,21 @@ __global__ __launch_bounds__(512, 1) void k_fp8_gemm2(Gemm2Args g) {
   const int chunk = wg >> 5, sl = wg & 31, band = chunk / cpb, cc = chunk - band * cpb;
   const int tm = band * 4 + (sl >> 3), tn = cc * 8 + (sl & 7);
   if (tm >= g.nmt || tn >= g.nnt) return;
-  const int64_t m0 = (int64_t)tm * T2, n0 = (int64_t)tn * T2;
+  const int64_t m0 = (int64_t)tm * TM, n0 = (int64_t)tn * TM;
   const int64_t nkb = g.K / BK;
   const int64_t kb0 = (int64_t)blockIdx.z * g.kb_per_split;
   int64_t nk = nkb - kb0;
   if (nk > g.kb_per_split) nk = g.kb_per_split;
 
-  // staging: piece j (0..7) of wave w = 8 rows (w * 8 + j * 64 .. ) of A (j < 4) or B (j >= 4)
-  // 8 rows x 128 B = 64 lanes x 16 B; lane l -> row l / 8, physical chunk l % 8 = logical
-  // chunk (l % 8) ^ (row & 7)
+  // staging: piece j of wave w = rows j * 8 NW + w * 8 .. + 7 of A and of B; 8 rows x 128 B =
+  // 64 lanes x 16 B; lane l -> row l / 8, physical chunk l % 8 = logical chunk (l % 8) ^ (row & 7)
   const __amdgpu_buffer_rsrc_t ra = rsrc(g.a + m0 * g.K, (g.M - m0) * g.K);
   const __amdgpu_buffer_rsrc_t rb = rsrc(g.b + n0 * g.K, (g.N - n0) * g.K);
   const __amdgpu_buffer_rsrc_t rs = rsrc(g.ast + m0, (g.mp * nkb - m0) * 4);
-  uint32_t off[4];
-  int lrow[4];
+  uint32_t off[PIECES];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = j * 64 + w * 8 + (lane >> 3);
-    lrow[j] = row;
+  for (int j = 0; j < PIECES; ++j) {
+    const int row = j * 8 * NW + w * 8 + (lane >> 3);
     off[j] = (uint32_t)(row * g.K + (((lane & 7) ^ (row & 7)) * 16));
   }
   auto stage = [&](int buf, int64_t kbl) {  // kbl: K block index within the split
@@ -288,61 +299,64 @@ __global__ __launch_bounds__(512, 1) void k_fp8_gemm2(Gemm2Args g) {
     uint8_t* dst = lds + buf * STG;
     const int kofs = (int)(kb * BK);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(dst + (j * 64 + w * 8) * BK),
+    for (int j = 0; j < PIECES; ++j) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(dst + (j * 8 * NW + w * 8) * BK),
                                                16, off[j], kofs, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(dst + OPB +
-                                                                 (j * 64 + w * 8) * BK),
+                                                                 (j * 8 * NW + w * 8) * BK),
                                                16, off[j], kofs, 0, 0);
     }
-    // a_s of this K block: 256 floats = waves 0-3 x 64 lanes x 4 B (the K loop waits with
-    // vmcnt(0), so the per-wave piece counts need not match)
-    if (w < 4)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + 2 * OPB + w * 256), 4,
-                                               (uint32_t)(w * 256 + lane * 4),
-                                               (int)(kb * g.mp * 4), 0, 0);
+    // a_s of this K block: TM floats = TM / 64 pieces of 64 lanes x 4 B; wave w loads piece
+    // w % (TM / 64) (the waves past TM / 64 write the same bytes again) so that every wave
+    // issues LPS loads per stage and the K loop can wait with one counted vmcnt
+    const int sp = w % (TM / 64);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + 2 * OPB + sp * 256), 4,
+                                             (uint32_t)(sp * 256 + lane * 4),
+                                             (int)(kb * g.mp * 4), 0, 0);
   };
-  (void)lrow;
 
-  v4f acc[8][4];
+  v4f acc[MB][NB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MB; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NB; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   const v4f zero = {0.f, 0.f, 0.f, 0.f};
   const int r16 = lane & 15, q = lane >> 4;
-  int64_t nbr = (n0 + wc * 64) >> 7;  // this wave's 128-column scale block (clamped past N)
+  int64_t nbr = (n0 + wc * WN) >> 7;  // this wave's 128-column scale block (clamped past N)
   if (nbr > (g.N - 1) >> 7) nbr = (g.N - 1) >> 7;
   const float* bsrow = g.bs + nbr * nkb + kb0;
 
-  stage(0, 0);
+  // NS-stage ring: NS - 1 K blocks in flight ahead of the one being multiplied
+#pragma unroll
+  for (int j = 0; j + 1 < NS; ++j) stage(j, j);
   for (int64_t t = 0; t < nk; ++t) {
-    const int buf = (int)(t & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this K block's pieces landed
-    __builtin_amdgcn_s_barrier();                     // ... for every wave; buf ^ 1 is free
-    stage(buf ^ 1, t + 1);                            // past the end: re-fetch (unused)
+    const int buf = (int)(t % NS);
+    // this K block's pieces landed (the NS - 2 younger stages may still be in flight) ...
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * LPS) : "memory");
+    __builtin_amdgcn_s_barrier();  // ... for every wave; buffer (t - 1) % NS is free
+    stage((int)((t + NS - 1) % NS), t + NS - 1);  // past the end: re-fetch (unused)
     const uint8_t* At = lds + buf * STG;
     const uint8_t* Bt = At + OPB;
     const float* Sa = reinterpret_cast<const float*>(At + 2 * OPB);
     const float bsv = bsrow[t];
-    v8i bfr[4];
+    v8i bfr[NB];
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) bfr[nb] = frag2(Bt, wc * 64 + nb * 16 + r16, q);
-    float sc[8];
+    for (int nb = 0; nb < NB; ++nb) bfr[nb] = frag2(Bt, wc * WN + nb * 16 + r16, q);
+    float sc[MB];
 #pragma unroll
-    for (int mb = 0; mb < 8; ++mb) sc[mb] = Sa[wr * 128 + mb * 16 + r16] * bsv;
-    v8i afr = frag2(At, wr * 128 + r16, q);
+    for (int mb = 0; mb < MB; ++mb) sc[mb] = Sa[wr * WM + mb * 16 + r16] * bsv;
+    v8i afr = frag2(At, wr * WM + r16, q);
 #pragma unroll
-    for (int mb = 0; mb < 8; ++mb) {
+    for (int mb = 0; mb < MB; ++mb) {
       v8i anext = afr;
-      if (mb < 7) anext = frag2(At, wr * 128 + (mb + 1) * 16 + r16, q);
-      v4f d[4];
+      if (mb < MB - 1) anext = frag2(At, wr * WM + (mb + 1) * 16 + r16, q);
+      v4f d[NB];
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
+      for (int nb = 0; nb < NB; ++nb)
         d[nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[nb], afr, zero, 0, 0, 0, 0,
                                                                   0, 0);
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
+      for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[mb][nb][j] = __builtin_fmaf(d[nb][j], sc[mb], acc[mb][nb][j]);
       afr = anext;
@@ -351,14 +365,14 @@ __global__ __launch_bounds__(512, 1) void k_fp8_gemm2(Gemm2Args g) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // acc[mb][nb][j] (swapped layout): C[m0 + wr*128 + mb*16 + r16][n0 + wc*64 + nb*16 + 4q + j]
+  // acc[mb][nb][j] (swapped layout): C[m0 + wr*WM + mb*16 + r16][n0 + wc*WN + nb*16 + 4q + j]
 #pragma unroll
-  for (int mb = 0; mb < 8; ++mb) {
-    const int64_t m = m0 + wr * 128 + mb * 16 + r16;
+  for (int mb = 0; mb < MB; ++mb) {
+    const int64_t m = m0 + wr * WM + mb * 16 + r16;
     if (m >= g.M) continue;
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      const int64_t n = n0 + wc * 64 + nb * 16 + 4 * q;
+    for (int nb = 0; nb < NB; ++nb) {
+      const int64_t n = n0 + wc * WN + nb * 16 + 4 * q;
       if (n >= g.N) continue;
       const v4f v = acc[mb][nb];
       if (g.ws) {
@@ -382,6 +396,20 @@ __global__ __launch_bounds__(512, 1) void k_fp8_gemm2(Gemm2Args g) {
   }
 }
 
+// 256^2: 2 stages (133 KB; ~2000 MFMA cycles per K block cover the load latency); 128^2: 4
+// stages (133 KB; a K block is only ~500 MFMA cycles, measured 1.4 us per K block with 2)
+constexpr int NS256 = 2, NS128 = 4;
+
+__global__ __launch_bounds__(512, 1) void k_fp8_gemm2(Gemm2Args g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  gemm2_body<256, 2, 4, NS256>(g, lds);
+}
+
+__global__ __launch_bounds__(256, 1) void k_fp8_gemm2_128(Gemm2Args g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  gemm2_body<128, 2, 2, NS128>(g, lds);
+}
+
 // a_s [M, nkb] -> [nkb, mp] (rows past M zero)
 __global__ __launch_bounds__(256) void k_as_transpose(const float* __restrict__ as, int64_t M,
                                                       int64_t nkb, int64_t mp,
@@ -392,15 +420,24 @@ __global__ __launch_bounds__(256) void k_as_transpose(const float* __restrict__ 
   out[i] = m < M ? as[m * nkb + kb] : 0.f;
 }
 
-// split count for the 256^2 kernel: grids of fewer than 224 tiles split K (>= 4 K blocks each)
-int64_t gemm2_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = ((M + T2 - 1) / T2) * ((N + T2 - 1) / T2), nkb = K / BK;
-  if (tiles >= 224) return 1;
+// Tile plan of the MFMA-16x16x128 kernels: 256^2 tiles when they fill >= 7/8 of the chip,
+// else 128^2 tiles, with K split until ~256 workgroups (one per CU at this kernel's LDS) are in
+// flight, keeping >= 4 K blocks per split.
+struct Plan2 {
+  int tm;          // 256 or 128
+  int64_t splits;  // K splits (1: C written directly)
+};
+
+Plan2 gemm2_plan(int64_t M, int64_t N, int64_t K) {
+  const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256);
+  if (t256 >= 224) return {256, 1};
+  const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128), nkb = K / BK;
+  if (tiles >= 192) return {128, 1};
   int64_t s = (256 + tiles - 1) / tiles;
   if (s > nkb / 4) s = nkb / 4;
-  if (s < 2) return 1;
+  if (s < 2) return {128, 1};
   const int64_t per = (nkb + s - 1) / s;
-  return (nkb + per - 1) / per;
+  return {128, (nkb + per - 1) / per};  // no empty split
 }
 
 // K splits for a short batch: a 64-row grid of fewer than 256 tiles is split along K until
@@ -423,10 +460,10 @@ int64_t gemm_splits(int64_t M, int64_t N, int64_t K) {
 
 using namespace lcq;
 
-// workspace of the 256^2 kernel: the kb-major a_s copy, then the split-K partials
+// workspace of the 16x16x128 kernels: the kb-major a_s copy, then the split-K partials
 static int64_t ws2_bytes(int64_t M, int64_t N, int64_t K) {
-  const int64_t mp = (M + T2 - 1) / T2 * T2, nkb = K / BK;
-  const int64_t s = gemm2_splits(M, N, K);
+  const int64_t mp = (M + 255) / 256 * 256, nkb = K / BK;
+  const int64_t s = gemm2_plan(M, N, K).splits;
   return nkb * mp * 4 + (s > 1 ? s * M * N * 4 : 0);
 }
 
@@ -450,30 +487,35 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
                   (reinterpret_cast<uintptr_t>(b) & 15) == 0,
               "A / B must be 16-byte aligned");
   const int64_t nkb = K / BK;
-  const char* sel = getenv("LCQ_FP8_GEMM");  // 1 / 2: force the 64/128-row / the 256^2 kernel
-  // the 256^2 kernel on grids of >= 64 tiles (measured: 1.46 vs 1.01 PFLOP/s at 2048 x 7168 x
-  // 7168, 1.85 vs 1.30 at 8192^3, 65 vs 78 us at 2048 x 2048 x 7168 with 4 K splits), else the
-  // 64/128-row kernel (2x faster at M 512: the big tile's split-K partials cost more there)
-  const int64_t tiles2 = ((M + T2 - 1) / T2) * ((N + T2 - 1) / T2);
-  if (!(sel && sel[0] == '1') && (tiles2 >= 64 || (sel && sel[0] == '2')) && workspace &&
-      ws_bytes >= ws2_bytes(M, N, K) &&
-      N % 4 == 0 &&
+  // the 16x16x128 kernels from 128 rows up (measured at 2048 x 7168 x 7168: 1.46 vs 1.01
+  // PFLOP/s for the 256^2 tile against the 128-row 32x32x64 kernel below, 1.85 vs 1.30 at
+  // 8192^3); the 32x32x64 kernel keeps batches of <= 64 rows, where a 128-row tile is half empty
+  if (M > 64 && workspace && ws_bytes >= ws2_bytes(M, N, K) && N % 4 == 0 &&
       M * K < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31)) {
     hipStream_t st = as_stream(stream);
-    const int64_t mp = (M + T2 - 1) / T2 * T2;
-    const int64_t s2 = gemm2_splits(M, N, K);
+    const int64_t mp = (M + 255) / 256 * 256;
+    const Plan2 pl = gemm2_plan(M, N, K);
+    const int64_t s2 = pl.splits;
     float* ast = static_cast<float*>(workspace);
     float* part = s2 > 1 ? ast + nkb * mp : nullptr;
     hipLaunchKernelGGL(k_as_transpose, dim3((unsigned)((nkb * mp + 255) / 256)), 256, 0, st,
                        static_cast<const float*>(a_s), M, nkb, mp, ast);
     Gemm2Args g2{static_cast<const uint8_t*>(a), static_cast<const uint8_t*>(b), ast,
                  static_cast<const float*>(b_s), c, part, M, N, K, mp,
-                 (nkb + s2 - 1) / s2, c_dtype, (int)((M + T2 - 1) / T2),
-                 (int)((N + T2 - 1) / T2)};
+                 (nkb + s2 - 1) / s2, c_dtype, (int)((M + pl.tm - 1) / pl.tm),
+                 (int)((N + pl.tm - 1) / pl.tm)};
     const int nslots = 32 * ((g2.nmt + 3) / 4) * ((g2.nnt + 7) / 8);
-    (void)hipFuncSetAttribute((const void*)k_fp8_gemm2,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-    hipLaunchKernelGGL(k_fp8_gemm2, dim3((unsigned)nslots, 1, (unsigned)s2), 512, LDS2, st, g2);
+    if (pl.tm == 256) {
+      (void)hipFuncSetAttribute((const void*)k_fp8_gemm2,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, NS256 * stage_bytes<256>());
+      hipLaunchKernelGGL(k_fp8_gemm2, dim3((unsigned)nslots, 1, (unsigned)s2), 512,
+                         NS256 * stage_bytes<256>(), st, g2);
+    } else {
+      (void)hipFuncSetAttribute((const void*)k_fp8_gemm2_128,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, NS128 * stage_bytes<128>());
+      hipLaunchKernelGGL(k_fp8_gemm2_128, dim3((unsigned)nslots, 1, (unsigned)s2), 256,
+                         NS128 * stage_bytes<128>(), st, g2);
+    }
     if (s2 > 1) {
       const int rc = check_launch("lcq_fp8_gemm");
       if (rc) return rc;

@@ -229,24 +229,35 @@ def _gemm_inputs(M, Nn, K, seed):
     return a, a_s, b, b_s
 
 
+# The gfx950 f8f6f4 MFMAs (16x16x128 and 32x32x64) do not sum a 128-wide block like a
+# sequential fp32 loop: one block's dot product is off the exact sum by up to 2.7e-5 of
+# sum|a b| (scripts/fp8_mfma_precision.py, profiles/r3c_fp8_mfma_precision.txt: max 2.05e-5 /
+# 2.73e-5, mean 1.5e-6, unbiased on symmetric data). The reference's Triton tl.dot on this
+# chip issues the same instructions; the tolerance is that hardware bound with margin.
+GEMM_RTOL = 5e-5
+
+
 def _abs_gemm(a, a_s, b, b_s):
     return O.fp8_gemm(a.view(torch.uint8).bitwise_and(0x7F).view(torch.float8_e4m3fn), a_s.abs(),
                       b.view(torch.uint8).bitwise_and(0x7F).view(torch.float8_e4m3fn), b_s.abs())
 
 
-# ragged M / N tiles, one K block, the DeepSeek-V3 hidden size (K 7168)
+# ragged M / N tiles, one K block, the DeepSeek-V3 hidden size (K 7168); the tile plans of
+# fp8_gemm.hip: <= 64 rows (32x32x64 kernel), 128^2 split-K (256 x 512, 130 x 2048), 128^2
+# unsplit (1000 x 1500 ragged, 2048 x 1536), 256^2 (2048 x 7168)
 @pytest.mark.parametrize('M,Nn,K', [(1, 128, 128), (37, 200, 384), (256, 512, 1024),
-                                    (130, 2048, 7168)])
+                                    (130, 2048, 7168), (1000, 1500, 384), (2048, 1536, 256),
+                                    (2048, 7168, 256)])
 def test_fp8_gemm_vs_oracle(dev, M, Nn, K):
     """lcq_fp8_gemm vs the fp8_gemm restatement (kernel.py:141-214): same per-block scaling
-    order; only the fp32 accumulation order inside a 128-wide block differs (tolerance 1e-5 of
+    order; only the accumulation inside a 128-wide block differs (the MFMA's own, GEMM_RTOL of
     the |a||b| product)."""
     from lightcompress_amd import ops
     a, a_s, b, b_s = _gemm_inputs(M, Nn, K, seed=M * 7 + Nn)
     got = ops.fp8_gemm(a.to(dev), a_s.to(dev), b.to(dev), b_s.to(dev),
                        out_dtype=torch.float32).cpu()
     want = O.fp8_gemm(a, a_s, b, b_s)
-    tol = 1e-5 * _abs_gemm(a, a_s, b, b_s) + 1e-30
+    tol = GEMM_RTOL * _abs_gemm(a, a_s, b, b_s) + 1e-30
     err = (got - want).abs()
     assert (err <= tol).all(), float((err / tol).max())
 
@@ -263,7 +274,7 @@ def test_fp8_gemm_bf16_out_and_leading_dims(dev):
         torch.set_default_dtype(prev)
     assert got.dtype == torch.bfloat16 and got.shape == (2, 12, 384)
     want = O.fp8_gemm(a, a_s, b, b_s).reshape(2, 12, 384)
-    tol = 1e-5 * _abs_gemm(a, a_s, b, b_s).reshape(2, 12, 384) + want.abs() * 2.0 ** -8
+    tol = GEMM_RTOL * _abs_gemm(a, a_s, b, b_s).reshape(2, 12, 384) + want.abs() * 2.0 ** -8
     assert ((got.float() - want).abs() <= tol).all()
 
 
@@ -322,7 +333,7 @@ def test_fp8_gemm_split_k_matches_unsplit_and_is_deterministic(dev):
            N.dt(torch.float32), None, 0, N.stream_of(ad))
     assert torch.equal(split1, split2)
     want = O.fp8_gemm(a, a_s, b, b_s)
-    tol = 1e-5 * _abs_gemm(a, a_s, b, b_s) + 1e-30
+    tol = GEMM_RTOL * _abs_gemm(a, a_s, b, b_s) + 1e-30
     assert ((split1.cpu() - want).abs() <= tol).all()
     assert ((one.cpu() - want).abs() <= tol).all()
 
@@ -341,5 +352,5 @@ def test_fp8_gemm_f16_default_dtype(dev):
             torch.set_default_dtype(prev)
         assert got.dtype == torch.float16 and got.shape == (M, 384)
         want = O.fp8_gemm(a, a_s, b, b_s)
-        tol = 1e-5 * _abs_gemm(a, a_s, b, b_s) + want.abs() * 2.0 ** -11
+        tol = GEMM_RTOL * _abs_gemm(a, a_s, b, b_s) + want.abs() * 2.0 ** -11
         assert ((got.float() - want).abs() <= tol).all()
