@@ -529,6 +529,173 @@ __global__ void __launch_bounds__(256, 2) k_gemm_f32(Args a) {
       }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// k_gemm_f32d: the same product with LDS-DMA staging, for 16-byte aligned rows and K % 32 == 0
+// (every product of the recursion on 128-multiple Hessians). k_gemm_f32 above stages through
+// registers (per-element bounds checks, transposing scalar LDS stores) and measured 55-80 TF/s
+// (MFMA busy ~55 %, profiles/r3c_gemm_pmc.txt). Here:
+//  * 32-float K chunks of T rows land in LDS by buffer_load ... lds (16 B per lane, 8 rows x
+//    128 B per wave-instruction; rows / columns past the operand's end read as zero through
+//    the buffer descriptor's range) in an NS-stage ring, one barrier per chunk;
+//  * v_mfma_f32_16x16x4_f32 with the chunk's k permuted: lane group g = lane >> 4 supplies k =
+//    8g + s at step s (0..7) for both operands, so a lane's 8 values of a k-contiguous row are
+//    two ds_read_b128 (16-B chunks 2g, 2g + 1 of the row, swizzled by swz32 so that every
+//    16-lane group of the read hits 16 distinct bank slots). The k order of each output element
+//    is fixed (deterministic), not the sequential one: the recursion is checked at T2;
+//  * a k-major B [K, N] (bt = 0) is staged as [k][col] rows (T floats) with the 16-B chunks of
+//    row k XOR-ed by ((k >> 3) & 1) * 4 (lane groups g and g + 1 of one 32-lane half land 64 B
+//    apart) and read with ds_read_b32.
+// T x T tile per 256-thread workgroup (2 x 2 waves of T/2 x T/2, (T/32)^2 16x16 MFMA tiles
+// each): T = 128 where the grid fills the chip, 64 below.
+// ---------------------------------------------------------------------------------------
+typedef float v4f32 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+constexpr int DKC = 32;  // K chunk (floats): 128 B per k-contiguous row
+
+__device__ __forceinline__ int swz32(int row) { return ((row >> 1) & 1) | ((row >> 1) & 4); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t f32_rsrc(const float* p, int64_t bytes) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane(
+      (int)(bytes > 0x7fffffff ? 0x7fffffff : (bytes < 0 ? 0 : bytes)));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo),
+                                           (short)0, nb, 0x00020000);
+}
+
+template <int BT, int T, int NS>
+__global__ void __launch_bounds__(256, 1) k_gemm_f32d(Args a) {
+  constexpr int OPB = T * DKC * 4;        // one operand chunk image (bytes)
+  constexpr int STG = 2 * OPB;
+  constexpr int PA = T / 32;              // A pieces (8 rows x 128 B) per wave
+  constexpr int PB = T / 32;              // B pieces per wave (k-major: 1 KB of [k][col] rows)
+  constexpr int WT = T / 2, MT = WT / 16; // wave tile, 16x16 MFMA tiles per side
+  constexpr int LPS = PA + PB;            // DMA instructions per wave per stage
+  extern __shared__ __attribute__((aligned(16))) char f32lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int64_t r0 = (int64_t)blockIdx.y * T, c0 = (int64_t)blockIdx.x * T;
+  const int64_t nch = a.K / DKC;
+
+  const __amdgpu_buffer_rsrc_t ra = f32_rsrc(a.A + r0 * a.lda, (a.M - r0) * a.lda * 4);
+  __amdgpu_buffer_rsrc_t rb;
+  if constexpr (BT) rb = f32_rsrc(a.B + c0 * a.ldb, (a.N - c0) * a.ldb * 4);
+  else rb = f32_rsrc(a.B + c0, ((a.K - 1) * a.ldb + (a.N - c0)) * 4);
+  uint32_t aoff[PA], boff[PB];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {  // piece j of wave w: rows (j * 4 + w) * 8 .. + 7
+    const int row = (j * 4 + w) * 8 + (lane >> 3);
+    aoff[j] = (uint32_t)((row * a.lda + (((lane & 7) ^ swz32(row)) * 4)) * 4);
+  }
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    if constexpr (BT) {
+      const int row = (j * 4 + w) * 8 + (lane >> 3);
+      boff[j] = (uint32_t)((row * a.ldb + (((lane & 7) ^ swz32(row)) * 4)) * 4);
+    } else {  // [k][col] rows of T floats: a piece = 1024 / (4 T) k-rows
+      constexpr int CPR = T / 4;           // 16-B chunks per k-row
+      const int k = (j * 4 + w) * (256 / T) + lane / CPR, pc = lane % CPR;
+      const int lc = pc ^ (((k >> 3) & 1) * 4);
+      boff[j] = (uint32_t)((k * a.ldb + lc * 4) * 4);
+    }
+  }
+  auto stage = [&](int buf, int64_t ch) {
+    const int64_t cc = ch < nch ? ch : nch - 1;  // past the end: re-fetch (unused)
+    char* dst = f32lds + buf * STG;
+    // the chunk offset goes into voffset (not soffset), so the descriptor's range check covers
+    // every byte: past-the-end rows / columns read as zero and never leave the allocation
+    const uint32_t ka = (uint32_t)(cc * DKC * 4);
+    const uint32_t kbo = BT ? ka : (uint32_t)(cc * DKC * a.ldb * 4);
+#pragma unroll
+    for (int j = 0; j < PA; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(dst + (j * 4 + w) * 1024), 16,
+                                               aoff[j] + ka, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < PB; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (lds_void_t*)(dst + OPB + (j * 4 + w) * 1024), 16, boff[j] + kbo, 0, 0, 0);
+  };
+
+  v4f32 acc[MT][MT];
+#pragma unroll
+  for (int x = 0; x < MT; ++x)
+#pragma unroll
+    for (int y = 0; y < MT; ++y) acc[x][y] = v4f32{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, g = lane >> 4;
+
+#pragma unroll
+  for (int j = 0; j + 1 < NS; ++j) stage(j, j);
+  for (int64_t ch = 0; ch < nch; ++ch) {
+    const int buf = (int)(ch % NS);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * LPS) : "memory");
+    __builtin_amdgcn_s_barrier();
+    stage((int)((ch + NS - 1) % NS), ch + NS - 1);
+    const char* As = f32lds + buf * STG;
+    const char* Bs = As + OPB;
+    float av[MT][8], bv[MT][8];
+#pragma unroll
+    for (int x = 0; x < MT; ++x) {
+      const int row = wr * WT + x * 16 + r16;
+      const char* rp = As + row * 128;
+      const float4 lo = *reinterpret_cast<const float4*>(rp + ((2 * g) ^ swz32(row)) * 16);
+      const float4 hi = *reinterpret_cast<const float4*>(rp + ((2 * g + 1) ^ swz32(row)) * 16);
+      av[x][0] = lo.x; av[x][1] = lo.y; av[x][2] = lo.z; av[x][3] = lo.w;
+      av[x][4] = hi.x; av[x][5] = hi.y; av[x][6] = hi.z; av[x][7] = hi.w;
+    }
+#pragma unroll
+    for (int y = 0; y < MT; ++y) {
+      if constexpr (BT) {
+        const int row = wc * WT + y * 16 + r16;
+        const char* rp = Bs + row * 128;
+        const float4 lo = *reinterpret_cast<const float4*>(rp + ((2 * g) ^ swz32(row)) * 16);
+        const float4 hi = *reinterpret_cast<const float4*>(rp + ((2 * g + 1) ^ swz32(row)) * 16);
+        bv[y][0] = lo.x; bv[y][1] = lo.y; bv[y][2] = lo.z; bv[y][3] = lo.w;
+        bv[y][4] = hi.x; bv[y][5] = hi.y; bv[y][6] = hi.z; bv[y][7] = hi.w;
+      } else {
+        const int col = wc * WT + y * 16 + r16;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int k = 8 * g + s;
+          const int pc = (col >> 2) ^ (((k >> 3) & 1) * 4);
+          bv[y][s] = *reinterpret_cast<const float*>(Bs + (k * T + pc * 4 + (col & 3)) * 4);
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int x = 0; x < MT; ++x)
+#pragma unroll
+        for (int y = 0; y < MT; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[x][s], bv[y][s], acc[x][y], 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // 16x16 MFMA tile: lane holds column lane & 15, rows 4 (lane >> 4) + v
+#pragma unroll
+  for (int x = 0; x < MT; ++x)
+#pragma unroll
+    for (int y = 0; y < MT; ++y) {
+      const int64_t c = c0 + wc * WT + y * 16 + r16;
+      if (c >= a.N) continue;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int64_t r = r0 + wr * WT + x * 16 + 4 * g + v;
+        if (r < a.M) {
+          float* p = a.C + r * a.ldc + c;
+          const float val = a.alpha * acc[x][y][v];
+          *p = a.beta == 0.f ? val : __fmaf_rn(a.beta, *p, val);
+        }
+      }
+    }
+}
+
+constexpr int NS_F32D = 3;
+template <int T>
+constexpr int f32d_lds() { return NS_F32D * 2 * T * DKC * 4; }
+
 }  // namespace f32g
 }  // namespace lcq
 
@@ -552,7 +719,30 @@ extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const 
   hipStream_t st = as_stream(stream);
   // 128^2 tiles where they fill the chip, 64^2 below (4x the workgroups)
   const int64_t t128 = ((N + 127) / 128) * ((M + 127) / 128);
-  if (t128 >= 256) {
+  const bool big = t128 >= 256;
+  // LDS-DMA kernel: K % 32 == 0, 16-byte aligned rows, 32-bit byte offsets
+  const bool dma = K % f32g::DKC == 0 && a.vec && al(C) &&
+                   M * lda < ((int64_t)1 << 29) && (bt ? N * ldb : K * ldb) < ((int64_t)1 << 29);
+  if (dma) {
+    if (big) {
+      const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128));
+      constexpr int L = f32g::f32d_lds<128>();
+      if (bt) {
+        (void)hipFuncSetAttribute((const void*)f32g::k_gemm_f32d<1, 128, f32g::NS_F32D>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, L);
+        hipLaunchKernelGGL((f32g::k_gemm_f32d<1, 128, f32g::NS_F32D>), grid, 256, L, st, a);
+      } else {
+        (void)hipFuncSetAttribute((const void*)f32g::k_gemm_f32d<0, 128, f32g::NS_F32D>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, L);
+        hipLaunchKernelGGL((f32g::k_gemm_f32d<0, 128, f32g::NS_F32D>), grid, 256, L, st, a);
+      }
+    } else {
+      const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64));
+      constexpr int L = f32g::f32d_lds<64>();
+      if (bt) hipLaunchKernelGGL((f32g::k_gemm_f32d<1, 64, f32g::NS_F32D>), grid, 256, L, st, a);
+      else hipLaunchKernelGGL((f32g::k_gemm_f32d<0, 64, f32g::NS_F32D>), grid, 256, L, st, a);
+    }
+  } else if (big) {
     const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128));
     if (bt) hipLaunchKernelGGL((f32g::k_gemm_f32<1, 128>), grid, 256, 0, st, a);
     else hipLaunchKernelGGL((f32g::k_gemm_f32<0, 128>), grid, 256, 0, st, a);

@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) void k_fp8_gemm_reduce(const float* __restrict
 //     instead of 64; smaller grids split K on top (fp32 partials summed in split order).
 // Operands stream through LDS by LDS-DMA (buffer_load ... lds, 16 B per lane; 8 rows of 128 B
 // per wave-instruction, 4 A and 4 B pieces per wave per K block in both instances) into two
-// stage buffers (A TM x 128 B + B TM x 128 B, 16-B chunks XOR-swizzled by row & 7), plus the K
+// stage buffers (A TM x 128 B + B TM x 128 B, 16-B chunks XOR-swizzled per row, swz), plus the K
 // block's TM a_s values (kb-major copy made by k_as_transpose; 4 B per lane from the first
 // TM / 64 waves: an LDS-DMA lane writes a whole dword). One barrier per K block: after it the
 // next K block's loads go into the buffer every wave finished reading.
@@ -246,10 +246,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t by
                                            (short)0, nb, 0x00020000);
 }
 
-// 16-B chunk c (0..7) of row r of an operand tile lives at physical chunk c ^ (r & 7)
+// 16-B chunk c (0..7) of row r of an operand tile lives at physical chunk c ^ swz(r). A
+// fragment read (lane l: row l & 15 of a 16-row block, chunks 2q and 2q + 1, q = l >> 4) puts
+// each ds_read_b128 lane group of 16 on 16 distinct 16-byte bank slots with this swizzle (found
+// by exhaustive search over per-row tables; XOR by r & 7 gave every lane a 2-way conflict:
+// 47 % of the LDS cycles, profiles/r3c_gemm_pmc.txt)
+__device__ __forceinline__ int swz(int row) { return ((row >> 1) & 1) | ((row >> 1) & 4); }
+
 __device__ __forceinline__ v8i frag2(const uint8_t* tile, int row, int q) {
   const uint8_t* rp = tile + row * BK;
-  const int c0 = (2 * q) ^ (row & 7), c1 = (2 * q + 1) ^ (row & 7);
+  const int c0 = (2 * q) ^ swz(row), c1 = (2 * q + 1) ^ swz(row);
   const uint4 lo = *reinterpret_cast<const uint4*>(rp + c0 * 16);
   const uint4 hi = *reinterpret_cast<const uint4*>(rp + c1 * 16);
   return v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z,
@@ -284,7 +290,7 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds) {
   if (nk > g.kb_per_split) nk = g.kb_per_split;
 
   // staging: piece j of wave w = rows j * 8 NW + w * 8 .. + 7 of A and of B; 8 rows x 128 B =
-  // 64 lanes x 16 B; lane l -> row l / 8, physical chunk l % 8 = logical chunk (l % 8) ^ (row & 7)
+  // 64 lanes x 16 B; lane l -> row l / 8, physical chunk l % 8 = logical chunk (l % 8) ^ swz(row)
   const __amdgpu_buffer_rsrc_t ra = rsrc(g.a + m0 * g.K, (g.M - m0) * g.K);
   const __amdgpu_buffer_rsrc_t rb = rsrc(g.b + n0 * g.K, (g.N - n0) * g.K);
   const __amdgpu_buffer_rsrc_t rs = rsrc(g.ast + m0, (g.mp * nkb - m0) * 4);
@@ -292,7 +298,7 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds) {
 #pragma unroll
   for (int j = 0; j < PIECES; ++j) {
     const int row = j * 8 * NW + w * 8 + (lane >> 3);
-    off[j] = (uint32_t)(row * g.K + (((lane & 7) ^ (row & 7)) * 16));
+    off[j] = (uint32_t)(row * g.K + (((lane & 7) ^ swz(row)) * 16));
   }
   auto stage = [&](int buf, int64_t kbl) {  // kbl: K block index within the split
     const int64_t kb = kb0 + (kbl < nk ? kbl : nk - 1);

@@ -237,6 +237,41 @@ def test_trailing_update(dev, rows, ic, c0, K, c2):
     assert torch.equal(part, out[h:])
 
 
+@pytest.mark.parametrize('M,N,K', [(200, 136, 64), (1000, 700, 512), (2100, 2300, 1024),
+                                   (128, 4096, 4096)])
+@pytest.mark.parametrize('bt', [False, True])
+def test_gemm_f32_dma(dev, M, N, K, bt):
+    """lcq_gemm_f32's LDS-DMA kernel (16-byte aligned rows, K % 32 == 0: the recursion's
+    products on 128-multiple Hessians) on sub-views of larger matrices: ragged M / N at both
+    tile sizes, past-the-end rows / columns read as zero; against fp64 (same bound as above)
+    and deterministic."""
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    big_a = torch.randn(M + 8, K + 8, generator=g)
+    big_b = torch.randn((N + 4, K + 12) if bt else (K + 4, N + 12), generator=g)
+    A = big_a[4:M + 4, 4:K + 4]
+    B = big_b[:N, 8:K + 8] if bt else big_b[4:K + 4, :N]
+    C0 = torch.randn(M, N + 4, generator=g)[:, :N]
+    ref_p = A.double() @ (B.double().t() if bt else B.double())
+    bound0 = A.double().abs() @ (B.double().abs().t() if bt else B.double().abs())
+    Ad = big_a.to(dev)[4:M + 4, 4:K + 4]
+    Bd = big_b.to(dev)[:N, 8:K + 8] if bt else big_b.to(dev)[4:K + 4, :N]
+    for alpha, beta in ((1.0, 0.0), (-1.0, 1.0)):
+        Cd = C0.to(dev).clone()
+        if beta == 0.0:
+            Cd.fill_(float('nan'))
+        ops.gemm_f32(Ad, Bd, Cd, alpha, beta, b_trans=bt)
+        ref = alpha * ref_p + (beta * C0.double() if beta else 0)
+        bound = abs(alpha) * bound0 + abs(beta) * C0.double().abs()
+        err = ((Cd.cpu().double() - ref).abs() / (bound + 1e-30)).max().item()
+        assert err < 2e-6, (alpha, beta, err)
+    C1 = torch.empty(M, N, device=dev)
+    C2 = torch.empty(M, N, device=dev)
+    ops.gemm_f32(Ad, Bd, C1, 1.0, 0.0, b_trans=bt)
+    ops.gemm_f32(Ad, Bd, C2, 1.0, 0.0, b_trans=bt)
+    assert torch.equal(C1, C2)
+
+
 @pytest.mark.parametrize('M,N,K', [(1, 1, 1), (130, 77, 33), (256, 384, 128), (1000, 700, 517),
                                    (2048, 1536, 2048)])
 @pytest.mark.parametrize('bt', [False, True])
