@@ -531,7 +531,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_f32(Args a) {
 
 
 // ---------------------------------------------------------------------------------------
-// k_gemm_f32d: the same product with LDS-DMA staging, for 16-byte aligned rows and K % 32 == 0
+// k_gemm_f32d_*: the same product with LDS-DMA staging, for 16-byte aligned rows and K % 32 == 0
 // (every product of the recursion on 128-multiple Hessians). k_gemm_f32 above stages through
 // registers (per-element bounds checks, transposing scalar LDS stores) and measured 55-80 TF/s
 // (MFMA busy ~55 %, profiles/r3c_gemm_pmc.txt). Here:
@@ -566,14 +566,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t f32_rsrc(const float* p, int64
 }
 
 template <int BT, int T, int NS>
-__global__ void __launch_bounds__(256, 1) k_gemm_f32d(Args a) {
+__device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds) {
   constexpr int OPB = T * DKC * 4;        // one operand chunk image (bytes)
   constexpr int STG = 2 * OPB;
   constexpr int PA = T / 32;              // A pieces (8 rows x 128 B) per wave
   constexpr int PB = T / 32;              // B pieces per wave (k-major: 1 KB of [k][col] rows)
   constexpr int WT = T / 2, MT = WT / 16; // wave tile, 16x16 MFMA tiles per side
   constexpr int LPS = PA + PB;            // DMA instructions per wave per stage
-  extern __shared__ __attribute__((aligned(16))) char f32lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1;
@@ -696,6 +695,19 @@ constexpr int NS_F32D = 3;
 template <int T>
 constexpr int f32d_lds() { return NS_F32D * 2 * T * DKC * 4; }
 
+// fixed kernels around the body (a templated __global__ with device builtins inside its
+// lambda loses its host stub under hipcc)
+#define LCQ_F32D_KERNEL(NAME, BT, T)                                   \
+  __global__ void __launch_bounds__(256, 1) NAME(Args a) {             \
+    extern __shared__ __attribute__((aligned(16))) char f32lds[];      \
+    gemm_f32d_body<BT, T, NS_F32D>(a, f32lds);                         \
+  }
+LCQ_F32D_KERNEL(k_gemm_f32d_n128, 0, 128)
+LCQ_F32D_KERNEL(k_gemm_f32d_t128, 1, 128)
+LCQ_F32D_KERNEL(k_gemm_f32d_n64, 0, 64)
+LCQ_F32D_KERNEL(k_gemm_f32d_t64, 1, 64)
+#undef LCQ_F32D_KERNEL
+
 }  // namespace f32g
 }  // namespace lcq
 
@@ -728,19 +740,19 @@ extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const 
       const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128));
       constexpr int L = f32g::f32d_lds<128>();
       if (bt) {
-        (void)hipFuncSetAttribute((const void*)f32g::k_gemm_f32d<1, 128, f32g::NS_F32D>,
+        (void)hipFuncSetAttribute((const void*)f32g::k_gemm_f32d_t128,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, L);
-        hipLaunchKernelGGL((f32g::k_gemm_f32d<1, 128, f32g::NS_F32D>), grid, 256, L, st, a);
+        hipLaunchKernelGGL(f32g::k_gemm_f32d_t128, grid, 256, L, st, a);
       } else {
-        (void)hipFuncSetAttribute((const void*)f32g::k_gemm_f32d<0, 128, f32g::NS_F32D>,
+        (void)hipFuncSetAttribute((const void*)f32g::k_gemm_f32d_n128,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, L);
-        hipLaunchKernelGGL((f32g::k_gemm_f32d<0, 128, f32g::NS_F32D>), grid, 256, L, st, a);
+        hipLaunchKernelGGL(f32g::k_gemm_f32d_n128, grid, 256, L, st, a);
       }
     } else {
       const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64));
       constexpr int L = f32g::f32d_lds<64>();
-      if (bt) hipLaunchKernelGGL((f32g::k_gemm_f32d<1, 64, f32g::NS_F32D>), grid, 256, L, st, a);
-      else hipLaunchKernelGGL((f32g::k_gemm_f32d<0, 64, f32g::NS_F32D>), grid, 256, L, st, a);
+      if (bt) hipLaunchKernelGGL(f32g::k_gemm_f32d_t64, grid, 256, L, st, a);
+      else hipLaunchKernelGGL(f32g::k_gemm_f32d_n64, grid, 256, L, st, a);
     }
   } else if (big) {
     const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128));
