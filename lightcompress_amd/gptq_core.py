@@ -299,7 +299,20 @@ def _syrk_lower(L, C, alpha):
     _syrk_lower(L[h:], C[h:, h:], alpha)
 
 
-def _chol_inv_rec(A: torch.Tensor, X: torch.Tensor, info: torch.Tensor, row0: int = 0):
+_OVERLAP_MIN = 1024  # recursion levels from this size up run T = L21 X11 on a side stream
+_side_streams: dict = {}
+
+
+def _side_stream(dev, depth):
+    key = (dev.index, depth)
+    st = _side_streams.get(key)
+    if st is None:
+        st = _side_streams[key] = torch.cuda.Stream(device=dev)
+    return st
+
+
+def _chol_inv_rec(A: torch.Tensor, X: torch.Tensor, info: torch.Tensor, row0: int = 0,
+                  depth: int = 0):
     """X (zeroed square fp32 view) <- L^-1 for the lower Cholesky factor L of A (square fp32
     row-major view, lower part read; consumed as workspace).
 
@@ -307,9 +320,14 @@ def _chol_inv_rec(A: torch.Tensor, X: torch.Tensor, info: torch.Tensor, row0: in
     X22 = chol(A22)^-1 (recursion); X21 = -X22 (L21 X11). Tiles of <= 128 are factored and
     inverted in one workgroup (lcq_chol_inv_tile); everything else is fp32 MFMA GEMM
     (lcq_gemm_f32), written in place through strided views, with the triangular / symmetric
-    structure skipped block-wise (_mm_* / _syrk_lower). Under true_sequential the block's
-    Hessians (q/k/v, o, gate/up, down) are built one after another from the previous subsets'
-    quantized outputs, so their chains cannot overlap."""
+    structure skipped block-wise (_mm_* / _syrk_lower). T = L21 X11 needs neither the A22
+    update nor X22, so from _OVERLAP_MIN up it runs on a side stream (one per recursion depth:
+    an inner level's T never queues behind an outer one) while the main stream walks the
+    A22 -> X22 chain, whose mid-size products leave most of the chip idle; the streams join
+    before X21. Every product is the same kernel on the same operands either way (results are
+    identical). Under true_sequential the block's Hessians (q/k/v, o, gate/up, down) are built
+    one after another from the previous subsets' quantized outputs, so their chains cannot
+    overlap."""
     n = A.shape[0]
     if n <= _TILE:
         ops.chol_inv_tile(A, info, row0, out=X)
@@ -317,32 +335,86 @@ def _chol_inv_rec(A: torch.Tensor, X: torch.Tensor, info: torch.Tensor, row0: in
     n1 = _split(n)
     A21, A22 = A[n1:, :n1], A[n1:, n1:]
     X11, X22 = X[:n1, :n1], X[n1:, n1:]
-    _chol_inv_rec(A[:n1, :n1], X11, info, row0)
+    _chol_inv_rec(A[:n1, :n1], X11, info, row0, depth + 1)
     L21 = torch.empty_like(A21)
     _mm_lowT(A21, X11, L21, 1.0, 0.0)
-    _syrk_lower(L21, A22, -1.0)
-    _chol_inv_rec(A22, X22, info, row0 + n1)
     T = torch.empty_like(A21)
-    _mm_low_right(L21, X11, T, 1.0, 0.0)
+    if n >= _OVERLAP_MIN and A.is_cuda:
+        main = torch.cuda.current_stream(A.device)
+        side = _side_stream(A.device, depth)
+        side.wait_stream(main)  # L21, X11 ready
+        with torch.cuda.stream(side):
+            _mm_low_right(L21, X11, T, 1.0, 0.0)
+        _syrk_lower(L21, A22, -1.0)
+        _chol_inv_rec(A22, X22, info, row0 + n1, depth + 1)
+        main.wait_stream(side)  # T ready; L21 / T are released only after this join
+    else:
+        _syrk_lower(L21, A22, -1.0)
+        _chol_inv_rec(A22, X22, info, row0 + n1, depth + 1)
+        _mm_low_right(L21, X11, T, 1.0, 0.0)
     del L21
     _mm_low_left(X22, T, X[n1:, :n1], -1.0, 0.0)
 
 
-def inverse_cholesky_upper(H: torch.Tensor) -> torch.Tensor:
-    """U = chol(H^-1, upper) = J chol(J H J)^-1 J for SPD fp32 H (H is consumed)."""
-    Hr = H.flip(0, 1).contiguous()
-    del H
+def _chain(Hs: torch.Tensor):
+    """J chol(J H J)^-1 J on H (not modified): (U, info)."""
+    Hr = Hs.flip(0, 1).contiguous()
     info = torch.zeros(1, dtype=torch.int32, device=Hr.device)
     X = torch.zeros_like(Hr)
     _chol_inv_rec(Hr, X, info)
     del Hr
+    return X.flip(0, 1).contiguous(), info
+
+
+# One captured HIP graph per (device, Hessian size): the recursion issues ~600 launches per
+# chain at n = 14336 (the Llama-3-8B down_proj Hessian), many shorter than the host time to
+# issue them from Python; a replay issues them back to back. Every size's first chain runs
+# eagerly (it also loads every kernel), the graph is captured right after and replayed for the
+# following blocks. Same kernels, same operands: identical results.
+_GRAPH_MIN = 1024
+_chain_graphs: dict = {}
+
+
+def _chain_graphed(H: torch.Tensor):
+    key = (H.device.index, H.shape[0])
+    ent = _chain_graphs.get(key)
+    if ent is None:
+        U, info = _chain(H)
+        static_in = H.clone()
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(H.device)
+        with torch.cuda.graph(g):
+            out, g_info = _chain(static_in)
+        _chain_graphs[key] = (g, static_in, out, g_info)
+        return U, info
+    g, static_in, out, g_info = ent
+    static_in.copy_(H)
+    timer = ops.N._timer
+    if timer is not None:  # bench's per-kernel table: the replay as one entry
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        timer.events.setdefault('lcq_chol_chain_graph', []).append((e0, e1))
+    else:
+        g.replay()
+    # the static output is overwritten by the next replay of this size
+    return out.clone(), g_info
+
+
+def inverse_cholesky_upper(H: torch.Tensor) -> torch.Tensor:
+    """U = chol(H^-1, upper) = J chol(J H J)^-1 J for SPD fp32 H (H is consumed)."""
+    graphed = (H.is_cuda and H.shape[0] >= _GRAPH_MIN
+               and os.environ.get('LCQ_CHOL_GRAPH', '1') != '0')
+    U, info = _chain_graphed(H) if graphed else _chain(H)
+    del H
     bad = int(info.item())
     if bad:
         raise torch.linalg.LinAlgError(
             f'linalg.cholesky: The factorization could not be completed because the input '
             f'is not positive-definite (the leading minor of order {bad} is not '
             f'positive-definite).')
-    return X.flip(0, 1).contiguous()
+    return U
 
 
 def prepare_weight(W: torch.Tensor, perm, dead):

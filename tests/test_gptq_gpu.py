@@ -317,6 +317,29 @@ def test_inverse_cholesky_upper(dev, n):
     assert rel < 5e-4, rel
 
 
+def test_inverse_cholesky_graph_replay(dev, monkeypatch):
+    """The per-size captured chain (gptq_core._chain_graphed): the first call of a size runs
+    eagerly and captures, later calls replay; every result equals the eager recursion's bit
+    for bit, on new inputs of the same size (the static input is refilled each time)."""
+    from lightcompress_amd import gptq_core
+    n = 1536
+    g = torch.Generator().manual_seed(5)
+    Hs = []
+    for _ in range(3):
+        X = torch.randn(n, 2 * n, generator=g)
+        H = X @ X.T / (2 * n)
+        H.diagonal().add_(0.05)
+        Hs.append(H.to(dev))
+    gptq_core._chain_graphs.pop((torch.device(dev).index or 0, n), None)
+    monkeypatch.setenv('LCQ_CHOL_GRAPH', '0')
+    eager = [gptq_core.inverse_cholesky_upper(H.clone()) for H in Hs]
+    monkeypatch.setenv('LCQ_CHOL_GRAPH', '1')
+    graphed = [gptq_core.inverse_cholesky_upper(H.clone()) for H in Hs + Hs[:1]]
+    assert (torch.device(dev).index or 0, n) in gptq_core._chain_graphs
+    for a, b in zip(eager + eager[:1], graphed):
+        assert torch.equal(a, b)
+
+
 def test_inverse_cholesky_not_pd(dev):
     from lightcompress_amd import gptq_core
     H = torch.eye(256, device=dev)
