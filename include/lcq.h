@@ -425,6 +425,11 @@ int lcq_fp8_block_to_tensor_many(int n, const void* descs, int64_t max_elems, in
                                  int block, int fmt_out, float qmax, float clamp_min,
                                  int add_zero, void* amax_ws, void* scales_out, void* stream);
 
+/* A/B probe hook of lcq_fp8_gemm's tile plan (scripts/fp8_gemm_rate.py): 0 = automatic (the
+ * default), 1 = the <= 64-row 32x32x64 kernel, 128 / 256 = that 16x16x128 tile with the split-K
+ * count the plan computes for it. Process-wide; not for production use. */
+int lcq_fp8_gemm_force_plan(int plan);
+
 /* Block-scaled FP8 GEMM (fp8_gemm, kernel.py:141-242, called by block_wise_fp8_forward_func,
  * module_utils.py:41-46, for LlmcFp8Linear / fp8_forward linears): a [M, K] e4m3 codes with
  * per-token 128-column scales a_s fp32 [M, K/128] (act_quant); b [N, K] e4m3 codes with

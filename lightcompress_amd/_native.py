@@ -100,6 +100,7 @@ SIGNATURES = {
     'lcq_rmsnorm': ([_vp, _vp, _int, _i64, _i64, _f32, _vp, _vp], _int),
     'lcq_fp8_block_to_tensor': ([_vp, _int, _i64, _i64, _int, _vp, _int, _f32, _f32, _int, _vp,
                                  _vp, _vp, _vp], _int),
+    'lcq_fp8_gemm_force_plan': ([_int], _int),
     'lcq_fp8_block_to_tensor_many': ([_int, _vp, _i64, _int, _int, _int, _f32, _f32, _int, _vp,
                                       _vp, _vp], _int),
     'lcq_minmax_segments': ([_vp, _vp, _i64, _int, _vp, _vp, _vp], _int),

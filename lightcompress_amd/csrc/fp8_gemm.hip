@@ -328,9 +328,18 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds) {
     for (int j = 0; j < NB; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   const v4f zero = {0.f, 0.f, 0.f, 0.f};
   const int r16 = lane & 15, q = lane >> 4;
-  int64_t nbr = (n0 + wc * WN) >> 7;  // this wave's 128-column scale block (clamped past N)
-  if (nbr > (g.N - 1) >> 7) nbr = (g.N - 1) >> 7;
-  const float* bsrow = g.bs + nbr * nkb + kb0;
+  // the split's weight block-scales of the tile's TM / 128 column blocks, staged in LDS once (a
+  // global load per K block sat on every block's accumulation path: ~5x the MFMA time at
+  // 128^2, profiles/r3c_gemm_pmc.txt)
+  float* bsl = reinterpret_cast<float*>(lds + NS * STG);
+  for (int i = tid; i < (TM / 128) * nk; i += 64 * NW) {
+    const int cb = i / (int)nk, t = i - cb * (int)nk;
+    int64_t nb = (n0 >> 7) + cb;
+    if (nb > (g.N - 1) >> 7) nb = (g.N - 1) >> 7;  // clamped past N (columns never stored)
+    bsl[i] = g.bs[nb * nkb + kb0 + t];
+  }
+  __syncthreads();
+  const float* bsrow = bsl + ((wc * WN) >> 7) * nk;  // this wave's 128-column scale block
 
   // NS-stage ring: NS - 1 K blocks in flight ahead of the one being multiplied
 #pragma unroll
@@ -466,10 +475,39 @@ int64_t gemm_splits(int64_t M, int64_t N, int64_t K) {
 
 using namespace lcq;
 
+// plan override for A/B probes (lcq_fp8_gemm_force_plan): 0 = auto, 1 = the <= 64-row kernel,
+// 128 / 256 = that tile (split-K as gemm2_plan computes for it)
+static int g_force_plan = 0;
+
+static Plan2 pick_plan(int64_t M, int64_t N, int64_t K) {
+  Plan2 p = gemm2_plan(M, N, K);
+  if (g_force_plan == 128 || g_force_plan == 256) {
+    p.tm = g_force_plan;
+    const int64_t tiles = ((M + p.tm - 1) / p.tm) * ((N + p.tm - 1) / p.tm), nkb = K / BK;
+    int64_t s = (256 + tiles - 1) / tiles;
+    if (s > nkb / 4) s = nkb / 4;
+    if (s < 2 || (p.tm == 256 && tiles >= 224) || (p.tm == 128 && tiles >= 192)) {
+      p.splits = 1;
+    } else {
+      const int64_t per = (nkb + s - 1) / s;
+      p.splits = (nkb + per - 1) / per;
+    }
+  }
+  return p;
+}
+
 // workspace of the 16x16x128 kernels: the kb-major a_s copy, then the split-K partials
 static int64_t ws2_bytes(int64_t M, int64_t N, int64_t K) {
   const int64_t mp = (M + 255) / 256 * 256, nkb = K / BK;
-  const int64_t s = gemm2_plan(M, N, K).splits;
+  // the largest split count any plan takes (so a forced plan fits the queried workspace)
+  int64_t s = 1;
+  for (int tm : {128, 256}) {
+    const int64_t tiles = ((M + tm - 1) / tm) * ((N + tm - 1) / tm), nkb2 = K / BK;
+    int64_t c = (256 + tiles - 1) / tiles;
+    if (c > nkb2 / 4) c = nkb2 / 4;
+    if (c > s) s = c;
+  }
+  s = s > gemm2_plan(M, N, K).splits ? s : gemm2_plan(M, N, K).splits;
   return nkb * mp * 4 + (s > 1 ? s * M * N * 4 : 0);
 }
 
@@ -479,6 +517,12 @@ extern "C" int64_t lcq_fp8_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K)
   const int64_t old = s > 1 ? s * M * N * (int64_t)sizeof(float) : 0;
   const int64_t w2 = ws2_bytes(M, N, K);
   return old > w2 ? old : w2;
+}
+
+extern "C" int lcq_fp8_gemm_force_plan(int plan) {
+  LCQ_REQUIRE(plan == 0 || plan == 1 || plan == 128 || plan == 256, "plan: 0, 1, 128 or 256");
+  g_force_plan = plan;
+  return LCQ_OK;
 }
 
 extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const void* b_s,
@@ -496,11 +540,11 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
   // the 16x16x128 kernels from 128 rows up (measured at 2048 x 7168 x 7168: 1.46 vs 1.01
   // PFLOP/s for the 256^2 tile against the 128-row 32x32x64 kernel below, 1.85 vs 1.30 at
   // 8192^3); the 32x32x64 kernel keeps batches of <= 64 rows, where a 128-row tile is half empty
-  if (M > 64 && workspace && ws_bytes >= ws2_bytes(M, N, K) && N % 4 == 0 &&
+  if (M > 64 && g_force_plan != 1 && workspace && ws_bytes >= ws2_bytes(M, N, K) && N % 4 == 0 &&
       M * K < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31)) {
     hipStream_t st = as_stream(stream);
     const int64_t mp = (M + 255) / 256 * 256;
-    const Plan2 pl = gemm2_plan(M, N, K);
+    const Plan2 pl = pick_plan(M, N, K);
     const int64_t s2 = pl.splits;
     float* ast = static_cast<float*>(workspace);
     float* part = s2 > 1 ? ast + nkb * mp : nullptr;
@@ -511,16 +555,21 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
                  (nkb + s2 - 1) / s2, c_dtype, (int)((M + pl.tm - 1) / pl.tm),
                  (int)((N + pl.tm - 1) / pl.tm)};
     const int nslots = 32 * ((g2.nmt + 3) / 4) * ((g2.nnt + 7) / 8);
+    // stage ring + the split's block-scales (TM / 128 column blocks x K blocks per split)
+    const int bsb = (int)(((pl.tm / 128) * g2.kb_per_split * 4 + 15) / 16 * 16);
     if (pl.tm == 256) {
+      const int L = NS256 * stage_bytes<256>() + bsb;
+      LCQ_REQUIRE(L <= 160 * 1024, "K too large for the staged block-scales");
       (void)hipFuncSetAttribute((const void*)k_fp8_gemm2,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, NS256 * stage_bytes<256>());
-      hipLaunchKernelGGL(k_fp8_gemm2, dim3((unsigned)nslots, 1, (unsigned)s2), 512,
-                         NS256 * stage_bytes<256>(), st, g2);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, L);
+      hipLaunchKernelGGL(k_fp8_gemm2, dim3((unsigned)nslots, 1, (unsigned)s2), 512, L, st, g2);
     } else {
+      const int L = NS128 * stage_bytes<128>() + bsb;
+      LCQ_REQUIRE(L <= 160 * 1024, "K too large for the staged block-scales");
       (void)hipFuncSetAttribute((const void*)k_fp8_gemm2_128,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, NS128 * stage_bytes<128>());
-      hipLaunchKernelGGL(k_fp8_gemm2_128, dim3((unsigned)nslots, 1, (unsigned)s2), 256,
-                         NS128 * stage_bytes<128>(), st, g2);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, L);
+      hipLaunchKernelGGL(k_fp8_gemm2_128, dim3((unsigned)nslots, 1, (unsigned)s2), 256, L, st,
+                         g2);
     }
     if (s2 > 1) {
       const int rc = check_launch("lcq_fp8_gemm");
