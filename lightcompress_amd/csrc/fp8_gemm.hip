@@ -7,9 +7,10 @@
 // A [M, K] e4m3 (act_quant output, per-token 128-column scales a_s [M, K/128]); B [N, K] e4m3
 // with 128x128 block scales b_s [ceil(N/128), K/128]; fp32 accumulation; C fp32 / bf16 / fp16.
 //
-// Three kernels: k_fp8_gemm2 (256x256 tiles) and k_fp8_gemm2_128 (128x128 tiles, split-K on
-// small grids) on the 16x16x128 MFMA for batches of more than 64 rows (gemm2_plan picks the
-// tile), and k_fp8_gemm for batches of <= 64 rows:
+// Kernels: k_fp8_gemm2 (256x256 tiles on the 16x16x128 MFMA, split-K on grids under 224
+// tiles) for batches of more than 64 rows whose 256^2 grid has >= 64 tiles (gemm2_plan), its
+// 128x128 sibling k_fp8_gemm2_128 (L2-fill-bound for fp8, reached through the probe hook
+// only), and k_fp8_gemm for everything else:
 // Tile 128x128 (or 64x128 when the grid would be small) per workgroup, 4 waves on gfx950's
 // 32x32x64 f8f6f4 MFMA, one K block of 128 per step double-buffered through LDS (16-byte global
 // loads into registers one block ahead, padded rows); the block's partial dot products are
@@ -18,7 +19,6 @@
 // partials that a second kernel sums in split order (deterministic).
 #include "lcq_common.h"
 
-#include <stdlib.h>
 
 namespace lcq {
 namespace {
@@ -435,24 +435,31 @@ __global__ __launch_bounds__(256) void k_as_transpose(const float* __restrict__ 
   out[i] = m < M ? as[m * nkb + kb] : 0.f;
 }
 
-// Tile plan of the MFMA-16x16x128 kernels: 256^2 tiles when they fill >= 7/8 of the chip,
-// else 128^2 tiles, with K split until ~256 workgroups (one per CU at this kernel's LDS) are in
-// flight, keeping >= 4 K blocks per split.
+// Tile plan. An fp8 K block of a 128^2 tile is 4.2 MFLOP per 32 KB staged (128 flop/B): at the
+// CU's 8192 fp8 flop/cycle that needs ~64 B/cycle of L2 -> LDS fill, about twice what a CU
+// gets (profiles/r3c_gemm_pmc.txt, r3c_fp8_gemm_rate.txt: 78-83 us at 2048 x 2048 x 7168 with
+// the MFMAs ~17 % busy), so the 16x16x128 body runs 256^2 tiles (256 flop/B): unsplit when they
+// fill >= 7/8 of the chip, split along K (>= 4 K blocks per split, ~256 workgroups) from 64
+// tiles up; smaller grids take the 32x32x64 kernel with its 64-row tiles (tm = 0). 128^2 is
+// kept for the probe hook only.
 struct Plan2 {
-  int tm;          // 256 or 128
+  int tm;          // 256, 128 (probe), or 0: the <= 64-row-tile kernel
   int64_t splits;  // K splits (1: C written directly)
 };
 
-Plan2 gemm2_plan(int64_t M, int64_t N, int64_t K) {
-  const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256);
-  if (t256 >= 224) return {256, 1};
-  const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128), nkb = K / BK;
-  if (tiles >= 192) return {128, 1};
+static int64_t split_count(int64_t tiles, int64_t nkb, int64_t full) {
+  if (tiles >= full) return 1;
   int64_t s = (256 + tiles - 1) / tiles;
   if (s > nkb / 4) s = nkb / 4;
-  if (s < 2) return {128, 1};
+  if (s < 2) return 1;
   const int64_t per = (nkb + s - 1) / s;
-  return {128, (nkb + per - 1) / per};  // no empty split
+  return (nkb + per - 1) / per;  // no empty split
+}
+
+Plan2 gemm2_plan(int64_t M, int64_t N, int64_t K) {
+  const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256), nkb = K / BK;
+  if (M <= 64 || t256 < 64) return {0, 1};
+  return {256, split_count(t256, nkb, 224)};
 }
 
 // K splits for a short batch: a 64-row grid of fewer than 256 tiles is split along K until
@@ -480,34 +487,25 @@ using namespace lcq;
 static int g_force_plan = 0;
 
 static Plan2 pick_plan(int64_t M, int64_t N, int64_t K) {
-  Plan2 p = gemm2_plan(M, N, K);
+  if (g_force_plan == 1) return {0, 1};
   if (g_force_plan == 128 || g_force_plan == 256) {
-    p.tm = g_force_plan;
-    const int64_t tiles = ((M + p.tm - 1) / p.tm) * ((N + p.tm - 1) / p.tm), nkb = K / BK;
-    int64_t s = (256 + tiles - 1) / tiles;
-    if (s > nkb / 4) s = nkb / 4;
-    if (s < 2 || (p.tm == 256 && tiles >= 224) || (p.tm == 128 && tiles >= 192)) {
-      p.splits = 1;
-    } else {
-      const int64_t per = (nkb + s - 1) / s;
-      p.splits = (nkb + per - 1) / per;
-    }
+    const int tm = g_force_plan;
+    const int64_t tiles = ((M + tm - 1) / tm) * ((N + tm - 1) / tm);
+    return {tm, split_count(tiles, K / BK, tm == 256 ? 224 : 192)};
   }
-  return p;
+  return gemm2_plan(M, N, K);
 }
 
 // workspace of the 16x16x128 kernels: the kb-major a_s copy, then the split-K partials
 static int64_t ws2_bytes(int64_t M, int64_t N, int64_t K) {
   const int64_t mp = (M + 255) / 256 * 256, nkb = K / BK;
-  // the largest split count any plan takes (so a forced plan fits the queried workspace)
+  // the largest split count any plan takes (a forced plan fits the queried workspace too)
   int64_t s = 1;
   for (int tm : {128, 256}) {
-    const int64_t tiles = ((M + tm - 1) / tm) * ((N + tm - 1) / tm), nkb2 = K / BK;
-    int64_t c = (256 + tiles - 1) / tiles;
-    if (c > nkb2 / 4) c = nkb2 / 4;
+    const int64_t tiles = ((M + tm - 1) / tm) * ((N + tm - 1) / tm);
+    const int64_t c = split_count(tiles, nkb, tm == 256 ? 224 : 192);
     if (c > s) s = c;
   }
-  s = s > gemm2_plan(M, N, K).splits ? s : gemm2_plan(M, N, K).splits;
   return nkb * mp * 4 + (s > 1 ? s * M * N * 4 : 0);
 }
 
@@ -537,14 +535,12 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
                   (reinterpret_cast<uintptr_t>(b) & 15) == 0,
               "A / B must be 16-byte aligned");
   const int64_t nkb = K / BK;
-  // the 16x16x128 kernels from 128 rows up (measured at 2048 x 7168 x 7168: 1.46 vs 1.01
-  // PFLOP/s for the 256^2 tile against the 128-row 32x32x64 kernel below, 1.85 vs 1.30 at
-  // 8192^3); the 32x32x64 kernel keeps batches of <= 64 rows, where a 128-row tile is half empty
-  if (M > 64 && g_force_plan != 1 && workspace && ws_bytes >= ws2_bytes(M, N, K) && N % 4 == 0 &&
+  // the 16x16x128 body where the plan picks it (gemm2_plan), else the 32x32x64 kernel below
+  const Plan2 pl = pick_plan(M, N, K);
+  if (pl.tm != 0 && M > 64 && workspace && ws_bytes >= ws2_bytes(M, N, K) && N % 4 == 0 &&
       M * K < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31)) {
     hipStream_t st = as_stream(stream);
     const int64_t mp = (M + 255) / 256 * 256;
-    const Plan2 pl = pick_plan(M, N, K);
     const int64_t s2 = pl.splits;
     float* ast = static_cast<float*>(workspace);
     float* part = s2 > 1 ? ast + nkb * mp : nullptr;

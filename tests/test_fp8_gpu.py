@@ -242,9 +242,9 @@ def _abs_gemm(a, a_s, b, b_s):
                       b.view(torch.uint8).bitwise_and(0x7F).view(torch.float8_e4m3fn), b_s.abs())
 
 
-# ragged M / N tiles, one K block, the DeepSeek-V3 hidden size (K 7168); the tile plans of
-# fp8_gemm.hip: <= 64 rows (32x32x64 kernel), 128^2 split-K (256 x 512, 130 x 2048), 128^2
-# unsplit (1000 x 1500 ragged, 2048 x 1536), 256^2 (2048 x 7168)
+# ragged M / N tiles, one K block, the DeepSeek-V3 hidden size (K 7168); the automatic tile
+# plans of fp8_gemm.hip: the 32x32x64 kernel (<= 64 rows or < 64 tiles of 256^2, incl. its
+# split-K), 256^2 unsplit (2048 x 7168); the forced plans: test_fp8_gemm_forced_plans
 @pytest.mark.parametrize('M,Nn,K', [(1, 128, 128), (37, 200, 384), (256, 512, 1024),
                                     (130, 2048, 7168), (1000, 1500, 384), (2048, 1536, 256),
                                     (2048, 7168, 256)])
@@ -260,6 +260,26 @@ def test_fp8_gemm_vs_oracle(dev, M, Nn, K):
     tol = GEMM_RTOL * _abs_gemm(a, a_s, b, b_s) + 1e-30
     err = (got - want).abs()
     assert (err <= tol).all(), float((err / tol).max())
+
+
+@pytest.mark.parametrize('plan', [1, 128, 256])
+@pytest.mark.parametrize('M,Nn,K', [(200, 264, 1024), (1000, 1500, 896), (2048, 1536, 2048)])
+def test_fp8_gemm_forced_plans(dev, plan, M, Nn, K):
+    """Every kernel / tile plan of lcq_fp8_gemm (forced through lcq_fp8_gemm_force_plan: the
+    32x32x64 kernel, 128^2 and 256^2 with their split-K) against the oracle, ragged tiles."""
+    from lightcompress_amd import _native as N
+    from lightcompress_amd import ops
+    a, a_s, b, b_s = _gemm_inputs(M, Nn, K, seed=M + Nn + plan)
+    lib = N.load()
+    lib.lcq_fp8_gemm_force_plan(plan)
+    try:
+        got = ops.fp8_gemm(a.to(dev), a_s.to(dev), b.to(dev), b_s.to(dev),
+                           out_dtype=torch.float32).cpu()
+    finally:
+        lib.lcq_fp8_gemm_force_plan(0)
+    want = O.fp8_gemm(a, a_s, b, b_s)
+    tol = GEMM_RTOL * _abs_gemm(a, a_s, b, b_s) + 1e-30
+    assert ((got - want).abs() <= tol).all()
 
 
 def test_fp8_gemm_bf16_out_and_leading_dims(dev):
