@@ -38,12 +38,15 @@ struct GptqArgs {
   int64_t ngc;            // static groups: groups per row of s_in / z_in
 };
 
-// 8 lanes per row, 16 consecutive block columns per lane (32 rows per 256-thread workgroup).
-// Column c's owner lane (c / 16) quantizes it; its error is broadcast to the row's other 7
-// lanes with one shuffle; every lane applies the rank-1 update to its own columns > c. W, err
-// and losses are written once at the end with 16-byte stores (a row's 8 lanes cover 512
-// contiguous bytes). err is written k-major ([128][rows]) for the trailing GEMM's staging.
-constexpr int LPR = 8, CPL = GB / LPR;
+// 16 lanes per row, 8 consecutive block columns per lane (16 rows per 256-thread workgroup:
+// a 4096-row linear is 256 workgroups; with 8 lanes x 16 columns it was 128, half the chip,
+// each lane carrying twice the updates per column). Column c's owner lane (c / 8) quantizes
+// it; its error is broadcast to the row's other 15 lanes with one shuffle; every lane applies
+// the rank-1 update to its own columns > c -- the same per-element operations in any layout,
+// so the result is unchanged bit for bit. W, err and losses are written once at the end with
+// 16-byte stores (a row's 16 lanes cover 512 contiguous bytes). err is written k-major
+// ([128][rows]) for the trailing GEMM's staging.
+constexpr int LPR = 16, CPL = GB / LPR;
 
 // FMT = 0: IntegerQuantizer (quant.py:699-717); FMT = LCQ_FP8E4M3 / LCQ_FP8E5M2: FloatQuantizer
 // use_qtorch (quant.py:1061-1080): q = float_quantize(w / s + 0) * s in fp32, sym qparams with
@@ -69,7 +72,7 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
   }
   __syncthreads();
   const int sub = tid & (LPR - 1);
-  const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + (tid >> 3);
+  const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + (tid / LPR);
   const bool valid = r < a.rows;  // invalid lanes still run (shuffles), never store
   const int cb = sub * CPL;       // first block column of this lane
   float* wrow = a.W + (valid ? r : 0) * a.ld + a.col0;
@@ -85,10 +88,10 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
     }
   }
   // group qparams from the block-start weights (gptq.py:215-223 reads W, not W1); GS >= 32
-  // so a lane's 16 columns lie in one group of GS / 16 adjacent lanes
+  // so a lane's 8 columns lie in one group of GS / 8 adjacent lanes
   float qs, qz;
   if constexpr (GS > 0) {
-    constexpr int LG = GS / CPL;  // lanes per group (2, 4, 8)
+    constexpr int LG = GS / CPL;  // lanes per group (4, 8, 16)
     float mn = INFINITY, mx = -INFINITY;
 #pragma unroll
     for (int k = 0; k < CPL; ++k)
