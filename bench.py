@@ -651,8 +651,8 @@ def bench_fp8_forward(args, weights, dev, world):
     t = kern.get('lcq_fp8_gemm')
     if t:
         tf = flops * args.steps / (t['total_ms'] * 1e-3) / 1e12
-        out['roofline'] = {'kernel': 'lcq_fp8_gemm (k_fp8_gemm2 on grids of >= 128 256x256 tiles, '
-                                     'else k_fp8_gemm)', 'bound': 'mfma',
+        out['roofline'] = {'kernel': 'lcq_fp8_gemm (k_fp8_gemm2 on grids of >= 64 256x256 tiles, '
+                                     'split-K below 224; else k_fp8_gemm)', 'bound': 'mfma',
                            'achieved': round(tf, 1), 'peak': PEAK_FP8_TFLOPS, 'unit': 'TFLOP/s',
                            'frac': round(tf / PEAK_FP8_TFLOPS, 4), 'traffic': None,
                            'flops_per_launch': flops / len(weights),
