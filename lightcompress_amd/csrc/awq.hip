@@ -184,12 +184,7 @@ __global__ void __launch_bounds__(1024) k_awq_scales(const void* xmean, int64_t 
 // ----------------------------------------------------------------------------------------
 constexpr int SB_ROWS = 32;
 
-__device__ __forceinline__ float div_exact(float x, float s, float rs) {
-  const float q = div_mk(x, s, rs);
-  const float a = fabsf(q);
-  return (a >= 0x1p-100f && a <= 3.40282347e38f && fabsf(x) >= 0x1p-100f) ? q
-                                                                         : __fdiv_rn(x, s);
-}
+// div_exact: lcq_common.h
 
 template <int DT, int OP, int AXIS>
 __global__ void __launch_bounds__(256) k_scale_bcast(const void* x, int64_t rows, int64_t cols,

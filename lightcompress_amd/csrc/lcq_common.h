@@ -66,6 +66,18 @@ __device__ __forceinline__ float div_mk(float a, float b, float rb) {
   const float e = __fmaf_rn(-b, q0, a);
   return __fmaf_rn(e, rb, q0);
 }
+// a / b exactly as IEEE division, from rb = RN(1 / b): the Markstein quotient where the
+// residual and the correction stay clear of the subnormal range (|a|, |q| >= 2^-100, q finite,
+// rb normal), the IEEE division otherwise (zero, tiny, inf, NaN). Checked bit for bit against
+// __fdiv_rn (tests/test_awq_gpu.py scale-broadcast exhaustive test, gptq in-block tests).
+__device__ __forceinline__ float div_exact(float a, float b, float rb) {
+  const float q = div_mk(a, b, rb);
+  const float aq = fabsf(q);
+  return (aq >= 0x1p-100f && aq <= 3.40282347e38f && fabsf(a) >= 0x1p-100f &&
+          fabsf(rb) >= 0x1p-126f)
+             ? q
+             : __fdiv_rn(a, b);
+}
 __device__ __forceinline__ float f16_rne(float f) { return (float)(_Float16)f; }
 
 // Translation units that define LCQ_BF16_HW before including this header (the streaming
