@@ -363,9 +363,21 @@ class Llama(BaseModel):
         """Block kwargs the Catcher would capture for an unpadded causal batch."""
         device = device or next(self.model.parameters()).device
         pos = torch.arange(seq_len, device=device).unsqueeze(0)
-        dummy = torch.empty((1, seq_len, 1), dtype=self.torch_dtype, device=device)
-        cos, sin = self.rotary_emb(dummy, pos)
+        cos, sin = self._rotary_table(pos)
         return {'position_embeddings': (cos, sin), 'attention_mask': None, 'position_ids': pos}
+
+    def _rotary_table(self, pos):
+        """LlamaRotaryEmbedding.forward's cos / sin (the model's own inv_freq and attention
+        scaling, rope_scaling included) with its `inv_freq @ position_ids` -- a K = 1 product,
+        one rounding per element -- as an elementwise outer product: the same values bit for
+        bit, without a vendor GEMM launch."""
+        re = self.rotary_emb
+        inv = re.inv_freq.float().to(pos.device)
+        freqs = pos[0].float()[:, None] * inv[None, :]
+        emb = torch.cat((freqs, freqs), dim=-1)
+        scale = getattr(re, 'attention_scaling', 1.0)
+        dt = self.torch_dtype
+        return (emb.cos() * scale).to(dt)[None], (emb.sin() * scale).to(dt)[None]
 
     # -- BaseModel contract ---------------------------------------------------------------------
     def get_subsets_in_block(self, block):
