@@ -79,6 +79,11 @@ def parse():
     ap.add_argument('--gptq-samples', type=int, default=128)
     ap.add_argument('--gptq-seq-len', type=int, default=2048)
     ap.add_argument('--cpu-budget-s', type=float, default=20.0)
+    ap.add_argument('--no-stream', action='store_true',
+                    help='skip the host-resident (streamed) e2e runs')
+    ap.add_argument('--rank-timeout', type=float, default=3000.0,
+                    help='bench.py --gpus N without a launcher: kill every rank after this many '
+                         'seconds (0: no limit)')
     ap.add_argument('--no-l70b', action='store_true',
                     help='skip the Llama-3-70B-shaped block leg (BASELINE configs[3])')
     return ap.parse_args()
@@ -427,14 +432,15 @@ def bench_gptq(args, rank, world, dev):
            'workload': (f'Llama-3-8B GPTQ w4a16 g128 asym act-order true_sequential quant_out, '
                         f'{args.gptq_samples}x{seq} calib tokens (bs 1)'),
            'lcq_kernels': kernel_table(kern, elapsed)}
-    h = kern.get('lcq_hessian_accum')
+    h = kern.get('lcq_hessian_grouped') or kern.get('lcq_hessian_accum')
     if h:
         # algorithmic: symmetric rank-n update n*ic*(ic+1) flops per launch
         tf = h['flops'] / (h['total_ms'] * 1e-3) / 1e12
-        traffic, src = pmc_traffic('gptq', ('k_syrk_x',))
-        out['roofline'] = {'kernel': 'lcq_hessian_accum (k_syrk_x: bf16 MFMA XᵀX read from '
-                                     'token-major X through transposed LDS reads; one launch '
-                                     'per calibration-sample group)',
+        traffic, src = pmc_traffic('gptq', ('k_syrk_x', 'k_syrk_reduce'))
+        out['roofline'] = {'kernel': 'lcq_hessian_grouped (k_syrk_x: bf16 MFMA XᵀX read from '
+                                     'token-major X through transposed LDS reads, all 8 '
+                                     'calibration-sample groups in one launch; k_syrk_reduce: '
+                                     'per-group fold + fixed group tree)',
                            'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
                            'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4),
                            'traffic': traffic, 'traffic_source': src,
@@ -445,16 +451,23 @@ def bench_gptq(args, rank, world, dev):
     return out
 
 
-def bench_e2e(args, rank, world, dev, which):
+def bench_e2e(args, rank, world, dev, which, residency='device'):
     """Whole-model wall-clock (MEASURED, not extrapolated): a random-init 32-block Llama-3-8B
     through build_algo -> run_block_loop -> deploy, the span the reference times as
-    llmc_duration_time (llmc/__main__.py:182, 265-267) minus model loading / dataset / eval."""
+    llmc_duration_time (llmc/__main__.py:182, 265-267) minus model loading / dataset / eval.
+    residency 'stream': the blocks live in pinned host memory and pass through HBM one at a
+    time (the reference's block.cuda() / block.cpu() scheme, base_blockwise_quantization.py:397,
+    418, with the uploads and write-backs on side streams)."""
     from transformers import LlamaConfig
     from lightcompress_amd.llama import Llama
     from lightcompress_amd.pipeline import build_algo
     cfg = LlamaConfig(**LLAMA3_8B)
     nb = args.e2e_blocks
-    model = Llama.random(cfg, num_layers=nb, device=dev, seed=3000 if which == 'awq' else 4000)
+    model = Llama.random(cfg, num_layers=nb, device=dev, seed=3000 if which == 'awq' else 4000,
+                         residency=residency)
+    torch.cuda.empty_cache()
+    hbm0 = torch.cuda.memory_allocated(dev)
+    torch.cuda.reset_peak_memory_stats(dev)
     if which == 'awq':
         hidden = synthetic_hidden(args.n_samples, args.seq_len, cfg.hidden_size, dev, 41)
         calib = {'data': [hidden], 'kwargs': [model.rotary_kwargs(args.seq_len)]}
@@ -476,12 +489,20 @@ def bench_e2e(args, rank, world, dev, which):
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     t_loop = max_over_ranks(t_loop, world, dev)
     mode = algo.parallel_mode()
+    out = {'wall_s': round(elapsed, 2), 'block_loop_s': round(t_loop, 2),
+           'blocks': nb, 'linears': N_LINEARS_PER_BLOCK * nb,
+           'linears_per_s': round(N_LINEARS_PER_BLOCK * nb / elapsed, 3),
+           'deploy': fmt, 'parallel_mode': mode, 'residency': residency,
+           'hbm_at_start_gb': round(hbm0 / 2 ** 30, 2),
+           'hbm_peak_gb': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)}
+    if model.streamer is not None:
+        st = model.streamer.stats
+        out['streamed'] = {'h2d_gb': round(st['h2d_bytes'] / 2 ** 30, 2),
+                           'd2h_gb': round(st['d2h_bytes'] / 2 ** 30, 2),
+                           'fetches': st['fetches'], 'prefetched': st['prefetched']}
     del algo, model, hidden, calib
     torch.cuda.empty_cache()
-    return {'wall_s': round(elapsed, 2), 'block_loop_s': round(t_loop, 2),
-            'blocks': nb, 'linears': N_LINEARS_PER_BLOCK * nb,
-            'linears_per_s': round(N_LINEARS_PER_BLOCK * nb / elapsed, 3),
-            'deploy': fmt, 'parallel_mode': mode}
+    return out
 
 
 def bench_l70b(args, rank, world, dev):
@@ -548,67 +569,107 @@ def bench_l70b(args, rank, world, dev):
 DSV3_EXPERT = dict(hidden=7168, moe_inter=2048, block=128)
 
 
+def dsv3_config(n_layers, n_experts):
+    """DeepSeek-V3's layer shapes (public config: hidden 7168, MLA q_lora 1536 / kv_lora 512 /
+    128 heads of 128 + 64 rope, routed experts 2048 wide, one shared expert) with every layer
+    an MoE layer; the vocabulary is cut to 1024 (embeddings are not on the deploy path)."""
+    from transformers import DeepseekV3Config
+    cfg = DeepseekV3Config(hidden_size=7168, intermediate_size=18432, moe_intermediate_size=2048,
+                           num_hidden_layers=n_layers, num_attention_heads=128,
+                           num_key_value_heads=128, n_shared_experts=1,
+                           n_routed_experts=n_experts, num_experts_per_tok=8, n_group=1,
+                           topk_group=1, first_k_dense_replace=0, q_lora_rank=1536,
+                           kv_lora_rank=512, qk_nope_head_dim=128, qk_rope_head_dim=64,
+                           v_head_dim=128, vocab_size=1024, max_position_embeddings=4096,
+                           tie_word_embeddings=False)
+    cfg._attn_implementation = 'sdpa'
+    return cfg
+
+
+def fp8_rtn_config(world):
+    """BASELINE configs[4]'s quantization (configs/quantization/backend/vllm/fp8/rtn_fp8.yml
+    with per-tensor granularity): RTN, e4m3 weights + e4m3 activations per tensor, data-free,
+    deployed as vllm_quant; each rank materialises only its LPT share of the units (a routed
+    expert's three linears are one unit: EP-style), so N ranks hold N x the experts."""
+    from lightcompress_amd.utils import load_config
+    return load_config({
+        'model': {'type': 'DeepseekV3', 'torch_dtype': 'torch.float8_e4m3fn',
+                  'block_wise_quant': True, 'materialize': 'owned' if world > 1 else 'all'},
+        'quant': {'method': 'RTN',
+                  'weight': {'quant_type': 'float-quant', 'bit': 'e4m3', 'symmetric': True,
+                             'granularity': 'per_tensor', 'use_qtorch': True},
+                  'act': {'quant_type': 'float-quant', 'bit': 'e4m3', 'symmetric': True,
+                          'granularity': 'per_tensor', 'use_qtorch': True}}})
+
+
 def bench_fp8(args, rank, world, dev):
-    """FP8 leg (BASELINE.json configs[4]): DeepSeek-V3 expert linears (gate/up 2048x7168,
-    down 7168x2048) stored block-fp8 (128x128, fp32 scale_inv) as in the checkpoints; one unit
-    = one expert linear through the reference's real-quant deploy for an fp8 weight:
-    weight_cast_to_bf16 (module_utils.py:917-922) + FloatQuantizer(e4m3, per_tensor)
-    .real_quant_weight_dynamic (quant.py:1191-1221). One step = args.fp8_experts experts x 3
-    linears per rank (experts shard across ranks: weak scaling, no collective)."""
-    from lightcompress_amd import _native, ops
-    from lightcompress_amd.quant import FloatQuantizer
-    E = args.fp8_experts
-    H, I = DSV3_EXPERT['hidden'], DSV3_EXPERT['moe_inter']
-    g = torch.Generator(device=dev).manual_seed(77 + rank)
-    shapes = [(I, H), (I, H), (H, I)]
-    weights = []
-    for e in range(E):
-        for (m, n) in shapes:
-            w = (torch.randn(m, n, device=dev, generator=g) * 0.02).to(torch.bfloat16)
-            r = ops.fp8_quant_blocks(w, torch.float8_e4m3fn, 128, qmax=448.0, clamp_min=0.0,
-                                     add_zero=False)
-            weights.append((r['codes'], r['scales']))
-        del w
-    q = FloatQuantizer('e4m3', True, 'per_tensor', use_qtorch=True)
-    codes_l = [c for c, _ in weights]
-    sinv_l = [s for _, s in weights]
+    """FP8 leg (BASELINE.json configs[4]): DeepSeek-V3 MoE layers stored block-fp8 (128x128,
+    fp32 weight_scale_inv) as in the checkpoints, through the reference's data-free RTN
+    pipeline: build_algo -> run_block_loop -> algo.deploy('vllm_quant') (per-tensor e4m3 real
+    quant of every block linear: module_utils.py:914-927 + quant.py:1191-1221; each block's
+    fp8 linears requantized in one batched launch pair). One step = one MoE layer: MLA (5
+    linears), shared expert (3), args.fp8_experts routed experts per rank (x 3); at N > 1 the
+    units are LPT-sharded with materialize: owned (no collective), weak scaling."""
+    from lightcompress_amd import _native
+    from lightcompress_amd.deepseekv3 import DeepseekV3
+    from lightcompress_amd.pipeline import build_algo
+    E = args.fp8_experts * world
+    config = fp8_rtn_config(world)
 
-    def step():  # one MoE layer slice: all its expert linears in one batched launch pair
-        q.real_quant_weights_from_block_fp8(codes_l, sinv_l, 128)
+    def build(n_layers, seed):
+        return DeepseekV3(config, device=dev, dtype=torch.float8_e4m3fn,
+                          hf_config=dsv3_config(n_layers, E),
+                          random_init={'seed': seed, 'std': 0.02})
 
-    step()
+    wm = build(1, 7)   # warm-up: one layer through the same path
+    build_algo(wm, config, None).deploy('vllm_quant')
+    del wm
+    torch.cuda.empty_cache()
+    model = build(args.steps, 77)
+    algo = build_algo(model, config, None)
+    mine = [(m.weight.numel()) for b in model.get_blocks()
+            for m in model.get_block_linears(b).values() if not m.weight.is_meta]
+    n_units, elems = len(mine), float(sum(mine))
+    fwd_w = [(m.weight.data, m.weight_scale_inv.data)
+             for n, m in model.get_block_linears(model.get_blocks()[0]).items()
+             if '.experts.' in n and not m.weight.is_meta][:12]
+    fwd_w = [(c.clone(), s.clone()) for c, s in fwd_w]
     timer = _native.KernelTimer()
     sync_barrier(world)
     t0 = time.perf_counter()
     with timer:
-        for _ in range(args.steps):
-            step()
+        algo.run_block_loop()
+        algo.deploy('vllm_quant')
     sync_barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     kern = timer.summary()
-    units = 3 * E * args.steps * world
-    elems = sum(c.numel() for c, _ in weights)
-    out = {'linears_per_s': round(units / elapsed, 1),
+    units = torch.tensor([n_units], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(units)
+    out = {'linears_per_s': round(units.item() / elapsed, 1),
            'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'steps': args.steps,
-           'warmup': 1,
-           'workload': (f'DeepSeek-V3 MoE expert linears (gate/up 2048x7168, down 7168x2048), '
-                        f'block-fp8 source -> bf16 -> FP8 e4m3 per-tensor real quant; '
-                        f'{E} experts x 3 linears per rank per step'),
+           'warmup': 1, 'mode': algo.parallel_mode(),
+           'workload': (f'DeepSeek-V3 MoE layers (MLA + shared expert + {E} routed experts of '
+                        f'2048x7168 / 7168x2048), block-fp8 checkpoint layout, data-free RTN '
+                        f'e4m3 per-tensor W+A (rtn_fp8.yml per_tensor) through algo.deploy('
+                        f"'vllm_quant'); {args.fp8_experts} experts x 3 linears per rank per "
+                        f'layer, 1 layer per step'),
+           'linears_per_rank': n_units,
            'lcq_kernels': kernel_table(kern, elapsed)}
     t = kern.get('lcq_fp8_block_to_tensor_many')
     if t:
-        # algorithmic bytes per expert linear: 1 B fp8 read + 1 B fp8 written per element
-        gbs = elems * 2.0 * t['launches'] / (t['total_ms'] * 1e-3) / 1e9
+        # algorithmic bytes: 1 B fp8 read + 1 B fp8 written per weight element
+        gbs = elems * 2.0 / (t['total_ms'] * 1e-3) / 1e9
         traffic, src = pmc_traffic('fp8', ('k_bmax16_many', 'k_requant16_many'))
         out['roofline'] = {'kernel': 'lcq_fp8_block_to_tensor_many (k_bmax16_many + '
                                      'k_requant16_many)', 'bound': 'hbm',
                            'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                            'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic,
-                           'traffic_source': src, 'avg_launch_ms': round(t['avg_ms'], 4)}
-    n_fwd = min(4, E) * 3
-    out['calib_forward'] = bench_fp8_forward(args, weights[:n_fwd], dev, world)
-    del weights
+                           'traffic_source': src, 'avg_launch_ms': round(t['avg_ms'], 4),
+                           'algorithmic_bytes_per_launch': elems * 2.0 / t['launches']}
+    del algo, model
     torch.cuda.empty_cache()
+    out['calib_forward'] = bench_fp8_forward(args, fwd_w, dev, world)
     return out
 
 
@@ -660,45 +721,54 @@ def bench_fp8_forward(args, weights, dev, world):
     return out
 
 
-def launch_ranks(n: int) -> int:
+def launch_ranks(n: int, limit_s: float = 0.0) -> int:
     """`bench.py --gpus N` without a launcher: start N rank processes of this script (one per
     GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1 rendezvous) and wait. This
     process never touches the GPU (children are fresh interpreters, no exec of a GPU process);
-    rank 0 prints the JSON line. Returns the first non-zero child exit code (others killed)."""
+    rank 0 prints the JSON line. Returns the first non-zero child exit code (others killed), or
+    124 when ranks are still running after `limit_s` seconds (all killed, the stragglers
+    named)."""
     import socket
     import subprocess
     with socket.socket() as sk:
         sk.bind(('127.0.0.1', 0))
         port = sk.getsockname()[1]
-    procs = []
+    procs = {}
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__),
-                                       *sys.argv[1:]], env=env))
+        procs[r] = subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__),
+                                     *sys.argv[1:]], env=env)
     rc = 0
+    t0 = time.time()
     try:
         while procs:
-            for p in list(procs):
+            if limit_s and time.time() - t0 > limit_s:
+                print(f'bench.py: ranks {sorted(procs)} still running after {limit_s:.0f} s: '
+                      'killing every rank', file=sys.stderr, flush=True)
+                return 124
+            for r, p in list(procs.items()):
                 code = p.poll()
                 if code is None:
                     continue
-                procs.remove(p)
+                del procs[r]
                 if code != 0 and rc == 0:
                     rc = code
-                    for q in procs:
+                    for q in procs.values():
                         q.terminate()
             time.sleep(0.2)
     finally:
-        for q in procs:
+        for q in procs.values():
             q.kill()
+        for q in procs.values():
+            q.wait()
     return rc
 
 
 def main():
     args = parse()
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
-        raise SystemExit(launch_ranks(args.gpus))
+        raise SystemExit(launch_ranks(args.gpus, args.rank_timeout))
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
@@ -761,6 +831,10 @@ def main():
     if not args.no_e2e and args.algo == 'all':
         e2e = {'awq': bench_e2e(args, rank, world, dev, 'awq'),
                'gptq': bench_e2e(args, rank, world, dev, 'gptq')}
+        if not args.no_stream:
+            # the same two runs with the model host-resident, streamed block by block
+            e2e['awq_stream'] = bench_e2e(args, rank, world, dev, 'awq', 'stream')
+            e2e['gptq_stream'] = bench_e2e(args, rank, world, dev, 'gptq', 'stream')
 
     if rank == 0:
         roofline = gemm_roofline(kern, elapsed)
@@ -791,6 +865,11 @@ def main():
             'lcq_kernels': kernel_table(kern, elapsed),
             'cpu_baseline': cpu,
         }
+        try:
+            import psutil
+            line['child_processes_at_exit'] = len(psutil.Process().children(recursive=True))
+        except ImportError:
+            pass
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

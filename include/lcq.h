@@ -181,6 +181,18 @@ int64_t lcq_hessian_workspace_bytes(int64_t n, int64_t ic);
 int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t ic, void* H, float alpha,
                       float beta, void* workspace, int64_t ws_bytes, void* stream);
 
+/* The grouped GPTQ Hessian (gptq_core.HessianAccumulator) in ONE launch: x [n, ic] token-major,
+ * bounds (host int64 [ng + 1], bounds[0] = 0) cut it into ng = 1 / 2 / 4 / 8 token groups;
+ * every group's X^T X is split over K-tile slabs by a plan that depends only on the group's
+ * token count and ic (world-independent), each slab's upper-tile partial goes to the workspace,
+ * and one reduce folds each group's slabs in order, sums the groups in the fixed tree
+ * ((g0 + g1) + (g2 + g3)) + ((g4 + g5) + (g6 + g7)) and writes H = alpha * tree, mirrored
+ * (gptq.py:253-295 accumulates the same samples as a running average). Bit-identical to one
+ * lcq_hessian_accum per group + lcq_tree_sum. */
+int64_t lcq_hessian_grouped_workspace_bytes(const int64_t* bounds, int ng, int64_t ic);
+int lcq_hessian_grouped(const void* x, int x_dtype, int64_t ic, const int64_t* bounds, int ng,
+                        void* H, float alpha, void* workspace, int64_t ws_bytes, void* stream);
+
 /* Deterministic reduction of Hessian partials (the grouped GPTQ Hessian: the calibration
  * samples of add_batch, gptq.py:253-295, cut into 8 fixed groups, so that token-sharded ranks
  * and one GPU sum them in the same order): out[i] = alpha * tree(parts[0..np)[i]) with the
@@ -233,6 +245,18 @@ int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const void* A, in
  * failure and only if still 0 (the order of the leading minor torch.linalg.cholesky reports). */
 int lcq_chol_inv_tile(const void* A, int64_t lda, int n, void* L, int64_t ldl, void* X,
                       int64_t ldx, void* info, int64_t row0, void* stream);
+
+/* GPTQ act-order preparation (gptq.py:58-64, 128-176) as one gather pass: out[i][j] =
+ * f(A[rsrc[i]][csrc[j]]) (rsrc / csrc int64 index arrays, NULL = identity), A bf16 or fp32
+ * [rows, lda], out fp32 [rows, ldo]; f widens to fp32, zeroes dead_col[csrc[j]] columns
+ * (prepare_weight: W[:, dead] = 0; W[:, perm]), and on the diagonal i == j sets
+ * dead_diag[csrc[j]] entries to 1 then adds *damp (prepare_hessian: H[dead, dead] = 1;
+ * H[perm][:, perm]; H[d, d] += damp, with rsrc = csrc = perm reversed for the chain's J H J).
+ * uint8 masks / damp may be NULL. cols <= 40960 (one LDS row). */
+int lcq_gather_rc(const void* A, int a_dtype, int64_t rows, int64_t cols, int64_t lda,
+                  const int64_t* rsrc, const int64_t* csrc, const uint8_t* dead_col,
+                  const uint8_t* dead_diag, const float* damp, void* out, int64_t ldo,
+                  void* stream);
 
 /* GPTQ trailing update W[:, c1:c2] -= err^T[:, :cnt] @ U[c0:c0+cnt, c1:c2] (gptq.py:244) on
  * fp32 MFMA (k-ordered fma chain: deterministic and independent of the row range, so

@@ -59,12 +59,16 @@ SIGNATURES = {
     'lcq_hessian_workspace_bytes': ([_i64, _i64], _i64),
     'lcq_hessian_accum': ([_vp, _int, _i64, _i64, _vp, _f32, _f32, _vp, _i64, _vp], _int),
     'lcq_tree_sum': ([_vp, _int, _i64, _f32, _vp, _vp], _int),
+    'lcq_hessian_grouped_workspace_bytes': ([_vp, _int, _i64], _i64),
+    'lcq_hessian_grouped': ([_vp, _int, _i64, _vp, _int, _vp, _f32, _vp, _i64, _vp], _int),
     'lcq_gptq_block': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _int, _int, _int, _int,
                         _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
     'lcq_gptq_block_cols': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _int, _int, _vp, _vp, _vp,
                              _i64, _vp, _vp, _vp], _int),
     'lcq_chol_inv_tile': ([_vp, _i64, _int, _vp, _i64, _vp, _i64, _vp, _i64, _vp], _int),
     'lcq_gptq_trailing': ([_vp, _i64, _i64, _i64, _int, _i64, _i64, _vp, _vp, _i64, _vp], _int),
+    'lcq_gather_rc': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp],
+                      _int),
     'lcq_colmean_workspace_bytes': ([_i64, _i64], _i64),
     'lcq_absmean_cols': ([_vp, _int, _i64, _i64, _vp, _vp, _vp], _int),
     'lcq_awq_weight_scale': ([_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp], _int),

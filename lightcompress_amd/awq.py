@@ -182,8 +182,7 @@ class Awq(BaseBlockwiseQuantization):
         setting (activation quant, awq_bs batching, padding masks: the module forward runs).
         Same math as the module forward on the lcq GEMM (fp32 accumulation, one rounding per
         output), so a reused capture-forward org_out and the ratios' outputs stay comparable."""
-        from .module_utils import _GEMM_ON
-        if not (_GEMM_ON and self.fused_search and getattr(self, 'w_only', True)
+        if not (self.fused_search and getattr(self, 'w_only', True)
                 and self._bs == x.shape[0] and not getattr(self, 'padding_mask', None)):
             return None
         mods = list(layers)

@@ -73,7 +73,8 @@ class BlockwiseOpt:
     sequential_parallel_mode = 'replicate'
 
     def parallel_mode(self) -> str:
-        """'single' | 'shard_blocks' | 'shard_search' | 'shard_tokens' | 'replicate'.
+        """'single' | 'shard_blocks' | 'shard_units' | 'shard_search' | 'shard_tokens' |
+        'replicate'.
 
         Blocks can be sharded when each block's input does not depend on the quantization of
         the previous one (quant_out False); otherwise the work inside a block
@@ -87,7 +88,7 @@ class BlockwiseOpt:
         if mode:
             return mode
         if self.data_free:
-            return 'replicate'
+            return 'shard_units'   # independent linears / experts
         if not self.quant_config.get('quant_out', False):
             return 'shard_blocks'
         return self.sequential_parallel_mode
@@ -120,26 +121,64 @@ class BlockwiseOpt:
     def run_block_loop(self):
         mode = self.parallel_mode()
         rank, world = P.dist_world()
+        own = getattr(self.model, 'ownership', None)
+        if own is not None and own.mode != mode:
+            raise RuntimeError(f'model materialised for {own.mode}, algorithm runs {mode}')
         if mode == 'shard_blocks' and not self.data_free and self._handoff_ok():
             self._run_block_loop_ring(rank, world)
             return
-        for i in range(len(self.blocks)):
+        if own is not None and mode == 'shard_blocks':
+            raise NotImplementedError('materialize: owned with shard_blocks needs the ring '
+                                      'pipeline (tensor block inputs, the base block_opt)')
+        n = len(self.blocks)
+        for i in range(n):
             self.block_idx = i
             if mode == 'shard_blocks' and i % world != rank:
                 # not ours: only advance the float activation chain (quant_out False); the
                 # staged forward's memo of this block (stage outputs: GBs at calibration
                 # sizes) is dropped at once, as block_opt does for owned blocks
                 if not self.data_free:
-                    self.input['data'] = self.block_forward(self.blocks[i])
-                    self._clear_block_cache(self.blocks[i])
+                    def fwd(i=i):
+                        self.input['data'] = self.block_forward(self.blocks[i])
+                        self._clear_block_cache(self.blocks[i])
+                    self.visit_block(i, fwd, next_i=i + 1, dirty=False)
                 continue
-            self.block_opt(self.blocks[i])
+            if not self.block_has_work():
+                continue   # nothing to do per block (weight-only RTN): deploy streams itself
+            self.visit_block(i, lambda i=i: self.block_opt(self.blocks[i]), next_i=i + 1)
+        self._drain_blocks()
         if mode == 'shard_blocks':
             # blocks stay on their owners until it is known what the other ranks need: a
             # real-quant deploy gathers the quantized shards only (packed codes + scales,
-            # _publish_deployed), anything else the transformed float blocks (materialize)
+            # P.publish), anything else the transformed float blocks (materialize)
             self._pending_owner = {i: i % world for i in range(len(self.blocks))}
         self.save_transforms()
+
+    def block_has_work(self) -> bool:
+        """Whether block_opt does anything (RTN weight-only: no -- its blocks are not even
+        uploaded by a streaming run's block loop)."""
+        return True
+
+    # ---- block residency (residency.py) --------------------------------------------------
+    def visit_block(self, i, fn, next_i=None, dirty=True):
+        """Run fn with block i in HBM. Streaming models upload block i (or take the prefetch
+        already in flight), start block next_i's upload on the H2D stream, run fn, and write
+        block i back on the D2H stream (``dirty`` False: forward only, nothing to write)."""
+        st = getattr(self.model, 'streamer', None)
+        if st is None:
+            return fn()
+        st.fetch(i)
+        if next_i is not None:
+            st.prefetch(next_i)
+        try:
+            return fn()
+        finally:
+            st.evict(i, dirty=dirty)
+
+    def _drain_blocks(self):
+        st = getattr(self.model, 'streamer', None)
+        if st is not None:
+            st.drain()
 
     def _handoff_ok(self):
         """The ring hand-off passes self.input['data'] as a list of tensors whose shapes every
@@ -162,11 +201,12 @@ class BlockwiseOpt:
                 P.pass_tensors(self.input['data'], src, groups[src])
             self.block_idx = i
             self._handoff = (rank, groups[rank]) if i + 1 < n else None
-            self.block_opt(self.blocks[i])
+            self.visit_block(i, lambda i=i: self.block_opt(self.blocks[i]), next_i=i + world)
             # every owner of a non-last block hands its output on exactly once (run() does it
             # right after the forward; a path that did not forward must not leave the next
             # owner waiting)
             self._send_handoff()
+        self._drain_blocks()
         self._pending_owner = {i: i % world for i in range(n)}
         self.save_transforms()
 
@@ -182,52 +222,19 @@ class BlockwiseOpt:
         pending = getattr(self, '_pending_owner', None)
         if not pending:
             return
-        for i, block in enumerate(self.blocks):
-            P.broadcast_block(block, owner=pending[i])
+        if getattr(self.model, 'ownership', None) is not None:
+            raise RuntimeError('materialize: owned -- this rank holds only its own blocks '
+                               '(save_model writes per-rank shards)')
+
+        def pub(block, owner):
+            P.broadcast_block(block, owner=owner)
             # the broadcast writes weights through .data (no version bump): no memoised
             # stage may survive it
             self._clear_block_cache(block)
+        for i, block in enumerate(self.blocks):
+            self.visit_block(i, lambda b=block, o=pending[i]: pub(b, o), next_i=i + 1)
+        self._drain_blocks()
         self._pending_owner = None
-
-    @torch.no_grad()
-    def _publish_deployed(self, block, owner):
-        """After the owner replaced this block's linears by real-quant modules: the other
-        ranks build empty modules of the same class, buffer shapes and plain attributes
-        (their float linears are dropped unread), then every parameter and buffer of the
-        block -- norms in float, linears as packed codes + scales -- comes from the owner."""
-        import importlib
-        rank, _ = P.dist_world()
-        lins = self.model.get_block_linears(block)
-        spec = [None]
-        if rank == owner:
-            spec = [[(n, type(m).__module__, type(m).__qualname__,
-                      {k: v for k, v in m.__dict__.items()
-                       if not k.startswith('_') and k != 'training'
-                       and isinstance(v, (int, float, str, bool, tuple, torch.Size,
-                                          torch.dtype, type(None)))},
-                      [(bn, None if b is None else tuple(b.shape),
-                        None if b is None else str(b.dtype).split('.')[-1])
-                       for bn, b in m._buffers.items()])
-                     for n, m in lins.items()]]
-        dist.broadcast_object_list(spec, src=owner)
-        if rank != owner:
-            dev = next(block.parameters(), next(block.buffers(), None)).device
-            for n, modname, qual, attrs, bufs in spec[0]:
-                cls = importlib.import_module(modname)
-                for part in qual.split('.'):
-                    cls = getattr(cls, part)
-                m = cls.__new__(cls)
-                nn.Module.__init__(m)
-                for bn, shape, dt in bufs:
-                    m.register_buffer(bn, None if shape is None else
-                                      torch.empty(shape, dtype=getattr(torch, dt), device=dev))
-                for k, v in attrs.items():
-                    setattr(m, k, v)
-                parent_name, _, child = n.rpartition('.')
-                parent = block.get_submodule(parent_name) if parent_name else block
-                setattr(parent, child, m)
-        P.broadcast_block(block, owner=owner)
-        self._clear_block_cache(block)
 
     def save_transforms(self):
         """blockwise_optimization.py:40-52: the AWQ scales (save_scale) and v2 clip factors
@@ -755,36 +762,77 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                 input_feat[name][i] = done[key]
 
     # ---- deploy / save (:932-1029) ---------------------------------------------------------
+    def unit_owner(self, block_idx: int, linear_name: str) -> int:
+        """The rank that quantizes (and packs) this linear in a sharded deploy: its block's
+        owner under shard_blocks, else the LPT unit plan (residency.Ownership, shared by the
+        loader of a ``materialize: owned`` model)."""
+        own = getattr(self.model, 'ownership', None)
+        if own is not None:
+            return own.owner_of(block_idx, linear_name)
+        pending = getattr(self, '_pending_owner', None)
+        if pending:
+            return pending[block_idx]
+        if getattr(self, '_unit_plan', None) is None:
+            from .residency import Ownership
+            rank, world = P.dist_world()
+            self._unit_plan = Ownership.plan('shard_units', rank, world, self.model)
+        return self._unit_plan.owner_of(block_idx, linear_name)
+
+    def owned_linears(self, block) -> dict:
+        """The block linears this rank works on: all of them, except under shard_units."""
+        lins = self.model.get_block_linears(block)
+        if self.parallel_mode() != 'shard_units':
+            return lins
+        rank, _ = P.dist_world()
+        return {n: m for n, m in lins.items() if self.unit_owner(self.block_idx, n) == rank}
+
     @torch.no_grad()
     def deploy(self, quant_format, keep_device=True):
+        """base_blockwise_quantization.py:932-977. Sharded runs (shard_units, shard_blocks
+        with a real-quant format, or a ``materialize: owned`` model) quantize on each rank
+        only what it owns; the results -- packed codes + scales for real-quant formats -- are
+        then published to every rank (P.publish: one flat broadcast per block and owner), or
+        stay on their owners for a sharded save when each rank holds only its own units.
+        Streaming models pass every block through HBM once (visit_block)."""
         mapping = {'origin_float': OriginFloatLinear, 'fake_quant': EffcientFakeQuantLinear,
                    'fake_quant_wo_kv': EffcientFakeQuantLinear, **_REALQUANT_LINEAR_MAP_}
         if quant_format not in mapping:
             raise NotImplementedError(f"Quant format '{quant_format}' is not implemented.")
+        module = mapping[quant_format]
+        real = quant_format in _REALQUANT_LINEAR_MAP_
+        params = self.get_replacement_params(quant_format, self.w_only)
+        rank, world = P.dist_world()
+        own = getattr(self.model, 'ownership', None)
         pending = getattr(self, '_pending_owner', None)
-        if pending and quant_format in _REALQUANT_LINEAR_MAP_:
-            # shard_blocks: every rank packs its own blocks, then the quantized shards are
-            # gathered (a quarter of the float bytes at int4), never the float weights
-            rank, _ = P.dist_world()
-            self._prequant_fp8_blocks(only={i for i, o in pending.items() if o == rank})
-            params = self.get_replacement_params(quant_format, self.w_only)
-            for i, block in enumerate(self.blocks):
-                if pending[i] == rank:
-                    self.model.replace_module_block(mapping[quant_format], block, i, params)
-            for i, block in enumerate(self.blocks):
-                self._publish_deployed(block, pending[i])
-            self._pending_owner = None
-            return
-        self.materialize_blocks()
-        if quant_format in _REALQUANT_LINEAR_MAP_:
-            self._prequant_fp8_blocks()
-        self.model.replace_module_all(mapping[quant_format],
-                                      self.get_replacement_params(quant_format, self.w_only))
+        sharded = world > 1 and (self.parallel_mode() == 'shard_units' or own is not None
+                                 or (pending and real))
+        if not sharded:
+            self.materialize_blocks()   # shard_blocks + a float format: publish first
+        for i, block in enumerate(self.blocks):
+            def one(i=i, block=block):
+                self.block_idx = i
+                lins = self.model.get_block_linears(block)
+                if not sharded:
+                    if real:
+                        self._prequant_fp8_block(block, lins)
+                    self.model.replace_module_block(module, block, i, params)
+                    return
+                assign = {n: self.unit_owner(i, n) for n in lins}
+                mine = {n: m for n, m in lins.items() if assign[n] == rank}
+                if real:
+                    self._prequant_fp8_block(block, mine)
+                self.model.replace_module_subset(module, block, {'layers': mine}, i, params)
+                if own is None:
+                    P.publish(block, assign, rest_owner=pending[i] if pending else None)
+                self._clear_block_cache(block)
+            self.visit_block(i, one, next_i=i + 1)
+        self._drain_blocks()
+        self._pending_owner = None
 
     @torch.no_grad()
-    def _prequant_fp8_blocks(self, only=None):
+    def _prequant_fp8_block(self, block, mods: dict):
         """Block-fp8 checkpoint linears (DeepSeek-V3 experts) headed for a per-tensor FP8
-        real-quant format: requantize every such linear of a block in ONE batched launch
+        real-quant format: requantize every such linear of the block in ONE batched launch
         (lcq_fp8_block_to_tensor_many) instead of one dequant + quant chain per linear;
         quant_pack picks the results up (bit-identical to the per-linear chain)."""
         wq = self.wquantizer
@@ -793,26 +841,29 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
             return
         if self.quant_config['weight'].get('need_pack', False):
             return
-        from . import ops
-        for bi, block in enumerate(self.blocks):
-            if only is not None and bi not in only:
-                continue
-            mods = [m for m in self.model.get_block_linears(block).values()
-                    if getattr(m, 'weight', None) is not None
-                    and m.weight.dtype == torch.float8_e4m3fn and hasattr(m, 'weight_scale_inv')]
-            if not mods:
-                continue
-            bs = getattr(mods[0], 'block_size', getattr(self, 'fp8_block_size', 128))
-            codes, scales = ops.fp8_block_to_tensor_many(
-                [m.weight.data for m in mods], [m.weight_scale_inv.data for m in mods], bs,
-                wq.fp8_dtype, qmax=wq._qmax_f())
-            for i, m in enumerate(mods):
-                m._lcq_prequant = (codes[i], scales[i:i + 1].view(1))
+        mods = [m for m in mods.values()
+                if getattr(m, 'weight', None) is not None and not getattr(m, 'no_quant', False)
+                and m.weight.dtype == torch.float8_e4m3fn and hasattr(m, 'weight_scale_inv')]
+        if not mods:
+            return
+        bs = getattr(mods[0], 'block_size', getattr(self, 'fp8_block_size', 128))
+        codes, scales = ops.fp8_block_to_tensor_many(
+            [m.weight.data for m in mods], [m.weight_scale_inv.data for m in mods], bs,
+            wq.fp8_dtype, qmax=wq._qmax_f())
+        for i, m in enumerate(mods):
+            m._lcq_prequant = (codes[i], scales[i:i + 1].view(1))
 
     @torch.no_grad()
     def save_model(self, path):
+        rank, world = P.dist_world()
+        if getattr(self.model, 'ownership', None) is not None and world > 1:
+            # every rank holds only its own blocks / units: per-rank safetensors shards and
+            # one index, loadable as a whole HF checkpoint
+            self._drain_blocks()
+            self.model.save_sharded(path, self.unit_owner)
+            return
         self.materialize_blocks()
-        rank, _, _ = world()
+        self._drain_blocks()
         if rank != 0:
             return
         self.model.save_pretrained(path)

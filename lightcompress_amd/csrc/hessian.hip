@@ -51,10 +51,23 @@ struct Args {
   int64_t ld, ic, icp;
   int64_t nk_main, nk;   // whole K-tiles read from x; all K-tiles (nk_main + tail)
   float* H;
-  float* part;           // split-K partials [ns][icp][icp] or null
+  float* part;           // split partials, upper tiles packed: [ns][ntiles][256 * 256], or null
   float alpha, beta;
   int nt, ns, ntiles;
   int64_t ktps;          // K-tiles per split
+};
+
+// Token groups of one launch (the grouped GPTQ Hessian, gptq_core.HessianAccumulator): group g
+// holds tokens [row0[g], row0[g] + 64 nk_main[g]) of x plus an optional zero-padded tail
+// K-tile, split into splits split0[g] .. split0[g + 1] - 1 of ktps[g] K-tiles each. Every
+// split writes its own partial; k_syrk_reduce folds each group's splits in order, then sums
+// the groups in the fixed pairwise tree. ng = 1 describes a plain (ungrouped) launch.
+constexpr int GMAX = 8;
+struct GArgs {
+  int64_t row0[GMAX], nk_main[GMAX], nk[GMAX], ktps[GMAX];
+  const uint16_t* tail[GMAX];
+  int split0[GMAX + 1];
+  int ng;
 };
 
 // upper-triangle tile index -> (ti, tj), row-major over ti
@@ -284,7 +297,7 @@ __device__ __forceinline__ void ktile(v4f (&acc)[8][8], v8s (&bf)[2][8][2], v8s 
 }
 
 template <bool FP16>
-__global__ void __launch_bounds__(256, 1) k_syrk_x(Args a) {
+__global__ void __launch_bounds__(256, 1) k_syrk_x(Args a, GArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -295,7 +308,15 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a) {
   const int split = wgid / a.ntiles;
   int ti, tj;
   valid_tile(wgid - split * a.ntiles, a.nt, ti, tj);
-  const int64_t kt0 = (int64_t)split * a.ktps;
+  // this split's token group: its rows of x, tail and K-tile range
+  int g = 0;
+  while (g + 1 < ga.ng && split >= ga.split0[g + 1]) ++g;
+  a.x += ga.row0[g] * a.ld;
+  a.tail = ga.tail[g];
+  a.nk_main = ga.nk_main[g];
+  a.nk = ga.nk[g];
+  a.ktps = ga.ktps[g];
+  const int64_t kt0 = (int64_t)(split - ga.split0[g]) * a.ktps;
   int64_t nk = a.nk - kt0;
   if (nk > a.ktps) nk = a.ktps;
   Stage st;
@@ -361,13 +382,15 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a) {
   const int i0 = ti * ST + wr * 128 + fr;
   const int j0 = tj * ST + wc * 128 + fq * 4;
   const int ic = (int)a.ic, icp = (int)a.icp;
-  if (a.ns > 1) {
-    float* Pp = a.part + (int64_t)split * a.icp * a.icp;
+  if (a.part != nullptr) {  // the split's partial tile, packed (tile-contiguous 256 KB)
+    const int tri = ti * a.nt - ti * (ti - 1) / 2 + (tj - ti);
+    float* Pp = a.part + ((int64_t)split * a.ntiles + tri) * (ST * ST);
+    const int li = wr * 128 + fr, lj = wc * 128 + fq * 4;
 #pragma unroll
     for (int m = 0; m < 8; ++m)
 #pragma unroll
       for (int n = 0; n < 8; ++n)
-        *reinterpret_cast<float4*>(Pp + (uint32_t)((i0 + m * 16) * icp + j0 + n * 16)) =
+        *reinterpret_cast<float4*>(Pp + (uint32_t)((li + m * 16) * ST + lj + n * 16)) =
             make_float4(acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]);
     return;
   }
@@ -432,10 +455,12 @@ __global__ void __launch_bounds__(256) k_tail_copy(const uint16_t* __restrict__ 
   }
 }
 
-// split-K combine: H = beta*H + alpha * sum_s P[s] (fixed order), upper tiles + mirror. A
-// workgroup = one 64 x 64 piece of an upper tile: the row-major store and the mirrored store
-// both go out coalesced (the mirror through an LDS transpose)
-__global__ void __launch_bounds__(256) k_syrk_reduce(Args a) {
+// split combine: per group the fold of its splits in order (the first partial, + the next,
+// ...), the groups in the fixed pairwise tree ((g0 + g1) + (g2 + g3)) + ((g4 + g5) + (g6 + g7))
+// (ng = 1, 2, 4, 8; a group without tokens counts 0), then H = beta*H + alpha * sum, upper tiles
+// + mirror. A workgroup = one 64 x 64 piece of an upper tile: the row-major store and the
+// mirrored store both go out coalesced (the mirror through an LDS transpose)
+__global__ void __launch_bounds__(256) k_syrk_reduce(Args a, GArgs ga) {
   __shared__ float tp[64][65];
   int ti, tj;
   tri_tile(blockIdx.x, a.nt, ti, tj);
@@ -443,14 +468,32 @@ __global__ void __launch_bounds__(256) k_syrk_reduce(Args a) {
   const int pr = blockIdx.y >> 2, pc = blockIdx.y & 3;  // 4 x 4 pieces of the 256^2 tile
   const int64_t r0 = (int64_t)ti * ST + pr * 64, c0 = (int64_t)tj * ST + pc * 64;
   const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int64_t tstride = (int64_t)a.ntiles * (ST * ST);
+  const float* tbase = a.part + (int64_t)blockIdx.x * (ST * ST);
   for (int rr = ry; rr < 64; rr += 4) {
     const int64_t r = r0 + rr, c = c0 + cx;
     float v = 0.f;
     if (r < a.ic && c < a.ic) {
-      float s = 0.f;
-      for (int k = 0; k < a.ns; ++k)
-        s = __fadd_rn(s, a.part[(int64_t)k * a.icp * a.icp + r * a.icp + c]);
-      v = __fmul_rn(a.alpha, s);
+      const int64_t e = (int64_t)(pr * 64 + rr) * ST + pc * 64 + cx;
+      float gs[GMAX];
+#pragma unroll
+      for (int g = 0; g < GMAX; ++g) {
+        gs[g] = 0.f;
+        if (g < ga.ng) {
+          const int s0 = ga.split0[g], s1 = ga.split0[g + 1];
+          if (s1 > s0) {
+            float s = tbase[s0 * tstride + e];
+            for (int k = s0 + 1; k < s1; ++k) s = __fadd_rn(s, tbase[k * tstride + e]);
+            gs[g] = s;
+          }
+        }
+      }
+#pragma unroll
+      for (int wdt = 1; wdt < GMAX; wdt *= 2)
+#pragma unroll
+        for (int g = 0; g < GMAX; g += 2 * wdt)
+          if (g + wdt < ga.ng) gs[g] = __fadd_rn(gs[g], gs[g + wdt]);
+      v = a.alpha != 1.0f ? __fmul_rn(a.alpha, gs[0]) : gs[0];
       if (a.beta != 0.f) v = __fadd_rn(__fmul_rn(a.beta, a.H[r * a.ic + c]), v);
       a.H[r * a.ic + c] = v;
     }
@@ -515,6 +558,59 @@ static void plan(int64_t n, int64_t ic, int& nt, int& ntiles, int& ns, int64_t& 
 using namespace lcq;
 using namespace lcq::hx;
 
+// Per-group split count of the grouped launch: the same cost model with the grid taken as
+// GMAX groups launched together. It depends only on (group tokens, ic) -- never on how many
+// groups this process launches -- so a token-sharded rank splits its groups exactly as one GPU
+// does (the fp32 fold order per group is world-independent).
+static void plan_group(int64_t n, int64_t ic, int64_t& ns, int64_t& ktps, int64_t& nkt) {
+  const int64_t icp = ceil_to(ic, ST);
+  const int64_t nt = icp / ST, ntiles = nt * (nt + 1) / 2;
+  nkt = ceil_to(n, SKT) / SKT;
+  int64_t best_ns = 1;
+  double best = 1e300;
+  for (int64_t c = 1; c <= 64; ++c) {
+    if (c > 1 && nkt / c < 8) break;
+    const int64_t per = (nkt + c - 1) / c, cc = (nkt + per - 1) / per;
+    const int64_t per_xcd = (ntiles * cc * GMAX + 7) / 8, rounds = (per_xcd + 31) / 32;
+    const double cost = (double)rounds * (double)(per + 6) + 0.034 * (double)(cc * ntiles * GMAX);
+    if (cost < best * 0.995) {
+      best = cost;
+      best_ns = cc;
+    }
+  }
+  ktps = (nkt + best_ns - 1) / best_ns;
+  ns = nkt ? (nkt + ktps - 1) / ktps : 0;
+}
+
+struct GroupedPlan {
+  GArgs ga;
+  int64_t splits, tail_bytes, part_bytes;
+};
+
+static int grouped_plan(const int64_t* bounds, int ng, int64_t ic, GroupedPlan& p) {
+  p = GroupedPlan{};
+  const int64_t icp = ceil_to(ic, ST), nt = icp / ST, ntiles = nt * (nt + 1) / 2;
+  p.ga.ng = ng;
+  int64_t sp = 0;
+  for (int g = 0; g < ng; ++g) {
+    const int64_t n = bounds[g + 1] - bounds[g];
+    if (n < 0) return -1;
+    int64_t ns = 0, ktps = 1, nkt = 0;
+    if (n > 0) plan_group(n, ic, ns, ktps, nkt);
+    p.ga.row0[g] = bounds[g];
+    p.ga.nk_main[g] = n / SKT;
+    p.ga.nk[g] = nkt;
+    p.ga.ktps[g] = ktps;
+    p.ga.split0[g] = (int)sp;
+    if (n % SKT) p.tail_bytes += ceil_to(SKT * ic * 2, 256);
+    sp += ns;
+  }
+  p.ga.split0[ng] = (int)sp;
+  p.splits = sp;
+  p.part_bytes = sp * ntiles * ST * ST * 4;
+  return 0;
+}
+
 extern "C" int64_t lcq_hessian_workspace_bytes(int64_t n, int64_t ic) {
   if (n <= 0 || ic <= 0) return 0;
   int nt, ntiles, ns;
@@ -522,7 +618,7 @@ extern "C" int64_t lcq_hessian_workspace_bytes(int64_t n, int64_t ic) {
   plan(n, ic, nt, ntiles, ns, ktps, nkt, icp);
   int64_t b = (n % SKT) ? SKT * ceil_to(ic, 8) * 2 : 0;  // tail copy
   b = ceil_to(b, 256);
-  if (ns > 1) b += (int64_t)ns * icp * icp * 4;
+  if (ns > 1) b += (int64_t)ns * ntiles * ST * ST * 4;
   return b;
 }
 
@@ -562,15 +658,87 @@ extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t 
   a.part = a.ns > 1 ? reinterpret_cast<float*>(ws + off) : nullptr;
   a.alpha = alpha;
   a.beta = beta;
+  GArgs ga{};
+  ga.ng = 1;
+  ga.row0[0] = 0;
+  ga.nk_main[0] = a.nk_main;
+  ga.nk[0] = a.nk;
+  ga.ktps[0] = a.ktps;
+  ga.tail[0] = a.tail;
+  ga.split0[0] = 0;
+  ga.split0[1] = a.ns;
   auto k = x_dtype == LCQ_F16 ? k_syrk_x<true> : k_syrk_x<false>;
   // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
-  hipLaunchKernelGGL(k, dim3((unsigned)(a.ntiles * a.ns)), 256, 2 * BUF, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)(a.ntiles * a.ns)), 256, 2 * BUF, st, a, ga);
   int rc = check_launch("lcq_hessian_accum: syrk");
   if (rc) return rc;
   if (a.ns > 1) {
-    hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)a.ntiles, 16), 256, 0, st, a);
+    hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)a.ntiles, 16), 256, 0, st, a, ga);
     rc = check_launch("lcq_hessian_accum: reduce");
   }
   return rc;
+}
+
+extern "C" int64_t lcq_hessian_grouped_workspace_bytes(const int64_t* bounds, int ng,
+                                                       int64_t ic) {
+  if (bounds == nullptr || ng < 1 || ng > GMAX || ic <= 0) return 0;
+  GroupedPlan p;
+  if (grouped_plan(bounds, ng, ic, p)) return 0;
+  return p.tail_bytes + p.part_bytes;
+}
+
+extern "C" int lcq_hessian_grouped(const void* x, int x_dtype, int64_t ic,
+                                   const int64_t* bounds, int ng, void* H, float alpha,
+                                   void* workspace, int64_t ws_bytes, void* stream) {
+  LCQ_REQUIRE(x_dtype == LCQ_BF16 || x_dtype == LCQ_F16, "x must be bf16 or fp16");
+  LCQ_REQUIRE(ng == 1 || ng == 2 || ng == 4 || ng == 8, "ng must be 1, 2, 4 or 8");
+  LCQ_REQUIRE(bounds != nullptr && bounds[0] == 0, "bounds: host token offsets from 0");
+  LCQ_REQUIRE(ic > 0 && ic % 8 == 0, "ic must be a positive multiple of 8");
+  LCQ_REQUIRE(ic <= 46336, "ic must be <= 46336 (32-bit H offsets)");
+  LCQ_REQUIRE(x != nullptr && (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+              "x must be 16-byte aligned");
+  GroupedPlan p;
+  LCQ_REQUIRE(grouped_plan(bounds, ng, ic, p) == 0, "bounds must not decrease");
+  const int64_t need = p.tail_bytes + p.part_bytes;
+  LCQ_REQUIRE(workspace != nullptr && ws_bytes >= need,
+              "workspace smaller than lcq_hessian_grouped_workspace_bytes");
+  hipStream_t st = as_stream(stream);
+  Args a{};
+  a.x = reinterpret_cast<const uint16_t*>(x);
+  a.ld = ic;
+  a.ic = ic;
+  a.icp = ceil_to(ic, ST);
+  a.nt = (int)(a.icp / ST);
+  a.ntiles = a.nt * (a.nt + 1) / 2;
+  a.ns = (int)p.splits;
+  a.H = reinterpret_cast<float*>(H);
+  a.alpha = alpha;
+  a.beta = 0.f;
+  char* ws = reinterpret_cast<char*>(workspace);
+  int64_t off = 0;
+  for (int g = 0; g < ng; ++g) {
+    const int64_t n = bounds[g + 1] - bounds[g];
+    p.ga.tail[g] = nullptr;
+    if (n % SKT) {  // this group's last partial K-tile, zero padded
+      uint16_t* tail = reinterpret_cast<uint16_t*>(ws + off);
+      hipLaunchKernelGGL(k_tail_copy, dim3((unsigned)((SKT * ic / 8 + 255) / 256)), 256, 0, st,
+                         a.x + bounds[g] * ic, p.ga.nk_main[g] * SKT, n, ic, tail);
+      int rc = check_launch("lcq_hessian_grouped: tail");
+      if (rc) return rc;
+      p.ga.tail[g] = tail;
+      off += ceil_to(SKT * ic * 2, 256);
+    }
+  }
+  a.part = reinterpret_cast<float*>(ws + off);
+  if (p.splits > 0) {
+    auto k = x_dtype == LCQ_F16 ? k_syrk_x<true> : k_syrk_x<false>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * BUF);
+    hipLaunchKernelGGL(k, dim3((unsigned)(a.ntiles * p.splits)), 256, 2 * BUF, st, a, p.ga);
+    int rc = check_launch("lcq_hessian_grouped: syrk");
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)a.ntiles, 16), 256, 0, st, a, p.ga);
+  return check_launch("lcq_hessian_grouped: reduce");
 }

@@ -12,9 +12,6 @@ and deploy. Block-fp8 checkpoints (``torch_dtype: torch.float8_e4m3fn``,
 """
 from __future__ import annotations
 
-import json
-import os
-
 import torch
 import torch.nn as nn
 
@@ -61,12 +58,15 @@ def unfuse_experts(model: nn.Module) -> nn.Module:
         fused, cfg = mod.experts, mod.config
         inter = fused.intermediate_dim
         experts = ExpertList()
+        dev = fused.gate_up_proj.device
         for e in range(fused.num_experts):
-            mlp = md.DeepseekV3MLP(cfg, intermediate_size=inter).to(
-                device=fused.gate_up_proj.device, dtype=fused.gate_up_proj.dtype)
-            mlp.gate_proj.weight.copy_(fused.gate_up_proj[e, :inter])
-            mlp.up_proj.weight.copy_(fused.gate_up_proj[e, inter:])
-            mlp.down_proj.weight.copy_(fused.down_proj[e])
+            with torch.device(dev):   # meta stays meta (BaseModel.load_checkpoint)
+                mlp = md.DeepseekV3MLP(cfg, intermediate_size=inter).to(
+                    dtype=fused.gate_up_proj.dtype)
+            if dev.type != 'meta':
+                mlp.gate_proj.weight.copy_(fused.gate_up_proj[e, :inter])
+                mlp.up_proj.weight.copy_(fused.gate_up_proj[e, inter:])
+                mlp.down_proj.weight.copy_(fused.down_proj[e])
             experts.append(mlp)
         mod.experts = experts
     return model
@@ -76,14 +76,14 @@ def unfuse_experts(model: nn.Module) -> nn.Module:
 class DeepseekV3(BaseModel):
     block_name_prefix = 'model.layers'
 
-    def __init__(self, config=None, hf_model=None, device='cuda', dtype=None):
+    def __init__(self, config=None, hf_model=None, device='cuda', dtype=None, **kw):
         mcfg = (config or {}).get('model', {}) if config is not None else {}
         td = mcfg.get('torch_dtype', 'auto')
-        if hf_model is None and (td in ('torch.float8_e4m3fn', 'float8_e4m3fn')
-                                 or dtype == torch.float8_e4m3fn):
-            assert mcfg.get('block_wise_quant', False), 'fp8 checkpoints need block_wise_quant'
-            hf_model = load_block_fp8(mcfg['path'], device)
-        super().__init__(config, hf_model=hf_model, device=device, dtype=dtype)
+        # block-fp8 checkpoints (torch_dtype float8_e4m3fn + block_wise_quant) load into
+        # LlmcFp8Linear modules (BaseModel.load_checkpoint)
+        self.block_fp8 = td in ('torch.float8_e4m3fn', 'float8_e4m3fn') or \
+            dtype == torch.float8_e4m3fn
+        super().__init__(config, hf_model=hf_model, device=device, dtype=dtype, **kw)
 
     def prepare_model(self, hf_model):
         return unfuse_experts(hf_model)
@@ -175,62 +175,3 @@ class DeepseekV3(BaseModel):
                          'prev_op': [mlp.up_proj], 'input': ['mlp.down_proj'],
                          'inspect': mlp.down_proj, 'has_kwargs': False})
         return subs
-
-
-def _safetensor_files(path):
-    idx = os.path.join(path, 'model.safetensors.index.json')
-    if os.path.exists(idx):
-        with open(idx) as f:
-            return sorted({os.path.join(path, v) for v in json.load(f)['weight_map'].values()})
-    return [os.path.join(path, 'model.safetensors')]
-
-
-@torch.no_grad()
-def load_block_fp8(path, device='cuda'):
-    """base_model.py:205-264: a block-fp8 checkpoint (e4m3 weights + per-128x128-block
-    ``weight_scale_inv``) as a model whose block linears are LlmcFp8Linear, loaded straight
-    from the safetensors shards (no bf16 copy of the weights is made)."""
-    from safetensors import safe_open
-    from transformers import AutoConfig, AutoModelForCausalLM
-
-    from .module_utils import LlmcFp8Linear
-    cfg = AutoConfig.from_pretrained(path, local_files_only=True)
-    qc = getattr(cfg, 'quantization_config', None) or {}
-    qc = qc if isinstance(qc, dict) else qc.to_dict()
-    bs = int(qc.get('weight_block_size', [128, 128])[0])
-    if hasattr(cfg, 'quantization_config'):
-        del cfg.quantization_config  # plain linears; the fp8 ones are built below
-    with torch.device(device):
-        model = AutoModelForCausalLM.from_config(cfg, torch_dtype=torch.bfloat16)
-    unfuse_experts(model)
-    inner = model.model
-    with torch.device(device):
-        for block in inner.layers:
-            for name, m in list(block.named_modules()):
-                if type(m) is not nn.Linear:
-                    continue
-                parent_name, _, child = name.rpartition('.')
-                parent = block.get_submodule(parent_name) if parent_name else block
-                new = LlmcFp8Linear.new(m, bs)
-                if new.bias is not None:
-                    new.bias.data = new.bias.data.to(torch.bfloat16)
-                setattr(parent, child, new)
-    params = dict(model.named_parameters())
-    params.update(dict(model.named_buffers()))
-    seen = set()
-    for f in _safetensor_files(path):
-        with safe_open(f, framework='pt', device='cpu') as st:
-            for k in st.keys():
-                if k in params:
-                    t = st.get_tensor(k)
-                    p = params[k]
-                    if p.shape != t.shape:
-                        raise ValueError(f'{k}: checkpoint {tuple(t.shape)} vs model '
-                                         f'{tuple(p.shape)}')
-                    p.data.copy_(t)
-                    seen.add(k)
-    missing = [k for k, p in model.named_parameters() if k not in seen]
-    if missing:
-        raise ValueError(f'block-fp8 checkpoint lacks {len(missing)} tensors, e.g. {missing[:3]}')
-    model.config = cfg
-    return model

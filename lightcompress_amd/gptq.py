@@ -8,7 +8,6 @@ input (q/k/v, gate/up) share one Hessian accumulator instead of accumulating ide
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.distributed as dist
@@ -33,7 +32,10 @@ class GPTQ(BaseBlockwiseQuantization):
         self.model_dtype = next(self.model.model.parameters()).dtype
         self.add_quant_config()
         self.layers_cache = {}
-        self.collect_model_qparams()
+        # the original weights' qparams (buf_scales / zeros / qmax / qmin, gptq.py:27-33 via
+        # collect_model_qparams) are taken per block when the block is reached, before any
+        # of its weights change: the same values, without a pass over the whole model here
+        # (a streamed model's blocks are on the host until visited)
 
     def add_quant_config(self):
         sp = self.quant_config['special']
@@ -52,6 +54,12 @@ class GPTQ(BaseBlockwiseQuantization):
             raise NotImplementedError('device GPTQ uses blocksize 128')
         self.need_perm = (self.wquantizer.granularity == 'per_group' and not self.static_groups
                           and self.actorder) or self.owq
+
+    def run_block_loop(self):
+        try:
+            super().run_block_loop()
+        finally:
+            gptq_core.clear_chain_graphs()  # the chain graphs' pools end with the run
 
     @torch.no_grad()
     def collect_model_qparams(self):
@@ -107,6 +115,8 @@ class GPTQ(BaseBlockwiseQuantization):
     @torch.no_grad()
     def block_init(self, block):
         self.named_layers = self.model.get_block_linears(block)
+        if any(not hasattr(m, 'buf_scales') for m in self.named_layers.values()):
+            self.collect_block_qparams(block)
         subsets = self.model.get_subsets_in_block(block)
         # with true_sequential the reference re-initialises every later subset's Hessian in
         # rehook_next_subset, so only the first subset's first-pass Hessian is ever used
@@ -143,8 +153,8 @@ class GPTQ(BaseBlockwiseQuantization):
     # rows are independent given U, so their column loops run as ONE loop over
     # the concatenated rows: the same per-row arithmetic (each element's update order is fixed
     # by its column, not by the row count), one latency-bound chain of block / trailing kernels
-    # instead of one per linear. LCQ_GPTQ_CONCAT=0 quantizes them one by one.
-    concat_rows = os.environ.get('LCQ_GPTQ_CONCAT', '1') != '0'
+    # instead of one per linear. (Tests set concat_rows False to quantize them one by one.)
+    concat_rows = True
 
     @torch.no_grad()
     def block_transform(self, block, input_feat=None, block_kwargs=None):

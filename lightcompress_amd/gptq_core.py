@@ -6,13 +6,13 @@ Kept separate from the plugin class (``gptq.py``) so the algorithm can be driven
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
 from . import ops
 
 BLOCK = 128
+SUPERBLOCK = 1024  # column_loop's two-level trailing update (see there)
 
 
 HESSIAN_GROUPS = 8  # fixed calibration-sample groups of the grouped Hessian (see below)
@@ -100,22 +100,16 @@ class HessianAccumulator:
         ops.hessian_accum(x, self.H, _alpha(self.nsamples), beta)
 
     def _add_grouped(self, x: torch.Tensor, tpe: int):
-        parts = []
-        for _, s0, s1 in self.plan.local:
-            if s1 > s0:  # beta 0: the kernel never reads P
-                P = torch.empty((self.ic, self.ic), dtype=torch.float32, device=x.device)
-                ops.hessian_accum(x[s0 * tpe:s1 * tpe], P, 1.0, 0.0)
-            else:
-                P = torch.zeros((self.ic, self.ic), dtype=torch.float32, device=x.device)
-            parts.append(P)
-        if self.plan.world == 1:  # the whole tree here: H = alpha * tree
-            ops.tree_sum(parts, _alpha(self.plan.n_global), out=self.H)
+        """Every local group's x^T x and their fixed tree in ONE launch (lcq_hessian_grouped):
+        the whole H at world 1 (alpha(n)), else this rank's unscaled subtree."""
+        bounds = [0] + [s1 * tpe for _, _, s1 in self.plan.local]
+        if self.plan.world == 1:
+            ops.hessian_grouped(x, bounds, self.H, _alpha(self.plan.n_global))
             self.subtree = self.H
             self.finalized = True
         else:
-            self.subtree = ops.tree_sum(parts, 1.0)
+            self.subtree = ops.hessian_grouped(x, bounds, torch.empty_like(self.H), 1.0)
             self.finalized = False
-        del parts
 
     def ready_grouped(self) -> bool:
         """Grouped and waiting for (or done with) the cross-rank tree. A rank whose share of
@@ -192,48 +186,20 @@ def prepare_hessian(H: torch.Tensor, actorder: bool, percdamp: float, owq_nout: 
         keep = torch.ones(H.shape[0], dtype=torch.bool, device=H.device)
         keep[desc[:owq_nout]] = False
         perm = torch.cat([torch.arange(H.shape[0], device=H.device)[keep], desc[:owq_nout]])
-    dead = torch.diag(H) == 0
-    if bool(dead.any()):
-        idx = torch.nonzero(dead).flatten()
-        H[idx, idx] = 1
-    if perm is not None:
-        H = H[perm][:, perm]
-    cols = H.shape[0]
-    damp = percdamp * torch.mean(torch.diag(H))
-    d = torch.arange(cols, device=H.device)
-    H[d, d] += damp
-    backend = os.environ.get('LCQ_CHOL', 'lcq')
-    if backend == 'lcq':
-        U = inverse_cholesky_upper(H)
-    else:
-        with _linalg_backend():
-            C = torch.linalg.cholesky(H.flip(0, 1))
-            del H
-            eye = torch.eye(cols, dtype=C.dtype, device=C.device)
-            U = torch.linalg.solve_triangular(C, eye, upper=False).flip(0, 1).contiguous()
+    # gptq.py:58-64, 128-176 in one gather pass (lcq_gather_rc): dead diagonal -> 1, the
+    # act-order permutation, damp = percdamp * mean(diag) on the diagonal, written reversed
+    # (J H J) straight into the chain's input -- the torch form (two index gathers, a flip copy,
+    # a diagonal add) reads and writes the n^2 fp32 matrix four times
+    d = torch.diag(H)
+    dead = d == 0
+    dfix = torch.where(dead, torch.ones_like(d), d)
+    damp = percdamp * torch.mean(dfix if perm is None else dfix[perm])
+    n = H.shape[0]
+    rev = (perm if perm is not None else torch.arange(n, device=H.device)).flip(0)
+    U = _inverse_cholesky_upper_filled(
+        lambda buf: ops.gather_rc(H, rsrc=rev, csrc=rev, dead_diag=dead, damp=damp, out=buf),
+        n, H.device)
     return U, perm, dead
-
-
-class _linalg_backend:
-    """Scoped torch linalg backend for the factorisation (env LCQ_LINALG = magma (default:
-    41 ms/block faster than rocSOLVER on the Llama-3-8B GPTQ step) | default | cusolver);
-    restores the caller's choice on exit."""
-
-    def __enter__(self):
-        import os
-        self.want = os.environ.get('LCQ_LINALG', 'magma')
-        if self.want != 'default' and torch.cuda.is_available():
-            self.prev = torch.backends.cuda.preferred_linalg_library()
-            try:
-                torch.backends.cuda.preferred_linalg_library(self.want)
-            except RuntimeError:
-                self.want = 'default'
-        else:
-            self.want = 'default'
-
-    def __exit__(self, *exc):
-        if self.want != 'default':
-            torch.backends.cuda.preferred_linalg_library(self.prev)
 
 
 def _gemm(A, B, out, alpha, beta, b_trans=False):
@@ -356,69 +322,90 @@ def _chol_inv_rec(A: torch.Tensor, X: torch.Tensor, info: torch.Tensor, row0: in
     _mm_low_left(X22, T, X[n1:, :n1], -1.0, 0.0)
 
 
-def _chain(Hs: torch.Tensor):
-    """J chol(J H J)^-1 J on H (not modified): (U, info)."""
-    Hr = Hs.flip(0, 1).contiguous()
+def _chol_core(Hr: torch.Tensor):
+    """(X, info): X = chol(Hr)^-1 (lower), Hr consumed as workspace."""
     info = torch.zeros(1, dtype=torch.int32, device=Hr.device)
     X = torch.zeros_like(Hr)
     _chol_inv_rec(Hr, X, info)
-    del Hr
-    return X.flip(0, 1).contiguous(), info
+    return X, info
 
 
 # One captured HIP graph per (device, Hessian size): the recursion issues ~600 launches per
 # chain at n = 14336 (the Llama-3-8B down_proj Hessian), many shorter than the host time to
 # issue them from Python; a replay issues them back to back. Every size's first chain runs
 # eagerly (it also loads every kernel), the graph is captured right after and replayed for the
-# following blocks. Same kernels, same operands: identical results.
+# following blocks. Same kernels, same operands: identical results. The graph's input buffer
+# is filled in place by the caller's preparation kernel, and its output flipped into a fresh
+# tensor (no staging copies around the replay).
 _GRAPH_MIN = 1024
+CHAIN_GRAPHS = True   # tests switch this off to compare the eager chain with the replay
 _chain_graphs: dict = {}
 
 
-def _chain_graphed(H: torch.Tensor):
-    key = (H.device.index, H.shape[0])
-    ent = _chain_graphs.get(key)
+def clear_chain_graphs():
+    """Drop every captured chain graph with its private memory pool (static input, output and
+    recursion temporaries: ~4-5 n^2 fp32 per Hessian size, ~4 GB at n 14336). GPTQ calls this
+    when its block loop ends, so the pools do not outlive the run."""
+    _chain_graphs.clear()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+def _inverse_cholesky_upper_filled(fill, n: int, device) -> torch.Tensor:
+    """U = J chol(Hr)^-1 J where fill(buf) writes Hr = J H J (n x n fp32) into buf."""
+    graphed = torch.device(device).type == 'cuda' and n >= _GRAPH_MIN and CHAIN_GRAPHS
+    key = (torch.device(device).index, n)
+    ent = _chain_graphs.get(key) if graphed else None
     if ent is None:
-        U, info = _chain(H)
-        static_in = H.clone()
-        g = torch.cuda.CUDAGraph()
-        torch.cuda.synchronize(H.device)
-        with torch.cuda.graph(g):
-            out, g_info = _chain(static_in)
-        _chain_graphs[key] = (g, static_in, out, g_info)
-        return U, info
-    g, static_in, out, g_info = ent
-    static_in.copy_(H)
-    timer = ops.N._timer
-    if timer is not None:  # bench's per-kernel table: the replay as one entry
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        g.replay()
-        e1.record()
-        timer.events.setdefault('lcq_chol_chain_graph', []).append((e0, e1))
+        Hr = torch.empty((n, n), dtype=torch.float32, device=device)
+        fill(Hr)
+        X, info = _chol_core(Hr)
+        del Hr
+        if graphed:
+            static_in = torch.empty((n, n), dtype=torch.float32, device=device)
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(device)
+            timer, ops.N._timer = ops.N._timer, None  # captured launches do not run: no events
+            try:
+                with torch.cuda.graph(g):
+                    Xs, infos = _chol_core(static_in)
+            finally:
+                ops.N._timer = timer
+            _chain_graphs[key] = (g, static_in, Xs, infos)
     else:
-        g.replay()
-    # the static output is overwritten by the next replay of this size
-    return out.clone(), g_info
-
-
-def inverse_cholesky_upper(H: torch.Tensor) -> torch.Tensor:
-    """U = chol(H^-1, upper) = J chol(J H J)^-1 J for SPD fp32 H (H is consumed)."""
-    graphed = (H.is_cuda and H.shape[0] >= _GRAPH_MIN
-               and os.environ.get('LCQ_CHOL_GRAPH', '1') != '0')
-    U, info = _chain_graphed(H) if graphed else _chain(H)
-    del H
-    bad = int(info.item())
+        g, static_in, X, info = ent
+        fill(static_in)
+        timer = ops.N._timer
+        if timer is not None:  # bench's per-kernel table: the replay as one entry
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            timer.events.setdefault('lcq_chol_chain_graph', []).append((e0, e1))
+        else:
+            g.replay()
+    bad = int(info.item())   # (a static info is read before the next replay)
     if bad:
         raise torch.linalg.LinAlgError(
             f'linalg.cholesky: The factorization could not be completed because the input '
             f'is not positive-definite (the leading minor of order {bad} is not '
             f'positive-definite).')
-    return U
+    return X.flip(0, 1).contiguous()
+
+
+def inverse_cholesky_upper(H: torch.Tensor) -> torch.Tensor:
+    """U = chol(H^-1, upper) = J chol(J H J)^-1 J for SPD fp32 H."""
+    return _inverse_cholesky_upper_filled(lambda buf: buf.copy_(H.flip(0, 1)), H.shape[0],
+                                          H.device)
 
 
 def prepare_weight(W: torch.Tensor, perm, dead):
-    """Weight side of gptq.py:128-176: fp32 copy, dead columns zeroed, act-order permuted."""
+    """Weight side of gptq.py:128-176: fp32 copy, dead columns zeroed, act-order permuted --
+    one lcq_gather_rc pass from the (bf16) weight."""
+    if W.is_cuda and W.dim() == 2 and W.dtype in (torch.bfloat16, torch.float32) \
+            and W.stride(1) == 1:
+        return ops.gather_rc(W, csrc=perm, dead_col=dead if bool(dead.any()) else None)
     W = W.float().clone()
     if bool(dead.any()):
         W[:, dead] = 0
@@ -478,7 +465,7 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     s_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng else None
     z_out = torch.empty((rows, ng), dtype=torch.float32, device=dev) if ng and not sym else None
     if superblock is None:
-        superblock = int(os.environ.get('LCQ_GPTQ_SUPERBLOCK', '1024'))
+        superblock = SUPERBLOCK
     SB = max(BLOCK, superblock // BLOCK * BLOCK)
     errT = torch.empty((SB, rows), dtype=torch.float32, device=dev)  # k-major stacked Err1
     L = torch.zeros_like(W) if losses else None
@@ -614,7 +601,7 @@ def quantize_layer(W: torch.Tensor, H: torch.Tensor | None, wquantizer, actorder
                               col_group=col_group, ncols_q=ncq, col_qparams=col_qparams,
                               fp8=fp8)
     invperm = torch.argsort(perm) if perm is not None else None
-    weight = Wp[:, invperm] if invperm is not None else Wp
+    weight = ops.gather_rc(Wp, csrc=invperm) if invperm is not None else Wp
     if owq_fixed is not None:
         s, z = owq_fixed
     return dict(weight=weight, scales=None if s is None else s.reshape(-1, 1),

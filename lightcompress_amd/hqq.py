@@ -39,7 +39,8 @@ class HQQ(BaseBlockwiseQuantization):
 
     @torch.no_grad()
     def block_opt(self, block):
-        for name, layer in self.model.get_block_linears(block).items():
+        # shard_units (data-free, world > 1): only this rank's linears; deploy publishes
+        for name, layer in self.owned_linears(block).items():
             tensor = layer.weight.data.float()
             if self.axis == 0:
                 tensor = tensor.T

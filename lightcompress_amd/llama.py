@@ -4,7 +4,6 @@ replacement, first-block input capture. The model lives in HBM for the whole run
 """
 from __future__ import annotations
 
-import os
 import types
 
 import torch
@@ -34,8 +33,8 @@ def _fused_apply_rotary(q, k, cos, sin, unsqueeze_dim=1):
 _ORIG_SDPA = None
 # measured on MI355X (scripts/attn_rate.py, B 128, H 32, KV 8): the lcq flash kernel vs torch's
 # SDPA (aotriton) 0.87 vs 1.66 ms at S 512 (AWQ calibration), 9.26 vs 10.79 ms at S 2048 (GPTQ);
-# longer sequences (not measured) go to torch. Env override.
-_LCQ_ATTN_MAX_S = int(os.environ.get('LCQ_ATTN_MAX_S', '4096'))
+# longer sequences (not measured) go to torch.
+_LCQ_ATTN_MAX_S = 4096
 
 
 def _lcq_sdpa(module, query, key, value, attention_mask, dropout=0.0, scaling=None,
@@ -105,9 +104,8 @@ def _gate_up_silu(mlp, x):
     and the two [M, I] projections are never written); otherwise the projections run as
     modules (hooks fire in order) and lcq_silu_mul makes the product."""
     from . import ops
-    from .module_utils import _GEMM_ON
     gp, up = mlp.gate_proj, mlp.up_proj
-    if (_GEMM_ON and getattr(mlp.config, 'hidden_act', None) == 'silu'
+    if (getattr(mlp.config, 'hidden_act', None) == 'silu'
             and _input_only_hooked(gp, up)):
         (gw, gb), (uw, ub) = _linear_wb(gp), _linear_wb(up)
         if (gb is None and ub is None and ops.gemm_supported(x, gw, uw)
@@ -171,9 +169,6 @@ def _stage(cache, name, key, mods, fn):
         return hit[1]
     why = 'hooked' if hooked else ('miss' if hit is None else 'stale')
     STAGE_STATS[(name, why)] = STAGE_STATS.get((name, why), 0) + 1
-    if hit is not None and hit[0] != key and os.environ.get('LCQ_STAGE_DEBUG'):
-        diff = [i for i, (a, b) in enumerate(zip(hit[0], key)) if a != b]
-        print(f'[stage {name}] stale: key fields {diff[:6]}', flush=True)
     val = fn()
     cache[name] = (key, val)
     return val
@@ -185,7 +180,6 @@ def qkv_proj(attn, xn, weights=None):
     the three modules. `weights` overrides the three weights (the AWQ search's
     fake-quantized copies; their modules' hooks are not fired)."""
     from . import ops
-    from .module_utils import _GEMM_ON
     mods = (attn.q_proj, attn.k_proj, attn.v_proj)
     fused = weights is not None or _input_only_hooked(*mods)
     if weights is not None:
@@ -193,7 +187,7 @@ def qkv_proj(attn, xn, weights=None):
     elif fused:
         wb = [_linear_wb(m) for m in mods]
         ws, bs = [w for w, _ in wb], [b for _, b in wb]
-    if (_GEMM_ON and fused and ops.gemm_supported(xn, *ws)
+    if (fused and ops.gemm_supported(xn, *ws)
             and len({w.stride(0) for w in ws}) == 1
             and all(w.shape[0] % 256 == 0 for w in ws[:2])
             and all(b is None or b.dtype == xn.dtype for b in bs)):
@@ -275,24 +269,20 @@ def clear_stage_cache(block: nn.Module):
 
 
 def install_fused_forward(model: nn.Module):
-    """Route the Llama calibration forward's elementwise chains through the lcq fusions
-    (env LCQ_FUSED_FORWARD=0 disables)."""
+    """Route the Llama calibration forward's elementwise chains through the lcq fusions."""
     global _ORIG_ROTARY
-    if os.environ.get('LCQ_FUSED_FORWARD', '1') == '0':
-        return
     from transformers.models.llama import modeling_llama as ml
     if _ORIG_ROTARY is None:
         _ORIG_ROTARY = ml.apply_rotary_pos_emb
         ml.apply_rotary_pos_emb = _fused_apply_rotary
     global _ORIG_SDPA
-    if _ORIG_SDPA is None and os.environ.get('LCQ_FLASH_ATTN', '1') != '0':
+    if _ORIG_SDPA is None:
         from transformers.modeling_utils import AttentionInterface
         _ORIG_SDPA = AttentionInterface._global_mapping['sdpa']
         AttentionInterface.register('sdpa', _lcq_sdpa)
     global _STOCK_DECODER_FORWARD
     if _STOCK_DECODER_FORWARD is None:
         _STOCK_DECODER_FORWARD = ml.LlamaDecoderLayer.forward
-    staged = os.environ.get('LCQ_STAGED_FORWARD', '1') != '0'
     for m in model.modules():
         if type(m) is nn.Linear:
             m.forward = types.MethodType(_linear_forward, m)
@@ -300,7 +290,7 @@ def install_fused_forward(model: nn.Module):
             m.forward = types.MethodType(_fused_mlp_forward, m)
         elif isinstance(m, ml.LlamaRMSNorm):
             m.forward = types.MethodType(_fused_rmsnorm_forward, m)
-        elif isinstance(m, ml.LlamaDecoderLayer) and staged:
+        elif isinstance(m, ml.LlamaDecoderLayer):
             m.forward = types.MethodType(_staged_decoder_forward, m)
 
 
@@ -337,7 +327,7 @@ class Llama(BaseModel):
     # -- random-init constructor (synthetic benchmark / tests) --------------------------------
     @classmethod
     def random(cls, model_config, num_layers=None, device='cuda', dtype=torch.bfloat16,
-               seed=0, std=0.02):
+               seed=0, std=0.02, residency=None):
         from transformers.models.llama import modeling_llama as ml
         cfg = model_config
         cfg._attn_implementation = getattr(cfg, '_attn_implementation', None) or 'sdpa'
@@ -357,11 +347,11 @@ class Llama(BaseModel):
             rot = ml.LlamaRotaryEmbedding(cfg)
         blocks = _Blocks(layers, rot)
         blocks.config = cfg
-        return cls(hf_model=blocks, device=device)
+        return cls(hf_model=blocks, device=device, residency=residency)
 
     def rotary_kwargs(self, seq_len, device=None):
         """Block kwargs the Catcher would capture for an unpadded causal batch."""
-        device = device or next(self.model.parameters()).device
+        device = device or self.device
         pos = torch.arange(seq_len, device=device).unsqueeze(0)
         cos, sin = self._rotary_table(pos)
         return {'position_embeddings': (cos, sin), 'attention_mask': None, 'position_ids': pos}
@@ -370,8 +360,12 @@ class Llama(BaseModel):
         """LlamaRotaryEmbedding.forward's cos / sin (the model's own inv_freq and attention
         scaling, rope_scaling included) with its `inv_freq @ position_ids` -- a K = 1 product,
         one rounding per element -- as an elementwise outer product: the same values bit for
-        bit, without a vendor GEMM launch."""
+        bit, without a vendor GEMM launch. Rope types whose table depends on the sequence
+        length (dynamic, longrope: `@dynamic_rope_update` rescales inv_freq) run the module."""
         re = self.rotary_emb
+        if getattr(re, 'rope_type', 'default') not in ('default', 'llama3'):
+            dummy = torch.empty(1, dtype=self.torch_dtype, device=pos.device)
+            return re(dummy, pos)
         inv = re.inv_freq.float().to(pos.device)
         freqs = pos[0].float()[:, None] * inv[None, :]
         emb = torch.cat((freqs, freqs), dim=-1)

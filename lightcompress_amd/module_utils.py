@@ -12,20 +12,14 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-import os
-
 from . import ops
-
-# F.linear of the calibration forwards on the lcq projection GEMM (csrc/gemm256.hip);
-# LCQ_GEMM=0 hands every linear back to torch (hipBLASLt) for A/B runs
-_GEMM_ON = os.environ.get('LCQ_GEMM', '1') != '0'
 
 
 def lcq_linear(x, weight, bias=None):
     """F.linear(x, weight, bias) on the lcq GEMM when the operands fit it (bf16 / fp16 on the
     device, K % 64 == 0, out_features % 16 == 0, bias in the input dtype); other operands
     (fp32 GPTQ weights, odd shapes) take torch's F.linear."""
-    if (_GEMM_ON and ops.gemm_supported(x, weight)
+    if (ops.gemm_supported(x, weight)
             and (bias is None or (bias.dtype == x.dtype and bias.is_contiguous()))):
         return ops.linear(x, weight, bias)
     return F.linear(x, weight, bias)
@@ -241,7 +235,7 @@ class VllmRealQuantLinear(nn.Module):
     @torch.no_grad()
     def quant_pack(cls, module, w_q, quant_config):
         pre = getattr(module, '_lcq_prequant', None)
-        if pre is not None:  # batched by BaseBlockwiseQuantization._prequant_fp8_blocks
+        if pre is not None:  # batched by BaseBlockwiseQuantization._prequant_fp8_block
             del module._lcq_prequant
             return pre
         wq = getattr(w_q, 'keywords', {}).get('wquantizer')
@@ -318,6 +312,11 @@ class AutoawqRealQuantLinear(nn.Module):
     @classmethod
     @torch.no_grad()
     def quant_pack(cls, module, w_q, quant_config):
+        if module.weight.data.dtype == torch.float8_e4m3fn:  # module_utils.py:1079-1085
+            from .kernel import weight_cast_to_bf16
+            module.weight.data = weight_cast_to_bf16(
+                module.weight.data, module.weight_scale_inv.data,
+                module.block_size).to(torch.bfloat16)
         _, scales, zeros = w_q(module)
         if quant_config['weight']['pack_version'] != 'gemm_pack':
             raise NotImplementedError(f"Not support {quant_config['weight']['pack_version']}.")

@@ -221,6 +221,28 @@ def hessian_accum(x: torch.Tensor, H: torch.Tensor, alpha: float, beta: float) -
     return H
 
 
+def hessian_grouped(x: torch.Tensor, bounds, H: torch.Tensor, alpha: float) -> torch.Tensor:
+    """H <- alpha * tree over token groups of the groups' x^T x (lcq_hessian_grouped: one
+    launch; ``bounds`` = token offsets [0, ..., n] of the ng = 1 / 2 / 4 / 8 groups)."""
+    import ctypes
+    x2 = x.reshape(-1, x.shape[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    n, ic = x2.shape
+    if H.dtype != torch.float32 or tuple(H.shape) != (ic, ic) or not H.is_contiguous():
+        raise ValueError('H must be contiguous fp32 [ic, ic]')
+    if bounds[0] != 0 or bounds[-1] != n:
+        raise ValueError('bounds must run from 0 to the token count')
+    b = (ctypes.c_int64 * len(bounds))(*[int(v) for v in bounds])
+    ng = len(bounds) - 1
+    ws_bytes = N.load().lcq_hessian_grouped_workspace_bytes(b, ng, ic)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=x2.device)
+    N.call('lcq_hessian_grouped', N.ptr(x2), N.dt(x2), ic, b, ng, N.ptr(H), float(alpha),
+           N.ptr(ws), ws_bytes, N.stream_of(x2))
+    N.note_work('lcq_hessian_grouped', n * ic * (ic + 1))  # symmetric rank-n update (§8d)
+    return H
+
+
 def tree_sum(parts, alpha: float = 1.0, out: torch.Tensor | None = None) -> torch.Tensor:
     """out = alpha * the fixed pairwise tree sum of 1 / 2 / 4 / 8 equal fp32 tensors
     (lcq_tree_sum; deterministic, the grouped Hessian's reduction order)."""
@@ -303,6 +325,25 @@ def chol_inv_tile(A: torch.Tensor, info: torch.Tensor, row0: int = 0,
            0 if L is None else L.data_ptr(), 0 if L is None else _ld(L),
            X.data_ptr(), _ld(X), N.ptr(info), row0, N.stream_of(A))
     return X
+
+
+def gather_rc(A: torch.Tensor, rsrc=None, csrc=None, dead_col=None, dead_diag=None,
+              damp=None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i][j] = f(A[rsrc[i]][csrc[j]]) in fp32 (lcq_gather_rc): GPTQ's act-order
+    permutation, dead-column handling and damping in one pass (see include/lcq.h)."""
+    if A.dim() != 2 or A.stride(1) != 1:
+        raise ValueError('gather_rc: 2-D row-major A')
+    rows = A.shape[0] if rsrc is None else rsrc.numel()
+    cols = A.shape[1] if csrc is None else csrc.numel()
+    if out is None:
+        out = torch.empty((rows, cols), dtype=torch.float32, device=A.device)
+    idx = [None if t is None else t.to(torch.int64).contiguous() for t in (rsrc, csrc)]
+    msk = [None if t is None else t.to(torch.uint8).contiguous() for t in (dead_col, dead_diag)]
+    dmp = None if damp is None else damp.to(torch.float32).reshape(1).contiguous()
+    N.call('lcq_gather_rc', N.ptr_strided(A), N.dt(A.dtype), rows, cols, A.stride(0),
+           N.ptr(idx[0]), N.ptr(idx[1]), N.ptr(msk[0]), N.ptr(msk[1]), N.ptr(dmp),
+           N.ptr(out), out.stride(0), N.stream_of(A))
+    return out
 
 
 def gptq_trailing(W: torch.Tensor, c0: int, cnt: int, c1: int, err: torch.Tensor,

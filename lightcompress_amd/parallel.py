@@ -8,10 +8,16 @@ SURVEY.md §8e: the hot path shards naturally —
 * GPTQ within a block: rows independent given U -> ``row_shard`` + ``gather_rows``.
 The reference's own data-parallel semantics (replicas with averaged statistics) are kept by
 ``allreduce_mean_`` and ``awq_pick_best`` (awq.py:255-273) for drop-in DP runs.
+
+Independent-unit deploys (data-free RTN, DSv3 experts) run as ``shard_units``: every rank
+real-quants the units ``residency.Ownership`` assigns it (LPT on parameter counts) and the
+packed results are published with ``publish`` -- one flat byte broadcast per (block, owner),
+never a float weight.
 """
 from __future__ import annotations
 
 import heapq
+import importlib
 
 import torch
 import torch.distributed as dist
@@ -130,3 +136,135 @@ def pass_tensors(tensors, src: int, group):
     for t in tensors:
         dist.broadcast(t, src=src, group=group)
 
+
+
+def planned_mode(config, world: int) -> str:
+    """The parallel mode a run of `config` takes at `world` ranks, known before the model is
+    built (BlockwiseOpt.parallel_mode decides the same from the algorithm object): the
+    YAML's special.parallel, else shard_units for a data-free run (no calib section,
+    llmc/__main__.py:42), shard_blocks when quant_out is off, else the algorithm's own
+    sequential mode."""
+    if world == 1:
+        return 'single'
+    q = config['quant']
+    mode = (q.get('special', {}) or {}).get('parallel', None)
+    if mode:
+        return mode
+    if not config.get('calib', False):
+        return 'shard_units'
+    if not q.get('quant_out', False):
+        return 'shard_blocks'
+    from .registry import ALGO_REGISTRY
+    return getattr(ALGO_REGISTRY[q['method']], 'sequential_parallel_mode', 'replicate')
+
+
+def _plain_attrs(m):
+    return {k: v for k, v in m.__dict__.items()
+            if not k.startswith('_') and k != 'training'
+            and isinstance(v, (int, float, str, bool, tuple, torch.Size, torch.dtype,
+                               type(None)))}
+
+
+def _slots(m, recurse):
+    mods = m.named_modules() if recurse else [('', m)]
+    for mn, mod in mods:
+        for kind in ('_parameters', '_buffers'):
+            for tn, t in getattr(mod, kind).items():
+                yield mn, mod, kind, tn, t
+
+
+def _dt(t):
+    return str(t.dtype).split('.')[-1]
+
+
+@torch.no_grad()
+def publish(block: torch.nn.Module, assign: dict, rest_owner: int | None = None):
+    """After each rank replaced the block's modules it owns (``assign``: module name relative
+    to the block -> owner rank), give every rank the same block: the non-owners rebuild each
+    module as an empty instance of the owner's class (same plain attributes, parameters and
+    buffers of the owner's shapes and dtypes; their old modules are dropped unread), then
+    every owner broadcasts ALL its modules' tensors as one flat byte buffer. With
+    ``rest_owner`` the block's other tensors (norms, ...) come from that rank the same way,
+    buffers it registered included. Collectives: one all_gather_object of the specs, one
+    broadcast per owner with data."""
+    rank, world = dist_world()
+    if world == 1:
+        return
+    mine = []
+    for n, r in sorted(assign.items()):
+        if r != rank:
+            continue
+        m = block.get_submodule(n)
+        mine.append((n, type(m).__module__, type(m).__qualname__, _plain_attrs(m),
+                     [(kind, tn, None if t is None else tuple(t.shape),
+                       None if t is None else _dt(t))
+                      for _, _, kind, tn, t in _slots(m, recurse=False)]))
+    rest = None
+    if rest_owner == rank:
+        under = tuple(f'{n}.' for n in assign)
+        rest = [(mn, kind, tn, tuple(t.shape), _dt(t))
+                for mn, _, kind, tn, t in _slots(block, recurse=True)
+                if t is not None and mn not in assign and not mn.startswith(under)]
+    specs = [None] * world
+    dist.all_gather_object(specs, (mine, rest))
+    dev = next((t.device for _, _, _, _, t in _slots(block, True)
+                if t is not None and not t.is_meta), torch.device('cpu'))
+    for r, (mods, rst) in enumerate(specs):
+        if r == rank:
+            continue
+        for n, modname, qual, attrs, tensors in mods:
+            cls = importlib.import_module(modname)
+            for part in qual.split('.'):
+                cls = getattr(cls, part)
+            m = cls.__new__(cls)
+            torch.nn.Module.__init__(m)
+            for kind, tn, shape, dt in tensors:
+                t = None if shape is None else torch.empty(shape, dtype=getattr(torch, dt),
+                                                           device=dev)
+                if kind == '_parameters':
+                    m.register_parameter(tn, None if t is None else
+                                         torch.nn.Parameter(t, requires_grad=False))
+                else:
+                    m.register_buffer(tn, t)
+            for k, v in attrs.items():
+                setattr(m, k, v)
+            parent_name, _, child = n.rpartition('.')
+            parent = block.get_submodule(parent_name) if parent_name else block
+            setattr(parent, child, m)
+        for mn, kind, tn, shape, dt in (rst or []):
+            mod = block.get_submodule(mn) if mn else block
+            t = getattr(mod, kind).get(tn)
+            if t is None or tuple(t.shape) != shape or _dt(t) != dt or t.is_meta:
+                new = torch.empty(shape, dtype=getattr(torch, dt), device=dev)
+                if kind == '_parameters' and t is not None:
+                    t.data = new
+                elif kind == '_parameters':
+                    mod.register_parameter(tn, torch.nn.Parameter(new, requires_grad=False))
+                else:
+                    mod.register_buffer(tn, new)
+    for r, (mods, rst) in enumerate(specs):
+        ts = []
+        for n, _, _, _, tensors in mods:
+            m = block.get_submodule(n)
+            ts += [getattr(m, kind)[tn] for kind, tn, shape, _ in tensors if shape is not None]
+        for mn, kind, tn, _, _ in (rst or []):
+            ts.append(getattr(block.get_submodule(mn) if mn else block, kind)[tn])
+        sizes = [t.numel() * t.element_size() for t in ts]
+        total = sum(sizes)
+        if total == 0:
+            continue
+        if r == rank:
+            flat = torch.cat([t.detach().contiguous().reshape(-1).view(torch.uint8)
+                              for t in ts])
+        else:
+            flat = torch.empty(total, dtype=torch.uint8, device=dev)
+        dist.broadcast(flat, src=r)
+        if r != rank:
+            off = 0
+            for t, nb in zip(ts, sizes):
+                dst = t.data if t.data.is_contiguous() else torch.empty_like(
+                    t.data, memory_format=torch.contiguous_format)
+                dst.reshape(-1).view(torch.uint8).copy_(flat[off:off + nb])
+                if dst is not t.data:
+                    t.data.copy_(dst)
+                off += nb

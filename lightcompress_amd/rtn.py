@@ -10,6 +10,9 @@ from .registry import ALGO_REGISTRY
 
 @ALGO_REGISTRY
 class RTN(BaseBlockwiseQuantization):
+    def block_has_work(self):
+        return self.act_static
+
     @torch.no_grad()
     def block_opt(self, block, *opt_kwargs):
         if self.act_static:  # rtn.py:16-20 (kv-cache quant is out of scope)

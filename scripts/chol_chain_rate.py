@@ -1,7 +1,6 @@
 """Probe: wall time of one inverse_cholesky_upper chain (gptq_core: recursion on lcq_gemm_f32
 + lcq_chol_inv_tile) at the Llama-3-8B Hessian sizes, eager without / with the side-stream
 overlap of T = L21 X11 (gptq_core._OVERLAP_MIN), and replayed as a captured HIP graph."""
-import os
 import sys
 from pathlib import Path
 
@@ -16,9 +15,9 @@ for n in (4096, 14336):
     X = torch.randn(n, 2 * n, device=dev, generator=g)
     H = X @ X.T / (2 * n)
     H.diagonal().add_(0.01)
-    for ov, graph in ((10 ** 9, '0'), (1024, '0'), (1024, '1')):
+    for ov, graph in ((10 ** 9, False), (1024, False), (1024, True)):
         gptq_core._OVERLAP_MIN = ov
-        os.environ['LCQ_CHOL_GRAPH'] = graph
+        gptq_core.CHAIN_GRAPHS = graph
         U0 = gptq_core.inverse_cholesky_upper(H.clone())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 3

@@ -15,7 +15,8 @@ import tiny_models as TM
 from pipeline_configs import CONFIGS
 
 
-def run_ours(name, dev, monkeypatch=None, config_override=None):
+def run_ours(name, dev, monkeypatch=None, config_override=None, model_override=None,
+             return_model=False):
     from lightcompress_amd.pipeline import build_algo, build_model
     from lightcompress_amd.utils import load_config
     spec = CONFIGS[name]
@@ -63,6 +64,8 @@ def run_ours(name, dev, monkeypatch=None, config_override=None):
         sp['clip_path'] = f'{tmp}/clip'
     cfg = {'model': {'type': family, 'path': str(TM.MODEL_DIRS[family]), 'torch_dtype': dtype},
            'quant': quant}
+    if model_override:
+        cfg['model'].update(model_override)
     if spec['calib']:
         cfg['calib'] = dict(spec['calib'])
     config = load_config(cfg)
@@ -99,6 +102,8 @@ def run_ours(name, dev, monkeypatch=None, config_override=None):
             got[f'b{bi}__{ln.replace(".", "__")}'] = lin.weight.data.detach().cpu()
             if hasattr(lin, 'buf_act_scales_0'):  # static act qparams
                 diag[f'a_b{bi}__{ln.replace(".", "__")}'] = lin.buf_act_scales_0.detach().cpu()
+    if return_model:
+        return ref, got, diag, model
     return ref, got, diag
 
 

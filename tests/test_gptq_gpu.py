@@ -331,9 +331,9 @@ def test_inverse_cholesky_graph_replay(dev, monkeypatch):
         H.diagonal().add_(0.05)
         Hs.append(H.to(dev))
     gptq_core._chain_graphs.pop((torch.device(dev).index or 0, n), None)
-    monkeypatch.setenv('LCQ_CHOL_GRAPH', '0')
+    monkeypatch.setattr(gptq_core, 'CHAIN_GRAPHS', False)
     eager = [gptq_core.inverse_cholesky_upper(H.clone()) for H in Hs]
-    monkeypatch.setenv('LCQ_CHOL_GRAPH', '1')
+    monkeypatch.setattr(gptq_core, 'CHAIN_GRAPHS', True)
     graphed = [gptq_core.inverse_cholesky_upper(H.clone()) for H in Hs + Hs[:1]]
     assert (torch.device(dev).index or 0, n) in gptq_core._chain_graphs
     for a, b in zip(eager + eager[:1], graphed):
@@ -639,3 +639,40 @@ def test_grouped_hessian_world_independent(dev, n, tpe, ic):
     err = (H1.double() - ref).abs()
     assert (err <= 2e-6 * bound + 1e-30).all().item(), (err / bound).max().item()
     assert torch.equal(H1, H1.t())
+
+
+@pytest.mark.parametrize('n', [1000, 4096])
+def test_gather_rc_equals_torch_prepare(dev, n):
+    """lcq_gather_rc (one pass) against the torch form of gptq.py:58-64, 128-176 it replaces:
+    H[dead, dead] = 1; H[perm][:, perm]; + damp on the diagonal; flipped for the chain
+    (J H J) -- and on the weight: fp32 widening, dead columns zeroed, column gather, and the
+    inverse permutation afterwards. Bit-equal."""
+    from lightcompress_amd import ops
+    g = torch.Generator(device=dev).manual_seed(n)
+    X = torch.randn(n, n + 7, generator=g, device=dev)
+    H = X @ X.T
+    dead = torch.zeros(n, dtype=torch.bool, device=dev)
+    dead[torch.randperm(n, generator=g, device=dev)[:5]] = True
+    H[dead, :] = 0
+    H[:, dead] = 0
+    perm = torch.randperm(n, generator=g, device=dev)
+    damp = 0.01 * torch.mean(torch.where(dead, torch.ones_like(torch.diag(H)),
+                                         torch.diag(H))[perm])
+    ref = H.clone()
+    idx = torch.nonzero(dead).flatten()
+    ref[idx, idx] = 1
+    ref = ref[perm][:, perm]
+    d = torch.arange(n, device=dev)
+    ref[d, d] += damp
+    ref = ref.flip(0, 1).contiguous()
+    rev = perm.flip(0)
+    got = ops.gather_rc(H, rsrc=rev, csrc=rev, dead_diag=dead, damp=damp)
+    assert torch.equal(got, ref)
+    W = (torch.randn(300, n, generator=g, device=dev) * 0.02).to(torch.bfloat16)
+    wref = W.float().clone()
+    wref[:, dead] = 0
+    wref = wref[:, perm].contiguous()
+    wgot = ops.gather_rc(W, csrc=perm, dead_col=dead)
+    assert torch.equal(wgot, wref)
+    inv = torch.argsort(perm)
+    assert torch.equal(ops.gather_rc(wgot, csrc=inv), wref[:, inv])

@@ -113,7 +113,7 @@ def test_entry_view_unequal_entries():
     assert B.entry_view(ctx, m, xr) is xr
 
 
-@pytest.mark.parametrize('scaling', [None, 'llama3'])
+@pytest.mark.parametrize('scaling', [None, 'llama3', 'dynamic'])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
 def test_rotary_kwargs_equal_module(scaling, dtype):
     """Llama.rotary_kwargs builds cos / sin as an elementwise outer product (no K = 1 GEMM
@@ -123,9 +123,12 @@ def test_rotary_kwargs_equal_module(scaling, dtype):
     rs = None if scaling is None else {'rope_type': 'llama3', 'factor': 8.0,
                                        'low_freq_factor': 1.0, 'high_freq_factor': 4.0,
                                        'original_max_position_embeddings': 8192}
+    maxpos = 131072
+    if scaling == 'dynamic':  # the table depends on seq_len past the original context
+        rs, maxpos = {'rope_type': 'dynamic', 'factor': 2.0}, 1024
     cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=2,
                       num_key_value_heads=1, num_hidden_layers=1, rope_theta=500000.0,
-                      max_position_embeddings=131072, rope_scaling=rs, torch_dtype=dtype)
+                      max_position_embeddings=maxpos, rope_scaling=rs, torch_dtype=dtype)
     m = Llama.random(cfg, num_layers=1, device=torch.device('cpu'), seed=0)
     m.torch_dtype = dtype
     for S in (64, 2048):

@@ -35,7 +35,19 @@ def run2(fn, world=2):
     procs = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
+    import queue
+    import time
+    res, t0 = {}, time.time()
+    while len(res) < len(procs):   # a worker that dies fails the test at once, not at timeout
+        try:
+            r, v = q.get(timeout=1)
+            res[r] = v
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() - t0 > 240:
+                for p in procs:
+                    p.kill()
+                raise AssertionError(f'worker exit codes {[p.exitcode for p in procs]}')
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

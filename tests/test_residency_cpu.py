@@ -1,0 +1,258 @@
+"""Host logic of block residency and sharded deploys, on CPU with gloo:
+
+* the unit plan (residency.Ownership): every linear owned once, a routed expert's linears
+  together, deterministic on every rank;
+* ``materialize: owned`` loading: a rank reads and allocates only its blocks / units, the rest
+  stays on the meta device;
+* the sharded deploy: every rank quantizes its units, P.publish hands the packed shards to the
+  others (one flat byte broadcast per block and owner) -- world 2 equals one process;
+* the sharded save: per-rank safetensors + index, whose union equals the one-process save.
+
+Real quantization needs the HIP library; here the packers run as the oracle's CPU restatement
+(monkeypatched into VllmRealQuantLinear) so the multi-rank plumbing is what is tested; the
+same flows on the GPU kernels are in test_residency_gpu.py."""
+import functools
+import json
+import os
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from test_parallel_gloo import run2  # noqa: E402
+
+import tiny_models as TM  # noqa: E402
+
+
+def _config(family, calib=False, materialize='all', extra_quant=None):
+    from lightcompress_amd.utils import load_config
+    cfg = {'model': {'type': family, 'path': str(TM.MODEL_DIRS[family]),
+                     'torch_dtype': 'float16' if family == 'Opt' else 'bfloat16',
+                     'materialize': materialize, 'residency': 'device'},
+           'quant': {'method': 'RTN', 'weight': {'bit': 8, 'symmetric': True,
+                                                 'granularity': 'per_channel'}}}
+    if calib:
+        cfg['calib'] = {'seq_len': 16, 'bs': -1, 'n_samples': 2}
+        cfg['quant'] = {'method': 'Awq', 'weight': {'bit': 4, 'symmetric': True,
+                                                    'granularity': 'per_group',
+                                                    'group_size': 128},
+                        'special': {'trans': True, 'trans_version': 'v2'}, 'quant_out': False}
+    if extra_quant:
+        cfg['quant'].update(extra_quant)
+    return load_config(cfg)
+
+
+def _cpu_packers(monkeypatch_like=None):
+    """VllmRealQuantLinear.quant_pack on the oracle (CPU): real_quant_dynamic + pack_vllm."""
+    from lightcompress_amd.module_utils import VllmRealQuantLinear
+    from oracle import quant_ref as Q
+
+    def quant_pack(cls, module, w_q, quant_config):
+        w = quant_config['weight']
+        gran = w['granularity']
+        codes, s, _ = Q.real_quant_dynamic(module.weight.data, w['bit'], w['symmetric'],
+                                           gran, w.get('group_size', 128))
+        if w.get('need_pack', False):
+            return torch.from_numpy(Q.pack_vllm(codes, w['bit'])), s.to(torch.float16)
+        return codes, s
+    VllmRealQuantLinear.quant_pack = classmethod(quant_pack)
+
+
+def test_unit_plan_covers_each_linear_once():
+    from lightcompress_amd.pipeline import build_model
+    from lightcompress_amd.residency import Ownership, unit_key
+    assert unit_key('mlp.experts.12.down_proj') == 'mlp.experts.12'
+    assert unit_key('mlp.shared_experts.gate_proj') == 'mlp.shared_experts.gate_proj'
+    assert unit_key('self_attn.q_a_proj') == 'self_attn.q_a_proj'
+    model = build_model(_config('DeepseekV3'), device='cpu')
+    for world in (1, 2, 3, 8):
+        plans = [Ownership.plan('shard_units', r, world, model) for r in range(world)]
+        assert all(p.unit_owner == plans[0].unit_owner for p in plans)  # rank-independent
+        loads = [0] * world
+        for bi, block in enumerate(model.get_blocks()):
+            lins = model.get_block_linears(block)
+            for n, m in lins.items():
+                owners = [r for r in range(world) if plans[r].owns(bi, n)]
+                assert len(owners) == 1, (bi, n)
+                loads[owners[0]] += m.weight.numel()
+                if '.experts.' in n and not n.startswith('mlp.shared'):
+                    e = n.rsplit('.', 1)[0]
+                    assert all(plans[0].owner_of(bi, f'{e}.{p}') == owners[0]
+                               for p in ('gate_proj', 'up_proj', 'down_proj'))
+        biggest = max(m.weight.numel() * (3 if '.experts.' in n else 1)
+                      for b in model.get_blocks() for n, m in model.get_block_linears(b).items())
+        assert max(loads) - min(loads) <= biggest
+
+
+def _owned_load(rank, world):
+    from safetensors.torch import load_file
+    from lightcompress_amd.pipeline import build_model
+    out = {}
+    for family, calib in (('DeepseekV3', False), ('Llama', True)):
+        model = build_model(_config(family, calib=calib, materialize='owned'), device='cpu')
+        sd = load_file(str(TM.MODEL_DIRS[family] / 'model.safetensors'))
+        prefix = model.blocks_container_name()
+        own = model.ownership
+        held, meta = [], []
+        for bi, block in enumerate(model.get_blocks()):
+            lins = set(model.get_block_linears(block))
+            for n, t in list(block.named_parameters()) + list(block.named_buffers()):
+                owned = own.owns_block_tensor(bi, n, lins)
+                if owned:
+                    assert not t.is_meta and torch.equal(t, sd[f'{prefix}.{bi}.{n}']), n
+                    held.append(f'{bi}.{n}')
+                else:
+                    assert t.is_meta, n   # never allocated, never read
+                    meta.append(f'{bi}.{n}')
+        for n, t in model.model.named_parameters():
+            if not n.startswith(prefix):
+                assert not t.is_meta and torch.equal(t, sd[n]), n
+        out[family] = (own.mode, sorted(held), sorted(meta))
+    return out
+
+
+def test_materialize_owned_loads_only_own_units():
+    res = run2(_owned_load)
+    for family, mode in (('DeepseekV3', 'shard_units'), ('Llama', 'shard_blocks')):
+        (m0, h0, x0), (m1, h1, x1) = res[0][family], res[1][family]
+        assert m0 == m1 == mode
+        shared = set(h0) & set(h1)
+        # what both hold is exactly the non-unit block tensors (norms, router) of shard_units
+        if mode == 'shard_blocks':
+            assert not shared and all(k.startswith('0.') for k in h0)
+            assert all(k.startswith('1.') for k in h1)
+        else:
+            assert all('_proj' not in k for k in shared), sorted(shared)[:4]
+        assert sorted(set(h0) | set(h1)) == sorted(set(h0 + x0))
+        assert x0 and x1
+
+
+def _deploy(rank, world, materialize, path, fmt='vllm_quant'):
+    from lightcompress_amd.pipeline import build_algo, build_model
+    _cpu_packers()
+    cfg = _config('DeepseekV3', materialize=materialize,
+                  extra_quant={'weight': {'bit': 4, 'symmetric': True,
+                                          'granularity': 'per_group', 'group_size': 64,
+                                          'need_pack': True}})
+    model = build_model(cfg, device='cpu')
+    algo = build_algo(model, cfg, None)
+    assert algo.parallel_mode() == ('single' if world == 1 else 'shard_units')
+    algo.run_block_loop()
+    algo.deploy(fmt)
+    if materialize == 'owned':
+        algo.save_model(path)
+        return None
+    # plain bytes: tensors through a multiprocessing queue would go via shared memory that the
+    # exiting worker tears down
+    return {f'{i}.{n}': (str(t.dtype), tuple(t.shape),
+                         t.detach().contiguous().reshape(-1).view(torch.uint8).numpy().tobytes())
+            for i, b in enumerate(model.get_blocks())
+            for n, t in [*b.named_parameters(), *b.named_buffers()]}
+
+
+def test_shard_units_deploy_matches_single_process(tmp_path):
+    single = _deploy(0, 1, 'all', None)
+    res = run2(functools.partial(_deploy, materialize='all', path=None))
+    assert any('weight_packed' in k for k in single)
+    for r in (0, 1):
+        assert res[r].keys() == single.keys()
+        for k in single:
+            assert res[r][k] == single[k], k   # dtype, shape and bytes
+
+
+def _load_dir(path):
+    from safetensors.torch import load_file
+    out = {}
+    files = sorted(f for f in os.listdir(path) if f.endswith('.safetensors'))
+    for f in files:
+        out.update(load_file(os.path.join(path, f)))
+    return out, files
+
+
+def test_sharded_save_equals_single_save(tmp_path):
+    from lightcompress_amd.pipeline import build_algo, build_model
+    _cpu_packers()
+    cfg = _config('DeepseekV3', extra_quant={'weight': {'bit': 4, 'symmetric': True,
+                                                         'granularity': 'per_group',
+                                                         'group_size': 64, 'need_pack': True}})
+    model = build_model(cfg, device='cpu')
+    algo = build_algo(model, cfg, None)
+    algo.run_block_loop()
+    algo.deploy('vllm_quant')
+    one = str(tmp_path / 'one')
+    algo.save_model(one)
+    two = str(tmp_path / 'two')
+    run2(functools.partial(_deploy, materialize='owned', path=two))
+    a, _ = _load_dir(one)
+    b, files = _load_dir(two)
+    assert files == ['model-00001-of-00002.safetensors', 'model-00002-of-00002.safetensors']
+    idx = json.load(open(os.path.join(two, 'model.safetensors.index.json')))
+    assert sorted(idx['weight_map']) == sorted(b)
+    assert idx['metadata']['total_size'] == sum(t.numel() * t.element_size() for t in b.values())
+    assert sorted(a) == sorted(b)
+    for k in a:
+        assert a[k].dtype == b[k].dtype and torch.equal(a[k], b[k]), k
+    assert os.path.exists(os.path.join(two, 'config.json'))
+
+
+def _publish_mixed(rank, world):
+    """publish: modules of several classes / dtypes (int32 packed, fp16 scales, 0-dim int64
+    buffers, a Parameter-holding nn.Linear left unquantized), and owner-registered rest
+    buffers, from two owners."""
+    from lightcompress_amd import parallel as P
+    torch.manual_seed(0)
+    blk = torch.nn.Module()
+    blk.a = torch.nn.Linear(8, 4)
+    blk.b = torch.nn.Linear(8, 4, bias=False)
+    blk.norm = torch.nn.LayerNorm(8)
+    if rank == 0:
+        q = torch.nn.Module()
+        q.register_buffer('weight_packed', torch.arange(8, dtype=torch.int32).view(4, 2))
+        q.register_buffer('weight_scale', torch.full((4, 1), 0.5, dtype=torch.float16))
+        q.register_buffer('qmax', torch.tensor(7))
+        q.register_buffer('input_scale', None)
+        q.in_features, q.out_features = 8, 4
+        blk.a = q
+        blk.norm.register_buffer('buf_extra', torch.tensor(3.0, dtype=torch.bfloat16))
+        with torch.no_grad():
+            blk.norm.weight.fill_(2.0)
+    if rank == 1:
+        with torch.no_grad():
+            blk.b.weight.fill_(5.0)
+    P.publish(blk, {'a': 0, 'b': 1}, rest_owner=0)
+    return {'a_cls': type(blk.a).__name__, 'packed': blk.a.weight_packed.tolist(),
+            'scale': blk.a.weight_scale.tolist(), 'qmax': int(blk.a.qmax),
+            'input_scale': blk.a.input_scale, 'in': blk.a.in_features,
+            'b': blk.b.weight.sum().item(), 'b_param': isinstance(blk.b.weight,
+                                                                 torch.nn.Parameter),
+            'norm': blk.norm.weight.sum().item(), 'extra': blk.norm.buf_extra.item()}
+
+
+def test_publish_mixed_modules():
+    res = run2(_publish_mixed)
+    assert res[0] == res[1]
+    r = res[1]
+    assert r['packed'] == [[0, 1], [2, 3], [4, 5], [6, 7]] and r['qmax'] == 7
+    assert r['input_scale'] is None and r['in'] == 8 and r['b'] == 160.0 and r['b_param']
+    assert r['norm'] == 16.0 and r['extra'] == 3.0
+
+
+@pytest.mark.parametrize('calib,quant_out,special,expect', [
+    (False, False, None, 'shard_units'), (True, False, None, 'shard_blocks'),
+    (True, True, None, 'shard_tokens'), (True, True, 'replicate', 'replicate')])
+def test_planned_mode_matches_algorithm(calib, quant_out, special, expect):
+    from lightcompress_amd.parallel import planned_mode
+    from lightcompress_amd.utils import load_config
+    q = {'method': 'GPTQ', 'weight': {'bit': 4, 'symmetric': False,
+                                      'granularity': 'per_channel'},
+         'special': {'actorder': True, 'static_groups': False, 'percdamp': 0.01,
+                     'blocksize': 128, 'true_sequential': True}, 'quant_out': quant_out}
+    if special:
+        q['special']['parallel'] = special
+    cfg = {'quant': q}
+    if calib:
+        cfg['calib'] = {'seq_len': 16}
+    assert planned_mode(load_config(cfg), 2) == expect
+    assert planned_mode(load_config(cfg), 1) == 'single'
