@@ -238,6 +238,15 @@ int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const void* A, in
                  const void* B, int64_t ldb, int bt, float beta, void* C, int64_t ldc,
                  void* stream);
 
+/* lcq_gemm_f32 with a caller workspace (lcq_gemm_f32_workspace_bytes(M, N, K) bytes, 0 when
+ * not needed): grids whose last round of 256 workgroups would run more than 10 % empty go
+ * stream-K -- the tiles x K-chunks work split evenly over 256 workgroups, k segments of cut
+ * tiles summed in k order by a fixup pass (deterministic). */
+int64_t lcq_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int lcq_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
+                    const void* B, int64_t ldb, int bt, float beta, void* C, int64_t ldc,
+                    void* workspace, int64_t ws_bytes, void* stream);
+
 /* Diagonal tile of the recursive fp32 factorisation behind U = chol(H^-1, upper)
  * (gptq.py:169-174): for SPD A (n x n, n <= 128, row-major fp32, leading dim lda), X <- L^-1
  * and, if L is not NULL, L <- the lower Cholesky factor (upper parts zeroed). A is only read.

@@ -565,8 +565,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t f32_rsrc(const float* p, int64
                                            (short)0, nb, 0x00020000);
 }
 
+// One output tile (rows r0.., columns c0..) over K chunks [ch0, ch1): `part` null -> the
+// alpha / beta epilogue into C, else the raw fp32 accumulators into the T x T partial tile
+// `part` (stream-K segments, summed in k order by k_gemm_f32_sk_fixup).
 template <int BT, int T, int NS>
-__device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds) {
+__device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds, int64_t r0,
+                                               int64_t c0, int64_t ch0, int64_t ch1,
+                                               float* part) {
   constexpr int OPB = T * DKC * 4;        // one operand chunk image (bytes)
   constexpr int STG = 2 * OPB;
   constexpr int PA = T / 32;              // A pieces (8 rows x 128 B) per wave
@@ -576,8 +581,7 @@ __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1;
-  const int64_t r0 = (int64_t)blockIdx.y * T, c0 = (int64_t)blockIdx.x * T;
-  const int64_t nch = a.K / DKC;
+  const int64_t nch = ch1;
 
   const __amdgpu_buffer_rsrc_t ra = f32_rsrc(a.A + r0 * a.lda, (a.M - r0) * a.lda * 4);
   __amdgpu_buffer_rsrc_t rb;
@@ -625,13 +629,14 @@ __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds) {
     for (int y = 0; y < MT; ++y) acc[x][y] = v4f32{0.f, 0.f, 0.f, 0.f};
   const int r16 = lane & 15, g = lane >> 4;
 
+  __syncthreads();  // a previous segment of this workgroup may still read the ring
 #pragma unroll
-  for (int j = 0; j + 1 < NS; ++j) stage(j, j);
-  for (int64_t ch = 0; ch < nch; ++ch) {
-    const int buf = (int)(ch % NS);
+  for (int j = 0; j + 1 < NS; ++j) stage(j, ch0 + j);
+  for (int64_t ch = ch0; ch < nch; ++ch) {
+    const int buf = (int)((ch - ch0) % NS);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * LPS) : "memory");
     __builtin_amdgcn_s_barrier();
-    stage((int)((ch + NS - 1) % NS), ch + NS - 1);
+    stage((int)((ch - ch0 + NS - 1) % NS), ch + NS - 1);
     const char* As = f32lds + buf * STG;
     const char* Bs = As + OPB;
     float av[MT][8], bv[MT][8];
@@ -673,6 +678,16 @@ __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // 16x16 MFMA tile: lane holds column lane & 15, rows 4 (lane >> 4) + v
+  if (part != nullptr) {
+#pragma unroll
+    for (int x = 0; x < MT; ++x)
+#pragma unroll
+      for (int y = 0; y < MT; ++y)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          part[(wr * WT + x * 16 + 4 * g + v) * T + wc * WT + y * 16 + r16] = acc[x][y][v];
+    return;
+  }
 #pragma unroll
   for (int x = 0; x < MT; ++x)
 #pragma unroll
@@ -697,10 +712,11 @@ constexpr int f32d_lds() { return NS_F32D * 2 * T * DKC * 4; }
 
 // fixed kernels around the body (a templated __global__ with device builtins inside its
 // lambda loses its host stub under hipcc)
-#define LCQ_F32D_KERNEL(NAME, BT, T)                                   \
-  __global__ void __launch_bounds__(256, 1) NAME(Args a) {             \
-    extern __shared__ __attribute__((aligned(16))) char f32lds[];      \
-    gemm_f32d_body<BT, T, NS_F32D>(a, f32lds);                         \
+#define LCQ_F32D_KERNEL(NAME, BT, T)                                                   \
+  __global__ void __launch_bounds__(256, 1) NAME(Args a) {                             \
+    extern __shared__ __attribute__((aligned(16))) char f32lds[];                      \
+    gemm_f32d_body<BT, T, NS_F32D>(a, f32lds, (int64_t)blockIdx.y * T,                 \
+                                   (int64_t)blockIdx.x * T, 0, a.K / DKC, nullptr);    \
   }
 LCQ_F32D_KERNEL(k_gemm_f32d_n128, 0, 128)
 LCQ_F32D_KERNEL(k_gemm_f32d_t128, 1, 128)
@@ -708,12 +724,92 @@ LCQ_F32D_KERNEL(k_gemm_f32d_n64, 0, 64)
 LCQ_F32D_KERNEL(k_gemm_f32d_t64, 1, 64)
 #undef LCQ_F32D_KERNEL
 
+// Stream-K over 128^2 tiles: the tiles x K-chunks work units split evenly over SK_WG
+// workgroups (one per CU: SK_WG = 256 on MI355X), so a grid of e.g. 784 tiles (3.06 rounds of
+// 256, 76 % of the last round idle) runs as one full round. Workgroup w takes units
+// [b(w), b(w + 1)), b(w) = w U / SK_WG, tile-major (t = u / nch): a whole tile goes straight
+// to C with the normal epilogue (the same k order as k_gemm_f32d_*128); a tile cut by a
+// workgroup boundary leaves its k segments as raw partial tiles in fixed slots (the segment
+// that starts the workgroup's range -> slot 2w, the one that ends it -> slot 2w + 1) and
+// k_gemm_f32_sk_fixup sums them in k order (deterministic: no atomics, no spin-waits).
+constexpr int SK_WG = 256;
+struct SkArgs {
+  int64_t tiles, ntn, nch, units;
+  float* part;   // 2 * SK_WG slots of 128 x 128 fp32
+};
+__device__ __forceinline__ int64_t sk_bound(const SkArgs& s, int64_t w) {
+  return w * s.units / SK_WG;
+}
+
+#define LCQ_F32D_SK_KERNEL(NAME, BT)                                                  \
+  __global__ void __launch_bounds__(256, 1) NAME(Args a, SkArgs sk) {                 \
+    extern __shared__ __attribute__((aligned(16))) char f32lds[];                     \
+    const int64_t w = blockIdx.x, u0 = sk_bound(sk, w), u1 = sk_bound(sk, w + 1);     \
+    for (int64_t u = u0; u < u1;) {                                                   \
+      const int64_t t = u / sk.nch, ts = t * sk.nch, te = ts + sk.nch;                \
+      const int64_t e = te < u1 ? te : u1;                                            \
+      float* part = nullptr;                                                          \
+      if (u != ts || e != te)                                                         \
+        part = sk.part + (u == u0 && u != ts ? 2 * w : 2 * w + 1) * (128 * 128);      \
+      gemm_f32d_body<BT, 128, NS_F32D>(a, f32lds, (t / sk.ntn) * 128,                 \
+                                       (t % sk.ntn) * 128, u - ts, e - ts, part);      \
+      u = e;                                                                          \
+    }                                                                                 \
+  }
+LCQ_F32D_SK_KERNEL(k_gemm_f32d_sk_n128, 0)
+LCQ_F32D_SK_KERNEL(k_gemm_f32d_sk_t128, 1)
+#undef LCQ_F32D_SK_KERNEL
+
+// C tile t = beta C + alpha * (((seg_0 + seg_1) + ...) in k order) for every tile cut by a
+// workgroup boundary; a workgroup per (tile, 16-row piece), whole tiles exit at once
+__global__ void __launch_bounds__(256) k_gemm_f32_sk_fixup(Args a, SkArgs sk) {
+  const int64_t t = blockIdx.x;
+  const int64_t ts = t * sk.nch, tl = ts + sk.nch - 1;
+  // the workgroups holding the tile's first and last unit (b(w) = w U / SK_WG)
+  int64_t wa = (ts * SK_WG) / sk.units, wb = (tl * SK_WG) / sk.units;
+  while (sk_bound(sk, wa + 1) <= ts) ++wa;
+  while (wa > 0 && sk_bound(sk, wa) > ts) --wa;
+  while (sk_bound(sk, wb + 1) <= tl) ++wb;
+  while (wb > 0 && sk_bound(sk, wb) > tl) --wb;
+  if (wa == wb) return;  // one workgroup: written by the main kernel
+  const int64_t r0 = (t / sk.ntn) * 128, c0 = (t % sk.ntn) * 128;
+  const int cx = threadIdx.x & 127, rr0 = blockIdx.y * 16 + (threadIdx.x >> 7);
+  for (int rr = rr0; rr < blockIdx.y * 16 + 16; rr += 2) {
+    const int64_t r = r0 + rr, c = c0 + cx;
+    if (r >= a.M || c >= a.N) continue;
+    float v = sk.part[(2 * wa + 1) * (128 * 128) + rr * 128 + cx];
+    for (int64_t w = wa + 1; w <= wb; ++w)
+      if (sk_bound(sk, w + 1) > sk_bound(sk, w))  // (an empty range holds no segment)
+        v = __fadd_rn(v, sk.part[(2 * w) * (128 * 128) + rr * 128 + cx]);
+    float* p = a.C + r * a.ldc + c;
+    const float val = a.alpha * v;
+    *p = a.beta == 0.f ? val : __fmaf_rn(a.beta, *p, val);
+  }
+}
+
 }  // namespace f32g
 }  // namespace lcq
 
-extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
-                            int64_t lda, const void* B, int64_t ldb, int bt, float beta, void* C,
-                            int64_t ldc, void* stream) {
+static int64_t sk_ws_bytes() { return (int64_t)2 * f32g::SK_WG * 128 * 128 * 4; }
+
+// Stream-K (k_gemm_f32d_sk_*) where a 128^2-tile grid leaves more than 10 % of its last round
+// of 256 workgroups idle and every workgroup still gets >= 32 K chunks of work
+static bool use_stream_k(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((N + 127) / 128) * ((M + 127) / 128);
+  if (tiles < 128 || K % f32g::DKC) return false;
+  const int64_t rounds = (tiles + f32g::SK_WG - 1) / f32g::SK_WG;
+  const bool ragged = tiles * 10 < rounds * f32g::SK_WG * 9;
+  return ragged && tiles * (K / f32g::DKC) >= (int64_t)32 * f32g::SK_WG;
+}
+
+extern "C" int64_t lcq_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  return use_stream_k(M, N, K) ? sk_ws_bytes() : 0;
+}
+
+static int gemm_f32_impl(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
+                         int64_t lda, const void* B, int64_t ldb, int bt, float beta, void* C,
+                         int64_t ldc, void* ws, int64_t ws_bytes, void* stream) {
+
   LCQ_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
   if (M == 0 || N == 0) return LCQ_OK;
   LCQ_REQUIRE(A != nullptr && B != nullptr && C != nullptr, "null pointers");
@@ -735,7 +831,22 @@ extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const 
   // LDS-DMA kernel: K % 32 == 0, 16-byte aligned rows, 32-bit byte offsets
   const bool dma = K % f32g::DKC == 0 && a.vec && al(C) &&
                    M * lda < ((int64_t)1 << 29) && (bt ? N * ldb : K * ldb) < ((int64_t)1 << 29);
-  if (dma) {
+  if (dma && ws != nullptr && ws_bytes >= sk_ws_bytes() && use_stream_k(M, N, K)) {
+    f32g::SkArgs sk{};
+    sk.ntn = (N + 127) / 128;
+    sk.tiles = sk.ntn * ((M + 127) / 128);
+    sk.nch = K / f32g::DKC;
+    sk.units = sk.tiles * sk.nch;
+    sk.part = reinterpret_cast<float*>(ws);
+    constexpr int L = f32g::f32d_lds<128>();
+    auto k = bt ? f32g::k_gemm_f32d_sk_t128 : f32g::k_gemm_f32d_sk_n128;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, L);
+    hipLaunchKernelGGL(k, dim3(f32g::SK_WG), 256, L, st, a, sk);
+    int rc = check_launch("lcq_gemm_f32: stream-k");
+    if (rc) return rc;
+    hipLaunchKernelGGL(f32g::k_gemm_f32_sk_fixup, dim3((unsigned)sk.tiles, 8), 256, 0, st, a,
+                       sk);
+  } else if (dma) {
     if (big) {
       const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128));
       constexpr int L = f32g::f32d_lds<128>();
@@ -764,4 +875,18 @@ extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const 
     else hipLaunchKernelGGL((f32g::k_gemm_f32<0, 64>), grid, 256, 0, st, a);
   }
   return check_launch("lcq_gemm_f32");
+}
+
+extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
+                            int64_t lda, const void* B, int64_t ldb, int bt, float beta, void* C,
+                            int64_t ldc, void* stream) {
+  return gemm_f32_impl(M, N, K, alpha, A, lda, B, ldb, bt, beta, C, ldc, nullptr, 0, stream);
+}
+
+extern "C" int lcq_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
+                               int64_t lda, const void* B, int64_t ldb, int bt, float beta,
+                               void* C, int64_t ldc, void* workspace, int64_t ws_bytes,
+                               void* stream) {
+  return gemm_f32_impl(M, N, K, alpha, A, lda, B, ldb, bt, beta, C, ldc, workspace, ws_bytes,
+                       stream);
 }

@@ -302,12 +302,17 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a, GArgs ga) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int split = wgid / a.ntiles;
+  // Splits run one after another in launch order, each spread over all 8 XCDs: XCD x (bid & 7)
+  // takes the contiguous valid-tile range [x q, x q + q) of every split (q = ceil(ntiles / 8)),
+  // so the 8 XCDs stream the SAME token slab at a time (its panels shared through the MALL)
+  // while each XCD's 32 CUs share 12 operand panels in its L2 (valid_tile chunks).
+  const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+  const int q = (a.ntiles + 7) >> 3;
+  const int split = j / q;
+  const int v = xcd * q + (j - split * q);
+  if (v >= a.ntiles || split >= a.ns) return;   // padding workgroups: before any barrier
   int ti, tj;
-  valid_tile(wgid - split * a.ntiles, a.nt, ti, tj);
+  valid_tile(v, a.nt, ti, tj);
   // this split's token group: its rows of x, tail and K-tile range
   int g = 0;
   while (g + 1 < ga.ng && split >= ga.split0[g + 1]) ++g;
@@ -562,13 +567,21 @@ using namespace lcq::hx;
 // GMAX groups launched together. It depends only on (group tokens, ic) -- never on how many
 // groups this process launches -- so a token-sharded rank splits its groups exactly as one GPU
 // does (the fp32 fold order per group is world-independent).
+static int forced_gns() {  // probe override of the per-group split count (read once)
+  static const int v = [] {
+    const char* e = getenv("LCQ_SYRK_GNS");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 static void plan_group(int64_t n, int64_t ic, int64_t& ns, int64_t& ktps, int64_t& nkt) {
   const int64_t icp = ceil_to(ic, ST);
   const int64_t nt = icp / ST, ntiles = nt * (nt + 1) / 2;
   nkt = ceil_to(n, SKT) / SKT;
   int64_t best_ns = 1;
   double best = 1e300;
-  for (int64_t c = 1; c <= 64; ++c) {
+  for (int64_t c = 1; c <= 64 && forced_gns() <= 0; ++c) {
     if (c > 1 && nkt / c < 8) break;
     const int64_t per = (nkt + c - 1) / c, cc = (nkt + per - 1) / per;
     const int64_t per_xcd = (ntiles * cc * GMAX + 7) / 8, rounds = (per_xcd + 31) / 32;
@@ -578,6 +591,7 @@ static void plan_group(int64_t n, int64_t ic, int64_t& ns, int64_t& ktps, int64_
       best_ns = cc;
     }
   }
+  if (forced_gns() > 0) best_ns = forced_gns() < nkt ? forced_gns() : nkt;
   ktps = (nkt + best_ns - 1) / best_ns;
   ns = nkt ? (nkt + ktps - 1) / ktps : 0;
 }
@@ -670,7 +684,8 @@ extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t 
   auto k = x_dtype == LCQ_F16 ? k_syrk_x<true> : k_syrk_x<false>;
   // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
-  hipLaunchKernelGGL(k, dim3((unsigned)(a.ntiles * a.ns)), 256, 2 * BUF, st, a, ga);
+  hipLaunchKernelGGL(k, dim3((unsigned)(8 * ((a.ntiles + 7) / 8) * a.ns)), 256, 2 * BUF, st, a,
+                     ga);
   int rc = check_launch("lcq_hessian_accum: syrk");
   if (rc) return rc;
   if (a.ns > 1) {
@@ -735,7 +750,8 @@ extern "C" int lcq_hessian_grouped(const void* x, int x_dtype, int64_t ic,
     auto k = x_dtype == LCQ_F16 ? k_syrk_x<true> : k_syrk_x<false>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               2 * BUF);
-    hipLaunchKernelGGL(k, dim3((unsigned)(a.ntiles * p.splits)), 256, 2 * BUF, st, a, p.ga);
+    hipLaunchKernelGGL(k, dim3((unsigned)(8 * ((a.ntiles + 7) / 8) * p.splits)), 256, 2 * BUF,
+                       st, a, p.ga);
     int rc = check_launch("lcq_hessian_grouped: syrk");
     if (rc) return rc;
   }

@@ -303,9 +303,19 @@ def gemm_f32(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, alpha: float =
         raise ValueError('gemm_f32: shape mismatch')
     if any(t.dtype != torch.float32 for t in (A, B, out)):
         raise ValueError('gemm_f32: fp32 operands')
+    ws_bytes = int(N.load().lcq_gemm_f32_workspace_bytes(M, n_, K)) if STREAM_K else 0
+    if ws_bytes:   # stream-K: 32 MB of partial tiles (from the graph's pool under capture)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=A.device)
+        N.call('lcq_gemm_f32_ws', M, n_, K, float(alpha), A.data_ptr(), _ld(A), B.data_ptr(),
+               _ld(B), int(b_trans), float(beta), out.data_ptr(), _ld(out), ws.data_ptr(),
+               ws_bytes, N.stream_of(A))
+        return out
     N.call('lcq_gemm_f32', M, n_, K, float(alpha), A.data_ptr(), _ld(A), B.data_ptr(), _ld(B),
            int(b_trans), float(beta), out.data_ptr(), _ld(out), N.stream_of(A))
     return out
+
+
+STREAM_K = True   # gemm_f32's stream-K grids (tests compare them with the tiled kernel)
 
 
 def chol_inv_tile(A: torch.Tensor, info: torch.Tensor, row0: int = 0,
@@ -860,8 +870,12 @@ def fp8_block_to_tensor(codes: torch.Tensor, scales_inv: torch.Tensor, block: in
 
 def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
                              fp8: torch.dtype = torch.float8_e4m3fn, qmax: float | None = None):
-    """Batched fp8_block_to_tensor: one launch pair for a list of block-fp8 weights (all on
-    one device). Returns (list of fp8 codes, fp32 scales [n])."""
+    """Batched fp8_block_to_tensor: block-fp8 weights (all on one device) requantized per
+    tensor. Returns (list of fp8 codes, fp32 scales [n]). The launch pair sizes its grid by the
+    largest tensor, so weights of very different sizes (a DeepSeek-V3 layer: o_proj 117 M
+    elements, kv_a 4 M, experts 15 M) go in size classes -- one launch pair per class of
+    tensors within 2x of each other -- instead of every small tensor carrying the largest one's
+    idle workgroups."""
     n = len(codes)
     if n == 0:
         return [], torch.empty(0)
@@ -869,19 +883,34 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
     codes = [c.contiguous() for c in codes]
     sinv = [s.contiguous().float() for s in scales_inv]
     outs = [torch.empty(c.shape, dtype=fp8, device=dev) for c in codes]
-    rec = []
-    for c, s, o in zip(codes, sinv, outs):
-        M, Nn = c.shape
-        if Nn % 8:
+    for c in codes:
+        if c.shape[1] % 8:
             raise ValueError('N must be a multiple of 8')
-        rec += [N.ptr(c), N.ptr(s), N.ptr(o), M, Nn]
     sc = torch.empty(n, dtype=torch.float32, device=dev)
     qmax = fp8_max(fp8) if qmax is None else float(qmax)
-    descs = torch.tensor(rec, dtype=torch.int64).to(dev, non_blocking=False)
-    ws = torch.empty(n * FP8_PARTIALS, dtype=torch.float32, device=dev)
-    N.call('lcq_fp8_block_to_tensor_many', n, N.ptr(descs), max(c.numel() for c in codes),
-           N.dt(codes[0].dtype), block, N.dt(fp8), qmax, 1e-5, 1, N.ptr(ws), N.ptr(sc),
-           N.stream_of(codes[0]))
+    order = sorted(range(n), key=lambda i: -codes[i].numel())
+    classes, cur = [], []
+    for i in order:
+        if cur and codes[i].numel() * 2 < codes[cur[0]].numel():
+            classes.append(cur)
+            cur = []
+        cur.append(i)
+    classes.append(cur)
+    ws = torch.empty(max(len(c) for c in classes) * FP8_PARTIALS, dtype=torch.float32,
+                     device=dev)
+    for cls in classes:
+        rec = []
+        for i in cls:
+            M, Nn = codes[i].shape
+            rec += [N.ptr(codes[i]), N.ptr(sinv[i]), N.ptr(outs[i]), M, Nn]
+        descs = torch.tensor(rec, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+        part = sc if len(classes) == 1 else torch.empty(len(cls), dtype=torch.float32,
+                                                        device=dev)
+        N.call('lcq_fp8_block_to_tensor_many', len(cls), N.ptr(descs), codes[cls[0]].numel(),
+               N.dt(codes[0].dtype), block, N.dt(fp8), qmax, 1e-5, 1, N.ptr(ws), N.ptr(part),
+               N.stream_of(codes[0]))
+        if len(classes) > 1:
+            sc[torch.tensor(cls, device=dev)] = part
     return outs, sc
 
 

@@ -238,14 +238,18 @@ def test_trailing_update(dev, rows, ic, c0, K, c2):
 
 
 @pytest.mark.parametrize('M,N,K', [(200, 136, 64), (1000, 700, 512), (2100, 2300, 1024),
-                                   (128, 4096, 4096)])
+                                   (128, 4096, 4096), (1792, 1792, 1792), (3000, 1900, 1792)])
 @pytest.mark.parametrize('bt', [False, True])
-def test_gemm_f32_dma(dev, M, N, K, bt):
+@pytest.mark.parametrize('stream_k', [True, False])
+def test_gemm_f32_dma(dev, M, N, K, bt, stream_k, monkeypatch):
     """lcq_gemm_f32's LDS-DMA kernel (16-byte aligned rows, K % 32 == 0: the recursion's
     products on 128-multiple Hessians) on sub-views of larger matrices: ragged M / N at both
     tile sizes, past-the-end rows / columns read as zero; against fp64 (same bound as above)
-    and deterministic."""
+    and deterministic -- the tiled grids and, where the last round of 256 workgroups would
+    run ragged (2100 x 2300, 1792^2, 3000 x 1900), the stream-K split with its k-ordered
+    fixup of the cut tiles."""
     from lightcompress_amd import ops
+    monkeypatch.setattr(ops, 'STREAM_K', stream_k)
     g = torch.Generator().manual_seed(M + 3 * N + K)
     big_a = torch.randn(M + 8, K + 8, generator=g)
     big_b = torch.randn((N + 4, K + 12) if bt else (K + 4, N + 12), generator=g)
