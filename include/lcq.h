@@ -514,7 +514,8 @@ int lcq_silu_mul(const void* gate, const void* up, int dtype, int64_t n, void* o
                  void* stream);
 
 /* LlamaRMSNorm.forward: out = weight * rnd(x_f32 * rsqrt(mean(x_f32^2) + eps)), one pass per
- * row; x, out [rows, H] contiguous, weight [H] (same dtype). */
+ * row (the row read once, held in registers); x, out [rows, H] contiguous, weight [H] (same
+ * dtype), H % 8 == 0, H <= 16384. */
 int lcq_rmsnorm(const void* x, const void* weight, int dtype, int64_t rows, int64_t H,
                 float eps, void* out, void* stream);
 
@@ -574,6 +575,14 @@ int lcq_act_static_hist_qparams(const void* const* segs, const int64_t* seg_lens
 int lcq_gemm(const void* a, int dtype, int64_t lda, int64_t m, int64_t k, int nseg,
              const void* const* b, const int64_t* b_rows, int64_t ldb, const void* const* bias,
              void* const* c, const int64_t* ldc, void* stream);
+
+/* C = rnd(res + rnd(A B^T + bias)) (one segment): the decoder block's `residual + o_proj(x)`
+ * and `h + down_proj(m)` (transformers LlamaDecoderLayer.forward, the calibration forwards of
+ * base_blockwise_quantization.py:367-381) with the add in the GEMM epilogue. res [M, N] (ldr),
+ * c [M, N] (ldc). */
+int lcq_gemm_residual(const void* a, int dtype, int64_t lda, int64_t m, int64_t k, const void* b,
+                      int64_t ldb, int64_t n, const void* bias, const void* res, int64_t ldr,
+                      void* c, int64_t ldc, void* stream);
 
 /* LlamaMLP's act_fn(gate_proj(x)) * up_proj(x) (SiLU) in one GEMM: h [m, n] =
  * rnd(rnd(silu(rnd(A . gate^T))) * rnd(A . up^T)); gate / up [n, k]; the two [m, n]

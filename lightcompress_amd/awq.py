@@ -312,6 +312,21 @@ class Awq(BaseBlockwiseQuantization):
             best_scales = awq_pick_best(best, best_scales)  # awq.py:255-273
         return best_scales
 
+    # quant_out False: block i + 1's input is block i's FLOAT output, so nothing of block
+    # i + 1 depends on block i's clip search -- it runs on a side stream while the next block's
+    # calibration forward and scale search run on the compute stream (the VALU-bound clip
+    # kernels fill the gaps of the MFMA-bound search). Same kernels on the same operands:
+    # bit-identical; joined before anything reads the clipped weights (_join_side_work).
+    overlap_clip = True
+
+    def _clip_async_ok(self):
+        # only inside run_block_loop, whose end joins the side stream (a caller driving
+        # block_opt itself may read the clipped weights right after it)
+        return (self.overlap_clip and getattr(self, '_in_block_loop', False)
+                and torch.cuda.is_available() and not self.quant_out
+                and self.parallel_mode() in ('single', 'shard_blocks')
+                and getattr(self.model, 'streamer', None) is None)
+
     @torch.no_grad()
     def block_transform(self, block, input_feat, block_kwargs):
         if self.trans:
@@ -320,7 +335,20 @@ class Awq(BaseBlockwiseQuantization):
             n_tok = self.config.get('calib', {}).get('seq_len', None)
             self.auto_clipper.reduce_across_ranks = self.parallel_mode() == 'replicate'
             self.auto_clipper.shard_rows = self.parallel_mode() == 'shard_search'
-            self.auto_clipper.run(block, self.block_idx, input_feat, n_sample_token=n_tok)
+            if not self._clip_async_ok():
+                self.auto_clipper.run(block, self.block_idx, input_feat, n_sample_token=n_tok)
+                return
+            if getattr(self, '_clip_stream', None) is None:
+                self._clip_stream = torch.cuda.Stream()
+            side = self._clip_stream
+            side.wait_stream(torch.cuda.current_stream())  # scaled weights + features ready
+            for feats in input_feat.values():  # freed by the block loop before the clip ends
+                for t in feats:
+                    for u in (t if isinstance(t, (tuple, list)) else (t,)):
+                        if torch.is_tensor(u) and u.is_cuda:
+                            u.record_stream(side)
+            with torch.cuda.stream(side):
+                self.auto_clipper.run(block, self.block_idx, input_feat, n_sample_token=n_tok)
 
     @torch.no_grad()
     def subset_transform(self, subset, input_feat, subset_kwargs):

@@ -119,6 +119,14 @@ class BlockwiseOpt:
         return P.row_shard(total, rank, world)
 
     def run_block_loop(self):
+        self._in_block_loop = True
+        try:
+            self._block_loop()
+        finally:
+            self._in_block_loop = False
+            self._join_side_work()
+
+    def _block_loop(self):
         mode = self.parallel_mode()
         rank, world = P.dist_world()
         own = getattr(self.model, 'ownership', None)
@@ -176,9 +184,17 @@ class BlockwiseOpt:
             st.evict(i, dirty=dirty)
 
     def _drain_blocks(self):
+        self._join_side_work()
         st = getattr(self.model, 'streamer', None)
         if st is not None:
             st.drain()
+
+    def _join_side_work(self):
+        """The compute stream waits for side-stream transforms (AWQ's overlapped clip search)
+        before anything reads the weights they wrote."""
+        st = getattr(self, '_clip_stream', None)
+        if st is not None:
+            torch.cuda.current_stream().wait_stream(st)
 
     def _handoff_ok(self):
         """The ring hand-off passes self.input['data'] as a list of tensors whose shapes every
@@ -219,6 +235,7 @@ class BlockwiseOpt:
     def materialize_blocks(self):
         """shard_blocks: publish every transformed float block from its owner (the state one
         GPU would hold after run_block_loop); a no-op otherwise or once done."""
+        self._join_side_work()
         pending = getattr(self, '_pending_owner', None)
         if not pending:
             return
@@ -798,6 +815,7 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                    'fake_quant_wo_kv': EffcientFakeQuantLinear, **_REALQUANT_LINEAR_MAP_}
         if quant_format not in mapping:
             raise NotImplementedError(f"Quant format '{quant_format}' is not implemented.")
+        self._join_side_work()
         module = mapping[quant_format]
         real = quant_format in _REALQUANT_LINEAR_MAP_
         params = self.get_replacement_params(quant_format, self.w_only)
@@ -855,6 +873,7 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
 
     @torch.no_grad()
     def save_model(self, path):
+        self._join_side_work()
         rank, world = P.dist_world()
         if getattr(self.model, 'ownership', None) is not None and world > 1:
             # every rank holds only its own blocks / units: per-rank safetensors shards and

@@ -76,19 +76,29 @@ __global__ void __launch_bounds__(256) k_silu_mul(const void* __restrict__ g, co
 // (the torch chain makes 6 passes: cast, pow, mean, rsqrt-mul, cast, weight-mul). The sum of
 // squares uses a fixed per-lane + tree order (deterministic; not torch's reduction order, so
 // outputs can differ from the unfused chain by one rounding of the variance).
-template <int DT>
+template <int DT, int CH>
 __global__ void __launch_bounds__(256) k_rmsnorm(const void* __restrict__ x,
                                                  const void* __restrict__ w, int64_t H,
                                                  float eps, void* __restrict__ out) {
+  // the row's CH 2048-element slices stay in registers between the sum and the scaling (one
+  // HBM read of x); all loads are issued before the first FMA
   __shared__ float red[4];
   const int64_t row = blockIdx.x;
   const int64_t base = row * H;
-  float ss = 0.f;
-  for (int64_t c = threadIdx.x * 8; c < H; c += 256 * 8) {
-    float v[8];
-    ld8<DT>(x, base + c, v);
+  float v[CH][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ss = __fadd_rn(ss, __fmul_rn(v[j], v[j]));
+  for (int k = 0; k < CH; ++k) {
+    const int64_t c = threadIdx.x * 8 + (int64_t)k * 2048;
+    if (c < H) ld8<DT>(x, base + c, v[k]);
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int64_t c = threadIdx.x * 8 + (int64_t)k * 2048;
+    if (c < H) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss = __fadd_rn(ss, __fmul_rn(v[k][j], v[k][j]));
+    }
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) ss = __fadd_rn(ss, __shfl_xor(ss, m, 64));
@@ -97,13 +107,16 @@ __global__ void __launch_bounds__(256) k_rmsnorm(const void* __restrict__ x,
   const float var = __fdiv_rn(__fadd_rn(__fadd_rn(red[0], red[1]), __fadd_rn(red[2], red[3])),
                               (float)H);
   const float r = rsqrtf(__fadd_rn(var, eps));
-  for (int64_t c = threadIdx.x * 8; c < H; c += 256 * 8) {
-    float v[8], g[8], o[8];
-    ld8<DT>(x, base + c, v);
-    ld8<DT>(w, c, g);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = rnd<DT>(g[j] * rnd<DT>(v[j] * r));
-    st8<DT>(out, base + c, o);
+  for (int k = 0; k < CH; ++k) {
+    const int64_t c = threadIdx.x * 8 + (int64_t)k * 2048;
+    if (c < H) {
+      float g[8], o[8];
+      ld8<DT>(w, c, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = rnd<DT>(g[j] * rnd<DT>(v[k][j] * r));
+      st8<DT>(out, base + c, o);
+    }
   }
 }
 
@@ -116,11 +129,29 @@ extern "C" int lcq_rmsnorm(const void* x, const void* weight, int dtype, int64_t
   LCQ_REQUIRE(dtype == LCQ_BF16 || dtype == LCQ_F16, "dtype must be bf16 or fp16");
   LCQ_REQUIRE(rows > 0 && rows <= 0x7fffffffLL && H > 0 && H % 8 == 0,
               "H must be a positive multiple of 8");
+  LCQ_REQUIRE(H <= 8 * 2048, "H must be <= 16384");
   hipStream_t st = as_stream(stream);
-  if (dtype == LCQ_BF16)
-    hipLaunchKernelGGL(k_rmsnorm<LCQ_BF16>, dim3((unsigned)rows), 256, 0, st, x, weight, H, eps, out);
-  else
-    hipLaunchKernelGGL(k_rmsnorm<LCQ_F16>, dim3((unsigned)rows), 256, 0, st, x, weight, H, eps, out);
+  const int ch = (int)((H + 2047) / 2048);
+#define LCQ_RMS(DT, CH) \
+  hipLaunchKernelGGL((k_rmsnorm<DT, CH>), dim3((unsigned)rows), 256, 0, st, x, weight, H, eps, out)
+#define LCQ_RMS_CH(DT)                             \
+  switch (ch) {                                    \
+    case 1: LCQ_RMS(DT, 1); break;                 \
+    case 2: LCQ_RMS(DT, 2); break;                 \
+    case 3: LCQ_RMS(DT, 3); break;                 \
+    case 4: LCQ_RMS(DT, 4); break;                 \
+    case 5: LCQ_RMS(DT, 5); break;                 \
+    case 6: LCQ_RMS(DT, 6); break;                 \
+    case 7: LCQ_RMS(DT, 7); break;                 \
+    default: LCQ_RMS(DT, 8); break;                \
+  }
+  if (dtype == LCQ_BF16) {
+    LCQ_RMS_CH(LCQ_BF16)
+  } else {
+    LCQ_RMS_CH(LCQ_F16)
+  }
+#undef LCQ_RMS_CH
+#undef LCQ_RMS
   return check_launch("lcq_rmsnorm");
 }
 

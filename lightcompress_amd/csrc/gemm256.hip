@@ -17,6 +17,8 @@
 //               h = rnd(rnd(g / (1 + exp(-g))) * u) with g = rnd(acc_gate), u = rnd(acc_up)
 //               (LlamaMLP act_fn(gate_proj(x)) * up_proj(x), the two [M, I] projections are
 //               never written)
+//   EPI_RESID   C[t, c] = rnd(res[t, c] + rnd(acc + bias)): a block's `residual + o_proj(x)` /
+//               `h + down_proj(m)` (the residual read through the ref pointer, one segment)
 //   EPI_SQDIFF  out = rnd(acc + bias) is never written: d = rnd(ref - out), the tile's
 //               sum of fp32 d*d goes to an fp64 partial per tile; k_loss_reduce sums the
 //               partials in tile order (deterministic) and writes sum / numel to a device slot
@@ -50,7 +52,7 @@ constexpr int SKT = 64;            // K-tile
 constexpr int HALF_B = 16384;      // 128 rows x 64 k x 2 B
 constexpr int BUF_B = 4 * HALF_B;  // A_lo, A_hi, B_lo, B_hi
 enum { H_ALO = 0, H_AHI = 1, H_BLO = 2, H_BHI = 3 };
-enum { EPI_STORE = 0, EPI_SILU = 1, EPI_SQDIFF = 2 };
+enum { EPI_STORE = 0, EPI_SILU = 1, EPI_SQDIFF = 2, EPI_RESID = 3 };
 constexpr int MAXSEG = 3;
 
 struct Args {
@@ -392,11 +394,11 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
         dst[n] = (full_n || col0 + n * 16 < a.n) ? *reinterpret_cast<const uint2*>(rrow + n * 16)
                                                  : make_uint2(0u, 0u);
     };
-    if constexpr (EPI == EPI_SQDIFF) load_ref(0, rv[0]);
+    if constexpr (EPI == EPI_SQDIFF || EPI == EPI_RESID) load_ref(0, rv[0]);
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
-      if constexpr (EPI == EPI_SQDIFF) {
+      if constexpr (EPI == EPI_SQDIFF || EPI == EPI_RESID) {
         if (m + 1 < 8) load_ref(m + 1, rv[(m + 1) & 1]);
       }
       if (trow >= a.m) continue;
@@ -406,7 +408,16 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           o[n][j] = rnd<DT>(bp != nullptr ? __fadd_rn(acc[m][n][j], bias[n][j]) : acc[m][n][j]);
-      if constexpr (EPI == EPI_STORE) {
+      if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          float r[4];
+          unpack4<DT>(rv[m & 1][n], r);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[n][j] = rnd<DT>(__fadd_rn(r[j], o[n][j]));
+        }
+      }
+      if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
         uint16_t* crow = a.c[s] + trow * a.ldc[s] + lcol0;
         if (a.wide && full_n) {
           uint16_t* cpair = crow - fq * 4 + poff;
@@ -621,6 +632,31 @@ extern "C" int lcq_gemm(const void* a, int dtype, int64_t lda, int64_t m, int64_
     if (!aligned16(c[s]) || ldc[s] % 8 != 0) g.wide = 0;
   plan(g, ST);
   return dispatch<EPI_STORE>(dtype, g, as_stream(stream));
+}
+
+extern "C" int lcq_gemm_residual(const void* a, int dtype, int64_t lda, int64_t m, int64_t k,
+                                 const void* b, int64_t ldb, int64_t n, const void* bias,
+                                 const void* res, int64_t ldr, void* c, int64_t ldc,
+                                 void* stream) {
+  int rc = check_common(dtype, a, lda, m, k, ldb);
+  if (rc) return rc;
+  LCQ_REQUIRE(n > 0 && n % 16 == 0, "N must be a multiple of 16");
+  LCQ_REQUIRE(b && aligned16(b) && res && aligned8(res) && ldr >= n && ldr % 4 == 0,
+              "weight / residual pointers, ldr >= N multiple of 4");
+  LCQ_REQUIRE(c && aligned8(c) && ldc >= n && ldc % 4 == 0, "c pointer, ldc >= N multiple of 4");
+  Args g{};
+  g.a = reinterpret_cast<const uint16_t*>(a);
+  g.lda = lda; g.m = m; g.k = k; g.ldb = ldb; g.n = n; g.nseg = 1;
+  g.b[0] = reinterpret_cast<const uint16_t*>(b);
+  g.bend[0] = n;
+  g.bias[0] = reinterpret_cast<const uint16_t*>(bias);
+  g.c[0] = reinterpret_cast<uint16_t*>(c);
+  g.ldc[0] = ldc;
+  g.ref = reinterpret_cast<const uint16_t*>(res);
+  g.ldr = ldr;
+  g.wide = aligned16(c) && ldc % 8 == 0;
+  plan(g, ST);
+  return dispatch<EPI_RESID>(dtype, g, as_stream(stream));
 }
 
 extern "C" int lcq_gemm_silu_mul(const void* a, int dtype, int64_t lda, int64_t m, int64_t k,

@@ -134,13 +134,29 @@ def _fused_rmsnorm_forward(self, hidden_states):
     a fixed order of its own)."""
     from . import ops
     if (hidden_states.is_cuda and hidden_states.dtype in (torch.bfloat16, torch.float16)
-            and self.weight.dtype == hidden_states.dtype and hidden_states.shape[-1] % 8 == 0):
+            and self.weight.dtype == hidden_states.dtype and hidden_states.shape[-1] % 8 == 0
+            and hidden_states.shape[-1] <= 16384):
         return ops.rmsnorm(hidden_states, self.weight, self.variance_epsilon)
     input_dtype = hidden_states.dtype
     h = hidden_states.to(torch.float32)
     variance = h.pow(2).mean(-1, keepdim=True)
     h = h * torch.rsqrt(variance + self.variance_epsilon)
     return self.weight * h.to(input_dtype)
+
+
+def _proj_residual(mod, x, res):
+    """res + mod(x) (the decoder block's residual adds after o_proj and down_proj) with the
+    add in the GEMM epilogue when mod is a linear the GEMM takes and carries no hooks, or only
+    input-capture hooks (fired first, as the module call would); otherwise the module runs."""
+    from . import ops
+    if _input_only_hooked(mod):
+        w, b = _linear_wb(mod)
+        if (ops.gemm_supported(x, w) and res.dtype == x.dtype
+                and res.shape[:-1] == x.shape[:-1] and res.shape[-1] == w.shape[0]
+                and (b is None or b.dtype == x.dtype)):
+            _fire_input_hooks(mod, x)
+            return ops.linear_residual(x, w, res, b)
+    return res + mod(x)
 
 
 def _mkey(*mods):
@@ -252,7 +268,8 @@ def _staged_decoder_forward(self, hidden_states, attention_mask=None, position_i
                                      position_embeddings, attention_mask,
                                      position_ids=position_ids, use_cache=use_cache, **kwargs))
     key = key + _mkey(attn.o_proj)
-    h = _stage(cache, 'h', key, (attn.o_proj,), lambda: hidden_states + attn.o_proj(core))
+    h = _stage(cache, 'h', key, (attn.o_proj,),
+               lambda: _proj_residual(attn.o_proj, core, hidden_states))
     key = key + _mkey(self.post_attention_layernorm, mlp.gate_proj, mlp.up_proj)
 
     def _mlp_in():
@@ -260,7 +277,7 @@ def _staged_decoder_forward(self, hidden_states, attention_mask=None, position_i
 
     m = _stage(cache, 'm', key, (self.post_attention_layernorm, mlp.gate_proj, mlp.up_proj),
                _mlp_in)
-    return h + mlp.down_proj(m)
+    return _proj_residual(mlp.down_proj, m, h)
 
 
 def clear_stage_cache(block: nn.Module):

@@ -520,6 +520,30 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
     return linear_multi(x, [weight], None if bias is None else [bias])[0]
 
 
+def linear_residual(x: torch.Tensor, weight: torch.Tensor, residual: torch.Tensor,
+                    bias=None) -> torch.Tensor:
+    """residual + F.linear(x, weight, bias) with the add in the GEMM epilogue (lcq_gemm_residual:
+    the same two roundings as the torch expression)."""
+    x2 = _rows2d(x)
+    M, K = x2.shape
+    Nn = weight.shape[0]
+    r2 = residual.reshape(-1, Nn)
+    if r2.shape[0] != M or r2.dtype != x.dtype:
+        raise ValueError('residual must be [.., N] matching x rows and dtype')
+    if r2.stride(-1) != 1 or r2.stride(0) % 4 != 0 or r2.data_ptr() % 8 != 0:
+        r2 = r2.contiguous()
+    if bias is not None and (bias.dtype != x.dtype or bias.numel() != Nn
+                             or not bias.is_contiguous()):
+        raise ValueError('bias must be contiguous [N] in the input dtype')
+    out = torch.empty((M, Nn), dtype=x.dtype, device=x.device)
+    N.call('lcq_gemm_residual', N.ptr_strided(x2), N.dt(x2), x2.stride(0), M, K,
+           weight.data_ptr(), weight.stride(0), Nn, None if bias is None else N.ptr(bias),
+           N.ptr_strided(r2), r2.stride(0), N.ptr(out), Nn, N.stream_of(x2))
+    N.note_work('lcq_gemm_residual', 2.0 * M * K * Nn)
+    N.note_bytes('lcq_gemm_residual', 2.0 * (M * K + Nn * K + 2 * M * Nn))
+    return out.view(*x.shape[:-1], Nn)
+
+
 def linear_silu_mul(x: torch.Tensor, gate_w: torch.Tensor, up_w: torch.Tensor) -> torch.Tensor:
     """act_fn(gate_proj(x)) * up_proj(x) (SiLU, no bias) in one GEMM; the [.., I] projections
     are never materialised."""
@@ -593,8 +617,7 @@ def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, 
         return _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym,
                                     version=2)
     T = x.shape[0]
-    factors = torch.tensor([float(1 - i / n_grid) for i in range(nsteps)], dtype=torch.float32,
-                           device=w.device)
+    factors = _const_f32([float(1 - i / n_grid) for i in range(nsteps)], w.device)
     ng = ic // group
     bmax = torch.empty((oc, ng, 1), dtype=w.dtype, device=w.device)
     bmin = torch.empty((oc, ng, 1), dtype=w.dtype, device=w.device)
@@ -603,13 +626,26 @@ def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, 
     msteps, mp, norm = 0, None, 0.0
     if mse is not None:
         msteps, grid, norm = int(mse[0]), float(mse[1]), float(mse[2])
-        mp = torch.tensor([float(1 - i / grid) for i in range(msteps)], dtype=torch.float32,
-                          device=w.device)
+        mp = _const_f32([float(1 - i / grid) for i in range(msteps)], w.device)
     N.call('lcq_auto_clip_search_act', N.ptr(w.contiguous()), N.ptr(x.contiguous()),
            N.ptr(qx.contiguous() if qx is not None else None), N.dt(w), oc, ic, T, int(group),
            int(nsteps), N.ptr(factors), int(qmin), int(qmax), int(sym), int(clip_sym), msteps,
            N.ptr(mp), norm, N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
     return bmax, bmin
+
+
+_CONST_CACHE: dict = {}
+
+
+def _const_f32(values, device) -> torch.Tensor:
+    """A small constant fp32 vector on the device, uploaded once per (device, values): a
+    fresh torch.tensor(list, device=...) is a pageable copy that blocks the host until the
+    stream drains (the overlapped clip search would lose its overlap to it)."""
+    key = (torch.device(device).index, tuple(values))
+    t = _CONST_CACHE.get(key)
+    if t is None:
+        t = _CONST_CACHE[key] = torch.tensor(list(values), dtype=torch.float32, device=device)
+    return t
 
 
 def _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym, fp8=None,
@@ -619,8 +655,7 @@ def _auto_clip_search_pc(w, x, qx, nsteps, n_grid, qmin, qmax, sym, clip_sym, fp
     T = x.shape[0]
     if x.dtype != w.dtype:
         raise ValueError('auto-clip: x and w must share the model dtype')
-    factors = torch.tensor([float(1 - i / n_grid) for i in range(nsteps)], dtype=torch.float32,
-                           device=w.device)
+    factors = _const_f32([float(1 - i / n_grid) for i in range(nsteps)], w.device)
     bmax = torch.empty((oc, 1, 1), dtype=w.dtype, device=w.device)
     bmin = torch.empty((oc, 1, 1), dtype=w.dtype, device=w.device)
     wsb = N.load().lcq_auto_clip_pc_workspace_bytes(oc, T, int(nsteps))
@@ -898,19 +933,23 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
     classes.append(cur)
     ws = torch.empty(max(len(c) for c in classes) * FP8_PARTIALS, dtype=torch.float32,
                      device=dev)
+    flat = [i for cls in classes for i in cls]    # class order
+    rec = []
+    for i in flat:
+        M, Nn = codes[i].shape
+        rec += [N.ptr(codes[i]), N.ptr(sinv[i]), N.ptr(outs[i]), M, Nn]
+    # every class's descriptors (and the class order, to put the scales back) in ONE upload
+    upload = torch.tensor(rec + flat, dtype=torch.int64).to(dev)
+    descs = upload[:5 * n]
+    sc_cls = sc if len(classes) == 1 else torch.empty(n, dtype=torch.float32, device=dev)
+    off = 0
     for cls in classes:
-        rec = []
-        for i in cls:
-            M, Nn = codes[i].shape
-            rec += [N.ptr(codes[i]), N.ptr(sinv[i]), N.ptr(outs[i]), M, Nn]
-        descs = torch.tensor(rec, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
-        part = sc if len(classes) == 1 else torch.empty(len(cls), dtype=torch.float32,
-                                                        device=dev)
-        N.call('lcq_fp8_block_to_tensor_many', len(cls), N.ptr(descs), codes[cls[0]].numel(),
-               N.dt(codes[0].dtype), block, N.dt(fp8), qmax, 1e-5, 1, N.ptr(ws), N.ptr(part),
-               N.stream_of(codes[0]))
-        if len(classes) > 1:
-            sc[torch.tensor(cls, device=dev)] = part
+        N.call('lcq_fp8_block_to_tensor_many', len(cls), descs.data_ptr() + off * 40,
+               codes[cls[0]].numel(), N.dt(codes[0].dtype), block, N.dt(fp8), qmax, 1e-5, 1,
+               N.ptr(ws), sc_cls.data_ptr() + off * 4, N.stream_of(codes[0]))
+        off += len(cls)
+    if len(classes) > 1:
+        sc[upload[5 * n:]] = sc_cls
     return outs, sc
 
 

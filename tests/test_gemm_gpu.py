@@ -175,3 +175,19 @@ def test_gemm_rejects_bad_shapes():
     assert not ops.gemm_supported(x, w)
     with pytest.raises(ValueError):
         ops.linear(x, w)
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('M,N,K', [(2048, 4096, 4096), (777, 512, 1024), (300, 272, 192)])
+def test_linear_residual_equals_add(M, N, K, dtype):
+    """lcq_gemm_residual (the block's residual + o_proj / down_proj in the epilogue) equals the
+    separate residual + linear bit for bit: the same two roundings, with and without bias."""
+    g = torch.Generator(device=DEV).manual_seed(M + 5 * N + K)
+    x = torch.randn(M, K, generator=g, device=DEV).to(dtype)
+    w = (torch.randn(N, K, generator=g, device=DEV) * 0.02).to(dtype)
+    r = torch.randn(M, N, generator=g, device=DEV).to(dtype)
+    b = (torch.randn(N, generator=g, device=DEV) * 0.1).to(dtype)
+    for bias in (None, b):
+        got = ops.linear_residual(x, w, r, bias)
+        ref = r + ops.linear(x, w, bias)
+        assert torch.equal(got.view(torch.int16), ref.view(torch.int16))

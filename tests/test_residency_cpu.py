@@ -129,13 +129,19 @@ def test_materialize_owned_loads_only_own_units():
         assert x0 and x1
 
 
-def _deploy(rank, world, materialize, path, fmt='vllm_quant'):
+RECIPES = {
+    # rtn_w_only_dsv3-shaped (int4 g64, packed) on the tiny DeepSeek-V3
+    'DeepseekV3': {'weight': {'bit': 4, 'symmetric': True, 'granularity': 'per_group',
+                              'group_size': 64, 'need_pack': True}},
+    # BASELINE config 1's recipe on the tiny OPT: w8 per-channel
+    'Opt': {'weight': {'bit': 8, 'symmetric': True, 'granularity': 'per_channel'}},
+}
+
+
+def _deploy(rank, world, materialize, path, fmt='vllm_quant', family='DeepseekV3'):
     from lightcompress_amd.pipeline import build_algo, build_model
     _cpu_packers()
-    cfg = _config('DeepseekV3', materialize=materialize,
-                  extra_quant={'weight': {'bit': 4, 'symmetric': True,
-                                          'granularity': 'per_group', 'group_size': 64,
-                                          'need_pack': True}})
+    cfg = _config(family, materialize=materialize, extra_quant=RECIPES[family])
     model = build_model(cfg, device='cpu')
     algo = build_algo(model, cfg, None)
     assert algo.parallel_mode() == ('single' if world == 1 else 'shard_units')
@@ -152,10 +158,11 @@ def _deploy(rank, world, materialize, path, fmt='vllm_quant'):
             for n, t in [*b.named_parameters(), *b.named_buffers()]}
 
 
-def test_shard_units_deploy_matches_single_process(tmp_path):
-    single = _deploy(0, 1, 'all', None)
-    res = run2(functools.partial(_deploy, materialize='all', path=None))
-    assert any('weight_packed' in k for k in single)
+@pytest.mark.parametrize('family', ['DeepseekV3', 'Opt'])
+def test_shard_units_deploy_matches_single_process(tmp_path, family):
+    single = _deploy(0, 1, 'all', None, family=family)
+    res = run2(functools.partial(_deploy, materialize='all', path=None, family=family))
+    assert any('weight_packed' in k or k.endswith('.weight') for k in single)
     for r in (0, 1):
         assert res[r].keys() == single.keys()
         for k in single:
