@@ -43,6 +43,8 @@ class Awq(BaseBlockwiseQuantization):
         self._org_capture_active = False
         self.org_reuse_stats = {'reused': 0, 'recomputed': 0}
         self.reuse_org = True
+        if special.get('overlap_clip') is not None:
+            self.overlap_clip = bool(special['overlap_clip'])
 
     # -- original inspect outputs from the block's own forward ------------------------------
     # search_scale_subset starts from the inspect module's output on the captured input
@@ -313,11 +315,14 @@ class Awq(BaseBlockwiseQuantization):
         return best_scales
 
     # quant_out False: block i + 1's input is block i's FLOAT output, so nothing of block
-    # i + 1 depends on block i's clip search -- it runs on a side stream while the next block's
-    # calibration forward and scale search run on the compute stream (the VALU-bound clip
-    # kernels fill the gaps of the MFMA-bound search). Same kernels on the same operands:
-    # bit-identical; joined before anything reads the clipped weights (_join_side_work).
-    overlap_clip = True
+    # i + 1 depends on block i's clip search -- with `special.overlap_clip: True` it runs on a
+    # side stream while the next block's calibration forward and scale search run on the
+    # compute stream. Same kernels on the same operands: bit-identical; joined before anything
+    # reads the clipped weights (_join_side_work). Off by default: measured on MI355X the two
+    # time-share the CUs rather than overlap (the projection GEMM holds all 512 registers of
+    # its one wave per SIMD, so no clip wave fits beside it): 692.4 vs 698.9 ms per Llama-3-8B
+    # block, and the per-launch GEMM times (the roofline) then include the contention.
+    overlap_clip = False
 
     def _clip_async_ok(self):
         # only inside run_block_loop, whose end joins the side stream (a caller driving

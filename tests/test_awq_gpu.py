@@ -277,8 +277,8 @@ def test_auto_clip_pc_llama_shape(dev):
 
 def test_overlapped_clip_bit_identical(dev, monkeypatch):
     """quant_out False: block i's auto-clip search runs on a side stream while block i + 1's
-    calibration forward and scale search run (Awq.overlap_clip); the deployed weights equal
-    the serial run's bit for bit."""
+    calibration forward and scale search run (Awq.overlap_clip, special.overlap_clip); the
+    deployed weights equal the serial run's bit for bit."""
     from transformers import LlamaConfig
 
     from lightcompress_amd.awq import Awq
