@@ -632,7 +632,7 @@ def bench_fp8(args, rank, world, dev):
     n_units, elems = len(mine), float(sum(mine))
     fwd_w = [(m.weight.data, m.weight_scale_inv.data)
              for n, m in model.get_block_linears(model.get_blocks()[0]).items()
-             if '.experts.' in n and not m.weight.is_meta][:12]
+             if '.experts.' in n and not m.weight.is_meta][:48]
     fwd_w = [(c.clone(), s.clone()) for c, s in fwd_w]
     timer = _native.KernelTimer()
     sync_barrier(world)
@@ -673,50 +673,87 @@ def bench_fp8(args, rank, world, dev):
     return out
 
 
+def _fp8_expert_list(weights, dev):
+    """An ExpertList (deepseekv3.py) of DeepseekV3MLP experts whose gate / up / down are
+    LlmcFp8Linear modules holding `weights` (consecutive (w, scale_inv) triples)."""
+    from transformers.models.deepseek_v3 import modeling_deepseek_v3 as md
+
+    from lightcompress_amd.deepseekv3 import ExpertList
+    from lightcompress_amd.module_utils import LlmcFp8Linear
+    inter, H = weights[0][0].shape
+    cfg = md.DeepseekV3Config(hidden_size=H, intermediate_size=inter, hidden_act='silu')
+    experts = ExpertList()
+    for e in range(len(weights) // 3):
+        with torch.device('meta'):
+            mlp = md.DeepseekV3MLP(cfg, intermediate_size=inter)
+        for p, (w, s) in zip(('gate_proj', 'up_proj', 'down_proj'), weights[3 * e:3 * e + 3]):
+            m = LlmcFp8Linear(w.shape[1], w.shape[0], False, 128)
+            m.weight = torch.nn.Parameter(w, requires_grad=False)
+            m.weight_scale_inv = torch.nn.Parameter(s, requires_grad=False)
+            setattr(mlp, p, m)
+        experts.append(mlp)
+    return experts.to(dev)
+
+
 def bench_fp8_forward(args, weights, dev, world):
-    """Calibration forward of block-fp8 expert linears (LlmcFp8Linear.forward =
-    block_wise_fp8_forward_func, module_utils.py:41-46, 244-262): act_quant + the block-scaled
-    fp8 GEMM (kernel.py:141-242) for args.fp8_tokens tokens per expert linear. Every rank runs
-    its own experts (weak scaling); linears_per_s is the job total over ranks.
-    Roofline: 2*M*N*K flops per lcq_fp8_gemm launch over its HIP-event time vs fp8 dense peak."""
+    """Calibration forward of the routed block-fp8 experts of a DeepSeek-V3 MoE layer
+    (the experts call of DeepseekV3MoE.forward -> per expert LlmcFp8Linear.forward =
+    block_wise_fp8_forward_func, module_utils.py:41-46, 244-262: act_quant + the block-scaled
+    fp8 GEMM, kernel.py:141-242): 2 x args.fp8_tokens tokens routed top-8 over 16 experts
+    (2048 tokens per expert on average, ragged), through ExpertList's grouped path (one
+    lcq_fp8_gemm_grouped launch per projection). The reference's per-expert loop over the same
+    routing is timed beside it (`loop`). Every rank runs its own experts (weak scaling);
+    linears_per_s is the job total over ranks.
+    Roofline: 2 * rows * N * K flops per lcq_fp8_gemm_grouped launch (rows = tokens x top-k)
+    over its HIP-event time vs the fp8 dense peak."""
     from lightcompress_amd import _native
-    from lightcompress_amd.module_utils import block_wise_fp8_forward_func
-    T = args.fp8_tokens
+    E = len(weights) // 3
+    k = min(8, E)
+    T = 2 * args.fp8_tokens * E // 16
+    experts = _fp8_expert_list(weights, dev)
+    inter, H = weights[0][0].shape
     g = torch.Generator(device=dev).manual_seed(5)
-    xs = {}
-    for c, _ in weights:
-        K = c.shape[1]
-        if K not in xs:
-            xs[K] = (torch.randn(T, K, device=dev, generator=g)).to(torch.bfloat16)
+    x = torch.randn(T, H, device=dev, generator=g).to(torch.bfloat16)
+    idx = torch.argsort(torch.rand(T, E, device=dev, generator=g), dim=1)[:, :k].contiguous()
+    w = torch.softmax(torch.randn(T, k, device=dev, generator=g), dim=1)
+    assert experts._grouped_fp8_ok(x), 'grouped fp8 expert path not taken'
 
-    def step():
-        for c, s in weights:
-            block_wise_fp8_forward_func(xs[c.shape[1]], c, s, 128, None)
+    def run(grouped):
+        if not grouped:
+            experts._grouped_fp8_ok = lambda x: False   # the reference's per-expert loop
+        try:
+            experts(x, idx, w)
+            timer = _native.KernelTimer()
+            sync_barrier(world)
+            t0 = time.perf_counter()
+            with timer:
+                for _ in range(args.steps):
+                    experts(x, idx, w)
+            sync_barrier(world)
+            return max_over_ranks(time.perf_counter() - t0, world, dev), timer.summary()
+        finally:
+            experts.__dict__.pop('_grouped_fp8_ok', None)
 
-    step()
-    timer = _native.KernelTimer()
-    sync_barrier(world)
-    t0 = time.perf_counter()
-    with timer:
-        for _ in range(args.steps):
-            step()
-    sync_barrier(world)
-    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
-    kern = timer.summary()
-    flops = sum(2.0 * T * c.shape[0] * c.shape[1] for c, _ in weights)
-    out = {'linears_per_s': round(len(weights) * args.steps * world / elapsed, 1),
+    loop_elapsed, _ = run(False)
+    elapsed, kern = run(True)
+    flops = 2.0 * T * k * 3 * inter * H   # per step: gate, up, down over all routed rows
+    out = {'linears_per_s': round(3 * E * args.steps * world / elapsed, 1),
            'ms_per_step': round(elapsed / args.steps * 1e3, 3),
-           'workload': (f'{len(weights) // 3} DSv3 block-fp8 experts x 3 linears (2048x7168 / '
-                        f'7168x2048) per rank, {T} bf16 tokens each: act_quant + fp8 GEMM + bf16'),
+           'loop_ms_per_step': round(loop_elapsed / args.steps * 1e3, 3),
+           'workload': (f'{E} DSv3 block-fp8 routed experts (gate/up {inter}x{H}, down '
+                        f'{H}x{inter}) per rank, {T} bf16 tokens routed top-{k} '
+                        f'(~{T * k // E} per expert): ExpertList forward, grouped (loop = the '
+                        'per-expert act_quant + fp8 GEMM loop)'),
            'lcq_kernels': kernel_table(kern, elapsed)}
-    t = kern.get('lcq_fp8_gemm')
+    t = kern.get('lcq_fp8_gemm_grouped')
     if t:
         tf = flops * args.steps / (t['total_ms'] * 1e-3) / 1e12
-        out['roofline'] = {'kernel': 'lcq_fp8_gemm (k_fp8_gemm2 on grids of >= 64 256x256 tiles, '
-                                     'split-K below 224; else k_fp8_gemm)', 'bound': 'mfma',
+        traffic, src = pmc_traffic('fp8', 'k_fp8_gemm2_grouped')
+        out['roofline'] = {'kernel': 'lcq_fp8_gemm_grouped (k_fp8_gemm2_grouped: 256x256 '
+                                     'tiles of every expert in one launch)', 'bound': 'mfma',
                            'achieved': round(tf, 1), 'peak': PEAK_FP8_TFLOPS, 'unit': 'TFLOP/s',
-                           'frac': round(tf / PEAK_FP8_TFLOPS, 4), 'traffic': None,
-                           'flops_per_launch': flops / len(weights),
+                           'frac': round(tf / PEAK_FP8_TFLOPS, 4), 'traffic': traffic,
+                           'traffic_source': src, 'flops_per_launch': flops / 3,
                            'avg_launch_ms': round(t['avg_ms'], 4)}
     return out
 

@@ -478,6 +478,34 @@ int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const void* b_s,
                  int64_t N, int64_t K, void* c, int c_dtype, void* workspace, int64_t ws_bytes,
                  void* stream);
 
+/* Grouped block-scaled FP8 GEMM: one launch for the G routed experts of an MoE projection
+ * (replaces the per-expert block_wise_fp8_forward_func calls of the expert loop, reference
+ * models/deepseekv3.py MoE forward -> module_utils.py:41-46 per expert; kernel.py:141-242 per
+ * call). The `rows` GEMM rows are the token slots sorted by expert, group g's rows
+ * [row_off[g], row_off[g + 1]) (row_off: DEVICE int64 [G + 1], so the routing is never read on
+ * the host). a: e4m3 with a_s fp32 [.., K/128] (act_quant) -- `a_rows_total` rows, and sorted
+ * row i is a row a_rows[i] (DEVICE int64 [rows]: the token gather happens inside the kernel,
+ * act_quant runs once per token), or a_rows null and a already sorted (a_rows_total == rows).
+ * wtab: DEVICE int64 [nsets][G][2] = (weight [N, K] e4m3 16-byte aligned, block scales fp32
+ * [ceil(N/128), K/128]) addresses; nsets 1 or 2 (gate and up of the same rows in one launch).
+ * c [nsets][rows][N] (c_dtype). Every row equals what lcq_fp8_gemm computes for it on an
+ * unsplit 256^2 plan. `workspace`: lcq_fp8_gemm_grouped_workspace_bytes(rows, G, N, K). */
+int64_t lcq_fp8_gemm_grouped_workspace_bytes(int64_t rows, int64_t G, int64_t N, int64_t K);
+int lcq_fp8_gemm_grouped(const void* a, const void* a_s, int64_t a_rows_total,
+                         const int64_t* a_rows, int64_t rows, const int64_t* row_off,
+                         const int64_t* wtab, int64_t G, int nsets, int64_t N, int64_t K,
+                         void* c, int c_dtype, void* workspace, int64_t ws_bytes, void* stream);
+
+/* MoE combine (the expert loop's `out.index_add_(0, tok, (h_e * w).to(out.dtype))` over hit
+ * experts in ascending index; reference models/deepseekv3.py MoE forward): out [T, H] bf16,
+ * out[t] = fold over token t's k slots in ascending expert[t k + j] of
+ * acc = rnd(acc + rnd(y[slot_row[t k + j]] * w[t k + j])), acc from 0, rnd = bf16 RNE; y bf16
+ * [.., H] (the grouped GEMM's sorted rows), w fp32 / bf16 (w_dtype) [T, k]; k <= 16,
+ * H % 8 == 0, y / out 16-byte aligned. */
+int lcq_moe_combine(const void* y, const int64_t* slot_row, const int64_t* expert,
+                    const void* w, int w_dtype, int64_t T, int k, int64_t H, void* out,
+                    void* stream);
+
 /* Causal flash-attention forward of the calibration forwards (the sdpa call inside
  * LlamaAttention.forward, reached from awq.py:110-126 inspect forwards and the block forwards
  * of base_blockwise_quantization.py:367-381): out[b, s, h, :] = softmax(q k^T * scale, causal)

@@ -111,6 +111,7 @@ class BlockwiseOpt:
                                   and v.shape[0] == b and b > 1 else v) for k, v in kw.items()})
             off += b
         self.input['data'], self.input['kwargs'] = new_d, new_k
+        self.global_entry_sizes = [d.shape[0] for d in data]
         self.n_samples_global = total
         self.n_samples = e - s
 
@@ -672,11 +673,12 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         """base_blockwise_quantization.py:567-588: per-tensor static activation qparams from
         the calibration inputs (HBM-resident, not copied), averaged over ranks in the
         reference's replica mode, registered as buf_act_{scales,zeros,qmin,qmax}_{i}."""
-        if self.parallel_mode() == 'shard_tokens':
-            raise NotImplementedError('static activation calibration with token-sharded '
-                                      'calibration data: set special.parallel: replicate')
         entries = self._reference_entries(act_tensors)
-        scales_l, zeros_l, qmin_l, qmax_l = self.aquantizer.get_batch_tensors_qparams(entries)
+        if self.parallel_mode() == 'shard_tokens':
+            scales_l, zeros_l, qmin_l, qmax_l = self._token_sharded_act_qparams(entries)
+        else:
+            scales_l, zeros_l, qmin_l, qmax_l = self.aquantizer.get_batch_tensors_qparams(
+                entries)
         _, ws, _ = world()
         for i, (scales, zeros, qmin, qmax) in enumerate(zip(scales_l, zeros_l, qmin_l, qmax_l)):
             if ws > 1 and dist.is_initialized() and self.parallel_mode() == 'replicate':
@@ -689,6 +691,53 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                 layer.register_buffer(f'buf_act_zeros_{i}', zeros)
                 layer.register_buffer(f'buf_act_qmin_{i}', qmin)
                 layer.register_buffer(f'buf_act_qmax_{i}', qmax)
+
+    @torch.no_grad()
+    def _token_sharded_act_qparams(self, entries):
+        """Static act qparams under shard_tokens, equal to the one-process result: the
+        reference ranges are functions of one (min, max) per calibration segment (a sample
+        when the calibration set is one batch, else an entry; quant.py:103-120, 221-263,
+        524-543), and a segment's min / max is the min / max of its samples'. Each rank takes
+        (min, max) of each of its samples (lcq_minmax_segments), the per-sample table is
+        all-gathered in rank order (= global sample order, _shard_input_tokens), folded into the
+        global segments, and the range + get_qparams kernel runs on the full table on every
+        rank. static_hist merges whole-tensor histograms in segment order and stays
+        single-process (the reference's replica mode averages per-rank scales instead)."""
+        from . import ops
+        aq = self.aquantizer
+        if aq.calib_algo not in ('static_minmax', 'static_moving_minmax'):
+            raise NotImplementedError(f'{aq.calib_algo} with token-sharded calibration data: '
+                                      'set special.parallel: replicate')
+        if aq.granularity != 'per_tensor' or not aq.round_zp:
+            raise NotImplementedError('token-sharded static act qparams: per_tensor, round_zp')
+        if not entries or any(not torch.is_tensor(e) for e in entries):
+            raise NotImplementedError('token-sharded static act qparams take one input tensor')
+        rank, world = P.dist_world()
+        total = self.n_samples_global
+        ranges = [self.sample_shard(total, r, world) for r in range(world)]
+        samples = [e[i] for e in entries for i in range(e.shape[0])]
+        if len(samples) != ranges[rank][1] - ranges[rank][0]:
+            raise RuntimeError('captured inputs do not match this rank\'s calibration samples')
+        dev = samples[0].device if samples else self.model.device
+        local = (ops.minmax_segments(samples) if samples
+                 else torch.empty((0, 2), dtype=torch.float32, device=dev))
+        mm = P.gather_ranges(local, ranges)
+        sizes = self.global_entry_sizes
+        if len(sizes) > 1:   # segments = entries: fold their samples
+            seg = torch.repeat_interleave(torch.arange(len(sizes), device=mm.device),
+                                          torch.tensor(sizes, device=mm.device))
+            lo = torch.full((len(sizes),), float('inf'), device=mm.device).scatter_reduce(
+                0, seg, mm[:, 0], 'amin')
+            hi = torch.full((len(sizes),), float('-inf'), device=mm.device).scatter_reduce(
+                0, seg, mm[:, 1], 'amax')
+            mm = torch.stack([lo, hi], dim=1)
+        rdt = torch.float32 if aq.calib_algo == 'static_minmax' else entries[0].dtype
+        sdt = aq._static_scale_dtype(rdt)
+        r = ops.act_static_qparams(mm, aq.calib_algo, 0.01, rdt, sdt, aq.sym, float(aq.qmin),
+                                   float(aq.qmax))
+        return ([r[0].to(sdt)],
+                [torch.tensor(0.0, device=dev) if aq.sym else r[1].to(sdt)],
+                [aq.qmin.to(dev)], [aq.qmax.to(dev)])
 
     def rehook_next_subset(self, block, subset, next_subset):
         self.subset_init(next_subset)

@@ -706,14 +706,20 @@ __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds, int6
     }
 }
 
-constexpr int NS_F32D = 3;
+#ifndef LCQ_F32D_NS
+#define LCQ_F32D_NS 3
+#endif
+#ifndef LCQ_F32D_OCC
+#define LCQ_F32D_OCC 1
+#endif
+constexpr int NS_F32D = LCQ_F32D_NS;  // (probe builds vary the ring depth / occupancy)
 template <int T>
 constexpr int f32d_lds() { return NS_F32D * 2 * T * DKC * 4; }
 
 // fixed kernels around the body (a templated __global__ with device builtins inside its
 // lambda loses its host stub under hipcc)
 #define LCQ_F32D_KERNEL(NAME, BT, T)                                                   \
-  __global__ void __launch_bounds__(256, 1) NAME(Args a) {                             \
+  __global__ void __launch_bounds__(256, LCQ_F32D_OCC) NAME(Args a) {                             \
     extern __shared__ __attribute__((aligned(16))) char f32lds[];                      \
     gemm_f32d_body<BT, T, NS_F32D>(a, f32lds, (int64_t)blockIdx.y * T,                 \
                                    (int64_t)blockIdx.x * T, 0, a.K / DKC, nullptr);    \

@@ -234,6 +234,9 @@ struct Gemm2Args {
   int64_t kb_per_split;
   int c_dt;
   int nmt, nnt;
+  int64_t ast_elems;  // a_s floats readable from ast (the grouped kernel shifts ast per group)
+  const int64_t* arows;  // grouped, gathered A: tile row i reads A row arows[i] (null: a + i)
+  int64_t a_bytes;       // bytes of A behind `a` when gathered
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
@@ -262,8 +265,22 @@ __device__ __forceinline__ v8i frag2(const uint8_t* tile, int row, int q) {
              (int)hi.w};
 }
 
+// XCD-aware order of one GEMM's tiles: the 32 workgroups an XCD runs at once take a 4 (M) x 8
+// (N) block (sharing 4 A row bands and 8 B column bands in that XCD's L2)
+__device__ __forceinline__ bool tile_of_slot(const Gemm2Args& g, int& tm, int& tn) {
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int cpb = (g.nnt + 7) / 8;
+  const int chunk = wg >> 5, sl = wg & 31, band = chunk / cpb, cc = chunk - band * cpb;
+  tm = band * 4 + (sl >> 3);
+  tn = cc * 8 + (sl & 7);
+  return tm < g.nmt && tn < g.nnt;
+}
+
 template <int TM, int WR, int WC, int NS>
-__device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds) {
+__device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int tm, int tn,
+                                           int kz) {
   constexpr int NW = WR * WC;                 // waves
   constexpr int OPB = TM * BK;                // one operand tile
   constexpr int STG = stage_bytes<TM>();
@@ -275,30 +292,29 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w / WC, wc = w % WC;
-  // XCD-aware order: the 32 workgroups an XCD runs at once take a 4 (M) x 8 (N) block
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int cpb = (g.nnt + 7) / 8;
-  const int chunk = wg >> 5, sl = wg & 31, band = chunk / cpb, cc = chunk - band * cpb;
-  const int tm = band * 4 + (sl >> 3), tn = cc * 8 + (sl & 7);
-  if (tm >= g.nmt || tn >= g.nnt) return;
   const int64_t m0 = (int64_t)tm * TM, n0 = (int64_t)tn * TM;
   const int64_t nkb = g.K / BK;
-  const int64_t kb0 = (int64_t)blockIdx.z * g.kb_per_split;
+  const int64_t kb0 = (int64_t)kz * g.kb_per_split;
   int64_t nk = nkb - kb0;
   if (nk > g.kb_per_split) nk = g.kb_per_split;
 
   // staging: piece j of wave w = rows j * 8 NW + w * 8 .. + 7 of A and of B; 8 rows x 128 B =
   // 64 lanes x 16 B; lane l -> row l / 8, physical chunk l % 8 = logical chunk (l % 8) ^ swz(row)
-  const __amdgpu_buffer_rsrc_t ra = rsrc(g.a + m0 * g.K, (g.M - m0) * g.K);
+  const __amdgpu_buffer_rsrc_t ra =
+      g.arows ? rsrc(g.a, g.a_bytes) : rsrc(g.a + m0 * g.K, (g.M - m0) * g.K);
   const __amdgpu_buffer_rsrc_t rb = rsrc(g.b + n0 * g.K, (g.N - n0) * g.K);
-  const __amdgpu_buffer_rsrc_t rs = rsrc(g.ast + m0, (g.mp * nkb - m0) * 4);
-  uint32_t off[PIECES];
+  const __amdgpu_buffer_rsrc_t rs = rsrc(g.ast + m0, (g.ast_elems - m0) * 4);
+  uint32_t off[PIECES], aoff[PIECES];
 #pragma unroll
   for (int j = 0; j < PIECES; ++j) {
     const int row = j * 8 * NW + w * 8 + (lane >> 3);
     off[j] = (uint32_t)(row * g.K + (((lane & 7) ^ swz(row)) * 16));
+    aoff[j] = off[j];
+    if (g.arows) {  // gathered rows; rows past M read past the descriptor's range: zeros
+      const int64_t m = m0 + row;
+      aoff[j] = m < g.M ? (uint32_t)(g.arows[m] * g.K + (((lane & 7) ^ swz(row)) * 16))
+                        : 0x80000000u;
+    }
   }
   auto stage = [&](int buf, int64_t kbl) {  // kbl: K block index within the split
     const int64_t kb = kb0 + (kbl < nk ? kbl : nk - 1);
@@ -307,7 +323,7 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds) {
 #pragma unroll
     for (int j = 0; j < PIECES; ++j) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(dst + (j * 8 * NW + w * 8) * BK),
-                                               16, off[j], kofs, 0, 0);
+                                               16, aoff[j], kofs, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(dst + OPB +
                                                                  (j * 8 * NW + w * 8) * BK),
                                                16, off[j], kofs, 0, 0);
@@ -391,7 +407,7 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds) {
       if (n >= g.N) continue;
       const v4f v = acc[mb][nb];
       if (g.ws) {
-        *reinterpret_cast<float4*>(g.ws + ((int64_t)blockIdx.z * g.M + m) * g.N + n) =
+        *reinterpret_cast<float4*>(g.ws + ((int64_t)kz * g.M + m) * g.N + n) =
             make_float4(v[0], v[1], v[2], v[3]);
       } else if (g.c_dt == LCQ_F32) {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.c) + m * g.N + n) =
@@ -417,22 +433,122 @@ constexpr int NS256 = 2, NS128 = 4;
 
 __global__ __launch_bounds__(512, 1) void k_fp8_gemm2(Gemm2Args g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  gemm2_body<256, 2, 4, NS256>(g, lds);
+  int tm, tn;
+  if (!tile_of_slot(g, tm, tn)) return;
+  gemm2_body<256, 2, 4, NS256>(g, lds, tm, tn, blockIdx.z);
 }
 
 __global__ __launch_bounds__(256, 1) void k_fp8_gemm2_128(Gemm2Args g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  gemm2_body<128, 2, 2, NS128>(g, lds);
+  int tm, tn;
+  if (!tile_of_slot(g, tm, tn)) return;
+  gemm2_body<128, 2, 2, NS128>(g, lds, tm, tn, blockIdx.z);
+}
+
+// ---------------------------------------------------------------------------------------
+// Grouped GEMM: G independent problems C_g = A_g B_g^T (the routed experts of one MoE layer,
+// one launch per projection). A is the tokens sorted by expert, [rows, K] e4m3 with rows
+// [row_off[g], row_off[g + 1]) for group g (row_off on the device: the routing never visits the
+// host); group g's weight and block-scales are wtab[2 g], wtab[2 g + 1] (device pointers, all
+// [N, K] / [ceil(N/128), K/128]); C is [rows, N] in the same row order. Each output row is
+// computed exactly as the single-problem k_fp8_gemm2 computes it unsplit (same body, same K
+// order), so grouping changes which rows share a launch, not a row's value.
+//   k_group_tiles (one workgroup per group) lays the groups' 256^2 tile slots end to end: group
+//   g owns slots [tile0[g], tile0[g + 1]), nmt_g x 8 ceil(nnt / 8) of them, and writes its
+//   group index into tmap for each; the last group also writes the total.
+//   k_fp8_gemm2_grouped runs on an upper bound of the slot count: XCD x takes slots
+//   [x q, (x + 1) q), q = ceil(total / 8), so one XCD walks consecutive tiles of one or two
+//   experts (their A bands and B columns stay in its L2); inside a group, 4 (M) x 8 (N) tile
+//   blocks (a last band of nmt % 4 rows) so that the 32 concurrent workgroups of an XCD share
+//   operands as in the single-problem order. Slots past N's tile count return at once.
+// ---------------------------------------------------------------------------------------
+struct GroupedArgs {
+  const uint8_t* a;
+  const float* ast;      // [nkb][mp] (k_as_transpose of the act_quant scales, sorted rows)
+  const int64_t* row_off;
+  const int64_t* wtab;   // [nsets][G][2]: weight, block-scales
+  const int* tile0;      // [G + 1]
+  const int* tmap;       // [slots]: group of each slot
+  const int64_t* arows;  // sorted row -> A row, or null (A already sorted)
+  int64_t a_bytes;
+  void* c;               // [nsets][rows][N]
+  int64_t N, K, mp, rows;
+  int G, c_dt, nnt, nsets;
+};
+
+__global__ __launch_bounds__(256) void k_group_tiles(const int64_t* __restrict__ row_off, int G,
+                                                     int nnt, int* __restrict__ tile0,
+                                                     int* __restrict__ tmap) {
+  __shared__ int part[256];
+  const int g = blockIdx.x, tid = threadIdx.x;
+  const int row8 = 8 * ((nnt + 7) / 8);
+  int s = 0;  // slots of the groups before g
+  for (int j = tid; j < g; j += 256)
+    s += (int)((row_off[j + 1] - row_off[j] + 255) / 256) * row8;
+  part[tid] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) part[tid] += part[tid + w];
+    __syncthreads();
+  }
+  const int base = part[0];
+  const int mine = (int)((row_off[g + 1] - row_off[g] + 255) / 256) * row8;
+  if (tid == 0) {
+    tile0[g] = base;
+    if (g == G - 1) tile0[G] = base + mine;
+  }
+  for (int i = tid; i < mine; i += 256) tmap[base + i] = g;
+}
+
+__global__ __launch_bounds__(512, 1) void k_fp8_gemm2_grouped(GroupedArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int bid = blockIdx.x;
+  const int total = __builtin_amdgcn_readfirstlane(ga.tile0[ga.G]) * ga.nsets;
+  const int q = (total + 7) >> 3;
+  const int j = bid >> 3, vs = (bid & 7) * q + j;
+  if (j >= q || vs >= total) return;  // the grid covers 8 q slots (host bound)
+  // the weight sets of one tile are consecutive slots (they read the same A rows)
+  const int slot = vs / ga.nsets, set = vs - slot * ga.nsets;
+  const int grp = __builtin_amdgcn_readfirstlane(ga.tmap[slot]);
+  const int64_t r0 = ga.row_off[grp], M = ga.row_off[grp + 1] - r0;
+  const int l = slot - ga.tile0[grp];
+  const int nmt = (int)((M + 255) / 256), cpb = (ga.nnt + 7) / 8;
+  // 4 x 8 blocks over full 4-row bands, then the last band's (nmt % 4) x 8 blocks
+  const int full = nmt / 4, fslots = full * 32 * cpb;
+  int tm, tn;
+  if (l < fslots) {
+    const int chunk = l >> 5, sl = l & 31, band = chunk / cpb, cc = chunk - band * cpb;
+    tm = band * 4 + (sl >> 3);
+    tn = cc * 8 + (sl & 7);
+  } else {
+    const int bh = nmt - full * 4, ll = l - fslots, cs = bh * 8;
+    const int cc = ll / cs, sl = ll - cc * cs;
+    tm = full * 4 + sl / 8;
+    tn = cc * 8 + (sl & 7);
+  }
+  if (tn >= ga.nnt) return;
+  const int64_t nkb = ga.K / BK;
+  const int64_t wi = 2 * ((int64_t)set * ga.G + grp);
+  Gemm2Args g{ga.arows ? ga.a : ga.a + r0 * ga.K,
+              reinterpret_cast<const uint8_t*>(ga.wtab[wi]),
+              ga.ast + r0,
+              reinterpret_cast<const float*>(ga.wtab[wi + 1]),
+              static_cast<uint8_t*>(ga.c) +
+                  ((int64_t)set * ga.rows + r0) * ga.N * (ga.c_dt == LCQ_F32 ? 4 : 2),
+              nullptr, M, ga.N, ga.K, ga.mp, nkb, ga.c_dt, nmt, ga.nnt,
+              ga.mp * nkb - r0, ga.arows ? ga.arows + r0 : nullptr, ga.a_bytes};
+  gemm2_body<256, 2, 4, NS256>(g, lds, tm, tn, 0);
 }
 
 // a_s [M, nkb] -> [nkb, mp] (rows past M zero)
 __global__ __launch_bounds__(256) void k_as_transpose(const float* __restrict__ as, int64_t M,
                                                       int64_t nkb, int64_t mp,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out,
+                                                      const int64_t* __restrict__ rows) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= nkb * mp) return;
   const int64_t kb = i / mp, m = i - kb * mp;
-  out[i] = m < M ? as[m * nkb + kb] : 0.f;
+  out[i] = m < M ? as[(rows ? rows[m] : m) * nkb + kb] : 0.f;
 }
 
 // Tile plan. An fp8 K block of a 128^2 tile is 4.2 MFLOP per 32 KB staged (128 flop/B): at the
@@ -545,11 +661,11 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
     float* ast = static_cast<float*>(workspace);
     float* part = s2 > 1 ? ast + nkb * mp : nullptr;
     hipLaunchKernelGGL(k_as_transpose, dim3((unsigned)((nkb * mp + 255) / 256)), 256, 0, st,
-                       static_cast<const float*>(a_s), M, nkb, mp, ast);
+                       static_cast<const float*>(a_s), M, nkb, mp, ast, nullptr);
     Gemm2Args g2{static_cast<const uint8_t*>(a), static_cast<const uint8_t*>(b), ast,
                  static_cast<const float*>(b_s), c, part, M, N, K, mp,
                  (nkb + s2 - 1) / s2, c_dtype, (int)((M + pl.tm - 1) / pl.tm),
-                 (int)((N + pl.tm - 1) / pl.tm)};
+                 (int)((N + pl.tm - 1) / pl.tm), nkb * mp, nullptr, 0};
     const int nslots = 32 * ((g2.nmt + 3) / 4) * ((g2.nnt + 7) / 8);
     // stage ring + the split's block-scales (TM / 128 column blocks x K blocks per split)
     const int bsb = (int)(((pl.tm / 128) * g2.kb_per_split * 4 + 15) / 16 * 16);
@@ -602,4 +718,63 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
         static_cast<const float*>(workspace), (int)splits, mn, c, c_dtype);
   }
   return check_launch("lcq_fp8_gemm");
+}
+
+// grouped workspace: the kb-major a_s copy, tile0 [G + 1], tmap [slot bound]
+static int64_t grouped_slot_bound(int64_t rows, int64_t G, int64_t N) {
+  const int64_t nnt = (N + 255) / 256;
+  return ((rows + 255) / 256 + G) * 8 * ((nnt + 7) / 8);
+}
+
+extern "C" int64_t lcq_fp8_gemm_grouped_workspace_bytes(int64_t rows, int64_t G, int64_t N,
+                                                        int64_t K) {
+  if (rows < 0 || G <= 0 || N <= 0 || K <= 0 || K % BK != 0) return 0;
+  const int64_t mp = (rows + 255) / 256 * 256, nkb = K / BK;
+  return nkb * mp * 4 + (G + 1) * 4 + grouped_slot_bound(rows, G, N) * 4 + 64;
+}
+
+extern "C" int lcq_fp8_gemm_grouped(const void* a, const void* a_s, int64_t a_rows_total,
+                                    const int64_t* a_rows, int64_t rows,
+                                    const int64_t* row_off, const int64_t* wtab, int64_t G,
+                                    int nsets, int64_t N, int64_t K, void* c, int c_dtype,
+                                    void* workspace, int64_t ws_bytes, void* stream) {
+  LCQ_REQUIRE(a && a_s && row_off && wtab && c && workspace, "null pointer");
+  LCQ_REQUIRE(rows >= 0 && G > 0 && G <= (1 << 20) && N > 0 && K > 0, "bad grouped shape");
+  LCQ_REQUIRE(nsets == 1 || nsets == 2, "nsets must be 1 or 2");
+  LCQ_REQUIRE(a_rows ? (a_rows_total >= 0 && a_rows_total * K < ((int64_t)1 << 31))
+                     : a_rows_total == rows,
+              "gathered A must be < 2 GiB; ungathered A has `rows` rows");
+  LCQ_REQUIRE(K % BK == 0, "K must be a multiple of 128 (the scale block)");
+  LCQ_REQUIRE(N % 4 == 0, "N must be a multiple of 4");
+  LCQ_REQUIRE(256 * K < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31),
+              "K / N too large for the 32-bit tile offsets");
+  LCQ_REQUIRE(c_dtype == LCQ_F32 || c_dtype == LCQ_BF16 || c_dtype == LCQ_F16,
+              "C dtype must be F32, BF16 or F16");
+  LCQ_REQUIRE((reinterpret_cast<uintptr_t>(a) & 15) == 0, "A must be 16-byte aligned");
+  LCQ_REQUIRE(ws_bytes >= lcq_fp8_gemm_grouped_workspace_bytes(rows, G, N, K),
+              "workspace too small");
+  if (rows == 0) return LCQ_OK;
+  hipStream_t st = as_stream(stream);
+  const int64_t mp = (rows + 255) / 256 * 256, nkb = K / BK;
+  float* ast = static_cast<float*>(workspace);
+  int* tile0 = reinterpret_cast<int*>(ast + nkb * mp);
+  int* tmap = tile0 + (G + 1);
+  const int64_t bound = grouped_slot_bound(rows, G, N);
+  LCQ_REQUIRE(bound * nsets < ((int64_t)1 << 30), "too many tiles");
+  hipLaunchKernelGGL(k_as_transpose, dim3((unsigned)((nkb * mp + 255) / 256)), 256, 0, st,
+                     static_cast<const float*>(a_s), rows, nkb, mp, ast, a_rows);
+  const int nnt = (int)((N + 255) / 256);
+  hipLaunchKernelGGL(k_group_tiles, dim3((unsigned)G), 256, 0, st, row_off, (int)G, nnt, tile0,
+                     tmap);
+  GroupedArgs ga{static_cast<const uint8_t*>(a), ast, row_off, wtab, tile0, tmap, a_rows,
+                 a_rows_total * K, c, N, K, mp, rows, (int)G, c_dtype, nnt, nsets};
+  const int bsb = (int)((2 * nkb * 4 + 15) / 16 * 16);
+  const int L = NS256 * stage_bytes<256>() + bsb;
+  LCQ_REQUIRE(L <= 160 * 1024, "K too large for the staged block-scales");
+  (void)hipFuncSetAttribute((const void*)k_fp8_gemm2_grouped,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, L);
+  // the slot bound rounded to 8 XCD lanes (the kernel's q never exceeds bound / 8 rounded up)
+  const int64_t grid = (bound * nsets + 7) / 8 * 8;
+  hipLaunchKernelGGL(k_fp8_gemm2_grouped, dim3((unsigned)grid), 512, L, st, ga);
+  return check_launch("lcq_fp8_gemm_grouped");
 }

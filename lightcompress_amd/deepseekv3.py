@@ -29,6 +29,9 @@ class ExpertList(nn.ModuleList):
     (BaseBlockwiseQuantization.entry_view)."""
 
     def forward(self, hidden_states, top_k_index, top_k_weights):
+        if (top_k_weights.dtype in (torch.float32, torch.bfloat16, torch.float16)
+                and self._grouped_fp8_ok(hidden_states)):
+            return self._forward_grouped_fp8(hidden_states, top_k_index, top_k_weights)
         out = torch.zeros_like(hidden_states)
         with torch.no_grad():
             mask = torch.nn.functional.one_hot(top_k_index, num_classes=len(self)).permute(2, 1, 0)
@@ -41,6 +44,94 @@ class ExpertList(nn.ModuleList):
             h = self[e](hidden_states[tok]) * top_k_weights[tok, pos, None]
             out.index_add_(0, tok, h.to(out.dtype))
         return out
+
+    # ---- one launch per projection for block-fp8 experts ----------------------------------
+    # The loop above is the reference's expert loop: per hit expert, act_quant + fp8 GEMM for
+    # gate, up and down on that expert's tokens (3 x E launches of a few hundred workgroups,
+    # 0.18 of the fp8 MFMA peak at 2048 tokens per expert). When every expert is a plain
+    # block-fp8 MLP and nothing observes the per-expert calls (no hooks: calibration capture
+    # registers them and then takes the loop), the experts run as grouped GEMMs instead: the
+    # token slots are sorted by expert on the device (no host sync), act_quant runs once per
+    # token (it is per row), one lcq_fp8_gemm_grouped launch computes gate and up of every
+    # expert (the kernel gathers each slot's token row), act_fn(gate) * up as the MLP computes
+    # it, one launch for down, then lcq_moe_combine in the loop's order (per token, experts in
+    # ascending index, each product rounded to bf16 before its add, as index_add_ does).
+    # Every row's GEMM value equals lcq_fp8_gemm's on an unsplit 256^2 plan.
+    def _grouped_fp8_ok(self, x) -> bool:
+        from .module_utils import USE_FP8GEMM_TRITON_KERNEL, LlmcFp8Linear
+        if (not USE_FP8GEMM_TRITON_KERNEL or not len(self) or x.dim() != 2 or not x.is_cuda
+                or x.dtype != torch.bfloat16 or len(self) > 1 << 20
+                or torch.nn.modules.module._global_forward_hooks
+                or torch.nn.modules.module._global_forward_pre_hooks):
+            return False
+        mlp_forward = _mlp_forward()
+        for mlp in self:
+            if mlp_forward is None or type(mlp).forward is not mlp_forward:
+                return False
+            for m in (mlp, mlp.gate_proj, mlp.up_proj, mlp.down_proj):
+                if m._forward_hooks or m._forward_pre_hooks:
+                    return False
+            for lin in (mlp.gate_proj, mlp.up_proj, mlp.down_proj):
+                if (type(lin) is not LlmcFp8Linear or lin.bias is not None
+                        or lin.block_size != 128 or lin.weight.dtype != torch.float8_e4m3fn
+                        or lin.weight.device != x.device):
+                    return False
+        return True
+
+    def _fp8_tables(self, device):
+        """([2, E, 2] gate + up, [E, 2] down) device tables of the experts' (weight, scale)
+        addresses, rebuilt when any weight tensor changed (the modules keep the tensors)."""
+        key = tuple((lin.weight.data_ptr(), lin.weight_scale_inv.data_ptr())
+                    for mlp in self for lin in (mlp.gate_proj, mlp.up_proj, mlp.down_proj))
+        cached = getattr(self, '_lcq_fp8_tables', None)
+        if cached is None or cached[0] != key:
+            from . import ops
+            gate, up, down = (ops.fp8_weight_table(
+                [(getattr(mlp, p).weight.data, getattr(mlp, p).weight_scale_inv.data)
+                 for mlp in self], device) for p in ('gate_proj', 'up_proj', 'down_proj'))
+            cached = (key, (torch.stack([gate, up]).contiguous(), down))
+            self._lcq_fp8_tables = cached
+        return cached[1]
+
+    def _forward_grouped_fp8(self, hidden_states, top_k_index, top_k_weights):
+        from . import ops
+        from .kernel import act_quant
+        T, k = top_k_index.shape
+        E, H = len(self), hidden_states.shape[1]
+        if T == 0:
+            return torch.zeros_like(hidden_states)
+        inter = self[0].gate_proj.out_features
+        gate_up, down = self._fp8_tables(hidden_states.device)
+        # C in the default dtype, then bf16, as block_wise_fp8_forward_func (fp32 default:
+        # the kernel's round-to-nearest-even bf16 store is the same single rounding)
+        cdt = torch.get_default_dtype()
+        cdt = torch.bfloat16 if cdt == torch.float32 else cdt
+        with torch.no_grad():
+            flat = top_k_index.reshape(-1)
+            order = torch.argsort(flat, stable=True)          # sorted row -> (token, slot)
+            row_off = torch.zeros(E + 1, dtype=torch.int64, device=flat.device)
+            torch.cumsum(torch.bincount(flat, minlength=E), 0, out=row_off[1:])
+            slot_row = torch.empty_like(order)                # (token, slot) -> sorted row
+            slot_row[order] = torch.arange(order.numel(), device=order.device)
+        # act_quant is per token row: quantize each token once, the GEMM gathers its k copies
+        xq, xs = act_quant(hidden_states.contiguous(), 128)
+        gu = ops.fp8_gemm_grouped(xq, xs.reshape(-1), row_off, gate_up, inter, cdt,
+                                  a_rows=order // k).to(torch.bfloat16)
+        h = (self[0].act_fn(gu[0]) * gu[1]).contiguous()
+        del gu, xq, xs
+        hq, hs = act_quant(h, 128)
+        del h
+        y = ops.fp8_gemm_grouped(hq, hs.reshape(-1), row_off, down, H, cdt).to(torch.bfloat16)
+        del hq, hs
+        w = top_k_weights if top_k_weights.dtype != torch.float16 else top_k_weights.float()
+        return ops.moe_combine(y, slot_row, top_k_index.to(torch.int64), w, T)
+
+def _mlp_forward():
+    try:
+        from transformers.models.deepseek_v3 import modeling_deepseek_v3 as md
+    except ImportError:  # pragma: no cover - transformers without DeepSeek-V3
+        return None
+    return md.DeepseekV3MLP.forward
 
 
 @torch.no_grad()

@@ -886,6 +886,96 @@ def fp8_gemm(a: torch.Tensor, a_s: torch.Tensor, b: torch.Tensor, b_s: torch.Ten
     return c
 
 
+def fp8_weight_table(weights, device) -> torch.Tensor:
+    """Device table [G, 2] int64 of (weight, block-scale) addresses for fp8_gemm_grouped, after
+    checking every pair: weight [N, K] e4m3 contiguous 16-byte aligned, scales fp32 contiguous
+    [ceil(N/128), K/128], one (N, K) for all. The tensors must outlive every launch that reads
+    the table (the caller keeps them with it)."""
+    rows = []
+    shape = None
+    for w, s in weights:
+        if w.dtype != torch.float8_e4m3fn or not w.is_contiguous() or w.dim() != 2:
+            raise TypeError('grouped fp8 weights must be contiguous 2-D float8_e4m3fn')
+        if shape is None:
+            shape = tuple(w.shape)
+        if tuple(w.shape) != shape:
+            raise ValueError(f'grouped fp8 weights differ in shape: {tuple(w.shape)} vs {shape}')
+        n, k = shape
+        if (s.dtype != torch.float32 or not s.is_contiguous()
+                or tuple(s.shape) != ((n + 127) // 128, k // 128)):
+            raise ValueError(f'block scales must be contiguous fp32 [{(n + 127) // 128}, '
+                             f'{k // 128}]')
+        if w.data_ptr() % 16:
+            raise ValueError('grouped fp8 weights must be 16-byte aligned')
+        rows.append((w.data_ptr(), s.data_ptr()))
+    return torch.tensor(rows, dtype=torch.int64).to(device)
+
+
+def fp8_gemm_grouped(a: torch.Tensor, a_s: torch.Tensor, row_off: torch.Tensor,
+                     wtab: torch.Tensor, n: int, out_dtype: torch.dtype = torch.bfloat16,
+                     a_rows: torch.Tensor | None = None) -> torch.Tensor:
+    """One launch of G block-scaled fp8 GEMMs (the routed experts of an MoE projection), for
+    one or two weight sets. Rows: the token slots sorted by group, row_off int64 [G + 1] on
+    the device (group g = rows [row_off[g], row_off[g + 1])). a [R, K] e4m3 with a_s [R, K/128]
+    (act_quant): with ``a_rows`` (int64 [rows] on the device) sorted row i is a[a_rows[i]] --
+    the gather happens in the kernel -- else a itself is sorted (rows = R). wtab from
+    fp8_weight_table, [G, 2] or [2, G, 2] (two sets: gate and up of the same rows), all [n, K].
+    Returns c [rows, n], or [2, rows, n] for two sets; each row equals fp8_gemm's on an
+    unsplit 256^2 plan."""
+    if a.dtype != torch.float8_e4m3fn or not a.is_contiguous() or a.dim() != 2:
+        raise TypeError('a must be a contiguous 2-D float8_e4m3fn tensor')
+    R, K = a.shape
+    if K % 128:
+        raise ValueError(f'K={K} is not a multiple of the 128-column scale block')
+    if a_s.dtype != torch.float32 or not a_s.is_contiguous() or a_s.numel() != R * (K // 128):
+        raise ValueError(f'a_s must be contiguous fp32 with {R}x{K // 128} elements')
+    nsets = 1 if wtab.dim() == 2 else wtab.shape[0]
+    G = wtab.shape[-2]
+    if (wtab.dtype != torch.int64 or wtab.shape[-1] != 2 or nsets not in (1, 2)
+            or wtab.dim() not in (2, 3) or not wtab.is_contiguous()
+            or wtab.device != a.device):
+        raise ValueError('wtab must be int64 [G, 2] or [2, G, 2] on a\'s device')
+    if row_off.dtype != torch.int64 or row_off.numel() != G + 1 or row_off.device != a.device:
+        raise ValueError('row_off must be int64 [G + 1] on a\'s device')
+    if a_rows is not None:
+        if (a_rows.dtype != torch.int64 or a_rows.dim() != 1 or not a_rows.is_contiguous()
+                or a_rows.device != a.device):
+            raise ValueError('a_rows must be a contiguous int64 vector on a\'s device')
+        rows = a_rows.numel()
+    else:
+        rows = R
+    shape = (rows, n) if nsets == 1 else (nsets, rows, n)
+    c = torch.empty(shape, dtype=out_dtype, device=a.device)
+    if rows == 0:
+        return c
+    wsb = int(N.load().lcq_fp8_gemm_grouped_workspace_bytes(rows, G, n, K))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=a.device)
+    N.call('lcq_fp8_gemm_grouped', N.ptr(a), N.ptr(a_s), R,
+           None if a_rows is None else N.ptr(a_rows), rows, N.ptr(row_off), N.ptr(wtab), G,
+           nsets, n, K, N.ptr(c), N.dt(out_dtype), N.ptr(ws), wsb, N.stream_of(a))
+    return c
+
+
+def moe_combine(y: torch.Tensor, slot_row: torch.Tensor, expert: torch.Tensor,
+                weights: torch.Tensor, T: int) -> torch.Tensor:
+    """out [T, H] bf16: per token, its k slots' expert rows y[slot_row] (bf16, the grouped
+    GEMM's sorted order) times their routing weights, rounded to bf16 and summed in ascending
+    expert id with a bf16 rounding per add -- the expert loop's index_add_ combine
+    (lcq_moe_combine)."""
+    if y.dtype != torch.bfloat16 or not y.is_contiguous() or y.dim() != 2:
+        raise TypeError('y must be a contiguous 2-D bf16 tensor')
+    k = expert.shape[-1]
+    if (slot_row.dtype != torch.int64 or expert.dtype != torch.int64
+            or slot_row.numel() != T * k or expert.numel() != T * k
+            or weights.numel() != T * k or weights.dtype not in (torch.float32, torch.bfloat16)):
+        raise ValueError('slot_row / expert int64 and weights fp32 / bf16, all [T, k]')
+    H = y.shape[1]
+    out = torch.empty((T, H), dtype=torch.bfloat16, device=y.device)
+    N.call('lcq_moe_combine', N.ptr(y), N.ptr(slot_row.contiguous()),
+           N.ptr(expert.contiguous()), N.ptr(weights.contiguous()), N.dt(weights.dtype), T, k,
+           H, N.ptr(out), N.stream_of(y))
+    return out
+
 def fp8_block_to_tensor(codes: torch.Tensor, scales_inv: torch.Tensor, block: int = 128,
                         fp8: torch.dtype = torch.float8_e4m3fn, qmax: float | None = None):
     """Block-fp8 weight -> bf16 (weight_cast_to_bf16) -> per-tensor fp8 real quant, fused.

@@ -84,10 +84,20 @@ def awq_pick_best(best_error: float, best_scales: torch.Tensor) -> torch.Tensor:
 
 def gather_rows(local: torch.Tensor, rows: int, align: int = 1) -> torch.Tensor:
     """Reassemble a row-sharded matrix (row_shard layout) on every rank."""
+    _, world = dist_world()
+    if world == 1:
+        return local
+    return gather_ranges(local, [row_shard(rows, r, world, align) for r in range(world)])
+
+
+def gather_ranges(local: torch.Tensor, sizes) -> torch.Tensor:
+    """Reassemble rows held as contiguous [start, end) ranges, rank r holding sizes[r], on
+    every rank (one all_gather of equal padded parts, concatenated in rank order)."""
     rank, world = dist_world()
     if world == 1:
         return local
-    sizes = [row_shard(rows, r, world, align) for r in range(world)]
+    if local.shape[0] != sizes[rank][1] - sizes[rank][0]:
+        raise ValueError(f'rank {rank} holds {local.shape[0]} rows, its range is {sizes[rank]}')
     maxr = max(e - s for s, e in sizes)
     pad = torch.zeros((maxr,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local

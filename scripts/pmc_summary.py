@@ -9,7 +9,8 @@ import json
 import sys
 from collections import defaultdict
 
-KEYS = {'k_syrk_x': 'k_syrk_x', 'k_tree_sum': 'k_tree_sum', 'k_syrk16': 'k_syrk16', 'k_fp8_gemm2': 'k_fp8_gemm2', 'k_fp8_gemm': 'k_fp8_gemm',
+KEYS = {'k_fp8_gemm2_grouped': 'k_fp8_gemm2_grouped', 'k_syrk_reduce': 'k_syrk_reduce',
+        'k_gemm_f32d': 'k_gemm_f32d', 'k_gather_rc': 'k_gather_rc', 'k_syrk_x': 'k_syrk_x', 'k_tree_sum': 'k_tree_sum', 'k_syrk16': 'k_syrk16', 'k_fp8_gemm2': 'k_fp8_gemm2', 'k_fp8_gemm': 'k_fp8_gemm',
         'k_hqq_step': 'k_hqq_step', 'k_gemm16': 'k_gemm16', 'k_loss_reduce': 'k_loss_reduce', 'hipblaslt_gemm': 'Custom_Cijk_', 'blas_gemm_other': 'Cijk_',
         'k_chol_inv_tile': 'k_chol_inv_tile', 'k_rmsnorm': 'k_rmsnorm',
         'k_quant_static_cols': 'k_quant_static_cols', 'k_quant_dyn_rows': 'k_quant_dyn_rows', 'k_syrk256': 'k_syrk256', 'k_auto_clip': 'k_auto_clip',

@@ -374,3 +374,178 @@ def test_fp8_gemm_f16_default_dtype(dev):
         want = O.fp8_gemm(a, a_s, b, b_s)
         tol = GEMM_RTOL * _abs_gemm(a, a_s, b, b_s) + want.abs() * 2.0 ** -11
         assert ((got.float() - want).abs() <= tol).all()
+
+
+def _grouped(dev, counts, Nn, K, seed):
+    """Rows sorted by group (counts[g] rows each) + per-group fp8 weights, on the device."""
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(seed)
+    rows = sum(counts)
+    x = torch.randn(rows, K, generator=g) * torch.exp(torch.randn(rows, 1, generator=g))
+    a, a_s = O.act_quant(x)
+    ws = [O.weight_cast_to_fp8(torch.randn(Nn, K, generator=g) * 0.05) for _ in counts]
+    wd = [(b.to(dev), s.to(dev)) for b, s in ws]
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int64)
+    return a, a_s, ws, wd, off, ops.fp8_weight_table(wd, dev)
+
+
+@pytest.mark.parametrize('counts,Nn,K', [([0, 37, 300, 600, 1, 513, 0], 384, 512),
+                                         ([1000, 64, 257], 1500 - 1500 % 4, 896)])
+def test_fp8_gemm_grouped_vs_oracle(dev, counts, Nn, K):
+    """lcq_fp8_gemm_grouped (one launch over ragged groups, empty ones included) vs the
+    fp8_gemm restatement per group (kernel.py:141-214, GEMM_RTOL of |a||b|)."""
+    from lightcompress_amd import ops
+    a, a_s, ws, _, off, tab = _grouped(dev, counts, Nn, K, seed=sum(counts))
+    got = ops.fp8_gemm_grouped(a.to(dev), a_s.to(dev).reshape(-1), off.to(dev), tab, Nn,
+                               torch.float32).cpu()
+    for i, (b, b_s) in enumerate(ws):
+        r0, r1 = int(off[i]), int(off[i + 1])
+        if r1 == r0:
+            continue
+        want = O.fp8_gemm(a[r0:r1], a_s[r0:r1], b, b_s)
+        tol = GEMM_RTOL * _abs_gemm(a[r0:r1], a_s[r0:r1], b, b_s) + 1e-30
+        assert ((got[r0:r1] - want).abs() <= tol).all(), i
+
+
+def test_fp8_gemm_grouped_rows_equal_single_unsplit(dev):
+    """Each group's rows are bit-identical to lcq_fp8_gemm where that runs the unsplit 256^2
+    plan (2048 x 7168: 224 tiles), in bf16 and fp32 output; and repeatable."""
+    from lightcompress_amd import ops
+    counts, Nn, K = [2048, 2048], 7168, 256
+    a, a_s, _, wd, off, tab = _grouped(dev, counts, Nn, K, seed=3)
+    ad, asd, offd = a.to(dev), a_s.to(dev), off.to(dev)
+    for dt in (torch.float32, torch.bfloat16):
+        got = ops.fp8_gemm_grouped(ad, asd.reshape(-1), offd, tab, Nn, dt)
+        again = ops.fp8_gemm_grouped(ad, asd.reshape(-1), offd, tab, Nn, dt)
+        assert torch.equal(got, again)
+        for i, (b, b_s) in enumerate(wd):
+            r0, r1 = int(off[i]), int(off[i + 1])
+            one = ops.fp8_gemm(ad[r0:r1], asd[r0:r1].contiguous(), b, b_s, out_dtype=dt)
+            assert torch.equal(got[r0:r1], one), (dt, i)
+
+
+def test_fp8_gemm_grouped_gather_and_two_sets(dev):
+    """a_rows (the kernel gathers each sorted row from the token matrix) and two weight sets
+    in one launch (gate and up) give exactly the rows of the plain one-set launches on the
+    pre-gathered matrix."""
+    from lightcompress_amd import ops
+    counts, Nn, K = [300, 0, 77, 513], 512, 384
+    g = torch.Generator().manual_seed(8)
+    T = 400
+    x = torch.randn(T, K, generator=g) * torch.exp(torch.randn(T, 1, generator=g))
+    a, a_s = O.act_quant(x)
+    rows = torch.randint(0, T, (sum(counts),), generator=g)
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int64).to(dev)
+    sets = [[O.weight_cast_to_fp8(torch.randn(Nn, K, generator=g) * 0.05) for _ in counts]
+            for _ in range(2)]
+    keep = [[(b.to(dev), s.to(dev)) for b, s in ws] for ws in sets]  # the tables point here
+    tabs = [ops.fp8_weight_table(ws, dev) for ws in keep]
+    ad, asd, rd = a.to(dev), a_s.to(dev), rows.to(dev)
+    both = ops.fp8_gemm_grouped(ad, asd.reshape(-1), off, torch.stack(tabs), Nn,
+                                torch.float32, a_rows=rd)
+    assert both.shape == (2, sum(counts), Nn)
+    ag, sg = ad[rd].contiguous(), asd[rd].contiguous()
+    for i in range(2):
+        one = ops.fp8_gemm_grouped(ag, sg.reshape(-1), off, tabs[i], Nn, torch.float32)
+        assert torch.equal(both[i], one), i
+
+
+@pytest.mark.parametrize('wdt', [torch.float32, torch.bfloat16])
+def test_moe_combine_equals_index_add_loop(dev, wdt):
+    """lcq_moe_combine == the expert loop's combine: out.index_add_(0, tok, (y_e * w).to(bf16))
+    for the hit experts in ascending index (torch on the device)."""
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(int(wdt == torch.bfloat16))
+    T, E, k, H = 333, 12, 5, 264
+    idx = torch.stack([torch.randperm(E, generator=g)[:k] for _ in range(T)]).to(dev)
+    w = torch.rand(T, k, generator=g).to(wdt).to(dev)
+    flat = idx.reshape(-1)
+    order = torch.argsort(flat, stable=True)
+    slot_row = torch.empty_like(order)
+    slot_row[order] = torch.arange(order.numel(), device=dev)
+    y = (torch.randn(T * k, H, generator=g) * 3).to(torch.bfloat16).to(dev)
+    got = ops.moe_combine(y, slot_row, idx, w, T)
+    want = torch.zeros(T, H, dtype=torch.bfloat16, device=dev)
+    for e in range(E):
+        tok, pos = torch.where(idx == e)
+        if tok.numel():
+            want.index_add_(0, tok, (y[slot_row.view(T, k)[tok, pos]] * w[tok, pos, None]).to(
+                torch.bfloat16))
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+
+
+def test_fp8_gemm_grouped_rejects_bad_tables(dev):
+    from lightcompress_amd import ops
+    _, _, _, wd, _, _ = _grouped(dev, [4, 4], 256, 256, seed=1)
+    with pytest.raises(ValueError):   # shapes differ
+        ops.fp8_weight_table([wd[0], (wd[1][0][:128].contiguous(), wd[1][1][:1].contiguous())],
+                             dev)
+    with pytest.raises(TypeError):
+        ops.fp8_weight_table([(wd[0][0].float(), wd[0][1])], dev)
+
+
+def _fp8_experts(dev, E, H, inter, seed):
+    from transformers.models.deepseek_v3 import modeling_deepseek_v3 as md
+
+    from lightcompress_amd.deepseekv3 import ExpertList
+    from lightcompress_amd.module_utils import LlmcFp8Linear
+    cfg = md.DeepseekV3Config(hidden_size=H, intermediate_size=inter, hidden_act='silu')
+    g = torch.Generator().manual_seed(seed)
+    experts = ExpertList()
+    for _ in range(E):
+        mlp = md.DeepseekV3MLP(cfg, intermediate_size=inter)
+        for p in ('gate_proj', 'up_proj', 'down_proj'):
+            lin = getattr(mlp, p)
+            m = LlmcFp8Linear.new(lin, 128)
+            b, s = O.weight_cast_to_fp8(torch.randn(lin.out_features, lin.in_features,
+                                                    generator=g) * 0.05)
+            m.weight.data, m.weight_scale_inv.data = b, s
+            setattr(mlp, p, m)
+        experts.append(mlp)
+    return experts.to(dev)
+
+
+def _routing(dev, T, E, k, seed):
+    g = torch.Generator().manual_seed(seed)
+    idx = torch.stack([torch.randperm(E, generator=g)[:k] for _ in range(T)])
+    w = torch.rand(T, k, generator=g)
+    return idx.to(dev), (w / w.sum(1, keepdim=True)).to(dev)
+
+
+def test_expert_list_grouped_equals_loop(dev, monkeypatch):
+    """ExpertList's grouped block-fp8 forward (one lcq_fp8_gemm_grouped per projection) equals
+    the per-expert loop (models/deepseekv3.py's expert loop: act_quant + fp8 GEMM per expert,
+    index_add_ in expert order) bit for bit when each loop GEMM runs the same per-row
+    arithmetic (a one-group launch); with the loop's own per-expert plans (32x32x64 kernel,
+    split-K for short experts) within the fp8 GEMM tolerance. A forward hook (calibration
+    capture) sends the call back to the loop."""
+    from lightcompress_amd import module_utils, ops
+    from lightcompress_amd.kernel import act_quant
+    E, H, inter, T, k = 8, 512, 384, 300, 3
+    experts = _fp8_experts(dev, E, H, inter, seed=4)
+    idx, w = _routing(dev, T, E, k, seed=5)
+    x = (torch.randn(T, H, generator=torch.Generator().manual_seed(6)) * 2).to(
+        torch.bfloat16).to(dev)
+    assert experts._grouped_fp8_ok(x)
+    grouped = experts(x, idx, w)
+
+    def one_group(x, wt, ws, block, bias):
+        xq, xs = act_quant(x.contiguous(), block)
+        off = torch.tensor([0, xq.shape[0]], dtype=torch.int64, device=x.device)
+        return ops.fp8_gemm_grouped(xq, xs.reshape(-1), off,
+                                    ops.fp8_weight_table([(wt.data, ws.data)], x.device),
+                                    wt.shape[0], torch.bfloat16)
+
+    monkeypatch.setattr(type(experts), '_grouped_fp8_ok', lambda s, x: False)
+    loop_default = experts(x, idx, w)
+    monkeypatch.setattr(module_utils, 'block_wise_fp8_forward_func', one_group)
+    loop_same = experts(x, idx, w)
+    assert torch.equal(grouped, loop_same)
+    tol = 2.0 ** -6 * loop_default.float().abs().max()
+    assert (grouped.float() - loop_default.float()).abs().max() <= tol
+    monkeypatch.undo()
+    h = experts[0].down_proj.register_forward_hook(lambda *a: None)
+    try:
+        assert not experts._grouped_fp8_ok(x)
+    finally:
+        h.remove()

@@ -23,7 +23,7 @@ def _port():
     return p
 
 
-def _model_and_calib(layers):
+def _model_and_calib(layers, entries=(4,)):
     from transformers import LlamaConfig
     from lightcompress_amd.llama import Llama
     cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=4,
@@ -31,8 +31,9 @@ def _model_and_calib(layers):
                       max_position_embeddings=512, rms_norm_eps=1e-5)
     model = Llama.random(cfg, device='cuda:0', seed=3)
     g = torch.Generator(device='cuda:0').manual_seed(9)
-    x = torch.randn(4, 64, 256, generator=g, device='cuda:0').to(torch.bfloat16)
-    return model, {'data': [x], 'kwargs': [model.rotary_kwargs(64)]}
+    x = torch.randn(sum(entries), 64, 256, generator=g, device='cuda:0').to(torch.bfloat16)
+    return model, {'data': list(torch.split(x, list(entries))),
+                   'kwargs': [model.rotary_kwargs(64) for _ in entries]}
 
 
 AWQ = {'calib': {'seq_len': 64},
@@ -68,7 +69,8 @@ GPTQ_TOK_FLOAT = {'quant': {'method': 'GPTQ',
 def _run(cfg_dict, layers):
     from lightcompress_amd.pipeline import build_algo
     from lightcompress_amd.utils import load_config
-    model, calib = _model_and_calib(layers)
+    model, calib = _model_and_calib(layers, cfg_dict.get('entries', (4,)))
+    cfg_dict = {k: v for k, v in cfg_dict.items() if k != 'entries'}
     algo = build_algo(model, load_config(cfg_dict), calib)
     algo.run_block_loop()
     if cfg_dict.get('deploy'):
@@ -79,8 +81,12 @@ def _run(cfg_dict, layers):
         return {f'{i}.{n}': t.detach().cpu()   # norms) as the rank holds it after the gather
                 for i, b in enumerate(model.blocks)
                 for n, t in [*b.named_parameters(), *b.named_buffers()]}
-    return {f'{i}.{n}': m.weight.detach().float().cpu()
-            for i, b in enumerate(model.blocks) for n, m in model.get_block_linears(b).items()}
+    out = {f'{i}.{n}': m.weight.detach().float().cpu()
+           for i, b in enumerate(model.blocks) for n, m in model.get_block_linears(b).items()}
+    out.update({f'{i}.{n}.{bn}': t.detach().float().cpu()   # static act qparams
+                for i, b in enumerate(model.blocks) for n, m in model.get_block_linears(b).items()
+                for bn, t in m.named_buffers() if bn.startswith('buf_act_')})
+    return out
 
 
 def _worker(rank, world, port, cfg, layers, path):
@@ -151,6 +157,33 @@ def test_gptq_token_shards_bit_identical(dev, name, cfg, tmp_path):
     for k in ('RANK', 'WORLD_SIZE'):
         os.environ.pop(k, None)
     single = _run(cfg, 2)
+    multi = _two_ranks(cfg, 2, tmp_path)
+    assert single.keys() == multi.keys()
+    for k in single:
+        assert torch.equal(single[k], multi[k]), k
+
+
+def _static_act(entries, algo):
+    q = {k: dict(v) if isinstance(v, dict) else v for k, v in GPTQ_TOK_FLOAT['quant'].items()}
+    q['act'] = {'bit': 8, 'symmetric': algo != 'static_moving_minmax', 'granularity': 'per_tensor',
+                'static': True, 'calib_algo': algo}
+    return {'quant': q, 'deploy': 'fake_quant', 'entries': entries}
+
+
+@pytest.mark.parametrize('entries,algo', [((4,), 'static_minmax'),
+                                          ((3, 1), 'static_minmax'),
+                                          ((1, 2, 1), 'static_moving_minmax')])
+def test_static_act_qparams_token_shards_bit_identical(dev, entries, algo, tmp_path):
+    """Static per-tensor activation calibration (register_act_qparams,
+    base_blockwise_quantization.py:567-588) under shard_tokens: per-sample (min, max) gathered
+    in global order and folded into the reference's segments (samples of one batch, or entries
+    -- (3, 1) cuts entry 0 between the ranks), so buf_act_* and every GPTQ weight equal one
+    GPU's."""
+    for k in ('RANK', 'WORLD_SIZE'):
+        os.environ.pop(k, None)
+    cfg = _static_act(entries, algo)
+    single = _run(cfg, 2)
+    assert any('buf_act_scales_0' in k for k in single)
     multi = _two_ranks(cfg, 2, tmp_path)
     assert single.keys() == multi.keys()
     for k in single:
