@@ -753,7 +753,8 @@ def bench_fp8_forward(args, weights, dev, world):
                                      'tiles of every expert in one launch)', 'bound': 'mfma',
                            'achieved': round(tf, 1), 'peak': PEAK_FP8_TFLOPS, 'unit': 'TFLOP/s',
                            'frac': round(tf / PEAK_FP8_TFLOPS, 4), 'traffic': traffic,
-                           'traffic_source': src, 'flops_per_launch': flops / 3,
+                           'traffic_source': src,
+                           'flops_per_launch': flops * args.steps / t['launches'],
                            'avg_launch_ms': round(t['avg_ms'], 4)}
     return out
 

@@ -489,12 +489,16 @@ int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const void* b_s,
  * wtab: DEVICE int64 [nsets][G][2] = (weight [N, K] e4m3 16-byte aligned, block scales fp32
  * [ceil(N/128), K/128]) addresses; nsets 1 or 2 (gate and up of the same rows in one launch).
  * c [nsets][rows][N] (c_dtype). Every row equals what lcq_fp8_gemm computes for it on an
- * unsplit 256^2 plan. `workspace`: lcq_fp8_gemm_grouped_workspace_bytes(rows, G, N, K). */
+ * unsplit 256^2 plan. silu_mul (nsets 2, c_dtype BF16): set 0 = gate, set 1 = up, and c
+ * [rows][N] receives h = rnd(rnd(silu(rnd(gate))) * rnd(up)) (the expert MLP's
+ * act_fn(gate_proj(x)) * up_proj(x) on its bf16 projections, which are never stored).
+ * `workspace`: lcq_fp8_gemm_grouped_workspace_bytes(rows, G, silu_mul ? 2 N : N, K). */
 int64_t lcq_fp8_gemm_grouped_workspace_bytes(int64_t rows, int64_t G, int64_t N, int64_t K);
 int lcq_fp8_gemm_grouped(const void* a, const void* a_s, int64_t a_rows_total,
                          const int64_t* a_rows, int64_t rows, const int64_t* row_off,
-                         const int64_t* wtab, int64_t G, int nsets, int64_t N, int64_t K,
-                         void* c, int c_dtype, void* workspace, int64_t ws_bytes, void* stream);
+                         const int64_t* wtab, int64_t G, int nsets, int silu_mul, int64_t N,
+                         int64_t K, void* c, int c_dtype, void* workspace, int64_t ws_bytes,
+                         void* stream);
 
 /* MoE combine (the expert loop's `out.index_add_(0, tok, (h_e * w).to(out.dtype))` over hit
  * experts in ascending index; reference models/deepseekv3.py MoE forward): out [T, H] bf16,

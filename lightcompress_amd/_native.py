@@ -101,8 +101,8 @@ SIGNATURES = {
     'lcq_fp8_gemm': ([_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp],
                      _int),
     'lcq_fp8_gemm_workspace_bytes': ([_i64, _i64, _i64], _i64),
-    'lcq_fp8_gemm_grouped': ([_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _int, _i64, _i64,
-                              _vp, _int, _vp, _i64, _vp], _int),
+    'lcq_fp8_gemm_grouped': ([_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _int, _int, _i64,
+                              _i64, _vp, _int, _vp, _i64, _vp], _int),
     'lcq_moe_combine': ([_vp, _vp, _vp, _vp, _int, _i64, _int, _i64, _vp, _vp], _int),
     'lcq_fp8_gemm_grouped_workspace_bytes': ([_i64, _i64, _i64, _i64], _i64),
     'lcq_rotary': ([_vp, _vp, _vp, _vp, _int, _i64, _i64, _int, _int, _int, _i64, _vp, _vp, _vp],

@@ -372,12 +372,25 @@ def _same(a, b):
 
 
 def _batchable(inputs, kwargs):
-    """Several entries of equal shape whose kwargs (rotary tables, masks, positions) agree;
-    a per-sample attention mask (padding) keeps the per-sample loop."""
+    """Several entries of equal sample shape whose kwargs (rotary tables, masks, positions)
+    agree; a per-sample attention mask (padding) keeps the per-sample loop. Entries of
+    different batch sizes (calibration sets of unequal batches, or a token shard that cut an
+    entry) stack only when no kwarg tensor carries a batch dim."""
     if len(inputs) < 2 or len(kwargs) != len(inputs):
         return False
     s0 = inputs[0].shape
-    if any(x.shape != s0 for x in inputs):
+    if any(x.shape[1:] != s0[1:] for x in inputs):
+        return False
+    def tensors(v):
+        if torch.is_tensor(v):
+            yield v
+        elif isinstance(v, (tuple, list)):
+            for u in v:
+                yield from tensors(u)
+
+    if any(x.shape[0] != s0[0] for x in inputs) and any(
+            t.dim() > 0 and t.shape[0] > 1
+            for kw in kwargs for v in kw.values() for t in tensors(v)):
         return False
     if any(torch.is_tensor(v) and v.dim() > 0 and v.shape[0] == s0[0] and k == 'attention_mask'
            for k, v in kwargs[0].items()):

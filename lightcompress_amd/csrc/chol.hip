@@ -537,7 +537,8 @@ __global__ void __launch_bounds__(256, 2) k_gemm_f32(Args a) {
 // (MFMA busy ~55 %, profiles/r3c_gemm_pmc.txt). Here:
 //  * 32-float K chunks of T rows land in LDS by buffer_load ... lds (16 B per lane, 8 rows x
 //    128 B per wave-instruction; rows / columns past the operand's end read as zero through
-//    the buffer descriptor's range) in an NS-stage ring, one barrier per chunk;
+//    the buffer descriptor's range) in an NS-stage ring (2: one chunk in flight while the
+//    other is multiplied), one barrier per chunk;
 //  * v_mfma_f32_16x16x4_f32 with the chunk's k permuted: lane group g = lane >> 4 supplies k =
 //    8g + s at step s (0..7) for both operands, so a lane's 8 values of a k-contiguous row are
 //    two ds_read_b128 (16-B chunks 2g, 2g + 1 of the row, swizzled by swz32 so that every
@@ -707,7 +708,8 @@ __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds, int6
 }
 
 #ifndef LCQ_F32D_NS
-#define LCQ_F32D_NS 3
+#define LCQ_F32D_NS 2  // measured against 3 on the chain's shapes: 77-93 -> 96-114 TF/s,
+                       // 4096^3 110 -> 136 (profiles/r4_f32_variants.txt)
 #endif
 #ifndef LCQ_F32D_OCC
 #define LCQ_F32D_OCC 1

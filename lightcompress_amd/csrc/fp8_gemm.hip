@@ -237,6 +237,8 @@ struct Gemm2Args {
   int64_t ast_elems;  // a_s floats readable from ast (the grouped kernel shifts ast per group)
   const int64_t* arows;  // grouped, gathered A: tile row i reads A row arows[i] (null: a + i)
   int64_t a_bytes;       // bytes of A behind `a` when gathered
+  const uint8_t* b2;     // SILU pair mode: the up weight (b = gate) and its block-scales
+  const float* bs2;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
@@ -278,9 +280,17 @@ __device__ __forceinline__ bool tile_of_slot(const Gemm2Args& g, int& tm, int& t
   return tm < g.nmt && tn < g.nnt;
 }
 
-template <int TM, int WR, int WC, int NS>
+// SILU (256^2, 8 waves only): the pair mode of the grouped MoE gate / up projection. The tile
+// covers 128 output columns n0h = 128 tn of BOTH weights: virtual B row v (0..255) is gate
+// (bit 5 of v clear) or up (set) column n0h + 32 (v >> 6) + (v & 31), so each wave's 64 tile
+// columns hold 32 gate and the same 32 up columns (its accumulator blocks nb 0-1 and 2-3) and
+// the epilogue writes h = rnd(rnd(silu(rnd(g))) * rnd(u)) (LlamaMLP / DeepseekV3MLP
+// act_fn(gate_proj(x)) * up_proj(x) on the bf16 projections) -- neither projection is
+// stored. A staging wave loads only gate (waves 0-3) or only up (4-7) rows.
+template <int TM, int WR, int WC, int NS, bool SILU = false>
 __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int tm, int tn,
                                            int kz) {
+  static_assert(!SILU || (TM == 256 && WR == 2 && WC == 4), "pair mode: 256^2, 2 x 4 waves");
   constexpr int NW = WR * WC;                 // waves
   constexpr int OPB = TM * BK;                // one operand tile
   constexpr int STG = stage_bytes<TM>();
@@ -292,7 +302,7 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w / WC, wc = w % WC;
-  const int64_t m0 = (int64_t)tm * TM, n0 = (int64_t)tn * TM;
+  const int64_t m0 = (int64_t)tm * TM, n0 = SILU ? (int64_t)tn * (TM / 2) : (int64_t)tn * TM;
   const int64_t nkb = g.K / BK;
   const int64_t kb0 = (int64_t)kz * g.kb_per_split;
   int64_t nk = nkb - kb0;
@@ -302,14 +312,20 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
   // 64 lanes x 16 B; lane l -> row l / 8, physical chunk l % 8 = logical chunk (l % 8) ^ swz(row)
   const __amdgpu_buffer_rsrc_t ra =
       g.arows ? rsrc(g.a, g.a_bytes) : rsrc(g.a + m0 * g.K, (g.M - m0) * g.K);
-  const __amdgpu_buffer_rsrc_t rb = rsrc(g.b + n0 * g.K, (g.N - n0) * g.K);
+  const __amdgpu_buffer_rsrc_t rb =
+      rsrc((SILU && w >= 4 ? g.b2 : g.b) + n0 * g.K, (g.N - n0) * g.K);
   const __amdgpu_buffer_rsrc_t rs = rsrc(g.ast + m0, (g.ast_elems - m0) * 4);
-  uint32_t off[PIECES], aoff[PIECES];
+  uint32_t off[PIECES], aoff[PIECES], boff[PIECES];
 #pragma unroll
   for (int j = 0; j < PIECES; ++j) {
     const int row = j * 8 * NW + w * 8 + (lane >> 3);
     off[j] = (uint32_t)(row * g.K + (((lane & 7) ^ swz(row)) * 16));
     aoff[j] = off[j];
+    boff[j] = off[j];
+    if (SILU) {  // virtual row -> column of the gate / up weight
+      const int r = (row >> 6) * 32 + (row & 31);
+      boff[j] = (uint32_t)(r * g.K + (((lane & 7) ^ swz(row)) * 16));
+    }
     if (g.arows) {  // gathered rows; rows past M read past the descriptor's range: zeros
       const int64_t m = m0 + row;
       aoff[j] = m < g.M ? (uint32_t)(g.arows[m] * g.K + (((lane & 7) ^ swz(row)) * 16))
@@ -326,7 +342,7 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
                                                16, aoff[j], kofs, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(dst + OPB +
                                                                  (j * 8 * NW + w * 8) * BK),
-                                               16, off[j], kofs, 0, 0);
+                                               16, boff[j], kofs, 0, 0);
     }
     // a_s of this K block: TM floats = TM / 64 pieces of 64 lanes x 4 B; wave w loads piece
     // w % (TM / 64) (the waves past TM / 64 write the same bytes again) so that every wave
@@ -350,12 +366,12 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
   float* bsl = reinterpret_cast<float*>(lds + NS * STG);
   for (int i = tid; i < (TM / 128) * nk; i += 64 * NW) {
     const int cb = i / (int)nk, t = i - cb * (int)nk;
-    int64_t nb = (n0 >> 7) + cb;
+    int64_t nb = (n0 >> 7) + (SILU ? 0 : cb);   // SILU: cb 0 = gate's block, 1 = up's
     if (nb > (g.N - 1) >> 7) nb = (g.N - 1) >> 7;  // clamped past N (columns never stored)
-    bsl[i] = g.bs[nb * nkb + kb0 + t];
+    bsl[i] = (SILU && cb ? g.bs2 : g.bs)[nb * nkb + kb0 + t];
   }
   __syncthreads();
-  const float* bsrow = bsl + ((wc * WN) >> 7) * nk;  // this wave's 128-column scale block
+  const float* bsrow = bsl + (SILU ? 0 : ((wc * WN) >> 7) * nk);  // the wave's scale block
 
   // NS-stage ring: NS - 1 K blocks in flight ahead of the one being multiplied
 #pragma unroll
@@ -370,13 +386,27 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
     const uint8_t* Bt = At + OPB;
     const float* Sa = reinterpret_cast<const float*>(At + 2 * OPB);
     const float bsv = bsrow[t];
+    const float bsv2 = SILU ? bsrow[nk + t] : bsv;  // up's block-scale (nb >= NB / 2)
+    // every LDS read of the K block issued before the first MFMA waits on any of them
+    float sa[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) sa[mb] = Sa[wr * WM + mb * 16 + r16];
     v8i bfr[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) bfr[nb] = frag2(Bt, wc * WN + nb * 16 + r16, q);
-    float sc[MB];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) sc[mb] = Sa[wr * WM + mb * 16 + r16] * bsv;
     v8i afr = frag2(At, wr * WM + r16, q);
+    // software-pipelined: the scaled accumulation of row block mb - 1 runs while row block
+    // mb's MFMAs are in flight (no VALU read of a result the MFMA pipe has just begun)
+    v4f dprev[NB];
+    auto accumulate = [&](int mb) {
+      const float s1 = sa[mb] * bsv, s2 = SILU ? sa[mb] * bsv2 : s1;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[mb][nb][j] = __builtin_fmaf(dprev[nb][j], (SILU && nb >= NB / 2) ? s2 : s1,
+                                          acc[mb][nb][j]);
+    };
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       v8i anext = afr;
@@ -386,16 +416,40 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
       for (int nb = 0; nb < NB; ++nb)
         d[nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[nb], afr, zero, 0, 0, 0, 0,
                                                                   0, 0);
+      if (mb > 0) accumulate(mb - 1);
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[mb][nb][j] = __builtin_fmaf(d[nb][j], sc[mb], acc[mb][nb][j]);
+      for (int nb = 0; nb < NB; ++nb) dprev[nb] = d[nb];
       afr = anext;
     }
+    accumulate(MB - 1);
     __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  if constexpr (SILU) {  // h[m][n0 + 32 wc + 16 nb + 4q + j] from acc[mb][nb] (gate), [nb + 2] (up)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int64_t m = m0 + wr * WM + mb * 16 + r16;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int nb = 0; nb < NB / 2; ++nb) {
+        const int64_t n = n0 + wc * 32 + nb * 16 + 4 * q;
+        if (n >= g.N) continue;
+        float h[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float gg = rnd<LCQ_BF16>(acc[mb][nb][j]);
+          const float u = rnd<LCQ_BF16>(acc[mb][nb + NB / 2][j]);
+          h[j] = rnd<LCQ_BF16>(rnd<LCQ_BF16>(gg / (1.0f + expf(-gg))) * u);
+        }
+        uint2 o;
+        o.x = pack2<LCQ_BF16>(h[0], h[1]);
+        o.y = pack2<LCQ_BF16>(h[2], h[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(g.c) + m * g.N + n) = o;
+      }
+    }
+    return;
+  }
   // acc[mb][nb][j] (swapped layout): C[m0 + wr*WM + mb*16 + r16][n0 + wc*WN + nb*16 + 4q + j]
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
@@ -471,9 +525,10 @@ struct GroupedArgs {
   const int* tmap;       // [slots]: group of each slot
   const int64_t* arows;  // sorted row -> A row, or null (A already sorted)
   int64_t a_bytes;
-  void* c;               // [nsets][rows][N]
+  void* c;               // [nsets][rows][N], or [rows][N] (silu)
   int64_t N, K, mp, rows;
   int G, c_dt, nnt, nsets;
+  int silu;              // nsets 2 as gate / up, h = act(gate) * up stored (the pair mode)
 };
 
 __global__ __launch_bounds__(256) void k_group_tiles(const int64_t* __restrict__ row_off, int G,
@@ -500,15 +555,16 @@ __global__ __launch_bounds__(256) void k_group_tiles(const int64_t* __restrict__
   for (int i = tid; i < mine; i += 256) tmap[base + i] = g;
 }
 
-__global__ __launch_bounds__(512, 1) void k_fp8_gemm2_grouped(GroupedArgs ga) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+__device__ __forceinline__ void grouped_body(const GroupedArgs& ga, uint8_t* lds,
+                                             const bool SILU) {
   const int bid = blockIdx.x;
-  const int total = __builtin_amdgcn_readfirstlane(ga.tile0[ga.G]) * ga.nsets;
+  const int sets = SILU ? 1 : ga.nsets;   // the pair mode's tile holds both weights
+  const int total = __builtin_amdgcn_readfirstlane(ga.tile0[ga.G]) * sets;
   const int q = (total + 7) >> 3;
   const int j = bid >> 3, vs = (bid & 7) * q + j;
   if (j >= q || vs >= total) return;  // the grid covers 8 q slots (host bound)
   // the weight sets of one tile are consecutive slots (they read the same A rows)
-  const int slot = vs / ga.nsets, set = vs - slot * ga.nsets;
+  const int slot = vs / sets, set = vs - slot * sets;
   const int grp = __builtin_amdgcn_readfirstlane(ga.tmap[slot]);
   const int64_t r0 = ga.row_off[grp], M = ga.row_off[grp + 1] - r0;
   const int l = slot - ga.tile0[grp];
@@ -536,8 +592,23 @@ __global__ __launch_bounds__(512, 1) void k_fp8_gemm2_grouped(GroupedArgs ga) {
               static_cast<uint8_t*>(ga.c) +
                   ((int64_t)set * ga.rows + r0) * ga.N * (ga.c_dt == LCQ_F32 ? 4 : 2),
               nullptr, M, ga.N, ga.K, ga.mp, nkb, ga.c_dt, nmt, ga.nnt,
-              ga.mp * nkb - r0, ga.arows ? ga.arows + r0 : nullptr, ga.a_bytes};
-  gemm2_body<256, 2, 4, NS256>(g, lds, tm, tn, 0);
+              ga.mp * nkb - r0, ga.arows ? ga.arows + r0 : nullptr, ga.a_bytes,
+              SILU ? reinterpret_cast<const uint8_t*>(ga.wtab[2 * ((int64_t)ga.G + grp)])
+                   : nullptr,
+              SILU ? reinterpret_cast<const float*>(ga.wtab[2 * ((int64_t)ga.G + grp) + 1])
+                   : nullptr};
+  if (SILU) gemm2_body<256, 2, 4, NS256, true>(g, lds, tm, tn, 0);
+  else gemm2_body<256, 2, 4, NS256, false>(g, lds, tm, tn, 0);
+}
+
+__global__ __launch_bounds__(512, 1) void k_fp8_gemm2_grouped(GroupedArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  grouped_body(ga, lds, false);
+}
+
+__global__ __launch_bounds__(512, 1) void k_fp8_gemm2_grouped_silu(GroupedArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  grouped_body(ga, lds, true);
 }
 
 // a_s [M, nkb] -> [nkb, mp] (rows past M zero)
@@ -665,7 +736,7 @@ extern "C" int lcq_fp8_gemm(const void* a, const void* a_s, const void* b, const
     Gemm2Args g2{static_cast<const uint8_t*>(a), static_cast<const uint8_t*>(b), ast,
                  static_cast<const float*>(b_s), c, part, M, N, K, mp,
                  (nkb + s2 - 1) / s2, c_dtype, (int)((M + pl.tm - 1) / pl.tm),
-                 (int)((N + pl.tm - 1) / pl.tm), nkb * mp, nullptr, 0};
+                 (int)((N + pl.tm - 1) / pl.tm), nkb * mp, nullptr, 0, nullptr, nullptr};
     const int nslots = 32 * ((g2.nmt + 3) / 4) * ((g2.nnt + 7) / 8);
     // stage ring + the split's block-scales (TM / 128 column blocks x K blocks per split)
     const int bsb = (int)(((pl.tm / 128) * g2.kb_per_split * 4 + 15) / 16 * 16);
@@ -736,11 +807,14 @@ extern "C" int64_t lcq_fp8_gemm_grouped_workspace_bytes(int64_t rows, int64_t G,
 extern "C" int lcq_fp8_gemm_grouped(const void* a, const void* a_s, int64_t a_rows_total,
                                     const int64_t* a_rows, int64_t rows,
                                     const int64_t* row_off, const int64_t* wtab, int64_t G,
-                                    int nsets, int64_t N, int64_t K, void* c, int c_dtype,
-                                    void* workspace, int64_t ws_bytes, void* stream) {
+                                    int nsets, int silu_mul, int64_t N, int64_t K, void* c,
+                                    int c_dtype, void* workspace, int64_t ws_bytes,
+                                    void* stream) {
   LCQ_REQUIRE(a && a_s && row_off && wtab && c && workspace, "null pointer");
   LCQ_REQUIRE(rows >= 0 && G > 0 && G <= (1 << 20) && N > 0 && K > 0, "bad grouped shape");
   LCQ_REQUIRE(nsets == 1 || nsets == 2, "nsets must be 1 or 2");
+  LCQ_REQUIRE(!silu_mul || (nsets == 2 && c_dtype == LCQ_BF16),
+              "silu_mul pairs two weight sets (gate, up) into a bf16 output");
   LCQ_REQUIRE(a_rows ? (a_rows_total >= 0 && a_rows_total * K < ((int64_t)1 << 31))
                      : a_rows_total == rows,
               "gathered A must be < 2 GiB; ungathered A has `rows` rows");
@@ -751,7 +825,9 @@ extern "C" int lcq_fp8_gemm_grouped(const void* a, const void* a_s, int64_t a_ro
   LCQ_REQUIRE(c_dtype == LCQ_F32 || c_dtype == LCQ_BF16 || c_dtype == LCQ_F16,
               "C dtype must be F32, BF16 or F16");
   LCQ_REQUIRE((reinterpret_cast<uintptr_t>(a) & 15) == 0, "A must be 16-byte aligned");
-  LCQ_REQUIRE(ws_bytes >= lcq_fp8_gemm_grouped_workspace_bytes(rows, G, N, K),
+  // the pair mode's tiles are 128 output columns of two weights: the slot count of 2 N
+  const int64_t NT = silu_mul ? 2 * N : N;
+  LCQ_REQUIRE(ws_bytes >= lcq_fp8_gemm_grouped_workspace_bytes(rows, G, NT, K),
               "workspace too small");
   if (rows == 0) return LCQ_OK;
   hipStream_t st = as_stream(stream);
@@ -759,22 +835,29 @@ extern "C" int lcq_fp8_gemm_grouped(const void* a, const void* a_s, int64_t a_ro
   float* ast = static_cast<float*>(workspace);
   int* tile0 = reinterpret_cast<int*>(ast + nkb * mp);
   int* tmap = tile0 + (G + 1);
-  const int64_t bound = grouped_slot_bound(rows, G, N);
-  LCQ_REQUIRE(bound * nsets < ((int64_t)1 << 30), "too many tiles");
+  const int64_t bound = grouped_slot_bound(rows, G, NT);
+  const int sets = silu_mul ? 1 : nsets;
+  LCQ_REQUIRE(bound * sets < ((int64_t)1 << 30), "too many tiles");
   hipLaunchKernelGGL(k_as_transpose, dim3((unsigned)((nkb * mp + 255) / 256)), 256, 0, st,
                      static_cast<const float*>(a_s), rows, nkb, mp, ast, a_rows);
-  const int nnt = (int)((N + 255) / 256);
+  const int nnt = (int)((NT + 255) / 256);
   hipLaunchKernelGGL(k_group_tiles, dim3((unsigned)G), 256, 0, st, row_off, (int)G, nnt, tile0,
                      tmap);
   GroupedArgs ga{static_cast<const uint8_t*>(a), ast, row_off, wtab, tile0, tmap, a_rows,
-                 a_rows_total * K, c, N, K, mp, rows, (int)G, c_dtype, nnt, nsets};
+                 a_rows_total * K, c, N, K, mp, rows, (int)G, c_dtype, nnt, nsets, silu_mul};
   const int bsb = (int)((2 * nkb * 4 + 15) / 16 * 16);
   const int L = NS256 * stage_bytes<256>() + bsb;
   LCQ_REQUIRE(L <= 160 * 1024, "K too large for the staged block-scales");
-  (void)hipFuncSetAttribute((const void*)k_fp8_gemm2_grouped,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, L);
   // the slot bound rounded to 8 XCD lanes (the kernel's q never exceeds bound / 8 rounded up)
-  const int64_t grid = (bound * nsets + 7) / 8 * 8;
-  hipLaunchKernelGGL(k_fp8_gemm2_grouped, dim3((unsigned)grid), 512, L, st, ga);
+  const int64_t grid = (bound * sets + 7) / 8 * 8;
+  if (silu_mul) {
+    (void)hipFuncSetAttribute((const void*)k_fp8_gemm2_grouped_silu,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, L);
+    hipLaunchKernelGGL(k_fp8_gemm2_grouped_silu, dim3((unsigned)grid), 512, L, st, ga);
+  } else {
+    (void)hipFuncSetAttribute((const void*)k_fp8_gemm2_grouped,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, L);
+    hipLaunchKernelGGL(k_fp8_gemm2_grouped, dim3((unsigned)grid), 512, L, st, ga);
+  }
   return check_launch("lcq_fp8_gemm_grouped");
 }

@@ -53,8 +53,8 @@ class ExpertList(nn.ModuleList):
     # registers them and then takes the loop), the experts run as grouped GEMMs instead: the
     # token slots are sorted by expert on the device (no host sync), act_quant runs once per
     # token (it is per row), one lcq_fp8_gemm_grouped launch computes gate and up of every
-    # expert (the kernel gathers each slot's token row), act_fn(gate) * up as the MLP computes
-    # it, one launch for down, then lcq_moe_combine in the loop's order (per token, experts in
+    # expert (the kernel gathers each slot's token row) and, for SiLU, act_fn(gate) * up in its
+    # epilogue as the MLP computes it on the bf16 projections; one launch for down, then lcq_moe_combine in the loop's order (per token, experts in
     # ascending index, each product rounded to bf16 before its add, as index_add_ does).
     # Every row's GEMM value equals lcq_fp8_gemm's on an unsplit 256^2 plan.
     def _grouped_fp8_ok(self, x) -> bool:
@@ -115,10 +115,16 @@ class ExpertList(nn.ModuleList):
             slot_row[order] = torch.arange(order.numel(), device=order.device)
         # act_quant is per token row: quantize each token once, the GEMM gathers its k copies
         xq, xs = act_quant(hidden_states.contiguous(), 128)
-        gu = ops.fp8_gemm_grouped(xq, xs.reshape(-1), row_off, gate_up, inter, cdt,
-                                  a_rows=order // k).to(torch.bfloat16)
-        h = (self[0].act_fn(gu[0]) * gu[1]).contiguous()
-        del gu, xq, xs
+        if cdt == torch.bfloat16 and getattr(self[0].config, 'hidden_act', None) == 'silu':
+            # act_fn(gate) * up in the GEMM epilogue (the bf16 projections never stored)
+            h = ops.fp8_gemm_grouped(xq, xs.reshape(-1), row_off, gate_up, inter, cdt,
+                                     a_rows=order // k, silu_mul=True)
+        else:
+            gu = ops.fp8_gemm_grouped(xq, xs.reshape(-1), row_off, gate_up, inter, cdt,
+                                      a_rows=order // k).to(torch.bfloat16)
+            h = (self[0].act_fn(gu[0]) * gu[1]).contiguous()
+            del gu
+        del xq, xs
         hq, hs = act_quant(h, 128)
         del h
         y = ops.fp8_gemm_grouped(hq, hs.reshape(-1), row_off, down, H, cdt).to(torch.bfloat16)

@@ -475,17 +475,12 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     elif group is None or static:
         s_in = fixed[0].reshape(-1).float().contiguous()
         z_in = None if sym else fixed[1].reshape(-1).float().contiguous()
-    # Near-column updates, pipelined: after block j only the next block's columns are on the
-    # critical path, so they are updated first on the main stream; the rest of the superblock
-    # takes block j's errors on a side stream while block j + 1's (latency-bound, few
-    # workgroups) kernel runs. Each column still receives the blocks' errors in block order
-    # (the next near update waits for the previous side update), so W is bit-identical to
-    # the sequential order.
-    side = _side_stream(dev, 'near') if W.is_cuda else None
-    main = torch.cuda.current_stream(dev) if side is not None else None
+    # (Splitting each near update into the next block's columns on the compute stream and the
+    # rest on a side stream beside the next block kernel measured slower on every Llama-3-8B
+    # subset shape, e.g. 17.4 -> 19.4 ms at 4096 x 14336: scripts/column_loop_rate.py,
+    # profiles/r4_column_loop.txt.)
     for sb0 in range(0, ncq, SB):
         sb1 = min(sb0 + SB, ncq)
-        pending = None   # the side stream's last near update
         for i1 in range(sb0, sb1, BLOCK):
             i2 = min(i1 + BLOCK, sb1)
             cnt = i2 - i1
@@ -501,23 +496,8 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
             else:
                 ops.gptq_block(W, i1, cnt, U, group or 0, qmin, qmax, sym, s_out, z_out, e, L,
                                s_in, z_in, fp8=fp8)
-            if i2 < sb1 and side is None:  # near columns: the rest of this superblock
+            if i2 < sb1:  # near columns: the rest of this superblock
                 ops.gptq_trailing(W, i1, cnt, i2, e, U, c2=sb1)
-            elif i2 < sb1:
-                i3 = min(i2 + BLOCK, sb1)
-                if pending is not None:   # block j - 1's errors are in [i2, sb1) first
-                    main.wait_event(pending)
-                ops.gptq_trailing(W, i1, cnt, i2, e, U, c2=i3)
-                if i3 < sb1:
-                    ready = torch.cuda.Event()
-                    ready.record(main)
-                    side.wait_event(ready)
-                    with torch.cuda.stream(side):
-                        ops.gptq_trailing(W, i1, cnt, i3, e, U, c2=sb1)
-                    pending = torch.cuda.Event()
-                    pending.record(side)
-        if side is not None:
-            main.wait_stream(side)   # errT is rewritten by the next superblock
         if sb1 < cols:    # far columns: the whole superblock's errors at once
             ops.gptq_trailing(W, sb0, sb1 - sb0, sb1, errT, U, c2=cols)
     if searched:

@@ -913,7 +913,8 @@ def fp8_weight_table(weights, device) -> torch.Tensor:
 
 def fp8_gemm_grouped(a: torch.Tensor, a_s: torch.Tensor, row_off: torch.Tensor,
                      wtab: torch.Tensor, n: int, out_dtype: torch.dtype = torch.bfloat16,
-                     a_rows: torch.Tensor | None = None) -> torch.Tensor:
+                     a_rows: torch.Tensor | None = None, silu_mul: bool = False
+                     ) -> torch.Tensor:
     """One launch of G block-scaled fp8 GEMMs (the routed experts of an MoE projection), for
     one or two weight sets. Rows: the token slots sorted by group, row_off int64 [G + 1] on
     the device (group g = rows [row_off[g], row_off[g + 1])). a [R, K] e4m3 with a_s [R, K/128]
@@ -921,7 +922,9 @@ def fp8_gemm_grouped(a: torch.Tensor, a_s: torch.Tensor, row_off: torch.Tensor,
     the gather happens in the kernel -- else a itself is sorted (rows = R). wtab from
     fp8_weight_table, [G, 2] or [2, G, 2] (two sets: gate and up of the same rows), all [n, K].
     Returns c [rows, n], or [2, rows, n] for two sets; each row equals fp8_gemm's on an
-    unsplit 256^2 plan."""
+    unsplit 256^2 plan. ``silu_mul`` (two sets = gate, up; bf16): returns h [rows, n] =
+    rnd(rnd(silu(rnd(gate))) * rnd(up)), the expert MLP's act_fn(gate) * up, with neither
+    projection stored."""
     if a.dtype != torch.float8_e4m3fn or not a.is_contiguous() or a.dim() != 2:
         raise TypeError('a must be a contiguous 2-D float8_e4m3fn tensor')
     R, K = a.shape
@@ -944,15 +947,19 @@ def fp8_gemm_grouped(a: torch.Tensor, a_s: torch.Tensor, row_off: torch.Tensor,
         rows = a_rows.numel()
     else:
         rows = R
-    shape = (rows, n) if nsets == 1 else (nsets, rows, n)
+    if silu_mul and (nsets != 2 or out_dtype != torch.bfloat16):
+        raise ValueError('silu_mul takes the gate and up tables ([2, G, 2]) and a bf16 output')
+    shape = (rows, n) if nsets == 1 or silu_mul else (nsets, rows, n)
     c = torch.empty(shape, dtype=out_dtype, device=a.device)
     if rows == 0:
         return c
-    wsb = int(N.load().lcq_fp8_gemm_grouped_workspace_bytes(rows, G, n, K))
+    wsb = int(N.load().lcq_fp8_gemm_grouped_workspace_bytes(rows, G, 2 * n if silu_mul else n,
+                                                            K))
     ws = torch.empty(wsb, dtype=torch.uint8, device=a.device)
     N.call('lcq_fp8_gemm_grouped', N.ptr(a), N.ptr(a_s), R,
            None if a_rows is None else N.ptr(a_rows), rows, N.ptr(row_off), N.ptr(wtab), G,
-           nsets, n, K, N.ptr(c), N.dt(out_dtype), N.ptr(ws), wsb, N.stream_of(a))
+           nsets, int(bool(silu_mul)), n, K, N.ptr(c), N.dt(out_dtype), N.ptr(ws), wsb,
+           N.stream_of(a))
     return c
 
 
@@ -1000,7 +1007,8 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
     largest tensor, so weights of very different sizes (a DeepSeek-V3 layer: o_proj 117 M
     elements, kv_a 4 M, experts 15 M) go in size classes -- one launch pair per class of
     tensors within 2x of each other -- instead of every small tensor carrying the largest one's
-    idle workgroups."""
+    idle workgroups. (Cutting a class into pairs of <= 96 MB, so that the requant pass would
+    re-read the codes from the MALL, measured slower: 1.05 -> 1.29 ms per DSv3 layer.)"""
     n = len(codes)
     if n == 0:
         return [], torch.empty(0)

@@ -7,7 +7,7 @@ from pathlib import Path
 import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-from lightcompress_amd import gptq_core  # noqa: E402
+from lightcompress_amd import gptq_core, ops  # noqa: E402
 
 dev = torch.device('cuda:0')
 for n in (4096, 14336):
@@ -15,9 +15,12 @@ for n in (4096, 14336):
     X = torch.randn(n, 2 * n, device=dev, generator=g)
     H = X @ X.T / (2 * n)
     H.diagonal().add_(0.01)
-    for ov, graph in ((10 ** 9, False), (1024, False), (1024, True)):
+    for ov, graph, sk in ((10 ** 9, False, True), (1024, False, True), (1024, True, True),
+                          (1024, True, False)):
         gptq_core._OVERLAP_MIN = ov
         gptq_core.CHAIN_GRAPHS = graph
+        ops.STREAM_K = sk
+        gptq_core.clear_chain_graphs()
         U0 = gptq_core.inverse_cholesky_upper(H.clone())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 3
@@ -26,6 +29,7 @@ for n in (4096, 14336):
             U = gptq_core.inverse_cholesky_upper(H.clone())
         e1.record()
         torch.cuda.synchronize()
-        print(f'n {n} overlap_min {ov} graph {graph}: {e0.elapsed_time(e1) / reps:.2f} ms per chain '
+        print(f'n {n} overlap_min {ov} graph {graph} stream_k {sk}: '
+              f'{e0.elapsed_time(e1) / reps:.2f} ms per chain '
               f'(incl. one H copy); identical to the first run: {torch.equal(U, U0)}', flush=True)
     print(flush=True)

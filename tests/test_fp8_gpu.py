@@ -450,6 +450,30 @@ def test_fp8_gemm_grouped_gather_and_two_sets(dev):
         assert torch.equal(both[i], one), i
 
 
+def test_fp8_gemm_grouped_silu_mul_equals_two_sets(dev):
+    """The pair mode (gate and up tiles in one workgroup, act_fn(gate) * up in the epilogue)
+    equals torch's silu(gate) * up on the two-set launch's bf16 projections, bit for bit,
+    ragged groups and a partial 128-column block included."""
+    from lightcompress_amd import ops
+    counts, Nn, K = [300, 0, 77, 513], 384 + 64, 512
+    g = torch.Generator().manual_seed(9)
+    T = 500
+    x = torch.randn(T, K, generator=g) * torch.exp(torch.randn(T, 1, generator=g))
+    a, a_s = O.act_quant(x)
+    rows = torch.randint(0, T, (sum(counts),), generator=g).to(dev)
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int64).to(dev)
+    keep = [[tuple(t.to(dev) for t in O.weight_cast_to_fp8(
+        torch.randn(Nn, K, generator=g) * 0.2)) for _ in counts] for _ in range(2)]
+    tab = torch.stack([ops.fp8_weight_table(ws, dev) for ws in keep])
+    ad, asd = a.to(dev), a_s.to(dev).reshape(-1)
+    gu = ops.fp8_gemm_grouped(ad, asd, off, tab, Nn, torch.bfloat16, a_rows=rows)
+    h = ops.fp8_gemm_grouped(ad, asd, off, tab, Nn, torch.bfloat16, a_rows=rows,
+                             silu_mul=True)
+    want = torch.nn.functional.silu(gu[0]) * gu[1]
+    assert h.shape == want.shape
+    assert torch.equal(h.view(torch.int16), want.view(torch.int16))
+
+
 @pytest.mark.parametrize('wdt', [torch.float32, torch.bfloat16])
 def test_moe_combine_equals_index_add_loop(dev, wdt):
     """lcq_moe_combine == the expert loop's combine: out.index_add_(0, tok, (y_e * w).to(bf16))
