@@ -332,26 +332,41 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
                         : 0x80000000u;
     }
   }
-  auto stage = [&](int buf, int64_t kbl) {  // kbl: K block index within the split
+  // A pieces + the K block's a_s (stage_a) and B pieces (stage_b) of K block kbl (index within
+  // the split; past the end: re-fetch, unused) into ring buffer buf
+  auto stage_a = [&](int buf, int64_t kbl) {
     const int64_t kb = kb0 + (kbl < nk ? kbl : nk - 1);
     uint8_t* dst = lds + buf * STG;
     const int kofs = (int)(kb * BK);
 #pragma unroll
-    for (int j = 0; j < PIECES; ++j) {
+    for (int j = 0; j < PIECES; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(dst + (j * 8 * NW + w * 8) * BK),
                                                16, aoff[j], kofs, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(dst + OPB +
-                                                                 (j * 8 * NW + w * 8) * BK),
-                                               16, boff[j], kofs, 0, 0);
-    }
     // a_s of this K block: TM floats = TM / 64 pieces of 64 lanes x 4 B; wave w loads piece
     // w % (TM / 64) (the waves past TM / 64 write the same bytes again) so that every wave
-    // issues LPS loads per stage and the K loop can wait with one counted vmcnt
+    // issues the same count of loads per stage and the K loop can wait with counted vmcnts
     const int sp = w % (TM / 64);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + 2 * OPB + sp * 256), 4,
                                              (uint32_t)(sp * 256 + lane * 4),
                                              (int)(kb * g.mp * 4), 0, 0);
   };
+  auto stage_b = [&](int buf, int64_t kbl) {
+    const int64_t kb = kb0 + (kbl < nk ? kbl : nk - 1);
+    uint8_t* dst = lds + buf * STG;
+    const int kofs = (int)(kb * BK);
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(dst + OPB +
+                                                                 (j * 8 * NW + w * 8) * BK),
+                                               16, boff[j], kofs, 0, 0);
+  };
+  auto stage = [&](int buf, int64_t kbl) {
+    stage_a(buf, kbl);
+    stage_b(buf, kbl);
+  };
+  // 2 stages: the B half of a buffer is refilled as soon as every wave holds the K block's B
+  // fragments in registers (a second barrier), so B streams two K blocks ahead, A one
+  constexpr bool EARLY_B = NS == 2;
 
   v4f acc[MB][NB];
 #pragma unroll
@@ -373,15 +388,24 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
   __syncthreads();
   const float* bsrow = bsl + (SILU ? 0 : ((wc * WN) >> 7) * nk);  // the wave's scale block
 
-  // NS-stage ring: NS - 1 K blocks in flight ahead of the one being multiplied
+  // NS-stage ring: NS - 1 K blocks in flight ahead of the one being multiplied (EARLY_B: B
+  // two ahead)
+  if constexpr (EARLY_B) {
+    stage(0, 0);
+    stage_b(1, 1);
+  } else {
 #pragma unroll
-  for (int j = 0; j + 1 < NS; ++j) stage(j, j);
+    for (int j = 0; j + 1 < NS; ++j) stage(j, j);
+  }
   for (int64_t t = 0; t < nk; ++t) {
     const int buf = (int)(t % NS);
-    // this K block's pieces landed (the NS - 2 younger stages may still be in flight) ...
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * LPS) : "memory");
+    // this K block's pieces landed (younger in flight: EARLY_B the next block's B pieces,
+    // else the NS - 2 younger stages) ...
+    if constexpr (EARLY_B) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * LPS) : "memory");
     __builtin_amdgcn_s_barrier();  // ... for every wave; buffer (t - 1) % NS is free
-    stage((int)((t + NS - 1) % NS), t + NS - 1);  // past the end: re-fetch (unused)
+    if constexpr (EARLY_B) stage_a(buf ^ 1, t + 1);   // (its B half holds block t + 1)
+    else stage((int)((t + NS - 1) % NS), t + NS - 1);
     const uint8_t* At = lds + buf * STG;
     const uint8_t* Bt = At + OPB;
     const float* Sa = reinterpret_cast<const float*>(At + 2 * OPB);
@@ -394,6 +418,12 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
     v8i bfr[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) bfr[nb] = frag2(Bt, wc * WN + nb * 16 + r16, q);
+    if constexpr (EARLY_B) {
+      // every wave's B fragments of block t are in registers: block t + 2's B into this half
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      stage_b(buf, t + 2);
+    }
     v8i afr = frag2(At, wr * WM + r16, q);
     // software-pipelined: the scaled accumulation of row block mb - 1 runs while row block
     // mb's MFMAs are in flight (no VALU read of a result the MFMA pipe has just begun)

@@ -113,6 +113,25 @@ def test_entry_view_unequal_entries():
     assert B.entry_view(ctx, m, xr) is xr
 
 
+def test_batchable_unequal_batches():
+    """Entries of equal sample shape stack into one calibration forward even when their batch
+    sizes differ (an unequal calibration set, or a token shard that cut an entry), unless a
+    kwarg tensor carries a batch dim (it could not follow the stacked batch); a padding mask
+    keeps the per-sample loop."""
+    from lightcompress_amd.base_blockwise_quantization import _batchable
+    rot = (torch.ones(1, 8, 4), torch.zeros(1, 8, 4))
+    xs = [torch.zeros(3, 8, 16), torch.zeros(1, 8, 16)]
+    assert _batchable(xs, [{'position_embeddings': rot}] * 2)
+    assert not _batchable(xs, [{'position_ids': torch.zeros(3, 8)},
+                               {'position_ids': torch.zeros(1, 8)}])
+    assert not _batchable([torch.zeros(3, 8, 16), torch.zeros(1, 4, 16)],
+                          [{'position_embeddings': rot}] * 2)
+    eq = [torch.zeros(2, 8, 16), torch.zeros(2, 8, 16)]
+    assert _batchable(eq, [{'position_ids': torch.zeros(1, 8)}] * 2)
+    assert not _batchable(eq, [{'attention_mask': torch.ones(2, 8)}] * 2)
+    assert not _batchable(xs[:1], [{}])
+
+
 @pytest.mark.parametrize('scaling', [None, 'llama3', 'dynamic'])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
 def test_rotary_kwargs_equal_module(scaling, dtype):
