@@ -332,41 +332,26 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
                         : 0x80000000u;
     }
   }
-  // A pieces + the K block's a_s (stage_a) and B pieces (stage_b) of K block kbl (index within
-  // the split; past the end: re-fetch, unused) into ring buffer buf
-  auto stage_a = [&](int buf, int64_t kbl) {
+  auto stage = [&](int buf, int64_t kbl) {  // kbl: K block index within the split
     const int64_t kb = kb0 + (kbl < nk ? kbl : nk - 1);
     uint8_t* dst = lds + buf * STG;
     const int kofs = (int)(kb * BK);
 #pragma unroll
-    for (int j = 0; j < PIECES; ++j)
+    for (int j = 0; j < PIECES; ++j) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(dst + (j * 8 * NW + w * 8) * BK),
                                                16, aoff[j], kofs, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(dst + OPB +
+                                                                 (j * 8 * NW + w * 8) * BK),
+                                               16, boff[j], kofs, 0, 0);
+    }
     // a_s of this K block: TM floats = TM / 64 pieces of 64 lanes x 4 B; wave w loads piece
     // w % (TM / 64) (the waves past TM / 64 write the same bytes again) so that every wave
-    // issues the same count of loads per stage and the K loop can wait with counted vmcnts
+    // issues LPS loads per stage and the K loop can wait with one counted vmcnt
     const int sp = w % (TM / 64);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + 2 * OPB + sp * 256), 4,
                                              (uint32_t)(sp * 256 + lane * 4),
                                              (int)(kb * g.mp * 4), 0, 0);
   };
-  auto stage_b = [&](int buf, int64_t kbl) {
-    const int64_t kb = kb0 + (kbl < nk ? kbl : nk - 1);
-    uint8_t* dst = lds + buf * STG;
-    const int kofs = (int)(kb * BK);
-#pragma unroll
-    for (int j = 0; j < PIECES; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(dst + OPB +
-                                                                 (j * 8 * NW + w * 8) * BK),
-                                               16, boff[j], kofs, 0, 0);
-  };
-  auto stage = [&](int buf, int64_t kbl) {
-    stage_a(buf, kbl);
-    stage_b(buf, kbl);
-  };
-  // 2 stages: the B half of a buffer is refilled as soon as every wave holds the K block's B
-  // fragments in registers (a second barrier), so B streams two K blocks ahead, A one
-  constexpr bool EARLY_B = NS == 2;
 
   v4f acc[MB][NB];
 #pragma unroll
@@ -388,55 +373,35 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
   __syncthreads();
   const float* bsrow = bsl + (SILU ? 0 : ((wc * WN) >> 7) * nk);  // the wave's scale block
 
-  // NS-stage ring: NS - 1 K blocks in flight ahead of the one being multiplied (EARLY_B: B
-  // two ahead)
-  if constexpr (EARLY_B) {
-    stage(0, 0);
-    stage_b(1, 1);
-  } else {
+  // NS-stage ring: NS - 1 K blocks in flight ahead of the one being multiplied. (Round 4
+  // measured two reschedulings of this loop slower on every shape, 1.64 -> 1.45 PF at
+  // 2048 x 7168 x 7168: all of a K block's LDS reads issued first with the scaled
+  // accumulation software-pipelined one row block behind the MFMAs, and a buffer's B half
+  // refilled after a second barrier so that B streams two K blocks ahead;
+  // profiles/r4_fp8_gemm_rate_resched.txt against r3d_fp8_gemm_rate.txt.)
 #pragma unroll
-    for (int j = 0; j + 1 < NS; ++j) stage(j, j);
-  }
+  for (int j = 0; j + 1 < NS; ++j) stage(j, j);
   for (int64_t t = 0; t < nk; ++t) {
     const int buf = (int)(t % NS);
-    // this K block's pieces landed (younger in flight: EARLY_B the next block's B pieces,
-    // else the NS - 2 younger stages) ...
-    if constexpr (EARLY_B) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * LPS) : "memory");
+    // this K block's pieces landed (the NS - 2 younger stages may still be in flight) ...
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * LPS) : "memory");
     __builtin_amdgcn_s_barrier();  // ... for every wave; buffer (t - 1) % NS is free
-    if constexpr (EARLY_B) stage_a(buf ^ 1, t + 1);   // (its B half holds block t + 1)
-    else stage((int)((t + NS - 1) % NS), t + NS - 1);
+    stage((int)((t + NS - 1) % NS), t + NS - 1);  // past the end: re-fetch (unused)
     const uint8_t* At = lds + buf * STG;
     const uint8_t* Bt = At + OPB;
     const float* Sa = reinterpret_cast<const float*>(At + 2 * OPB);
     const float bsv = bsrow[t];
     const float bsv2 = SILU ? bsrow[nk + t] : bsv;  // up's block-scale (nb >= NB / 2)
-    // every LDS read of the K block issued before the first MFMA waits on any of them
-    float sa[MB];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) sa[mb] = Sa[wr * WM + mb * 16 + r16];
     v8i bfr[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) bfr[nb] = frag2(Bt, wc * WN + nb * 16 + r16, q);
-    if constexpr (EARLY_B) {
-      // every wave's B fragments of block t are in registers: block t + 2's B into this half
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      stage_b(buf, t + 2);
+    float sc[MB], sc2[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      sc[mb] = Sa[wr * WM + mb * 16 + r16] * bsv;
+      sc2[mb] = SILU ? Sa[wr * WM + mb * 16 + r16] * bsv2 : sc[mb];
     }
     v8i afr = frag2(At, wr * WM + r16, q);
-    // software-pipelined: the scaled accumulation of row block mb - 1 runs while row block
-    // mb's MFMAs are in flight (no VALU read of a result the MFMA pipe has just begun)
-    v4f dprev[NB];
-    auto accumulate = [&](int mb) {
-      const float s1 = sa[mb] * bsv, s2 = SILU ? sa[mb] * bsv2 : s1;
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[mb][nb][j] = __builtin_fmaf(dprev[nb][j], (SILU && nb >= NB / 2) ? s2 : s1,
-                                          acc[mb][nb][j]);
-    };
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       v8i anext = afr;
@@ -446,12 +411,14 @@ __device__ __forceinline__ void gemm2_body(const Gemm2Args& g, uint8_t* lds, int
       for (int nb = 0; nb < NB; ++nb)
         d[nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[nb], afr, zero, 0, 0, 0, 0,
                                                                   0, 0);
-      if (mb > 0) accumulate(mb - 1);
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) dprev[nb] = d[nb];
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[mb][nb][j] = __builtin_fmaf(d[nb][j], (SILU && nb >= NB / 2) ? sc2[mb] : sc[mb],
+                                          acc[mb][nb][j]);
       afr = anext;
     }
-    accumulate(MB - 1);
     __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -51,24 +51,37 @@ constexpr int LPR = 16, CPL = GB / LPR;
 // FMT = 0: IntegerQuantizer (quant.py:699-717); FMT = LCQ_FP8E4M3 / LCQ_FP8E5M2: FloatQuantizer
 // use_qtorch (quant.py:1061-1080): q = float_quantize(w / s + 0) * s in fp32, sym qparams with
 // qmax = finfo.max (per-group: the same fp32 formula as the int sym case).
+// The U block lives in LDS as its upper triangle, row c from column ustart(c) = c & ~3 (so
+// every row segment stays 16-byte aligned): 8448 floats, 33 KB instead of 64, so four
+// workgroups share a CU (the 28672-row gate / up blocks: 1792 workgroups) instead of two. A
+// lane's float4 of columns below ustart(c) reads the previous row's tail: those columns are
+// < c and never updated.
+constexpr int ustart(int c) { return c & ~3; }
+constexpr int ubase(int c) {  // sum over rows i < c of (GB - ustart(i))
+  return GB * c - 8 * (c >> 2) * ((c >> 2) - 1) - 4 * (c >> 2) * (c & 3);
+}
+constexpr int UPACK = ubase(GB);
+
 template <int GS, int FMT>
 __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
-  __shared__ float u[GB * GB];
+  __shared__ __attribute__((aligned(16))) float u[UPACK];
   const int tid = threadIdx.x;
-  for (int idx = tid * 4; idx < GB * GB; idx += 256 * 4) {
-    const int i = idx / GB, j = idx % GB;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < a.count) {
-      const float* src = a.U + (a.col0 + i) * a.ldu + a.col0 + j;
-      if (j + 3 < a.count) {
-        v = *reinterpret_cast<const float4*>(src);
-      } else {
-        if (j + 0 < a.count) v.x = src[0];
-        if (j + 1 < a.count) v.y = src[1];
-        if (j + 2 < a.count) v.z = src[2];
+  for (int i = tid >> 1; i < GB; i += 128) {   // two threads per row, 16-B pieces
+    for (int j4 = (i >> 2) + (tid & 1); j4 < GB / 4; j4 += 2) {
+      const int j = 4 * j4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < a.count) {
+        const float* src = a.U + (a.col0 + i) * a.ldu + a.col0 + j;
+        if (j + 3 < a.count) {
+          v = *reinterpret_cast<const float4*>(src);
+        } else {
+          if (j + 0 < a.count) v.x = src[0];
+          if (j + 1 < a.count) v.y = src[1];
+          if (j + 2 < a.count) v.z = src[2];
+        }
       }
+      *reinterpret_cast<float4*>(&u[ubase(i) + j - ustart(i)]) = v;
     }
-    *reinterpret_cast<float4*>(&u[idx]) = v;
   }
   __syncthreads();
   const int sub = tid & (LPR - 1);
@@ -132,7 +145,7 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
     if (c < a.count) {
       const int owner = c / CPL, jl = c % CPL;
       // every lane evaluates its own column jl; only the owner's value is used
-      const float d = u[c * GB + c];
+      const float d = u[ubase(c) + c - ustart(c)];
       const float wc = w[jl];
       const float cs = (GS < 0) ? qsk[jl] : qs, cz = (GS < 0) ? qzk[jl] : qz;
       float q;
@@ -151,7 +164,7 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
         lk[jl] = (diff * diff) / (2.f * (d * d));
       }
       const bool ge = sub >= owner, gt = sub > owner;
-      const float* urow = u + c * GB + cb;
+      const float* urow = u + ubase(c) - ustart(c) + cb;
 #pragma unroll
       for (int k = 0; k < CPL; k += 4) {
         const float4 uv = *reinterpret_cast<const float4*>(urow + k);
