@@ -205,7 +205,7 @@ int lcq_tree_sum(const void* const* parts, int np, int64_t n, float alpha, void*
  * GPTQ in-block column loop for one 128-column block (GPTQ.weight_transform, gptq.py:198-244,
  * group qparams gptq.py:358-366). W [rows, ld] fp32 in (act-order permuted) column space:
  * columns [col0, col0+count) are replaced by the error-compensated weights (`tmp`);
- * err (k-major [128, rows]: err[k * rows + r]) receives Err1 for the caller's trailing update
+ * err (k-major [128, ld_err], ld_err >= rows: err[k * ld_err + r]) receives Err1 for the caller's trailing update
  * W[:, col0+count:] -= err @ U[col0:col0+count, col0+count:].
  * U [ldu, ldu] fp32 upper Cholesky factor of H^-1. group in {32, 64, 128}: per-group minmax
  * qparams from the block-start weights written to s_out/z_out [rows, ng_total] (fp32);
@@ -219,7 +219,7 @@ int lcq_tree_sum(const void* const* parts, int np, int64_t n, float alpha, void*
 int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, const void* U,
                    int64_t ldu, int64_t group, int qmin, int qmax, int sym, int fmt,
                    const void* s_in, const void* z_in, void* s_out, void* z_out,
-                   int64_t ng_total, void* err, void* losses, void* stream);
+                   int64_t ng_total, void* err, int64_t ld_err, void* losses, void* stream);
 
 /* GPTQ static groups (gptq.py:224-227, static_groups: True): the same block loop with fixed
  * qparams per (row, ORIGINAL group): permuted column c uses s_in / z_in [rows, ngc] at group
@@ -227,7 +227,7 @@ int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, c
 int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t col0, int count,
                         const void* U, int64_t ldu, int qmin, int qmax, const void* s_in,
                         const void* z_in, const int32_t* col_group, int64_t ngc, void* err,
-                        void* losses, void* stream);
+                        int64_t ld_err, void* losses, void* stream);
 
 /* C = beta C + alpha A op(B) on row-major fp32 views (the fp32 updates of the recursive
  * factorisation behind U, gptq_core._chol_inv_rec: `addmm_` of the reference-equivalent
@@ -268,12 +268,17 @@ int lcq_gather_rc(const void* A, int a_dtype, int64_t rows, int64_t cols, int64_
                   void* stream);
 
 /* GPTQ trailing update W[:, c1:c2] -= err^T[:, :cnt] @ U[c0:c0+cnt, c1:c2] (gptq.py:244) on
- * fp32 MFMA (k-ordered fma chain: deterministic and independent of the row range, so
- * row-sharded GPTQ is bit-identical to one GPU). err k-major [cnt, rows] fp32 (cnt <= 8192):
- * one block's Err1 from lcq_gptq_block, or the stacked Err1 of several blocks (the host's
- * two-level lazy update applies a 1024-column superblock's errors to the far columns at once). */
+ * fp32 MFMA, the product rounded to fp32 then subtracted (the reference's two roundings).
+ * err k-major [cnt, ld_err] fp32 (ld_err >= rows, cnt <= 8192): one block's Err1 from
+ * lcq_gptq_block, or the stacked Err1 of several blocks (the host's two-level lazy update
+ * applies a 1024-column superblock's errors to the far columns at once). With 16-byte aligned
+ * operands (ld_err, ld, ldu % 4 == 0) and cnt % 32 == 0 it runs on lcq_gemm_f32's LDS-DMA
+ * kernel (A read k-major), else on a register-staged 32x32x2 kernel; both compute every
+ * element as the k-ordered fmaf chain (bit-identical to each other and independent of the row
+ * range, so row-sharded GPTQ is bit-identical to one GPU). */
 int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, int cnt, int64_t c1,
-                      int64_t c2, const void* err, const void* U, int64_t ldu, void* stream);
+                      int64_t c2, const void* err, int64_t ld_err, const void* U, int64_t ldu,
+                      void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * AWQ (awq.py) and auto-clip (auto_clip.py) building blocks. dtype = BF16/F16/F32; each op

@@ -569,7 +569,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t f32_rsrc(const float* p, int64
 // One output tile (rows r0.., columns c0..) over K chunks [ch0, ch1): `part` null -> the
 // alpha / beta epilogue into C, else the raw fp32 accumulators into the T x T partial tile
 // `part` (stream-K segments, summed in k order by k_gemm_f32_sk_fixup).
-template <int BT, int T, int NS>
+// AK: A given k-major (element (m, k) at A[k lda + m], the GPTQ trailing update's stacked
+// errors), staged and read like a k-major B.
+template <int BT, int T, int NS, int AK = 0>
 __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds, int64_t r0,
                                                int64_t c0, int64_t ch0, int64_t ch1,
                                                float* part) {
@@ -584,15 +586,24 @@ __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds, int6
   const int wr = w >> 1, wc = w & 1;
   const int64_t nch = ch1;
 
-  const __amdgpu_buffer_rsrc_t ra = f32_rsrc(a.A + r0 * a.lda, (a.M - r0) * a.lda * 4);
+  const __amdgpu_buffer_rsrc_t ra =
+      AK ? f32_rsrc(a.A + r0, ((a.K - 1) * a.lda + (a.M - r0)) * 4)
+         : f32_rsrc(a.A + r0 * a.lda, (a.M - r0) * a.lda * 4);
   __amdgpu_buffer_rsrc_t rb;
   if constexpr (BT) rb = f32_rsrc(a.B + c0 * a.ldb, (a.N - c0) * a.ldb * 4);
   else rb = f32_rsrc(a.B + c0, ((a.K - 1) * a.ldb + (a.N - c0)) * 4);
   uint32_t aoff[PA], boff[PB];
 #pragma unroll
   for (int j = 0; j < PA; ++j) {  // piece j of wave w: rows (j * 4 + w) * 8 .. + 7
-    const int row = (j * 4 + w) * 8 + (lane >> 3);
-    aoff[j] = (uint32_t)((row * a.lda + (((lane & 7) ^ swz32(row)) * 4)) * 4);
+    if constexpr (AK) {  // [k][row] rows of T floats, as a k-major B
+      constexpr int CPR = T / 4;
+      const int k = (j * 4 + w) * (256 / T) + lane / CPR, pc = lane % CPR;
+      const int lc = pc ^ (((k >> 3) & 1) * 4);
+      aoff[j] = (uint32_t)((k * a.lda + lc * 4) * 4);
+    } else {
+      const int row = (j * 4 + w) * 8 + (lane >> 3);
+      aoff[j] = (uint32_t)((row * a.lda + (((lane & 7) ^ swz32(row)) * 4)) * 4);
+    }
   }
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
@@ -612,11 +623,12 @@ __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds, int6
     // the chunk offset goes into voffset (not soffset), so the descriptor's range check covers
     // every byte: past-the-end rows / columns read as zero and never leave the allocation
     const uint32_t ka = (uint32_t)(cc * DKC * 4);
+    const uint32_t kao = AK ? (uint32_t)(cc * DKC * a.lda * 4) : ka;
     const uint32_t kbo = BT ? ka : (uint32_t)(cc * DKC * a.ldb * 4);
 #pragma unroll
     for (int j = 0; j < PA; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(dst + (j * 4 + w) * 1024), 16,
-                                               aoff[j] + ka, 0, 0, 0);
+                                               aoff[j] + kao, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < PB; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -644,11 +656,23 @@ __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds, int6
 #pragma unroll
     for (int x = 0; x < MT; ++x) {
       const int row = wr * WT + x * 16 + r16;
-      const char* rp = As + row * 128;
-      const float4 lo = *reinterpret_cast<const float4*>(rp + ((2 * g) ^ swz32(row)) * 16);
-      const float4 hi = *reinterpret_cast<const float4*>(rp + ((2 * g + 1) ^ swz32(row)) * 16);
-      av[x][0] = lo.x; av[x][1] = lo.y; av[x][2] = lo.z; av[x][3] = lo.w;
-      av[x][4] = hi.x; av[x][5] = hi.y; av[x][6] = hi.z; av[x][7] = hi.w;
+      if constexpr (AK) {
+        // both operands k-major: lane group g supplies k = 4 s + g at step s, so every
+        // output element accumulates k = 0, 1, 2, ... in order -- the same fmaf chain as the
+        // register-staged 32x32x2 kernel, bit for bit
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int k = 4 * s + g;
+          const int pc = (row >> 2) ^ (((k >> 3) & 1) * 4);
+          av[x][s] = *reinterpret_cast<const float*>(As + (k * T + pc * 4 + (row & 3)) * 4);
+        }
+      } else {
+        const char* rp = As + row * 128;
+        const float4 lo = *reinterpret_cast<const float4*>(rp + ((2 * g) ^ swz32(row)) * 16);
+        const float4 hi = *reinterpret_cast<const float4*>(rp + ((2 * g + 1) ^ swz32(row)) * 16);
+        av[x][0] = lo.x; av[x][1] = lo.y; av[x][2] = lo.z; av[x][3] = lo.w;
+        av[x][4] = hi.x; av[x][5] = hi.y; av[x][6] = hi.z; av[x][7] = hi.w;
+      }
     }
 #pragma unroll
     for (int y = 0; y < MT; ++y) {
@@ -663,7 +687,7 @@ __device__ __forceinline__ void gemm_f32d_body(const Args& a, char* f32lds, int6
         const int col = wc * WT + y * 16 + r16;
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-          const int k = 8 * g + s;
+          const int k = AK ? 4 * s + g : 8 * g + s;
           const int pc = (col >> 2) ^ (((k >> 3) & 1) * 4);
           bv[y][s] = *reinterpret_cast<const float*>(Bs + (k * T + pc * 4 + (col & 3)) * 4);
         }
@@ -726,6 +750,15 @@ constexpr int f32d_lds() { return NS_F32D * 2 * T * DKC * 4; }
     gemm_f32d_body<BT, T, NS_F32D>(a, f32lds, (int64_t)blockIdx.y * T,                 \
                                    (int64_t)blockIdx.x * T, 0, a.K / DKC, nullptr);    \
   }
+#define LCQ_F32D_AK_KERNEL(NAME, T)                                                    \
+  __global__ void __launch_bounds__(256, LCQ_F32D_OCC) NAME(Args a) {                  \
+    extern __shared__ __attribute__((aligned(16))) char f32lds[];                      \
+    gemm_f32d_body<0, T, NS_F32D, 1>(a, f32lds, (int64_t)blockIdx.y * T,               \
+                                     (int64_t)blockIdx.x * T, 0, a.K / DKC, nullptr);  \
+  }
+LCQ_F32D_AK_KERNEL(k_gemm_f32d_kn128, 128)
+LCQ_F32D_AK_KERNEL(k_gemm_f32d_kn64, 64)
+#undef LCQ_F32D_AK_KERNEL
 LCQ_F32D_KERNEL(k_gemm_f32d_n128, 0, 128)
 LCQ_F32D_KERNEL(k_gemm_f32d_t128, 1, 128)
 LCQ_F32D_KERNEL(k_gemm_f32d_n64, 0, 64)
@@ -884,6 +917,42 @@ static int gemm_f32_impl(int64_t M, int64_t N, int64_t K, float alpha, const voi
   }
   return check_launch("lcq_gemm_f32");
 }
+
+namespace lcq {
+int gemm_f32_sub_akn(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                     const float* B, int64_t ldb, float* C, int64_t ldc, hipStream_t st) {
+  if (M <= 0 || N <= 0) return LCQ_OK;
+  const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (K <= 0 || K % f32g::DKC != 0 || !al(A) || !al(B) || !al(C) || lda % 4 != 0 ||
+      ldb % 4 != 0 || ldc % 4 != 0 || lda < M || ldb < N ||
+      K * lda >= ((int64_t)1 << 29) || K * ldb >= ((int64_t)1 << 29) || M / 64 >= 65535)
+    return LCQ_EUNSUP;
+  f32g::Args a{};
+  a.A = A;
+  a.B = B;
+  a.C = C;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.alpha = -1.f; a.beta = 1.f;   // C = fma(1, C, -acc): the product rounded, then subtracted
+  a.vec = 1;
+  const int64_t t128 = ((N + 127) / 128) * ((M + 127) / 128);
+  if (t128 >= 256) {
+    constexpr int L = f32g::f32d_lds<128>();
+    (void)hipFuncSetAttribute((const void*)f32g::k_gemm_f32d_kn128,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, L);
+    hipLaunchKernelGGL(f32g::k_gemm_f32d_kn128,
+                       dim3((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128)), 256, L,
+                       st, a);
+  } else {
+    constexpr int L = f32g::f32d_lds<64>();
+    (void)hipFuncSetAttribute((const void*)f32g::k_gemm_f32d_kn64,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, L);
+    hipLaunchKernelGGL(f32g::k_gemm_f32d_kn64,
+                       dim3((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64)), 256, L, st,
+                       a);
+  }
+  return check_launch("gemm_f32_sub_akn");
+}
+}  // namespace lcq
 
 extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
                             int64_t lda, const void* B, int64_t ldb, int bt, float beta, void* C,

@@ -32,7 +32,8 @@ struct GptqArgs {
   float* s_out;       // [rows, ng_total] fp32 (group order = permuted column order)
   float* z_out;
   int64_t ng_total;
-  float* err;         // [rows, 128]
+  float* err;         // k-major [128][ld_err]: err[k ld_err + row]
+  int64_t ld_err;
   float* losses;      // optional [rows, ld]
   const int32_t* cgroup;  // static groups: group of every (permuted) column, [ld]
   int64_t ngc;            // static groups: groups per row of s_in / z_in
@@ -197,7 +198,7 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
     }
   }
 #pragma unroll
-  for (int k = 0; k < CPL; ++k) a.err[(int64_t)(cb + k) * a.rows + r] = ek[k];
+  for (int k = 0; k < CPL; ++k) a.err[(int64_t)(cb + k) * a.ld_err + r] = ek[k];
   if (a.losses) {
 #pragma unroll
     for (int k = 0; k < CPL; k += 4)
@@ -229,8 +230,8 @@ static void launch_gptq_block(const GptqArgs& a, int64_t group, dim3 grid, hipSt
 extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count,
                               const void* U, int64_t ldu, int64_t group, int qmin, int qmax,
                               int sym, int fmt, const void* s_in, const void* z_in, void* s_out,
-                              void* z_out, int64_t ng_total, void* err, void* losses,
-                              void* stream) {
+                              void* z_out, int64_t ng_total, void* err, int64_t ld_err,
+                              void* losses, void* stream) {
   LCQ_REQUIRE(rows > 0 && ld > 0 && count > 0 && count <= GB, "bad block shape");
   LCQ_REQUIRE(col0 >= 0 && col0 + count <= ld && col0 + count <= ldu, "block out of range");
   LCQ_REQUIRE(col0 % GB == 0, "col0 must be a multiple of the 128-column blocksize");
@@ -256,7 +257,9 @@ extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, i
   a.z_out = reinterpret_cast<float*>(z_out);
   a.ng_total = ng_total;
   a.err = reinterpret_cast<float*>(err);
+  a.ld_err = ld_err;
   a.losses = reinterpret_cast<float*>(losses);
+  LCQ_REQUIRE(ld_err >= rows, "ld_err < rows");
   LCQ_REQUIRE(group == 0 || group == 32 || group == 64 || group == 128,
               "group must be 0 (per-row qparams), 32, 64 or 128");
   LCQ_REQUIRE(group != 0 || s_in != nullptr, "fixed-qparams mode needs s_in");
@@ -289,15 +292,15 @@ constexpr int KC = 32;     // K chunk (double-buffered through LDS)
 __device__ __forceinline__ void trail_load(const float* __restrict__ ET, const float* __restrict__ U,
                                            int64_t rows, int64_t ld, int64_t ldu, int64_t c0,
                                            int cnt, int64_t r0, int64_t j0, int k0, int tid,
-                                           float4 (&ra)[4], float4 (&rb)[4]) {
+                                           float4 (&ra)[4], float4 (&rb)[4], int64_t lde) {
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int idx = it * 256 + tid;           // 0..1023 float4 of a 32 x 128 chunk
     const int k = k0 + idx / (TT / 4), c4 = (idx % (TT / 4)) * 4;
     float4 ea = make_float4(0.f, 0.f, 0.f, 0.f), ub = ea;
     if (k < cnt) {
-      const float* es = ET + (int64_t)k * rows + r0 + c4;
-      if (r0 + c4 + 3 < rows && (rows & 3) == 0) {
+      const float* es = ET + (int64_t)k * lde + r0 + c4;
+      if (r0 + c4 + 3 < rows && (lde & 3) == 0) {
         ea = *reinterpret_cast<const float4*>(es);
       } else {
         if (r0 + c4 + 0 < rows) ea.x = es[0];
@@ -321,7 +324,7 @@ __device__ __forceinline__ void trail_load(const float* __restrict__ ET, const f
 
 __global__ void __launch_bounds__(256, 2)
     k_gptq_trailing(float* __restrict__ W, int64_t rows, int64_t ld, int64_t c0, int cnt,
-                    int64_t c1, int64_t c2, const float* __restrict__ ET,
+                    int64_t c1, int64_t c2, const float* __restrict__ ET, int64_t lde,
                     const float* __restrict__ U, int64_t ldu) {
   __shared__ __attribute__((aligned(16))) float As[2][KC * TT];  // [k][row]
   __shared__ __attribute__((aligned(16))) float Bs[2][KC * TT];  // [k][col]
@@ -337,7 +340,7 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
   float4 ra[4], rb[4];
-  trail_load(ET, U, rows, c2, ldu, c0, cnt, r0, j0, 0, tid, ra, rb);
+  trail_load(ET, U, rows, c2, ldu, c0, cnt, r0, j0, 0, tid, ra, rb, lde);
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int idx = it * 256 + tid;
@@ -348,7 +351,8 @@ __global__ void __launch_bounds__(256, 2)
   const int nch = (cnt + KC - 1) / KC;
   for (int ch = 0; ch < nch; ++ch) {
     const int cur = ch & 1;
-    if (ch + 1 < nch) trail_load(ET, U, rows, c2, ldu, c0, cnt, r0, j0, (ch + 1) * KC, tid, ra, rb);
+    if (ch + 1 < nch)
+      trail_load(ET, U, rows, c2, ldu, c0, cnt, r0, j0, (ch + 1) * KC, tid, ra, rb, lde);
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 2) {
       const int k = kk + (lane >> 5);
@@ -390,25 +394,35 @@ __global__ void __launch_bounds__(256, 2)
 }  // namespace lcq
 
 extern "C" int lcq_gptq_trailing(void* W, int64_t rows, int64_t ld, int64_t c0, int cnt,
-                                 int64_t c1, int64_t c2, const void* err, const void* U,
-                                 int64_t ldu, void* stream) {
+                                 int64_t c1, int64_t c2, const void* err, int64_t ld_err,
+                                 const void* U, int64_t ldu, void* stream) {
   LCQ_REQUIRE(rows > 0 && ld > 0 && cnt > 0 && cnt <= 8192, "bad shape");
+  LCQ_REQUIRE(ld_err >= rows, "ld_err < rows");
   LCQ_REQUIRE(c0 >= 0 && c0 + cnt <= ldu && c1 >= c0 + cnt && c2 >= c1 && c2 <= ld &&
                   ld <= ldu,
               "bad column ranges");
   if (c2 == c1) return LCQ_OK;
+  // the recursion's LDS-DMA fp32 GEMM (A k-major) where the operands are 16-byte aligned and
+  // cnt % 32 == 0 -- decided by the column window and the strides only, never by the row count,
+  // so a row shard takes the same kernel (and the same k order) as the whole matrix
+  const float* Up = reinterpret_cast<const float*>(U) + c0 * ldu + c1;
+  float* Wp = reinterpret_cast<float*>(W) + c1;
+  const int rc = lcq::gemm_f32_sub_akn(rows, c2 - c1, cnt, reinterpret_cast<const float*>(err),
+                                       ld_err, Up, ldu, Wp, ld, as_stream(stream));
+  if (rc != LCQ_EUNSUP) return rc;
   const dim3 grid((unsigned)((c2 - c1 + TT - 1) / TT), (unsigned)((rows + TT - 1) / TT));
   hipLaunchKernelGGL(k_gptq_trailing, grid, 256, 0, as_stream(stream),
                      reinterpret_cast<float*>(W), rows, ld, c0, cnt, c1, c2,
-                     reinterpret_cast<const float*>(err), reinterpret_cast<const float*>(U),
-                     ldu);
+                     reinterpret_cast<const float*>(err), ld_err,
+                     reinterpret_cast<const float*>(U), ldu);
   return check_launch("lcq_gptq_trailing");
 }
 
 extern "C" int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t col0, int count,
                                    const void* U, int64_t ldu, int qmin, int qmax,
                                    const void* s_in, const void* z_in, const int32_t* col_group,
-                                   int64_t ngc, void* err, void* losses, void* stream) {
+                                   int64_t ngc, void* err, int64_t ld_err, void* losses,
+                                   void* stream) {
   LCQ_REQUIRE(rows > 0 && ld > 0 && count > 0 && count <= GB, "bad block shape");
   LCQ_REQUIRE(col0 >= 0 && col0 + count <= ld && col0 + count <= ldu, "block out of range");
   LCQ_REQUIRE(col0 % GB == 0, "col0 must be a multiple of the 128-column blocksize");
@@ -423,7 +437,9 @@ extern "C" int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t co
   a.s_in = reinterpret_cast<const float*>(s_in);
   a.z_in = reinterpret_cast<const float*>(z_in);
   a.cgroup = col_group; a.ngc = ngc;
+  LCQ_REQUIRE(ld_err >= rows, "ld_err < rows");
   a.err = reinterpret_cast<float*>(err);
+  a.ld_err = ld_err;
   a.losses = reinterpret_cast<float*>(losses);
   const dim3 grid((unsigned)((rows + (256 / LPR) - 1) / (256 / LPR)));
   hipLaunchKernelGGL((k_gptq_block<-1, 0>), grid, 256, 0, as_stream(stream), a);

@@ -24,6 +24,14 @@ int check_launch(const char* what);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// C[M, N] (ldc) = C - A B with A given k-major (element (m, k) at A[k lda + m]) and B [K, N]
+// (ldb) row-major, on the LDS-DMA fp32 MFMA GEMM of chol.hip (tiled, no stream-K): every
+// element is the k-ordered fmaf chain over k = 0 .. K-1 (bit-identical to lcq_gptq_trailing's
+// register-staged kernel). LCQ_EUNSUP (nothing launched) when the operands are not 16-byte
+// aligned row by row or K % 32 != 0. Used by lcq_gptq_trailing.
+int gemm_f32_sub_akn(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                     const float* B, int64_t ldb, float* C, int64_t ldc, hipStream_t st);
+
 inline int dtype_size(int dt) {
   switch (dt) {
     case LCQ_F32: return 4;

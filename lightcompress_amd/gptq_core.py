@@ -467,7 +467,9 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     if superblock is None:
         superblock = SUPERBLOCK
     SB = max(BLOCK, superblock // BLOCK * BLOCK)
-    errT = torch.empty((SB, rows), dtype=torch.float32, device=dev)  # k-major stacked Err1
+    # k-major stacked Err1, rows padded to 4 so that every k row is 16-byte aligned (the
+    # trailing update's LDS-DMA kernel; a row shard gets the same kernel as the whole matrix)
+    errT = torch.empty((SB, -(-rows // 4) * 4), dtype=torch.float32, device=dev)
     L = torch.zeros_like(W) if losses else None
     s_in = z_in = None
     if searched:

@@ -271,7 +271,8 @@ def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: i
     fmt = 0 if fp8 is None else N.dt(fp8)
     N.call('lcq_gptq_block', N.ptr(W), rows, ld, int(col0), int(count), N.ptr(U), U.shape[1],
            int(group), int(qmin), int(qmax), int(sym), fmt, N.ptr(s_in), N.ptr(z_in), N.ptr(s_out),
-           N.ptr(z_out), int(ng_total), N.ptr(err), N.ptr(losses), N.stream_of(W))
+           N.ptr(z_out), int(ng_total), N.ptr(err), _ld_err(err, rows), N.ptr(losses),
+           N.stream_of(W))
 
 
 def gptq_block_cols(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, qmin: int,
@@ -283,7 +284,14 @@ def gptq_block_cols(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, qmi
     ngc = s_in.numel() // rows
     N.call('lcq_gptq_block_cols', N.ptr(W), rows, ld, int(col0), int(count), N.ptr(U), U.shape[1],
            int(qmin), int(qmax), N.ptr(s_in), N.ptr(z_in), N.ptr(col_group), int(ngc), N.ptr(err),
-           N.ptr(losses), N.stream_of(W))
+           _ld_err(err, rows), N.ptr(losses), N.stream_of(W))
+
+
+def _ld_err(err: torch.Tensor, rows: int) -> int:
+    """Row stride of a k-major error matrix [k, >= rows] (unit column stride)."""
+    if err.dim() != 2 or err.stride(1) != 1 or err.stride(0) < rows or err.shape[1] < rows:
+        raise ValueError('err must be a k-major [k, >= rows] fp32 view with unit column stride')
+    return err.stride(0)
 
 
 def _ld(t: torch.Tensor) -> int:
@@ -358,12 +366,12 @@ def gather_rc(A: torch.Tensor, rsrc=None, csrc=None, dead_col=None, dead_diag=No
 
 def gptq_trailing(W: torch.Tensor, c0: int, cnt: int, c1: int, err: torch.Tensor,
                   U: torch.Tensor, c2: int | None = None):
-    """W[:, c1:c2] -= err.T[:, :cnt] @ U[c0:c0+cnt, c1:c2] in place (err k-major [cnt, rows];
-    fp32 MFMA, deterministic k order). c2 defaults to the last column."""
+    """W[:, c1:c2] -= err.T[:, :cnt] @ U[c0:c0+cnt, c1:c2] in place (err k-major
+    [cnt, >= rows] view; fp32 MFMA, deterministic k order). c2 defaults to the last column."""
     rows, ld = W.shape
     c2 = ld if c2 is None else int(c2)
     N.call('lcq_gptq_trailing', N.ptr(W), rows, ld, int(c0), int(cnt), int(c1), c2, N.ptr(err),
-           N.ptr(U), U.shape[1], N.stream_of(W))
+           _ld_err(err, rows), N.ptr(U), U.shape[1], N.stream_of(W))
 
 
 def _colmean_ws(rows: int, cols: int, device) -> torch.Tensor:

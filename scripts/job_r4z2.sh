@@ -1,13 +1,9 @@
-# round-4 final profile: full GPU suite, default bench line, per-leg kernel stats,
-# streamed-residency copy/compute trace, PMC HBM traffic per leg (separate FETCH_SIZE /
-# WRITE_SIZE passes, MI355X_MICROARCH.md HBM section)
+# round-4 final, part 2: per-leg kernel stats, streamed-residency copy/compute trace, PMC HBM
+# traffic per leg (separate FETCH_SIZE / WRITE_SIZE passes, MI355X_MICROARCH.md HBM section)
 set -o pipefail
 OUT=gpurun_out/r4z
 mkdir -p $OUT
 export TMPDIR=/tmp
-ok() { rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc; }
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $OUT/gputest.log 2>&1; ok
-timeout -k 10 600 python3 -u bench.py > $OUT/bench_default.log 2>&1 || exit 1
 for leg in awq gptq fp8; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$leg -o run \
     -- python3 bench.py --algo $leg --no-cpu-baseline > $OUT/kt_$leg.log 2>&1 || exit 1

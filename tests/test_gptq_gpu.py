@@ -213,10 +213,22 @@ def test_layer_end_to_end_vs_reference(dev, name):
 @pytest.mark.parametrize('rows,ic,c0,K,c2', [(300, 512, 128, 128, None), (256, 4096, 0, 128, None),
                                             (129, 392, 128, 128, None), (200, 2048, 0, 1024, None),
                                             (200, 2048, 128, 128, 1024)])
-def test_trailing_update(dev, rows, ic, c0, K, c2):
-    """lcq_gptq_trailing vs fp64 (incl. K = 1024 superblock updates and a column window),
-    and bit-identical on any row sub-range (row sharding)."""
+@pytest.mark.parametrize('padded', [True, False])
+def test_trailing_update(dev, rows, ic, c0, K, c2, padded):
+    """lcq_gptq_trailing vs fp64 (incl. K = 1024 superblock updates and a column window), and
+    bit-identical on any row sub-range (row sharding) and between its two kernels. padded: the
+    k-major error rows padded to a multiple of 4 floats as the column loop allocates them (the
+    LDS-DMA GEMM path whenever cnt % 32 == 0); unpadded ragged rows take the register-staged
+    kernel."""
     from lightcompress_amd import ops
+
+    def kmajor(e):   # [K, r] -> [K, ceil4(r)] (the column loop's layout) when padded
+        if not padded:
+            return e.contiguous()
+        buf = torch.zeros(e.shape[0], -(-e.shape[1] // 4) * 4, device=dev)
+        buf[:, :e.shape[1]] = e
+        return buf
+
     g = torch.Generator(device=dev).manual_seed(rows + ic)
     W = torch.randn(rows, ic, generator=g, device=dev)
     U = torch.randn(ic, ic, generator=g, device=dev).triu().contiguous()
@@ -227,13 +239,13 @@ def test_trailing_update(dev, rows, ic, c0, K, c2):
     ref = W.double().clone()
     ref[:, c1:end] -= err.t()[:, :cnt].double() @ U[c0:c1, c1:end].double()
     out = W.clone()
-    ops.gptq_trailing(out, c0, cnt, c1, err, U, c2=end)
+    ops.gptq_trailing(out, c0, cnt, c1, kmajor(err), U, c2=end)
     assert torch.equal(out[:, :c1], W[:, :c1]) and torch.equal(out[:, end:], W[:, end:])
     tol = 1e-5 * math.sqrt(cnt) * (1 + ref[:, c1:end].abs())
     assert ((out[:, c1:end].double() - ref[:, c1:end]).abs() <= tol).all()
-    h = rows // 3
+    h = rows // 3   # both kernels are the k-ordered fmaf chain: any row range, any path
     part = W[h:].clone()
-    ops.gptq_trailing(part, c0, cnt, c1, err[:, h:].contiguous(), U, c2=end)
+    ops.gptq_trailing(part, c0, cnt, c1, kmajor(err[:, h:]), U, c2=end)
     assert torch.equal(part, out[h:])
 
 
