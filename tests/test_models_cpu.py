@@ -156,3 +156,82 @@ def test_rotary_kwargs_equal_module(scaling, dtype):
         c0, s0 = m.rotary_emb(torch.empty(1, S, 1, dtype=dtype), pos)
         c, s = kw['position_embeddings']
         assert c.dtype == dtype and torch.equal(c, c0) and torch.equal(s, s0)
+
+
+def test_expert_list_grouped_host_logic_matches_loop(monkeypatch):
+    """The grouped block-fp8 expert forward's host logic (sort of the token slots by expert,
+    row_off, the per-slot token gather a_rows = order // k, gate + up as a SiLU pair, the
+    combine in ascending expert order) against the per-expert loop, on the CPU: every device
+    kernel is replaced by the oracle restatement (oracle/fp8_ref.py: act_quant, fp8_gemm), so the
+    two paths differ only in how rows are grouped and recombined -- the outputs must be equal."""
+    from transformers.models.deepseek_v3 import modeling_deepseek_v3 as md
+
+    from lightcompress_amd import deepseekv3, kernel, module_utils, ops
+    from lightcompress_amd.deepseekv3 import ExpertList
+    from lightcompress_amd.module_utils import LlmcFp8Linear
+    from oracle import fp8_ref as O
+    E, H, inter, T, k = 6, 256, 128, 40, 3
+    g = torch.Generator().manual_seed(3)
+    cfg = md.DeepseekV3Config(hidden_size=H, intermediate_size=inter, hidden_act='silu')
+    experts = ExpertList()
+    for _ in range(E):
+        mlp = md.DeepseekV3MLP(cfg, intermediate_size=inter)
+        for p in ('gate_proj', 'up_proj', 'down_proj'):
+            lin = getattr(mlp, p)
+            m = LlmcFp8Linear.new(lin, 128)
+            m.weight.data, m.weight_scale_inv.data = O.weight_cast_to_fp8(
+                torch.randn(lin.out_features, lin.in_features, generator=g) * 0.05)
+            setattr(mlp, p, m)
+        experts.append(mlp)
+    idx = torch.stack([torch.randperm(E, generator=g)[:k] for _ in range(T)])
+    w = torch.rand(T, k, generator=g)
+    x = (torch.randn(T, H, generator=g) * 2).to(torch.bfloat16)
+
+    def gemm_rows(a, a_s, b, b_s):   # oracle GEMM, C rounded to bf16 like the fp32 -> bf16 path
+        return O.fp8_gemm(a, a_s, b, b_s).to(torch.bfloat16)
+
+    def grouped(a, a_s, row_off, wtab, n, out_dtype, a_rows=None, silu_mul=False):
+        K = a.shape[1]
+        a_s = a_s.view(-1, K // 128)
+        if a_rows is not None:
+            a, a_s = a[a_rows], a_s[a_rows]
+        sets = [t for t in tables] if wtab.dim() == 3 else [tables_down]
+        outs = []
+        for ws in sets:
+            c = torch.empty(a.shape[0], n, dtype=torch.bfloat16)
+            for gi, (b, b_s) in enumerate(ws):
+                r0, r1 = int(row_off[gi]), int(row_off[gi + 1])
+                if r1 > r0:
+                    c[r0:r1] = gemm_rows(a[r0:r1], a_s[r0:r1], b, b_s)
+            outs.append(c)
+        if silu_mul:
+            return torch.nn.functional.silu(outs[0]) * outs[1]
+        return outs[0] if len(outs) == 1 else torch.stack(outs)
+
+    def combine(y, slot_row, expert, weights, T_):
+        out = torch.zeros(T_, y.shape[1], dtype=torch.bfloat16)
+        sr, ex = slot_row.view(T_, -1), expert.view(T_, -1)
+        for e in range(E):
+            tok, pos = torch.where(ex == e)
+            if tok.numel():
+                out.index_add_(0, tok, (y[sr[tok, pos]] * weights[tok, pos, None]).to(
+                    torch.bfloat16))
+        return out
+
+    tables = [[(getattr(m, p).weight.data, getattr(m, p).weight_scale_inv.data) for m in experts]
+              for p in ('gate_proj', 'up_proj')]
+    tables_down = [(m.down_proj.weight.data, m.down_proj.weight_scale_inv.data) for m in experts]
+    monkeypatch.setattr(kernel, 'act_quant', O.act_quant)
+    monkeypatch.setattr(ops, 'fp8_gemm_grouped', grouped)
+    monkeypatch.setattr(ops, 'moe_combine', combine)
+    monkeypatch.setattr(ExpertList, '_fp8_tables', lambda self, dev: (torch.zeros(2, E, 2),
+                                                                     torch.zeros(E, 2)))
+    monkeypatch.setattr(module_utils, 'block_wise_fp8_forward_func',
+                        lambda xx, wt, ws, bs, bias: gemm_rows(*O.act_quant(xx.contiguous()),
+                                                               wt, ws))
+    assert deepseekv3._mlp_forward() is md.DeepseekV3MLP.forward
+    got = experts._forward_grouped_fp8(x, idx, w)
+    monkeypatch.setattr(ExpertList, '_grouped_fp8_ok', lambda self, xx: False)
+    want = experts(x, idx, w)
+    assert got.dtype == want.dtype == torch.bfloat16
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))
