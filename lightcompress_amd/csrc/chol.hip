@@ -16,7 +16,9 @@
 // recursion (gptq_core._chol_inv_rec); L is written back only when asked for (L may alias A:
 // every read of A precedes the first barrier, every write of L follows the last).
 // Measured (scripts/probes/chol_tile_prof.py, one 128-tile): PW 16 / 256 threads 70 us, PW 8 /
-// 256 threads 60 us, PW 8 / 1024 threads 51 us -- S1 is VALU-bound in one wave at ~PW^3/6 FMAs
+// 256 threads 60 us, PW 8 / 1024 threads 51 us (PW 4 / 1024 threads in the n 14336 chain: 84 us
+// against 64 per tile, twice the barriers; profiles/r4_chain_breakdown.txt) -- S1 is VALU-bound
+// in one wave at ~PW^3/6 FMAs
 // per panel, S3 is LDS-latency-bound; what remains is the S1 -> S2 -> S3 chain per panel.
 #include "lcq_common.h"
 
