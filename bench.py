@@ -632,7 +632,7 @@ def bench_fp8(args, rank, world, dev):
     n_units, elems = len(mine), float(sum(mine))
     fwd_w = [(m.weight.data, m.weight_scale_inv.data)
              for n, m in model.get_block_linears(model.get_blocks()[0]).items()
-             if '.experts.' in n and not m.weight.is_meta][:48]
+             if '.experts.' in n and not m.weight.is_meta]   # this rank's routed experts
     fwd_w = [(c.clone(), s.clone()) for c, s in fwd_w]
     timer = _native.KernelTimer()
     sync_barrier(world)
@@ -699,9 +699,11 @@ def bench_fp8_forward(args, weights, dev, world):
     """Calibration forward of the routed block-fp8 experts of a DeepSeek-V3 MoE layer
     (the experts call of DeepseekV3MoE.forward -> per expert LlmcFp8Linear.forward =
     block_wise_fp8_forward_func, module_utils.py:41-46, 244-262: act_quant + the block-scaled
-    fp8 GEMM, kernel.py:141-242): 2 x args.fp8_tokens tokens routed top-8 over 16 experts
-    (2048 tokens per expert on average, ragged), through ExpertList's grouped path (one
-    lcq_fp8_gemm_grouped launch per projection). The reference's per-expert loop over the same
+    fp8 GEMM, kernel.py:141-242): the rank's args.fp8_experts routed experts (32: DSv3's 256
+    over 8 ranks, EP-style), args.fp8_tokens x E / 8 tokens routed top-8 (args.fp8_tokens
+    = 2048 tokens per expert on average, ragged: a 128 x 512-token calibration batch over
+    256 experts), through ExpertList's grouped path (one lcq_fp8_gemm_grouped launch per
+    projection). The reference's per-expert loop over the same
     routing is timed beside it (`loop`). Every rank runs its own experts (weak scaling);
     linears_per_s is the job total over ranks.
     Roofline: 2 * rows * N * K flops per lcq_fp8_gemm_grouped launch (rows = tokens x top-k)
@@ -709,7 +711,7 @@ def bench_fp8_forward(args, weights, dev, world):
     from lightcompress_amd import _native
     E = len(weights) // 3
     k = min(8, E)
-    T = 2 * args.fp8_tokens * E // 16
+    T = args.fp8_tokens * E // k
     experts = _fp8_expert_list(weights, dev)
     inter, H = weights[0][0].shape
     g = torch.Generator(device=dev).manual_seed(5)
