@@ -28,23 +28,27 @@ __global__ __launch_bounds__(256) void k_moe_combine(const uint16_t* __restrict_
                                                      uint16_t* __restrict__ out) {
   const int64_t t = blockIdx.x;
   const int64_t h0 = ((int64_t)blockIdx.y * 256 + threadIdx.x) * 8;
-  // the token's slots in ascending expert id (ids are distinct within a token)
+  // the token's slots in ascending (expert id, slot) order: the loop adds the experts in
+  // ascending index, and a repeated expert's slots in slot order (torch.where over its mask)
   int64_t rows[MAXK];
   float ws[MAXK];
   int cnt = 0;
-  int64_t last = -1;
+  int64_t last_e = -1;
+  int last_j = -1;
   for (int p = 0; p < k; ++p) {
     int best = -1;
     int64_t bid = 0;
     for (int j = 0; j < k; ++j) {
       const int64_t e = expert[t * k + j];
-      if (e > last && (best < 0 || e < bid)) {
+      const bool after = e > last_e || (e == last_e && j > last_j);
+      if (after && (best < 0 || e < bid)) {
         best = j;
         bid = e;
       }
     }
     if (best < 0) break;
-    last = bid;
+    last_e = bid;
+    last_j = best;
     rows[cnt] = slot_row[t * k + best];
     if constexpr (WDT == LCQ_F32) ws[cnt] = reinterpret_cast<const float*>(w)[t * k + best];
     else ws[cnt] = __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(w)[t * k + best]
