@@ -311,8 +311,10 @@ __device__ __forceinline__ float f16r_soft(float f) {
 template <int DT>
 __device__ __forceinline__ float dtr(float f) {
   if constexpr (DT == LCQ_BF16) {
-    const __bf16 h = (__bf16)f;
-    return __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, h) << 16);
+    // v_cvt_pk_bf16_f32 with a zero low half: the result register is the widened value (one
+    // VALU instead of convert + shift)
+    const v2bf h = __builtin_convertvector(v2f{0.f, f}, v2bf);
+    return __builtin_bit_cast(float, h);
   } else {
     return f16r_soft(f);
   }
@@ -398,12 +400,21 @@ __device__ __forceinline__ void dot_rows(const float* __restrict__ xr,
   }
 }
 
-template <int DT, int G>
-__device__ __forceinline__ void load_half(const uint16_t* __restrict__ wrow, int h,
-                                          float (&q)[G / 2]) {
+// this lane's half of a row's group (k = 8i + 4h + j), raw DT bits: loaded once per kernel and
+// kept in registers across the 1 + nsteps passes (re-reading it from global memory every pass
+// cost 11x the weight bytes -- the L2 does not hold a workgroup's 64 KB between passes -- and
+// a vmcnt stall at the head of each pass)
+template <int G>
+__device__ __forceinline__ void fetch_half(const uint16_t* __restrict__ wrow, int h,
+                                           uint2 (&raw)[G / 8]) {
 #pragma unroll
-  for (int i = 0; i < G / 8; ++i)
-    widen4<DT>(*reinterpret_cast<const uint2*>(wrow + 8 * i + 4 * h), &q[4 * i]);
+  for (int i = 0; i < G / 8; ++i) raw[i] = *reinterpret_cast<const uint2*>(wrow + 8 * i + 4 * h);
+}
+
+template <int DT, int G>
+__device__ __forceinline__ void widen_half(const uint2 (&raw)[G / 8], float (&q)[G / 2]) {
+#pragma unroll
+  for (int i = 0; i < G / 8; ++i) widen4<DT>(raw[i], &q[4 * i]);
 }
 
 // get_qparams in fp32 (quant.py:545-559) for the calib_algo mse search
@@ -472,13 +483,15 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)
   bool live[R];
   const uint16_t* wrow[R];
   float mxs[R], mn[R], org_max[R], org_min[R];
+  uint2 wraw[R][CHUNKS];
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     o[j] = (int64_t)blockIdx.x * RW + j * CROWS + r;
     live[j] = o[j] < oc;
     wrow[j] = w + (live[j] ? o[j] : 0) * ic + g * G;
+    fetch_half<G>(wrow[j], h, wraw[j]);
     float q[CH];
-    load_half<DT, G>(wrow[j], h, q);
+    widen_half<DT, G>(wraw[j], q);
     float mx = -INFINITY, mi = INFINITY, am = 0.f;
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
@@ -525,7 +538,7 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)
       }
       float q[R][CH];
 #pragma unroll
-      for (int j = 0; j < R; ++j) load_half<DT, G>(wrow[j], h, q[j]);
+      for (int j = 0; j < R; ++j) widen_half<DT, G>(wraw[j], q[j]);
       if (p > 0) {
         const float f = factors[p - 1];
 #pragma unroll
