@@ -18,8 +18,11 @@
 // 256-byte rows with XOR-swizzled 16-byte chunks, conflict-free for the row reads of K and the
 // ds_read_b64_tr_b16 transposed reads of V). Swapped QK^T (mfma(K, Q^T)): each lane holds the
 // scores of ONE query row (lane & 31) for 16 of every 32 keys, so the row max / sum is local
-// plus one cross-half exchange, and the score accumulator converts in place to the A operand
-// of P.V (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
+// plus one cross-half exchange (v_permlane32_swap), and the score accumulator converts in
+// place to the B operand of the swapped P.V, O^T += V^T P^T (cdna_hip_programming.md §3 "An
+// accumulator tile as the next MFMA's operand"): O is held transposed, so the softmax
+// rescale and the final 1 / l are lane-local too. The next K/V tile's LDS-DMA overlaps the
+// current tile (counted vmcnt + raw s_barrier).
 #include "lcq_common.h"
 
 namespace lcq {
@@ -50,9 +53,24 @@ __device__ __forceinline__ int img_off(int row, int ch) {
   return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
+// Transposed 8-byte LDS read as inline asm: the builtin form makes the compiler put a
+// vmcnt(0) before it (it cannot tell the read from the K / V stage being filled by LDS-DMA for
+// the next tile), which serialised every tile behind the next tile's loads. The asm reads are
+// invisible to the compiler's lgkmcnt tracking: tr_wait() below waits for them explicitly and
+// ties their results, so no consumer is scheduled above the wait.
 __device__ __forceinline__ v4s_t tr_read(const char* lds, int byte_off) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) v4s_t*)(lds + byte_off));
+  v4s_t r;
+  const uint32_t addr = (uint32_t)reinterpret_cast<uintptr_t>(lds + byte_off);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr) : "memory");
+  return r;
+}
+
+__device__ __forceinline__ void tr_wait(v4s_t (&lo)[4], v4s_t (&hi)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]),
+                 "+v"(hi[2]), "+v"(hi[3])
+               :
+               : "memory");
 }
 
 __device__ __forceinline__ v16f_t mfma32(v8s_t a, v8s_t b, v16f_t c) {
@@ -67,25 +85,43 @@ __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, hv);
 }
 
+// value of lane ^ 32 (the other half of a 32-lane query block): v_permlane32_swap, a VALU op,
+// where __shfl_xor lowers to ds_bpermute (an LDS round trip and an lgkmcnt wait per call)
+__device__ __forceinline__ float other_half(float v, int h) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(h ? r[0] : r[1]);
+}
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void g_void_t;
 
-// Stage one 64-key tile of K and V into LDS with global_load_lds (16 B per lane; a wave
-// instruction fills 1 KB = 4 rows lane-linearly, so the image's XOR swizzle is applied to the
-// global source chunk). Keys past S re-read row S-1 (finite data; masked later).
-__device__ __forceinline__ void stage_kv(char* kst, char* vst, const uint16_t* kp,
-                                         const uint16_t* vp, int64_t kss, int64_t vss, int k0,
-                                         int S, int w, int lane) {
+// Stage one 64-key tile of K and V into LDS by buffer-descriptor LDS-DMA (16 B per lane; a
+// wave instruction fills 1 KB = 4 rows lane-linearly, so the image's XOR swizzle is applied to
+// the global source chunk). Keys past S re-read row S-1 (finite data; masked later). Buffer
+// loads (not global_load_lds): the compiler then leaves the tile's vmcnt to the counted waits
+// in the loop instead of a vmcnt(0) before every LDS read of the stage.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const uint16_t* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  void* q = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, 0x7fffffff, 0x00020000);
+}
+
+__device__ __forceinline__ void stage_kv(char* kst, char* vst, __amdgpu_buffer_rsrc_t kr,
+                                         __amdgpu_buffer_rsrc_t vr, int64_t kss, int64_t vss,
+                                         int k0, int S, int w, int lane) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int row = 4 * (4 * w + j) + (lane >> 4);
     const int pc = lane & 15;
     const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
     const int key = min(k0 + row, S - 1);
-    __builtin_amdgcn_global_load_lds((g_void_t*)(kp + (int64_t)key * kss + ch * 8),
-                                     (lds_void_t*)(kst + 1024 * (4 * w + j)), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((g_void_t*)(vp + (int64_t)key * vss + ch * 8),
-                                     (lds_void_t*)(vst + 1024 * (4 * w + j)), 16, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (lds_void_t*)(kst + 1024 * (4 * w + j)), 16,
+                                             (uint32_t)(key * kss * 2 + ch * 16), 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(vr, (lds_void_t*)(vst + 1024 * (4 * w + j)), 16,
+                                             (uint32_t)(key * vss * 2 + ch * 16), 0, 0, 0);
   }
 }
 
@@ -98,9 +134,12 @@ __device__ __forceinline__ void stage_kv(char* kst, char* vst, const uint16_t* k
 template <int QB>
 __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnArgs a) {
   constexpr int QT = AQT * QB;
-  // two stages of [K image | V image], 16 KB each: 64 KB (reused to stage the output tile)
-  __shared__ __attribute__((aligned(1024))) char smem[2][2][AKT * 256];
-  __shared__ float xch[4][32 * QB];
+  // two stages of [K image | V image], 16 KB each: 64 KB (reused to stage the output tile);
+  // dynamic LDS: the compiler then tracks the K reads of a stage apart from the LDS-DMA
+  // filling the other one (with a static array it waited vmcnt(0) before them)
+  extern __shared__ __attribute__((aligned(1024))) char attn_lds[];
+  typedef char stage_t[2][AKT * 256];
+  stage_t* smem = reinterpret_cast<stage_t*>(attn_lds);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int qt = (int)gridDim.x - 1 - (int)blockIdx.x;  // longest (last) query tiles first
@@ -111,7 +150,8 @@ __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnAr
   const uint16_t* kp = a.k + b * a.ksb + hk * a.ksh;
   const uint16_t* vp = a.v + b * a.vsb + hk * a.vsh;
   const int kend = min(a.S, q0 + QT);
-  stage_kv(smem[0][0], smem[0][1], kp, vp, a.kss, a.vss, 0, a.S, w, lane);
+  const __amdgpu_buffer_rsrc_t kr = head_rsrc(kp), vr = head_rsrc(vp);
+  stage_kv(smem[0][0], smem[0][1], kr, vr, a.kss, a.vss, 0, a.S, w, lane);
 
   int qrow[QB];  // this lane's query row in block qb (both lane halves)
   // Q^T as the B operand of mfma(K, Q^T): lane holds Q[qrow][16 kk + 8 h + j]
@@ -144,14 +184,18 @@ __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnAr
   int it = 0;
   for (int k0 = 0; k0 < kend; k0 += AKT, ++it) {
     const int cur = it & 1;
-    __syncthreads();  // every wave is done with the stage the next tile overwrites
+    // Raw s_barrier with counted waits (not __syncthreads, whose release fence waits for
+    // vmcnt(0), i.e. for the NEXT tile's loads issued just before it: no prefetch at all).
+    // every wave is done with the stage the next tile overwrites (its reads were consumed)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     if (k0 + AKT < kend) {
-      stage_kv(smem[cur ^ 1][0], smem[cur ^ 1][1], kp, vp, a.kss, a.vss, k0 + AKT, a.S, w, lane);
+      stage_kv(smem[cur ^ 1][0], smem[cur ^ 1][1], kr, vr, a.kss, a.vss, k0 + AKT, a.S, w, lane);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this tile's loads, not the next's
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();  // this tile is in LDS for every wave
+    __builtin_amdgcn_s_barrier();  // this tile is in LDS for every wave
     const char* kimg = smem[cur][0];
     const char* vimg = smem[cur][1];
 
@@ -173,7 +217,7 @@ __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnAr
     }
     // causal mask, online softmax in the exp2 domain (scores scaled by scale * log2 e inside
     // the exponent's fma; v_exp_f32 directly: results below 2^-126 flush to 0), per block
-    bool rescale = false;
+    float alpha[QB];
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
       const bool diag = k0 + AKT - 1 > q0 + 32 * (QB * w + qb);  // a key can exceed a row
@@ -192,9 +236,9 @@ __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnAr
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[qb][t][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * a.sl2;  // sl2 > 0: max commutes with the scale
+      mx = fmaxf(mx, other_half(mx, h)) * a.sl2;  // sl2 > 0: max commutes with the scale
       const float mn = fmaxf(m[qb], mx);
-      const float alpha = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m[qb] - mn);
+      alpha[qb] = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m[qb] - mn);
       const float msub = (mn == -INFINITY) ? 0.f : mn;
       float rs = 0.f;
 #pragma unroll
@@ -205,30 +249,26 @@ __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnAr
           s[qb][t][r] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 32, 64);
-      l[qb] = l[qb] * alpha + rs;
+      rs += other_half(rs, h);
+      l[qb] = l[qb] * alpha[qb] + rs;
       m[qb] = mn;
-      rescale |= alpha != 1.f;
-      if (h == 0) xch[w][32 * qb + c] = alpha;
     }
-    // rescale O (skipped when no row's max moved: a multiply by 1 is exact): its registers
-    // hold rows (r & 3) + 8 (r >> 2) + 4 h of each 32-row block
-    __builtin_amdgcn_wave_barrier();
-    if (__builtin_amdgcn_read_exec() && __any(rescale)) {
+    // rescale O^T (skipped where no row's max moved: a multiply by 1 is exact). O is held
+    // transposed (see P.V below), so a lane's registers all belong to its own query row and
+    // alpha is lane-local: no exchange through LDS
 #pragma unroll
-      for (int qb = 0; qb < QB; ++qb) {
-        float ar[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) ar[r] = xch[w][32 * qb + (r & 3) + 8 * (r >> 2) + 4 * h];
+    for (int qb = 0; qb < QB; ++qb) {
+      if (alpha[qb] != 1.f) {
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) o[qb][dt][r] *= ar[r];
+          for (int r = 0; r < 16; ++r) o[qb][dt][r] *= alpha[qb];
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    // P.V: k-step (t, s2) takes score registers 8 s2 .. 8 s2 + 7 of tile t; element j is key
-    // 32 t + 16 s2 + 8 (j >> 2) + 4 h + (j & 3); V^T fragments by transposed reads of those rows
+    // O^T += V^T P^T: mfma(V^T, P^T), so the accumulator's columns are query rows (lane & 31)
+    // and its registers head dims 32 dt + (r & 3) + 8 (r >> 2) + 4 h. k-step (t, s2) takes
+    // score registers 8 s2 .. 8 s2 + 7 of tile t; element j is key 32 t + 16 s2 + 8 (j >> 2) +
+    // 4 h + (j & 3); V^T fragments by transposed reads of those rows
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -242,38 +282,40 @@ __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnAr
             pw[j] = pack_bf16(s[qb][t][8 * s2 + 2 * j], s[qb][t][8 * s2 + 2 * j + 1]);
         }
         const int r0 = 32 * t + 16 * s2 + 4 * (g >> 1);  // this 16-lane group's first key row
+        v4s_t lo[4], hi[4];
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
           const int ch = 4 * dt + 2 * (g & 1) + (pp >> 1);
-          const v4s_t lo = tr_read(vimg, img_off(r0 + qq, ch) + 8 * (pp & 1));
-          const v4s_t hi = tr_read(vimg, img_off(r0 + 8 + qq, ch) + 8 * (pp & 1));
-          const v8s_t vf = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+          lo[dt] = tr_read(vimg, img_off(r0 + qq, ch) + 8 * (pp & 1));
+          hi[dt] = tr_read(vimg, img_off(r0 + 8 + qq, ch) + 8 * (pp & 1));
+        }
+        tr_wait(lo, hi);
 #pragma unroll
-          for (int qb = 0; qb < QB; ++qb) o[qb][dt] = mfma32(pf[qb], vf, o[qb][dt]);
+        for (int dt = 0; dt < 4; ++dt) {
+          const v8s_t vf = {lo[dt].x, lo[dt].y, lo[dt].z, lo[dt].w,
+                            hi[dt].x, hi[dt].y, hi[dt].z, hi[dt].w};
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) o[qb][dt] = mfma32(vf, pf[qb], o[qb][dt]);
         }
       }
   }
-  // normalise: rows of O take 1 / l of their query row
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb)
-    if (h == 0) xch[w][32 * qb + c] = 1.f / l[qb];
-  __syncthreads();  // also: every wave is past its last read of the K / V images
-  // stage the QT x 128 bf16 output tile (QT rows of 256 B = 32 KB per 128 rows) in the stage
-  // buffers, then store whole 256-byte rows of out[b, q, hq, :]
+  __syncthreads();  // every wave is past its last read of the K / V images
+  // normalise (1 / l of the lane's own query row) and stage the QT x 128 bf16 output tile
+  // (QT rows of 256 B = 32 KB per 128 rows) in the stage buffers: registers 4 i .. 4 i + 3 of
+  // block dt are 4 consecutive head dims (8 bytes), then whole 256-byte rows of out[b, q, hq, :]
   char* ost = &smem[0][0][0];
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) {
-    float il[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) il[r] = xch[w][32 * qb + (r & 3) + 8 * (r >> 2) + 4 * h];
+    const float il = 1.f / l[qb];
+    const int row = 32 * (QB * w + qb) + c;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * (QB * w + qb) + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int col = 32 * dt + c;
-        *reinterpret_cast<__bf16*>(ost + img_off(row, col >> 3) + 2 * (col & 7)) =
-            (__bf16)(o[qb][dt][r] * il[r]);
+      for (int i = 0; i < 4; ++i) {
+        uint2 pk;
+        pk.x = pack_bf16(o[qb][dt][4 * i] * il, o[qb][dt][4 * i + 1] * il);
+        pk.y = pack_bf16(o[qb][dt][4 * i + 2] * il, o[qb][dt][4 * i + 3] * il);
+        *reinterpret_cast<uint2*>(ost + img_off(row, 4 * dt + i) + 8 * h) = pk;
       }
   }
   __syncthreads();
@@ -316,18 +358,25 @@ extern "C" int lcq_attn_fwd_causal(const void* q, const void* k, const void* v, 
   LCQ_REQUIRE(((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
                 reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(out)) & 15) == 0,
               "attention kernel: 16-byte aligned tensors required");
+  LCQ_REQUIRE(S * a.kss < (int64_t(1) << 30) && S * a.vss < (int64_t(1) << 30),
+              "attention kernel: one head's K / V span must stay below 2 GB (32-bit offsets)");
   a.S = (int)S; a.H = H; a.KVH = KVH;
   a.sl2 = scale * 1.44269504088896340736f;
   static const int qb_env = [] {
     const char* e = getenv("LCQ_ATTN_QB");  // probe override
     return e ? atoi(e) : 1;
   }();
+  constexpr int kLds = 2 * 2 * AKT * 256;
   if (qb_env != 2) {
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd_causal<1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     const dim3 grid((unsigned)((S + AQT - 1) / AQT), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL(k_attn_fwd_causal<1>, grid, 256, 0, as_stream(stream), a);
+    hipLaunchKernelGGL(k_attn_fwd_causal<1>, grid, 256, kLds, as_stream(stream), a);
   } else {
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd_causal<2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     const dim3 grid((unsigned)((S + 2 * AQT - 1) / (2 * AQT)), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL(k_attn_fwd_causal<2>, grid, 256, 0, as_stream(stream), a);
+    hipLaunchKernelGGL(k_attn_fwd_causal<2>, grid, 256, kLds, as_stream(stream), a);
   }
   return check_launch("lcq_attn_fwd_causal");
 }
