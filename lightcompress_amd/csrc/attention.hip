@@ -45,6 +45,7 @@ struct AttnArgs {
   int64_t ksb, ksh, kss;
   int64_t vsb, vsh, vss;
   int S, H, KVH;
+  int nqt;                // query tiles per (batch, head)
   float sl2;              // scale * log2(e)
 };
 
@@ -142,8 +143,20 @@ __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnAr
   stage_t* smem = reinterpret_cast<stage_t*>(attn_lds);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = lane & 31, h = lane >> 5;
-  const int qt = (int)gridDim.x - 1 - (int)blockIdx.x;  // longest (last) query tiles first
-  const int hq = blockIdx.y, b = blockIdx.z;
+  // XCD-aware work order: the dispatcher places workgroup p on XCD p % 8, so work id L is
+  // taken from contiguous ranges per XCD (L = xcd's base + p / 8). Consecutive ids are the
+  // query tiles of the H / KVH query heads sharing one key/value head, i.e. the workgroups
+  // that stream the same K / V rows run together on one XCD and share them in its L2 (with
+  // the hardware order every XCD fetched every (b, kv head)'s K / V from HBM).
+  const int nqt = a.nqt;
+  int L;
+  {
+    const int nwg = (int)gridDim.x, p = (int)blockIdx.x;
+    const int xcd = p & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (p >> 3);
+  }
+  const int qt = nqt - 1 - L % nqt;  // longest (last) query tiles first within a group
+  const int hq = (L / nqt) % a.H, b = L / (nqt * a.H);
   const int hk = hq / (a.H / a.KVH);
   const int q0 = qt * QT;
   const uint16_t* qp = a.q + b * a.qsb + hq * a.qsh;
@@ -342,7 +355,8 @@ extern "C" int lcq_attn_fwd_causal(const void* q, const void* k, const void* v, 
   LCQ_REQUIRE(dtype == LCQ_BF16, "attention kernel: bf16 only");
   LCQ_REQUIRE(D == AHD, "attention kernel: head dim 128 only");
   LCQ_REQUIRE(B > 0 && S > 0 && H > 0 && KVH > 0 && H % KVH == 0, "bad shape / GQA grouping");
-  LCQ_REQUIRE(B <= 65535 && H <= 65535 && S < (int64_t(1) << 30), "shape too large");
+  LCQ_REQUIRE(B * H * ((S + AQT - 1) / AQT) < (int64_t(1) << 31) && S < (int64_t(1) << 30),
+              "shape too large");
   LCQ_REQUIRE(q && k && v && out && q_strides && k_strides && v_strides, "null pointer");
   AttnArgs a{};
   a.q = reinterpret_cast<const uint16_t*>(q);
@@ -370,13 +384,15 @@ extern "C" int lcq_attn_fwd_causal(const void* q, const void* k, const void* v, 
   if (qb_env != 2) {
     (void)hipFuncSetAttribute((const void*)k_attn_fwd_causal<1>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-    const dim3 grid((unsigned)((S + AQT - 1) / AQT), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL(k_attn_fwd_causal<1>, grid, 256, kLds, as_stream(stream), a);
+    a.nqt = (int)((S + AQT - 1) / AQT);
+    hipLaunchKernelGGL(k_attn_fwd_causal<1>, dim3((unsigned)(a.nqt * H * B)), 256, kLds,
+                       as_stream(stream), a);
   } else {
     (void)hipFuncSetAttribute((const void*)k_attn_fwd_causal<2>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-    const dim3 grid((unsigned)((S + 2 * AQT - 1) / (2 * AQT)), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL(k_attn_fwd_causal<2>, grid, 256, kLds, as_stream(stream), a);
+    a.nqt = (int)((S + 2 * AQT - 1) / (2 * AQT));
+    hipLaunchKernelGGL(k_attn_fwd_causal<2>, dim3((unsigned)(a.nqt * H * B)), 256, kLds,
+                       as_stream(stream), a);
   }
   return check_launch("lcq_attn_fwd_causal");
 }

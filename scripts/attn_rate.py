@@ -20,7 +20,10 @@ def timed(fn, n=10):
     return a.elapsed_time(b) / n
 
 
-for (B, H, KVH, S) in [(128, 32, 8, 512), (128, 32, 8, 2048)]:
+shapes = [(128, 32, 8, 512), (128, 32, 8, 2048)]
+if len(sys.argv) > 1:  # e.g. `512`: only that sequence length (counter passes)
+    shapes = [c for c in shapes if c[3] == int(sys.argv[1])]
+for (B, H, KVH, S) in shapes:
     D = 128
     qs = torch.randn(B, S, H, D, device='cuda').to(torch.bfloat16)
     ks = torch.randn(B, S, KVH, D, device='cuda').to(torch.bfloat16)
