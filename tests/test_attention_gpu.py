@@ -16,8 +16,11 @@ def _ref(q, k, v, scale, dtype=torch.float32):
 
 
 @pytest.mark.parametrize('B,H,KVH,S', [(2, 4, 2, 64), (1, 8, 8, 200), (3, 8, 2, 33),
-                                        (2, 32, 8, 512), (1, 4, 1, 1000), (1, 2, 2, 1)])
+                                        (2, 32, 8, 512), (1, 4, 1, 1000), (1, 2, 2, 1),
+                                        (1, 6, 2, 300), (3, 3, 1, 129)])
 def test_attention_vs_fp32(dev, B, H, KVH, S):
+    """(1, 6, 2, 300) and (3, 3, 1, 129): workgroup counts 18 and 18 (not multiples of the 8
+    XCDs) for the XCD-contiguous work order."""
     from lightcompress_amd import ops
     g = torch.Generator(device=dev).manual_seed(B * 1000 + S)
     D = 128
