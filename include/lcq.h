@@ -521,7 +521,8 @@ int lcq_moe_combine(const void* y, const int64_t* slot_row, const int64_t* exper
  * v with GQA (kv head = h / (H / KVH)). q/k/v bf16 viewed as [B, heads, S, 128] with element
  * strides {batch, head, seq} (host int64[3] each; head dim contiguous, strides multiples of 8,
  * 16-byte aligned); out bf16 [B, S, H, 128] contiguous. fp32 scores and online softmax,
- * bf16 P.V. */
+ * bf16 P.V. One (batch, kv head)'s K / V rows must span < 2 GB (S * seq stride < 2^30
+ * elements: 32-bit buffer offsets), else LCQ_EINVAL. */
 int lcq_attn_fwd_causal(const void* q, const void* k, const void* v, int dtype, int64_t B,
                         int64_t S, int H, int KVH, int D, const int64_t* q_strides,
                         const int64_t* k_strides, const int64_t* v_strides, float scale,
