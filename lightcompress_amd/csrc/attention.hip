@@ -95,7 +95,6 @@ __device__ __forceinline__ float other_half(float v, int h) {
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) const void g_void_t;
 
 // Stage one 64-key tile of K and V into LDS by buffer-descriptor LDS-DMA (16 B per lane; a
 // wave instruction fills 1 KB = 4 rows lane-linearly, so the image's XOR swizzle is applied to
