@@ -128,9 +128,9 @@ __device__ __forceinline__ void stage_kv(char* kst, char* vst, __amdgpu_buffer_r
 // QB query blocks of 32 rows per wave (a workgroup covers 128 QB rows): every K / V fragment
 // read from LDS feeds QB MFMAs. QB 2 halves the LDS traffic per flop but needs 492 VGPRs, so
 // one wave per SIMD: without a hand-pipelined schedule its MFMA, softmax and LDS phases
-// serialise (measured: 164 vs 277 TFLOP/s at S 512, 194 vs 379 at S 2048). QB 1 (two
-// workgroups per CU, MFMA of one wave under the softmax of the other) is the default;
-// LCQ_ATTN_QB=2 selects the other for probes.
+// serialise (measured in round 3: 164 vs 277 TFLOP/s at S 512, 194 vs 379 at S 2048). QB 1
+// (two workgroups per CU, MFMA of one wave under the softmax of the other) is the one launched;
+// the QB 2 launch and its environment switch were removed.
 template <int QB>
 __global__ void __launch_bounds__(256, QB == 1 ? 2 : 1) k_attn_fwd_causal(AttnArgs a) {
   constexpr int QT = AQT * QB;
@@ -375,23 +375,11 @@ extern "C" int lcq_attn_fwd_causal(const void* q, const void* k, const void* v, 
               "attention kernel: one head's K / V span must stay below 2 GB (32-bit offsets)");
   a.S = (int)S; a.H = H; a.KVH = KVH;
   a.sl2 = scale * 1.44269504088896340736f;
-  static const int qb_env = [] {
-    const char* e = getenv("LCQ_ATTN_QB");  // probe override
-    return e ? atoi(e) : 1;
-  }();
   constexpr int kLds = 2 * 2 * AKT * 256;
-  if (qb_env != 2) {
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd_causal<1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-    a.nqt = (int)((S + AQT - 1) / AQT);
-    hipLaunchKernelGGL(k_attn_fwd_causal<1>, dim3((unsigned)(a.nqt * H * B)), 256, kLds,
-                       as_stream(stream), a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd_causal<2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-    a.nqt = (int)((S + 2 * AQT - 1) / (2 * AQT));
-    hipLaunchKernelGGL(k_attn_fwd_causal<2>, dim3((unsigned)(a.nqt * H * B)), 256, kLds,
-                       as_stream(stream), a);
-  }
+  (void)hipFuncSetAttribute((const void*)k_attn_fwd_causal<1>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+  a.nqt = (int)((S + AQT - 1) / AQT);
+  hipLaunchKernelGGL(k_attn_fwd_causal<1>, dim3((unsigned)(a.nqt * H * B)), 256, kLds,
+                     as_stream(stream), a);
   return check_launch("lcq_attn_fwd_causal");
 }
