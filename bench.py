@@ -35,6 +35,7 @@ Also in the line:
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -143,11 +144,91 @@ def pmc_traffic(leg, kernel):
     return sum(k['hbm_bytes'] for k in ks), str(files[-1].relative_to(ROOT))
 
 
+class ClockSampler:
+    """The GFX clock over a timed region, read by amdsmi on a host thread every `period` s
+    (`amdsmi_get_clock_info(GFX)['clk']`, and the firmware's `average_gfxclk_frequency` from
+    the GPU metrics table where present). MI355X lowers its clock under MFMA load (DVFS,
+    MI355X_MICROARCH.md 'DVFS give-back'); this puts the clock the chip held next to the
+    number, so a box-to-box difference can be told apart from a code regression. It reads
+    sysfs-level clocks, which run up to ~10 % above the in-kernel clock of an MFMA loop.
+    None when amdsmi is unavailable (never fails the bench)."""
+
+    def __init__(self, dev, period=0.05):
+        import threading
+        self.period, self.samples, self.avg = period, [], []
+        self._stop = threading.Event()
+        self._thread = None
+        self.handle = None
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            self._smi = amdsmi
+            handles = amdsmi.amdsmi_get_processor_handles()
+            idx = torch.device(dev).index or 0
+            try:
+                p = torch.cuda.get_device_properties(idx)
+                bdf = f'{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0'
+                self.handle = amdsmi.amdsmi_get_processor_handle_from_bdf(bdf)
+            except Exception:
+                self.handle = handles[idx] if idx < len(handles) else None
+        except Exception:
+            self.handle = None
+
+    def _run(self):
+        smi = self._smi
+        while not self._stop.is_set():
+            try:
+                self.samples.append(float(smi.amdsmi_get_clock_info(
+                    self.handle, smi.AmdSmiClkType.GFX)['clk']))
+            except Exception:
+                pass
+            try:
+                v = smi.amdsmi_get_gpu_metrics_info(self.handle).get('average_gfxclk_frequency')
+                if isinstance(v, (int, float)) and 0 < v < 10000:
+                    self.avg.append(float(v))
+            except Exception:
+                pass
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        if self.handle is not None:
+            import threading
+            self._thread = threading.Thread(target=self._run, daemon=True)
+            self._thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join(timeout=5)
+        return False
+
+    def summary(self):
+        if not self.samples:
+            return None
+        xs = sorted(self.samples)
+        out = {'mean': round(sum(xs) / len(xs), 1), 'median': xs[len(xs) // 2],
+               'min': xs[0], 'max': xs[-1], 'samples': len(xs),
+               'source': 'amdsmi GFX clock (MHz), sampled every 50 ms over the timed region'}
+        if self.avg:
+            out['fw_average_gfxclk_mean'] = round(sum(self.avg) / len(self.avg), 1)
+        return out
+
+
 def sync_barrier(world):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+
+
+def free_device():
+    """After a leg: collect the algorithm <-> model cycles (deployed modules hold the quant
+    callables) and return the allocator's free blocks, so the next leg starts from its own
+    model + calibration only (e2e's hbm_at_start_gb)."""
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
 
 
 def max_over_ranks(v, world, dev):
@@ -367,16 +448,18 @@ def bench_awq(args, rank, world, dev):
             walgo.block_opt(b)
             wm.replace_module_block(VllmRealQuantLinear, b, i,
                                     walgo.get_replacement_params('vllm_quant', walgo.w_only))
+        walgo.release()
         del walgo, wm, wx
-        torch.cuda.empty_cache()
+        free_device()
     nblk = args.steps * world
     model = Llama.random(cfg, num_layers=nblk, device=dev, seed=1000)   # same on every rank
     hidden = synthetic_hidden(args.n_samples, args.seq_len, cfg.hidden_size, dev, 17)
     algo = build_algo(model, config, {'data': [hidden], 'kwargs': [model.rotary_kwargs(args.seq_len)]})
     timer = _native.KernelTimer()
+    clock = ClockSampler(dev)
     sync_barrier(world)
     t0 = time.perf_counter()
-    with timer:
+    with timer, clock:
         algo.run_block_loop()
         # deploy: real-quant + vLLM pack; under shard_blocks each rank packs its own blocks and
         # the packed shards are gathered, so every rank ends with the whole deployed model
@@ -385,9 +468,10 @@ def bench_awq(args, rank, world, dev):
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     kern = timer.summary()
     mode = algo.parallel_mode()
+    algo.release()
     del algo, model, hidden
-    torch.cuda.empty_cache()
-    return elapsed, kern, mode
+    free_device()
+    return elapsed, kern, mode, clock.summary()
 
 
 def bench_gptq(args, rank, world, dev):
@@ -446,8 +530,9 @@ def bench_gptq(args, rank, world, dev):
                            'traffic': traffic, 'traffic_source': src,
                            'avg_launch_ms': round(h['avg_ms'], 4),
                            'flops_per_launch': h['flops'] / h['launches']}
+    algo.release()   # block_opt driven directly: the chain graphs go with the algorithm
     del algo, model, hidden, calib
-    torch.cuda.empty_cache()
+    free_device()
     return out
 
 
@@ -500,8 +585,9 @@ def bench_e2e(args, rank, world, dev, which, residency='device'):
         out['streamed'] = {'h2d_gb': round(st['h2d_bytes'] / 2 ** 30, 2),
                            'd2h_gb': round(st['d2h_bytes'] / 2 ** 30, 2),
                            'fetches': st['fetches'], 'prefetched': st['prefetched']}
+    algo.release()
     del algo, model, hidden, calib
-    torch.cuda.empty_cache()
+    free_device()
     return out
 
 
@@ -558,8 +644,9 @@ def bench_l70b(args, rank, world, dev):
                       'lcq_kernels': top}
         if which == 'awq':
             out[which]['roofline'] = gemm_roofline(kern, el)
+        algo.release()
         del algo, model, hidden, calib
-        torch.cuda.empty_cache()
+        free_device()
     out['workload'] = ('Llama-3-70B decoder block (8192 / 28672, 64q/8kv): AWQ w4a16 g128 '
                        '(configs[1] recipe) and GPTQ w4a16 g128 act-order (configs[2] recipe); '
                        'per-GPU replicas at N > 1')
@@ -622,9 +709,11 @@ def bench_fp8(args, rank, world, dev):
                           random_init={'seed': seed, 'std': 0.02})
 
     wm = build(1, 7)   # warm-up: one layer through the same path
-    build_algo(wm, config, None).deploy('vllm_quant')
-    del wm
-    torch.cuda.empty_cache()
+    walgo = build_algo(wm, config, None)
+    walgo.deploy('vllm_quant')
+    walgo.release()
+    del wm, walgo
+    free_device()
     model = build(args.steps, 77)
     algo = build_algo(model, config, None)
     mine = [(m.weight.numel()) for b in model.get_blocks()
@@ -667,8 +756,9 @@ def bench_fp8(args, rank, world, dev):
                            'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic,
                            'traffic_source': src, 'avg_launch_ms': round(t['avg_ms'], 4),
                            'algorithmic_bytes_per_launch': elems * 2.0 / t['launches']}
+    algo.release()
     del algo, model
-    torch.cuda.empty_cache()
+    free_device()
     out['calib_forward'] = bench_fp8_forward(args, fwd_w, dev, world)
     return out
 
@@ -837,7 +927,7 @@ def main():
     # MFMA clock, measured ~4 % on this step after the FP8 and GPTQ legs)
     awq_first = args.algo in ('awq', 'both', 'all')
     if awq_first:
-        elapsed, kern, mode = bench_awq(args, rank, world, dev)
+        elapsed, kern, mode, clock = bench_awq(args, rank, world, dev)
     fp8 = bench_fp8(args, rank, world, dev) if args.algo in ('fp8', 'all') else None
     if args.algo == 'fp8':
         if rank == 0:
@@ -858,7 +948,7 @@ def main():
         return
 
     if not awq_first:
-        elapsed, kern, mode = bench_awq(args, rank, world, dev)
+        elapsed, kern, mode, clock = bench_awq(args, rank, world, dev)
     linears = N_LINEARS_PER_BLOCK * args.steps * world
     value = linears / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -902,6 +992,7 @@ def main():
             'gptq': gptq,
             'fp8': fp8,
             'roofline': roofline,
+            'gpu_sclk_mhz': clock,
             'lcq_kernels': kernel_table(kern, elapsed),
             'cpu_baseline': cpu,
         }

@@ -261,7 +261,8 @@ int lcq_chol_inv_tile(const void* A, int64_t lda, int n, void* L, int64_t ldl, v
  * (prepare_weight: W[:, dead] = 0; W[:, perm]), and on the diagonal i == j sets
  * dead_diag[csrc[j]] entries to 1 then adds *damp (prepare_hessian: H[dead, dead] = 1;
  * H[perm][:, perm]; H[d, d] += damp, with rsrc = csrc = perm reversed for the chain's J H J).
- * uint8 masks / damp may be NULL. cols <= 40960 (one LDS row). */
+ * uint8 masks / damp may be NULL. Any width: rows of <= 40960 columns are staged in LDS,
+ * wider ones gathered straight from the (L2-resident) source row. */
 int lcq_gather_rc(const void* A, int a_dtype, int64_t rows, int64_t cols, int64_t lda,
                   const int64_t* rsrc, const int64_t* csrc, const uint8_t* dead_col,
                   const uint8_t* dead_diag, const float* damp, void* out, int64_t ldo,

@@ -33,32 +33,35 @@ def _needs(target: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
-def _compile(src: Path, headers) -> Path:
-    obj = BUILD / (src.stem + '.o')
+def _compile(src: Path, headers, build_dir: Path = BUILD, defines=()) -> Path:
+    obj = build_dir / (src.stem + '.o')
     if _needs(obj, [src, *headers]):
-        cmd = [HIPCC, *CFLAGS, '-c', str(src), '-o', str(obj)]
+        cmd = [HIPCC, *CFLAGS, *[f'-D{d}' for d in defines], '-c', str(src), '-o', str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f'hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}')
     return obj
 
 
-def build(verbose: bool = False) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
-    LIB_DIR.mkdir(parents=True, exist_ok=True)
+def build(verbose: bool = False, defines=(), lib: Path = LIB, build_dir: Path = BUILD) -> Path:
+    """Compile every csrc/*.hip and link ``lib``. ``defines`` (``NAME=VALUE`` strings) are for
+    probe builds only (scripts/probe_build.py: a separate build_dir and library, loaded through
+    LCQ_LIB_PATH); the product library is always built without them."""
+    build_dir.mkdir(parents=True, exist_ok=True)
+    lib.parent.mkdir(parents=True, exist_ok=True)
     sources = sorted(CSRC.glob('*.hip'))
     headers = sorted(CSRC.glob('*.h')) + sorted(INCLUDE.glob('*.h'))
     jobs = min(len(sources), int(os.environ.get('MAX_JOBS', '8')))
     with cf.ThreadPoolExecutor(max_workers=max(jobs, 1)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, headers), sources))
-    if _needs(LIB, objs):
-        cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(LIB), *map(str, objs)]
+        objs = list(ex.map(lambda s: _compile(s, headers, build_dir, defines), sources))
+    if _needs(lib, objs):
+        cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(lib), *map(str, objs)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f'link failed:\n{r.stdout}\n{r.stderr}')
     if verbose:
-        print(f'built {LIB}')
-    return LIB
+        print(f'built {lib}')
+    return lib
 
 
 if __name__ == '__main__':

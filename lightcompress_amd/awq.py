@@ -43,8 +43,6 @@ class Awq(BaseBlockwiseQuantization):
         self._org_capture_active = False
         self.org_reuse_stats = {'reused': 0, 'recomputed': 0}
         self.reuse_org = True
-        if special.get('overlap_clip') is not None:
-            self.overlap_clip = bool(special['overlap_clip'])
 
     # -- original inspect outputs from the block's own forward ------------------------------
     # search_scale_subset starts from the inspect module's output on the captured input
@@ -314,24 +312,6 @@ class Awq(BaseBlockwiseQuantization):
             best_scales = awq_pick_best(best, best_scales)  # awq.py:255-273
         return best_scales
 
-    # quant_out False: block i + 1's input is block i's FLOAT output, so nothing of block
-    # i + 1 depends on block i's clip search -- with `special.overlap_clip: True` it runs on a
-    # side stream while the next block's calibration forward and scale search run on the
-    # compute stream. Same kernels on the same operands: bit-identical; joined before anything
-    # reads the clipped weights (_join_side_work). Off by default: measured on MI355X the two
-    # time-share the CUs rather than overlap (the projection GEMM holds all 512 registers of
-    # its one wave per SIMD, so no clip wave fits beside it): 692.4 vs 698.9 ms per Llama-3-8B
-    # block, and the per-launch GEMM times (the roofline) then include the contention.
-    overlap_clip = False
-
-    def _clip_async_ok(self):
-        # only inside run_block_loop, whose end joins the side stream (a caller driving
-        # block_opt itself may read the clipped weights right after it)
-        return (self.overlap_clip and getattr(self, '_in_block_loop', False)
-                and torch.cuda.is_available() and not self.quant_out
-                and self.parallel_mode() in ('single', 'shard_blocks')
-                and getattr(self.model, 'streamer', None) is None)
-
     @torch.no_grad()
     def block_transform(self, block, input_feat, block_kwargs):
         if self.trans:
@@ -340,20 +320,7 @@ class Awq(BaseBlockwiseQuantization):
             n_tok = self.config.get('calib', {}).get('seq_len', None)
             self.auto_clipper.reduce_across_ranks = self.parallel_mode() == 'replicate'
             self.auto_clipper.shard_rows = self.parallel_mode() == 'shard_search'
-            if not self._clip_async_ok():
-                self.auto_clipper.run(block, self.block_idx, input_feat, n_sample_token=n_tok)
-                return
-            if getattr(self, '_clip_stream', None) is None:
-                self._clip_stream = torch.cuda.Stream()
-            side = self._clip_stream
-            side.wait_stream(torch.cuda.current_stream())  # scaled weights + features ready
-            for feats in input_feat.values():  # freed by the block loop before the clip ends
-                for t in feats:
-                    for u in (t if isinstance(t, (tuple, list)) else (t,)):
-                        if torch.is_tensor(u) and u.is_cuda:
-                            u.record_stream(side)
-            with torch.cuda.stream(side):
-                self.auto_clipper.run(block, self.block_idx, input_feat, n_sample_token=n_tok)
+            self.auto_clipper.run(block, self.block_idx, input_feat, n_sample_token=n_tok)
 
     @torch.no_grad()
     def subset_transform(self, subset, input_feat, subset_kwargs):

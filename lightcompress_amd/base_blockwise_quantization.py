@@ -15,6 +15,7 @@ reference's algorithm subclasses and YAML configs keep working. MI355X-first dif
 from __future__ import annotations
 
 import functools
+import gc
 from collections import defaultdict
 from functools import partial
 
@@ -65,6 +66,29 @@ class BlockwiseOpt:
         self._batch_ok = None
         if self.input and self.parallel_mode() == 'shard_tokens':
             self._shard_input_tokens()
+
+    def release(self):
+        """Give back what this algorithm object holds on the device beyond the model: the
+        calibration inputs and per-block caches, the algorithm's device-side caches
+        (_release_device_state: GPTQ's captured chain graphs and their pools), the reference
+        cycles that deployed modules form through their quant callables (module.a_qdq ->
+        algorithm -> model), and the caching allocator's free blocks. The reference collects
+        after every block (base_blockwise_quantization.py:420: gc.collect() +
+        torch.cuda.empty_cache()); a finished run -- or a caller that drove block_opt itself --
+        calls this once. deploy / save_model still work afterwards (they read the model only)."""
+        self.input = None
+        for name in ('layers_cache', '_org_cache'):
+            c = self.__dict__.get(name)
+            if isinstance(c, dict):
+                c.clear()
+        self._release_device_state()
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+
+    def _release_device_state(self):
+        """Algorithm-specific device caches (overridden by GPTQ)."""
 
     # how ranks split a block whose input depends on the previous block's quantization
     # (quant_out True): 'shard_search' (AWQ: the ratio grid and the clip rows),
@@ -125,7 +149,6 @@ class BlockwiseOpt:
             self._block_loop()
         finally:
             self._in_block_loop = False
-            self._join_side_work()
 
     def _block_loop(self):
         mode = self.parallel_mode()
@@ -185,17 +208,9 @@ class BlockwiseOpt:
             st.evict(i, dirty=dirty)
 
     def _drain_blocks(self):
-        self._join_side_work()
         st = getattr(self.model, 'streamer', None)
         if st is not None:
             st.drain()
-
-    def _join_side_work(self):
-        """The compute stream waits for side-stream transforms (AWQ's overlapped clip search)
-        before anything reads the weights they wrote."""
-        st = getattr(self, '_clip_stream', None)
-        if st is not None:
-            torch.cuda.current_stream().wait_stream(st)
 
     def _handoff_ok(self):
         """The ring hand-off passes self.input['data'] as a list of tensors whose shapes every
@@ -236,7 +251,6 @@ class BlockwiseOpt:
     def materialize_blocks(self):
         """shard_blocks: publish every transformed float block from its owner (the state one
         GPU would hold after run_block_loop); a no-op otherwise or once done."""
-        self._join_side_work()
         pending = getattr(self, '_pending_owner', None)
         if not pending:
             return
@@ -877,7 +891,6 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                    'fake_quant_wo_kv': EffcientFakeQuantLinear, **_REALQUANT_LINEAR_MAP_}
         if quant_format not in mapping:
             raise NotImplementedError(f"Quant format '{quant_format}' is not implemented.")
-        self._join_side_work()
         module = mapping[quant_format]
         real = quant_format in _REALQUANT_LINEAR_MAP_
         params = self.get_replacement_params(quant_format, self.w_only)
@@ -886,6 +899,9 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         pending = getattr(self, '_pending_owner', None)
         sharded = world > 1 and (self.parallel_mode() == 'shard_units' or own is not None
                                  or (pending and real))
+        # what a published module cannot carry (callables, dicts) is rebuilt from these on the
+        # non-owners: the same a_qdq / w_qdq / quant_config objects the owner's new() received
+        local_attrs = {**params, 'debug_print': {}}
         if not sharded:
             self.materialize_blocks()   # shard_blocks + a float format: publish first
         for i, block in enumerate(self.blocks):
@@ -903,7 +919,8 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                     self._prequant_fp8_block(block, mine)
                 self.model.replace_module_subset(module, block, {'layers': mine}, i, params)
                 if own is None:
-                    P.publish(block, assign, rest_owner=pending[i] if pending else None)
+                    P.publish(block, assign, rest_owner=pending[i] if pending else None,
+                              local_attrs=local_attrs)
                 self._clear_block_cache(block)
             self.visit_block(i, one, next_i=i + 1)
         self._drain_blocks()
@@ -935,7 +952,6 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
 
     @torch.no_grad()
     def save_model(self, path):
-        self._join_side_work()
         rank, world = P.dist_world()
         if getattr(self.model, 'ownership', None) is not None and world > 1:
             # every rank holds only its own blocks / units: per-rank safetensors shards and

@@ -35,8 +35,6 @@
 #define LCQ_BF16_HW 1  // conversion-instruction RNE in the epilogues
 #include "lcq_common.h"
 
-#include <stdlib.h>
-
 namespace lcq {
 namespace g256 {
 
@@ -545,14 +543,11 @@ __global__ void __launch_bounds__(1024) k_loss_reduce(const double* part, int64_
 }
 
 // tile order: 0 = per-XCD 4 x 8 chunks (slot_tile, the default), 1 = N-band-major (tile_nb,
-// measured neutral); LCQ_GEMM_ORDER is read once, at the first launch
-static int tile_order() {
-  static const int order = [] {
-    const char* e = getenv("LCQ_GEMM_ORDER");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return order;
-}
+// measured neutral; probe build -DLCQ_PROBE_GEMM_ORDER=1, scripts/probe_build.py)
+#ifndef LCQ_PROBE_GEMM_ORDER
+#define LCQ_PROBE_GEMM_ORDER 0
+#endif
+static constexpr int tile_order() { return LCQ_PROBE_GEMM_ORDER; }
 
 static void plan(Args& a, int64_t tile_n) {
   a.n_mt = (int)((a.m + ST - 1) / ST);

@@ -30,7 +30,6 @@
 // workspace, combined in a fixed order by k_syrk_reduce (deterministic: no float atomics).
 #include "lcq_common.h"
 
-#include <stdlib.h>
 
 namespace lcq {
 namespace hx {
@@ -520,14 +519,12 @@ static int64_t ceil_to(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // (6 ~ prologue + the 256 KB fp32 tile store); every split adds a 256 KB partial tile written
 // and re-read by k_syrk_reduce (~0.034 K-tile times at HBM rate). Pick the ns with the least
 // modelled time (n = 262144: ic 4096 -> 15, ic 8192 -> 8, ic 14336 -> 4). At least 8 K-tiles
-// per split; partial slabs capped at 8 GiB. LCQ_SYRK_NS (read once) forces a count.
-static int forced_ns() {
-  static const int v = [] {
-    const char* e = getenv("LCQ_SYRK_NS");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+// per split; partial slabs capped at 8 GiB. A probe build (-DLCQ_PROBE_SYRK_NS=<n>, see
+// scripts/probe_build.py) forces a count; the product library has no run-time override.
+#ifndef LCQ_PROBE_SYRK_NS
+#define LCQ_PROBE_SYRK_NS 0
+#endif
+static constexpr int forced_ns() { return LCQ_PROBE_SYRK_NS; }
 
 static void plan(int64_t n, int64_t ic, int& nt, int& ntiles, int& ns, int64_t& ktps,
                  int64_t& nkt, int64_t& icp) {
@@ -566,14 +563,13 @@ using namespace lcq::hx;
 // Per-group split count of the grouped launch: the same cost model with the grid taken as
 // GMAX groups launched together. It depends only on (group tokens, ic) -- never on how many
 // groups this process launches -- so a token-sharded rank splits its groups exactly as one GPU
-// does (the fp32 fold order per group is world-independent).
-static int forced_gns() {  // probe override of the per-group split count (read once)
-  static const int v = [] {
-    const char* e = getenv("LCQ_SYRK_GNS");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+// does (the fp32 fold order per group is world-independent). The split count changes the fp32
+// fold order, so it is never a run-time knob: only a probe build (-DLCQ_PROBE_SYRK_GNS=<n>,
+// scripts/probe_build.py) forces it.
+#ifndef LCQ_PROBE_SYRK_GNS
+#define LCQ_PROBE_SYRK_GNS 0
+#endif
+static constexpr int forced_gns() { return LCQ_PROBE_SYRK_GNS; }
 
 static void plan_group(int64_t n, int64_t ic, int64_t& ns, int64_t& ktps, int64_t& nkt) {
   const int64_t icp = ceil_to(ic, ST);

@@ -61,6 +61,11 @@ class GPTQ(BaseBlockwiseQuantization):
         finally:
             gptq_core.clear_chain_graphs()  # the chain graphs' pools end with the run
 
+    def _release_device_state(self):
+        # a caller that drove block_opt directly (no run_block_loop) leaves the chain graphs
+        # captured: their pools (~4-5 n^2 fp32 per Hessian size) go with the algorithm
+        gptq_core.release_device_state()
+
     @torch.no_grad()
     def collect_model_qparams(self):
         for block in self.blocks:
@@ -115,8 +120,14 @@ class GPTQ(BaseBlockwiseQuantization):
     @torch.no_grad()
     def block_init(self, block):
         self.named_layers = self.model.get_block_linears(block)
-        if any(not hasattr(m, 'buf_scales') for m in self.named_layers.values()):
+        # the reference collects every block's original-weight qparams at construction
+        # (gptq.py __init__ -> collect_model_qparams); here on this instance's first visit of the
+        # block (same weights: nothing else has touched them), never reusing buf_scales an
+        # earlier pass (HQQ, a reused model) left behind
+        done = self.__dict__.setdefault('_qparams_collected', set())
+        if self.block_idx not in done:
             self.collect_block_qparams(block)
+            done.add(self.block_idx)
         subsets = self.model.get_subsets_in_block(block)
         # with true_sequential the reference re-initialises every later subset's Hessian in
         # rehook_next_subset, so only the first subset's first-pass Hessian is ever used

@@ -352,6 +352,12 @@ def clear_chain_graphs():
         torch.cuda.empty_cache()
 
 
+def release_device_state():
+    """clear_chain_graphs + the recursion's side streams (BlockwiseOpt.release)."""
+    clear_chain_graphs()
+    _side_streams.clear()
+
+
 def _inverse_cholesky_upper_filled(fill, n: int, device) -> torch.Tensor:
     """U = J chol(Hr)^-1 J where fill(buf) writes Hr = J H J (n x n fp32) into buf."""
     graphed = torch.device(device).type == 'cuda' and n >= _GRAPH_MIN and CHAIN_GRAPHS

@@ -648,7 +648,7 @@ _CONST_CACHE: dict = {}
 def _const_f32(values, device) -> torch.Tensor:
     """A small constant fp32 vector on the device, uploaded once per (device, values): a
     fresh torch.tensor(list, device=...) is a pageable copy that blocks the host until the
-    stream drains (the overlapped clip search would lose its overlap to it)."""
+    stream drains (the host would stop running ahead of the kernels)."""
     key = (torch.device(device).index, tuple(values))
     t = _CONST_CACHE.get(key)
     if t is None:
@@ -1047,14 +1047,17 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
     # every class's descriptors (and the class order, to put the scales back) in ONE upload
     upload = torch.tensor(rec + flat, dtype=torch.int64).to(dev)
     descs = upload[:5 * n]
-    sc_cls = sc if len(classes) == 1 else torch.empty(n, dtype=torch.float32, device=dev)
+    # the kernel writes scale p for weight flat[p]: unless the class order is the input order,
+    # the scales land in a temporary and are scattered back to input order
+    in_order = flat == list(range(n))
+    sc_cls = sc if in_order else torch.empty(n, dtype=torch.float32, device=dev)
     off = 0
     for cls in classes:
         N.call('lcq_fp8_block_to_tensor_many', len(cls), descs.data_ptr() + off * 40,
                codes[cls[0]].numel(), N.dt(codes[0].dtype), block, N.dt(fp8), qmax, 1e-5, 1,
                N.ptr(ws), sc_cls.data_ptr() + off * 4, N.stream_of(codes[0]))
         off += len(cls)
-    if len(classes) > 1:
+    if not in_order:
         sc[upload[5 * n:]] = sc_cls
     return outs, sc
 

@@ -168,11 +168,19 @@ def planned_mode(config, world: int) -> str:
     return getattr(ALGO_REGISTRY[q['method']], 'sequential_parallel_mode', 'replicate')
 
 
+_PLAIN = (int, float, str, bool, tuple, torch.Size, torch.dtype, type(None))
+
+
 def _plain_attrs(m):
     return {k: v for k, v in m.__dict__.items()
-            if not k.startswith('_') and k != 'training'
-            and isinstance(v, (int, float, str, bool, tuple, torch.Size, torch.dtype,
-                               type(None)))}
+            if not k.startswith('_') and k != 'training' and isinstance(v, _PLAIN)}
+
+
+def _opaque_attrs(m):
+    """Names of a module's attributes that cannot travel as a spec (callables such as a fake-quant
+    module's a_qdq, dicts such as its debug_print): the non-owner rebuilds them locally."""
+    return sorted(k for k, v in m.__dict__.items()
+                  if not k.startswith('_') and k != 'training' and not isinstance(v, _PLAIN))
 
 
 def _slots(m, recurse):
@@ -188,15 +196,19 @@ def _dt(t):
 
 
 @torch.no_grad()
-def publish(block: torch.nn.Module, assign: dict, rest_owner: int | None = None):
+def publish(block: torch.nn.Module, assign: dict, rest_owner: int | None = None,
+            local_attrs: dict | None = None):
     """After each rank replaced the block's modules it owns (``assign``: module name relative
     to the block -> owner rank), give every rank the same block: the non-owners rebuild each
     module as an empty instance of the owner's class (same plain attributes, parameters and
     buffers of the owner's shapes and dtypes; their old modules are dropped unread), then
     every owner broadcasts ALL its modules' tensors as one flat byte buffer. With
     ``rest_owner`` the block's other tensors (norms, ...) come from that rank the same way,
-    buffers it registered included. Collectives: one all_gather_object of the specs, one
-    broadcast per owner with data."""
+    buffers it registered included. Attributes that are not plain values (a fake-quant
+    module's ``a_qdq`` callable, its ``debug_print`` dict) cannot be shipped: a rebuilt module
+    takes them from ``local_attrs`` (the local algorithm's replacement params -- the same
+    callables the owner used), and a missing one raises here rather than at the first forward.
+    Collectives: one all_gather_object of the specs, one broadcast per owner with data."""
     rank, world = dist_world()
     if world == 1:
         return
@@ -208,7 +220,7 @@ def publish(block: torch.nn.Module, assign: dict, rest_owner: int | None = None)
         mine.append((n, type(m).__module__, type(m).__qualname__, _plain_attrs(m),
                      [(kind, tn, None if t is None else tuple(t.shape),
                        None if t is None else _dt(t))
-                      for _, _, kind, tn, t in _slots(m, recurse=False)]))
+                      for _, _, kind, tn, t in _slots(m, recurse=False)], _opaque_attrs(m)))
     rest = None
     if rest_owner == rank:
         under = tuple(f'{n}.' for n in assign)
@@ -222,7 +234,7 @@ def publish(block: torch.nn.Module, assign: dict, rest_owner: int | None = None)
     for r, (mods, rst) in enumerate(specs):
         if r == rank:
             continue
-        for n, modname, qual, attrs, tensors in mods:
+        for n, modname, qual, attrs, tensors, opaque in mods:
             cls = importlib.import_module(modname)
             for part in qual.split('.'):
                 cls = getattr(cls, part)
@@ -238,6 +250,12 @@ def publish(block: torch.nn.Module, assign: dict, rest_owner: int | None = None)
                     m.register_buffer(tn, t)
             for k, v in attrs.items():
                 setattr(m, k, v)
+            for k in opaque:
+                if local_attrs is None or k not in local_attrs:
+                    raise RuntimeError(f'publish: attribute {k!r} of {qual} {n!r} (owner rank '
+                                       f'{r}) is not a plain value and no local value was '
+                                       'given (local_attrs)')
+                setattr(m, k, local_attrs[k])
             parent_name, _, child = n.rpartition('.')
             parent = block.get_submodule(parent_name) if parent_name else block
             setattr(parent, child, m)
@@ -254,7 +272,7 @@ def publish(block: torch.nn.Module, assign: dict, rest_owner: int | None = None)
                     mod.register_buffer(tn, new)
     for r, (mods, rst) in enumerate(specs):
         ts = []
-        for n, _, _, _, tensors in mods:
+        for n, _, _, _, tensors, _ in mods:
             m = block.get_submodule(n)
             ts += [getattr(m, kind)[tn] for kind, tn, shape, _ in tensors if shape is not None]
         for mn, kind, tn, _, _ in (rst or []):

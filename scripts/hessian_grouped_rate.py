@@ -1,6 +1,7 @@
 """Probe: the grouped GPTQ Hessian (one lcq_hessian_grouped launch over 8 sample groups) against
 the round-3 form (one lcq_hessian_accum per group + lcq_tree_sum), at the Llama-3-8B GPTQ
-calibration size (128 x 2048 tokens), IC 4096 and 14336. LCQ_SYRK_GNS forces the per-group
+calibration size (128 x 2048 tokens), IC 4096 and 14336. A probe library
+(scripts/probe_build.py LCQ_PROBE_SYRK_GNS=<n>, loaded via LCQ_LIB_PATH) forces the per-group
 split count of the grouped plan."""
 import sys
 from pathlib import Path

@@ -273,39 +273,3 @@ def test_auto_clip_pc_llama_shape(dev):
     grid = torch.stack([(am * (1 - i / 20)).to(torch.bfloat16).float() for i in range(10)], 1)
     assert bool((grid == bmax.cpu().float().view(-1, 1)).any(dim=1).all())
     assert torch.equal(bits(bmin), bits(-bmax))
-
-
-def test_overlapped_clip_bit_identical(dev, monkeypatch):
-    """quant_out False: block i's auto-clip search runs on a side stream while block i + 1's
-    calibration forward and scale search run (Awq.overlap_clip, special.overlap_clip); the
-    deployed weights equal the serial run's bit for bit."""
-    from transformers import LlamaConfig
-
-    from lightcompress_amd.awq import Awq
-    from lightcompress_amd.llama import Llama
-    from lightcompress_amd.pipeline import build_algo
-    from lightcompress_amd.utils import load_config
-    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=4,
-                      num_key_value_heads=2, num_hidden_layers=4, vocab_size=128,
-                      max_position_embeddings=512, rms_norm_eps=1e-5)
-    conf = {'calib': {'seq_len': 64},
-            'quant': {'method': 'Awq', 'weight': {'bit': 4, 'symmetric': True,
-                                                  'granularity': 'per_group', 'group_size': 128},
-                      'special': {'trans': True, 'trans_version': 'v2', 'weight_clip': True,
-                                  'clip_sym': True}, 'quant_out': False}}
-    out = []
-    for overlap in (False, True):
-        monkeypatch.setattr(Awq, 'overlap_clip', overlap)
-        model = Llama.random(cfg, device=dev, seed=3)
-        g = torch.Generator(device=dev).manual_seed(9)
-        x = torch.randn(4, 64, 256, generator=g, device=dev).to(torch.bfloat16)
-        algo = build_algo(model, load_config(conf), {'data': [x], 'kwargs': [model.rotary_kwargs(64)]})
-        algo.run_block_loop()
-        assert (getattr(algo, '_clip_stream', None) is not None) == overlap
-        algo.deploy('fake_quant')
-        out.append({f'{i}.{n}': m.weight.detach().clone()
-                    for i, b in enumerate(model.get_blocks())
-                    for n, m in model.get_block_linears(b).items()})
-    assert out[0].keys() == out[1].keys()
-    for k in out[0]:
-        assert torch.equal(out[0][k], out[1][k]), k

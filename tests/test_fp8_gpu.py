@@ -156,6 +156,18 @@ def test_block_fp8_to_tensor_batched_equals_single(dev):
         assert torch.equal(bits(outs[i]), bits(oc)) and scales[i].item() == os_.item()
 
 
+def test_block_fp8_to_tensor_many_one_class_unsorted(dev):
+    """Sizes within 2x of each other (ONE size class) given out of size order: the per-tensor
+    scales must still come back in input order (the kernel writes them in class order)."""
+    from lightcompress_amd import ops
+    cs, ss = zip(*[_random_block_fp8(sh, torch.float8_e4m3fn, 60 + i, dev)
+                   for i, sh in enumerate([(1024, 1280), (1536, 1280), (1280, 1280)])])
+    outs, scales = ops.fp8_block_to_tensor_many(list(cs), list(ss), 128)
+    for i, (c, s) in enumerate(zip(cs, ss)):
+        oc, os_ = ops.fp8_block_to_tensor(c, s, 128)
+        assert torch.equal(bits(outs[i]), bits(oc)) and scales[i].item() == os_.item(), i
+
+
 def _random_block_fp8(shape, fin, seed, dev, nan_free=True):
     """Random code bytes (every finite code of ``fin`` reachable) + random-sign block scales."""
     g = torch.Generator().manual_seed(seed)

@@ -692,3 +692,30 @@ def test_gather_rc_equals_torch_prepare(dev, n):
     assert torch.equal(wgot, wref)
     inv = torch.argsort(perm)
     assert torch.equal(ops.gather_rc(wgot, csrc=inv), wref[:, inv])
+
+
+def test_gather_rc_wider_than_lds(dev):
+    """Rows of 53248 fp32 columns (Llama-3.1-405B down_proj IC) exceed one LDS image: the
+    unstaged path must give the same gathers (weight side, and a row slice of the Hessian side
+    with the dead-diagonal fix and damp on the rows that hold the diagonal)."""
+    from lightcompress_amd import ops
+    n = 53248
+    g = torch.Generator(device=dev).manual_seed(7)
+    perm = torch.randperm(n, generator=g, device=dev)
+    dead = torch.zeros(n, dtype=torch.bool, device=dev)
+    dead[perm[:9]] = True
+    W = (torch.randn(64, n, generator=g, device=dev) * 0.02).to(torch.bfloat16)
+    wref = W.float().clone()
+    wref[:, dead] = 0
+    wref = wref[:, perm].contiguous()
+    assert torch.equal(ops.gather_rc(W, csrc=perm, dead_col=dead), wref)
+    Hrows = torch.randn(48, n, generator=g, device=dev)   # the source rows 0..47 of H
+    rsrc = torch.arange(48, device=dev)
+    damp = torch.tensor(0.5, device=dev)
+    csrc = torch.cat([torch.arange(48, device=dev), perm[perm >= 48][: n - 48]])
+    got = ops.gather_rc(Hrows, rsrc=rsrc, csrc=csrc, dead_diag=dead, damp=damp)
+    ref = Hrows[:, csrc].clone()
+    d = torch.arange(48, device=dev)
+    diag = torch.where(dead[csrc[:48]], torch.ones(48, device=dev), ref[d, d])
+    ref[d, d] = diag + damp
+    assert torch.equal(got, ref)

@@ -246,6 +246,50 @@ def test_publish_mixed_modules():
     assert r['norm'] == 16.0 and r['extra'] == 3.0
 
 
+def _fake_quant_w8a8(rank, world):
+    """Data-free W8A8 dynamic RTN (per-channel weights, per-token activations) deployed as
+    fake_quant under shard_units: the modules a rank did not quantize arrive through publish and
+    must still carry the fake-quant callables (a_qdq) -- a forward through every deployed linear
+    on every rank. Quantizers on the oracle (no HIP on the CPU); forwards through F.linear."""
+    from lightcompress_amd.module_utils import EffcientFakeQuantLinear
+    from lightcompress_amd.pipeline import build_algo, build_model
+    from lightcompress_amd.quant import IntegerQuantizer
+    from oracle import quant_ref as Q
+
+    def wfq(self, w, args={}):
+        return Q.fake_quant_dynamic(w, self.bit, self.sym, self.granularity,
+                                    getattr(self, 'group_size', 128))[0]
+
+    def afq(self, x, args={}):
+        return Q.fake_quant_dynamic(x.reshape(-1, x.shape[-1]), self.bit, self.sym,
+                                    'per_channel')[0].view(x.shape)
+    IntegerQuantizer.fake_quant_weight_dynamic = wfq
+    IntegerQuantizer.fake_quant_act_dynamic = afq
+    cfg = _config('Opt', extra_quant={
+        'weight': {'bit': 8, 'symmetric': True, 'granularity': 'per_channel'},
+        'act': {'bit': 8, 'symmetric': True, 'granularity': 'per_token'}})
+    model = build_model(cfg, device='cpu')
+    algo = build_algo(model, cfg, None)
+    assert algo.parallel_mode() == ('single' if world == 1 else 'shard_units')
+    algo.run_block_loop()
+    algo.deploy('fake_quant')
+    g = torch.Generator().manual_seed(3)
+    outs = {}
+    for i, b in enumerate(model.get_blocks()):
+        for n, m in model.get_block_linears(b).items():
+            assert isinstance(m, EffcientFakeQuantLinear), (n, type(m))
+            assert callable(m.a_qdq) and m.debug_print == {}, n
+            x = torch.randn(3, m.in_features, generator=g).to(m.weight.dtype)
+            outs[f'{i}.{n}'] = m(x).float().tolist()
+    return outs
+
+
+def test_shard_units_fake_quant_forward_on_every_rank():
+    single = _fake_quant_w8a8(0, 1)
+    res = run2(_fake_quant_w8a8)
+    assert res[0] == res[1] == single
+
+
 @pytest.mark.parametrize('calib,quant_out,special,expect', [
     (False, False, None, 'shard_units'), (True, False, None, 'shard_blocks'),
     (True, True, None, 'shard_tokens'), (True, True, 'replicate', 'replicate')])

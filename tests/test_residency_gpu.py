@@ -98,6 +98,14 @@ RECIPES = {
                                                      'group_size': 64,
                                                      'pack_version': 'gemm_pack'}},
                         'autoawq_quant'),
+    # data-free W8A8 dynamic (per-channel weights, per-token activations) deployed as
+    # fake_quant: the published modules must carry a_qdq (forward checked below)
+    'opt_rtn_w8a8_fake': ({'type': 'Opt', 'path': str(TM.MODEL_DIRS['Opt']),
+                           'torch_dtype': 'float16'},
+                          {'method': 'RTN', 'weight': {'bit': 8, 'symmetric': True,
+                                                       'granularity': 'per_channel'},
+                           'act': {'bit': 8, 'symmetric': True, 'granularity': 'per_token'}},
+                          'fake_quant'),
 }
 
 
@@ -125,6 +133,12 @@ def _run_recipe(name, fp8_dir, materialize='all', save=None):
         algo.save_model(save)
     out = {f'{i}.{n}': t.detach().cpu() for i, b in enumerate(model.get_blocks())
            for n, t in [*b.named_parameters(), *b.named_buffers()] if not t.is_meta}
+    if fmt == 'fake_quant':   # a forward through every deployed linear (act fake quant too)
+        g = torch.Generator(device='cuda:0').manual_seed(1)
+        for i, b in enumerate(model.get_blocks()):
+            for n, m in model.get_block_linears(b).items():
+                x = torch.randn(5, m.in_features, generator=g, device='cuda:0').to(m.weight.dtype)
+                out[f'fwd.{i}.{n}'] = m(x).detach().cpu()
     return out, never
 
 
@@ -154,14 +168,17 @@ def _two_ranks(name, fp8_dir, tmp_path, materialize='all', save=None):
     return [torch.load(f'{path}.{r}', weights_only=True) for r in range(2)]
 
 
-@pytest.mark.parametrize('name', ['opt_rtn_w8', 'dsv3_rtn_w_only'])
+@pytest.mark.parametrize('name', ['opt_rtn_w8', 'dsv3_rtn_w_only', 'opt_rtn_w8a8_fake'])
 def test_shard_units_two_ranks_match_single(dev, name, tmp_path):
     for k in ('RANK', 'WORLD_SIZE'):
         os.environ.pop(k, None)
     fp8_dir = _fp8_checkpoint(str(tmp_path / 'dsv3_fp8'))
     single, _ = _run_recipe(name, fp8_dir)
-    assert any(k.endswith(('weight', 'weight_packed', 'qweight')) and
-               v.dtype in (torch.int8, torch.int32) for k, v in single.items())
+    if name.endswith('_fake'):
+        assert any(k.startswith('fwd.') for k in single)
+    else:
+        assert any(k.endswith(('weight', 'weight_packed', 'qweight')) and
+                   v.dtype in (torch.int8, torch.int32) for k, v in single.items())
     for res in _two_ranks(name, fp8_dir, tmp_path):
         multi = res['out']
         assert single.keys() == multi.keys()
@@ -189,3 +206,58 @@ def test_owned_sharded_save_matches_single(dev, tmp_path):
     assert sorted(a) == sorted(b)
     for k in a:
         assert a[k].dtype == b[k].dtype and torch.equal(a[k], b[k]), k
+
+
+def test_stream_bounds_device_memory(dev):
+    """``residency: stream`` keeps at most ~3 blocks in HBM (the one being transformed, the
+    next one arriving, the previous one leaving: residency.py), so over the same AWQ run +
+    vLLM deploy its device-memory peak above the post-load footprint must undercut the
+    HBM-resident run's peak by at least (model bytes - 3 blocks): the reference's
+    block.cuda() / block.cpu() bound (base_blockwise_quantization.py:397, 418)."""
+    import gc
+
+    from transformers import LlamaConfig
+
+    from lightcompress_amd.llama import Llama
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.utils import load_config
+    cfg = LlamaConfig(hidden_size=512, intermediate_size=2048, num_attention_heads=8,
+                      num_key_value_heads=4, num_hidden_layers=12, vocab_size=128,
+                      max_position_embeddings=512, rms_norm_eps=1e-5)
+    conf = load_config({'calib': {'seq_len': 64},
+                        'quant': {'method': 'Awq',
+                                  'weight': {'bit': 4, 'symmetric': True,
+                                             'granularity': 'per_group', 'group_size': 128,
+                                             'need_pack': True},
+                                  'special': {'trans': True, 'trans_version': 'v2',
+                                              'weight_clip': True, 'clip_sym': True},
+                                  'quant_out': False}})
+
+    def run(residency):
+        model = Llama.random(cfg, device=dev, seed=3, residency=residency)
+        blocks = model.get_blocks()
+        block_bytes = sum(t.numel() * t.element_size()
+                          for t in [*blocks[0].parameters(), *blocks[0].buffers()])
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        start = torch.cuda.memory_allocated(dev)
+        torch.cuda.reset_peak_memory_stats(dev)
+        g = torch.Generator(device=dev).manual_seed(9)
+        x = torch.randn(4, 64, 512, generator=g, device=dev).to(torch.bfloat16)
+        algo = build_algo(model, conf, {'data': [x], 'kwargs': [model.rotary_kwargs(64)]})
+        algo.run_block_loop()
+        algo.deploy('vllm_quant')
+        torch.cuda.synchronize()
+        peak = torch.cuda.max_memory_allocated(dev)
+        algo.release()
+        del algo, x
+        return start, peak, block_bytes, len(blocks), model
+
+    s_dev, p_dev, bb, n, m_dev = run('device')
+    del m_dev
+    s_str, p_str, _, _, m_str = run('stream')
+    assert m_str.streamer is not None
+    model_bytes = n * bb
+    assert s_dev - s_str >= model_bytes - bb, (s_dev, s_str, model_bytes)  # blocks on the host
+    assert p_str <= p_dev - (model_bytes - 3 * bb), (p_str, p_dev, model_bytes, bb)
