@@ -12,8 +12,9 @@ the real shapes (no network: no checkpoints / datasets).
 metric: linear layers quantized per second (whole job, all ranks). Multi-GPU: one process per
 GPU (torchrun); quant_out=False makes AWQ blocks independent given the float activations
 (SURVEY.md §8e), so the timed run is the algorithm's own run_block_loop in shard_blocks mode
-over steps x N blocks: every rank quantizes its blocks, runs the float forward of the others
-(the activation chain) and receives their quantized weights by broadcast -- weak scaling.
+over steps x N blocks with materialize: owned: every rank allocates, quantizes and packs only
+its own blocks, the float activations pass from the owner of block i to the owner of block i + 1
+over a ring edge (the only collective on the data path) -- weak scaling.
 
 Also in the line:
 * "gptq" (configs[2]): Llama-3-8B GPTQ w4a16 g128 asym, act-order, true_sequential, quant_out,
@@ -452,7 +453,16 @@ def bench_awq(args, rank, world, dev):
         del walgo, wm, wx
         free_device()
     nblk = args.steps * world
-    model = Llama.random(cfg, num_layers=nblk, device=dev, seed=1000)   # same on every rank
+    if world == 1:
+        model = Llama.random(cfg, num_layers=nblk, device=dev, seed=1000)
+    else:
+        # shard_blocks: each rank materialises only its own blocks (materialize: owned; the
+        # other blocks stay on the meta device, every tensor seeded by its name so a block is
+        # the same whichever rank builds it); the deploy packs each rank's blocks in place
+        from lightcompress_amd.utils import load_config
+        config = load_config(dict(config, model={'type': 'Llama', 'materialize': 'owned'}))
+        model = Llama(config, hf_config=LlamaConfig(**dict(LLAMA3_8B, num_hidden_layers=nblk)),
+                      random_init={'seed': 1000, 'std': 0.02}, device=dev)
     hidden = synthetic_hidden(args.n_samples, args.seq_len, cfg.hidden_size, dev, 17)
     algo = build_algo(model, config, {'data': [hidden], 'kwargs': [model.rotary_kwargs(args.seq_len)]})
     timer = _native.KernelTimer()
@@ -985,8 +995,10 @@ def main():
                        'model': 'Llama-3-8B (4096/14336, 32q/8kv heads)',
                        'global_batch': args.n_samples, 'seq_len': args.seq_len,
                        'parallelism': (f'run_block_loop {mode}: {args.steps} blocks per GPU '
-                                       f'x {world} GPU(s); ring hand-off of block activations + '
-                                       'packed-shard gather included')},
+                                       f'x {world} GPU(s)' + ('' if world == 1 else
+                                       '; materialize: owned (each rank allocates and packs '
+                                       'its own blocks only), ring hand-off of the block '
+                                       'activations over the edge pairs'))},
             'e2e': e2e,
             'l70b': l70b,
             'gptq': gptq,

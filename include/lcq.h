@@ -247,6 +247,17 @@ int lcq_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
                     const void* B, int64_t ldb, int bt, float beta, void* C, int64_t ldc,
                     void* workspace, int64_t ws_bytes, void* stream);
 
+/* Rows [row0, row1) of the lcq_gemm_f32 product C = beta C + alpha A op(B) (A, C the FULL
+ * [M, *] operands): the kernel variant and tile size are those the full M x N product gets
+ * (never stream-K), so every output element is computed with the same k order whichever rank
+ * computes it -- the factorisation's large products row-split over the ranks of a
+ * token-sharded GPTQ run (gptq.py:161-170; gptq_core.chain_sharding) are bit-identical to one
+ * GPU's. row0 / row1 on multiples of lcq_gemm_f32_row_unit(M, N) (64 or 128; row1 may be M). */
+int64_t lcq_gemm_f32_row_unit(int64_t M, int64_t N);
+int lcq_gemm_f32_rows(int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
+                      const void* B, int64_t ldb, int bt, float beta, void* C, int64_t ldc,
+                      int64_t row0, int64_t row1, void* stream);
+
 /* Diagonal tile of the recursive fp32 factorisation behind U = chol(H^-1, upper)
  * (gptq.py:169-174): for SPD A (n x n, n <= 128, row-major fp32, leading dim lda), X <- L^-1
  * and, if L is not NULL, L <- the lower Cholesky factor (upper parts zeroed). A is only read.

@@ -909,15 +909,15 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
                 self.block_idx = i
                 lins = self.model.get_block_linears(block)
                 if not sharded:
-                    if real:
-                        self._prequant_fp8_block(block, lins)
-                    self.model.replace_module_block(module, block, i, params)
+                    pre = self._prequant_fp8_block(block, lins) if real else None
+                    self.model.replace_module_subset(module, block, {'layers': lins}, i, params,
+                                                     prequant=pre)
                     return
                 assign = {n: self.unit_owner(i, n) for n in lins}
                 mine = {n: m for n, m in lins.items() if assign[n] == rank}
-                if real:
-                    self._prequant_fp8_block(block, mine)
-                self.model.replace_module_subset(module, block, {'layers': mine}, i, params)
+                pre = self._prequant_fp8_block(block, mine) if real else None
+                self.model.replace_module_subset(module, block, {'layers': mine}, i, params,
+                                                 prequant=pre)
                 if own is None:
                     P.publish(block, assign, rest_owner=pending[i] if pending else None,
                               local_attrs=local_attrs)
@@ -931,24 +931,31 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
         """Block-fp8 checkpoint linears (DeepSeek-V3 experts) headed for a per-tensor FP8
         real-quant format: requantize every such linear of the block in ONE batched launch
         (lcq_fp8_block_to_tensor_many) instead of one dequant + quant chain per linear;
-        quant_pack picks the results up (bit-identical to the per-linear chain)."""
+        the real-quant module's new_batch takes the results (bit-identical to the per-linear
+        chain). Returns {id(module): (codes, scale)}, or None when the format does not apply."""
         wq = self.wquantizer
         if not (isinstance(wq, FloatQuantizer) and wq.granularity == 'per_tensor'
                 and wq.use_qtorch and wq.fp8_dtype is not None):
-            return
+            return None
         if self.quant_config['weight'].get('need_pack', False):
-            return
-        mods = [m for m in mods.values()
-                if getattr(m, 'weight', None) is not None and not getattr(m, 'no_quant', False)
-                and m.weight.dtype == torch.float8_e4m3fn and hasattr(m, 'weight_scale_inv')]
-        if not mods:
-            return
-        bs = getattr(mods[0], 'block_size', getattr(self, 'fp8_block_size', 128))
+            return None
+        sel = []   # (module, weight, weight_scale_inv): read from the slot dicts directly
+        for m in mods.values():
+            d = m.__dict__
+            w = d['_parameters'].get('weight', d['_buffers'].get('weight'))
+            if w is None or d.get('no_quant', False) or w.dtype != torch.float8_e4m3fn:
+                continue
+            si = d['_parameters'].get('weight_scale_inv', d['_buffers'].get('weight_scale_inv'))
+            if si is not None:
+                sel.append((m, w, si))
+        if not sel:
+            return None
+        bs = getattr(sel[0][0], 'block_size', getattr(self, 'fp8_block_size', 128))
         codes, scales = ops.fp8_block_to_tensor_many(
-            [m.weight.data for m in mods], [m.weight_scale_inv.data for m in mods], bs,
-            wq.fp8_dtype, qmax=wq._qmax_f())
-        for i, m in enumerate(mods):
-            m._lcq_prequant = (codes[i], scales[i:i + 1].view(1))
+            [w.data for _, w, _ in sel], [si.data for _, _, si in sel], bs, wq.fp8_dtype,
+            qmax=wq._qmax_f())
+        sv = scales.view(-1, 1)
+        return {id(m): (codes[i], sv[i]) for i, (m, _, _) in enumerate(sel)}
 
     @torch.no_grad()
     def save_model(self, path):

@@ -419,9 +419,29 @@ class BaseModel:
         return (same(m.w_qdq, params_dict.get('w_qdq')) and
                 same(m.a_qdq, params_dict.get('a_qdq')))
 
-    def replace_module_subset(self, module, block, subset, block_idx, params_dict):
+    def replace_module_subset(self, module, block, subset, block_idx, params_dict,
+                              prequant=None):
         """base_model.py:405-436 (linears only; the MoE router and other non-linear layers of
-        a subset keep their class)."""
+        a subset keep their class). Classes with new_batch (the real-quant linears) build the
+        whole subset at once, with `prequant` (module -> (codes, scales), a block's batched
+        requant) for the modules it covers."""
+        if hasattr(module, 'new_batch'):
+            items = [(name, m) for name, m in subset['layers'].items()
+                     if isinstance(m, _LINEAR_TYPES) and not getattr(m, 'no_quant', False)]
+            pre = None if prequant is None else [prequant.get(id(m)) for _, m in items]
+            news = module.new_batch([m for _, m in items], prequant=pre, **params_dict)
+            parents = {}
+            for (name, old), new in zip(items, news):
+                parent_name, _, child = name.rpartition('.')
+                parent = parents.get(parent_name)
+                if parent is None:
+                    parent = parents[parent_name] = (block.get_submodule(parent_name)
+                                                     if parent_name else block)
+                if parent._modules.get(child) is old:
+                    parent._modules[child] = new   # what nn.Module.__setattr__ does here
+                else:
+                    setattr(parent, child, new)
+            return
         for name, m in subset['layers'].items():
             if not isinstance(m, _LINEAR_TYPES) or getattr(m, 'no_quant', False):
                 continue
@@ -432,9 +452,9 @@ class BaseModel:
             parent = block.get_submodule(parent_name) if parent_name else block
             setattr(parent, child, new)
 
-    def replace_module_block(self, module, block, block_idx, params_dict):
+    def replace_module_block(self, module, block, block_idx, params_dict, prequant=None):
         self.replace_module_subset(module, block, {'layers': self.get_block_linears(block)},
-                                   block_idx, params_dict)
+                                   block_idx, params_dict, prequant=prequant)
 
     def replace_module_all(self, module, params_dict, keep_device=True):
         for i, block in enumerate(self.blocks):

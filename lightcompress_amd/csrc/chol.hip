@@ -1,348 +1,304 @@
 // Diagonal-tile kernel of the recursive fp32 Cholesky / triangular inverse behind GPTQ's
 // U = chol(H^-1, upper) (gptq.py:169-174; computed as J chol(J H J)^-1 J, see gptq_core).
 // The recursion (host side) does the large updates as fp32 GEMMs; this kernel factors a
-// <= 128 x 128 diagonal tile and inverts its factor, in one workgroup with both in LDS.
+// <= 128 x 128 diagonal tile and inverts its factor, in one 256-thread workgroup.
 //
-// Right-looking over PW-column panels on the augmented [A | R], R = I initially; after panel P
-// R's rows P hold X_P = L_PP^-1 R_P, the rows of L^-1 (blocked forward substitution of L X = I):
-//   S1 (one wave, registers): every lane factors the whole PW x PW diagonal block redundantly
-//      in its own registers (no cross-lane traffic, no barriers), then lane j computes column
-//      j of Z = L_PP^-1;
-//   S2 (threads 0-127) X_P = Z R_P, one thread per column; (threads 128-255)
-//      L_below = A_below Z^T, one thread per row;
-//   S3 (all threads, two tile loops): A22 -= L_below L_below^T (lower) and
-//      R_below -= L_below X_P, 4x4 register tiles with every LDS read issued before the FMAs.
-// Two barriers per panel; nothing leaves LDS until the end. Only X = L^-1 is needed by the
-// recursion (gptq_core._chol_inv_rec); L is written back only when asked for (L may alias A:
-// every read of A precedes the first barrier, every write of L follows the last).
-// Measured (scripts/probes/chol_tile_prof.py, one 128-tile): PW 16 / 256 threads 70 us, PW 8 /
-// 256 threads 60 us, PW 8 / 1024 threads 51 us (PW 4 / 1024 threads in the n 14336 chain: 84 us
-// against 64 per tile, twice the barriers; profiles/r4_chain_breakdown.txt) -- S1 is VALU-bound
-// in one wave at ~PW^3/6 FMAs
-// per panel, S3 is LDS-latency-bound; what remains is the S1 -> S2 -> S3 chain per panel.
+// Blocked right-looking over 16-column panels on the augmented [A | R], R = I initially
+// (after panel p, R's rows p hold X_p = L_pp^-1 R_p: the rows of X = L^-1, blocked forward
+// substitution of L X = I). The tile is 8 x 8 blocks of 16 x 16, each block kept in LDS in the
+// accumulator layout of v_mfma_f32_16x16x4_f32 (lane l, register j: row 4 (l >> 4) + j,
+// column l & 15; one ds_read_b128 / ds_write_b128 per lane per block, conflict-free):
+//   At(i, j), i >= j: the block A_ij^T (its transpose: see below); after panel j it holds L_ij^T
+//   Rt(i, k), i >= k: R_ik; after panel i, X_ik
+// With both operands' k permuted as k = 4 (l >> 4) + s at MFMA step s, the accumulator layout
+// of M^T is exactly M's A-operand fragment and the accumulator layout of N is N's B-operand
+// fragment, so every product below reads its operands straight from the stored blocks:
+//   S1 (wave 0): factor the 16 x 16 diagonal block -- lane r holds row r of A_pp in registers,
+//      column c's pivot and the L[k][c] it needs are taken by v_readlane (no LDS, no barrier);
+//      the same fmas run the forward substitution of Z = L_pp^-1 in lanes 16 + j (column j)
+//   S2 (all waves, 8 blocks): L_i^T = Z A_ip^T (i > p) and X_pk = Z R_pk (k <= p)
+//   S3: A_ij^T -= L_j L_i^T (p < j <= i), R_ik -= L_i X_pk (i > p, k <= p). Look-ahead: wave 0
+//      updates the next diagonal block first and runs S1 of panel p + 1 while waves 1-3 do the
+//      rest of S3, so the serial factorisation overlaps the trailing update (two barriers per
+//      panel).
+// Rows / columns past n are an identity pad (chol of [A 0; 0 I] is [L 0; 0 I]); only the n x n
+// corner is written. Only X = L^-1 is needed by the recursion (gptq_core._chol_inv_rec); L is
+// written back only when asked for (L may alias A: every read of A precedes the first barrier,
+// every write of L follows the last). fp32 throughout (the fp32 MFMA sums its products exactly
+// like an fmaf chain, in the permuted k order); checked against fp64 (tests/test_gptq_gpu.py).
+// Round 4's kernel (8-column panels, LDS-resident 4 x 4 register tiles, one wave redundantly
+// factoring each 8 x 8 block) took ~64 us per 128-tile in the GPTQ chain.
 #include "lcq_common.h"
 
 namespace lcq {
+namespace ctile {
 
 constexpr int CTILE = 128;
-constexpr int CLD = CTILE + 4;  // LDS row pitch: 16-byte aligned rows (ds_read_b128 of row
-                                // segments); 132 = 4 mod 64 banks, 16 rows per bank sweep
-#ifndef LCQ_CHOL_PW
-#define LCQ_CHOL_PW 8
-#endif
-constexpr int PW = LCQ_CHOL_PW;  // panel width
-#ifndef LCQ_CHOL_NT
-#define LCQ_CHOL_NT 1024
-#endif
-constexpr int NT = LCQ_CHOL_NT;  // threads; > 256 hides the LDS latency of the S3 tiles
-constexpr int VEC_PER_THREAD = CTILE * CTILE / 4 / NT;
+constexpr int TT = 16;                       // MFMA block side
+constexpr int NTL = CTILE / TT;              // 8 block rows / columns
+constexpr int NLOW = NTL * (NTL + 1) / 2;    // 36 lower blocks
+constexpr int TF = TT * TT;                  // floats per block
+constexpr int NT = 256;                      // 4 waves
+constexpr int OFF_A = 0, OFF_R = NLOW * TF, OFF_Z = 2 * NLOW * TF, OFF_L = OFF_Z + TF;
+constexpr int LDS_BYTES = (OFF_L + NTL * TF) * 4;  // 82944 B
 
-#ifdef LCQ_CHOL_PROF  // probe builds only (scripts/probes/chol_tile_prof.py): stage timestamps
-#define PROF_STAMP(k)                                                                 \
-  if (threadIdx.x == 0)                                                               \
-    reinterpret_cast<unsigned long long*>(info)[1 + (k)] = __builtin_amdgcn_s_memtime();
-#else
-#define PROF_STAMP(k)
-#endif
+typedef float v4f __attribute__((ext_vector_type(4)));
 
-// lower-triangle 4x4 tile index t -> (ti, tk), tk <= ti
-__device__ __forceinline__ void tri_tile(int t, int& ti, int& tk) {
-  ti = (int)((__builtin_amdgcn_sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);  // corrected below
-  while (ti * (ti + 1) / 2 > t) --ti;
-  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-  tk = t - ti * (ti + 1) / 2;
+__device__ __forceinline__ int tix(int i, int j) { return i * (i + 1) / 2 + j; }
+
+__device__ __forceinline__ void tri_ij(int t, int& i, int& j) {
+  i = 0;
+  while ((i + 1) * (i + 2) / 2 <= t) ++i;
+  j = t - i * (i + 1) / 2;
 }
 
-// S1: factor a[c0:c0+cw, c0:c0+cw] (lower) in every lane's registers; lane 0 writes L_PP back,
-// lanes < PW write column `lane` of Z = L_PP^-1 to zs[r*PW+lane]. Returns the first bad pivot
-// (1-based within the block) or 0 -- uniform.
-__device__ __forceinline__ int factor_diag(float* a, float* zs, int c0, int cw, int lane) {
-  float l[PW][PW];
+__device__ __forceinline__ float rl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__device__ __forceinline__ v4f ld4(const float* blk, int lane) {
+  return *reinterpret_cast<const v4f*>(blk + 4 * lane);
+}
+__device__ __forceinline__ void st4(float* blk, int lane, v4f v) {
+  *reinterpret_cast<v4f*>(blk + 4 * lane) = v;
+}
+
+// acc += A B over one block's 16 k: `at` = accumulator-layout block of A^T, `b` = of B
+__device__ __forceinline__ v4f mma16(v4f acc, v4f at, v4f b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(at.x, b.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(at.y, b.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(at.z, b.z, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(at.w, b.w, acc, 0, 0, 0);
+  return acc;
+}
+
+// S1 on wave 0: factor the (symmetric) diagonal block At(q, q); L_qq rows -> Ld[q] (row-major,
+// zero above the diagonal), Z = L_qq^-1 -> Zs column-major (Zs[j * 16 + r] = Z[r][j]).
+// Lanes 0-15 hold row r of the block (right-looking: A[r][k] -= L[r][c] L[k][c]), lanes 16-31
+// column j of W = I (forward substitution: W[k][j] -= L[k][c] Z[c][j]); both updates are
+// v[k] -= m * L[k][c] with the lane's own multiplier m = v[c] / L[c][c] (L[r][c], or Z[c][j]),
+// so ONE fma per (c, k) serves the factorisation and the inverse, and the L[k][c] come from
+// v_readlane of the row lanes' m. Non-positive pivots: recorded (first one, 1-based row
+// row0 + 16 q + c + 1), replaced by 1.
+__device__ __forceinline__ void factor_block(float* sm, int q, int lane, int* info, int64_t row0) {
+  const float* blk = sm + OFF_A + tix(q, q) * TF;
+  const int r = lane & 15;
+  const bool rowlane = lane < TT;
+  float v[TT];
 #pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    const float4* row = reinterpret_cast<const float4*>(a + (c0 + i) * CLD + c0);
-#pragma unroll
-    for (int q = 0; q < PW / 4; ++q) {
-      if (4 * q <= i) {
-        const float4 v = row[q];  // broadcast: every lane reads the same address
-        l[i][4 * q] = v.x;
-        l[i][4 * q + 1] = v.y;
-        l[i][4 * q + 2] = v.z;
-        l[i][4 * q + 3] = v.w;
-      }
-    }
-    if (i >= cw) {  // rows past the tile edge: identity, keeps the unrolled code finite
-#pragma unroll
-      for (int k = 0; k < PW; ++k) l[i][k] = (k == i) ? 1.f : 0.f;
-    }
-  }
-  float rinv[PW];
+  for (int c = 0; c < TT; ++c)   // row lanes: element (r, c); column lanes: identity column
+    v[c] = rowlane ? blk[4 * (c + 16 * (r >> 2)) + (r & 3)] : (c == r ? 1.f : 0.f);
   int bad = 0;
 #pragma unroll
-  for (int c = 0; c < PW; ++c) {
-    const float d = l[c][c];
-    const bool nb = !(d > 0.f);
+  for (int c = 0; c < TT; ++c) {
+    const float piv = rl(v[c], c);
+    const bool nb = !(piv > 0.f);
     if (nb && bad == 0) bad = c + 1;
-    const float sq = nb ? 1.f : sqrtf(d);
-    rinv[c] = 1.f / sq;
-    l[c][c] = sq;
+    // hardware v_sqrt / v_rcp (1 ulp): the IEEE-exact sequences are ~30 dependent
+    // instructions per column on the serial path
+    const float sq = nb ? 1.f : __builtin_amdgcn_sqrtf(piv);
+    const float rinv = __builtin_amdgcn_rcpf(sq);
+    const float m = v[c] * rinv;   // row lane r: L[r][c]; column lane j: Z[c][j]
 #pragma unroll
-    for (int i = c + 1; i < PW; ++i) l[i][c] *= rinv[c];
-#pragma unroll
-    for (int i = c + 1; i < PW; ++i)
-#pragma unroll
-      for (int k = c + 1; k <= i; ++k) l[i][k] = fmaf(-l[i][c], l[k][c], l[i][k]);
+    for (int k = c + 1; k < TT; ++k) v[k] = fmaf(-m, rl(m, k), v[k]);
+    v[c] = lane == c ? sq : m;
   }
-  if (lane == 0) {
+  if (lane < 2 * TT) {
+    float* dst = lane < TT ? sm + OFF_L + q * TF + TT * lane : sm + OFF_Z + TT * (lane - TT);
 #pragma unroll
-    for (int i = 0; i < PW; ++i)
-      if (i < cw)
-#pragma unroll
-        for (int k = 0; k <= i; ++k) a[(c0 + i) * CLD + c0 + k] = l[i][k];
+    for (int c = 0; c < TT; c += 4)
+      *reinterpret_cast<v4f*>(dst + c) =
+          rowlane ? v4f{c <= r ? v[c] : 0.f, c + 1 <= r ? v[c + 1] : 0.f,
+                        c + 2 <= r ? v[c + 2] : 0.f, c + 3 <= r ? v[c + 3] : 0.f}
+                  : v4f{v[c], v[c + 1], v[c + 2], v[c + 3]};
   }
-  // Z column `lane`: z[r] = (e_lane[r] - sum_{q<r} L[r][q] z[q]) / L[r][r]
-  float z[PW];
-#pragma unroll
-  for (int r = 0; r < PW; ++r) {
-    float sacc = (lane == r) ? 1.f : 0.f;
-#pragma unroll
-    for (int q = 0; q < r; ++q) sacc = fmaf(-l[r][q], z[q], sacc);
-    z[r] = sacc * rinv[r];
-  }
-  if (lane < PW) {
-#pragma unroll
-    for (int r = 0; r < PW; ++r) zs[r * PW + lane] = (r < cw && lane < cw) ? z[r] : 0.f;
-  }
-  return bad;
+  if (bad && lane == 0 && info) atomicCAS(info, 0, (int)(row0 + TT * q + bad));
 }
 
-// S3 tile: rows i0..i0+3 of L_below (panel columns c0..c0+PW-1) times either rows k0..k0+3 of
-// the panel (LOWER: A22 tile, lower part only) or X_P[:, k0..k0+3] (R tile); all b128
-// reads are issued before any FMA
-template <bool LOWER>
-__device__ __forceinline__ void rank_tile(float* a, float* x, int c0, int i0, int k0, int n) {
-  float4 pi[4][PW / 4], pk[4][PW / 4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int q = 0; q < PW / 4; ++q)
-      pi[u][q] = *reinterpret_cast<const float4*>(a + (i0 + u) * CLD + c0 + 4 * q);
-  if (LOWER) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int q = 0; q < PW / 4; ++q)
-        pk[u][q] = *reinterpret_cast<const float4*>(a + (k0 + u) * CLD + c0 + 4 * q);
+// one block job: dst = (init ? dst : 0) + sign * A B with the operands' blocks as above
+struct Job {
+  float* dst;
+  const float* at;
+  const float* b;
+};
+
+// S3 job list of panel p (trailing blocks from block row q = p + 1, except At(q, q)), job `idx`
+__device__ __forceinline__ Job s3_job(float* sm, int p, int ntl, int idx) {
+  const int q = p + 1, m = ntl - q;
+  const int nA = m * (m + 1) / 2 - 1;
+  Job j;
+  if (idx < nA) {
+    int ii, jj;
+    tri_ij(idx + 1, ii, jj);
+    const int i = q + ii, jc = q + jj;                       // At(i, jc) -= L_jc L_i^T
+    j.dst = sm + OFF_A + tix(i, jc) * TF;
+    j.at = sm + OFF_A + tix(jc, p) * TF;                     // A operand L_jc: block of L_jc^T
+    j.b = sm + OFF_A + tix(i, p) * TF;                       // B operand L_i^T
   } else {
-    // pk[v][q].{x,y,z,w} = X[c0+4q+{0..3}][k0+v], from X rows (k0..k0+3 contiguous)
-#pragma unroll
-    for (int q = 0; q < PW / 4; ++q) {
-      const float4 r0 = *reinterpret_cast<const float4*>(x + (c0 + 4 * q) * CLD + k0);
-      const float4 r1 = *reinterpret_cast<const float4*>(x + (c0 + 4 * q + 1) * CLD + k0);
-      const float4 r2 = *reinterpret_cast<const float4*>(x + (c0 + 4 * q + 2) * CLD + k0);
-      const float4 r3 = *reinterpret_cast<const float4*>(x + (c0 + 4 * q + 3) * CLD + k0);
-      pk[0][q] = make_float4(r0.x, r1.x, r2.x, r3.x);
-      pk[1][q] = make_float4(r0.y, r1.y, r2.y, r3.y);
-      pk[2][q] = make_float4(r0.z, r1.z, r2.z, r3.z);
-      pk[3][q] = make_float4(r0.w, r1.w, r2.w, r3.w);
-    }
+    const int t = idx - nA, i = q + t / (p + 1), k = t % (p + 1);  // Rt(i, k) -= L_i X_pk
+    j.dst = sm + OFF_R + tix(i, k) * TF;
+    j.at = sm + OFF_A + tix(i, p) * TF;
+    j.b = sm + OFF_R + tix(p, k) * TF;
   }
-  float acc[4][4] = {};
-#pragma unroll
-  for (int q = 0; q < PW / 4; ++q)
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        acc[u][v] = fmaf(pi[u][q].x, pk[v][q].x, acc[u][v]);
-        acc[u][v] = fmaf(pi[u][q].y, pk[v][q].y, acc[u][v]);
-        acc[u][v] = fmaf(pi[u][q].z, pk[v][q].z, acc[u][v]);
-        acc[u][v] = fmaf(pi[u][q].w, pk[v][q].w, acc[u][v]);
-      }
-  float* dst = LOWER ? a : x;
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int i = i0 + u, k = k0 + v;
-      if (i < n && (!LOWER || k <= i)) dst[i * CLD + k] -= acc[u][v];
-    }
+  return j;
 }
 
-__global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t lda,
-                                                       int n, float* Lout,
-                                                       int64_t ldl, float* __restrict__ X,
-                                                       int64_t ldx, int* __restrict__ info,
-                                                       int64_t row0, int vec) {
-  __shared__ __attribute__((aligned(16))) float a[CTILE * CLD];
-  __shared__ __attribute__((aligned(16))) float x[CTILE * CLD];
-  __shared__ __attribute__((aligned(16))) float zs[PW * PW];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  PROF_STAMP(0)
-  if (vec) {  // n == 128, lda % 4 == 0, 16-byte aligned: one batch of float4 loads per thread
-    float4 v[VEC_PER_THREAD];
+__global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t lda, int n,
+                                                       float* Lout, int64_t ldl,
+                                                       float* __restrict__ X, int64_t ldx,
+                                                       int* __restrict__ info, int64_t row0,
+                                                       int vec) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g4 = (lane >> 4) * 4;
+  const int ntl = (n + TT - 1) / TT;
+
+  // load: At(i, j) lane l register jj = A_ij^T[g4 + jj][r16] = A[16 i + r16][16 j + g4 + jj]
+  // (the lower triangle only: a diagonal block's upper half from its mirror; identity pad);
+  // Rt = I. 36 blocks = 9 per wave, every load issued before the first LDS store.
+  {
+    v4f v[NLOW / 4];
 #pragma unroll
-    for (int u = 0; u < VEC_PER_THREAD; ++u) {
-      const int e = tid + NT * u, i = e >> 5, j = (e & 31) * 4;
-      v[u] = *reinterpret_cast<const float4*>(A + (int64_t)i * lda + j);
-    }
+    for (int u = 0; u < NLOW / 4; ++u) {
+      int i, j;
+      tri_ij(w + 4 * u, i, j);
+      const int gr = TT * i + r16, gc0 = TT * j + g4;
+      if (vec && i != j) {
+        v[u] = *reinterpret_cast<const v4f*>(A + (int64_t)gr * lda + gc0);
+      } else {
 #pragma unroll
-    for (int u = 0; u < VEC_PER_THREAD; ++u) {
-      const int e = tid + NT * u, i = e >> 5, j = (e & 31) * 4;
-      *reinterpret_cast<float4*>(a + i * CLD + j) = v[u];
-    }
-  } else {
-#pragma unroll
-    for (int it0 = 0; it0 < CTILE * CTILE / NT; it0 += 16) {
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int idx = tid + NT * (it0 + u), i = idx >> 7, j = idx & 127;
-        v[u] = (i < n && j < n) ? A[(int64_t)i * lda + j] : 0.f;
+        for (int jj = 0; jj < 4; ++jj) {
+          const int gc = gc0 + jj;
+          float x;
+          if (gr < n && gc < n)
+            x = gr >= gc ? A[(int64_t)gr * lda + gc] : A[(int64_t)gc * lda + gr];
+          else
+            x = gr == gc ? 1.f : 0.f;
+          v[u][jj] = x;
+        }
       }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int idx = tid + NT * (it0 + u), i = idx >> 7, j = idx & 127;
-        a[i * CLD + j] = v[u];
-      }
     }
-  }
-  for (int idx = tid; idx < CTILE * CTILE; idx += NT) {
-    const int i = idx >> 7, j = idx & 127;
-    x[i * CLD + j] = (i == j) ? 1.f : 0.f;
+#pragma unroll
+    for (int u = 0; u < NLOW / 4; ++u) {
+      int i, j;
+      tri_ij(w + 4 * u, i, j);
+      const int t = w + 4 * u;
+      st4(sm + OFF_A + t * TF, lane, v[u]);
+      v4f e = {0.f, 0.f, 0.f, 0.f};
+      if (i == j) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) e[jj] = g4 + jj == r16 ? 1.f : 0.f;
+      }
+      st4(sm + OFF_R + t * TF, lane, e);
+    }
   }
   __syncthreads();
-  PROF_STAMP(1)
+  if (w == 0) factor_block(sm, 0, lane, info, row0);
+  __syncthreads();
 
-  for (int c0 = 0; c0 < n; c0 += PW) {
-    const int cw = min(PW, n - c0);
-    const int b0 = c0 + PW, m2 = n - b0;
-    if (wave == 0) {
-      const int bad = factor_diag(a, zs, c0, cw, lane);
-      if (bad && lane == 0 && info) atomicCAS(info, 0, (int)(row0 + c0 + bad));
+  for (int p = 0; p < ntl; ++p) {
+    // S2: L_i^T = Z A_ip^T (i = p+1 .. ntl-1) and X_pk = Z R_pk (k = 0 .. p): <= 8 blocks
+    {
+      v4f zt;  // accumulator-layout block of Z^T: Z[r16][g4 + jj]
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) zt[jj] = sm[OFF_Z + (g4 + jj) * TT + r16];
+      const int nL = ntl - 1 - p, njobs = nL + p + 1;
+      for (int t = w; t < njobs; t += 4) {
+        float* blk = t < nL ? sm + OFF_A + tix(p + 1 + t, p) * TF
+                            : sm + OFF_R + tix(p, t - nL) * TF;
+        const v4f b = ld4(blk, lane);
+        const v4f o = mma16(v4f{0.f, 0.f, 0.f, 0.f}, zt, b);
+        st4(blk, lane, o);
+      }
     }
-    PROF_STAMP(2 + 4 * (c0 / PW))
     __syncthreads();
-    if (tid < 128) {
-      // X_P = Z R_P for column j (columns >= c0 + cw of R_P are zero)
-      const int j = tid;
-      if (j < c0 + cw) {
-        float rp[PW], t[PW];
-#pragma unroll
-        for (int q = 0; q < PW; ++q) rp[q] = (q < cw) ? x[(c0 + q) * CLD + j] : 0.f;
-#pragma unroll
-        for (int r = 0; r < PW; ++r) {
-          const float4* z4 = reinterpret_cast<const float4*>(zs + r * PW);
-          float sacc = 0.f;
-#pragma unroll
-          for (int q4 = 0; q4 < PW / 4; ++q4) {
-            const float4 zz = z4[q4];
-            sacc = fmaf(zz.x, rp[4 * q4], sacc);
-            sacc = fmaf(zz.y, rp[4 * q4 + 1], sacc);
-            sacc = fmaf(zz.z, rp[4 * q4 + 2], sacc);
-            sacc = fmaf(zz.w, rp[4 * q4 + 3], sacc);
-          }
-          t[r] = sacc;
-        }
-#pragma unroll
-        for (int r = 0; r < PW; ++r)
-          if (r < cw) x[(c0 + r) * CLD + j] = t[r];
-      }
-    } else if (m2 > 0) {
-      // L_below row i = A row i (panel columns) Z^T
-      const int i = b0 + tid - 128;
-      if (i < n) {
-        float ar[PW];
-#pragma unroll
-        for (int q = 0; q < PW / 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(a + i * CLD + c0 + 4 * q);
-          ar[4 * q] = v.x;
-          ar[4 * q + 1] = v.y;
-          ar[4 * q + 2] = v.z;
-          ar[4 * q + 3] = v.w;
-        }
-#pragma unroll
-        for (int c = 0; c < PW; ++c) {
-          const float4* z4 = reinterpret_cast<const float4*>(zs + c * PW);
-          float sacc = 0.f;
-#pragma unroll
-          for (int q4 = 0; q4 < PW / 4; ++q4) {
-            const float4 zz = z4[q4];
-            sacc = fmaf(zz.x, ar[4 * q4], sacc);
-            sacc = fmaf(zz.y, ar[4 * q4 + 1], sacc);
-            sacc = fmaf(zz.z, ar[4 * q4 + 2], sacc);
-            sacc = fmaf(zz.w, ar[4 * q4 + 3], sacc);
-          }
-          a[i * CLD + c0 + c] = sacc;
+    if (p + 1 < ntl) {
+      if (w == 0) {
+        // look-ahead: the next diagonal block first, then its factorisation
+        const int q = p + 1;
+        float* d = sm + OFF_A + tix(q, q) * TF;
+        const v4f lq = ld4(sm + OFF_A + tix(q, p) * TF, lane);
+        const v4f o = mma16(ld4(d, lane), -lq, lq);
+        st4(d, lane, o);
+        factor_block(sm, q, lane, info, row0);
+      } else {
+        const int q = p + 1, m = ntl - q;
+        const int njobs = m * (m + 1) / 2 - 1 + m * (p + 1);
+        // two blocks per iteration: their LDS reads and MFMA chains interleave
+        for (int idx = w - 1; idx < njobs; idx += 6) {
+          const Job j0 = s3_job(sm, p, ntl, idx);
+          const bool two = idx + 3 < njobs;
+          const Job j1 = two ? s3_job(sm, p, ntl, idx + 3) : j0;
+          const v4f c0 = ld4(j0.dst, lane), a0 = ld4(j0.at, lane), b0 = ld4(j0.b, lane);
+          const v4f c1 = ld4(j1.dst, lane), a1 = ld4(j1.at, lane), b1 = ld4(j1.b, lane);
+          v4f o0 = c0, o1 = c1;
+          const v4f n0 = -a0, n1 = -a1;
+          o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(n0.x, b0.x, o0, 0, 0, 0);
+          o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(n1.x, b1.x, o1, 0, 0, 0);
+          o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(n0.y, b0.y, o0, 0, 0, 0);
+          o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(n1.y, b1.y, o1, 0, 0, 0);
+          o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(n0.z, b0.z, o0, 0, 0, 0);
+          o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(n1.z, b1.z, o1, 0, 0, 0);
+          o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(n0.w, b0.w, o0, 0, 0, 0);
+          o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(n1.w, b1.w, o1, 0, 0, 0);
+          st4(j0.dst, lane, o0);
+          if (two) st4(j1.dst, lane, o1);
         }
       }
     }
-    PROF_STAMP(3 + 4 * (c0 / PW))
-    __syncthreads();
-    PROF_STAMP(4 + 4 * (c0 / PW))
-    if (m2 > 0) {
-      // S3: tiles of A22 (lower) then tiles of R_below (columns < c0 + PW); rows stay < 128
-      const int nt = (m2 + 3) >> 2, T = nt * (nt + 1) / 2, nc = (c0 + PW) >> 2;
-      int t = tid;
-      for (; t < T; t += NT) {
-        int ti, tk;
-        tri_tile(t, ti, tk);
-        rank_tile<true>(a, x, c0, b0 + 4 * ti, b0 + 4 * tk, n);
-      }
-      for (; t < T + nt * nc; t += NT) {
-        const int t2 = t - T;
-        rank_tile<false>(a, x, c0, b0 + 4 * (t2 / nc), 4 * (t2 % nc), n);
-      }
-    }
-    PROF_STAMP(5 + 4 * (c0 / PW))
     __syncthreads();
   }
-  PROF_STAMP(70)
 
-  if (vec) {
+  // X = the final R (lower blocks), zero above the diagonal; L when asked for
+  for (int t = w; t < NTL * NTL; t += 4) {
+    const int i = t >> 3, k = t & 7;
+    if (i >= ntl || k >= ntl) continue;
+    v4f x = {0.f, 0.f, 0.f, 0.f};
+    if (i >= k) x = ld4(sm + OFF_R + tix(i, k) * TF, lane);
+    const int col = TT * k + r16;
 #pragma unroll
-    for (int u = 0; u < VEC_PER_THREAD; ++u) {
-      const int e = tid + NT * u, i = e >> 5, j = (e & 31) * 4;
-      float4 o = *reinterpret_cast<const float4*>(x + i * CLD + j);
-      if (j > i) o.x = 0.f;
-      if (j + 1 > i) o.y = 0.f;
-      if (j + 2 > i) o.z = 0.f;
-      if (j + 3 > i) o.w = 0.f;
-      *reinterpret_cast<float4*>(X + (int64_t)i * ldx + j) = o;
-      if (Lout) {
-        o = *reinterpret_cast<const float4*>(a + i * CLD + j);
-        if (j > i) o.x = 0.f;
-        if (j + 1 > i) o.y = 0.f;
-        if (j + 2 > i) o.z = 0.f;
-        if (j + 3 > i) o.w = 0.f;
-        *reinterpret_cast<float4*>(Lout + (int64_t)i * ldl + j) = o;
-      }
+    for (int jj = 0; jj < 4; ++jj) {
+      const int row = TT * i + g4 + jj;
+      if (row < n && col < n) X[(int64_t)row * ldx + col] = col <= row ? x[jj] : 0.f;
     }
-  } else {
-#pragma unroll 8
-    for (int it = 0; it < CTILE * CTILE / NT; ++it) {
-      const int idx = tid + NT * it, i = idx >> 7, j = idx & 127;
-      if (i < n && j < n) {
-        X[(int64_t)i * ldx + j] = (j <= i) ? x[i * CLD + j] : 0.f;
-        if (Lout) Lout[(int64_t)i * ldl + j] = (j <= i) ? a[i * CLD + j] : 0.f;
+    if (Lout) {
+      // L_ik = (block of L_ik^T)^T: lane l holds L[16 i + r16][16 k + g4 + jj]
+      const int lrow = TT * i + r16, lc0 = TT * k + g4;
+      v4f l4 = {0.f, 0.f, 0.f, 0.f};
+      if (i > k) {
+        l4 = ld4(sm + OFF_A + tix(i, k) * TF, lane);
+      } else if (i == k) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) l4[jj] = sm[OFF_L + i * TF + r16 * TT + g4 + jj];
+      }
+      if (vec) {
+        *reinterpret_cast<v4f*>(Lout + (int64_t)lrow * ldl + lc0) = l4;
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (lrow < n && lc0 + jj < n) Lout[(int64_t)lrow * ldl + lc0 + jj] = l4[jj];
       }
     }
   }
-  PROF_STAMP(71)
 }
 
+}  // namespace ctile
 }  // namespace lcq
 
 using namespace lcq;
 
 extern "C" int lcq_chol_inv_tile(const void* A, int64_t lda, int n, void* L, int64_t ldl,
                                  void* X, int64_t ldx, void* info, int64_t row0, void* stream) {
+  using namespace lcq::ctile;
   LCQ_REQUIRE(n > 0 && n <= CTILE && lda >= n && ldx >= n && (!L || ldl >= n),
               "tile must be 1..128 wide");
   const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  const int vec = n == CTILE && lda % 4 == 0 && ldx % 4 == 0 && al(A) && al(X) &&
-                  (!L || (ldl % 4 == 0 && al(L)));
-  hipLaunchKernelGGL(k_chol_inv_tile, dim3(1), NT, 0, as_stream(stream),
+  const int vec = n == CTILE && lda % 4 == 0 && al(A) && (!L || (ldl % 4 == 0 && al(L)));
+  // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
+  (void)hipFuncSetAttribute((const void*)k_chol_inv_tile,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+  hipLaunchKernelGGL(k_chol_inv_tile, dim3(1), NT, LDS_BYTES, as_stream(stream),
                      reinterpret_cast<const float*>(A), lda, n, reinterpret_cast<float*>(L), ldl,
                      reinterpret_cast<float*>(X), ldx, reinterpret_cast<int*>(info), row0, vec);
   return check_launch("lcq_chol_inv_tile");
@@ -849,10 +805,14 @@ extern "C" int64_t lcq_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K)
   return use_stream_k(M, N, K) ? sk_ws_bytes() : 0;
 }
 
+// plan_m: the row count the kernel variant (tile size, LDS-DMA or register staging) is chosen
+// for -- M itself, or the full product's rows when this launch computes a row range of it
+// (lcq_gemm_f32_rows: the same variant, hence the same per-element k order, on every rank)
 static int gemm_f32_impl(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
                          int64_t lda, const void* B, int64_t ldb, int bt, float beta, void* C,
-                         int64_t ldc, void* ws, int64_t ws_bytes, void* stream) {
-
+                         int64_t ldc, void* ws, int64_t ws_bytes, void* stream,
+                         int64_t plan_m = -1) {
+  if (plan_m < 0) plan_m = M;
   LCQ_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
   if (M == 0 || N == 0) return LCQ_OK;
   LCQ_REQUIRE(A != nullptr && B != nullptr && C != nullptr, "null pointers");
@@ -869,12 +829,13 @@ static int gemm_f32_impl(int64_t M, int64_t N, int64_t K, float alpha, const voi
   if (K == 0) a.alpha = 0.f;  // C = beta C
   hipStream_t st = as_stream(stream);
   // 128^2 tiles where they fill the chip, 64^2 below (4x the workgroups)
-  const int64_t t128 = ((N + 127) / 128) * ((M + 127) / 128);
+  const int64_t t128 = ((N + 127) / 128) * ((plan_m + 127) / 128);
   const bool big = t128 >= 256;
   // LDS-DMA kernel: K % 32 == 0, 16-byte aligned rows, 32-bit byte offsets
-  const bool dma = K % f32g::DKC == 0 && a.vec && al(C) &&
-                   M * lda < ((int64_t)1 << 29) && (bt ? N * ldb : K * ldb) < ((int64_t)1 << 29);
-  if (dma && ws != nullptr && ws_bytes >= sk_ws_bytes() && use_stream_k(M, N, K)) {
+  const bool dma = K % f32g::DKC == 0 && a.vec && al(C) && plan_m * lda < ((int64_t)1 << 29) &&
+                   (bt ? N * ldb : K * ldb) < ((int64_t)1 << 29);
+  if (dma && ws != nullptr && ws_bytes >= sk_ws_bytes() && plan_m == M &&
+      use_stream_k(M, N, K)) {
     f32g::SkArgs sk{};
     sk.ntn = (N + 127) / 128;
     sk.tiles = sk.ntn * ((M + 127) / 128);
@@ -960,6 +921,26 @@ extern "C" int lcq_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha, const 
                             int64_t lda, const void* B, int64_t ldb, int bt, float beta, void* C,
                             int64_t ldc, void* stream) {
   return gemm_f32_impl(M, N, K, alpha, A, lda, B, ldb, bt, beta, C, ldc, nullptr, 0, stream);
+}
+
+extern "C" int64_t lcq_gemm_f32_row_unit(int64_t M, int64_t N) {
+  return ((N + 127) / 128) * ((M + 127) / 128) >= 256 ? 128 : 64;
+}
+
+extern "C" int lcq_gemm_f32_rows(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
+                                 int64_t lda, const void* B, int64_t ldb, int bt, float beta,
+                                 void* C, int64_t ldc, int64_t row0, int64_t row1,
+                                 void* stream) {
+  const int64_t unit = lcq_gemm_f32_row_unit(M, N);
+  LCQ_REQUIRE(0 <= row0 && row0 <= row1 && row1 <= M, "row range outside [0, M]");
+  LCQ_REQUIRE(row0 % unit == 0 && (row1 % unit == 0 || row1 == M),
+              "row range must be cut on the plan's tile rows (lcq_gemm_f32_row_unit)");
+  if (row1 == row0) return LCQ_OK;
+  LCQ_REQUIRE(A != nullptr && C != nullptr, "null pointers");
+  const float* Ar = reinterpret_cast<const float*>(A) + row0 * lda;
+  float* Cr = reinterpret_cast<float*>(C) + row0 * ldc;
+  return gemm_f32_impl(row1 - row0, N, K, alpha, Ar, lda, B, ldb, bt, beta, Cr, ldc, nullptr, 0,
+                       stream, M);
 }
 
 extern "C" int lcq_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha, const void* A,

@@ -246,7 +246,11 @@ class GPTQ(BaseBlockwiseQuantization):
                 # reduces after every sample); averaging matches its H /= world_size
                 dist.all_reduce(H, op=dist.ReduceOp.SUM)
                 H /= ws
-            cache[nout] = gptq_core.prepare_hessian(H, self.actorder, self.percdamp, nout)
+            # every rank now holds the same H: the factorisation's large products are
+            # row-split over the ranks (bit-identical to one GPU; gptq_core.chain_sharding)
+            rank = dist.get_rank() if replicate else 0
+            with gptq_core.chain_sharding(rank, ws if replicate else 1):
+                cache[nout] = gptq_core.prepare_hessian(H, self.actorder, self.percdamp, nout)
         acc.prepared = cache[nout]
         return acc.prepared
 

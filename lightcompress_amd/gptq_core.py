@@ -5,6 +5,7 @@ Kept separate from the plugin class (``gptq.py``) so the algorithm can be driven
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -202,9 +203,52 @@ def prepare_hessian(H: torch.Tensor, actorder: bool, percdamp: float, owq_nout: 
     return U, perm, dead
 
 
+# Products with at least SHARD_MIN_ROWS output rows (at n 14336: the ~20 of ~600 launches that
+# carry ~60 % of the chain's flops) run on the tiled kernel planned for their full shape
+# (lcq_gemm_f32_rows; never stream-K -- measured equal at n 14336, 39.09 vs 39.51 ms) in every
+# world, so that a token-sharded run (chain_sharding) can row-split them over its ranks and
+# all-gather the row blocks in rank order with every element computed exactly as on one GPU.
+SHARD_MIN_ROWS = 3584
+_chain_shard = None          # (rank, world) while a sharded chain runs
+shard_stats = {'split_products': 0, 'gathered_rows': 0}   # per process, for tests / probes
+
+
+@contextlib.contextmanager
+def chain_sharding(rank: int, world: int):
+    """Row-split the large products of every factorisation run inside this context over the
+    `world` ranks of the default process group (each rank must hold the same Hessian: token
+    shards after the Hessian's fixed-tree finish, or replicas). The sharded chain runs eagerly
+    (an all-gather sits inside it) and without the side-stream overlap (one collective order
+    on every rank); results are bit-identical to the unsharded chain."""
+    global _chain_shard
+    prev = _chain_shard
+    _chain_shard = (rank, world) if world > 1 else None
+    try:
+        yield
+    finally:
+        _chain_shard = prev
+
+
 def _gemm(A, B, out, alpha, beta, b_trans=False):
     """out = beta out + alpha A op(B): the recursion's products (lcq_gemm_f32)."""
-    return ops.gemm_f32(A, B, out, alpha, beta, b_trans=b_trans)
+    M = out.shape[0]
+    if M < SHARD_MIN_ROWS or not out.is_cuda:
+        return ops.gemm_f32(A, B, out, alpha, beta, b_trans=b_trans)
+    sh = _chain_shard
+    if sh is None:
+        return ops.gemm_f32_rows(A, B, out, alpha, beta, b_trans, 0, M)
+    from . import parallel as P
+    rank, world = sh
+    unit = ops.gemm_f32_row_unit(M, out.shape[1])
+    ranges = [tuple(min(u * unit, M) for u in P.row_shard(-(-M // unit), r, world))
+              for r in range(world)]
+    r0, r1 = ranges[rank]
+    ops.gemm_f32_rows(A, B, out, alpha, beta, b_trans, r0, r1)
+    full = P.gather_ranges(out[r0:r1], ranges)   # rank order: rows 0 .. M
+    out.copy_(full)
+    shard_stats['split_products'] += 1
+    shard_stats['gathered_rows'] += M - (r1 - r0)
+    return out
 
 
 _TILE = 128
@@ -305,7 +349,7 @@ def _chol_inv_rec(A: torch.Tensor, X: torch.Tensor, info: torch.Tensor, row0: in
     L21 = torch.empty_like(A21)
     _mm_lowT(A21, X11, L21, 1.0, 0.0)
     T = torch.empty_like(A21)
-    if n >= _OVERLAP_MIN and A.is_cuda:
+    if n >= _OVERLAP_MIN and A.is_cuda and _chain_shard is None:
         main = torch.cuda.current_stream(A.device)
         side = _side_stream(A.device, depth)
         side.wait_stream(main)  # L21, X11 ready
@@ -360,7 +404,8 @@ def release_device_state():
 
 def _inverse_cholesky_upper_filled(fill, n: int, device) -> torch.Tensor:
     """U = J chol(Hr)^-1 J where fill(buf) writes Hr = J H J (n x n fp32) into buf."""
-    graphed = torch.device(device).type == 'cuda' and n >= _GRAPH_MIN and CHAIN_GRAPHS
+    graphed = (torch.device(device).type == 'cuda' and n >= _GRAPH_MIN and CHAIN_GRAPHS
+               and _chain_shard is None)
     key = (torch.device(device).index, n)
     ent = _chain_graphs.get(key) if graphed else None
     if ent is None:

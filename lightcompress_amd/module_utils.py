@@ -198,6 +198,26 @@ class OriginFloatLinear(nn.Module):
         return m
 
 
+_SHELL_PROTO = nn.Module()
+_SHELL_PLAIN = {k: v for k, v in _SHELL_PROTO.__dict__.items() if not isinstance(v, (dict, set))}
+_SHELL_CONT = [(k, v) for k, v in _SHELL_PROTO.__dict__.items() if isinstance(v, (dict, set))]
+
+
+def _module_shell(cls, buffers: dict, attrs: dict):
+    """An instance of nn.Module subclass `cls` with exactly the state its __init__ +
+    register_buffer calls would give (fresh hook / child containers, `buffers` registered
+    persistent, `attrs` as plain attributes), built without nn.Module.__setattr__'s per-call
+    bookkeeping: a deploy builds hundreds of these per MoE block (new_batch)."""
+    m = object.__new__(cls)
+    d = m.__dict__
+    d.update(_SHELL_PLAIN)
+    for k, v in _SHELL_CONT:
+        d[k] = v.copy()
+    d['_buffers'].update(buffers)
+    d.update(attrs)
+    return m
+
+
 class VllmRealQuantLinear(nn.Module):
     """module_utils.py:855-955 — vLLM compressed-tensors int layout."""
 
@@ -233,11 +253,40 @@ class VllmRealQuantLinear(nn.Module):
 
     @classmethod
     @torch.no_grad()
+    def new_batch(cls, modules, w_q, quant_config, prequant=None):
+        """new() for every module of a list (a block's linears), the same modules and buffers:
+        codes / scales from `prequant` (one batched requant launch pair per block,
+        BaseBlockwiseQuantization._prequant_fp8_block) where given, quant_pack otherwise; the
+        module objects built as shells (_module_shell) -- for a DeepSeek-V3 MoE block the
+        per-linear Python of new() (nn.Module construction, register_buffer and __setattr__
+        bookkeeping) cost ~10x the deploy kernels."""
+        need_pack = quant_config['weight'].get('need_pack', False)
+        scales_name = ('weight_scale_inv' if quant_config['weight']['granularity'] == 'per_block'
+                       else 'weight_scale')
+        wname = 'weight_packed' if need_pack else 'weight'
+        out = []
+        for i, module in enumerate(modules):
+            pre = prequant[i] if prequant is not None else None
+            weight, scales = pre if pre is not None else cls.quant_pack(module, w_q, quant_config)
+            b = module.__dict__['_parameters'].get('bias', module.__dict__['_buffers'].get('bias'))
+            bufs = {wname: weight}
+            attrs = {}
+            if b is not None:
+                bufs['bias'] = b.data
+            else:
+                attrs['bias'] = None
+            bufs[scales_name] = scales
+            bufs['input_scale'] = module.__dict__['_buffers'].get('buf_act_scales_0')
+            attrs.update(in_features=module.in_features, out_features=module.out_features,
+                         weight_shape=weight.shape, weight_dtype=weight.dtype,
+                         scales_shape=scales.shape, scales_dtype=scales.dtype,
+                         zeros_shape=None, zeros_dtype=None)
+            out.append(_module_shell(cls, bufs, attrs))
+        return out
+
+    @classmethod
+    @torch.no_grad()
     def quant_pack(cls, module, w_q, quant_config):
-        pre = getattr(module, '_lcq_prequant', None)
-        if pre is not None:  # batched by BaseBlockwiseQuantization._prequant_fp8_block
-            del module._lcq_prequant
-            return pre
         wq = getattr(w_q, 'keywords', {}).get('wquantizer')
         if (module.weight.data.dtype == torch.float8_e4m3fn and wq is not None
                 and hasattr(wq, 'real_quant_weight_from_block_fp8')

@@ -326,6 +326,29 @@ def gemm_f32(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, alpha: float =
 STREAM_K = True   # gemm_f32's stream-K grids (tests compare them with the tiled kernel)
 
 
+def gemm_f32_row_unit(m: int, n: int) -> int:
+    """Row granularity of a gemm_f32_rows range of an m x n product (its plan's tile rows)."""
+    return int(N.load().lcq_gemm_f32_row_unit(m, n))
+
+
+def gemm_f32_rows(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, alpha: float,
+                  beta: float, b_trans: bool, row0: int, row1: int) -> torch.Tensor:
+    """Rows [row0, row1) of gemm_f32(A, B, out, alpha, beta, b_trans) -- A and out the full
+    operands -- computed with the kernel the full product is planned for (never stream-K):
+    every element gets the same k order on any rank (lcq_gemm_f32_rows)."""
+    M, K = A.shape
+    n_ = out.shape[1]
+    ok = B.shape == ((n_, K) if b_trans else (K, n_))
+    if not ok or out.shape[0] != M:
+        raise ValueError('gemm_f32_rows: shape mismatch')
+    if any(t.dtype != torch.float32 for t in (A, B, out)):
+        raise ValueError('gemm_f32_rows: fp32 operands')
+    N.call('lcq_gemm_f32_rows', M, n_, K, float(alpha), A.data_ptr(), _ld(A), B.data_ptr(),
+           _ld(B), int(b_trans), float(beta), out.data_ptr(), _ld(out), int(row0), int(row1),
+           N.stream_of(A))
+    return out
+
+
 def chol_inv_tile(A: torch.Tensor, info: torch.Tensor, row0: int = 0,
                   L: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """Returns L^-1 for the lower Cholesky factor L of A (<= 128 x 128 fp32 view, unit column
@@ -1045,7 +1068,10 @@ def fp8_block_to_tensor_many(codes: list, scales_inv: list, block: int = 128,
         M, Nn = codes[i].shape
         rec += [N.ptr(codes[i]), N.ptr(sinv[i]), N.ptr(outs[i]), M, Nn]
     # every class's descriptors (and the class order, to put the scales back) in ONE upload
-    upload = torch.tensor(rec + flat, dtype=torch.int64).to(dev)
+    # pinned + non_blocking: a pageable upload would hold the host until the stream drains
+    # (the deploy's host work would stop running ahead of its kernels)
+    upload = torch.tensor(rec + flat, dtype=torch.int64, pin_memory=True).to(dev,
+                                                                              non_blocking=True)
     descs = upload[:5 * n]
     # the kernel writes scale p for weight flat[p]: unless the class order is the input order,
     # the scales land in a temporary and are scattered back to input order

@@ -204,19 +204,19 @@ class Ownership:
         if mode != 'shard_units':
             raise ValueError(f'no ownership plan for parallel mode {mode}')
         from .parallel import lpt_shard
-        units, costs = [], []
+        # LPT within each block (a block's units are published together, so the block's
+        # slowest rank sets its publish time: per-block balance, not only global balance), the
+        # ranks rotated by block index so that the per-block leftovers spread over the ranks
+        owner = {}
         for bi, block in enumerate(blocks):
             per = {}
             for n, m in model_adapter.get_block_linears(block).items():
                 w = getattr(m, 'weight', None)
                 per[unit_key(n)] = per.get(unit_key(n), 0) + (w.numel() if w is not None else 0)
-            for k, c in per.items():
-                units.append((bi, k))
-                costs.append(float(c))
-        owner = {}
-        for r, idx in enumerate(lpt_shard(costs, world)):
-            for j in idx:
-                owner[units[j]] = r
+            keys = list(per)
+            for r, idx in enumerate(lpt_shard([float(per[k]) for k in keys], world)):
+                for j in idx:
+                    owner[(bi, keys[j])] = (r + bi) % world
         return cls(mode, rank, world, unit_owner=owner)
 
     def block_of(self, i: int) -> int | None:

@@ -356,6 +356,30 @@ def test_inverse_cholesky_graph_replay(dev, monkeypatch):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize('M,N,K,bt', [(3584, 1792, 1792, 1), (4096, 128, 128, 0),
+                                       (1000, 384, 256, 1)])
+def test_gemm_f32_rows_match_full_plan(dev, M, N, K, bt):
+    """lcq_gemm_f32_rows: row ranges cut on lcq_gemm_f32_row_unit, assembled, equal the
+    whole-range call bit for bit (the same kernel plan per element), and the whole range equals
+    the tiled lcq_gemm_f32 product to fp32 accuracy."""
+    from lightcompress_amd import ops
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    A = torch.randn(M, K, generator=g, device=dev)
+    B = torch.randn((N, K) if bt else (K, N), generator=g, device=dev)
+    C0 = torch.randn(M, N, generator=g, device=dev)
+    full = ops.gemm_f32_rows(A, B, C0.clone(), 0.5, 1.0, bool(bt), 0, M)
+    unit = ops.gemm_f32_row_unit(M, N)
+    parts = C0.clone()
+    cuts = list(range(0, M, 3 * unit)) + [M]
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        ops.gemm_f32_rows(A, B, parts, 0.5, 1.0, bool(bt), r0, r1)
+    assert torch.equal(parts, full)
+    ref = C0.double() + 0.5 * (A.double() @ (B.double().T if bt else B.double()))
+    assert ((full.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+    with pytest.raises(Exception):
+        ops.gemm_f32_rows(A, B, parts, 0.5, 1.0, bool(bt), unit // 2, M)
+
+
 def test_inverse_cholesky_not_pd(dev):
     from lightcompress_amd import gptq_core
     H = torch.eye(256, device=dev)

@@ -67,10 +67,23 @@ GPTQ_TOK_FLOAT = {'quant': {'method': 'GPTQ',
 
 
 def _run(cfg_dict, layers):
+    from lightcompress_amd import gptq_core
+    model, calib = _model_and_calib(layers, cfg_dict.get('entries', (4,)))
+    old_min = gptq_core.SHARD_MIN_ROWS
+    if 'chain_shard_min' in cfg_dict:   # the tiny Hessians (256, 512) take the split path too
+        gptq_core.SHARD_MIN_ROWS = cfg_dict['chain_shard_min']
+    try:
+        return _run_algo(cfg_dict, model, calib)
+    finally:
+        gptq_core.SHARD_MIN_ROWS = old_min
+
+
+def _run_algo(cfg_dict, model, calib):
+    from lightcompress_amd import gptq_core
     from lightcompress_amd.pipeline import build_algo
     from lightcompress_amd.utils import load_config
-    model, calib = _model_and_calib(layers, cfg_dict.get('entries', (4,)))
-    cfg_dict = {k: v for k, v in cfg_dict.items() if k != 'entries'}
+    split0 = gptq_core.shard_stats['split_products']
+    cfg_dict = {k: v for k, v in cfg_dict.items() if k not in ('entries', 'chain_shard_min')}
     algo = build_algo(model, load_config(cfg_dict), calib)
     algo.run_block_loop()
     if cfg_dict.get('deploy'):
@@ -86,6 +99,8 @@ def _run(cfg_dict, layers):
     out.update({f'{i}.{n}.{bn}': t.detach().float().cpu()   # static act qparams
                 for i, b in enumerate(model.blocks) for n, m in model.get_block_linears(b).items()
                 for bn, t in m.named_buffers() if bn.startswith('buf_act_')})
+    out['_stats.split_products'] = torch.tensor(
+        [gptq_core.shard_stats['split_products'] - split0])
     return out
 
 
@@ -130,6 +145,8 @@ def test_two_ranks_match_single(dev, name, cfg, layers, tmp_path):
     multi = _two_ranks(cfg, layers, tmp_path)
     assert single.keys() == multi.keys()
     for k in single:
+        if k.startswith('_stats.'):
+            continue
         assert single[k].dtype == multi[k].dtype, k
         assert torch.equal(single[k], multi[k]), k
 
@@ -147,20 +164,27 @@ def _codes_vs_single(cfg, tmp_path):
     return eq, rel
 
 
-@pytest.mark.parametrize('name,cfg', [('float_inputs', GPTQ_TOK_FLOAT), ('quant_out', GPTQ_TOK)])
+@pytest.mark.parametrize('name,cfg', [('float_inputs', GPTQ_TOK_FLOAT), ('quant_out', GPTQ_TOK),
+                                      ('quant_out_split_chain', dict(GPTQ_TOK, chain_shard_min=128))])
 def test_gptq_token_shards_bit_identical(dev, name, cfg, tmp_path):
     """Each rank forwards its half of the calibration samples (cut on the grouped Hessian's
     group boundaries); every Hessian is the same fixed tree of 8 group partials
     (gptq_core.HessianAccumulator), finished across the ranks, so H -- hence U, the row-sharded
     column loop and every deployed weight -- equals one GPU's bit for bit, with float inputs
-    and under quant_out + true_sequential (gptq_w_only.yml) alike."""
+    and under quant_out + true_sequential (gptq_w_only.yml) alike. With chain_shard_min the
+    factorisation's products of >= 128 rows are row-split over the two ranks
+    (gptq_core.chain_sharding): still bit for bit."""
     for k in ('RANK', 'WORLD_SIZE'):
         os.environ.pop(k, None)
     single = _run(cfg, 2)
     multi = _two_ranks(cfg, 2, tmp_path)
     assert single.keys() == multi.keys()
+    assert int(single['_stats.split_products']) == 0
+    if 'chain_shard_min' in cfg:
+        assert int(multi['_stats.split_products']) > 0   # the launch list shows the split
     for k in single:
-        assert torch.equal(single[k], multi[k]), k
+        if not k.startswith('_stats.'):
+            assert torch.equal(single[k], multi[k]), k
 
 
 def _static_act(entries, algo):
@@ -187,4 +211,114 @@ def test_static_act_qparams_token_shards_bit_identical(dev, entries, algo, tmp_p
     multi = _two_ranks(cfg, 2, tmp_path)
     assert single.keys() == multi.keys()
     for k in single:
-        assert torch.equal(single[k], multi[k]), k
+        if not k.startswith('_stats.'):
+            assert torch.equal(single[k], multi[k]), k
+
+
+def _chain_worker(rank, world, port, n, path):
+    from lightcompress_amd import gptq_core
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK='0')
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        gptq_core.SHARD_MIN_ROWS = 256
+        H = torch.load(path + '.H', weights_only=True).to('cuda:0')
+        with gptq_core.chain_sharding(rank, world):
+            U = gptq_core.inverse_cholesky_upper(H)
+        torch.save({'U': U.cpu(), 'split': gptq_core.shard_stats['split_products']},
+                   f'{path}.{rank}')
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chain_row_split_bit_identical(dev, tmp_path):
+    """gptq_core.chain_sharding at n 1536: every product of >= 256 output rows is computed
+    by each rank for its rows only (lcq_gemm_f32_rows, the full shape's kernel plan) and
+    all-gathered in rank order; U equals the one-process chain (same products, unsplit) bit for
+    bit on both ranks."""
+    from lightcompress_amd import gptq_core
+    n = 1536
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(n, 2 * n, generator=g)
+    H = X @ X.T / (2 * n)
+    H.diagonal().add_(0.05)
+    path = str(tmp_path / 'chain')
+    torch.save(H, path + '.H')
+    old = gptq_core.SHARD_MIN_ROWS
+    try:
+        gptq_core.SHARD_MIN_ROWS = 256
+        single = gptq_core.inverse_cholesky_upper(H.to(dev)).cpu()
+    finally:
+        gptq_core.SHARD_MIN_ROWS = old
+    ctx = mp.get_context('spawn')
+    port = _port()
+    procs = [ctx.Process(target=_chain_worker, args=(r, 2, port, n, path)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    for r in range(2):
+        res = torch.load(f'{path}.{r}', weights_only=True)
+        assert res['split'] > 0
+        assert torch.equal(res['U'], single), r
+
+
+def _owned_awq_run(materialize):
+    from transformers import LlamaConfig
+
+    from lightcompress_amd.llama import Llama
+    from lightcompress_amd.pipeline import build_algo
+    from lightcompress_amd.utils import load_config
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                      num_key_value_heads=2, num_hidden_layers=4, vocab_size=128,
+                      max_position_embeddings=512, rms_norm_eps=1e-5)
+    conf = load_config(dict(AWQ, model={'type': 'Llama', 'materialize': materialize}))
+    model = Llama(conf, hf_config=cfg, random_init={'seed': 3, 'std': 0.02}, device='cuda:0')
+    g = torch.Generator(device='cuda:0').manual_seed(9)
+    x = torch.randn(4, 64, 256, generator=g, device='cuda:0').to(torch.bfloat16)
+    algo = build_algo(model, conf, {'data': [x], 'kwargs': [model.rotary_kwargs(64)]})
+    algo.run_block_loop()
+    algo.deploy('vllm_quant')
+    return {f'{i}.{n}': t.detach().cpu() for i, b in enumerate(model.get_blocks())
+            for n, t in [*b.named_parameters(), *b.named_buffers()] if not t.is_meta}
+
+
+def _owned_awq_worker(rank, world, port, path):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK='0')
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        torch.save(_owned_awq_run('owned'), f'{path}.{rank}')
+    finally:
+        dist.destroy_process_group()
+
+
+def test_awq_shard_blocks_owned_matches_single(dev, tmp_path):
+    """bench.py --gpus N's AWQ leg: shard_blocks with materialize: owned (a synthetic
+    random_init model whose tensors are seeded by name) -- each rank allocates, transforms and
+    vLLM-packs only its own blocks (ring hand-off of the activations, no weight gather); every
+    tensor a rank holds equals the one-process run's, and the ranks together hold every block."""
+    for k in ('RANK', 'WORLD_SIZE'):
+        os.environ.pop(k, None)
+    single = _owned_awq_run('all')
+    ctx = mp.get_context('spawn')
+    port = _port()
+    path = str(tmp_path / 'owned')
+    procs = [ctx.Process(target=_owned_awq_worker, args=(r, 2, port, path)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    held = set()
+    for r in range(2):
+        res = torch.load(f'{path}.{r}', weights_only=True)
+        blocks = {int(k.split('.')[0]) for k in res}
+        assert blocks == {i for i in range(4) if i % 2 == r}, (r, blocks)
+        for k, v in res.items():
+            assert v.dtype == single[k].dtype and torch.equal(v, single[k]), k
+        held |= set(res)
+    assert held == set(single)

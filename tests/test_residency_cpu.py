@@ -73,14 +73,19 @@ def test_unit_plan_covers_each_linear_once():
         loads = [0] * world
         for bi, block in enumerate(model.get_blocks()):
             lins = model.get_block_linears(block)
+            bload, unit = [0] * world, {}
             for n, m in lins.items():
                 owners = [r for r in range(world) if plans[r].owns(bi, n)]
                 assert len(owners) == 1, (bi, n)
                 loads[owners[0]] += m.weight.numel()
+                bload[owners[0]] += m.weight.numel()
+                unit[unit_key(n)] = unit.get(unit_key(n), 0) + m.weight.numel()
                 if '.experts.' in n and not n.startswith('mlp.shared'):
                     e = n.rsplit('.', 1)[0]
                     assert all(plans[0].owner_of(bi, f'{e}.{p}') == owners[0]
                                for p in ('gate_proj', 'up_proj', 'down_proj'))
+            # per block (its units are published together): balanced to within one unit
+            assert max(bload) - min(bload) <= max(unit.values()), (world, bi, bload)
         biggest = max(m.weight.numel() * (3 if '.experts.' in n else 1)
                       for b in model.get_blocks() for n, m in model.get_block_linears(b).items())
         assert max(loads) - min(loads) <= biggest
