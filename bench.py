@@ -541,7 +541,7 @@ def bench_gptq(args, rank, world, dev):
                            'avg_launch_ms': round(h['avg_ms'], 4),
                            'flops_per_launch': h['flops'] / h['launches']}
     algo.release()   # block_opt driven directly: the chain graphs go with the algorithm
-    del algo, model, hidden, calib
+    del algo, model, hidden, calib, blocks
     free_device()
     return out
 
@@ -558,6 +558,7 @@ def bench_e2e(args, rank, world, dev, which, residency='device'):
     from lightcompress_amd.pipeline import build_algo
     cfg = LlamaConfig(**LLAMA3_8B)
     nb = args.e2e_blocks
+    free_device()   # whatever an earlier leg left to the cyclic collector goes first
     model = Llama.random(cfg, num_layers=nb, device=dev, seed=3000 if which == 'awq' else 4000,
                          residency=residency)
     torch.cuda.empty_cache()
@@ -655,7 +656,7 @@ def bench_l70b(args, rank, world, dev):
         if which == 'awq':
             out[which]['roofline'] = gemm_roofline(kern, el)
         algo.release()
-        del algo, model, hidden, calib
+        del algo, model, hidden, calib, blocks
         free_device()
     out['workload'] = ('Llama-3-70B decoder block (8192 / 28672, 64q/8kv): AWQ w4a16 g128 '
                        '(configs[1] recipe) and GPTQ w4a16 g128 act-order (configs[2] recipe); '

@@ -38,6 +38,16 @@ def install_linear_forward(model: nn.Module):
             m.forward = types.MethodType(_linear_forward, m)
 
 
+def retire_module(m: nn.Module):
+    """A module just replaced in the model: drop the instance-level forward that
+    install_linear_forward bound to it (module -> bound method -> module is a reference cycle,
+    which would keep the replaced linear -- and its device weight -- alive until the next cyclic
+    garbage collection: a whole model's float weights through a deploy)."""
+    f = m.__dict__.get('forward')
+    if isinstance(f, types.MethodType) and f.__self__ is m:
+        del m.__dict__['forward']
+
+
 def _torch_dtype(name, default=torch.bfloat16):
     """The YAML's model.torch_dtype ('auto', 'bfloat16', 'torch.float16', ...)."""
     if name in (None, 'auto'):
@@ -441,6 +451,7 @@ class BaseModel:
                     parent._modules[child] = new   # what nn.Module.__setattr__ does here
                 else:
                     setattr(parent, child, new)
+                retire_module(old)
             return
         for name, m in subset['layers'].items():
             if not isinstance(m, _LINEAR_TYPES) or getattr(m, 'no_quant', False):
@@ -451,6 +462,7 @@ class BaseModel:
             parent_name, _, child = name.rpartition('.')
             parent = block.get_submodule(parent_name) if parent_name else block
             setattr(parent, child, new)
+            retire_module(m)
 
     def replace_module_block(self, module, block, block_idx, params_dict, prequant=None):
         self.replace_module_subset(module, block, {'layers': self.get_block_linears(block)},

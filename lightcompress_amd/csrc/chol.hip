@@ -40,11 +40,27 @@ constexpr int NLOW = NTL * (NTL + 1) / 2;    // 36 lower blocks
 constexpr int TF = TT * TT;                  // floats per block
 constexpr int NT = 256;                      // 4 waves
 constexpr int OFF_A = 0, OFF_R = NLOW * TF, OFF_Z = 2 * NLOW * TF, OFF_L = OFF_Z + TF;
-constexpr int LDS_BYTES = (OFF_L + NTL * TF) * 4;  // 82944 B
+constexpr int OFF_SCR = OFF_L + NTL * TF;            // one scratch block (padding jobs)
+constexpr int OFF_Z2 = OFF_SCR + TF;                 // Z of odd panels (Zs double-buffered)
+constexpr int OFF_SYNC = OFF_Z2 + TF;                // per panel: S2 arrivals of waves 1-3,
+                                                     // and wave 0's "L_{p+1} written" flag
+constexpr int LDS_BYTES = (OFF_SYNC + 2 * NTL) * 4;  // 85056 B
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int tix(int i, int j) { return i * (i + 1) / 2 + j; }
+#ifdef LCQ_CHOL_PROF  // probe builds only (scripts/probes/chol_tile_prof2.py): s_memtime stamps
+#define PROF_STAMP(k, who)                                                              \
+  if (w == (who) && lane == 0)                                                          \
+    reinterpret_cast<unsigned long long*>(info)[1 + (k)] = __builtin_amdgcn_s_memtime();
+#define PROF_REAL(k)                                                                     \
+  if (w == 0 && lane == 0)                                                              \
+    reinterpret_cast<unsigned long long*>(info)[1 + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define PROF_STAMP(k, who)
+#define PROF_REAL(k)
+#endif
+
+__host__ __device__ constexpr int tix(int i, int j) { return i * (i + 1) / 2 + j; }
 
 __device__ __forceinline__ void tri_ij(int t, int& i, int& j) {
   i = 0;
@@ -72,13 +88,20 @@ __device__ __forceinline__ v4f mma16(v4f acc, v4f at, v4f b) {
   return acc;
 }
 
+#ifndef LCQ_PROBE_CHOL_FAST_RSQ
+#define LCQ_PROBE_CHOL_FAST_RSQ 0   // probe builds: hardware v_sqrt / v_rcp in S1
+#endif
+
 // S1 on wave 0: factor the (symmetric) diagonal block At(q, q); L_qq rows -> Ld[q] (row-major,
-// zero above the diagonal), Z = L_qq^-1 -> Zs column-major (Zs[j * 16 + r] = Z[r][j]).
+// zero above the diagonal), Z = L_qq^-1 -> Zs column-major (Zs[j * 16 + r] = Z[r][j]; Zs of
+// panel q at OFF_Z (q even) or OFF_Z2 (q odd): S1 of panel q + 1 runs while the other waves
+// still read panel q's).
 // Lanes 0-15 hold row r of the block (right-looking: A[r][k] -= L[r][c] L[k][c]), lanes 16-31
 // column j of W = I (forward substitution: W[k][j] -= L[k][c] Z[c][j]); both updates are
 // v[k] -= m * L[k][c] with the lane's own multiplier m = v[c] / L[c][c] (L[r][c], or Z[c][j]),
 // so ONE fma per (c, k) serves the factorisation and the inverse, and the L[k][c] come from
-// v_readlane of the row lanes' m. Non-positive pivots: recorded (first one, 1-based row
+// v_readlane of the row lanes' m. sqrt and the reciprocal are IEEE (LAPACK's spotf2: ajj =
+// sqrt(ajj), column scaled by 1 / ajj). Non-positive pivots: recorded (first one, 1-based row
 // row0 + 16 q + c + 1), replaced by 1.
 __device__ __forceinline__ void factor_block(float* sm, int q, int lane, int* info, int64_t row0) {
   const float* blk = sm + OFF_A + tix(q, q) * TF;
@@ -94,17 +117,21 @@ __device__ __forceinline__ void factor_block(float* sm, int q, int lane, int* in
     const float piv = rl(v[c], c);
     const bool nb = !(piv > 0.f);
     if (nb && bad == 0) bad = c + 1;
-    // hardware v_sqrt / v_rcp (1 ulp): the IEEE-exact sequences are ~30 dependent
-    // instructions per column on the serial path
+#if LCQ_PROBE_CHOL_FAST_RSQ   // probe builds only: hardware v_sqrt / v_rcp (1 ulp)
     const float sq = nb ? 1.f : __builtin_amdgcn_sqrtf(piv);
     const float rinv = __builtin_amdgcn_rcpf(sq);
+#else
+    const float sq = nb ? 1.f : sqrtf(piv);
+    const float rinv = 1.f / sq;
+#endif
     const float m = v[c] * rinv;   // row lane r: L[r][c]; column lane j: Z[c][j]
 #pragma unroll
     for (int k = c + 1; k < TT; ++k) v[k] = fmaf(-m, rl(m, k), v[k]);
     v[c] = lane == c ? sq : m;
   }
   if (lane < 2 * TT) {
-    float* dst = lane < TT ? sm + OFF_L + q * TF + TT * lane : sm + OFF_Z + TT * (lane - TT);
+    float* dst = lane < TT ? sm + OFF_L + q * TF + TT * lane
+                           : sm + ((q & 1) ? OFF_Z2 : OFF_Z) + TT * (lane - TT);
 #pragma unroll
     for (int c = 0; c < TT; c += 4)
       *reinterpret_cast<v4f*>(dst + c) =
@@ -115,33 +142,72 @@ __device__ __forceinline__ void factor_block(float* sm, int q, int lane, int* in
   if (bad && lane == 0 && info) atomicCAS(info, 0, (int)(row0 + TT * q + bad));
 }
 
-// one block job: dst = (init ? dst : 0) + sign * A B with the operands' blocks as above
+// Trailing-update jobs: dst -= A B, the product summed first (from 0, in the MFMA k order) and
+// subtracted once (BLAS's C - A B^T of the reference's blocked factorisation), four jobs per
+// call so that their LDS reads and MFMA chains overlap. A job whose dst is the scratch block
+// (Tail) is a no-op padding the last group.
 struct Job {
   float* dst;
   const float* at;
   const float* b;
 };
 
-// S3 job list of panel p (trailing blocks from block row q = p + 1, except At(q, q)), job `idx`
-__device__ __forceinline__ Job s3_job(float* sm, int p, int ntl, int idx) {
-  const int q = p + 1, m = ntl - q;
-  const int nA = m * (m + 1) / 2 - 1;
-  Job j;
-  if (idx < nA) {
-    int ii, jj;
-    tri_ij(idx + 1, ii, jj);
-    const int i = q + ii, jc = q + jj;                       // At(i, jc) -= L_jc L_i^T
-    j.dst = sm + OFF_A + tix(i, jc) * TF;
-    j.at = sm + OFF_A + tix(jc, p) * TF;                     // A operand L_jc: block of L_jc^T
-    j.b = sm + OFF_A + tix(i, p) * TF;                       // B operand L_i^T
-  } else {
-    const int t = idx - nA, i = q + t / (p + 1), k = t % (p + 1);  // Rt(i, k) -= L_i X_pk
-    j.dst = sm + OFF_R + tix(i, k) * TF;
-    j.at = sm + OFF_A + tix(i, p) * TF;
-    j.b = sm + OFF_R + tix(p, k) * TF;
+__device__ __forceinline__ void run4(const Job& j0, const Job& j1, const Job& j2, const Job& j3,
+                                     int lane) {
+  const Job* j[4] = {&j0, &j1, &j2, &j3};
+  v4f c[4], a[4], b[4], o[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    c[u] = ld4(j[u]->dst, lane);
+    a[u] = ld4(j[u]->at, lane);
+    b[u] = ld4(j[u]->b, lane);
+    o[u] = v4f{0.f, 0.f, 0.f, 0.f};
   }
-  return j;
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      o[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][s], b[u][s], o[u], 0, 0, 0);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) st4(j[u]->dst, lane, c[u] - o[u]);
 }
+
+// lower 16-block (i, j) of the load phase's block t = w + 4 u (row-major over the triangle)
+__device__ constexpr int kTi[NLOW] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5,
+                                      5, 5, 5, 6, 6, 6, 6, 6, 6, 6, 7, 7, 7, 7, 7, 7, 7, 7};
+
+// S3 job lists of a full 128-tile (ntl 8), panel p, wave 1 + w3: job n of the panel's list
+// (blocks A_{i,jc}, q <= jc <= i but (q, q), then R_{i,k}, k <= p, row by row) goes to
+// wave 1 + n % 3. Entries are LDS float offsets (dst, A-operand block, B-operand block).
+struct JobTab {
+  uint16_t d[NTL - 1][3][12], a[NTL - 1][3][12], b[NTL - 1][3][12];
+  uint8_t cnt[NTL - 1][3];
+};
+
+constexpr JobTab make_jobs() {
+  JobTab t{};
+  for (int p = 0; p < NTL - 1; ++p) {
+    const int q = p + 1;
+    int jn = 0;
+    for (int i = q; i < NTL; ++i) {
+      for (int jc = q; jc <= i; ++jc) {
+        if (jc == q && i == q) continue;
+        const int w3 = jn++ % 3, u = t.cnt[p][w3]++;
+        t.d[p][w3][u] = (uint16_t)(OFF_A + tix(i, jc) * TF);
+        t.a[p][w3][u] = (uint16_t)(OFF_A + tix(jc, p) * TF);
+        t.b[p][w3][u] = (uint16_t)(OFF_A + tix(i, p) * TF);
+      }
+      for (int k = 0; k <= p; ++k) {
+        const int w3 = jn++ % 3, u = t.cnt[p][w3]++;
+        t.d[p][w3][u] = (uint16_t)(OFF_R + tix(i, k) * TF);
+        t.a[p][w3][u] = (uint16_t)(OFF_A + tix(i, p) * TF);
+        t.b[p][w3][u] = (uint16_t)(OFF_R + tix(p, k) * TF);
+      }
+    }
+  }
+  return t;
+}
+__device__ constexpr JobTab kJobs = make_jobs();
 
 __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t lda, int n,
                                                        float* Lout, int64_t ldl,
@@ -153,118 +219,205 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g4 = (lane >> 4) * 4;
   const int ntl = (n + TT - 1) / TT;
+  float* const scratch = sm + OFF_SCR;
+  PROF_STAMP(0, 0)
+  PROF_REAL(42)
 
   // load: At(i, j) lane l register jj = A_ij^T[g4 + jj][r16] = A[16 i + r16][16 j + g4 + jj]
-  // (the lower triangle only: a diagonal block's upper half from its mirror; identity pad);
-  // Rt = I. 36 blocks = 9 per wave, every load issued before the first LDS store.
-  {
-    v4f v[NLOW / 4];
+  // (one float4 per lane and block when the tile is a full, aligned 128^2; the lower triangle
+  // only: a diagonal block's upper half is then taken from its mirror in LDS by the same wave;
+  // identity pad past n); Rt = I. Wave 0 loads block (0, 0) and factors it (S1 of panel 0)
+  // while waves 1-3 load the other 35 blocks (12 each, every load issued before the stores).
+  auto load_blk = [&](int t) {
+    const int i = kTi[t], j = t - i * (i + 1) / 2;
+    const int gr = TT * i + r16, gc0 = TT * j + g4;
+    v4f v;
+    if (vec) {
+      v = *reinterpret_cast<const v4f*>(A + (int64_t)gr * lda + gc0);
+    } else {
 #pragma unroll
-    for (int u = 0; u < NLOW / 4; ++u) {
-      int i, j;
-      tri_ij(w + 4 * u, i, j);
-      const int gr = TT * i + r16, gc0 = TT * j + g4;
-      if (vec && i != j) {
-        v[u] = *reinterpret_cast<const v4f*>(A + (int64_t)gr * lda + gc0);
-      } else {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int gc = gc0 + jj;
-          float x;
-          if (gr < n && gc < n)
-            x = gr >= gc ? A[(int64_t)gr * lda + gc] : A[(int64_t)gc * lda + gr];
-          else
-            x = gr == gc ? 1.f : 0.f;
-          v[u][jj] = x;
-        }
+      for (int jj = 0; jj < 4; ++jj) {
+        const int gc = gc0 + jj;
+        v[jj] = gr < n && gc < n && gc <= gr ? A[(int64_t)gr * lda + gc] : (gr == gc ? 1.f : 0.f);
       }
     }
+    return v;
+  };
+  auto store_blk = [&](int t, v4f v) {
+    const int i = kTi[t], j = t - i * (i + 1) / 2;
+    float* blk = sm + OFF_A + t * TF;
+    st4(blk, lane, v);
+    v4f e = {0.f, 0.f, 0.f, 0.f};
+    if (i == j) {
 #pragma unroll
-    for (int u = 0; u < NLOW / 4; ++u) {
-      int i, j;
-      tri_ij(w + 4 * u, i, j);
-      const int t = w + 4 * u;
-      st4(sm + OFF_A + t * TF, lane, v[u]);
-      v4f e = {0.f, 0.f, 0.f, 0.f};
-      if (i == j) {
+      for (int jj = 0; jj < 4; ++jj) e[jj] = g4 + jj == r16 ? 1.f : 0.f;
+      // diagonal block: element (a, b) = A_ii[b][a] with a = g4 + jj > b = r16 lies above the
+      // diagonal (not read); take its mirror A_ii[a][b] = element (b, a), stored at lane
+      // a + 16 (b >> 2), register b & 3 (this wave's own store: LDS is in order per wave)
+      v4f x = ld4(blk, lane);
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) e[jj] = g4 + jj == r16 ? 1.f : 0.f;
+      for (int jj = 0; jj < 4; ++jj) {
+        const int a = g4 + jj;
+        if (a > r16) x[jj] = blk[4 * (a + 16 * (r16 >> 2)) + (r16 & 3)];
       }
-      st4(sm + OFF_R + t * TF, lane, e);
+      st4(blk, lane, x);
+    }
+    st4(sm + OFF_R + t * TF, lane, e);
+  };
+  if (w == 0) {
+    store_blk(0, load_blk(0));
+    if (lane < 2 * NTL) reinterpret_cast<int*>(sm + OFF_SYNC)[lane] = 0;
+    PROF_STAMP(1, 0)
+    factor_block(sm, 0, lane, info, row0);
+    PROF_STAMP(2, 0)
+  } else {
+    constexpr int PER = (NLOW - 1 + 2) / 3;   // 12
+    v4f v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int t = 1 + (w - 1) + 3 * u;
+      if (t < NLOW) v[u] = load_blk(t);
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int t = 1 + (w - 1) + 3 * u;
+      if (t < NLOW) store_blk(t, v[u]);
     }
   }
   __syncthreads();
-  if (w == 0) factor_block(sm, 0, lane, info, row0);
-  __syncthreads();
 
-  for (int p = 0; p < ntl; ++p) {
-    // S2: L_i^T = Z A_ip^T (i = p+1 .. ntl-1) and X_pk = Z R_pk (k = 0 .. p): <= 8 blocks
-    {
-      v4f zt;  // accumulator-layout block of Z^T: Z[r16][g4 + jj]
+  // X block row p is final once S2 of panel p wrote it: its writer stores it to global memory
+  // right away (row 16 p + r16, columns 16 k + g4 .. + 3 per lane: one float4, read back from
+  // the accumulator layout -- element (r, c) at lane c + 16 (r >> 2), register r & 3 -- its own
+  // LDS writes, in order), so the output overlaps the later panels; the zero blocks above the
+  // diagonal are written by the waves with spare S2 slots.
+  const bool xvec = vec && (ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  auto store_x = [&](int i, int k, const float* blk) {
+    const int row = TT * i + r16, c0 = TT * k + g4;
+    v4f x = {0.f, 0.f, 0.f, 0.f};
+    if (blk != nullptr) {
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) zt[jj] = sm[OFF_Z + (g4 + jj) * TT + r16];
-      const int nL = ntl - 1 - p, njobs = nL + p + 1;
-      for (int t = w; t < njobs; t += 4) {
+      for (int jj = 0; jj < 4; ++jj) {
+        const float e = blk[4 * (g4 + jj + 16 * (r16 >> 2)) + (r16 & 3)];
+        x[jj] = i > k || g4 + jj <= r16 ? e : 0.f;
+      }
+    }
+    if (xvec) {
+      *reinterpret_cast<v4f*>(X + (int64_t)row * ldx + c0) = x;
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        if (row < n && c0 + jj < n) X[(int64_t)row * ldx + c0 + jj] = x[jj];
+    }
+  };
+
+  // Panel p. S2 (<= 8 blocks): L_i^T = Z A_ip^T (i = p+1 .. ntl-1) and X_pk = Z R_pk
+  // (k = 0 .. p). Wave 0 takes the first (L_{p+1}), updates the next diagonal block with it
+  // (A_{p+1,p+1} -= L_{p+1} L_{p+1}^T: it needs no other wave's result), flags L_{p+1} and runs
+  // S1 of panel p + 1 at once; waves 1-3 take the other S2 blocks, meet in an LDS counter (the
+  // blocks they wrote, and wave 0's flag), then run S3 of panel p. One workgroup barrier per
+  // panel: the S1 chain on wave 0 overlaps both S2 and S3 of the other waves.
+  int* const arrive = reinterpret_cast<int*>(sm + OFF_SYNC);
+  int* const lflag = arrive + NTL;
+  for (int p = 0; p < ntl; ++p) {
+    PROF_STAMP(30 + p, 0)
+    const int nL = ntl - 1 - p, njobs = nL + p + 1;
+    v4f zt;  // accumulator-layout block of Z^T: Z[r16][g4 + jj]
+    {
+      const float* zs = sm + ((p & 1) ? OFF_Z2 : OFF_Z);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) zt[jj] = zs[(g4 + jj) * TT + r16];
+    }
+    if (w == 0) {
+      float* blk = nL > 0 ? sm + OFF_A + tix(p + 1, p) * TF : sm + OFF_R + tix(p, 0) * TF;
+      const v4f o = mma16(v4f{0.f, 0.f, 0.f, 0.f}, zt, ld4(blk, lane));
+      st4(blk, lane, o);
+      if (nL == 0) store_x(p, 0, blk);
+      if (nL > 0) {
+        float* d = sm + OFF_A + tix(p + 1, p + 1) * TF;
+        st4(d, lane, ld4(d, lane) - mma16(v4f{0.f, 0.f, 0.f, 0.f}, o, o));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(lflag + p, 1, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+        PROF_STAMP(3 + 4 * p, 0)
+        factor_block(sm, p + 1, lane, info, row0);   // look-ahead: S1 of the next panel
+        PROF_STAMP(5 + 4 * p, 0)
+      }
+    } else {
+      for (int t = w; t < njobs; t += 3) {
         float* blk = t < nL ? sm + OFF_A + tix(p + 1 + t, p) * TF
                             : sm + OFF_R + tix(p, t - nL) * TF;
-        const v4f b = ld4(blk, lane);
-        const v4f o = mma16(v4f{0.f, 0.f, 0.f, 0.f}, zt, b);
-        st4(blk, lane, o);
+        st4(blk, lane, mma16(v4f{0.f, 0.f, 0.f, 0.f}, zt, ld4(blk, lane)));
+        if (t >= nL) store_x(p, t - nL, blk);
       }
-    }
-    __syncthreads();
-    if (p + 1 < ntl) {
-      if (w == 0) {
-        // look-ahead: the next diagonal block first, then its factorisation
+      for (int k = p + w; k < ntl; k += 3)   // X_pk = 0 above the diagonal (k = p+1 ..)
+        if (k > p) store_x(p, k, nullptr);
+      if (nL > 0) {
+        // waves 1-3 meet: every S2 block written (LDS requests of a wave complete in order,
+        // so a block is visible once its writer's arrival is), and L_{p+1} from wave 0
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(arrive + p, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(arrive + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 3 ||
+               __hip_atomic_load(lflag + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+          __builtin_amdgcn_s_sleep(1);
+        PROF_STAMP(4 + 4 * p, 1)
+        // S3 of panel p: A_{i,j} (q <= j <= i, but the diagonal block q done by wave 0) then
+        // R_{i,k} (i >= q, k <= p), job n to wave 1 + n % 3, four at a time
         const int q = p + 1;
-        float* d = sm + OFF_A + tix(q, q) * TF;
-        const v4f lq = ld4(sm + OFF_A + tix(q, p) * TF, lane);
-        const v4f o = mma16(ld4(d, lane), -lq, lq);
-        st4(d, lane, o);
-        factor_block(sm, q, lane, info, row0);
-      } else {
-        const int q = p + 1, m = ntl - q;
-        const int njobs = m * (m + 1) / 2 - 1 + m * (p + 1);
-        // two blocks per iteration: their LDS reads and MFMA chains interleave
-        for (int idx = w - 1; idx < njobs; idx += 6) {
-          const Job j0 = s3_job(sm, p, ntl, idx);
-          const bool two = idx + 3 < njobs;
-          const Job j1 = two ? s3_job(sm, p, ntl, idx + 3) : j0;
-          const v4f c0 = ld4(j0.dst, lane), a0 = ld4(j0.at, lane), b0 = ld4(j0.b, lane);
-          const v4f c1 = ld4(j1.dst, lane), a1 = ld4(j1.at, lane), b1 = ld4(j1.b, lane);
-          v4f o0 = c0, o1 = c1;
-          const v4f n0 = -a0, n1 = -a1;
-          o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(n0.x, b0.x, o0, 0, 0, 0);
-          o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(n1.x, b1.x, o1, 0, 0, 0);
-          o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(n0.y, b0.y, o0, 0, 0, 0);
-          o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(n1.y, b1.y, o1, 0, 0, 0);
-          o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(n0.z, b0.z, o0, 0, 0, 0);
-          o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(n1.z, b1.z, o1, 0, 0, 0);
-          o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(n0.w, b0.w, o0, 0, 0, 0);
-          o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(n1.w, b1.w, o1, 0, 0, 0);
-          st4(j0.dst, lane, o0);
-          if (two) st4(j1.dst, lane, o1);
+        const Job pad = {scratch, scratch, scratch};
+        if (ntl == NTL) {   // the full tile: the precomputed job list
+          const int w3 = w - 1, cnt = kJobs.cnt[p][w3];
+          const uint16_t* td = kJobs.d[p][w3];
+          const uint16_t* ta = kJobs.a[p][w3];
+          const uint16_t* tb = kJobs.b[p][w3];
+          auto job = [&](int u) {
+            return u < cnt ? Job{sm + td[u], sm + ta[u], sm + tb[u]} : pad;
+          };
+          for (int u = 0; u < cnt; u += 4) run4(job(u), job(u + 1), job(u + 2), job(u + 3), lane);
+        } else {
+          Job j0 = pad, j1 = pad, j2 = pad, j3 = pad;   // a shift register (no indexed array)
+          int cnt = 0, jn = 0;
+          auto push = [&](const Job& jb) {
+            j3 = j2;
+            j2 = j1;
+            j1 = j0;
+            j0 = jb;
+            if (++cnt == 4) {
+              run4(j0, j1, j2, j3, lane);
+              cnt = 0;
+            }
+          };
+          for (int i = q; i < ntl; ++i) {
+            const float* li = sm + OFF_A + tix(i, p) * TF;           // L_i^T
+            for (int jc = q; jc <= i; ++jc) {
+              if (jc == q && i == q) continue;
+              if (jn++ % 3 != w - 1) continue;
+              // At(i, jc) = A_{i,jc}^T -= L_jc L_i^T: A operand L_jc (block L_jc^T), B L_i^T
+              push(Job{sm + OFF_A + tix(i, jc) * TF, sm + OFF_A + tix(jc, p) * TF, li});
+            }
+            for (int k = 0; k <= p; ++k) {
+              if (jn++ % 3 != w - 1) continue;
+              // Rt(i, k) -= L_i X_pk: A operand L_i (block L_i^T), B operand X_pk
+              push(Job{sm + OFF_R + tix(i, k) * TF, li, sm + OFF_R + tix(p, k) * TF});
+            }
+          }
+          while (cnt) push(pad);   // the remainder, padded with no-op jobs
         }
+        PROF_STAMP(6 + 4 * p, 1)
       }
     }
     __syncthreads();
   }
+  PROF_STAMP(40, 0)
 
-  // X = the final R (lower blocks), zero above the diagonal; L when asked for
-  for (int t = w; t < NTL * NTL; t += 4) {
-    const int i = t >> 3, k = t & 7;
-    if (i >= ntl || k >= ntl) continue;
-    v4f x = {0.f, 0.f, 0.f, 0.f};
-    if (i >= k) x = ld4(sm + OFF_R + tix(i, k) * TF, lane);
-    const int col = TT * k + r16;
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int row = TT * i + g4 + jj;
-      if (row < n && col < n) X[(int64_t)row * ldx + col] = col <= row ? x[jj] : 0.f;
-    }
-    if (Lout) {
+  // L when asked for (X went out panel by panel)
+  if (Lout) {
+    for (int t = w; t < NTL * NTL; t += 4) {
+      const int i = t >> 3, k = t & 7;
+      if (i >= ntl || k >= ntl) continue;
+      const int row = TT * i + r16, c0 = TT * k + g4;
       // L_ik = (block of L_ik^T)^T: lane l holds L[16 i + r16][16 k + g4 + jj]
-      const int lrow = TT * i + r16, lc0 = TT * k + g4;
       v4f l4 = {0.f, 0.f, 0.f, 0.f};
       if (i > k) {
         l4 = ld4(sm + OFF_A + tix(i, k) * TF, lane);
@@ -273,14 +426,16 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
         for (int jj = 0; jj < 4; ++jj) l4[jj] = sm[OFF_L + i * TF + r16 * TT + g4 + jj];
       }
       if (vec) {
-        *reinterpret_cast<v4f*>(Lout + (int64_t)lrow * ldl + lc0) = l4;
+        *reinterpret_cast<v4f*>(Lout + (int64_t)row * ldl + c0) = l4;
       } else {
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
-          if (lrow < n && lc0 + jj < n) Lout[(int64_t)lrow * ldl + lc0 + jj] = l4[jj];
+          if (row < n && c0 + jj < n) Lout[(int64_t)row * ldl + c0 + jj] = l4[jj];
       }
     }
   }
+  PROF_STAMP(41, 0)
+  PROF_REAL(43)
 }
 
 }  // namespace ctile

@@ -232,7 +232,7 @@ def chain_sharding(rank: int, world: int):
 def _gemm(A, B, out, alpha, beta, b_trans=False):
     """out = beta out + alpha A op(B): the recursion's products (lcq_gemm_f32)."""
     M = out.shape[0]
-    if M < SHARD_MIN_ROWS or not out.is_cuda:
+    if M < SHARD_MIN_ROWS:
         return ops.gemm_f32(A, B, out, alpha, beta, b_trans=b_trans)
     sh = _chain_shard
     if sh is None:

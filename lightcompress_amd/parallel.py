@@ -258,7 +258,11 @@ def publish(block: torch.nn.Module, assign: dict, rest_owner: int | None = None,
                 setattr(m, k, local_attrs[k])
             parent_name, _, child = n.rpartition('.')
             parent = block.get_submodule(parent_name) if parent_name else block
+            old = parent._modules.get(child)
             setattr(parent, child, m)
+            if old is not None:
+                from .base_model import retire_module
+                retire_module(old)
         for mn, kind, tn, shape, dt in (rst or []):
             mod = block.get_submodule(mn) if mn else block
             t = getattr(mod, kind).get(tn)
