@@ -24,11 +24,12 @@
 //               partials in tile order (deterministic) and writes sum / numel to a device slot
 //               (calculate_loss without materialising `out`)
 //
-// Structure (k_gemm16b): one 256-thread workgroup (4 waves, 2 x 2) per 256x256 output tile,
-// each wave 128x128 = 8x8 accumulators of mfma_f32_16x16x32 in AGPRs. K-tile 64; A and B tiles
-// staged by buffer-descriptor LDS-DMA (raw_ptr_buffer_load_lds) into two 64 KB LDS buffers,
-// 4 barriers per K-tile with counted `s_waitcnt vmcnt` (never vmcnt(0) in the loop), B fragments
-// double-buffered in registers. The MFMA runs swapped (B fragment as the A operand), so each
+// Structure (k_gemm16h, the product; k_gemm16b is its round-4 predecessor, kept as a probe
+// build): one 256-thread workgroup (4 waves, 2 x 2) per 256x256 output tile, each wave
+// 128x128 = 8x8 accumulators of mfma_f32_16x16x32 in AGPRs. K-tile 64; A and B tiles staged by
+// buffer-descriptor LDS-DMA (raw_ptr_buffer_load_lds) into two 64 KB LDS buffers; k_gemm16h
+// double-buffers the fragments by k half and needs 3 barriers and one counted vmcnt per K-tile
+// (k_gemm16b: 4 barriers, B fragments double-buffered across K-tiles). The MFMA runs swapped (B fragment as the A operand), so each
 // lane's accumulator holds 4 consecutive output columns of one token row: 8 / 16-byte stores in
 // the epilogues. Tile order is XCD-aware: consecutive work ids go to one XCD and a chunk of
 // 32 = a 4 (M) x 8 (N) block of tiles shares 12 operand panels in L2.
@@ -299,18 +300,20 @@ __device__ __forceinline__ uint4 pair16(uint2 a, uint2 b) {
   return make_uint4(rx[0], ry[0], rx[1], ry[1]);
 }
 
-// Epilogue of the 4-wave 16x16x32 kernels (swapped layout, see k_gemm16).
-template <int DT, int EPI>
-__device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, int tn, int w,
+// Epilogue of the 16x16x32 kernels (swapped layout): NB = 16-column blocks per wave (8 in the
+// 4-wave kernels: wave columns of 128; 4 was the 8-wave ping-pong probe's 64, round 5).
+template <int DT, int EPI, int NB>
+__device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][NB], int tm, int tn, int w,
                                       int wr, int wc, int lane, int tid, char* lds) {
   // epilogue (swapped 16x16 layout): acc[m][n][j] = token tm*256 + wr*128 + m*16 + fr, tile
-  // column wc*128 + n*16 + fq*4 + j (EPI_SILU: n < 4 gate, n + 4 up of output column
-  // tn*128 + wc*64 + n*16 + fq*4 + j). Segment, bias and row pointers are resolved once per
+  // column wc*NB*16 + n*16 + fq*4 + j (EPI_SILU: n < NB/2 gate, n + NB/2 up of output column
+  // tn*128 + wc*NB*8 + n*16 + fq*4 + j). Segment, bias and row pointers are resolved once per
   // tile / row (a tile never straddles a segment), loads are batched per row.
+  constexpr int NH = NB / 2;
   const int fr = lane & 15, fq = lane >> 4;
   const int poff = (fq & 1) * 16 + (fq >> 1) * 8;  // pair16 column offset of this lane
   if constexpr (EPI == EPI_SILU) {
-    const int64_t col0 = (int64_t)tn * 128 + wc * 64 + fq * 4;
+    const int64_t col0 = (int64_t)tn * 128 + wc * (NB * 8) + fq * 4;
     const bool wide = a.wide && (int64_t)tn * 128 + 128 <= a.n;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -318,14 +321,14 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
       if (trow >= a.m) break;
       uint16_t* crow = a.c[0] + trow * a.ldc[0] + col0;
       if (wide) {  // partner lanes (lane ^ 16) share the row: same branch
-        uint2 wv[4];
+        uint2 wv[NH];
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
+        for (int n = 0; n < NH; ++n) {
           float o[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const float gg = rnd<DT>(acc[m][n][j]);
-            const float u = rnd<DT>(acc[m][n + 4][j]);
+            const float u = rnd<DT>(acc[m][n + NH][j]);
             const float sl = rnd<DT>(gg / (1.0f + expf(-gg)));
             o[j] = rnd<DT>(sl * u);
           }
@@ -334,18 +337,18 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
         }
         uint16_t* cpair = crow - fq * 4 + poff;
 #pragma unroll
-        for (int n = 0; n < 4; n += 2)
+        for (int n = 0; n < NH; n += 2)
           *reinterpret_cast<uint4*>(cpair + n * 16) = pair16(wv[n], wv[n + 1]);
         continue;
       }
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
+      for (int n = 0; n < NH; ++n) {
         if (col0 + n * 16 >= a.n) break;
         float o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float gg = rnd<DT>(acc[m][n][j]);
-          const float u = rnd<DT>(acc[m][n + 4][j]);
+          const float u = rnd<DT>(acc[m][n + NH][j]);
           const float sl = rnd<DT>(gg / (1.0f + expf(-gg)));
           o[j] = rnd<DT>(sl * u);
         }
@@ -361,15 +364,15 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
     int64_t base = 0;
     if (a.nseg > 1 && tcol >= a.bend[0]) { s = 1; base = a.bend[0]; }
     if (a.nseg > 2 && tcol >= a.bend[1]) { s = 2; base = a.bend[1]; }
-    const int64_t col0 = tcol + wc * 128 + fq * 4;  // + n * 16
+    const int64_t col0 = tcol + wc * (NB * 16) + fq * 4;  // + n * 16
     const int64_t lcol0 = col0 - base;              // column within segment s
     const bool full_n = tcol + ST <= a.n;
     // bias (uniform presence): 4 values per n, read once
-    float bias[8][4];
+    float bias[NB][4];
     const uint16_t* bp = a.bias[s];
     if (bp != nullptr) {
 #pragma unroll
-      for (int n = 0; n < 8; ++n) {
+      for (int n = 0; n < NB; ++n) {
         if (full_n || col0 + n * 16 < a.n) {
           float b4[4];
           unpack4<DT>(*reinterpret_cast<const uint2*>(bp + lcol0 + n * 16), b4);
@@ -383,12 +386,12 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
     }
     double dsum = 0.0;
     // EPI_SQDIFF: the reference rows are loaded one row block ahead (16 loads in flight)
-    uint2 rv[2][8];
-    auto load_ref = [&](int m, uint2 (&dst)[8]) {
+    uint2 rv[2][NB];
+    auto load_ref = [&](int m, uint2 (&dst)[NB]) {
       const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
       const uint16_t* rrow = a.ref + (trow < a.m ? trow : a.m - 1) * a.ldr + col0;
 #pragma unroll
-      for (int n = 0; n < 8; ++n)
+      for (int n = 0; n < NB; ++n)
         dst[n] = (full_n || col0 + n * 16 < a.n) ? *reinterpret_cast<const uint2*>(rrow + n * 16)
                                                  : make_uint2(0u, 0u);
     };
@@ -400,15 +403,15 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
         if (m + 1 < 8) load_ref(m + 1, rv[(m + 1) & 1]);
       }
       if (trow >= a.m) continue;
-      float o[8][4];
+      float o[NB][4];
 #pragma unroll
-      for (int n = 0; n < 8; ++n)
+      for (int n = 0; n < NB; ++n)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           o[n][j] = rnd<DT>(bp != nullptr ? __fadd_rn(acc[m][n][j], bias[n][j]) : acc[m][n][j]);
       if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-        for (int n = 0; n < 8; ++n) {
+        for (int n = 0; n < NB; ++n) {
           float r[4];
           unpack4<DT>(rv[m & 1][n], r);
 #pragma unroll
@@ -420,7 +423,7 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
         if (a.wide && full_n) {
           uint16_t* cpair = crow - fq * 4 + poff;
 #pragma unroll
-          for (int n = 0; n < 8; n += 2) {
+          for (int n = 0; n < NB; n += 2) {
             uint2 w0, w1;
             w0.x = pack2<DT>(o[n][0], o[n][1]);
             w0.y = pack2<DT>(o[n][2], o[n][3]);
@@ -431,7 +434,7 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
           continue;
         }
 #pragma unroll
-        for (int n = 0; n < 8; ++n) {
+        for (int n = 0; n < NB; ++n) {
           if (!full_n && col0 + n * 16 >= a.n) break;
           uint2 wv;
           wv.x = pack2<DT>(o[n][0], o[n][1]);
@@ -440,7 +443,7 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
         }
       } else {
 #pragma unroll
-        for (int n = 0; n < 8; ++n) {
+        for (int n = 0; n < NB; ++n) {
           if (!full_n && col0 + n * 16 >= a.n) break;
           float r[4];
           unpack4<DT>(rv[m & 1][n], r);
@@ -459,7 +462,10 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][8], int tm, i
       double* red = reinterpret_cast<double*>(lds);
       if (lane == 0) red[w] = dsum;
       __syncthreads();
-      if (tid < 4) a.part[((int64_t)tm * a.n_nt + tn) * 4 + tid] = red[tid];
+      // 4 partials per tile (an 8-wave NB = 4 layout folds waves q and q + 4: the same 64
+      // columns, rows 0-127 and 128-255)
+      if (tid < 4)
+        a.part[((int64_t)tm * a.n_nt + tn) * 4 + tid] = NB == 8 ? red[tid] : red[tid] + red[tid + 4];
     }
   }
 }
@@ -520,7 +526,129 @@ __global__ void __launch_bounds__(256, 1) k_gemm16b(Args a) {
                :
                : "memory");
 
-  epi16<DT, EPI>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
+  epi16<DT, EPI, 8>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
+}
+
+// ---------------------------------------------------------------------------------------
+// k_gemm16h: k_gemm16b's tile, waves, LDS image and staging with a three-barrier K-tile:
+// the fragments are double-buffered by k half instead (set X0 = k 0-31 of the A and B
+// fragments, X1 = k 32-63; 128 VGPRs), so every fragment read of a K-tile overlaps the other
+// half's 64 MFMAs and the loop needs one vmcnt wait per K-tile:
+//   MFMA  0-63  (X0): read X1.A of K-tile t | barrier 1 | DMA A of t+2, read X1.B | barrier 2 |
+//                     DMA A, DMA B of t+2
+//   MFMA 64-127 (X1): DMA B of t+2 | vmcnt(13) + barrier 3 (K-tile t+1 landed) |
+//                     read X0 of K-tile t+1, DMA B of t+2
+// K-tile t+2 goes into K-tile t's buffer: its A region after barrier 1 (every wave has read
+// t's A halves), its B region after barrier 2. Each accumulator sees k 0-31 then 32-63 per
+// K-tile, as in k_gemm16b: identical outputs.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void load_a(const Stage4& st, char* buf, int kofs, int w, int j) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(st.ra, (lds_void_t*)(buf + (w + 4 * j) * 1024), 16,
+                                           st.aoff[j], kofs, 0, 0);
+}
+
+__device__ __forceinline__ void load_b(const Stage4& st, char* buf, int kofs, int w, int j) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(((st.bsel >> j) & 1) ? st.rb[1] : st.rb[0],
+                                           (lds_void_t*)(buf + TILE_B + (w + 4 * j) * 1024), 16,
+                                           st.boff[j], kofs, 0, 0);
+}
+
+__device__ __forceinline__ void lgkm_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// bc: the buffer of the current K-tile (DMA target of the K-tile two ahead, `st` at `kofs`),
+// bn: the next K-tile's buffer
+template <bool FP16>
+__device__ __forceinline__ void ktile16h(v4f (&acc)[8][8], v8s (&x0a)[8], v8s (&x0b)[8],
+                                         v8s (&x1a)[8], v8s (&x1b)[8], const Stage4& st,
+                                         int kofs, char* bc, const char* bn, int w, int wr,
+                                         int wc, int lane) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const int i = h * 64 + m * 8 + n;
+    if (h == 0) mfma16a<FP16>(acc[m][n], x0b[n], x0a[m]);
+    else mfma16a<FP16>(acc[m][n], x1b[n], x1a[m]);
+    if (i < 16 && (i & 1) == 0) x1a[i >> 1] = read_frag(bc, wr * 8 + (i >> 1), 1, lane);
+    if (i == 20) lgkm_barrier();
+    if (i >= 22 && i <= 34 && (i - 22) % 3 == 0) load_a(st, bc, kofs, w, (i - 22) / 3);
+    if (i == 24 || i == 27 || i == 30 || i == 33 || i == 36 || i == 38 || i == 40 || i == 42) {
+      const int f = i <= 36 ? (i - 24) / 3 : 5 + (i - 38) / 2;
+      x1b[f] = read_frag(bc + TILE_B, wc * 8 + f, 1, lane);
+    }
+    if (i == 50) lgkm_barrier();
+    if (i == 52 || i == 55 || i == 58) load_a(st, bc, kofs, w, 5 + (i - 52) / 3);
+    if (i == 61 || i == 64) load_b(st, bc, kofs, w, (i - 61) / 3);
+    if (i == 85 || i == 87 || i == 89) load_b(st, bc, kofs, w, 2 + (i - 85) / 2);
+    if (i == 91) {
+      asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    if (i >= 93 && i <= 100) x0a[i - 93] = read_frag(bn, wr * 8 + (i - 93), 0, lane);
+    if (i >= 101 && i <= 115 && ((i - 101) & 1) == 0)
+      x0b[(i - 101) >> 1] = read_frag(bn + TILE_B, wc * 8 + ((i - 101) >> 1), 0, lane);
+    if (i == 96 || i == 100) load_b(st, bc, kofs, w, 5 + (i - 96) / 4);
+    if (i == 124) load_b(st, bc, kofs, w, 7);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int DT, int EPI>
+__global__ void __launch_bounds__(256, 1) k_gemm16h(Args a) {
+  constexpr bool FP16 = DT == LCQ_F16;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  int tm, tn;
+  {
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    if (!slot_tile(a, wgid, tm, tn)) return;
+  }
+  const int64_t nk = a.k / SKT;
+  Stage4 st;
+  make_stage16<EPI>(a, tm, tn, w, lane, st);
+
+  v4f acc[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s x0a[8], x0b[8], x1a[8], x1b[8];
+  const int k1 = nk > 1 ? SKT * 2 : 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) load_a(st, lds, 0, w, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) load_b(st, lds, 0, w, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) load_a(st, lds + BUF4, k1, w, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) load_b(st, lds + BUF4, k1, w, j);
+  wait_barrier<16>();  // K-tile 0 landed (K-tile 1's 16 pieces may be in flight)
+#pragma unroll
+  for (int m = 0; m < 8; ++m) x0a[m] = read_frag(lds, wr * 8 + m, 0, lane);
+#pragma unroll
+  for (int n = 0; n < 8; ++n) x0b[n] = read_frag(lds + TILE_B, wc * 8 + n, 0, lane);
+  asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
+  for (int64_t t = 0; t < nk; ++t) {
+    const int cur = (int)(t & 1);
+    const int64_t kt2 = t + 2 < nk ? t + 2 : nk - 1;
+    ktile16h<FP16>(acc, x0a, x0b, x1a, x1b, st, (int)(kt2 * (SKT * 2)), lds + cur * BUF4,
+                   lds + (cur ^ 1) * BUF4, w, wr, wc, lane);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 7"
+               : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]),
+                 "+a"(acc[7][4]), "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7])
+               :
+               : "memory");
+  epi16<DT, EPI, 8>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
 }
 
 // one 1024-thread workgroup: thread l sums partials l, l + 1024, ... in order, then a fixed
@@ -559,9 +687,22 @@ static void plan(Args& a, int64_t tile_n) {
   if (a.order == 1) a.nslots = 256 * ((a.n_mt + 31) / 32) * a.cpb;
 }
 
+// kernel: 2 = k_gemm16h (the product), 0 = k_gemm16b (probe build -DLCQ_PROBE_GEMM_PP=0, for
+// A/B runs: 1.5-3 % slower on the AWQ shapes, profiles/r5_gemm_variants.md)
+#ifndef LCQ_PROBE_GEMM_PP
+#define LCQ_PROBE_GEMM_PP 2
+#endif
+static constexpr int gemm_kernel() { return LCQ_PROBE_GEMM_PP; }
+
 template <int DT, int EPI>
 static int launch(Args& a, hipStream_t st) {
   // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
+  if (gemm_kernel() == 2 && a.order == 0) {
+    (void)hipFuncSetAttribute((const void*)k_gemm16h<DT, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
+    hipLaunchKernelGGL((k_gemm16h<DT, EPI>), dim3((unsigned)a.nslots), 256, 2 * BUF4, st, a);
+    return check_launch("lcq_gemm: k_gemm16h");
+  }
   (void)hipFuncSetAttribute((const void*)k_gemm16b<DT, EPI>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
   hipLaunchKernelGGL((k_gemm16b<DT, EPI>), dim3((unsigned)a.nslots), 256, 2 * BUF4, st, a);
