@@ -44,7 +44,9 @@ constexpr int OFF_SCR = OFF_L + NTL * TF;            // one scratch block (paddi
 constexpr int OFF_Z2 = OFF_SCR + TF;                 // Z of odd panels (Zs double-buffered)
 constexpr int OFF_SYNC = OFF_Z2 + TF;                // per panel: S2 arrivals of waves 1-3,
                                                      // and wave 0's "L_{p+1} written" flag
-constexpr int LDS_BYTES = (OFF_SYNC + 2 * NTL) * 4;  // 85056 B
+constexpr int OFF_JOB = OFF_SYNC + 2 * NTL;          // the S3 job table (kJobs), copied in
+constexpr int JOB_WORDS = (NTL - 1) * 3 * (12 * 2 + 4);  // 21 rows of 24 entries + count, 16-B rows
+constexpr int LDS_BYTES = (OFF_JOB + JOB_WORDS) * 4;   // 87408 B
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 
@@ -88,8 +90,8 @@ __device__ __forceinline__ v4f mma16(v4f acc, v4f at, v4f b) {
   return acc;
 }
 
-#ifndef LCQ_PROBE_CHOL_FAST_RSQ
-#define LCQ_PROBE_CHOL_FAST_RSQ 0   // probe builds: hardware v_sqrt / v_rcp in S1
+#ifndef LCQ_PROBE_CHOL_IEEE_RSQ
+#define LCQ_PROBE_CHOL_IEEE_RSQ 0   // probe builds: IEEE sqrtf / division in S1
 #endif
 
 // S1 on wave 0: factor the (symmetric) diagonal block At(q, q); L_qq rows -> Ld[q] (row-major,
@@ -100,8 +102,12 @@ __device__ __forceinline__ v4f mma16(v4f acc, v4f at, v4f b) {
 // column j of W = I (forward substitution: W[k][j] -= L[k][c] Z[c][j]); both updates are
 // v[k] -= m * L[k][c] with the lane's own multiplier m = v[c] / L[c][c] (L[r][c], or Z[c][j]),
 // so ONE fma per (c, k) serves the factorisation and the inverse, and the L[k][c] come from
-// v_readlane of the row lanes' m. sqrt and the reciprocal are IEEE (LAPACK's spotf2: ajj =
-// sqrt(ajj), column scaled by 1 / ajj). Non-positive pivots: recorded (first one, 1-based row
+// v_readlane of the row lanes' m. LAPACK's spotf2 step (ajj = sqrt(ajj), column scaled by
+// 1 / ajj) on the hardware v_sqrt_f32 / v_rcp_f32 (1 ulp; the IEEE forms, a probe build, cost
+// 1.5x the S1 chain -- 5.5k against 3.7k cycles per panel -- and move U by ~1e-7 relative,
+// below the chain's GEMM rounding; profiles/r5_chol_tile.md). The trailing updates subtract
+// the summed product once (BLAS's C - A B), which keeps GPTQ's codes >= 99.9 % equal to the
+// reference with either. Non-positive pivots: recorded (first one, 1-based row
 // row0 + 16 q + c + 1), replaced by 1.
 __device__ __forceinline__ void factor_block(float* sm, int q, int lane, int* info, int64_t row0) {
   const float* blk = sm + OFF_A + tix(q, q) * TF;
@@ -117,12 +123,12 @@ __device__ __forceinline__ void factor_block(float* sm, int q, int lane, int* in
     const float piv = rl(v[c], c);
     const bool nb = !(piv > 0.f);
     if (nb && bad == 0) bad = c + 1;
-#if LCQ_PROBE_CHOL_FAST_RSQ   // probe builds only: hardware v_sqrt / v_rcp (1 ulp)
-    const float sq = nb ? 1.f : __builtin_amdgcn_sqrtf(piv);
-    const float rinv = __builtin_amdgcn_rcpf(sq);
-#else
+#if LCQ_PROBE_CHOL_IEEE_RSQ   // probe builds only: correctly rounded sqrt and reciprocal
     const float sq = nb ? 1.f : sqrtf(piv);
     const float rinv = 1.f / sq;
+#else
+    const float sq = nb ? 1.f : __builtin_amdgcn_sqrtf(piv);
+    const float rinv = __builtin_amdgcn_rcpf(sq);
 #endif
     const float m = v[c] * rinv;   // row lane r: L[r][c]; column lane j: Z[c][j]
 #pragma unroll
@@ -178,36 +184,47 @@ __device__ constexpr int kTi[NLOW] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 
 
 // S3 job lists of a full 128-tile (ntl 8), panel p, wave 1 + w3: job n of the panel's list
 // (blocks A_{i,jc}, q <= jc <= i but (q, q), then R_{i,k}, k <= p, row by row) goes to
-// wave 1 + n % 3. Entries are LDS float offsets (dst, A-operand block, B-operand block).
+// wave 1 + n % 3. Row pw = 3 p + w3: job u = {dst | A-operand << 16, B-operand} as LDS float
+// offsets, padded to a multiple of 4 with no-op jobs on the scratch block, then the padded
+// count. The table is copied into LDS in the load phase; a wave reads its row with uniform-
+// address LDS reads at the start of the panel (hidden behind S2).
+constexpr int JMAX = 12;
+constexpr int JROW = JMAX * 2 + 4;   // words per row: 12 jobs x {dst | A << 16, B}, n4, pad
 struct JobTab {
-  uint16_t d[NTL - 1][3][12], a[NTL - 1][3][12], b[NTL - 1][3][12];
-  uint8_t cnt[NTL - 1][3];
+  uint32_t w[(NTL - 1) * 3][JROW];
 };
 
 constexpr JobTab make_jobs() {
   JobTab t{};
+  int cnt[(NTL - 1) * 3] = {};
   for (int p = 0; p < NTL - 1; ++p) {
     const int q = p + 1;
     int jn = 0;
+    auto add = [&](int d, int a, int b) {
+      const int pw = 3 * p + jn++ % 3, u = cnt[pw]++;
+      t.w[pw][2 * u] = (uint32_t)d | ((uint32_t)a << 16);
+      t.w[pw][2 * u + 1] = (uint32_t)b;
+    };
     for (int i = q; i < NTL; ++i) {
       for (int jc = q; jc <= i; ++jc) {
         if (jc == q && i == q) continue;
-        const int w3 = jn++ % 3, u = t.cnt[p][w3]++;
-        t.d[p][w3][u] = (uint16_t)(OFF_A + tix(i, jc) * TF);
-        t.a[p][w3][u] = (uint16_t)(OFF_A + tix(jc, p) * TF);
-        t.b[p][w3][u] = (uint16_t)(OFF_A + tix(i, p) * TF);
+        add(OFF_A + tix(i, jc) * TF, OFF_A + tix(jc, p) * TF, OFF_A + tix(i, p) * TF);
       }
-      for (int k = 0; k <= p; ++k) {
-        const int w3 = jn++ % 3, u = t.cnt[p][w3]++;
-        t.d[p][w3][u] = (uint16_t)(OFF_R + tix(i, k) * TF);
-        t.a[p][w3][u] = (uint16_t)(OFF_A + tix(i, p) * TF);
-        t.b[p][w3][u] = (uint16_t)(OFF_R + tix(p, k) * TF);
-      }
+      for (int k = 0; k <= p; ++k)
+        add(OFF_R + tix(i, k) * TF, OFF_A + tix(i, p) * TF, OFF_R + tix(p, k) * TF);
+    }
+  }
+  for (int pw = 0; pw < (NTL - 1) * 3; ++pw) {
+    t.w[pw][2 * JMAX] = (uint32_t)((cnt[pw] + 3) & ~3);
+    for (int u = cnt[pw]; u < JMAX; ++u) {
+      t.w[pw][2 * u] = (uint32_t)OFF_SCR | ((uint32_t)OFF_SCR << 16);
+      t.w[pw][2 * u + 1] = (uint32_t)OFF_SCR;
     }
   }
   return t;
 }
-__device__ constexpr JobTab kJobs = make_jobs();
+static_assert(sizeof(JobTab) == JOB_WORDS * 4, "job table size");
+__constant__ constexpr JobTab kJobs = make_jobs();
 
 __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t lda, int n,
                                                        float* Lout, int64_t ldl,
@@ -271,6 +288,9 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
     factor_block(sm, 0, lane, info, row0);
     PROF_STAMP(2, 0)
   } else {
+    // the S3 job table into LDS (full tiles only use it)
+    for (int e = tid - 64; e < JOB_WORDS; e += NT - 64)
+      reinterpret_cast<uint32_t*>(sm + OFF_JOB)[e] = (&kJobs.w[0][0])[e];
     constexpr int PER = (NLOW - 1 + 2) / 3;   // 12
     v4f v[PER];
 #pragma unroll
@@ -286,12 +306,13 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
   }
   __syncthreads();
 
-  // X block row p is final once S2 of panel p wrote it: its writer stores it to global memory
-  // right away (row 16 p + r16, columns 16 k + g4 .. + 3 per lane: one float4, read back from
-  // the accumulator layout -- element (r, c) at lane c + 16 (r >> 2), register r & 3 -- its own
-  // LDS writes, in order), so the output overlaps the later panels; the zero blocks above the
-  // diagonal are written by the waves with spare S2 slots.
-  const bool xvec = vec && (ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  // X output. A full tile (vec) keeps X in LDS and writes it after the last panel, all four
+  // waves in parallel (per panel it sat on the critical S2 -> S3 path). A partial tile stores
+  // block row p once S2 of panel p wrote it, from its writers (row 16 p + r16, columns
+  // 16 k + g4 .. + 3 per lane, read back from the accumulator layout -- element (r, c) at lane
+  // c + 16 (r >> 2), register r & 3), the zero blocks above the diagonal from the waves with
+  // spare S2 slots.
+  const bool xvec = vec;   // the host checks X's alignment and ldx into vec
   auto store_x = [&](int i, int k, const float* blk) {
     const int row = TT * i + r16, c0 = TT * k + g4;
     v4f x = {0.f, 0.f, 0.f, 0.f};
@@ -332,7 +353,7 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
       float* blk = nL > 0 ? sm + OFF_A + tix(p + 1, p) * TF : sm + OFF_R + tix(p, 0) * TF;
       const v4f o = mma16(v4f{0.f, 0.f, 0.f, 0.f}, zt, ld4(blk, lane));
       st4(blk, lane, o);
-      if (nL == 0) store_x(p, 0, blk);
+      if (nL == 0 && !vec) store_x(p, 0, blk);
       if (nL > 0) {
         float* d = sm + OFF_A + tix(p + 1, p + 1) * TF;
         st4(d, lane, ld4(d, lane) - mma16(v4f{0.f, 0.f, 0.f, 0.f}, o, o));
@@ -344,20 +365,30 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
         PROF_STAMP(5 + 4 * p, 0)
       }
     } else {
+      // this wave's S3 job row (full tiles): uniform-address LDS reads, in flight during S2
+      v4f jrow[JROW / 4];
+      if (ntl == NTL && nL > 0) {
+        const v4f* jr = reinterpret_cast<const v4f*>(sm + OFF_JOB + (3 * p + w - 1) * JROW);
+#pragma unroll
+        for (int c = 0; c < JROW / 4; ++c) jrow[c] = jr[c];
+      }
       for (int t = w; t < njobs; t += 3) {
         float* blk = t < nL ? sm + OFF_A + tix(p + 1 + t, p) * TF
                             : sm + OFF_R + tix(p, t - nL) * TF;
         st4(blk, lane, mma16(v4f{0.f, 0.f, 0.f, 0.f}, zt, ld4(blk, lane)));
-        if (t >= nL) store_x(p, t - nL, blk);
+        if (t >= nL && !vec) store_x(p, t - nL, blk);
       }
-      for (int k = p + w; k < ntl; k += 3)   // X_pk = 0 above the diagonal (k = p+1 ..)
-        if (k > p) store_x(p, k, nullptr);
+      if (!vec)
+        for (int k = p + w; k < ntl; k += 3)   // X_pk = 0 above the diagonal (k = p+1 ..)
+          if (k > p) store_x(p, k, nullptr);
+      PROF_STAMP(52 + p, 1)
       if (nL > 0) {
         // waves 1-3 meet: every S2 block written (LDS requests of a wave complete in order,
         // so a block is visible once its writer's arrival is), and L_{p+1} from wave 0
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_fetch_add(arrive + p, 1, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+
         while (__hip_atomic_load(arrive + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 3 ||
                __hip_atomic_load(lflag + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
           __builtin_amdgcn_s_sleep(1);
@@ -366,15 +397,16 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
         // R_{i,k} (i >= q, k <= p), job n to wave 1 + n % 3, four at a time
         const int q = p + 1;
         const Job pad = {scratch, scratch, scratch};
-        if (ntl == NTL) {   // the full tile: the precomputed job list
-          const int w3 = w - 1, cnt = kJobs.cnt[p][w3];
-          const uint16_t* td = kJobs.d[p][w3];
-          const uint16_t* ta = kJobs.a[p][w3];
-          const uint16_t* tb = kJobs.b[p][w3];
+        if (ntl == NTL) {   // the full tile: the precomputed job list (jrow, read above)
+          auto word = [&](int e) { return __float_as_uint(jrow[e >> 2][e & 3]); };
           auto job = [&](int u) {
-            return u < cnt ? Job{sm + td[u], sm + ta[u], sm + tb[u]} : pad;
+            const uint32_t da = word(2 * u);
+            return Job{sm + (da & 0xffffu), sm + (da >> 16), sm + word(2 * u + 1)};
           };
-          for (int u = 0; u < cnt; u += 4) run4(job(u), job(u + 1), job(u + 2), job(u + 3), lane);
+          const uint32_t jn4 = word(2 * JMAX);
+#pragma unroll
+          for (int u = 0; u < JMAX; u += 4)
+            if (u < (int)jn4) run4(job(u), job(u + 1), job(u + 2), job(u + 3), lane);
         } else {
           Job j0 = pad, j1 = pad, j2 = pad, j3 = pad;   // a shift register (no indexed array)
           int cnt = 0, jn = 0;
@@ -411,7 +443,30 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
   }
   PROF_STAMP(40, 0)
 
-  // L when asked for (X went out panel by panel)
+  // X of a full tile: every block row-major from LDS (store_x), the four waves in parallel;
+  // the blocks above the diagonal are zeros
+  if (vec) {
+    // wave w: block rows w and w + 4; a row's LDS reads all issued before its stores
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = w + 4 * h;
+      const float* rrow = sm + OFF_R + tix(i, 0) * TF + 4 * (g4 + 16 * (r16 >> 2)) + (r16 & 3);
+      v4f xb[NTL];
+#pragma unroll
+      for (int k = 0; k < NTL; ++k) {
+        xb[k] = v4f{0.f, 0.f, 0.f, 0.f};
+        if (k <= i) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            xb[k][jj] = k < i || g4 + jj <= r16 ? rrow[k * TF + 4 * jj] : 0.f;
+        }
+      }
+      float* xr = X + (int64_t)(TT * i + r16) * ldx + g4;
+#pragma unroll
+      for (int k = 0; k < NTL; ++k) *reinterpret_cast<v4f*>(xr + TT * k) = xb[k];
+    }
+  }
+  // L when asked for
   if (Lout) {
     for (int t = w; t < NTL * NTL; t += 4) {
       const int i = t >> 3, k = t & 7;
@@ -449,7 +504,8 @@ extern "C" int lcq_chol_inv_tile(const void* A, int64_t lda, int n, void* L, int
   LCQ_REQUIRE(n > 0 && n <= CTILE && lda >= n && ldx >= n && (!L || ldl >= n),
               "tile must be 1..128 wide");
   const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  const int vec = n == CTILE && lda % 4 == 0 && al(A) && (!L || (ldl % 4 == 0 && al(L)));
+  const int vec = n == CTILE && lda % 4 == 0 && al(A) && (!L || (ldl % 4 == 0 && al(L))) &&
+                  ldx % 4 == 0 && al(X);
   // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
   (void)hipFuncSetAttribute((const void*)k_chol_inv_tile,
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);

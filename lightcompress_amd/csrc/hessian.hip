@@ -295,6 +295,75 @@ __device__ __forceinline__ void ktile(v4f (&acc)[8][8], v8s (&bf)[2][8][2], v8s 
   }
 }
 
+// The three-barrier K-tile of the projection GEMM's k_gemm16h (gemm256.hip), on this kernel's
+// token-major image: fragments double-buffered by k half (X0 = tokens 0-31 of the K-tile,
+// X1 = tokens 32-63), K-tile t + 2 loaded into K-tile t's buffer -- its A pieces after barrier 1,
+// its B pieces after barrier 2 -- and one counted vmcnt per K-tile (barrier 3: K-tile t + 1
+// landed, its X0 is read during the last 32 MFMAs). The transposed reads are asm: their
+// completion is waited for explicitly (barriers 1 and 2 for X1, the end of the K-tile for X0).
+// Same k order per accumulator as ktile(): identical sums.
+#ifndef LCQ_PROBE_SYRK_3B
+#define LCQ_PROBE_SYRK_3B 0   // 1: the three-barrier schedule (probe builds until measured)
+#endif
+template <bool FP16, int P>
+__device__ __forceinline__ void ktile3(v4f (&acc)[8][8], v8s (&x0a)[8], v8s (&x0b)[8],
+                                       v8s (&x1a)[8], v8s (&x1b)[8], const Stage& st,
+                                       const FragOff& fo, const Args& a, char* lds, int64_t kt0,
+                                       int64_t t, int64_t nk, int w) {
+  constexpr int cur = P;  // t & 1
+  constexpr int At = cur * BUF;
+  constexpr int An = (cur ^ 1) * BUF;
+  const int64_t t2 = t + 2 < nk ? t + 2 : nk - 1;
+  const __amdgpu_buffer_rsrc_t rs = ktile_rsrc(a, kt0 + t2);
+  char* d = lds + cur * BUF;
+  auto load_a = [&](int j) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(d + (j * 4 + w) * 1024), 16,
+                                             st.aoff[j], 0, 0, 0);
+  };
+  auto load_b = [&](int j) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(d + TILE_B + (j * 4 + w) * 1024),
+                                             16, st.boff[j], 0, 0, 0);
+  };
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const int i = h * 64 + m * 8 + n;
+    if (h == 0) mfma16a<FP16>(acc[m][n], x0b[n], x0a[m]);
+    else mfma16a<FP16>(acc[m][n], x1b[n], x1a[m]);
+    if (i < 16 && (i & 1) == 0) x1a[i >> 1] = frag_at<At>(fo, 0, i >> 1, 1);
+    if (i == 20) {                     // X1.A landed; every wave is past t's A
+      block_wait();
+      __builtin_amdgcn_s_barrier();
+    }
+    if (i >= 22 && i <= 34 && (i - 22) % 3 == 0) load_a((i - 22) / 3);
+    if (i == 24 || i == 27 || i == 30 || i == 33 || i == 36 || i == 38 || i == 40 || i == 42) {
+      const int f = i <= 36 ? (i - 24) / 3 : 5 + (i - 38) / 2;
+      x1b[f] = frag_at<At + TILE_B>(fo, 1, f, 1);
+    }
+    if (i == 50) {                     // X1.B landed; every wave is past t's B
+      block_wait();
+      __builtin_amdgcn_s_barrier();
+    }
+    if (i == 52 || i == 55 || i == 58) load_a(5 + (i - 52) / 3);
+    if (i == 61 || i == 64) load_b((i - 61) / 3);
+    if (i == 85 || i == 87 || i == 89) load_b(2 + (i - 85) / 2);
+    if (i == 91) {
+      asm volatile("s_waitcnt vmcnt(13)" ::: "memory");   // K-tile t + 1 landed
+      __builtin_amdgcn_s_barrier();
+    }
+    if (i >= 93 && i <= 100) x0a[i - 93] = frag_at<An>(fo, 0, i - 93, 0);
+    if (i >= 101 && i <= 115 && ((i - 101) & 1) == 0)
+      x0b[(i - 101) >> 1] = frag_at<An + TILE_B>(fo, 1, (i - 101) >> 1, 0);
+    if (i == 96 || i == 100) load_b(5 + (i - 96) / 4);
+    if (i == 124) load_b(7);
+    if (i == 127) block_wait();        // X0 of K-tile t + 1 landed
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <bool FP16>
 __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a, GArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -342,7 +411,6 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a, GArgs ga) {
   for (int m = 0; m < 8; ++m)
 #pragma unroll
     for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
-  v8s af[2][2][2], bf[2][8][2];
   {
     const __amdgpu_buffer_rsrc_t r0 = ktile_rsrc(a, kt0);
     const __amdgpu_buffer_rsrc_t r1 = ktile_rsrc(a, kt0 + (nk > 1 ? 1 : 0));
@@ -351,6 +419,23 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a, GArgs ga) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) load_piece(st, r1, lds, 1, w, i);
   }
+  if constexpr (LCQ_PROBE_SYRK_3B) {
+    wait_barrier<16>();  // K-tile 0 landed (K-tile 1's 16 pieces may be in flight)
+    v8s x0a[8], x0b[8], x1a[8], x1b[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) x0a[m] = frag_at<0>(fo, 0, m, 0);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) x0b[n] = frag_at<TILE_B>(fo, 1, n, 0);
+    block_wait();
+    asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
+    int64_t t = 0;
+    for (; t + 1 < nk; t += 2) {
+      ktile3<FP16, 0>(acc, x0a, x0b, x1a, x1b, st, fo, a, lds, kt0, t, nk, w);
+      ktile3<FP16, 1>(acc, x0a, x0b, x1a, x1b, st, fo, a, lds, kt0, t + 1, nk, w);
+    }
+    if (t < nk) ktile3<FP16, 0>(acc, x0a, x0b, x1a, x1b, st, fo, a, lds, kt0, t, nk, w);
+  } else {
+  v8s af[2][2][2], bf[2][8][2];
   wait_barrier<22>();
 #pragma unroll
   for (int n = 0; n < 8; ++n)
@@ -368,6 +453,7 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a, GArgs ga) {
     ktile<FP16, 1>(acc, bf, af, st, fo, a, lds, kt0, t + 1, nk, w, wr, wc);
   }
   if (t < nk) ktile<FP16, 0>(acc, bf, af, st, fo, a, lds, kt0, t, nk, w, wr, wc);
+  }
   // drain, and cover the last MFMA's result latency before the accumulators are read (the asm
   // MFMA is opaque to the hazard recognizer: 16x16x32 = 8 passes -> 4 * 8 + 2 wait states)
   // The nops carry the last block's accumulators as operands: an epilogue read of them cannot

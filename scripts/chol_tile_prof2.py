@@ -35,9 +35,10 @@ for p in range(8):
     row = f'panel {p}: total {nxt - st:5d}'
     if p < 7:
         row += (f'  w0: L+diag {t[b] - st:5d}  S1 {t[b + 2] - t[b]:5d}'
-                f'  w1: S2+meet {t[b + 1] - st:5d}  S3 {t[b + 3] - t[b + 1]:5d}')
+                f'  w1: S2 {t[52 + p] - st:5d}'
+                f'  +meet {t[b + 1] - st:5d}  S3 {t[b + 3] - t[b + 1]:5d}')
     print(row)
-print('store', t[40 + 1] - t[40])
+print('X + L store', t[40 + 1] - t[40])
 torch.cuda.synchronize()
 t1 = time.perf_counter()
 for _ in range(200):
