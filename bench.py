@@ -259,7 +259,7 @@ def gemm_roofline(kern, elapsed):
     by = sum(f.get('bytes', 0.0) for f in fam)
     tf = fl / (ms * 1e-3) / 1e12
     traffic, src = pmc_traffic('awq', 'k_gemm16')
-    return {'kernel': 'k_gemm16b (csrc/gemm256.hip): bf16 MFMA projection GEMMs of the AWQ loss '
+    return {'kernel': 'k_gemm16h (csrc/gemm256.hip): bf16 MFMA projection GEMMs of the AWQ loss '
                       'search + calibration forwards, epilogues fused (q/k/v, SiLU*up, loss)',
             'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS,
             'unit': 'TFLOP/s', 'frac': round(tf / PEAK_BF16_TFLOPS, 4), 'traffic': traffic,
@@ -979,6 +979,12 @@ def main():
 
     if rank == 0:
         roofline = gemm_roofline(kern, elapsed)
+        if roofline and clock and clock.get('mean'):
+            # informative: the dense peak scaled to the GFX clock held over the timed region
+            # (MI355X_MICROARCH.md's 2.5 PF is quoted at 2.4 GHz); `frac` stays against 2.5 PF
+            at_clk = PEAK_BF16_TFLOPS * clock['mean'] / 2400.0
+            roofline['peak_at_sampled_clock'] = round(at_clk, 1)
+            roofline['frac_at_sampled_clock'] = round(roofline['achieved'] / at_clk, 4)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             cpu = cpu_baseline_awq(args, args.cpu_budget_s)

@@ -301,10 +301,9 @@ __device__ __forceinline__ void ktile(v4f (&acc)[8][8], v8s (&bf)[2][8][2], v8s 
 // its B pieces after barrier 2 -- and one counted vmcnt per K-tile (barrier 3: K-tile t + 1
 // landed, its X0 is read during the last 32 MFMAs). The transposed reads are asm: their
 // completion is waited for explicitly (barriers 1 and 2 for X1, the end of the K-tile for X0).
-// Same k order per accumulator as ktile(): identical sums.
-#ifndef LCQ_PROBE_SYRK_3B
-#define LCQ_PROBE_SYRK_3B 0   // 1: the three-barrier schedule (probe builds until measured)
-#endif
+// Same k order per accumulator as ktile(): identical sums, so the host picks either per launch
+// (profiles/r5_hessian_schedule_ab.txt: faster for the per-input accumulation at every IC and
+// for the grouped launch at IC 4096, 5 % slower for the grouped launch at IC 14336).
 template <bool FP16, int P>
 __device__ __forceinline__ void ktile3(v4f (&acc)[8][8], v8s (&x0a)[8], v8s (&x0b)[8],
                                        v8s (&x1a)[8], v8s (&x1b)[8], const Stage& st,
@@ -364,7 +363,7 @@ __device__ __forceinline__ void ktile3(v4f (&acc)[8][8], v8s (&x0a)[8], v8s (&x0
   }
 }
 
-template <bool FP16>
+template <bool FP16, bool S3>
 __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a, GArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -419,7 +418,7 @@ __global__ void __launch_bounds__(256, 1) k_syrk_x(Args a, GArgs ga) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) load_piece(st, r1, lds, 1, w, i);
   }
-  if constexpr (LCQ_PROBE_SYRK_3B) {
+  if constexpr (S3) {
     wait_barrier<16>();  // K-tile 0 landed (K-tile 1's 16 pieces may be in flight)
     v8s x0a[8], x0b[8], x1a[8], x1b[8];
 #pragma unroll
@@ -763,7 +762,8 @@ extern "C" int lcq_hessian_accum(const void* x, int x_dtype, int64_t n, int64_t 
   ga.tail[0] = a.tail;
   ga.split0[0] = 0;
   ga.split0[1] = a.ns;
-  auto k = x_dtype == LCQ_F16 ? k_syrk_x<true> : k_syrk_x<false>;
+  // ktile3: the faster schedule for this launch at every IC measured
+  auto k = x_dtype == LCQ_F16 ? k_syrk_x<true, true> : k_syrk_x<false, true>;
   // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
   hipLaunchKernelGGL(k, dim3((unsigned)(8 * ((a.ntiles + 7) / 8) * a.ns)), 256, 2 * BUF, st, a,
@@ -829,7 +829,9 @@ extern "C" int lcq_hessian_grouped(const void* x, int x_dtype, int64_t ic,
   }
   a.part = reinterpret_cast<float*>(ws + off);
   if (p.splits > 0) {
-    auto k = x_dtype == LCQ_F16 ? k_syrk_x<true> : k_syrk_x<false>;
+    const bool s3 = ic <= 8192;   // the schedule measured faster at this IC (ktile3)
+    auto k = x_dtype == LCQ_F16 ? (s3 ? k_syrk_x<true, true> : k_syrk_x<true, false>)
+                                : (s3 ? k_syrk_x<false, true> : k_syrk_x<false, false>);
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               2 * BUF);
     hipLaunchKernelGGL(k, dim3((unsigned)(8 * ((a.ntiles + 7) / 8) * p.splits)), 256, 2 * BUF,
