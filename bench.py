@@ -60,7 +60,8 @@ LLAMA3_8B = dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=
 LLAMA3_70B = dict(LLAMA3_8B, hidden_size=8192, intermediate_size=28672,
                   num_attention_heads=64, num_key_value_heads=8, num_hidden_layers=80)
 N_LINEARS_PER_BLOCK = 7
-GEMM_FAMILY = ('lcq_gemm', 'lcq_gemm_silu_mul', 'lcq_gemm_sq_diff', 'lcq_gemm_residual')
+GEMM_FAMILY = ('lcq_gemm', 'lcq_gemm_rope', 'lcq_gemm_silu_mul', 'lcq_gemm_sq_diff',
+               'lcq_gemm_residual')
 
 
 def parse():

@@ -626,6 +626,19 @@ int lcq_gemm(const void* a, int dtype, int64_t lda, int64_t m, int64_t k, int ns
              const void* const* b, const int64_t* b_rows, int64_t ldb, const void* const* bias,
              void* const* c, const int64_t* ldc, void* stream);
 
+/* lcq_gemm with transformers' apply_rotary_pos_emb (models/llama/modeling_llama.py; the
+ * calibration forward of LlamaAttention, base_blockwise_quantization.py:367-381, and the AWQ
+ * inspect forward of the q/k/v subset, awq.py:110-126) fused into the epilogue: the first
+ * rope_segs segments (q, k: multiples of 256 rows, heads of head_dim 128) are written as
+ * rnd(rnd(x cos) + rnd(rotate_half(x) sin)) of their rounded outputs x -- bit-identical to
+ * lcq_gemm followed by lcq_rotary. cos / sin [1 or B, seq, 128] in dtype, batch stride
+ * cs_bstride (0: shared); m = B * seq rows, token row t at position t % seq. */
+int lcq_gemm_rope(const void* a, int dtype, int64_t lda, int64_t m, int64_t k, int nseg,
+                  const void* const* b, const int64_t* b_rows, int64_t ldb,
+                  const void* const* bias, void* const* c, const int64_t* ldc, int rope_segs,
+                  const void* cos, const void* sin, int64_t seq, int64_t cs_bstride,
+                  int64_t head_dim, void* stream);
+
 /* C = rnd(res + rnd(A B^T + bias)) (one segment): the decoder block's `residual + o_proj(x)`
  * and `h + down_proj(m)` (transformers LlamaDecoderLayer.forward, the calibration forwards of
  * base_blockwise_quantization.py:367-381) with the add in the GEMM epilogue. res [M, N] (ldr),

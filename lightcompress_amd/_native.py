@@ -126,6 +126,8 @@ SIGNATURES = {
     'lcq_mse_qparams': ([_vp, _int, _i64, _i64, _int, _int, _int, _int, _f32, _f32, _vp, _vp,
                          _vp, _vp, _vp], _int),
     'lcq_gemm': ([_vp, _int, _i64, _i64, _i64, _int, _vp, _vp, _i64, _vp, _vp, _vp, _vp], _int),
+    'lcq_gemm_rope': ([_vp, _int, _i64, _i64, _i64, _int, _vp, _vp, _i64, _vp, _vp, _vp, _int,
+                       _vp, _vp, _i64, _i64, _i64, _vp], _int),
     'lcq_gemm_residual': ([_vp, _int, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp,
                            _i64, _vp], _int),
     'lcq_gemm_silu_mul': ([_vp, _int, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp],

@@ -19,6 +19,10 @@
 //               never written)
 //   EPI_RESID   C[t, c] = rnd(res[t, c] + rnd(acc + bias)): a block's `residual + o_proj(x)` /
 //               `h + down_proj(m)` (the residual read through the ref pointer, one segment)
+//   EPI_ROPE    EPI_STORE + the rotary embedding of the leading segments (q, k) on the rounded
+//               outputs: transformers' apply_rotary_pos_emb, out = rnd(rnd(x cos) + rnd(rh(x) sin))
+//               with rh(x) = cat(-x2, x1) -- a head (128 columns) is one wave's tile columns,
+//               column c and its partner c +- 64 sit in the same lane (blocks n and n + 4)
 //   EPI_SQDIFF  out = rnd(acc + bias) is never written: d = rnd(ref - out), the tile's
 //               sum of fp32 d*d goes to an fp64 partial per tile; k_loss_reduce sums the
 //               partials in tile order (deterministic) and writes sum / numel to a device slot
@@ -51,7 +55,7 @@ constexpr int SKT = 64;            // K-tile
 constexpr int HALF_B = 16384;      // 128 rows x 64 k x 2 B
 constexpr int BUF_B = 4 * HALF_B;  // A_lo, A_hi, B_lo, B_hi
 enum { H_ALO = 0, H_AHI = 1, H_BLO = 2, H_BHI = 3 };
-enum { EPI_STORE = 0, EPI_SILU = 1, EPI_SQDIFF = 2, EPI_RESID = 3 };
+enum { EPI_STORE = 0, EPI_SILU = 1, EPI_SQDIFF = 2, EPI_RESID = 3, EPI_ROPE = 4 };
 constexpr int MAXSEG = 3;
 
 struct Args {
@@ -72,6 +76,12 @@ struct Args {
   int n_mt, n_nt, cpb, nslots;
   int order;  // tile order of k_gemm16: 0 = per-XCD bands (slot_tile), 1 = N-band-major (tile_nb)
   int wide;   // every output pointer 16-B aligned and every ldc % 8 == 0: 16-B epilogue stores
+  // EPI_ROPE: segments s < rope_segs are rotated (head dim 128 = one wave's 128 columns);
+  // token row t = b * seq + p reads cos / sin [.., seq, 128] at b * cs_bstride + p * 128
+  const uint16_t* cos;
+  const uint16_t* sin;
+  int64_t seq, cs_bstride;
+  int rope_segs;
 };
 
 // work slot -> tile (4 x 8 blocks of tiles, bands of 4 tile rows walked along N)
@@ -418,7 +428,30 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][NB], int tm, 
           for (int j = 0; j < 4; ++j) o[n][j] = rnd<DT>(__fadd_rn(r[j], o[n][j]));
         }
       }
-      if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
+      if constexpr (EPI == EPI_ROPE) {
+        static_assert(NB == 8, "rotary epilogue: one head per wave column");
+        if (s < a.rope_segs) {
+          const int64_t b = trow / a.seq, p = trow - b * a.seq;
+          const uint16_t* cr = a.cos + b * a.cs_bstride + p * 128 + fq * 4;
+          const uint16_t* sr = a.sin + b * a.cs_bstride + p * 128 + fq * 4;
+          float cs[NB][4], sn[NB][4];
+#pragma unroll
+          for (int n = 0; n < NB; ++n) {
+            unpack4<DT>(*reinterpret_cast<const uint2*>(cr + n * 16), cs[n]);
+            unpack4<DT>(*reinterpret_cast<const uint2*>(sr + n * 16), sn[n]);
+          }
+#pragma unroll
+          for (int n = 0; n < NB / 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float x1 = o[n][j], x2 = o[n + NB / 2][j];
+              o[n][j] = rnd<DT>(rnd<DT>(x1 * cs[n][j]) + rnd<DT>(-x2 * sn[n][j]));
+              o[n + NB / 2][j] =
+                  rnd<DT>(rnd<DT>(x2 * cs[n + NB / 2][j]) + rnd<DT>(x1 * sn[n + NB / 2][j]));
+            }
+        }
+      }
+      if constexpr (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_ROPE) {
         uint16_t* crow = a.c[s] + trow * a.ldc[s] + lcol0;
         if (a.wide && full_n) {
           uint16_t* cpair = crow - fq * 4 + poff;
@@ -768,6 +801,50 @@ extern "C" int lcq_gemm(const void* a, int dtype, int64_t lda, int64_t m, int64_
     if (!aligned16(c[s]) || ldc[s] % 8 != 0) g.wide = 0;
   plan(g, ST);
   return dispatch<EPI_STORE>(dtype, g, as_stream(stream));
+}
+
+extern "C" int lcq_gemm_rope(const void* a, int dtype, int64_t lda, int64_t m, int64_t k,
+                             int nseg, const void* const* b, const int64_t* b_rows, int64_t ldb,
+                             const void* const* bias, void* const* c, const int64_t* ldc,
+                             int rope_segs, const void* cos, const void* sin, int64_t seq,
+                             int64_t cs_bstride, int64_t head_dim, void* stream) {
+  int rc = check_common(dtype, a, lda, m, k, ldb);
+  if (rc) return rc;
+  LCQ_REQUIRE(nseg >= 1 && nseg <= MAXSEG && b && b_rows && c && ldc, "1..3 segments");
+  LCQ_REQUIRE(head_dim == 128, "the rotary epilogue takes head_dim 128 (one wave column)");
+  LCQ_REQUIRE(rope_segs >= 0 && rope_segs <= nseg, "rope_segs must be 0..nseg");
+  LCQ_REQUIRE(seq > 0 && m % seq == 0, "m must be a whole number of sequences");
+  LCQ_REQUIRE(cos && sin && aligned8(cos) && aligned8(sin) && cs_bstride >= 0 &&
+                  cs_bstride % 4 == 0, "cos / sin [1 or B, seq, 128], 8-byte aligned");
+  Args g{};
+  g.a = reinterpret_cast<const uint16_t*>(a);
+  g.lda = lda; g.m = m; g.k = k; g.ldb = ldb; g.nseg = nseg;
+  int64_t end = 0;
+  for (int s = 0; s < nseg; ++s) {
+    LCQ_REQUIRE(b_rows[s] > 0 && b_rows[s] % 16 == 0, "segment rows must be multiples of 16");
+    LCQ_REQUIRE(s == nseg - 1 || b_rows[s] % ST == 0,
+                "all but the last segment must be multiples of 256 rows");
+    LCQ_REQUIRE(s >= rope_segs || b_rows[s] % ST == 0, "rotated segments: multiples of 256");
+    LCQ_REQUIRE(b[s] && aligned16(b[s]) && c[s] && aligned8(c[s]), "segment pointers");
+    LCQ_REQUIRE(ldc[s] >= b_rows[s] && ldc[s] % 4 == 0, "ldc must be >= rows, multiple of 4");
+    end += b_rows[s];
+    g.b[s] = reinterpret_cast<const uint16_t*>(b[s]);
+    g.bend[s] = end;
+    g.bias[s] = bias ? reinterpret_cast<const uint16_t*>(bias[s]) : nullptr;
+    g.c[s] = reinterpret_cast<uint16_t*>(c[s]);
+    g.ldc[s] = ldc[s];
+  }
+  g.n = end;
+  g.wide = 1;
+  for (int s = 0; s < nseg; ++s)
+    if (!aligned16(c[s]) || ldc[s] % 8 != 0) g.wide = 0;
+  g.cos = reinterpret_cast<const uint16_t*>(cos);
+  g.sin = reinterpret_cast<const uint16_t*>(sin);
+  g.seq = seq;
+  g.cs_bstride = cs_bstride;
+  g.rope_segs = rope_segs;
+  plan(g, ST);
+  return dispatch<EPI_ROPE>(dtype, g, as_stream(stream));
 }
 
 extern "C" int lcq_gemm_residual(const void* a, int dtype, int64_t lda, int64_t m, int64_t k,

@@ -190,11 +190,26 @@ def _stage(cache, name, key, mods, fn):
     return val
 
 
-def qkv_proj(attn, xn, weights=None):
+def _rope_fusable(attn, xn, rope):
+    """The rotary embedding can go into the q/k/v GEMM's epilogue (lcq_gemm_rope): the
+    patched apply_rotary_pos_emb would have run lcq_rotary on these shapes, heads of 128."""
+    if rope is None or xn.dim() != 3 or getattr(attn, 'head_dim', None) != 128:
+        return False
+    from transformers.models.llama import modeling_llama as ml
+    cos, sin = rope
+    B, S = xn.shape[0], xn.shape[1]
+    return (ml.apply_rotary_pos_emb is _fused_apply_rotary and cos.dim() == 3
+            and cos.dtype == xn.dtype and sin.dtype == xn.dtype and sin.shape == cos.shape
+            and cos.shape[0] in (1, B) and tuple(cos.shape[1:]) == (S, 128))
+
+
+def qkv_proj(attn, xn, weights=None, rope=None):
     """q / k / v projections of LlamaAttention: one lcq GEMM launch for the three when they
     are linears the GEMM takes with no hooks or only input-capture hooks (x read once), else
     the three modules. `weights` overrides the three weights (the AWQ search's
-    fake-quantized copies; their modules' hooks are not fired)."""
+    fake-quantized copies; their modules' hooks are not fired). `rope` = (cos, sin): when
+    the launch can take it, q and k come back already rotated (lcq_gemm_rope) and the
+    returned flag is True; callers then skip apply_rotary_pos_emb."""
     from . import ops
     mods = (attn.q_proj, attn.k_proj, attn.v_proj)
     fused = weights is not None or _input_only_hooked(*mods)
@@ -210,11 +225,13 @@ def qkv_proj(attn, xn, weights=None):
         if weights is None:  # input-capture hooks fire first, in module order
             for m in mods:
                 _fire_input_hooks(m, xn)
-        return ops.linear_multi(xn, ws, bs)
+        if _rope_fusable(attn, xn, rope):
+            return (*ops.linear_multi_rope(xn, ws, bs, rope[0], rope[1], rope_segs=2), True)
+        return (*ops.linear_multi(xn, ws, bs), False)
     if weights is not None:
         from .module_utils import lcq_linear
-        return [lcq_linear(xn, w, m.bias) for w, m in zip(ws, mods)]
-    return [m(xn) for m in mods]
+        return (*[lcq_linear(xn, w, m.bias) for w, m in zip(ws, mods)], False)
+    return (*[m(xn) for m in mods], False)
 
 
 def _attn_core(attn, xn, position_embeddings, attention_mask, qkv_weights=None, **kwargs):
@@ -222,12 +239,13 @@ def _attn_core(attn, xn, position_embeddings, attention_mask, qkv_weights=None, 
     from transformers.models.llama import modeling_llama as ml
     input_shape = xn.shape[:-1]
     hidden_shape = (*input_shape, -1, attn.head_dim)
-    q, k, v = qkv_proj(attn, xn, qkv_weights)
+    cos, sin = position_embeddings
+    q, k, v, rotated = qkv_proj(attn, xn, qkv_weights, rope=(cos, sin))
     q = q.view(hidden_shape).transpose(1, 2)
     k = k.view(hidden_shape).transpose(1, 2)
     v = v.view(hidden_shape).transpose(1, 2)
-    cos, sin = position_embeddings
-    q, k = ml.apply_rotary_pos_emb(q, k, cos, sin)
+    if not rotated:
+        q, k = ml.apply_rotary_pos_emb(q, k, cos, sin)
     iface = ml.ALL_ATTENTION_FUNCTIONS.get_interface(attn.config._attn_implementation,
                                                       ml.eager_attention_forward)
     out, _ = iface(attn, q, k, v, attention_mask,

@@ -13,7 +13,7 @@ from . import _native as N
 
 __all__ = ['int_quant_dynamic', 'int_quant_static', 'pack_vllm', 'pack_autoawq_gemm',
            'hessian_accum', 'gptq_block', 'absmean_cols', 'awq_weight_scale', 'awq_scales', 'scale_bcast',
-           'sq_diff_mean', 'auto_clip_search', 'clip_apply', 'linear', 'linear_multi',
+           'sq_diff_mean', 'auto_clip_search', 'clip_apply', 'linear', 'linear_multi', 'linear_multi_rope',
            'linear_silu_mul', 'linear_sq_diff', 'gemm_supported']
 
 
@@ -544,6 +544,48 @@ def linear_multi(x: torch.Tensor, weights, biases=None):
     N.note_work('lcq_gemm', 2.0 * M * K * Ntot)
     N.note_bytes('lcq_gemm', 2.0 * (M * K + Ntot * K + M * Ntot))
     return [o.view(*x.shape[:-1], o.shape[1]) for o in outs]
+
+
+def linear_multi_rope(x: torch.Tensor, weights, biases, cos: torch.Tensor, sin: torch.Tensor,
+                      rope_segs: int = 2):
+    """linear_multi with transformers' apply_rotary_pos_emb applied to the first `rope_segs`
+    outputs in the GEMM epilogue (lcq_gemm_rope; the q / k of LlamaAttention): x [B, S, C],
+    cos / sin [1 or B, S, 128] in x's dtype, heads of 128. Bit-identical to linear_multi
+    followed by rotary on the head-transposed views, without the rotary kernel's extra
+    read + write of q and k."""
+    import ctypes
+    if x.dim() != 3:
+        raise ValueError('x must be [B, S, C]')
+    B, S, _ = x.shape
+    x2 = _rows2d(x)
+    M, K = x2.shape
+    n = len(weights)
+    if not 1 <= n <= 3 or not 0 <= rope_segs <= n:
+        raise ValueError('1..3 weights, rope_segs <= n')
+    for w in weights[:-1]:
+        if w.shape[0] % 256 != 0:
+            raise ValueError('all but the last weight need a multiple of 256 rows')
+    cos, sin = cos.contiguous(), sin.contiguous()
+    if (cos.dim() != 3 or tuple(cos.shape[1:]) != (S, 128) or cos.shape[0] not in (1, B)
+            or sin.shape != cos.shape or cos.dtype != x.dtype or sin.dtype != x.dtype):
+        raise ValueError('cos / sin must be [1 or B, S, 128] in the input dtype')
+    outs = [torch.empty((M, w.shape[0]), dtype=x.dtype, device=x.device) for w in weights]
+    bs = list(biases) if biases is not None else [None] * n
+    for b, w in zip(bs, weights):
+        if b is not None and (b.dtype != x.dtype or b.numel() != w.shape[0] or not b.is_contiguous()):
+            raise ValueError('bias must be contiguous [N] in the input dtype')
+    arr_b = (ctypes.c_void_p * 3)(*[w.data_ptr() for w in weights])
+    arr_r = (ctypes.c_int64 * 3)(*[w.shape[0] for w in weights])
+    arr_bias = (ctypes.c_void_p * 3)(*[None if b is None else b.data_ptr() for b in bs])
+    arr_c = (ctypes.c_void_p * 3)(*[o.data_ptr() for o in outs])
+    arr_ld = (ctypes.c_int64 * 3)(*[o.shape[1] for o in outs])
+    N.call('lcq_gemm_rope', N.ptr_strided(x2), N.dt(x2), x2.stride(0), M, K, n, arr_b, arr_r,
+           _wstride(weights), arr_bias, arr_c, arr_ld, int(rope_segs), N.ptr(cos), N.ptr(sin),
+           S, 0 if cos.shape[0] == 1 else S * 128, 128, N.stream_of(x2))
+    Ntot = sum(w.shape[0] for w in weights)
+    N.note_work('lcq_gemm_rope', 2.0 * M * K * Ntot)
+    N.note_bytes('lcq_gemm_rope', 2.0 * (M * K + Ntot * K + M * Ntot + 2 * cos.numel()))
+    return [o.view(B, S, o.shape[1]) for o in outs]
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:

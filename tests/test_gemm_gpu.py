@@ -110,6 +110,65 @@ def test_linear_multi_segments_from_one_buffer():
     assert torch.equal(torch.cat(outs, dim=1).view(torch.int16), full.view(torch.int16))
 
 
+def _rope_tables(B, S, g):
+    """HF-style cos / sin [B or 1, S, 128] (emb = cat(freqs, freqs), positions per sample)."""
+    inv = 1.0 / (500000.0 ** (torch.arange(0, 128, 2, device=DEV).float() / 128))
+    pos = torch.arange(S, device=DEV).float()[None, :] + (
+        torch.randint(0, 50, (B, 1), generator=g, device=DEV).float())
+    fr = pos[..., None] * inv[None, None, :]
+    emb = torch.cat([fr, fr], -1)
+    return emb.cos().to(torch.bfloat16), emb.sin().to(torch.bfloat16)
+
+
+@pytest.mark.parametrize('B,S,shared', [(2, 300, True), (3, 128, False), (1, 2048, True),
+                                        (4, 77, False)])
+def test_linear_multi_rope_equals_gemm_then_rotary(B, S, shared):
+    """lcq_gemm_rope (q / k rotated in the GEMM epilogue) equals lcq_gemm followed by
+    lcq_rotary bit for bit: shared ([1, S, 128]) and per-sample ([B, S, 128]) cos / sin,
+    ragged row counts (B * S not a multiple of 256), a bias on k."""
+    g = torch.Generator(device=DEV).manual_seed(11 + S)
+    x = torch.randn(B, S, 512, generator=g, device=DEV).to(torch.bfloat16)
+    ws = [(torch.randn(n, 512, generator=g, device=DEV) * 0.05).to(torch.bfloat16)
+          for n in (512, 256, 256)]
+    bs = [None, torch.randn(256, generator=g, device=DEV).to(torch.bfloat16), None]
+    cos, sin = _rope_tables(B, S, g)
+    if shared:
+        cos, sin = cos[:1].contiguous(), sin[:1].contiguous()
+    q, k, v = ops.linear_multi_rope(x, ws, bs, cos, sin, rope_segs=2)
+    q0, k0, v0 = ops.linear_multi(x, ws, bs)
+    qh = q0.view(B, S, 4, 128).transpose(1, 2)
+    kh = k0.view(B, S, 2, 128).transpose(1, 2)
+    qr, kr = ops.rotary(qh, kh, cos, sin)
+    for a, b in ((q, qr.transpose(1, 2).reshape(B, S, 512)),
+                 (k, kr.transpose(1, 2).reshape(B, S, 256)), (v, v0)):
+        assert torch.equal(a.view(torch.int16), b.reshape(a.shape).view(torch.int16))
+
+
+def test_attention_core_rope_fused_equals_unfused(monkeypatch):
+    """LlamaAttention up to o_proj (llama._attn_core) with the rotary in the q/k/v GEMM
+    epilogue equals the path through apply_rotary_pos_emb (lcq_rotary) bit for bit."""
+    from transformers import LlamaConfig
+    from transformers.models.llama.modeling_llama import LlamaAttention, LlamaRotaryEmbedding
+
+    from lightcompress_amd import llama
+    cfg = LlamaConfig(hidden_size=512, num_attention_heads=4, num_key_value_heads=2,
+                      head_dim=128, intermediate_size=1024)
+    cfg._attn_implementation = 'sdpa'
+    torch.manual_seed(0)
+    attn = LlamaAttention(cfg, 0).to(DEV, torch.bfloat16).eval()
+    llama.install_fused_forward(attn)   # the lcq rotary / attention patches
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(2, 256, 512, generator=g, device=DEV).to(torch.bfloat16)
+    rot = LlamaRotaryEmbedding(cfg).to(DEV)
+    pe = rot(x, torch.arange(256, device=DEV)[None].expand(2, -1))
+    fused = llama._attn_core(attn, x, pe, None)
+    calls = []
+    monkeypatch.setattr(llama, '_rope_fusable', lambda *a: calls.append(1) or False)
+    plain = llama._attn_core(attn, x, pe, None)
+    assert calls, 'the unfused path was not taken'
+    assert torch.equal(fused.view(torch.int16), plain.view(torch.int16))
+
+
 @pytest.mark.parametrize('M,I,K', [(512, 1024, 256), (300, 272, 512), (4096, 512, 4096)])
 def test_linear_silu_mul_exact(M, I, K):
     g = torch.Generator(device=DEV).manual_seed(M + I)
