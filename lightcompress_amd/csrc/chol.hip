@@ -372,11 +372,33 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
 #pragma unroll
         for (int c = 0; c < JROW / 4; ++c) jrow[c] = jr[c];
       }
-      for (int t = w; t < njobs; t += 3) {
-        float* blk = t < nL ? sm + OFF_A + tix(p + 1 + t, p) * TF
-                            : sm + OFF_R + tix(p, t - nL) * TF;
-        st4(blk, lane, mma16(v4f{0.f, 0.f, 0.f, 0.f}, zt, ld4(blk, lane)));
-        if (t >= nL && !vec) store_x(p, t - nL, blk);
+      // S2 jobs t = w, w + 3, w + 6 (njobs <= 8, wave 0 has t = 0): all operands read first,
+      // the three 4-MFMA chains interleaved, then the stores
+      {
+        float* blk[3];
+        v4f b[3], o[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int t = w + 3 * u;
+          blk[u] = t >= njobs ? sm + OFF_SCR
+                   : t < nL   ? sm + OFF_A + tix(p + 1 + t, p) * TF
+                              : sm + OFF_R + tix(p, t - nL) * TF;
+          b[u] = ld4(blk[u], lane);
+          o[u] = v4f{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+          for (int u = 0; u < 3; ++u)
+            o[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(zt[st], b[u][st], o[u], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int t = w + 3 * u;
+          if (t < njobs) {
+            st4(blk[u], lane, o[u]);
+            if (t >= nL && !vec) store_x(p, t - nL, blk[u]);
+          }
+        }
       }
       if (!vec)
         for (int k = p + w; k < ntl; k += 3)   // X_pk = 0 above the diagonal (k = p+1 ..)
