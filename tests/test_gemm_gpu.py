@@ -120,18 +120,21 @@ def _rope_tables(B, S, g):
     return emb.cos().to(torch.bfloat16), emb.sin().to(torch.bfloat16)
 
 
-@pytest.mark.parametrize('B,S,shared', [(2, 300, True), (3, 128, False), (1, 2048, True),
-                                        (4, 77, False)])
-def test_linear_multi_rope_equals_gemm_then_rotary(B, S, shared):
+@pytest.mark.parametrize('B,S,shared,dt', [(2, 300, True, torch.bfloat16),
+                                           (3, 128, False, torch.bfloat16),
+                                           (1, 2048, True, torch.bfloat16),
+                                           (4, 77, False, torch.bfloat16),
+                                           (2, 200, False, torch.float16)])
+def test_linear_multi_rope_equals_gemm_then_rotary(B, S, shared, dt):
     """lcq_gemm_rope (q / k rotated in the GEMM epilogue) equals lcq_gemm followed by
     lcq_rotary bit for bit: shared ([1, S, 128]) and per-sample ([B, S, 128]) cos / sin,
-    ragged row counts (B * S not a multiple of 256), a bias on k."""
+    ragged row counts (B * S not a multiple of 256), a bias on k, bf16 and fp16."""
     g = torch.Generator(device=DEV).manual_seed(11 + S)
-    x = torch.randn(B, S, 512, generator=g, device=DEV).to(torch.bfloat16)
-    ws = [(torch.randn(n, 512, generator=g, device=DEV) * 0.05).to(torch.bfloat16)
-          for n in (512, 256, 256)]
-    bs = [None, torch.randn(256, generator=g, device=DEV).to(torch.bfloat16), None]
+    x = torch.randn(B, S, 512, generator=g, device=DEV).to(dt)
+    ws = [(torch.randn(n, 512, generator=g, device=DEV) * 0.05).to(dt) for n in (512, 256, 256)]
+    bs = [None, torch.randn(256, generator=g, device=DEV).to(dt), None]
     cos, sin = _rope_tables(B, S, g)
+    cos, sin = cos.to(dt), sin.to(dt)
     if shared:
         cos, sin = cos[:1].contiguous(), sin[:1].contiguous()
     q, k, v = ops.linear_multi_rope(x, ws, bs, cos, sin, rope_segs=2)
