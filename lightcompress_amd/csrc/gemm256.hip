@@ -55,7 +55,7 @@ constexpr int SKT = 64;            // K-tile
 constexpr int HALF_B = 16384;      // 128 rows x 64 k x 2 B
 constexpr int BUF_B = 4 * HALF_B;  // A_lo, A_hi, B_lo, B_hi
 enum { H_ALO = 0, H_AHI = 1, H_BLO = 2, H_BHI = 3 };
-enum { EPI_STORE = 0, EPI_SILU = 1, EPI_SQDIFF = 2, EPI_RESID = 3, EPI_ROPE = 4 };
+enum { EPI_STORE = 0, EPI_SILU = 1, EPI_SQDIFF = 2, EPI_RESID = 3, EPI_ROPE = 4, EPI_F32 = 5 };
 constexpr int MAXSEG = 3;
 
 struct Args {
@@ -82,6 +82,8 @@ struct Args {
   const uint16_t* sin;
   int64_t seq, cs_bstride;
   int rope_segs;
+  // EPI_F32: c[0] is fp32, c = beta c + alpha acc (beta 0 never reads c)
+  float alpha, beta;
 };
 
 // work slot -> tile (4 x 8 blocks of tiles, bands of 4 tile rows walked along N)
@@ -322,6 +324,39 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][NB], int tm, 
   constexpr int NH = NB / 2;
   const int fr = lane & 15, fq = lane >> 4;
   const int poff = (fq & 1) * 16 + (fq >> 1) * 8;  // pair16 column offset of this lane
+  if constexpr (EPI == EPI_F32) {
+    // 4 consecutive fp32 columns per lane and block: one 16-B store (n % 4 == 0, ldc % 4 == 0)
+    const int64_t col0 = (int64_t)tn * ST + wc * (NB * 16) + fq * 4;
+    const bool full_n = (int64_t)tn * ST + ST <= a.n;
+    float* cb = reinterpret_cast<float*>(a.c[0]);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
+      if (trow >= a.m) break;
+      float* crow = cb + trow * a.ldc[0] + col0;
+      float4 cv[NB];
+      if (a.beta != 0.f) {
+#pragma unroll
+        for (int n = 0; n < NB; ++n)
+          cv[n] = (full_n || col0 + n * 16 < a.n) ? *reinterpret_cast<const float4*>(crow + n * 16)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        if (!full_n && col0 + n * 16 >= a.n) break;
+        float4 o = make_float4(a.alpha * acc[m][n][0], a.alpha * acc[m][n][1],
+                               a.alpha * acc[m][n][2], a.alpha * acc[m][n][3]);
+        if (a.beta != 0.f) {
+          o.x = __fadd_rn(a.beta * cv[n].x, o.x);
+          o.y = __fadd_rn(a.beta * cv[n].y, o.y);
+          o.z = __fadd_rn(a.beta * cv[n].z, o.z);
+          o.w = __fadd_rn(a.beta * cv[n].w, o.w);
+        }
+        *reinterpret_cast<float4*>(crow + n * 16) = o;
+      }
+    }
+    return;
+  }
   if constexpr (EPI == EPI_SILU) {
     const int64_t col0 = (int64_t)tn * 128 + wc * (NB * 8) + fq * 4;
     const bool wide = a.wide && (int64_t)tn * 128 + 128 <= a.n;
@@ -764,6 +799,101 @@ static int check_common(int dtype, const void* x, int64_t lda, int64_t m, int64_
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------------------
+// fp32 products as bf16 MFMA (the factorisation chain's large updates, lcq_gemm_f32x6):
+// fp32 MFMA runs at 1/16 of the bf16 rate on gfx950. Each fp32 operand value is split into
+// three bf16 planes x = x0 + x1 + x2 (x0 = RN(x), x1 = RN(x - x0), x2 = RN(x - x0 - x1): ~24
+// significant bits), and the six plane products down to the 2^-16 level,
+//   a2 b0 + a1 b1 + a0 b2 + a1 b0 + a0 b1 + a0 b0   (small terms first),
+// are ONE k_gemm16h GEMM over K' = 6 Kp with fp32 accumulation: A' = [a2 a1 a0 a1 a0 a0],
+// B' = [b0 b1 b2 b0 b1 b0] along k (Kp = K rounded up to 64, zero padded). Dropped terms are
+// O(2^-24) relative, like fp32 rounding (scripts/chain_split_study.py: the chain's inverse
+// factor is as accurate as with the fp32 GEMM).
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t ROLES_A = 2u | 1u << 2 | 0u << 4 | 1u << 6 | 0u << 8 | 0u << 10;
+constexpr uint32_t ROLES_B = 0u | 1u << 2 | 2u << 4 | 0u << 6 | 1u << 8 | 0u << 10;
+
+__device__ __forceinline__ void split3(float x, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
+  const float h0 = bf16_rne_hw(x);
+  const float r1 = x - h0;            // exact
+  const float h1 = bf16_rne_hw(r1);
+  const float h2 = bf16_rne_hw(r1 - h1);
+  p0 = (uint16_t)(__float_as_uint(h0) >> 16);
+  p1 = (uint16_t)(__float_as_uint(h1) >> 16);
+  p2 = (uint16_t)(__float_as_uint(h2) >> 16);
+}
+
+// 8 consecutive k of one row -> the six segments of dst (16 B each)
+__device__ __forceinline__ void put_split8(const float (&v)[8], uint16_t* drow, int64_t kp,
+                                           uint32_t roles) {
+  uint16_t p[3][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) split3(v[j], p[0][j], p[1][j], p[2][j]);
+  uint4 q[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    q[i] = make_uint4((uint32_t)p[i][0] | (uint32_t)p[i][1] << 16,
+                      (uint32_t)p[i][2] | (uint32_t)p[i][3] << 16,
+                      (uint32_t)p[i][4] | (uint32_t)p[i][5] << 16,
+                      (uint32_t)p[i][6] | (uint32_t)p[i][7] << 16);
+#pragma unroll
+  for (int sgm = 0; sgm < 6; ++sgm) {
+    const uint32_t r = (roles >> (2 * sgm)) & 3u;
+    *reinterpret_cast<uint4*>(drow + sgm * kp) = r == 0 ? q[0] : (r == 1 ? q[1] : q[2]);
+  }
+}
+
+// row-major source: element (r, k) at src[r * ld + k]; one thread per (row, 8 k)
+__global__ void __launch_bounds__(256) k_split6(const float* src, int64_t ld, int64_t rows,
+                                                int64_t k, int64_t kp, uint32_t roles,
+                                                uint16_t* dst, int64_t ldd) {
+  const int64_t g8 = kp / 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * g8) return;
+  const int64_t r = i / g8, k0 = (i - r * g8) * 8;
+  const float* s = src + r * ld + k0;
+  float v[8];
+  if (k0 + 8 <= k && (ld & 3) == 0 && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
+    const float4 a = *reinterpret_cast<const float4*>(s);
+    const float4 b = *reinterpret_cast<const float4*>(s + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = k0 + j < k ? s[j] : 0.f;
+  }
+  put_split8(v, dst + r * ldd + k0, kp, roles);
+}
+
+// transposed source: element (r, k) at src[k * ld + r]; a 64 (r) x 64 (k) tile per workgroup
+// through LDS (coalesced reads along r, 16-B segment writes along k)
+__global__ void __launch_bounds__(256) k_split6_t(const float* src, int64_t ld, int64_t rows,
+                                                  int64_t k, int64_t kp, uint32_t roles,
+                                                  uint16_t* dst, int64_t ldd) {
+  __shared__ float t[64][65];
+  const int64_t r0 = (int64_t)blockIdx.x * 64, k0 = (int64_t)blockIdx.y * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int kk = i * 4 + (tid >> 6), rr = tid & 63;
+    const int64_t gk = k0 + kk, gr = r0 + rr;
+    t[kk][rr] = (gk < k && gr < rows) ? src[gk * ld + gr] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int task = h * 256 + tid;
+    const int rr = task & 63, kg = task >> 6;  // kg 0..7: k 8 kg .. 8 kg + 7
+    const int64_t gr = r0 + rr, gk = k0 + kg * 8;
+    if (gr >= rows || gk >= kp) continue;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t[kg * 8 + j][rr];
+    put_split8(v, dst + gr * ldd + gk, kp, roles);
+  }
+}
+
 }  // namespace g256
 
 }  // namespace lcq
@@ -926,4 +1056,60 @@ extern "C" int lcq_gemm_sq_diff(const void* a, int dtype, int64_t lda, int64_t m
   hipLaunchKernelGGL(k_loss_reduce, 1, 1024, 0, st, g.part, (int64_t)g.n_mt * g.n_nt * 4, m * n,
                      reinterpret_cast<float*>(out_f32), slot);
   return check_launch("lcq_gemm_sq_diff: reduce");
+}
+
+// ---- fp32 GEMM on bf16 MFMA (split planes; see k_split6) ---------------------------------
+static int64_t x6_kp(int64_t k) { return (k + SKT - 1) / SKT * SKT; }
+
+extern "C" int64_t lcq_gemm_f32x6_workspace_bytes(int64_t rows, int64_t n, int64_t k) {
+  if (rows <= 0 || n <= 0 || k <= 0) return 0;
+  return (rows + n) * 6 * x6_kp(k) * 2 + 256;
+}
+
+extern "C" int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
+                              int64_t lda, const void* B, int64_t ldb, int bt, float beta,
+                              void* C, int64_t ldc, int64_t row0, int64_t row1, void* workspace,
+                              int64_t ws_bytes, void* stream) {
+  LCQ_REQUIRE(M > 0 && N > 0 && K > 0 && 0 <= row0 && row0 < row1 && row1 <= M,
+              "shape / row range");
+  LCQ_REQUIRE(N % 16 == 0 && ldc % 4 == 0 && ldc >= N, "N % 16 == 0, ldc % 4 == 0");
+  LCQ_REQUIRE(A && B && C && aligned16(C), "pointers (C 16-byte aligned)");
+  LCQ_REQUIRE(lda >= K && (bt ? ldb >= K : ldb >= N), "leading dimensions");
+  const int64_t kp = x6_kp(K), rows = row1 - row0;
+  LCQ_REQUIRE(6 * kp < ((int64_t)1 << 21), "K too large for 32-bit panel offsets");
+  LCQ_REQUIRE(workspace && aligned16(workspace) &&
+                  ws_bytes >= lcq_gemm_f32x6_workspace_bytes(rows, N, K),
+              "workspace smaller than lcq_gemm_f32x6_workspace_bytes");
+  hipStream_t st = as_stream(stream);
+  const int64_t ldd = 6 * kp;
+  uint16_t* ap = reinterpret_cast<uint16_t*>(workspace);
+  uint16_t* bp = ap + rows * ldd;
+  const float* a32 = reinterpret_cast<const float*>(A) + row0 * lda;
+  const float* b32 = reinterpret_cast<const float*>(B);
+  {
+    const int64_t items = rows * (kp / 8);
+    hipLaunchKernelGGL(k_split6, dim3((unsigned)((items + 255) / 256)), 256, 0, st, a32, lda,
+                       rows, K, kp, ROLES_A, ap, ldd);
+  }
+  if (bt) {
+    const int64_t items = N * (kp / 8);
+    hipLaunchKernelGGL(k_split6, dim3((unsigned)((items + 255) / 256)), 256, 0, st, b32, ldb, N,
+                       K, kp, ROLES_B, bp, ldd);
+  } else {
+    hipLaunchKernelGGL(k_split6_t, dim3((unsigned)((N + 63) / 64), (unsigned)((kp + 63) / 64)),
+                       256, 0, st, b32, ldb, N, K, kp, ROLES_B, bp, ldd);
+  }
+  int rc = check_launch("lcq_gemm_f32x6: split");
+  if (rc) return rc;
+  Args g{};
+  g.a = ap;
+  g.lda = ldd; g.m = rows; g.k = ldd; g.ldb = ldd; g.n = N; g.nseg = 1;
+  g.b[0] = bp;
+  g.bend[0] = N;
+  g.c[0] = reinterpret_cast<uint16_t*>(reinterpret_cast<float*>(C) + row0 * ldc);
+  g.ldc[0] = ldc;
+  g.alpha = alpha;
+  g.beta = beta;
+  plan(g, ST);
+  return launch<LCQ_BF16, EPI_F32>(g, st);
 }

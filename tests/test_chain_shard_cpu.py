@@ -4,9 +4,11 @@ unsharded chain bit for bit. The device kernels are replaced by CPU stand-ins wh
 output row is independent of the row range asked for (a full-shape fp64 product, rows taken
 from it), the property lcq_gemm_f32_rows gives on the GPU (tests/test_multirank_gpu.py checks
 the kernels themselves)."""
+import functools
 import sys
 from pathlib import Path
 
+import pytest
 import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parent))
@@ -31,6 +33,8 @@ def _cpu_kernels():
     ops.gemm_f32 = lambda A, B, out, alpha=1.0, beta=0.0, b_trans=False: rows(
         A, B, out, alpha, beta, b_trans, 0, A.shape[0])
     ops.gemm_f32_rows = rows
+    ops.gemm_f32x6 = lambda A, B, out, alpha, beta, b_trans, r0=0, r1=None: rows(
+        A, B, out, alpha, beta, b_trans, r0, A.shape[0] if r1 is None else r1)
     ops.gemm_f32_row_unit = lambda m, n: 64
     ops.chol_inv_tile = tile
 
@@ -43,19 +47,21 @@ def _H(n):
     return H
 
 
-def _chain(rank, world, n=640):
-    from lightcompress_amd import gptq_core
+def _chain(rank, world, n=640, x6_tiles=10 ** 9):
+    from lightcompress_amd import gptq_core, ops
     _cpu_kernels()
     gptq_core.SHARD_MIN_ROWS = 128
+    ops.X6_MIN_TILES = x6_tiles   # 1: every product routed to the split-plane entry
     with gptq_core.chain_sharding(rank, world):
         U = gptq_core.inverse_cholesky_upper(_H(n))
     return U.numpy().tobytes(), gptq_core.shard_stats['split_products']
 
 
-def test_chain_row_split_cpu_bit_identical():
-    single, split1 = run2(_chain, world=1)[0]   # in a child: the stand-ins stay out of here
+@pytest.mark.parametrize('x6_tiles', [10 ** 9, 1])
+def test_chain_row_split_cpu_bit_identical(x6_tiles):
+    single, split1 = run2(functools.partial(_chain, x6_tiles=x6_tiles), world=1)[0]   # in a child
     assert split1 == 0
-    res = run2(_chain)
+    res = run2(functools.partial(_chain, x6_tiles=x6_tiles))
     for r in (0, 1):
         u, split = res[r]
         assert split > 0

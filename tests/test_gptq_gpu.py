@@ -380,6 +380,88 @@ def test_gemm_f32_rows_match_full_plan(dev, M, N, K, bt):
         ops.gemm_f32_rows(A, B, parts, 0.5, 1.0, bool(bt), unit // 2, M)
 
 
+@pytest.mark.parametrize('M,N,K', [(1000, 384, 517), (2048, 1536, 2048), (300, 96, 64),
+                                   (3584, 1792, 1792)])
+@pytest.mark.parametrize('bt', [False, True])
+def test_gemm_f32x6(dev, M, N, K, bt):
+    """lcq_gemm_f32x6 (fp32 product on bf16 MFMA over split planes): C = beta C + alpha A op(B)
+    on strided fp32 views (ragged K padded to 64, transposed and K-major B), against fp64 with
+    the same elementwise bound as test_gemm_f32; beta 0 ignores a NaN-filled C; its error is
+    within 2x the fp32 kernel's on the same product."""
+    from lightcompress_amd import ops
+    g = torch.Generator().manual_seed(M * 5 + N + K)
+    big_a = torch.randn(M + 3, K + 5, generator=g)
+    big_b = torch.randn((N + 2, K + 3) if bt else (K + 2, N + 4), generator=g)
+    A = big_a[1:M + 1, 1:K + 1]
+    B = big_b[:N, 2:K + 2] if bt else big_b[2:K + 2, :N]
+    C0 = torch.randn(M, N, generator=g)
+    ref_p = A.double() @ (B.double().t() if bt else B.double())
+    Ad = big_a.to(dev)[1:M + 1, 1:K + 1]
+    Bd = big_b.to(dev)[:N, 2:K + 2] if bt else big_b.to(dev)[2:K + 2, :N]
+    bound_p = A.double().abs() @ (B.double().abs().t() if bt else B.double().abs())
+    for alpha, beta in ((1.0, 0.0), (-1.0, 1.0), (0.5, 2.0)):
+        ref = alpha * ref_p + (beta * C0.double() if beta else 0)
+        bound = abs(alpha) * bound_p + abs(beta) * C0.double().abs() + 1e-30
+        Cd = C0.to(dev).clone()
+        if beta == 0.0:
+            Cd.fill_(float('nan'))
+        ops.gemm_f32x6(Ad, Bd, Cd, alpha, beta, bt)
+        err6 = ((Cd.cpu().double() - ref).abs() / bound).max().item()
+        Cf = C0.to(dev).clone()
+        ops.gemm_f32(Ad, Bd, Cf, alpha, beta, b_trans=bt)
+        err32 = ((Cf.cpu().double() - ref).abs() / bound).max().item()
+        assert err6 < 2e-6 and err6 <= 2 * err32 + 1e-7, (alpha, beta, err6, err32)
+
+
+@pytest.mark.parametrize('bt', [False, True])
+def test_gemm_f32x6_rows_match_full(dev, bt):
+    """Row ranges of lcq_gemm_f32x6 (as a token-sharded chain cuts them) assembled equal the
+    whole product bit for bit."""
+    from lightcompress_amd import ops
+    M, N, K = 3584, 1792, 1792
+    g = torch.Generator(device=dev).manual_seed(17)
+    A = torch.randn(M, K, generator=g, device=dev)
+    B = torch.randn((N, K) if bt else (K, N), generator=g, device=dev)
+    C0 = torch.randn(M, N, generator=g, device=dev)
+    full = ops.gemm_f32x6(A, B, C0.clone(), -1.0, 1.0, bt)
+    parts = C0.clone()
+    cuts = [0, 128, 1792, 1920, M]
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        ops.gemm_f32x6(A, B, parts, -1.0, 1.0, bt, r0, r1)
+    assert torch.equal(parts, full)
+
+
+def test_inverse_cholesky_x6_vs_fp32_products(dev, monkeypatch):
+    """The chain with its large products on lcq_gemm_f32x6 (n 8192: the 4096 x 2048 updates
+    go there) is as accurate as with every product on the fp32 kernels, against fp64."""
+    from lightcompress_amd import gptq_core, ops
+    n = 8192
+    g = torch.Generator(device=dev).manual_seed(3)
+    mag = torch.exp(torch.randn(n, generator=g, device=dev))
+    X = torch.randn(2 * n, n, generator=g, device=dev) * mag
+    H = X.T @ X / (2 * n)
+    H.diagonal().add_(0.01 * H.diagonal().mean())
+    Hd = H.double()
+    ref = torch.linalg.cholesky(torch.cholesky_inverse(torch.linalg.cholesky(Hd)),
+                                upper=True).cpu()
+    monkeypatch.setattr(gptq_core, 'CHAIN_GRAPHS', False)
+    errs = {}
+    for x6 in (True, False):
+        monkeypatch.setattr(ops, 'X6', x6)
+        calls = [0]
+        orig = ops.gemm_f32x6
+
+        def spy(*a, **k):
+            calls[0] += 1
+            return orig(*a, **k)
+        monkeypatch.setattr(ops, 'gemm_f32x6', spy)
+        U = gptq_core.inverse_cholesky_upper(H.clone()).double().cpu()
+        monkeypatch.setattr(ops, 'gemm_f32x6', orig)
+        assert (calls[0] > 0) == x6
+        errs[x6] = ((U - ref).norm() / ref.norm()).item()
+    assert errs[True] <= 1.5 * errs[False] + 1e-7, errs
+
+
 def test_inverse_cholesky_not_pd(dev):
     from lightcompress_amd import gptq_core
     H = torch.eye(256, device=dev)
