@@ -82,8 +82,12 @@ struct Args {
   const uint16_t* sin;
   int64_t seq, cs_bstride;
   int rope_segs;
-  // EPI_F32: c[0] is fp32, c = beta c + alpha acc (beta 0 never reads c)
+  // EPI_F32: c[0] is fp32, c = beta c + alpha acc (beta 0 never reads c); the K loop walks 6
+  // segments of x6_kt K-tiles, segment s reading plane (x6_roles_* >> 2 s) & 3 of the
+  // [rows][3][x6_kp] split operands (lcq_gemm_f32x6)
   float alpha, beta;
+  int x6_kt, x6_kp;
+  uint32_t x6_roles_a, x6_roles_b;
 };
 
 // work slot -> tile (4 x 8 blocks of tiles, bands of 4 tile rows walked along N)
@@ -631,8 +635,8 @@ __device__ __forceinline__ void lgkm_barrier() {
 template <bool FP16>
 __device__ __forceinline__ void ktile16h(v4f (&acc)[8][8], v8s (&x0a)[8], v8s (&x0b)[8],
                                          v8s (&x1a)[8], v8s (&x1b)[8], const Stage4& st,
-                                         int kofs, char* bc, const char* bn, int w, int wr,
-                                         int wc, int lane) {
+                                         int kofs, int kofs_b, char* bc, const char* bn, int w,
+                                         int wr, int wc, int lane) {
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -651,8 +655,8 @@ __device__ __forceinline__ void ktile16h(v4f (&acc)[8][8], v8s (&x0a)[8], v8s (&
     }
     if (i == 50) lgkm_barrier();
     if (i == 52 || i == 55 || i == 58) load_a(st, bc, kofs, w, 5 + (i - 52) / 3);
-    if (i == 61 || i == 64) load_b(st, bc, kofs, w, (i - 61) / 3);
-    if (i == 85 || i == 87 || i == 89) load_b(st, bc, kofs, w, 2 + (i - 85) / 2);
+    if (i == 61 || i == 64) load_b(st, bc, kofs_b, w, (i - 61) / 3);
+    if (i == 85 || i == 87 || i == 89) load_b(st, bc, kofs_b, w, 2 + (i - 85) / 2);
     if (i == 91) {
       asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -660,8 +664,8 @@ __device__ __forceinline__ void ktile16h(v4f (&acc)[8][8], v8s (&x0a)[8], v8s (&
     if (i >= 93 && i <= 100) x0a[i - 93] = read_frag(bn, wr * 8 + (i - 93), 0, lane);
     if (i >= 101 && i <= 115 && ((i - 101) & 1) == 0)
       x0b[(i - 101) >> 1] = read_frag(bn + TILE_B, wc * 8 + ((i - 101) >> 1), 0, lane);
-    if (i == 96 || i == 100) load_b(st, bc, kofs, w, 5 + (i - 96) / 4);
-    if (i == 124) load_b(st, bc, kofs, w, 7);
+    if (i == 96 || i == 100) load_b(st, bc, kofs_b, w, 5 + (i - 96) / 4);
+    if (i == 124) load_b(st, bc, kofs_b, w, 7);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -690,15 +694,26 @@ __global__ void __launch_bounds__(256, 1) k_gemm16h(Args a) {
 #pragma unroll
     for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
   v8s x0a[8], x0b[8], x1a[8], x1b[8];
-  const int k1 = nk > 1 ? SKT * 2 : 0;
+  // byte offset of K-tile kt in the A / B rows (EPI_F32: its segment's plane)
+  auto kofs_of = [&](int kt, uint32_t roles) -> int {
+    if constexpr (EPI == EPI_F32) {
+      const int sgm = kt / a.x6_kt;
+      const int p = (int)((roles >> (2 * sgm)) & 3u);
+      return (p * a.x6_kp + (kt - sgm * a.x6_kt) * SKT) * 2;
+    } else {
+      (void)roles;
+      return kt * (SKT * 2);
+    }
+  };
+  const int k1 = nk > 1 ? 1 : 0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) load_a(st, lds, 0, w, j);
+  for (int j = 0; j < 8; ++j) load_a(st, lds, kofs_of(0, a.x6_roles_a), w, j);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) load_b(st, lds, 0, w, j);
+  for (int j = 0; j < 8; ++j) load_b(st, lds, kofs_of(0, a.x6_roles_b), w, j);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) load_a(st, lds + BUF4, k1, w, j);
+  for (int j = 0; j < 8; ++j) load_a(st, lds + BUF4, kofs_of(k1, a.x6_roles_a), w, j);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) load_b(st, lds + BUF4, k1, w, j);
+  for (int j = 0; j < 8; ++j) load_b(st, lds + BUF4, kofs_of(k1, a.x6_roles_b), w, j);
   wait_barrier<16>();  // K-tile 0 landed (K-tile 1's 16 pieces may be in flight)
 #pragma unroll
   for (int m = 0; m < 8; ++m) x0a[m] = read_frag(lds, wr * 8 + m, 0, lane);
@@ -707,9 +722,10 @@ __global__ void __launch_bounds__(256, 1) k_gemm16h(Args a) {
   asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
   for (int64_t t = 0; t < nk; ++t) {
     const int cur = (int)(t & 1);
-    const int64_t kt2 = t + 2 < nk ? t + 2 : nk - 1;
-    ktile16h<FP16>(acc, x0a, x0b, x1a, x1b, st, (int)(kt2 * (SKT * 2)), lds + cur * BUF4,
-                   lds + (cur ^ 1) * BUF4, w, wr, wc, lane);
+    const int kt2 = (int)(t + 2 < nk ? t + 2 : nk - 1);
+    ktile16h<FP16>(acc, x0a, x0b, x1a, x1b, st, kofs_of(kt2, a.x6_roles_a),
+                   kofs_of(kt2, a.x6_roles_b), lds + cur * BUF4, lds + (cur ^ 1) * BUF4, w, wr,
+                   wc, lane);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 7"
                : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]),
@@ -806,8 +822,9 @@ static int check_common(int dtype, const void* x, int64_t lda, int64_t m, int64_
 // three bf16 planes x = x0 + x1 + x2 (x0 = RN(x), x1 = RN(x - x0), x2 = RN(x - x0 - x1): ~24
 // significant bits), and the six plane products down to the 2^-16 level,
 //   a2 b0 + a1 b1 + a0 b2 + a1 b0 + a0 b1 + a0 b0   (small terms first),
-// are ONE k_gemm16h GEMM over K' = 6 Kp with fp32 accumulation: A' = [a2 a1 a0 a1 a0 a0],
-// B' = [b0 b1 b2 b0 b1 b0] along k (Kp = K rounded up to 64, zero padded). Dropped terms are
+// are ONE k_gemm16h GEMM over K' = 6 Kp with fp32 accumulation: its K loop walks six segments,
+// reading planes (2 1 0 1 0 0) of A and (0 1 2 0 1 0) of B, stored once per row as
+// [plane][Kp] (Kp = K rounded up to 64, zero padded; ROLES_*). Dropped terms are
 // O(2^-24) relative, like fp32 rounding (scripts/chain_split_study.py: the chain's inverse
 // factor is as accurate as with the fp32 GEMM).
 // ---------------------------------------------------------------------------------------
@@ -824,9 +841,8 @@ __device__ __forceinline__ void split3(float x, uint16_t& p0, uint16_t& p1, uint
   p2 = (uint16_t)(__float_as_uint(h2) >> 16);
 }
 
-// 8 consecutive k of one row -> the six segments of dst (16 B each)
-__device__ __forceinline__ void put_split8(const float (&v)[8], uint16_t* drow, int64_t kp,
-                                           uint32_t roles) {
+// 8 consecutive k of one row -> its three planes in dst (16 B each, kp apart)
+__device__ __forceinline__ void put_split8(const float (&v)[8], uint16_t* drow, int64_t kp) {
   uint16_t p[3][8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) split3(v[j], p[0][j], p[1][j], p[2][j]);
@@ -838,16 +854,13 @@ __device__ __forceinline__ void put_split8(const float (&v)[8], uint16_t* drow, 
                       (uint32_t)p[i][4] | (uint32_t)p[i][5] << 16,
                       (uint32_t)p[i][6] | (uint32_t)p[i][7] << 16);
 #pragma unroll
-  for (int sgm = 0; sgm < 6; ++sgm) {
-    const uint32_t r = (roles >> (2 * sgm)) & 3u;
-    *reinterpret_cast<uint4*>(drow + sgm * kp) = r == 0 ? q[0] : (r == 1 ? q[1] : q[2]);
-  }
+  for (int i = 0; i < 3; ++i) *reinterpret_cast<uint4*>(drow + i * kp) = q[i];
 }
 
 // row-major source: element (r, k) at src[r * ld + k]; one thread per (row, 8 k)
-__global__ void __launch_bounds__(256) k_split6(const float* src, int64_t ld, int64_t rows,
-                                                int64_t k, int64_t kp, uint32_t roles,
-                                                uint16_t* dst, int64_t ldd) {
+__global__ void __launch_bounds__(256) k_split3(const float* src, int64_t ld, int64_t rows,
+                                                int64_t k, int64_t kp, uint16_t* dst,
+                                                int64_t ldd) {
   const int64_t g8 = kp / 8;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * g8) return;
@@ -863,34 +876,40 @@ __global__ void __launch_bounds__(256) k_split6(const float* src, int64_t ld, in
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = k0 + j < k ? s[j] : 0.f;
   }
-  put_split8(v, dst + r * ldd + k0, kp, roles);
+  put_split8(v, dst + r * ldd + k0, kp);
 }
 
 // transposed source: element (r, k) at src[k * ld + r]; a 64 (r) x 64 (k) tile per workgroup
 // through LDS (coalesced reads along r, 16-B segment writes along k)
-__global__ void __launch_bounds__(256) k_split6_t(const float* src, int64_t ld, int64_t rows,
-                                                  int64_t k, int64_t kp, uint32_t roles,
-                                                  uint16_t* dst, int64_t ldd) {
+__global__ void __launch_bounds__(256) k_split3_t(const float* src, int64_t ld, int64_t rows,
+                                                  int64_t k, int64_t kp, uint16_t* dst,
+                                                  int64_t ldd) {
   __shared__ float t[64][65];
   const int64_t r0 = (int64_t)blockIdx.x * 64, k0 = (int64_t)blockIdx.y * 64;
   const int tid = threadIdx.x;
+  // reads: 16 k-rows of 64 r per pass, all 16 loads issued before the LDS writes
+  float ld16[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int kk = i * 4 + (tid >> 6), rr = tid & 63;
     const int64_t gk = k0 + kk, gr = r0 + rr;
-    t[kk][rr] = (gk < k && gr < rows) ? src[gk * ld + gr] : 0.f;
+    ld16[i] = (gk < k && gr < rows) ? src[gk * ld + gr] : 0.f;
   }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i * 4 + (tid >> 6)][tid & 63] = ld16[i];
   __syncthreads();
+  // writes: 8 lanes per row cover its 64 k (128 B per plane contiguous); LDS bank of
+  // (kg, rr) = 8 kg + rr + 65 j mod 64: conflict-free over a wave
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int task = h * 256 + tid;
-    const int rr = task & 63, kg = task >> 6;  // kg 0..7: k 8 kg .. 8 kg + 7
+    const int kg = task & 7, rr = task >> 3;  // kg 0..7: k 8 kg .. 8 kg + 7
     const int64_t gr = r0 + rr, gk = k0 + kg * 8;
     if (gr >= rows || gk >= kp) continue;
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = t[kg * 8 + j][rr];
-    put_split8(v, dst + gr * ldd + gk, kp, roles);
+    put_split8(v, dst + gr * ldd + gk, kp);
   }
 }
 
@@ -1058,12 +1077,12 @@ extern "C" int lcq_gemm_sq_diff(const void* a, int dtype, int64_t lda, int64_t m
   return check_launch("lcq_gemm_sq_diff: reduce");
 }
 
-// ---- fp32 GEMM on bf16 MFMA (split planes; see k_split6) ---------------------------------
+// ---- fp32 GEMM on bf16 MFMA (split planes; see k_split3) ---------------------------------
 static int64_t x6_kp(int64_t k) { return (k + SKT - 1) / SKT * SKT; }
 
 extern "C" int64_t lcq_gemm_f32x6_workspace_bytes(int64_t rows, int64_t n, int64_t k) {
   if (rows <= 0 || n <= 0 || k <= 0) return 0;
-  return (rows + n) * 6 * x6_kp(k) * 2 + 256;
+  return (rows + n) * 3 * x6_kp(k) * 2 + 256;
 }
 
 extern "C" int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
@@ -1081,35 +1100,39 @@ extern "C" int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, cons
                   ws_bytes >= lcq_gemm_f32x6_workspace_bytes(rows, N, K),
               "workspace smaller than lcq_gemm_f32x6_workspace_bytes");
   hipStream_t st = as_stream(stream);
-  const int64_t ldd = 6 * kp;
+  const int64_t ldd = 3 * kp;  // [rows][3 planes][kp]
   uint16_t* ap = reinterpret_cast<uint16_t*>(workspace);
   uint16_t* bp = ap + rows * ldd;
   const float* a32 = reinterpret_cast<const float*>(A) + row0 * lda;
   const float* b32 = reinterpret_cast<const float*>(B);
   {
     const int64_t items = rows * (kp / 8);
-    hipLaunchKernelGGL(k_split6, dim3((unsigned)((items + 255) / 256)), 256, 0, st, a32, lda,
-                       rows, K, kp, ROLES_A, ap, ldd);
+    hipLaunchKernelGGL(k_split3, dim3((unsigned)((items + 255) / 256)), 256, 0, st, a32, lda,
+                       rows, K, kp, ap, ldd);
   }
   if (bt) {
     const int64_t items = N * (kp / 8);
-    hipLaunchKernelGGL(k_split6, dim3((unsigned)((items + 255) / 256)), 256, 0, st, b32, ldb, N,
-                       K, kp, ROLES_B, bp, ldd);
+    hipLaunchKernelGGL(k_split3, dim3((unsigned)((items + 255) / 256)), 256, 0, st, b32, ldb, N,
+                       K, kp, bp, ldd);
   } else {
-    hipLaunchKernelGGL(k_split6_t, dim3((unsigned)((N + 63) / 64), (unsigned)((kp + 63) / 64)),
-                       256, 0, st, b32, ldb, N, K, kp, ROLES_B, bp, ldd);
+    hipLaunchKernelGGL(k_split3_t, dim3((unsigned)((N + 63) / 64), (unsigned)((kp + 63) / 64)),
+                       256, 0, st, b32, ldb, N, K, kp, bp, ldd);
   }
   int rc = check_launch("lcq_gemm_f32x6: split");
   if (rc) return rc;
   Args g{};
   g.a = ap;
-  g.lda = ldd; g.m = rows; g.k = ldd; g.ldb = ldd; g.n = N; g.nseg = 1;
+  g.lda = ldd; g.m = rows; g.k = 6 * kp; g.ldb = ldd; g.n = N; g.nseg = 1;
   g.b[0] = bp;
   g.bend[0] = N;
   g.c[0] = reinterpret_cast<uint16_t*>(reinterpret_cast<float*>(C) + row0 * ldc);
   g.ldc[0] = ldc;
   g.alpha = alpha;
   g.beta = beta;
+  g.x6_kt = (int)(kp / SKT);
+  g.x6_kp = (int)kp;
+  g.x6_roles_a = ROLES_A;
+  g.x6_roles_b = ROLES_B;
   plan(g, ST);
   return launch<LCQ_BF16, EPI_F32>(g, st);
 }
