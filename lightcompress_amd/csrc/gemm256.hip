@@ -88,6 +88,10 @@ struct Args {
   float alpha, beta;
   int x6_kt, x6_kp;
   uint32_t x6_roles_a, x6_roles_b;
+  // split K (grid y = x6_splits): split y sums K-tiles [y nk / S, (y + 1) nk / S) into the fp32
+  // partial y of x6_part ([S][m][n]), folded in split order by k_x6_reduce
+  int x6_splits;
+  float* x6_part;
 };
 
 // work slot -> tile (4 x 8 blocks of tiles, bands of 4 tile rows walked along N)
@@ -332,14 +336,17 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][NB], int tm, 
     // 4 consecutive fp32 columns per lane and block: one 16-B store (n % 4 == 0, ldc % 4 == 0)
     const int64_t col0 = (int64_t)tn * ST + wc * (NB * 16) + fq * 4;
     const bool full_n = (int64_t)tn * ST + ST <= a.n;
-    float* cb = reinterpret_cast<float*>(a.c[0]);
+    const bool part = a.x6_splits > 1;
+    float* cb = part ? a.x6_part + (int64_t)blockIdx.y * a.m * a.n : reinterpret_cast<float*>(a.c[0]);
+    const int64_t ldc = part ? a.n : a.ldc[0];
+    const float alpha = part ? 1.f : a.alpha, beta = part ? 0.f : a.beta;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int64_t trow = (int64_t)tm * ST + wr * 128 + m * 16 + fr;
       if (trow >= a.m) break;
-      float* crow = cb + trow * a.ldc[0] + col0;
+      float* crow = cb + trow * ldc + col0;
       float4 cv[NB];
-      if (a.beta != 0.f) {
+      if (beta != 0.f) {
 #pragma unroll
         for (int n = 0; n < NB; ++n)
           cv[n] = (full_n || col0 + n * 16 < a.n) ? *reinterpret_cast<const float4*>(crow + n * 16)
@@ -348,13 +355,13 @@ __device__ __forceinline__ void epi16(const Args& a, v4f (&acc)[8][NB], int tm, 
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         if (!full_n && col0 + n * 16 >= a.n) break;
-        float4 o = make_float4(a.alpha * acc[m][n][0], a.alpha * acc[m][n][1],
-                               a.alpha * acc[m][n][2], a.alpha * acc[m][n][3]);
-        if (a.beta != 0.f) {
-          o.x = __fadd_rn(a.beta * cv[n].x, o.x);
-          o.y = __fadd_rn(a.beta * cv[n].y, o.y);
-          o.z = __fadd_rn(a.beta * cv[n].z, o.z);
-          o.w = __fadd_rn(a.beta * cv[n].w, o.w);
+        float4 o = make_float4(alpha * acc[m][n][0], alpha * acc[m][n][1],
+                               alpha * acc[m][n][2], alpha * acc[m][n][3]);
+        if (beta != 0.f) {
+          o.x = __fadd_rn(beta * cv[n].x, o.x);
+          o.y = __fadd_rn(beta * cv[n].y, o.y);
+          o.z = __fadd_rn(beta * cv[n].z, o.z);
+          o.w = __fadd_rn(beta * cv[n].w, o.w);
         }
         *reinterpret_cast<float4*>(crow + n * 16) = o;
       }
@@ -684,7 +691,15 @@ __global__ void __launch_bounds__(256, 1) k_gemm16h(Args a) {
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     if (!slot_tile(a, wgid, tm, tn)) return;
   }
-  const int64_t nk = a.k / SKT;
+  int64_t nk = a.k / SKT;
+  int kt0 = 0;  // first K-tile of this workgroup's split (EPI_F32 split K)
+  if constexpr (EPI == EPI_F32) {
+    if (a.x6_splits > 1) {
+      const int y = blockIdx.y;
+      kt0 = (int)(nk * y / a.x6_splits);
+      nk = nk * (y + 1) / a.x6_splits - kt0;
+    }
+  }
   Stage4 st;
   make_stage16<EPI>(a, tm, tn, w, lane, st);
 
@@ -697,6 +712,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm16h(Args a) {
   // byte offset of K-tile kt in the A / B rows (EPI_F32: its segment's plane)
   auto kofs_of = [&](int kt, uint32_t roles) -> int {
     if constexpr (EPI == EPI_F32) {
+      kt += kt0;
       const int sgm = kt / a.x6_kt;
       const int p = (int)((roles >> (2 * sgm)) & 3u);
       return (p * a.x6_kp + (kt - sgm * a.x6_kt) * SKT) * 2;
@@ -784,7 +800,8 @@ static int launch(Args& a, hipStream_t st) {
   if (gemm_kernel() == 2 && a.order == 0) {
     (void)hipFuncSetAttribute((const void*)k_gemm16h<DT, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
-    hipLaunchKernelGGL((k_gemm16h<DT, EPI>), dim3((unsigned)a.nslots), 256, 2 * BUF4, st, a);
+    const unsigned gy = (EPI == EPI_F32 && a.x6_splits > 1) ? (unsigned)a.x6_splits : 1u;
+    hipLaunchKernelGGL((k_gemm16h<DT, EPI>), dim3((unsigned)a.nslots, gy), 256, 2 * BUF4, st, a);
     return check_launch("lcq_gemm: k_gemm16h");
   }
   (void)hipFuncSetAttribute((const void*)k_gemm16b<DT, EPI>,
@@ -911,6 +928,31 @@ __global__ void __launch_bounds__(256) k_split3_t(const float* src, int64_t ld, 
     for (int j = 0; j < 8; ++j) v[j] = t[kg * 8 + j][rr];
     put_split8(v, dst + gr * ldd + gk, kp);
   }
+}
+
+
+// out = beta out + alpha (part_0 + part_1 + ...) in split order (4 columns per thread)
+__global__ void __launch_bounds__(256) k_x6_reduce(const float* part, int splits, int64_t rows,
+                                                   int64_t n, float* c, int64_t ldc,
+                                                   float alpha, float beta) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, n4 = n / 4;
+  if (i >= rows * n4) return;
+  const int64_t r = i / n4, c4 = (i - r * n4) * 4;
+  float4 acc = *reinterpret_cast<const float4*>(part + r * n + c4);
+  for (int sp = 1; sp < splits; ++sp) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (sp * rows + r) * n + c4);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  float4 o = make_float4(alpha * acc.x, alpha * acc.y, alpha * acc.z, alpha * acc.w);
+  float* cp = c + r * ldc + c4;
+  if (beta != 0.f) {
+    const float4 cv = *reinterpret_cast<const float4*>(cp);
+    o.x = __fadd_rn(beta * cv.x, o.x);
+    o.y = __fadd_rn(beta * cv.y, o.y);
+    o.z = __fadd_rn(beta * cv.z, o.z);
+    o.w = __fadd_rn(beta * cv.w, o.w);
+  }
+  *reinterpret_cast<float4*>(cp) = o;
 }
 
 }  // namespace g256
@@ -1080,9 +1122,22 @@ extern "C" int lcq_gemm_sq_diff(const void* a, int dtype, int64_t lda, int64_t m
 // ---- fp32 GEMM on bf16 MFMA (split planes; see k_split3) ---------------------------------
 static int64_t x6_kp(int64_t k) { return (k + SKT - 1) / SKT * SKT; }
 
-extern "C" int64_t lcq_gemm_f32x6_workspace_bytes(int64_t rows, int64_t n, int64_t k) {
-  if (rows <= 0 || n <= 0 || k <= 0) return 0;
-  return (rows + n) * 3 * x6_kp(k) * 2 + 256;
+// K splits of the FULL M x N x K product (so every row range of it sums the same K-tile
+// groups): enough workgroups for the 256 CUs, >= 16 K-tiles per split
+static int x6_splits(int64_t M, int64_t n, int64_t k) {
+  const int64_t tiles = ((M + ST - 1) / ST) * ((n + ST - 1) / ST);
+  int64_t sp = tiles >= 256 ? 1 : 256 / tiles;
+  const int64_t nk = 6 * x6_kp(k) / SKT;
+  if (sp > 8) sp = 8;
+  while (sp > 1 && nk / sp < 16) --sp;
+  return (int)sp;
+}
+
+extern "C" int64_t lcq_gemm_f32x6_workspace_bytes(int64_t M, int64_t rows, int64_t n,
+                                                  int64_t k) {
+  if (M <= 0 || rows <= 0 || n <= 0 || k <= 0) return 0;
+  const int sp = x6_splits(M, n, k);
+  return (rows + n) * 3 * x6_kp(k) * 2 + (sp > 1 ? sp * rows * n * 4 : 0) + 512;
 }
 
 extern "C" int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
@@ -1097,7 +1152,7 @@ extern "C" int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, cons
   const int64_t kp = x6_kp(K), rows = row1 - row0;
   LCQ_REQUIRE(6 * kp < ((int64_t)1 << 21), "K too large for 32-bit panel offsets");
   LCQ_REQUIRE(workspace && aligned16(workspace) &&
-                  ws_bytes >= lcq_gemm_f32x6_workspace_bytes(rows, N, K),
+                  ws_bytes >= lcq_gemm_f32x6_workspace_bytes(M, rows, N, K),
               "workspace smaller than lcq_gemm_f32x6_workspace_bytes");
   hipStream_t st = as_stream(stream);
   const int64_t ldd = 3 * kp;  // [rows][3 planes][kp]
@@ -1133,6 +1188,17 @@ extern "C" int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, cons
   g.x6_kp = (int)kp;
   g.x6_roles_a = ROLES_A;
   g.x6_roles_b = ROLES_B;
+  g.x6_splits = x6_splits(M, N, K);
+  if (g.x6_splits > 1) {
+    const uintptr_t pp = reinterpret_cast<uintptr_t>(bp + N * ldd);
+    g.x6_part = reinterpret_cast<float*>((pp + 255) & ~(uintptr_t)255);
+  }
   plan(g, ST);
-  return launch<LCQ_BF16, EPI_F32>(g, st);
+  rc = launch<LCQ_BF16, EPI_F32>(g, st);
+  if (rc || g.x6_splits == 1) return rc;
+  const int64_t items = rows * (N / 4);
+  hipLaunchKernelGGL(k_x6_reduce, dim3((unsigned)((items + 255) / 256)), 256, 0, st, g.x6_part,
+                     g.x6_splits, rows, N, reinterpret_cast<float*>(C) + row0 * ldc, ldc, alpha,
+                     beta);
+  return check_launch("lcq_gemm_f32x6: reduce");
 }

@@ -349,15 +349,15 @@ def gemm_f32_rows(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, alpha: fl
     return out
 
 
-X6_MIN_TILES = 96   # 256 x 256 output tiles from which the split-plane product beats fp32 MFMA
+X6_MIN_TILES = 40   # 256 x 256 output tiles from which the split-plane product beats fp32 MFMA
 
 
 def gemm_f32x6_fits(M: int, n: int, K: int, out: torch.Tensor) -> bool:
-    """Whether the M x n x K product goes to gemm_f32x6: enough 256 x 256 tiles to fill the chip
-    (scripts/chain_split_rate.py: 1.6-2x the fp32 kernel from ~100 tiles, slower on the 49-tile
-    shapes), K >= 256, n % 16 == 0 and 16-byte fp32 output rows. A function of the FULL
-    product's shape and layout, so every rank of a row-split product makes the same choice."""
-    return (X6 and -(-M // 256) * -(-n // 256) >= X6_MIN_TILES and K >= 256 and n % 16 == 0
+    """Whether the M x n x K product goes to gemm_f32x6: enough 256 x 256 tiles (with its K
+    split below 256 tiles; scripts/chain_split_rate.py, profiles/r5_chain_x6.md), K >= 1024,
+    n % 16 == 0 and 16-byte fp32 output rows. A function of the FULL product's shape and
+    layout, so every rank of a row-split product makes the same choice."""
+    return (X6 and -(-M // 256) * -(-n // 256) >= X6_MIN_TILES and K >= 1024 and n % 16 == 0
             and out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0)
 
 
@@ -377,7 +377,7 @@ def gemm_f32x6(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, alpha: float
         raise ValueError('gemm_f32x6: shape mismatch')
     if any(t.dtype != torch.float32 for t in (A, B, out)):
         raise ValueError('gemm_f32x6: fp32 operands')
-    ws_bytes = int(N.load().lcq_gemm_f32x6_workspace_bytes(row1 - row0, n_, K))
+    ws_bytes = int(N.load().lcq_gemm_f32x6_workspace_bytes(M, row1 - row0, n_, K))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=A.device)
     N.call('lcq_gemm_f32x6', M, n_, K, float(alpha), A.data_ptr(), _ld(A), B.data_ptr(), _ld(B),
            int(b_trans), float(beta), out.data_ptr(), _ld(out), int(row0), int(row1),

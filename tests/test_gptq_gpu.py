@@ -413,19 +413,20 @@ def test_gemm_f32x6(dev, M, N, K, bt):
         assert err6 < 2e-6 and err6 <= 2 * err32 + 1e-7, (alpha, beta, err6, err32)
 
 
+@pytest.mark.parametrize('M,N,K', [(3584, 1792, 1792), (1792, 1792, 7168)])
 @pytest.mark.parametrize('bt', [False, True])
-def test_gemm_f32x6_rows_match_full(dev, bt):
+def test_gemm_f32x6_rows_match_full(dev, M, N, K, bt):
     """Row ranges of lcq_gemm_f32x6 (as a token-sharded chain cuts them) assembled equal the
-    whole product bit for bit."""
+    whole product bit for bit, also where K is split (fewer than 256 tiles: the split count
+    comes from the full shape)."""
     from lightcompress_amd import ops
-    M, N, K = 3584, 1792, 1792
     g = torch.Generator(device=dev).manual_seed(17)
     A = torch.randn(M, K, generator=g, device=dev)
     B = torch.randn((N, K) if bt else (K, N), generator=g, device=dev)
     C0 = torch.randn(M, N, generator=g, device=dev)
     full = ops.gemm_f32x6(A, B, C0.clone(), -1.0, 1.0, bt)
     parts = C0.clone()
-    cuts = [0, 128, 1792, 1920, M]
+    cuts = [0, 128, M // 2, M // 2 + 128, M]
     for r0, r1 in zip(cuts[:-1], cuts[1:]):
         ops.gemm_f32x6(A, B, parts, -1.0, 1.0, bt, r0, r1)
     assert torch.equal(parts, full)
