@@ -264,14 +264,16 @@ int lcq_gemm_f32_rows(int64_t M, int64_t N, int64_t K, float alpha, const void* 
  * one k_gemm16h GEMM over K' = 6 * roundup(K, 64) with fp32 accumulation (accuracy of an fp32
  * GEMM at ~2x its rate on gfx950, where fp32 MFMA runs at 1/16 of bf16). The recursion's large
  * products (gptq_core._gemm; gptq.py:161-170). Each output element's k order is independent of
- * the row range, so a row-split product is bit-identical to the whole one. Products with
- * fewer than 256 output tiles split K (by the FULL shape) into fp32 partials folded in split
- * order. Workspace: lcq_gemm_f32x6_workspace_bytes(M, row1 - row0, N, K) bytes, 16-byte
- * aligned. */
-int64_t lcq_gemm_f32x6_workspace_bytes(int64_t M, int64_t rows, int64_t n, int64_t k);
+ * the row range, so a row-split product is bit-identical to the whole one. at 1: A stored
+ * k-major [K, lda] (GPTQ's stacked Err1). Products with fewer than 256 output tiles split K (by
+ * the FULL shape, at most max_splits) into fp32 partials folded in split order. Workspace:
+ * lcq_gemm_f32x6_workspace_bytes(M, row1 - row0, N, K, max_splits) bytes, 16-byte aligned. */
+int64_t lcq_gemm_f32x6_workspace_bytes(int64_t M, int64_t rows, int64_t n, int64_t k,
+                                       int max_splits);
 int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
-                   const void* B, int64_t ldb, int bt, float beta, void* C, int64_t ldc,
-                   int64_t row0, int64_t row1, void* workspace, int64_t ws_bytes, void* stream);
+                   int at, const void* B, int64_t ldb, int bt, float beta, void* C, int64_t ldc,
+                   int64_t row0, int64_t row1, int max_splits, void* workspace, int64_t ws_bytes,
+                   void* stream);
 
 /* Diagonal tile of the recursive fp32 factorisation behind U = chol(H^-1, upper)
  * (gptq.py:169-174): for SPD A (n x n, n <= 128, row-major fp32, leading dim lda), X <- L^-1

@@ -87,9 +87,9 @@ SIGNATURES = {
     'lcq_gemm_f32': ([_i64, _i64, _i64, _f32, _vp, _i64, _vp, _i64, _int, _f32, _vp, _i64, _vp],
                      _int),
     'lcq_gemm_f32_workspace_bytes': ([_i64, _i64, _i64], _i64),
-    'lcq_gemm_f32x6_workspace_bytes': ([_i64, _i64, _i64, _i64], _i64),
-    'lcq_gemm_f32x6': ([_i64, _i64, _i64, _f32, _vp, _i64, _vp, _i64, _int, _f32, _vp, _i64,
-                        _i64, _i64, _vp, _i64, _vp], _int),
+    'lcq_gemm_f32x6_workspace_bytes': ([_i64, _i64, _i64, _i64, _int], _i64),
+    'lcq_gemm_f32x6': ([_i64, _i64, _i64, _f32, _vp, _i64, _int, _vp, _i64, _int, _f32, _vp,
+                        _i64, _i64, _i64, _int, _vp, _i64, _vp], _int),
     'lcq_gemm_f32_row_unit': ([_i64, _i64], _i64),
     'lcq_gemm_f32_rows': ([_i64, _i64, _i64, _f32, _vp, _i64, _vp, _i64, _int, _f32, _vp, _i64,
                            _i64, _i64, _vp], _int),

@@ -1124,43 +1124,48 @@ static int64_t x6_kp(int64_t k) { return (k + SKT - 1) / SKT * SKT; }
 
 // K splits of the FULL M x N x K product (so every row range of it sums the same K-tile
 // groups): enough workgroups for the 256 CUs, >= 16 K-tiles per split
-static int x6_splits(int64_t M, int64_t n, int64_t k) {
+static int x6_splits(int64_t M, int64_t n, int64_t k, int max_splits) {
   const int64_t tiles = ((M + ST - 1) / ST) * ((n + ST - 1) / ST);
   int64_t sp = tiles >= 256 ? 1 : 256 / tiles;
   const int64_t nk = 6 * x6_kp(k) / SKT;
+  if (sp > max_splits) sp = max_splits;
   if (sp > 8) sp = 8;
   while (sp > 1 && nk / sp < 16) --sp;
   return (int)sp;
 }
 
 extern "C" int64_t lcq_gemm_f32x6_workspace_bytes(int64_t M, int64_t rows, int64_t n,
-                                                  int64_t k) {
-  if (M <= 0 || rows <= 0 || n <= 0 || k <= 0) return 0;
-  const int sp = x6_splits(M, n, k);
+                                                  int64_t k, int max_splits) {
+  if (M <= 0 || rows <= 0 || n <= 0 || k <= 0 || max_splits < 1) return 0;
+  const int sp = x6_splits(M, n, k, max_splits);
   return (rows + n) * 3 * x6_kp(k) * 2 + (sp > 1 ? sp * rows * n * 4 : 0) + 512;
 }
 
 extern "C" int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
-                              int64_t lda, const void* B, int64_t ldb, int bt, float beta,
-                              void* C, int64_t ldc, int64_t row0, int64_t row1, void* workspace,
-                              int64_t ws_bytes, void* stream) {
+                              int64_t lda, int at, const void* B, int64_t ldb, int bt,
+                              float beta, void* C, int64_t ldc, int64_t row0, int64_t row1,
+                              int max_splits, void* workspace, int64_t ws_bytes, void* stream) {
   LCQ_REQUIRE(M > 0 && N > 0 && K > 0 && 0 <= row0 && row0 < row1 && row1 <= M,
               "shape / row range");
   LCQ_REQUIRE(N % 16 == 0 && ldc % 4 == 0 && ldc >= N, "N % 16 == 0, ldc % 4 == 0");
   LCQ_REQUIRE(A && B && C && aligned16(C), "pointers (C 16-byte aligned)");
-  LCQ_REQUIRE(lda >= K && (bt ? ldb >= K : ldb >= N), "leading dimensions");
+  LCQ_REQUIRE((at ? lda >= M : lda >= K) && (bt ? ldb >= K : ldb >= N), "leading dimensions");
+  LCQ_REQUIRE(max_splits >= 1, "max_splits >= 1");
   const int64_t kp = x6_kp(K), rows = row1 - row0;
   LCQ_REQUIRE(6 * kp < ((int64_t)1 << 21), "K too large for 32-bit panel offsets");
   LCQ_REQUIRE(workspace && aligned16(workspace) &&
-                  ws_bytes >= lcq_gemm_f32x6_workspace_bytes(M, rows, N, K),
+                  ws_bytes >= lcq_gemm_f32x6_workspace_bytes(M, rows, N, K, max_splits),
               "workspace smaller than lcq_gemm_f32x6_workspace_bytes");
   hipStream_t st = as_stream(stream);
   const int64_t ldd = 3 * kp;  // [rows][3 planes][kp]
   uint16_t* ap = reinterpret_cast<uint16_t*>(workspace);
   uint16_t* bp = ap + rows * ldd;
-  const float* a32 = reinterpret_cast<const float*>(A) + row0 * lda;
+  const float* a32 = reinterpret_cast<const float*>(A) + (at ? row0 : row0 * lda);
   const float* b32 = reinterpret_cast<const float*>(B);
-  {
+  if (at) {  // A stored k-major [K, lda]: row r of A is column r
+    hipLaunchKernelGGL(k_split3_t, dim3((unsigned)((rows + 63) / 64), (unsigned)((kp + 63) / 64)),
+                       256, 0, st, a32, lda, rows, K, kp, ap, ldd);
+  } else {
     const int64_t items = rows * (kp / 8);
     hipLaunchKernelGGL(k_split3, dim3((unsigned)((items + 255) / 256)), 256, 0, st, a32, lda,
                        rows, K, kp, ap, ldd);
@@ -1188,7 +1193,7 @@ extern "C" int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, cons
   g.x6_kp = (int)kp;
   g.x6_roles_a = ROLES_A;
   g.x6_roles_b = ROLES_B;
-  g.x6_splits = x6_splits(M, N, K);
+  g.x6_splits = x6_splits(M, N, K, max_splits);
   if (g.x6_splits > 1) {
     const uintptr_t pp = reinterpret_cast<uintptr_t>(bp + N * ldd);
     g.x6_part = reinterpret_cast<float*>((pp + 255) & ~(uintptr_t)255);

@@ -365,11 +365,13 @@ X6 = True   # module switch for A/B runs and tests (False: every product on the 
 
 
 def gemm_f32x6(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, alpha: float, beta: float,
-               b_trans: bool, row0: int = 0, row1: int | None = None) -> torch.Tensor:
-    """Rows [row0, row1) of out = beta out + alpha A op(B) (fp32 views as gemm_f32) on bf16
-    MFMA over three bf16 planes per operand (lcq_gemm_f32x6: fp32-GEMM accuracy, ~2x the fp32
-    MFMA rate). Row ranges compute every element exactly as the whole product does."""
-    M, K = A.shape
+               b_trans: bool, row0: int = 0, row1: int | None = None, a_trans: bool = False,
+               max_splits: int = 8) -> torch.Tensor:
+    """Rows [row0, row1) of out = beta out + alpha op(A) op(B) (fp32 views as gemm_f32; a_trans:
+    A given k-major as [K, M]) on bf16 MFMA over three bf16 planes per operand (lcq_gemm_f32x6:
+    fp32-GEMM accuracy, ~2x the fp32 MFMA rate). Row ranges compute every element exactly as
+    the whole product does; max_splits 1 keeps K unsplit whatever the shape."""
+    K, M = A.shape if a_trans else A.shape[::-1]
     n_ = out.shape[1]
     row1 = M if row1 is None else row1
     ok = B.shape == ((n_, K) if b_trans else (K, n_))
@@ -377,11 +379,12 @@ def gemm_f32x6(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, alpha: float
         raise ValueError('gemm_f32x6: shape mismatch')
     if any(t.dtype != torch.float32 for t in (A, B, out)):
         raise ValueError('gemm_f32x6: fp32 operands')
-    ws_bytes = int(N.load().lcq_gemm_f32x6_workspace_bytes(M, row1 - row0, n_, K))
+    ws_bytes = int(N.load().lcq_gemm_f32x6_workspace_bytes(M, row1 - row0, n_, K,
+                                                            int(max_splits)))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=A.device)
-    N.call('lcq_gemm_f32x6', M, n_, K, float(alpha), A.data_ptr(), _ld(A), B.data_ptr(), _ld(B),
-           int(b_trans), float(beta), out.data_ptr(), _ld(out), int(row0), int(row1),
-           ws.data_ptr(), ws_bytes, N.stream_of(A))
+    N.call('lcq_gemm_f32x6', M, n_, K, float(alpha), A.data_ptr(), _ld(A), int(a_trans),
+           B.data_ptr(), _ld(B), int(b_trans), float(beta), out.data_ptr(), _ld(out), int(row0),
+           int(row1), int(max_splits), ws.data_ptr(), ws_bytes, N.stream_of(A))
     return out
 
 
@@ -423,12 +426,25 @@ def gather_rc(A: torch.Tensor, rsrc=None, csrc=None, dead_col=None, dead_diag=No
     return out
 
 
+TRAIL_X6_MIN_K = 1024   # trailing updates from this K (the superblock's far update) use x6
+
+
 def gptq_trailing(W: torch.Tensor, c0: int, cnt: int, c1: int, err: torch.Tensor,
                   U: torch.Tensor, c2: int | None = None):
     """W[:, c1:c2] -= err.T[:, :cnt] @ U[c0:c0+cnt, c1:c2] in place (err k-major
-    [cnt, >= rows] view; fp32 MFMA, deterministic k order). c2 defaults to the last column."""
+    [cnt, >= rows] view; deterministic k order). c2 defaults to the last column. The far
+    updates (cnt >= TRAIL_X6_MIN_K) run on split-plane bf16 MFMA (lcq_gemm_f32x6, K never split,
+    the product rounded to fp32 then subtracted as on the fp32 kernel); the rest on fp32 MFMA.
+    The choice depends on cnt and the column layout only, never on the row count, so a row
+    shard computes its rows exactly as one GPU does."""
     rows, ld = W.shape
     c2 = ld if c2 is None else int(c2)
+    if (X6 and cnt >= TRAIL_X6_MIN_K and (c2 - c1) % 16 == 0 and c1 % 4 == 0 and ld % 4 == 0
+            and W.stride(1) == 1 and W.data_ptr() % 16 == 0 and err.stride(1) == 1
+            and U.stride(1) == 1):
+        gemm_f32x6(err[:cnt, :rows], U[c0:c0 + cnt, c1:c2], W[:, c1:c2], -1.0, 1.0, False,
+                   a_trans=True, max_splits=1)
+        return
     N.call('lcq_gptq_trailing', N.ptr(W), rows, ld, int(c0), int(cnt), int(c1), c2, N.ptr(err),
            _ld_err(err, rows), N.ptr(U), U.shape[1], N.stream_of(W))
 

@@ -432,6 +432,51 @@ def test_gemm_f32x6_rows_match_full(dev, M, N, K, bt):
     assert torch.equal(parts, full)
 
 
+def test_gemm_f32x6_a_trans(dev):
+    """A given k-major ([K, M] view, GPTQ's stacked Err1) equals the row-major call on the
+    transposed copy bit for bit (same planes, same k order), also on row ranges with K unsplit
+    (max_splits 1, the trailing update's setting)."""
+    from lightcompress_amd import ops
+    M, N, K = 1000, 768, 1024
+    g = torch.Generator(device=dev).manual_seed(23)
+    At = torch.randn(K, M + 8, generator=g, device=dev)[:, :M]
+    B = torch.randn(K, N, generator=g, device=dev)
+    C0 = torch.randn(M, N, generator=g, device=dev)
+    a = ops.gemm_f32x6(At, B, C0.clone(), -1.0, 1.0, False, a_trans=True, max_splits=1)
+    b = ops.gemm_f32x6(At.t().contiguous(), B, C0.clone(), -1.0, 1.0, False, max_splits=1)
+    assert torch.equal(a, b)
+    parts = C0.clone()
+    for r0, r1 in ((0, 64), (64, 640), (640, M)):
+        ops.gemm_f32x6(At, B, parts, -1.0, 1.0, False, r0, r1, a_trans=True, max_splits=1)
+    assert torch.equal(parts, a)
+    ref = C0.double() - At.double().t() @ B.double()
+    assert ((a.double() - ref).abs().max() / ref.abs().max()).item() < 1e-6
+
+
+def test_gptq_trailing_far_update_x6(dev, monkeypatch):
+    """The superblock's far update (cnt >= TRAIL_X6_MIN_K) on lcq_gemm_f32x6 agrees with the
+    fp32 kernel's to fp32 accuracy and is independent of the row count (row shards)."""
+    from lightcompress_amd import ops
+    rows, cols, cnt = 512, 3072, 1024
+    g = torch.Generator(device=dev).manual_seed(29)
+    W0 = torch.randn(rows, cols, generator=g, device=dev)
+    err = torch.randn(cnt, rows, generator=g, device=dev) * 0.01
+    U = torch.randn(cols, cols, generator=g, device=dev).triu() * 0.05
+    out = {}
+    for x6 in (True, False):
+        monkeypatch.setattr(ops, 'X6', x6)
+        W = W0.clone()
+        ops.gptq_trailing(W, 0, cnt, cnt, err, U)
+        out[x6] = W
+    assert torch.equal(out[True][:, :cnt], W0[:, :cnt])
+    d = (out[True] - out[False]).abs().max().item()
+    assert d <= 1e-5 * out[False].abs().max().item(), d
+    monkeypatch.setattr(ops, 'X6', True)
+    Ws = W0[128:384].clone()
+    ops.gptq_trailing(Ws, 0, cnt, cnt, err[:, 128:384].contiguous(), U)
+    assert torch.equal(Ws, out[True][128:384])
+
+
 def test_inverse_cholesky_x6_vs_fp32_products(dev, monkeypatch):
     """The chain with its large products on lcq_gemm_f32x6 (n 8192: the 4096 x 2048 updates
     go there) is as accurate as with every product on the fp32 kernels, against fp64."""
