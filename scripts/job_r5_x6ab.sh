@@ -1,6 +1,7 @@
-# round 5: GPTQ leg A/B, chain products on lcq_gemm_f32x6 (X6=1) vs fp32 MFMA (X6=0), one box
+# round 5: GPTQ leg A/B, chain products + far column-loop updates on lcq_gemm_f32x6 (X6=1) vs
+# fp32 MFMA (X6=0), one box
 set -o pipefail
-O=gpurun_out/r5x6ab
+O=gpurun_out/r5x6ab2
 mkdir -p $O
 A="--algo gptq --no-cpu-baseline --no-e2e --no-l70b --steps 3 --warmup 1"
 for i in 1 2; do
