@@ -186,6 +186,23 @@ constexpr int SB_ROWS = 32;
 
 // div_exact: lcq_common.h
 
+// st8 with the bf16 rounding on v_cvt_pk_bf16_f32 (RNE like bf16_rne; a NaN stays a NaN with
+// its payload dropped): this streaming kernel is VALU-heavy enough for the integer form to show
+template <int DT>
+__device__ __forceinline__ void st8_cvt(void* base, int64_t e0, const float (&v)[8]) {
+  if constexpr (DT == LCQ_BF16) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = (__float_as_uint(bf16_rne_hw(v[2 * i])) >> 16) |
+             (__float_as_uint(bf16_rne_hw(v[2 * i + 1])) & 0xffff0000u);
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(base) + e0) =
+        make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    st8<DT>(base, e0, v);
+  }
+}
+
 template <int DT, int OP, int AXIS>
 __global__ void __launch_bounds__(256) k_scale_bcast(const void* x, int64_t rows, int64_t cols,
                                                     const void* s, void* out, int64_t rb) {
@@ -219,7 +236,7 @@ __global__ void __launch_bounds__(256) k_scale_bcast(const void* x, int64_t rows
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         v[u][j] = (OP == 0) ? v[u][j] * sv[j] : div_exact(v[u][j], sv[j], rs[j]);
-      st8<DT>(out, (rb4 + u) * cols + c8 * 8, v[u]);
+      st8_cvt<DT>(out, (rb4 + u) * cols + c8 * 8, v[u]);
     }
   }
 }
