@@ -241,6 +241,15 @@ def max_over_ranks(v, world, dev):
     return v
 
 
+def take_linear_fallbacks():
+    """lcq_linear calls since the last call that took torch's F.linear instead of the lcq GEMM
+    (module_utils.LINEAR_FALLBACKS), as {"dtype x / w K->N": count}; resets the counter."""
+    from lightcompress_amd import module_utils as mu
+    got = {f'{a}/{b} {k}->{n}': c for (a, b, k, n), c in mu.LINEAR_FALLBACKS.items()}
+    mu.LINEAR_FALLBACKS.clear()
+    return got
+
+
 def kernel_table(kern, elapsed):
     return {k: {'launches': v['launches'], 'avg_ms': round(v['avg_ms'], 4),
                 'share_of_step': round(v['total_ms'] / (elapsed * 1e3), 4)}
@@ -740,6 +749,8 @@ def bench_fp8(args, rank, world, dev):
     t0 = time.perf_counter()
     with timer:
         algo.run_block_loop()
+        torch.cuda.synchronize(dev)
+        t_loop = time.perf_counter() - t0
         algo.deploy('vllm_quant')
     sync_barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
@@ -749,6 +760,8 @@ def bench_fp8(args, rank, world, dev):
         dist.all_reduce(units)
     out = {'linears_per_s': round(units.item() / elapsed, 1),
            'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'steps': args.steps,
+           'block_loop_ms_per_step': round(t_loop / args.steps * 1e3, 3),
+           'deploy_ms_per_step': round((elapsed - t_loop) / args.steps * 1e3, 3),
            'warmup': 1, 'mode': algo.parallel_mode(),
            'workload': (f'DeepSeek-V3 MoE layers (MLA + shared expert + {E} routed experts of '
                         f'2048x7168 / 7168x2048), block-fp8 checkpoint layout, data-free RTN '
@@ -938,9 +951,14 @@ def main():
     # the headline first, on a cold chip (the side legs heat it: a warm MI355X holds a lower
     # MFMA clock, measured ~4 % on this step after the FP8 and GPTQ legs)
     awq_first = args.algo in ('awq', 'both', 'all')
+    fallbacks = {}
+    take_linear_fallbacks()
     if awq_first:
         elapsed, kern, mode, clock = bench_awq(args, rank, world, dev)
+        fallbacks['awq'] = take_linear_fallbacks()
     fp8 = bench_fp8(args, rank, world, dev) if args.algo in ('fp8', 'all') else None
+    if fp8 is not None:
+        fallbacks['fp8'] = take_linear_fallbacks()
     if args.algo == 'fp8':
         if rank == 0:
             print(json.dumps({'metric': 'FP8 expert linears quantized/sec (DSv3 MoE, e4m3 '
@@ -950,6 +968,8 @@ def main():
             dist.destroy_process_group()
         return
     gptq = bench_gptq(args, rank, world, dev) if args.algo in ('gptq', 'both', 'all') else None
+    if gptq is not None:
+        fallbacks['gptq'] = take_linear_fallbacks()
     if args.algo == 'gptq':
         if rank == 0:
             print(json.dumps({'metric': 'linear-layers quantized/sec (Llama-3-8B GPTQ w4a16 '
@@ -961,6 +981,7 @@ def main():
 
     if not awq_first:
         elapsed, kern, mode, clock = bench_awq(args, rank, world, dev)
+        fallbacks['awq'] = take_linear_fallbacks()
     linears = N_LINEARS_PER_BLOCK * args.steps * world
     value = linears / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -968,6 +989,7 @@ def main():
     l70b = None
     if not args.no_l70b and args.algo == 'all':
         l70b = bench_l70b(args, rank, world, dev)
+        fallbacks['l70b'] = take_linear_fallbacks()
 
     e2e = None
     if not args.no_e2e and args.algo == 'all':
@@ -977,6 +999,7 @@ def main():
             # the same two runs with the model host-resident, streamed block by block
             e2e['awq_stream'] = bench_e2e(args, rank, world, dev, 'awq', 'stream')
             e2e['gptq_stream'] = bench_e2e(args, rank, world, dev, 'gptq', 'stream')
+        fallbacks['e2e'] = take_linear_fallbacks()
 
     if rank == 0:
         roofline = gemm_roofline(kern, elapsed)
@@ -1015,6 +1038,9 @@ def main():
             'gpu_sclk_mhz': clock,
             'lcq_kernels': kernel_table(kern, elapsed),
             'cpu_baseline': cpu,
+            # lcq_linear calls per leg that fell back to torch's F.linear (vendor BLAS): {}
+            # means every projection of every leg ran on the lcq GEMM
+            'linear_fallbacks': fallbacks,
         }
         try:
             import psutil

@@ -261,13 +261,15 @@ int lcq_gemm_f32_rows(int64_t M, int64_t N, int64_t K, float alpha, const void* 
 /* Rows [row0, row1) of C = beta C + alpha A op(B) (A, C the FULL [M, *] fp32 operands, B as in
  * lcq_gemm_f32; N % 16 == 0, ldc % 4 == 0, C 16-byte aligned) on bf16 MFMA: every operand
  * value split into three bf16 planes, the six plane products above the 2^-24 level summed by
- * one k_gemm16h GEMM over K' = 6 * roundup(K, 64) with fp32 accumulation (accuracy of an fp32
- * GEMM at ~2x its rate on gfx950, where fp32 MFMA runs at 1/16 of bf16). The recursion's large
+ * one k_gemm16h GEMM over K' = 6 * roundup(K, 64) with fp32 accumulation (the three dropped
+ * plane products are below 2^-24 relative: close to, not identical with, an fp32 GEMM's error;
+ * ~2x its rate on gfx950, where fp32 MFMA runs at 1/16 of bf16). The recursion's large
  * products (gptq_core._gemm; gptq.py:161-170). Each output element's k order is independent of
  * the row range, so a row-split product is bit-identical to the whole one. at 1: A stored
  * k-major [K, lda] (GPTQ's stacked Err1). Products with fewer than 256 output tiles split K (by
  * the FULL shape, at most max_splits) into fp32 partials folded in split order. Workspace:
- * lcq_gemm_f32x6_workspace_bytes(M, row1 - row0, N, K, max_splits) bytes, 16-byte aligned. */
+ * lcq_gemm_f32x6_workspace_bytes(M, row1 - row0, N, K, max_splits) bytes, 16-byte aligned.
+ * row0 == row1 (an empty rank share) is a no-op, as for lcq_gemm_f32_rows. */
 int64_t lcq_gemm_f32x6_workspace_bytes(int64_t M, int64_t rows, int64_t n, int64_t k,
                                        int max_splits);
 int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,

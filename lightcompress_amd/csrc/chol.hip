@@ -414,6 +414,9 @@ __global__ void __launch_bounds__(NT) k_chol_inv_tile(const float* A, int64_t ld
         while (__hip_atomic_load(arrive + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 3 ||
                __hip_atomic_load(lflag + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
           __builtin_amdgcn_s_sleep(1);
+        // acquire side: no LDS read of the S2 blocks / L_{p+1} may move above the spin (LDS
+        // requests of the CU are coherent and in order; only the compiler can reorder them)
+        asm volatile("" ::: "memory");
         PROF_STAMP(4 + 4 * p, 1)
         // S3 of panel p: A_{i,j} (q <= j <= i, but the diagonal block q done by wave 0) then
         // R_{i,k} (i >= q, k <= p), job n to wave 1 + n % 3, four at a time
@@ -1065,7 +1068,10 @@ static int gemm_f32_impl(int64_t M, int64_t N, int64_t K, float alpha, const voi
   const int64_t t128 = ((N + 127) / 128) * ((plan_m + 127) / 128);
   const bool big = t128 >= 256;
   // LDS-DMA kernel: K % 32 == 0, 16-byte aligned rows, 32-bit byte offsets
-  const bool dma = K % f32g::DKC == 0 && a.vec && al(C) && plan_m * lda < ((int64_t)1 << 29) &&
+  // ldc % 4 == 0 with al(C): the choice is the same for every row range of C (a shifted C of
+  // lcq_gemm_f32_rows stays aligned), so the ranks of a row split run one kernel
+  const bool dma = K % f32g::DKC == 0 && a.vec && al(C) && ldc % 4 == 0 &&
+                   plan_m * lda < ((int64_t)1 << 29) &&
                    (bt ? N * ldb : K * ldb) < ((int64_t)1 << 29);
   if (dma && ws != nullptr && ws_bytes >= sk_ws_bytes() && plan_m == M &&
       use_stream_k(M, N, K)) {

@@ -1145,8 +1145,9 @@ extern "C" int lcq_gemm_f32x6(int64_t M, int64_t N, int64_t K, float alpha, cons
                               int64_t lda, int at, const void* B, int64_t ldb, int bt,
                               float beta, void* C, int64_t ldc, int64_t row0, int64_t row1,
                               int max_splits, void* workspace, int64_t ws_bytes, void* stream) {
-  LCQ_REQUIRE(M > 0 && N > 0 && K > 0 && 0 <= row0 && row0 < row1 && row1 <= M,
+  LCQ_REQUIRE(M > 0 && N > 0 && K > 0 && 0 <= row0 && row0 <= row1 && row1 <= M,
               "shape / row range");
+  if (row0 == row1) return LCQ_OK;   // an empty rank share of a row split (as lcq_gemm_f32_rows)
   LCQ_REQUIRE(N % 16 == 0 && ldc % 4 == 0 && ldc >= N, "N % 16 == 0, ldc % 4 == 0");
   LCQ_REQUIRE(A && B && C && aligned16(C), "pointers (C 16-byte aligned)");
   LCQ_REQUIRE((at ? lda >= M : lda >= K) && (bt ? ldb >= K : ldb >= N), "leading dimensions");

@@ -15,13 +15,26 @@ import torch.nn.functional as F
 from . import ops
 
 
+# Calls of lcq_linear that took torch's F.linear (vendor BLAS) instead of the lcq GEMM, by
+# (dtype, K, N): bench.py reports them per leg, and STRICT_LINEAR turns them into errors.
+LINEAR_FALLBACKS: dict = {}
+STRICT_LINEAR = False
+
+
 def lcq_linear(x, weight, bias=None):
     """F.linear(x, weight, bias) on the lcq GEMM when the operands fit it (bf16 / fp16 on the
     device, K % 64 == 0, out_features % 16 == 0, bias in the input dtype); other operands
-    (fp32 GPTQ weights, odd shapes) take torch's F.linear."""
+    (fp32 GPTQ weights, odd shapes) take torch's F.linear, counted in LINEAR_FALLBACKS (an
+    error under STRICT_LINEAR)."""
     if (ops.gemm_supported(x, weight)
             and (bias is None or (bias.dtype == x.dtype and bias.is_contiguous()))):
         return ops.linear(x, weight, bias)
+    key = (str(x.dtype).replace('torch.', ''), str(weight.dtype).replace('torch.', ''),
+           int(weight.shape[-1]), int(weight.shape[0]))
+    if STRICT_LINEAR:
+        raise ops.N.LcqError(f'lcq_linear: operands {key} do not fit the lcq GEMM '
+                             '(STRICT_LINEAR forbids the F.linear fallback)')
+    LINEAR_FALLBACKS[key] = LINEAR_FALLBACKS.get(key, 0) + 1
     return F.linear(x, weight, bias)
 
 

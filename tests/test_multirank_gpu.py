@@ -215,45 +215,60 @@ def test_static_act_qparams_token_shards_bit_identical(dev, entries, algo, tmp_p
             assert torch.equal(single[k], multi[k]), k
 
 
-def _chain_worker(rank, world, port, n, path):
-    from lightcompress_amd import gptq_core
+def _chain_worker(rank, world, port, n, path, x6):
+    from lightcompress_amd import gptq_core, ops
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK='0')
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         gptq_core.SHARD_MIN_ROWS = 256
+        x6_split = []
+        if x6:
+            ops.X6_MIN_TILES = 1
+            real = ops.gemm_f32x6
+
+            def spy(A, B, out, alpha, beta, b_trans, row0=0, row1=None, **kw):
+                if row1 is not None and row1 - row0 < out.shape[0]:
+                    x6_split.append((out.shape[0], row0, row1))
+                return real(A, B, out, alpha, beta, b_trans, row0, row1, **kw)
+            ops.gemm_f32x6 = spy
         H = torch.load(path + '.H', weights_only=True).to('cuda:0')
         with gptq_core.chain_sharding(rank, world):
             U = gptq_core.inverse_cholesky_upper(H)
-        torch.save({'U': U.cpu(), 'split': gptq_core.shard_stats['split_products']},
-                   f'{path}.{rank}')
+        torch.save({'U': U.cpu(), 'split': gptq_core.shard_stats['split_products'],
+                    'x6_split': len(x6_split)}, f'{path}.{rank}')
     finally:
         dist.destroy_process_group()
 
 
-def test_chain_row_split_bit_identical(dev, tmp_path):
-    """gptq_core.chain_sharding at n 1536: every product of >= 256 output rows is computed
-    by each rank for its rows only (lcq_gemm_f32_rows, the full shape's kernel plan) and
-    all-gathered in rank order; U equals the one-process chain (same products, unsplit) bit for
-    bit on both ranks."""
-    from lightcompress_amd import gptq_core
-    n = 1536
+@pytest.mark.parametrize('n,x6', [(1536, False), (2304, True)])
+def test_chain_row_split_bit_identical(dev, tmp_path, n, x6):
+    """gptq_core.chain_sharding: every product of >= 256 output rows is computed by each rank
+    for its rows only (the full shape's kernel plan: lcq_gemm_f32_rows, or with x6 the
+    split-plane lcq_gemm_f32x6 row ranges, K split by the full shape and folded per row range)
+    and all-gathered in rank order; U equals the one-process chain (same products, unsplit) bit
+    for bit on both ranks. n 2304 with X6_MIN_TILES 1 puts the K >= 1024 products on x6."""
+    from lightcompress_amd import gptq_core, ops
     g = torch.Generator().manual_seed(3)
     X = torch.randn(n, 2 * n, generator=g)
     H = X @ X.T / (2 * n)
     H.diagonal().add_(0.05)
     path = str(tmp_path / 'chain')
     torch.save(H, path + '.H')
-    old = gptq_core.SHARD_MIN_ROWS
+    old = gptq_core.SHARD_MIN_ROWS, ops.X6_MIN_TILES
     try:
         gptq_core.SHARD_MIN_ROWS = 256
+        if x6:
+            ops.X6_MIN_TILES = 1
         single = gptq_core.inverse_cholesky_upper(H.to(dev)).cpu()
     finally:
-        gptq_core.SHARD_MIN_ROWS = old
+        gptq_core.SHARD_MIN_ROWS, ops.X6_MIN_TILES = old
+        gptq_core.clear_chain_graphs()   # captured under the probe thresholds
     ctx = mp.get_context('spawn')
     port = _port()
-    procs = [ctx.Process(target=_chain_worker, args=(r, 2, port, n, path)) for r in range(2)]
+    procs = [ctx.Process(target=_chain_worker, args=(r, 2, port, n, path, x6))
+             for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -262,6 +277,8 @@ def test_chain_row_split_bit_identical(dev, tmp_path):
     for r in range(2):
         res = torch.load(f'{path}.{r}', weights_only=True)
         assert res['split'] > 0
+        if x6:
+            assert res['x6_split'] > 0, 'no row-split product reached lcq_gemm_f32x6'
         assert torch.equal(res['U'], single), r
 
 
