@@ -387,6 +387,25 @@ int lcq_auto_clip_search_act(const void* w, const void* x, const void* qx, int d
                              const void* mse_p, float norm, void* best_max, void* best_min,
                              void* stream);
 
+/* lcq_auto_clip_search_act with a caller workspace of lcq_auto_clip_workspace_bytes(oc, ic, T,
+ * group, nsteps) bytes (16-byte aligned; 0 = not applicable). Weight-only searches (qx NULL)
+ * with group 128, min/max qparams and nsteps 10 run the scalar-operand kernels: the candidate
+ * weights of every (row, step) tabulated once in the workspace (row chunks of at most 1 GiB),
+ * then one lane per weight row with the sampled tokens streamed through scalar registers (an
+ * fp32 copy of x in the workspace). Results are bit-identical to lcq_auto_clip_search_act,
+ * which every other case (and a workspace too small for 192 rows) runs. */
+int64_t lcq_auto_clip_workspace_bytes(int64_t oc, int64_t ic, int64_t T, int group, int nsteps);
+int lcq_auto_clip_search_ws(const void* w, const void* x, const void* qx, int dtype, int64_t oc,
+                            int64_t ic, int64_t T, int group, int nsteps, const void* factors,
+                            int qmin, int qmax, int sym, int clip_sym, int mse_steps,
+                            const void* mse_p, float norm, void* best_max, void* best_min,
+                            void* workspace, int64_t ws_bytes, void* stream);
+
+/* A/B probe hook of lcq_auto_clip_search_ws (scripts/clip_rate.py): 0 = automatic, 1 = the
+ * token-lane kernel (one lane per token, candidates as scalar operands), 2 = the row-lane
+ * kernel. Process-wide; not for production use. */
+int lcq_auto_clip_force_variant(int variant);
+
 /* AutoClipper.auto_clip_layer for per_channel integer weights (group = ic, auto_clip.py:96-99;
  * awq_w8a8.yml): w [oc, ic] (ic % 128 == 0), x [T, ic] sampled tokens, qx [T, ic] their
  * activation fake-quant or NULL (weight-only), nsteps <= 10 with factors[nsteps] =

@@ -81,6 +81,11 @@ SIGNATURES = {
                               _int, _int, _int, _vp, _f32, _vp, _vp, _vp], _int),
     'lcq_auto_clip_search_act': ([_vp, _vp, _vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int,
                                   _int, _int, _int, _int, _vp, _f32, _vp, _vp, _vp], _int),
+    'lcq_auto_clip_workspace_bytes': ([_i64, _i64, _i64, _int, _int], _i64),
+    'lcq_auto_clip_force_variant': ([_int], _int),
+    'lcq_auto_clip_search_ws': ([_vp, _vp, _vp, _int, _i64, _i64, _i64, _int, _int, _vp, _int,
+                                 _int, _int, _int, _int, _vp, _f32, _vp, _vp, _vp, _i64, _vp],
+                                _int),
     'lcq_auto_clip_pc_workspace_bytes': ([_i64, _i64, _int], _i64),
     'lcq_auto_clip_search_pc': ([_vp, _vp, _vp, _int, _i64, _i64, _i64, _int, _vp, _int, _int,
                                  _int, _int, _int, _int, _int, _vp, _i64, _vp, _vp, _vp], _int),

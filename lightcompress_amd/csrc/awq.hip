@@ -476,6 +476,28 @@ __device__ __forceinline__ float dt_val(uint16_t b) {
   else return (float)__builtin_bit_cast(_Float16, b);
 }
 
+// One shrink step's candidate weights (auto_clip.py:160-172 with fake_quantize, quant.py
+// get_qparams + quant_dequant in DT): q <- fq(clamp(q, smin, smax)) with the qparams of the
+// clamped group range [cmn, cmx].
+template <int DT, int N>
+__device__ __forceinline__ void clip_candidates(float (&q)[N], float smin, float smax, float cmn,
+                                                float cmx, float qmin, float qmax, int sym) {
+  float qs, qz;
+  qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
+  const float rqs = 1.0f / qs;  // RN(1/s): qs >= DT(1e-5) / qmax, so it is normal
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const float v = fminf(fmaxf(q[k], smin), smax);
+    // correctly rounded fp32 quotient (Markstein's from RN(1/s), 3 VALU: |v / s| <= qmax + 1,
+    // normal or rounding to zero either way, as mk_safe in quant_group.hip), then rounded to
+    // DT. A plain v * RN(1/s) can miss by an ulp, which fp16's extra mantissa bits expose.
+    float tq = rintf(dtr<DT>(div_mk(v, qs, rqs)));
+    if (!sym) tq = dtr<DT>(tq + qz);
+    tq = fminf(fmaxf(tq, qmin), qmax);
+    q[k] = dtr<DT>((sym ? tq : dtr<DT>(tq - qz)) * qs);
+  }
+}
+
 template <int DT, int G, int R, bool MSE>
 __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)
     k_auto_clip(const uint16_t* __restrict__ w, const uint16_t* __restrict__ x, int64_t oc,
@@ -596,20 +618,7 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)
               q[j][k] = dtr<DT>((tq - qz) * qs);
             }
           } else {
-            qparams_ct<DT>(cmn, cmx, qmin, qmax, sym, qs, qz);
-            const float rqs = 1.0f / qs;  // RN(1/s): qs >= DT(1e-5) / qmax, so it is normal
-#pragma unroll
-            for (int k = 0; k < CH; ++k) {
-              const float v = fminf(fmaxf(q[j][k], smin), smax);
-              // correctly rounded fp32 quotient (Markstein's from RN(1/s), 3 VALU: |v / s| <=
-              // qmax + 1, normal or rounding to zero either way, as mk_safe in
-              // quant_group.hip), then rounded to DT. A plain v * RN(1/s) can miss by an ulp,
-              // which fp16's extra mantissa bits expose.
-              float tq = rintf(dtr<DT>(div_mk(v, qs, rqs)));
-              if (!sym) tq = dtr<DT>(tq + qz);
-              tq = fminf(fmaxf(tq, qmin), qmax);
-              q[j][k] = dtr<DT>((sym ? tq : dtr<DT>(tq - qz)) * qs);
-            }
+            clip_candidates<DT, CH>(q[j], smin, smax, cmn, cmx, qmin, qmax, sym);
           }
         }
       }
@@ -657,6 +666,366 @@ __global__ void __launch_bounds__(2 * CROWS, G >= 256 ? 1 : 2)
       best_max[oi] = __builtin_bit_cast(uint16_t, (_Float16)bmax);
       best_min[oi] = __builtin_bit_cast(uint16_t, (_Float16)bmin);
     }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Token-lane form of the same search (G = 128, minmax qparams, weight-only: the AWQ headline's
+// auto-clip). k_auto_clip puts a row on a lane pair and broadcasts x from LDS: one LDS read per
+// 16 products and a pair exchange per output kept the VALU issue at ~45 % of its peak
+// (profiles/r3b_clip_pmc.json). Here a lane is a token and keeps that token's 128 x values
+// of the group in VGPRs for all of a wave's rows; the candidate weights of every (row, step)
+// are precomputed once (k_clip_qtable, the same arithmetic) and read as wave-uniform scalar
+// loads, so the inner loop is VALU only: per product pair one v_pk_mul_f32, two
+// v_cvt_pk_bf16_f32 and one v_pk_add_f32, in the same 8 partial sums and halving tree as
+// dot_rows. A wave walks ALL tokens of its rows in order (64 per chunk), so each step's
+// squared-error sum is accumulated in token order exactly as in k_auto_clip: the per-token
+// errors of three rows go through a small per-wave LDS transpose and one lane per
+// (row, step) adds them sequentially. Bit-identical to k_auto_clip (tests/test_awq_gpu.py).
+// ----------------------------------------------------------------------------------------
+constexpr int TL_G = 128;
+constexpr int TL_RB = 6;        // rows per wave: two error flushes of three rows
+constexpr int TL_WAVES = 4;     // waves per workgroup (independent; no block barrier)
+constexpr int TL_EPAD = 66;     // u16 per (row, step) error row: 64 tokens + pad (no conflicts)
+
+// candidate table of one (row, group): [nsteps + 1][G] fp32 -- pass 0 the weights themselves,
+// pass s + 1 shrink step s -- and the group's (org_max, org_min)
+template <int DT, int G>
+__global__ void __launch_bounds__(2 * CROWS)
+    k_clip_qtable(const uint16_t* __restrict__ w, int64_t ic, int64_t row0, int64_t nrows,
+                  int nsteps, const float* __restrict__ factors, float qmin, float qmax, int sym,
+                  int clip_sym, float* __restrict__ qt, float* __restrict__ om) {
+  constexpr int CH = G / 2, CHUNKS = G / 8;
+  const int tid = threadIdx.x, r = tid >> 1, h = tid & 1;
+  const int64_t g = blockIdx.y, ng = ic / G;
+  const int64_t lr = (int64_t)blockIdx.x * CROWS + r;
+  const bool live = lr < nrows;
+  uint2 raw[CHUNKS];
+  fetch_half<G>(w + (row0 + (live ? lr : 0)) * ic + g * G, h, raw);
+  float q0[CH];
+  widen_half<DT, G>(raw, q0);
+  float mx = -INFINITY, mi = INFINITY, am = 0.f;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    mx = fmaxf(mx, q0[k]);
+    mi = fminf(mi, q0[k]);
+    am = fmaxf(am, fabsf(q0[k]));
+  }
+  const float mxs = fmaxf(mx, xor1(mx)), mn = fminf(mi, xor1(mi));
+  am = fmaxf(am, xor1(am));
+  const float org_max = clip_sym ? am : mxs, org_min = mn;
+  if (!live) return;
+  float* dst = qt + (lr * ng + g) * (int64_t)(nsteps + 1) * G;
+  auto put = [&](const float (&q)[CH], int p) {
+#pragma unroll
+    for (int i = 0; i < CHUNKS; ++i)
+      *reinterpret_cast<float4*>(dst + p * G + 8 * i + 4 * h) =
+          make_float4(q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
+  };
+  put(q0, 0);
+  for (int p = 1; p <= nsteps; ++p) {
+    float q[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) q[k] = q0[k];
+    const float f = factors[p - 1];
+    const float smax = dtr<DT>(org_max * f);
+    const float smin = clip_sym ? -smax : dtr<DT>(org_min * f);
+    const float cmn = fminf(fmaxf(mn, smin), smax);
+    const float cmx = fminf(fmaxf(mxs, smin), smax);
+    clip_candidates<DT, CH>(q, smin, smax, cmn, cmx, qmin, qmax, sym);
+    put(q, p);
+  }
+  if (h == 0) {
+    om[(lr * ng + g) * 2] = org_max;
+    om[(lr * ng + g) * 2 + 1] = org_min;
+  }
+}
+
+// Candidate rows reach the VALU as scalar operands: 16 floats per s_load_dwordx16, issued one
+// sub-chunk ahead. Scalar loads may return out of order, so a wait is always lgkmcnt(0); the
+// next load is therefore issued right AFTER the wait for the current one and runs under the
+// current sub-chunk's 32 VALU. Written as inline asm because the compiler's own scalar loads
+// wait immediately (one 16-float buffer, the L2 latency exposed per 16 products: 0.65x the
+// lane-pair kernel's rate). The "+s" operands order the asm statements against the compute
+// that reads the buffers.
+typedef uint32_t sv16 __attribute__((ext_vector_type(16)));
+
+template <int V>
+struct ic_t {
+  static constexpr int value = V;
+};
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(ic_t<I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// s_load_dwordx16 of base[OFF .. OFF + 16) with the offset as the instruction's immediate (one
+// base pointer in SGPRs for a whole candidate row); `pin` orders the compute that reads the
+// previous buffer after this issue
+template <int OFF>
+__device__ __forceinline__ sv16 sload16(const float* base, sv16& pin) {
+  sv16 r;
+  asm volatile("s_load_dwordx16 %0, %2, %3" : "=s"(r), "+s"(pin) : "s"(base), "n"(OFF * 4));
+  return r;
+}
+// wait for the outstanding scalar load; the accumulators tie the previous sub-chunk's compute
+// before the wait (else the compiler hoists the wait and exposes the load latency)
+__device__ __forceinline__ void swait(sv16& r, v2f& a0, v2f& a1, v2f& a2, v2f& a3) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(r), "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+}
+
+// 16 products of this lane's token with a 16-float candidate sub-chunk, into the partial sums
+// acc_{k mod 8} (a0 = (acc0, acc1) .. a3 = (acc6, acc7)) exactly as dot_rows forms them
+template <int DT>
+__device__ __forceinline__ void mac16(const float (&xf)[TL_G], int k0, const sv16& q, v2f& a0,
+                                      v2f& a1, v2f& a2, v2f& a3) {
+#pragma unroll
+  for (int o = 0; o < 16; o += 8) {
+    const int k = k0 + o;
+    // the four products first, then their roundings, then the sums: independent instructions
+    // between each result and its use (no hazard nops in the chain)
+    v2f p0 = v2f{xf[k], xf[k + 1]} * v2f{__uint_as_float(q[o]), __uint_as_float(q[o + 1])};
+    v2f p1 = v2f{xf[k + 2], xf[k + 3]} *
+             v2f{__uint_as_float(q[o + 2]), __uint_as_float(q[o + 3])};
+    v2f p2 = v2f{xf[k + 4], xf[k + 5]} *
+             v2f{__uint_as_float(q[o + 4]), __uint_as_float(q[o + 5])};
+    v2f p3 = v2f{xf[k + 6], xf[k + 7]} *
+             v2f{__uint_as_float(q[o + 6]), __uint_as_float(q[o + 7])};
+    p0 = dtr2<DT>(p0);
+    p1 = dtr2<DT>(p1);
+    p2 = dtr2<DT>(p2);
+    p3 = dtr2<DT>(p3);
+    a0 += p0;
+    a1 += p1;
+    a2 += p2;
+    a3 += p3;
+  }
+}
+
+// one weight row against this lane's token: pass 0 (the original output, org) and the NS
+// shrink steps, each dot product summed as dot_rows does (8 partial sums, halving tree, one
+// DT rounding); the step errors DT(DT(d - org)^2) go to er[step * TL_EPAD] (DT bits). The
+// (NS + 1) x 8 sub-chunk loads form one chain, each issued one sub-chunk ahead.
+template <int DT, int NS>
+__device__ __forceinline__ void clip_row_tl(const float (&xf)[TL_G], const float* qr,
+                                            uint16_t* er) {
+  constexpr int SUB = TL_G / 16;
+  sv16 cur = {}, nxt;
+  cur = sload16<0>(qr, nxt);
+  float org = 0.f;
+  static_for<0, NS + 1>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    v2f a0 = v2f{0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    static_for<0, SUB>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      swait(cur, a0, a1, a2, a3);
+      if constexpr (p == NS && c == SUB - 1) {
+        mac16<DT>(xf, 16 * c, cur, a0, a1, a2, a3);
+      } else {
+        constexpr int off = c < SUB - 1 ? p * TL_G + 16 * (c + 1) : (p + 1) * TL_G;
+        nxt = sload16<off>(qr, cur);
+        mac16<DT>(xf, 16 * c, cur, a0, a1, a2, a3);
+        cur = nxt;
+      }
+    });
+    const v2f l01 = a0 + a2, l23 = a1 + a3;   // (l0, l1), (l2, l3): l_m = acc_m + acc_{m+4}
+    const v2f s2 = l01 + l23;                 // (l0 + l2, l1 + l3)
+    const float d = dtr<DT>(s2.x + s2.y);
+    if constexpr (p == 0) {
+      org = d;
+    } else {
+      const float dd = dtr<DT>(d - org);
+      er[(p - 1) * TL_EPAD] = dt_bits<DT>(dtr<DT>(dd * dd));
+    }
+  });
+}
+
+// NS = 10 shrink steps (max_shrink 0.5 x n_grid 20, every shipped AWQ config)
+template <int DT, int NS>
+__global__ void __launch_bounds__(64 * TL_WAVES)
+    k_auto_clip_tl(const uint16_t* __restrict__ x, int64_t ic, int T,
+                   const float* __restrict__ qt, const float* __restrict__ om, int64_t row0,
+                   int64_t nrows, const float* __restrict__ factors, int clip_sym,
+                   uint16_t* __restrict__ best_max, uint16_t* __restrict__ best_min) {
+  constexpr int G = TL_G, P = NS + 1, NP = 3 * NS;
+  static_assert(NP <= 64, "one lane per (row, step) pair of a row triple");
+  __shared__ uint16_t ebuf[TL_WAVES][NP * TL_EPAD];   // [pair][token] error bits
+  __shared__ float sums[TL_WAVES][2 * NP];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t g = blockIdx.y, ng = ic / G;
+  const int64_t rb = ((int64_t)blockIdx.x * TL_WAVES + w) * TL_RB;  // this wave's first row
+  if (rb >= nrows) return;
+  uint16_t* eb = ebuf[w];
+  float* sm = sums[w];
+  // row triples outermost: a triple's 3 x 11 candidate rows (17 KB) are re-read once per
+  // 64-token chunk while they are still in L2
+  for (int tr = 0; tr < TL_RB / 3; ++tr) {
+    float run = 0.f;   // lane < NP: the error sum of pair `lane`, in token order
+    for (int t0 = 0; t0 < T; t0 += 64) {
+      const int t = t0 + lane, tn = min(64, T - t0);
+      float xf[G];
+      {
+        const uint16_t* xr = x + (int64_t)(t < T ? t : 0) * ic + g * G;
+#pragma unroll
+        for (int i = 0; i < G / 8; ++i) {
+          const uint4 v = t < T ? *reinterpret_cast<const uint4*>(xr + 8 * i)
+                                : make_uint4(0, 0, 0, 0);
+          widen4<DT>(make_uint2(v.x, v.y), &xf[8 * i]);
+          widen4<DT>(make_uint2(v.z, v.w), &xf[8 * i + 4]);
+        }
+      }
+      for (int rr = 0; rr < 3; ++rr) {
+        const int64_t lr = min(rb + 3 * tr + rr, nrows - 1);
+        clip_row_tl<DT, NS>(xf, qt + (lr * ng + g) * (int64_t)P * G,
+                            eb + rr * NS * TL_EPAD + lane);
+      }
+      // the wave's LDS requests complete in order: the other lanes' error bits written above
+      // are visible to the reads below; keep the compiler from moving them across
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (lane < NP) {
+        const uint16_t* src = eb + lane * TL_EPAD;
+        for (int u = 0; u < tn; ++u) run += dt_val<DT>(src[u]);   // token order
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (lane < NP) sm[tr * NP + lane] = run;
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  if (lane < TL_RB && rb + lane < nrows) {
+    const int64_t lr = rb + lane;
+    const float omax = om[(lr * ng + g) * 2], omin = om[(lr * ng + g) * 2 + 1];
+    float bmax = omax, bmin = omin, best = dtr<DT>(1e9f);
+    const float* e = sm + (lane / 3) * NP + (lane % 3) * NS;
+    for (int s = 0; s < NS; ++s) {
+      const float em = dtr<DT>(e[s] / (float)T);
+      if (em < best) {
+        best = em;
+        const float f = factors[s];
+        bmax = dtr<DT>(omax * f);
+        bmin = clip_sym ? -bmax : dtr<DT>(omin * f);
+      }
+    }
+    const int64_t oi = (row0 + lr) * ng + g;
+    best_max[oi] = dt_bits<DT>(bmax);
+    best_min[oi] = dt_bits<DT>(bmin);
+  }
+}
+
+// Row-lane form with the activations as scalar operands (k_auto_clip_rl): a lane owns one
+// weight row (64 rows per one-wave workgroup) and holds the row's candidates for the current
+// pass in VGPRs (read from the k_clip_qtable table); the sampled tokens stream through SGPRs
+// from an fp32 copy of x, 16 values per s_load_dwordx16, issued one sub-chunk ahead. Every
+// wave of a CU on the same group reads the same token stream, so the scalar loads hit the
+// scalar cache; a lane accumulates its row's step errors itself in token order (no cross-lane
+// sum), the original outputs of a 128-token tile kept in LDS as DT bits.
+constexpr int RL_CT = 128;   // tokens per tile
+
+// sum_k DT(x[k] * q[k]) for this lane's candidates q (VGPRs) and the wave-uniform token row
+// xr (fp32, scalar loads), in dot_rows' 8 partial sums and halving tree
+template <int DT>
+__device__ __forceinline__ float dot_rl(const float (&q)[TL_G], const float* xr) {
+  constexpr int SUB = TL_G / 16;
+  v2f a0 = v2f{0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+  sv16 cur = {}, nxt;
+  cur = sload16<0>(xr, nxt);
+  static_for<0, SUB>([&](auto cc) {
+    constexpr int c = decltype(cc)::value;
+    swait(cur, a0, a1, a2, a3);
+    if constexpr (c == SUB - 1) {
+      mac16<DT>(q, 16 * c, cur, a0, a1, a2, a3);
+    } else {
+      nxt = sload16<16 * (c + 1)>(xr, cur);
+      mac16<DT>(q, 16 * c, cur, a0, a1, a2, a3);
+      cur = nxt;
+    }
+  });
+  const v2f l01 = a0 + a2, l23 = a1 + a3;
+  const v2f s2 = l01 + l23;
+  return dtr<DT>(s2.x + s2.y);
+}
+
+template <int DT, int NS>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))   // <= 168 VGPRs
+    k_auto_clip_rl(const float* __restrict__ xt, int64_t ic, int T, const float* __restrict__ qt,
+                   const float* __restrict__ om, int64_t row0, int64_t nrows,
+                   const float* __restrict__ factors, int clip_sym,
+                   uint16_t* __restrict__ best_max, uint16_t* __restrict__ best_min) {
+  constexpr int G = TL_G, P = NS + 1;
+  __shared__ uint16_t orgs[RL_CT * 64];   // [token][lane] original outputs (DT bits)
+  const int lane = threadIdx.x;
+  const int64_t g = blockIdx.y, ng = ic / G;
+  const int64_t lr = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = lr < nrows;
+  const float* qrow = qt + ((live ? lr : 0) * ng + g) * (int64_t)P * G;
+  const float* xg = xt + g * G;
+  float e[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) e[s] = 0.f;
+  for (int t0 = 0; t0 < T; t0 += RL_CT) {
+    const int tn = min(RL_CT, T - t0);
+    static_for<0, P>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      float q[G];
+      // re-read per tile (an opaque pointer: hoisting every pass's candidates out of the tile
+      // loop would hold 11 x 128 values per lane)
+      int poff = p * G;
+      asm volatile("" : "+s"(poff));
+      const float* qp = qrow + poff;
+#pragma unroll
+      for (int i = 0; i < G / 4; ++i) {
+        const float4 v = *reinterpret_cast<const float4*>(qp + 4 * i);
+        q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+      }
+      float acc = p > 0 ? e[p > 0 ? p - 1 : 0] : 0.f;
+      for (int t = 0; t < tn; ++t) {
+        const float d = dot_rl<DT>(q, xg + (int64_t)(t0 + t) * ic);
+        if constexpr (p == 0) {
+          orgs[t * 64 + lane] = dt_bits<DT>(d);
+        } else {
+          const float dd = dtr<DT>(d - dt_val<DT>(orgs[t * 64 + lane]));
+          acc += dtr<DT>(dd * dd);   // token order
+        }
+      }
+      if constexpr (p > 0) e[p - 1] = acc;
+    });
+  }
+  if (!live) return;
+  const float omax = om[(lr * ng + g) * 2], omin = om[(lr * ng + g) * 2 + 1];
+  float bmax = omax, bmin = omin, best = dtr<DT>(1e9f);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const float em = dtr<DT>(e[s] / (float)T);
+    if (em < best) {
+      best = em;
+      const float f = factors[s];
+      bmax = dtr<DT>(omax * f);
+      bmin = clip_sym ? -bmax : dtr<DT>(omin * f);
+    }
+  }
+  const int64_t oi = (row0 + lr) * ng + g;
+  best_max[oi] = dt_bits<DT>(bmax);
+  best_min[oi] = dt_bits<DT>(bmin);
+}
+
+// x [T, ic] in DT -> fp32 (the scalar-operand token stream of k_auto_clip_rl)
+template <int DT>
+__global__ void __launch_bounds__(256) k_widen_f32(const uint16_t* __restrict__ x, int64_t n8,
+                                                   float* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const uint4 v = reinterpret_cast<const uint4*>(x)[i];
+    float a[8];
+    widen4<DT>(make_uint2(v.x, v.y), a);
+    widen4<DT>(make_uint2(v.z, v.w), a + 4);
+    reinterpret_cast<float4*>(out)[2 * i] = make_float4(a[0], a[1], a[2], a[3]);
+    reinterpret_cast<float4*>(out)[2 * i + 1] = make_float4(a[4], a[5], a[6], a[7]);
   }
 }
 
@@ -892,6 +1261,102 @@ extern "C" int lcq_auto_clip_search_act(const void* w, const void* x, const void
     else auto_clip_group<LCQ_F16, false>(group, c, st);
   }
   return check_launch("lcq_auto_clip_search");
+}
+
+// scalar-operand paths: candidate-table bytes per weight row (fp32 [ng][nsteps + 1][128] + the
+// group ranges), the row chunk one table covers (tables of at most 1 GiB), and the fp32 copy
+// of x the row-lane kernel streams
+static int64_t tl_row_bytes(int64_t ic, int nsteps) {
+  return ic / TL_G * ((int64_t)(nsteps + 1) * TL_G + 2) * 4;
+}
+static constexpr int64_t TL_ROWS_PER_WG = TL_WAVES * TL_RB;   // token-lane rows per workgroup
+static constexpr int64_t CL_ROW_UNIT = 192;   // chunk rows: whole workgroups of both kernels
+static constexpr int TL_NS = 10;   // the kernels' shrink-step count
+
+// A/B probe hook (scripts/clip_rate.py): 0 = automatic (row-lane), 1 = token-lane,
+// 2 = row-lane. Process-wide; not for production use.
+static int g_clip_variant = 0;
+extern "C" int lcq_auto_clip_force_variant(int v) {
+  LCQ_REQUIRE(v >= 0 && v <= 2, "variant: 0, 1 or 2");
+  g_clip_variant = v;
+  return LCQ_OK;
+}
+
+extern "C" int64_t lcq_auto_clip_workspace_bytes(int64_t oc, int64_t ic, int64_t T, int group,
+                                                 int nsteps) {
+  if (group != TL_G || oc <= 0 || ic <= 0 || T <= 0 || ic % TL_G || nsteps != TL_NS) return 0;
+  const int64_t per = tl_row_bytes(ic, nsteps);
+  int64_t rows = ((int64_t)1 << 30) / per / CL_ROW_UNIT * CL_ROW_UNIT;
+  if (rows < CL_ROW_UNIT) rows = CL_ROW_UNIT;
+  const int64_t need = (oc + CL_ROW_UNIT - 1) / CL_ROW_UNIT * CL_ROW_UNIT;
+  return (rows < need ? rows : need) * per + T * ic * 4;
+}
+
+extern "C" int lcq_auto_clip_search_ws(const void* w, const void* x, const void* qx, int dtype,
+                                       int64_t oc, int64_t ic, int64_t T, int group,
+                                       int nsteps, const void* factors, int qmin, int qmax,
+                                       int sym, int clip_sym, int mse_steps, const void* mse_p,
+                                       float norm, void* best_max, void* best_min,
+                                       void* workspace, int64_t ws_bytes, void* stream) {
+  const bool shape_ok = group == TL_G && ic > 0 && ic % TL_G == 0 && nsteps == TL_NS && T > 0 &&
+                        T < ((int64_t)1 << 31) && oc > 0;
+  const int64_t per = shape_ok ? tl_row_bytes(ic, nsteps) : 0;
+  const int64_t xbytes = shape_ok ? T * ic * 4 : 0;
+  const int64_t chunk =
+      per && ws_bytes > xbytes ? (ws_bytes - xbytes) / per / CL_ROW_UNIT * CL_ROW_UNIT : 0;
+  const bool al16 = ((reinterpret_cast<uintptr_t>(workspace) | reinterpret_cast<uintptr_t>(x)) &
+                     15) == 0;
+  if (qx != nullptr || mse_steps != 0 || chunk < CL_ROW_UNIT || workspace == nullptr || !al16 ||
+      (dtype != LCQ_BF16 && dtype != LCQ_F16) || qmax <= qmin)
+    return lcq_auto_clip_search_act(w, x, qx, dtype, oc, ic, T, group, nsteps, factors, qmin,
+                                    qmax, sym, clip_sym, mse_steps, mse_p, norm, best_max,
+                                    best_min, stream);
+  hipStream_t st = as_stream(stream);
+  const int64_t ng = ic / TL_G;
+  const bool rl = g_clip_variant != 1;
+  float* xt = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + chunk * per);
+  float* qt = reinterpret_cast<float*>(workspace);
+  const auto* wp = reinterpret_cast<const uint16_t*>(w);
+  const auto* xp = reinterpret_cast<const uint16_t*>(x);
+  const auto* fp = reinterpret_cast<const float*>(factors);
+  auto* bx = reinterpret_cast<uint16_t*>(best_max);
+  auto* bn = reinterpret_cast<uint16_t*>(best_min);
+  if (rl) {
+    const int64_t n8 = T * ic / 8;
+    if (dtype == LCQ_BF16)
+      hipLaunchKernelGGL(k_widen_f32<LCQ_BF16>, stream_grid(n8, 256), 256, 0, st, xp, n8, xt);
+    else
+      hipLaunchKernelGGL(k_widen_f32<LCQ_F16>, stream_grid(n8, 256), 256, 0, st, xp, n8, xt);
+  }
+  for (int64_t r0 = 0; r0 < oc; r0 += chunk) {
+    const int64_t nr = oc - r0 < chunk ? oc - r0 : chunk;
+    float* om = qt + nr * ng * (int64_t)(nsteps + 1) * TL_G;
+    const dim3 g1((unsigned)((nr + CROWS - 1) / CROWS), (unsigned)ng);
+    const dim3 g2((unsigned)((nr + TL_ROWS_PER_WG - 1) / TL_ROWS_PER_WG), (unsigned)ng);
+    const dim3 g3((unsigned)((nr + 63) / 64), (unsigned)ng);
+    if (dtype == LCQ_BF16) {
+      hipLaunchKernelGGL((k_clip_qtable<LCQ_BF16, TL_G>), g1, 2 * CROWS, 0, st, wp, ic, r0, nr,
+                         nsteps, fp, (float)qmin, (float)qmax, sym, clip_sym, qt, om);
+      if (rl)
+        hipLaunchKernelGGL((k_auto_clip_rl<LCQ_BF16, TL_NS>), g3, 64, 0, st, xt, ic, (int)T, qt,
+                           om, r0, nr, fp, clip_sym, bx, bn);
+      else
+        hipLaunchKernelGGL((k_auto_clip_tl<LCQ_BF16, TL_NS>), g2, 64 * TL_WAVES, 0, st, xp, ic,
+                           (int)T, qt, om, r0, nr, fp, clip_sym, bx, bn);
+    } else {
+      hipLaunchKernelGGL((k_clip_qtable<LCQ_F16, TL_G>), g1, 2 * CROWS, 0, st, wp, ic, r0, nr,
+                         nsteps, fp, (float)qmin, (float)qmax, sym, clip_sym, qt, om);
+      if (rl)
+        hipLaunchKernelGGL((k_auto_clip_rl<LCQ_F16, TL_NS>), g3, 64, 0, st, xt, ic, (int)T, qt,
+                           om, r0, nr, fp, clip_sym, bx, bn);
+      else
+        hipLaunchKernelGGL((k_auto_clip_tl<LCQ_F16, TL_NS>), g2, 64 * TL_WAVES, 0, st, xp, ic,
+                           (int)T, qt, om, r0, nr, fp, clip_sym, bx, bn);
+    }
+    const int rc = check_launch("lcq_auto_clip_search_ws");
+    if (rc) return rc;
+  }
+  return LCQ_OK;
 }
 
 extern "C" int lcq_clip_apply(const void* x, int dtype, int64_t rows, int64_t cols,

@@ -752,11 +752,26 @@ def auto_clip_search(w: torch.Tensor, x: torch.Tensor, group: int, nsteps: int, 
     if mse is not None:
         msteps, grid, norm = int(mse[0]), float(mse[1]), float(mse[2])
         mp = _const_f32([float(1 - i / grid) for i in range(msteps)], w.device)
-    N.call('lcq_auto_clip_search_act', N.ptr(w.contiguous()), N.ptr(x.contiguous()),
-           N.ptr(qx.contiguous() if qx is not None else None), N.dt(w), oc, ic, T, int(group),
-           int(nsteps), N.ptr(factors), int(qmin), int(qmax), int(sym), int(clip_sym), msteps,
-           N.ptr(mp), norm, N.ptr(bmax), N.ptr(bmin), N.stream_of(w))
+    args = (N.ptr(w.contiguous()), N.ptr(x.contiguous()),
+            N.ptr(qx.contiguous() if qx is not None else None), N.dt(w), oc, ic, T, int(group),
+            int(nsteps), N.ptr(factors), int(qmin), int(qmax), int(sym), int(clip_sym), msteps,
+            N.ptr(mp), norm, N.ptr(bmax), N.ptr(bmin))
+    ws_bytes = (int(N.load().lcq_auto_clip_workspace_bytes(oc, ic, T, int(group), int(nsteps)))
+                if CLIP_TOKEN_LANE and qx is None and mse is None else 0)
+    if ws_bytes:   # the scalar-operand kernels (weight-only, group 128, minmax): same bits
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=w.device)
+        N.call('lcq_auto_clip_search_ws', *args, ws.data_ptr(), ws_bytes, N.stream_of(w))
+        name = 'lcq_auto_clip_search_ws'
+    else:
+        N.call('lcq_auto_clip_search_act', *args, N.stream_of(w))
+        name = 'lcq_auto_clip_search_act'
+    # algorithmic work: DT-rounded products, the original outputs and every shrink step
+    N.note_work(name, float(oc) * ic * T * (1 + nsteps))
     return bmax, bmin
+
+
+CLIP_TOKEN_LANE = True   # module switch for A/B runs and tests (False: k_auto_clip only)
+# (the name predates the row-lane kernel: True = lcq_auto_clip_search_ws's kernels)
 
 
 _CONST_CACHE: dict = {}

@@ -12,6 +12,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import torch  # noqa: E402
 
+from lightcompress_amd import _native as N  # noqa: E402
 from lightcompress_amd import ops  # noqa: E402
 
 ap = argparse.ArgumentParser()
@@ -27,20 +28,31 @@ for oc, ic in [(1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 
     qx = x.clone() if a.act else None
     for sym in (True, False):
         qmin, qmax = (-8, 7) if sym else (0, 15)
-        ops.auto_clip_search(w, x, 128, 10, 20, qmin, qmax, sym, sym, qx=qx)
-        torch.cuda.synchronize()
-        ts = []
-        for _ in range(3):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            ops.auto_clip_search(w, x, 128, 10, 20, qmin, qmax, sym, sym, qx=qx)
-            e1.record()
+        res = {}
+        lib = N.load()
+        for tl in ('row-lane  ', 'token-lane', 'lane-pair '):
+            ops.CLIP_TOKEN_LANE = tl != 'lane-pair '
+            lib.lcq_auto_clip_force_variant(1 if tl == 'token-lane' else 2)
+            res[tl] = ops.auto_clip_search(w, x, 128, 10, 20, qmin, qmax, sym, sym, qx=qx)
             torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1))
-        ms = statistics.median(ts)
-        if sym:
-            tot_ms += ms
-        prods = oc * ic * 512 * 11
-        print(f'{oc}x{ic} sym={sym}: {ms:7.2f} ms  {prods / ms / 1e9:6.1f} G products/s',
-              flush=True)
-print(f'one Llama-3-8B block (v, o, gate, up, down; sym): {tot_ms:.1f} ms')
+            ts = []
+            for _ in range(3):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ops.auto_clip_search(w, x, 128, 10, 20, qmin, qmax, sym, sym, qx=qx)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            ms = statistics.median(ts)
+            if sym and tl == 'row-lane  ':
+                tot_ms += ms
+            prods = oc * ic * 512 * 11
+            print(f'{oc}x{ic} sym={sym} {tl}: {ms:7.2f} ms  {prods / ms / 1e9:6.1f} G products/s',
+                  flush=True)
+        same = all(torch.equal(a.view(torch.int16), b.view(torch.int16))
+                   for k in res for a, b in zip(res[k], res['lane-pair ']))
+        print(f'  bit-identical: {same}', flush=True)
+ops.CLIP_TOKEN_LANE = True
+N.load().lcq_auto_clip_force_variant(0)
+print(f'one Llama-3-8B block (v, o, gate, up, down; sym, row-lane): {tot_ms:.1f} ms')

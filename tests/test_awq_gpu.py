@@ -127,6 +127,55 @@ def test_auto_clip_vs_reference(dev, name):
     assert torch.equal(bits(w), bits(c['w_clipped']))
 
 
+@pytest.mark.parametrize('variant', [2, 1])
+@pytest.mark.parametrize('oc,ic,T,dt,sym,clip_sym,small_ws', [
+    (1024, 4096, 512, torch.bfloat16, True, True, False),     # v_proj, the AWQ headline
+    (100, 384, 300, torch.bfloat16, False, False, True),      # ragged rows / tokens
+    (77, 256, 40, torch.float16, True, False, False),         # fp16, fewer tokens than a wave
+    (400, 512, 512, torch.bfloat16, False, True, True)])      # 3 row chunks
+def test_auto_clip_scalar_operand_matches_pair_kernel(dev, monkeypatch, variant, oc, ic, T, dt,
+                                                      sym, clip_sym, small_ws):
+    """lcq_auto_clip_search_ws (the candidate table + the row-lane kernel with the tokens as
+    scalar operands, or the token-lane kernel with the candidates as scalar operands) is
+    bit-identical to k_auto_clip (lcq_auto_clip_search_act) -- the same products, 8-way
+    partial sums, halving tree and token-order error sums -- including ragged tokens and rows,
+    fp16, and row chunks of a small workspace."""
+    from lightcompress_amd import _native as N
+    from lightcompress_amd import ops
+    g = torch.Generator(device=dev).manual_seed(oc + ic + T)
+    w = (torch.randn(oc, ic, generator=g, device=dev) * 0.02).to(dt)
+    x = (torch.randn(T, ic, generator=g, device=dev) *
+         torch.exp(torch.randn(ic, generator=g, device=dev))).to(dt)
+    if dt == torch.float16:
+        x = (x.float() * 1e-3).to(dt)
+    qmin, qmax = (-8, 7) if sym else (0, 15)
+    monkeypatch.setattr(ops, 'CLIP_TOKEN_LANE', False)
+    ref = ops.auto_clip_search(w, x, 128, 10, 20, qmin, qmax, sym, clip_sym)
+    monkeypatch.setattr(ops, 'CLIP_TOKEN_LANE', True)
+    lib = N.load()
+    assert lib.lcq_auto_clip_force_variant(variant) == 0
+    try:
+        if not small_ws:
+            got = ops.auto_clip_search(w, x, 128, 10, 20, qmin, qmax, sym, clip_sym)
+        else:   # a 192-row table: several chunks
+            per = int(lib.lcq_auto_clip_workspace_bytes(1, ic, T, 128, 10))
+            assert per > 0
+            ws = torch.empty(per, dtype=torch.uint8, device=dev)
+            factors = torch.tensor([1 - i / 20 for i in range(10)], dtype=torch.float32,
+                                   device=dev)
+            ng = ic // 128
+            got = (torch.empty((oc, ng, 1), dtype=dt, device=dev),
+                   torch.empty((oc, ng, 1), dtype=dt, device=dev))
+            N.call('lcq_auto_clip_search_ws', w.data_ptr(), x.data_ptr(), None, N.dt(w), oc, ic,
+                   T, 128, 10, factors.data_ptr(), qmin, qmax, int(sym), int(clip_sym), 0, None,
+                   0.0, got[0].data_ptr(), got[1].data_ptr(), ws.data_ptr(), per,
+                   N.stream_of(w))
+    finally:
+        lib.lcq_auto_clip_force_variant(0)
+    for a, b in zip(got, ref):
+        assert torch.equal(bits(a), bits(b))
+
+
 @pytest.mark.parametrize('subset', ['qkv', 'mlp', 'down'])
 @pytest.mark.parametrize('sym', [True, False])
 @pytest.mark.parametrize('version', ['v2', 'v1'])
