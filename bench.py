@@ -338,18 +338,24 @@ PEAK_CLIP_GPRODUCTS = 1024 * 2.4 / 2 * 32   # 3.93e4 G products/s
 
 def clip_roofline(kern):
     """The auto-clip search (AutoClipper.auto_clip_layer, auto_clip.py:83-191) against its
-    VALU issue bound: products per second over the launches' HIP-event time."""
-    t = kern.get('lcq_auto_clip_search_ws') or kern.get('lcq_auto_clip_search_act')
-    if not t or not t.get('flops'):
+    VALU issue bound: products per second over the launches' HIP-event time, both entries
+    together (lcq_auto_clip_search_ws runs the layers below 65536 row-groups on the token-lane
+    kernel, lcq_auto_clip_search_act the rest on the lane-pair k_auto_clip)."""
+    ts = [kern[k] for k in ('lcq_auto_clip_search_ws', 'lcq_auto_clip_search_act')
+          if kern.get(k) and kern[k].get('flops')]
+    if not ts:
         return None
-    gp = t['flops'] / (t['total_ms'] * 1e-3) / 1e9
-    return {'kernel': ('lcq_auto_clip_search_ws (k_clip_qtable + k_auto_clip_rl: one lane per '
-                       'weight row, the sampled tokens as scalar operands)'
-                       if 'lcq_auto_clip_search_ws' in kern else 'lcq_auto_clip_search_act'),
+    flops = sum(t['flops'] for t in ts)
+    ms = sum(t['total_ms'] for t in ts)
+    launches = sum(t['launches'] for t in ts)
+    gp = flops / (ms * 1e-3) / 1e9
+    return {'kernel': ('k_auto_clip (two weight rows per lane pair; layers of >= 65536 '
+                       'row-groups) + k_clip_qtable / k_auto_clip_tl (one lane per token, the '
+                       'candidates as scalar operands; v_proj)'),
             'bound': 'valu', 'achieved': round(gp, 1), 'peak': PEAK_CLIP_GPRODUCTS,
             'unit': 'G products/s', 'frac': round(gp / PEAK_CLIP_GPRODUCTS, 4),
-            'avg_launch_ms': round(t['avg_ms'], 4),
-            'products_per_launch': t['flops'] / t['launches'],
+            'avg_launch_ms': round(ms / launches, 4), 'launches': launches,
+            'products_per_launch': flops / launches,
             'pmc_source': 'profiles/r6_clip_pmc.txt'}
 
 
@@ -683,7 +689,11 @@ def bench_e2e(args, rank, world, dev, which, residency='device'):
         st = model.streamer.stats
         out['streamed'] = {'h2d_gb': round(st['h2d_bytes'] / 2 ** 30, 2),
                            'd2h_gb': round(st['d2h_bytes'] / 2 ** 30, 2),
-                           'fetches': st['fetches'], 'prefetched': st['prefetched']}
+                           'fetches': st['fetches'], 'prefetched': st['prefetched'],
+                           'pin_alloc_gb': round(st['pin_alloc_bytes'] / 2 ** 30, 2),
+                           'pin_alloc_s': round(st['pin_alloc_s'], 3),
+                           'evict_host_s': round(st['evict_host_s'], 3),
+                           'deploy_s': round(elapsed - t_loop, 3)}
     algo.release()
     del algo, model, hidden, calib
     free_device()

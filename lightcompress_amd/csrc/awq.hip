@@ -1272,9 +1272,14 @@ static int64_t tl_row_bytes(int64_t ic, int nsteps) {
 static constexpr int64_t TL_ROWS_PER_WG = TL_WAVES * TL_RB;   // token-lane rows per workgroup
 static constexpr int64_t CL_ROW_UNIT = 192;   // chunk rows: whole workgroups of both kernels
 static constexpr int TL_NS = 10;   // the kernels' shrink-step count
+static constexpr int64_t CL_PAIR_MIN_ROWGROUPS = 65536;   // automatic choice, see below
 
-// A/B probe hook (scripts/clip_rate.py): 0 = automatic (row-lane), 1 = token-lane,
-// 2 = row-lane. Process-wide; not for production use.
+// A/B probe hook (scripts/clip_rate.py): 0 = automatic, 1 = token-lane, 2 = row-lane.
+// Process-wide; not for production use. Automatic (profiles/r6_clip_rate.txt, Llama-3-8B
+// shapes): the token-lane kernel while the row-groups leave the lane-pair k_auto_clip's grid
+// short of the chip (v_proj 1024 x 4096: 2.46 vs 3.23 ms), k_auto_clip (lcq_auto_clip_search_act)
+// from 65536 row-groups up (o / gate / up / down: 8.25 / 27.1 ms against 10.2 / 34.6 for the
+// token-lane and 11.4 / 49.5 for the row-lane kernel). All three give the same bits.
 static int g_clip_variant = 0;
 extern "C" int lcq_auto_clip_force_variant(int v) {
   LCQ_REQUIRE(v >= 0 && v <= 2, "variant: 0, 1 or 2");
@@ -1285,6 +1290,7 @@ extern "C" int lcq_auto_clip_force_variant(int v) {
 extern "C" int64_t lcq_auto_clip_workspace_bytes(int64_t oc, int64_t ic, int64_t T, int group,
                                                  int nsteps) {
   if (group != TL_G || oc <= 0 || ic <= 0 || T <= 0 || ic % TL_G || nsteps != TL_NS) return 0;
+  if (g_clip_variant == 0 && oc * (ic / TL_G) >= CL_PAIR_MIN_ROWGROUPS) return 0;  // k_auto_clip
   const int64_t per = tl_row_bytes(ic, nsteps);
   int64_t rows = ((int64_t)1 << 30) / per / CL_ROW_UNIT * CL_ROW_UNIT;
   if (rows < CL_ROW_UNIT) rows = CL_ROW_UNIT;
@@ -1306,14 +1312,15 @@ extern "C" int lcq_auto_clip_search_ws(const void* w, const void* x, const void*
       per && ws_bytes > xbytes ? (ws_bytes - xbytes) / per / CL_ROW_UNIT * CL_ROW_UNIT : 0;
   const bool al16 = ((reinterpret_cast<uintptr_t>(workspace) | reinterpret_cast<uintptr_t>(x)) &
                      15) == 0;
+  const bool pair_wins = g_clip_variant == 0 && oc * (ic / TL_G) >= CL_PAIR_MIN_ROWGROUPS;
   if (qx != nullptr || mse_steps != 0 || chunk < CL_ROW_UNIT || workspace == nullptr || !al16 ||
-      (dtype != LCQ_BF16 && dtype != LCQ_F16) || qmax <= qmin)
+      (dtype != LCQ_BF16 && dtype != LCQ_F16) || qmax <= qmin || pair_wins)
     return lcq_auto_clip_search_act(w, x, qx, dtype, oc, ic, T, group, nsteps, factors, qmin,
                                     qmax, sym, clip_sym, mse_steps, mse_p, norm, best_max,
                                     best_min, stream);
   hipStream_t st = as_stream(stream);
   const int64_t ng = ic / TL_G;
-  const bool rl = g_clip_variant != 1;
+  const bool rl = g_clip_variant == 2;
   float* xt = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + chunk * per);
   float* qt = reinterpret_cast<float*>(workspace);
   const auto* wp = reinterpret_cast<const uint16_t*>(w);

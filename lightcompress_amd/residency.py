@@ -23,6 +23,7 @@ MI355X-first placements (YAML ``model.residency`` / ``model.materialize``):
 from __future__ import annotations
 
 import re
+import time
 import weakref
 
 import torch
@@ -89,7 +90,8 @@ class BlockStreamer:
         self.pending = {}        # block -> (event, moves)
         self.resident = set()
         self.host = {}           # (id(module), kind, name) -> (weakref(module), pinned host)
-        self.stats = {'h2d_bytes': 0, 'd2h_bytes': 0, 'fetches': 0, 'prefetched': 0}
+        self.stats = {'h2d_bytes': 0, 'd2h_bytes': 0, 'fetches': 0, 'prefetched': 0,
+                      'pin_alloc_bytes': 0, 'pin_alloc_s': 0.0, 'evict_host_s': 0.0}
 
     def __len__(self):
         return len(self.blocks)
@@ -154,6 +156,7 @@ class BlockStreamer:
         are still current, nothing is copied."""
         if i not in self.resident:
             return
+        t_ev = time.perf_counter()
         block = self.blocks[i]
         _scrub(block)
         main = torch.cuda.current_stream(self.dev)
@@ -165,7 +168,10 @@ class BlockStreamer:
                 h = self._host_of(m, kind, n)
                 if dirty or h is None or h.shape != d.shape or h.dtype != d.dtype:
                     if h is None or h.shape != d.shape or h.dtype != d.dtype:
+                        t_al = time.perf_counter()
                         h = torch.empty(d.shape, dtype=d.dtype, pin_memory=True)
+                        self.stats['pin_alloc_s'] += time.perf_counter() - t_al
+                        self.stats['pin_alloc_bytes'] += d.numel() * d.element_size()
                         self.host[(id(m), kind, n)] = (weakref.ref(m), h)
                     h.copy_(d, non_blocking=True)
                     self.stats['d2h_bytes'] += d.numel() * d.element_size()
@@ -175,6 +181,7 @@ class BlockStreamer:
         # modules replaced since (deploy swaps the linears): release their host copies
         for k in [k for k, (ref, _) in self.host.items() if ref() is None]:
             del self.host[k]
+        self.stats['evict_host_s'] += time.perf_counter() - t_ev
 
     def drain(self):
         self.d2h.synchronize()
