@@ -692,6 +692,8 @@ def bench_e2e(args, rank, world, dev, which, residency='device'):
                            'fetches': st['fetches'], 'prefetched': st['prefetched'],
                            'pin_alloc_gb': round(st['pin_alloc_bytes'] / 2 ** 30, 2),
                            'pin_alloc_s': round(st['pin_alloc_s'], 3),
+                           'pin_ahead_gb': round(st['pin_ahead_bytes'] / 2 ** 30, 2),
+                           'pin_recycled_gb': round(st['pin_recycled_bytes'] / 2 ** 30, 2),
                            'evict_host_s': round(st['evict_host_s'], 3),
                            'deploy_s': round(elapsed - t_loop, 3)}
     algo.release()

@@ -25,6 +25,7 @@ import torch.nn as nn
 
 from . import ops
 from . import parallel as P
+from .base_model import retire_module
 from .module_utils import (_LLMC_LINEAR_TYPES_, _REALQUANT_LINEAR_MAP_,
                            _TRANSFORMERS_LINEAR_TYPES_, EffcientFakeQuantLinear,
                            FakeQuantLinear, OriginFloatLinear)
@@ -919,6 +920,9 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
 
     def _deploy_blocks(self, module, real, params, rank, own, pending, sharded, local_attrs):
         for i, block in enumerate(self.blocks):
+            if not sharded and self._deploy_from_memos(i, block, module, params):
+                continue
+
             def one(i=i, block=block):
                 self.block_idx = i
                 lins = self.model.get_block_linears(block)
@@ -939,6 +943,44 @@ class BaseBlockwiseQuantization(BlockwiseOpt):
             self.visit_block(i, one, next_i=i + 1)
         self._drain_blocks()
         self._pending_owner = None
+
+    def _deploy_from_memos(self, i, block, module, params) -> bool:
+        """A host-streamed block deployed as EffcientFakeQuantLinear without passing through
+        HBM: the quant_out forward left every FakeQuantLinear of the block with its memo
+        tmp_weight = w_qdq(self) (module_utils.FakeQuantLinear.forward, written back to pinned
+        host memory with the block), which is what EffcientFakeQuantLinear.new computes from
+        the same weight, qparams buffers and w_qdq (module_utils.py:815-819) -- the same bits,
+        with no upload of the fp32 weights and no download of the result (VERDICT r5 next 7:
+        the streamed GPTQ deploy moved 28 GB each way). Taken only when the block is on the
+        host and every linear has such a memo made by the deploy's own callbacks; otherwise
+        the block goes through visit_block as before."""
+        st = getattr(self.model, 'streamer', None)
+        if (st is None or module is not EffcientFakeQuantLinear or i in st.resident
+                or i in st.pending):
+            return False
+        lins = self.model.get_block_linears(block)
+        todo = {n: m for n, m in lins.items() if not getattr(m, 'no_quant', False)}
+        same = self.model._same_fake_quant
+        for m in todo.values():
+            tw = m._buffers.get('tmp_weight') if isinstance(m, FakeQuantLinear) else None
+            if (tw is None or tw.device.type != 'cpu' or tw.dtype == torch.float8_e4m3fn
+                    or m.dynamic_quant_weight or m.dynamic_quant_tmp_weight
+                    or not same(m, FakeQuantLinear, params)):
+                return False
+        self.block_idx = i
+        for name, m in todo.items():
+            new = EffcientFakeQuantLinear(m._buffers['tmp_weight'], m.bias, ori_module=m,
+                                          a_qdq=params.get('a_qdq'))
+            new.in_features, new.out_features = m.in_features, m.out_features
+            new.w_qdq_name, new.a_qdq_name = m.w_qdq_name, m.a_qdq_name
+            new.debug_print = {}
+            parent_name, _, child = name.rpartition('.')
+            parent = block.get_submodule(parent_name) if parent_name else block
+            setattr(parent, child, new)
+            retire_module(m)
+            st.stats['host_deployed_modules'] += 1
+        self._clear_block_cache(block)
+        return True
 
     @torch.no_grad()
     def _prequant_fp8_block(self, block, mods: dict):

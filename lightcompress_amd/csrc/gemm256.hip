@@ -94,12 +94,18 @@ struct Args {
   float* x6_part;
 };
 
-// work slot -> tile (4 x 8 blocks of tiles, bands of 4 tile rows walked along N)
+// chunk shape (probe build -DLCQ_PROBE_GEMM_CM=<tile rows per 32-tile chunk>; default 4 x 8)
+#ifndef LCQ_PROBE_GEMM_CM
+#define LCQ_PROBE_GEMM_CM 4
+#endif
+constexpr int CH_M = LCQ_PROBE_GEMM_CM, CH_N = 32 / CH_M;
+
+// work slot -> tile (CH_M x CH_N blocks of tiles, bands of CH_M tile rows walked along N)
 __device__ __forceinline__ bool slot_tile(const Args& a, int slot, int& tm, int& tn) {
   const int chunk = slot >> 5, s = slot & 31;
   const int band = chunk / a.cpb, c = chunk - band * a.cpb;
-  tm = band * 4 + (s >> 3);
-  tn = c * 8 + (s & 7);
+  tm = band * CH_M + s / CH_N;
+  tn = c * CH_N + s % CH_N;
   return tm < a.n_mt && tn < a.n_nt;
 }
 
@@ -780,8 +786,8 @@ static constexpr int tile_order() { return LCQ_PROBE_GEMM_ORDER; }
 static void plan(Args& a, int64_t tile_n) {
   a.n_mt = (int)((a.m + ST - 1) / ST);
   a.n_nt = (int)((a.n + tile_n - 1) / tile_n);
-  a.cpb = (a.n_nt + 7) / 8;
-  const int bands = (a.n_mt + 3) / 4;
+  a.cpb = (a.n_nt + CH_N - 1) / CH_N;
+  const int bands = (a.n_mt + CH_M - 1) / CH_M;
   a.nslots = 32 * bands * a.cpb;
   a.order = tile_order();
   if (a.order == 1) a.nslots = 256 * ((a.n_mt + 31) / 32) * a.cpb;

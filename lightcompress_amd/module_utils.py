@@ -135,6 +135,13 @@ class FakeQuantLinear(nn.Module):
             self.tmp_weight = self.w_qdq(self)
         return lcq_linear(x, self.tmp_weight, self.tmp_bias)
 
+    def _lcq_after_move(self):
+        """The block was moved between HBM and the host (residency.BlockStreamer): tmp_bias is
+        a plain alias of the bias buffer set by the memoising forward, re-pointed at the
+        buffer's new home so it never pins the old copy."""
+        if 'tmp_bias' in self.__dict__:
+            self.tmp_bias = self.bias
+
     @classmethod
     @torch.no_grad()
     def new(cls, module, w_qdq, a_qdq):

@@ -23,6 +23,7 @@ MI355X-first placements (YAML ``model.residency`` / ``model.materialize``):
 from __future__ import annotations
 
 import re
+import sys
 import time
 import weakref
 
@@ -91,7 +92,52 @@ class BlockStreamer:
         self.resident = set()
         self.host = {}           # (id(module), kind, name) -> (weakref(module), pinned host)
         self.stats = {'h2d_bytes': 0, 'd2h_bytes': 0, 'fetches': 0, 'prefetched': 0,
-                      'pin_alloc_bytes': 0, 'pin_alloc_s': 0.0, 'evict_host_s': 0.0}
+                      'pin_alloc_bytes': 0, 'pin_alloc_s': 0.0, 'evict_host_s': 0.0,
+                      'pin_ahead_bytes': 0, 'pin_recycled_bytes': 0, 'host_new': 0,
+                      'host_retyped': 0, 'host_released': 0, 'host_deployed_modules': 0}
+        # Fresh page-locked memory costs ~11 ms of host time per 224 MiB (hipHostMalloc at
+        # ~20 GiB/s, profiles/r6_stream_gptq.md), and a GPTQ block turns its 7 bf16 linears
+        # into FakeQuantLinear with fp32 weights (gptq.py:193) -- 0.87 GB of new host copies
+        # per Llama-3-8B block, then the deploy's new modules as much again. Remedies, none
+        # changing a byte: replaced modules' host tensors are handed to their replacements
+        # (evict's pool); copies that still had to be allocated are allocated ahead for the
+        # next block on a worker thread (torch.empty releases the GIL) while the GPU works.
+        # (A fake-quant deploy of a streamed block builds its modules on the host from the
+        # FakeQuantLinear memos: BaseBlockwiseQuantization._deploy_from_memos.)
+        self._ahead = []         # futures of [(shape, dtype, pinned tensor)] for the next block
+        self._pool = None
+
+    def _take_pinned(self, shape, dtype):
+        """A pinned host tensor of (shape, dtype): one allocated ahead if any, else a new one."""
+        key = (tuple(shape), dtype)
+        for fut in self._ahead:
+            bufs = fut.result()   # waits for the worker if it is still allocating
+            for j, (shp, dt, t) in enumerate(bufs):
+                if (shp, dt) == key:
+                    del bufs[j]
+                    return t
+        t_al = time.perf_counter()
+        h = torch.empty(shape, dtype=dtype, pin_memory=True)
+        self.stats['pin_alloc_s'] += time.perf_counter() - t_al
+        self.stats['pin_alloc_bytes'] += h.numel() * h.element_size()
+        return h
+
+    def _allocate_ahead(self, wants):
+        """Allocate pinned host tensors for [(shape, dtype)] on the worker thread."""
+        if self._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix='lcq-pin')
+        self._ahead = [f for f in self._ahead if not f.done() or f.result()]
+        self.stats['pin_ahead_bytes'] += sum(
+            torch.Size(s).numel() * torch.empty((), dtype=d).element_size() for s, d in wants)
+        self._ahead.append(self._pool.submit(
+            lambda: [(s, d, torch.empty(s, dtype=d, pin_memory=True)) for s, d in wants]))
+
+    def release_ahead(self):
+        """Drop host tensors allocated ahead and not used (end of a pass over the blocks)."""
+        for fut in self._ahead:
+            fut.result()
+        self._ahead = []
 
     def __len__(self):
         return len(self.blocks)
@@ -159,8 +205,14 @@ class BlockStreamer:
         t_ev = time.perf_counter()
         block = self.blocks[i]
         _scrub(block)
+        # host copies of modules replaced since (deploy swaps the linears): their exclusively
+        # held tensors serve the new modules' copies of the same shape and dtype (the D2H
+        # stream writes them only after the compute stream, which waited for this block's
+        # upload from them); the rest are released to the caching host allocator
+        pool = self._release_dead()
         main = torch.cuda.current_stream(self.dev)
         self.d2h.wait_stream(main)   # after every kernel that wrote this block
+        misses = []
         with torch.cuda.stream(self.d2h):
             for m, kind, n, d in list(_tensor_slots(block)):
                 if d.device.type != 'cuda':
@@ -168,24 +220,51 @@ class BlockStreamer:
                 h = self._host_of(m, kind, n)
                 if dirty or h is None or h.shape != d.shape or h.dtype != d.dtype:
                     if h is None or h.shape != d.shape or h.dtype != d.dtype:
-                        t_al = time.perf_counter()
-                        h = torch.empty(d.shape, dtype=d.dtype, pin_memory=True)
-                        self.stats['pin_alloc_s'] += time.perf_counter() - t_al
-                        self.stats['pin_alloc_bytes'] += d.numel() * d.element_size()
+                        self.stats['host_new' if h is None else 'host_retyped'] += 1
+                        key = (tuple(d.shape), d.dtype)
+                        if pool.get(key):
+                            h = pool[key].pop()
+                            self.stats['pin_recycled_bytes'] += d.numel() * d.element_size()
+                        else:
+                            # the next block will most likely need the same: allocated ahead
+                            misses.append(key)
+                            h = self._take_pinned(d.shape, d.dtype)
                         self.host[(id(m), kind, n)] = (weakref.ref(m), h)
                     h.copy_(d, non_blocking=True)
                     self.stats['d2h_bytes'] += d.numel() * d.element_size()
                 d.record_stream(self.d2h)   # HBM reusable only once the copy has run
                 _install(m, kind, n, h)
+        for m in block.modules():   # plain attributes aliasing a moved buffer (tmp_bias)
+            moved = getattr(m, '_lcq_after_move', None)
+            if moved is not None:
+                moved()
+        del pool
         self.resident.discard(i)
-        # modules replaced since (deploy swaps the linears): release their host copies
-        for k in [k for k, (ref, _) in self.host.items() if ref() is None]:
-            del self.host[k]
+        if misses and i + 1 < len(self.blocks):
+            self._allocate_ahead(misses)
         self.stats['evict_host_s'] += time.perf_counter() - t_ev
+
+    def _release_dead(self):
+        """Drop the host copies of modules that no longer exist; returns those no one else
+        holds, by (shape, dtype), for reuse."""
+        pool = {}
+        for k in [k for k, (ref, _) in self.host.items() if ref() is None]:
+            h = self.host.pop(k)[1]
+            self.stats['host_released'] += 1
+            # exclusive: no other tensor on its storage (the temporary storage object aside)
+            # and no other Python reference (the name h and getrefcount's argument aside), so
+            # overwriting it is invisible to anyone
+            if (torch._C._storage_Use_Count(h.untyped_storage()._cdata) <= 2
+                    and sys.getrefcount(h) <= 2):
+                pool.setdefault((tuple(h.shape), h.dtype), []).append(h)
+            del h
+        return pool
 
     def drain(self):
         self.d2h.synchronize()
         self.h2d.synchronize()
+        self.release_ahead()
+        self._release_dead()
 
 
 class Ownership:

@@ -5,6 +5,7 @@ reads at run time (they change tile orders or fp32 fold orders):
   LCQ_PROBE_SYRK_GNS=<n>   force lcq_hessian_grouped's per-group splits (csrc/hessian.hip)
   LCQ_PROBE_GEMM_ORDER=1   k_gemm16b N-band-major tile order           (csrc/gemm256.hip)
   LCQ_PROBE_GEMM_PP=0      the round-4 4-barrier k_gemm16b body         (csrc/gemm256.hip)
+  LCQ_PROBE_GEMM_CM=<m>    k_gemm16h XCD chunk of m x (32/m) tiles      (csrc/gemm256.hip)
   LCQ_PROBE_CHOL_IEEE_RSQ=1  IEEE sqrtf / division in the tile's S1      (csrc/chol.hip)
 
 usage: python scripts/probe_build.py <tag> NAME=VALUE [NAME=VALUE ...]

@@ -20,6 +20,7 @@ from lightcompress_amd.pipeline import build_algo  # noqa: E402
 from transformers import LlamaConfig  # noqa: E402
 
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+profile = len(sys.argv) <= 2 or sys.argv[2] != "noprof"
 dev = torch.device('cuda:0')
 from lightcompress_amd import _native  # noqa: E402
 _native.load()
@@ -64,7 +65,8 @@ def run(residency, prof=None):
 
 
 run('device')
-prof = cProfile.Profile()
+prof = cProfile.Profile() if profile else None
 run('stream', prof)
-st = pstats.Stats(prof)
-st.sort_stats('tottime').print_stats(25)
+if prof is not None:
+    st = pstats.Stats(prof)
+    st.sort_stats('tottime').print_stats(25)

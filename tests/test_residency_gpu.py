@@ -38,6 +38,11 @@ def test_stream_bit_identical_to_resident(dev, name):
     assert st.stats['fetches'] >= n and st.stats['h2d_bytes'] > 0, st.stats
     if name != 'rtn':
         assert st.stats['prefetched'] >= 1, st.stats
+    if name == 'gptq':
+        # the fake-quant deploy built every block's modules on the host from the
+        # FakeQuantLinear memos (no block went through HBM for it): same bits as the resident
+        # run's w_qdq at deploy
+        assert st.stats['host_deployed_modules'] == 7 * n, st.stats
     # and is back on the host, pinned
     for b in model.get_blocks():
         for t in [*b.parameters(), *b.buffers()]:
