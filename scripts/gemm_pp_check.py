@@ -41,5 +41,22 @@ for (M, N, K) in [(65536, 4096, 4096), (1000, 784, 512), (257, 272, 128), (4096,
         ops.linear_sq_diff(x, w, org, lb, 0)
         ops.linear_sq_diff(x, w, org, lb, 1, bias=b)
         print('sqdiff', M, N, K, dt, h(lb.out), lb.out.tolist())
+# q/k/v with the rotary in the epilogue (lcq_gemm_rope), ragged rows
+for B, S in ((2, 384), (3, 100)):
+    x = rnd(B, S, 512)
+    ws = [rnd(n, 512, sc=0.05) for n in (512, 256, 256)]
+    cos, sin = rnd(B, S, 128), rnd(B, S, 128)
+    print('rope', B, S, *[h(o) for o in ops.linear_multi_rope(x, ws, [None] * 3, cos, sin,
+                                                             rope_segs=2)])
+# split-plane fp32 products (lcq_gemm_f32x6): split K below 256 tiles, k-major A, row ranges
+for (M, N, K, at) in [(3584, 3584, 7168, False), (1792, 1792, 1792, False),
+                      (4096, 3072, 1024, True), (1000, 528, 1100, False)]:
+    A = torch.randn((K, M) if at else (M, K), generator=g, device='cuda')
+    Bm = torch.randn(K, N, generator=g, device='cuda')
+    C = torch.randn(M, N, generator=g, device='cuda')
+    ops.gemm_f32x6(A, Bm, C, -1.0, 1.0, False, a_trans=at)
+    C2 = torch.randn(M, N, generator=g, device='cuda')
+    ops.gemm_f32x6(A, Bm, C2, 1.0, 0.0, False, M // 4, M // 2, a_trans=at)
+    print('x6', M, N, K, at, h(C), h(C2[M // 4:M // 2]))
 torch.cuda.synchronize()
 print('done')
