@@ -38,6 +38,9 @@
 // the epilogues. Tile order is XCD-aware: consecutive work ids go to one XCD and a chunk of
 // 32 = a 4 (M) x 8 (N) block of tiles shares 12 operand panels in L2.
 #define LCQ_BF16_HW 1  // conversion-instruction RNE in the epilogues
+#ifndef LCQ_PROBE_GEMM_PP
+#define LCQ_PROBE_GEMM_PP 2
+#endif
 #include "lcq_common.h"
 
 namespace lcq {
@@ -757,143 +760,6 @@ __global__ void __launch_bounds__(256, 1) k_gemm16h(Args a) {
   epi16<DT, EPI, 8>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
 }
 
-// ---------------------------------------------------------------------------------------
-// k_gemm16t (probe build -DLCQ_PROBE_GEMM_PP=3): k_gemm16h with the B operand three K-tiles
-// deep. B panels are the ones re-read per band of 4 tile rows (n_mt / 4 times, mostly from the
-// MALL), so their DMA gets one more K-tile of lead: LDS = A ring of 2 + B ring of 3 K-tiles
-// (160 KB, the whole CU). K-tile t reads A from ring slot t % 2 and B from slot t % 3; A(t + 2)
-// is loaded into A's slot after barrier 1 and B(t + 3) into B's slot after barrier 2, as in
-// k_gemm16h. Barrier 3 waits for A(t + 1) and B(t + 1) with the 21 younger pieces (B(t + 2),
-// A(t + 2) and the first 5 of B(t + 3)) still in flight. Same MFMAs in the same order:
-// identical outputs.
-// ---------------------------------------------------------------------------------------
-constexpr int RING_A = 2, RING_B = 3;
-constexpr int LDS_T = (RING_A + RING_B) * TILE_B;   // 160 KB
-
-__device__ __forceinline__ void load_bt(const Stage4& st, char* bbuf, int kofs, int w, int j) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(((st.bsel >> j) & 1) ? st.rb[1] : st.rb[0],
-                                           (lds_void_t*)(bbuf + (w + 4 * j) * 1024), 16,
-                                           st.boff[j], kofs, 0, 0);
-}
-
-template <bool FP16>
-__device__ __forceinline__ void ktile16t(v4f (&acc)[8][8], v8s (&x0a)[8], v8s (&x0b)[8],
-                                         v8s (&x1a)[8], v8s (&x1b)[8], const Stage4& st,
-                                         int kofs_a, int kofs_b, char* ac, char* bc,
-                                         const char* an, const char* bn, int w, int wr, int wc,
-                                         int lane) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    const int i = h * 64 + m * 8 + n;
-    if (h == 0) mfma16a<FP16>(acc[m][n], x0b[n], x0a[m]);
-    else mfma16a<FP16>(acc[m][n], x1b[n], x1a[m]);
-    if (i < 16 && (i & 1) == 0) x1a[i >> 1] = read_frag(ac, wr * 8 + (i >> 1), 1, lane);
-    if (i == 20) lgkm_barrier();
-    if (i >= 22 && i <= 34 && (i - 22) % 3 == 0) load_a(st, ac, kofs_a, w, (i - 22) / 3);
-    if (i == 24 || i == 27 || i == 30 || i == 33 || i == 36 || i == 38 || i == 40 || i == 42) {
-      const int f = i <= 36 ? (i - 24) / 3 : 5 + (i - 38) / 2;
-      x1b[f] = read_frag(bc, wc * 8 + f, 1, lane);
-    }
-    if (i == 50) lgkm_barrier();
-    if (i == 52 || i == 55 || i == 58) load_a(st, ac, kofs_a, w, 5 + (i - 52) / 3);
-    if (i == 61 || i == 64) load_bt(st, bc, kofs_b, w, (i - 61) / 3);
-    if (i == 85 || i == 87 || i == 89) load_bt(st, bc, kofs_b, w, 2 + (i - 85) / 2);
-    if (i == 91) {
-      asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    if (i >= 93 && i <= 100) x0a[i - 93] = read_frag(an, wr * 8 + (i - 93), 0, lane);
-    if (i >= 101 && i <= 115 && ((i - 101) & 1) == 0)
-      x0b[(i - 101) >> 1] = read_frag(bn, wc * 8 + ((i - 101) >> 1), 0, lane);
-    if (i == 96 || i == 100) load_bt(st, bc, kofs_b, w, 5 + (i - 96) / 4);
-    if (i == 124) load_bt(st, bc, kofs_b, w, 7);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-template <int DT, int EPI>
-__global__ void __launch_bounds__(256, 1) k_gemm16t(Args a) {
-  constexpr bool FP16 = DT == LCQ_F16;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  int tm, tn;
-  {
-    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    if (!slot_tile(a, wgid, tm, tn)) return;
-  }
-  int64_t nk = a.k / SKT;
-  int kt0 = 0;
-  if constexpr (EPI == EPI_F32) {
-    if (a.x6_splits > 1) {
-      const int y = blockIdx.y;
-      kt0 = (int)(nk * y / a.x6_splits);
-      nk = nk * (y + 1) / a.x6_splits - kt0;
-    }
-  }
-  Stage4 st;
-  make_stage16<EPI>(a, tm, tn, w, lane, st);
-  char* const ra = lds;                        // A ring: slots 0, 1
-  char* const rb = lds + RING_A * TILE_B;      // B ring: slots 0, 1, 2
-  v4f acc[8][8];
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-    for (int n = 0; n < 8; ++n) acc[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
-  v8s x0a[8], x0b[8], x1a[8], x1b[8];
-  auto kofs_of = [&](int64_t kt, uint32_t roles) -> int {
-    if (kt > nk - 1) kt = nk - 1;
-    if constexpr (EPI == EPI_F32) {
-      kt += kt0;
-      const int sgm = (int)(kt / a.x6_kt);
-      const int p = (int)((roles >> (2 * sgm)) & 3u);
-      return (int)((p * a.x6_kp + (kt - (int64_t)sgm * a.x6_kt) * SKT) * 2);
-    } else {
-      (void)roles;
-      return (int)(kt * (SKT * 2));
-    }
-  };
-  // prologue, in issue order A0 B0 A1 B1 B2 (barrier 3's counts assume it)
-#pragma unroll
-  for (int j = 0; j < 8; ++j) load_a(st, ra, kofs_of(0, a.x6_roles_a), w, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) load_bt(st, rb, kofs_of(0, a.x6_roles_b), w, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) load_a(st, ra + TILE_B, kofs_of(1, a.x6_roles_a), w, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) load_bt(st, rb + TILE_B, kofs_of(1, a.x6_roles_b), w, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) load_bt(st, rb + 2 * TILE_B, kofs_of(2, a.x6_roles_b), w, j);
-  wait_barrier<24>();  // K-tile 0 landed
-#pragma unroll
-  for (int m = 0; m < 8; ++m) x0a[m] = read_frag(ra, wr * 8 + m, 0, lane);
-#pragma unroll
-  for (int n = 0; n < 8; ++n) x0b[n] = read_frag(rb, wc * 8 + n, 0, lane);
-  asm volatile("s_nop 4" ::: "memory");  // accumulator init (VALU) -> first MFMA srcC
-  int sa = 0, sb = 0;   // ring slots of K-tile t
-  for (int64_t t = 0; t < nk; ++t) {
-    const int sa1 = sa ^ 1, sb1 = sb == 2 ? 0 : sb + 1;
-    ktile16t<FP16>(acc, x0a, x0b, x1a, x1b, st, kofs_of(t + 2, a.x6_roles_a),
-                   kofs_of(t + 3, a.x6_roles_b), ra + sa * TILE_B, rb + sb * TILE_B,
-                   ra + sa1 * TILE_B, rb + sb1 * TILE_B, w, wr, wc, lane);
-    sa = sa1;
-    sb = sb1;
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 7"
-               : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]),
-                 "+a"(acc[7][4]), "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7])
-               :
-               : "memory");
-  epi16<DT, EPI, 8>(a, acc, tm, tn, w, wr, wc, lane, tid, lds);
-}
-
 // one 1024-thread workgroup: thread l sums partials l, l + 1024, ... in order, then a fixed
 // xor tree per wave and the 16 wave sums in wave order (deterministic; 16 K partials at the
 // down_proj shape: one wave took ~0.1 ms, 240 launches per AWQ block step)
@@ -931,24 +797,14 @@ static void plan(Args& a, int64_t tile_n) {
 }
 
 // kernel: 2 = k_gemm16h (the product), 0 = k_gemm16b (probe build -DLCQ_PROBE_GEMM_PP=0, for
-// A/B runs: 1.5-3 % slower on the AWQ shapes, profiles/r5_gemm_variants.md)
-#ifndef LCQ_PROBE_GEMM_PP
-#define LCQ_PROBE_GEMM_PP 2
-#endif
+// A/B runs: 1.5-3 % slower on the AWQ shapes, profiles/r5_gemm_variants.md). Round 6 probes,
+// measured and removed (profiles/r6_gemm_vs_hipblaslt.txt): a B ring three K-tiles deep
+// (160 KB LDS) and a two-barrier K-tile (both k-half-1 fragment sets read first).
 static constexpr int gemm_kernel() { return LCQ_PROBE_GEMM_PP; }
 
 template <int DT, int EPI>
 static int launch(Args& a, hipStream_t st) {
   // the dynamic-LDS attribute is per device: set it on every launch (cheap, thread-safe)
-  if constexpr (gemm_kernel() == 3) {
-    if (a.order == 0) {
-      (void)hipFuncSetAttribute((const void*)k_gemm16t<DT, EPI>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_T);
-      const unsigned gy = (EPI == EPI_F32 && a.x6_splits > 1) ? (unsigned)a.x6_splits : 1u;
-      hipLaunchKernelGGL((k_gemm16t<DT, EPI>), dim3((unsigned)a.nslots, gy), 256, LDS_T, st, a);
-      return check_launch("lcq_gemm: k_gemm16t");
-    }
-  }
   if (gemm_kernel() == 2 && a.order == 0) {
     (void)hipFuncSetAttribute((const void*)k_gemm16h<DT, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF4);
