@@ -312,3 +312,39 @@ def test_planned_mode_matches_algorithm(calib, quant_out, special, expect):
         cfg['calib'] = {'seq_len': 16}
     assert planned_mode(load_config(cfg), 2) == expect
     assert planned_mode(load_config(cfg), 1) == 'single'
+
+
+def test_streamer_releases_only_exclusive_host_copies():
+    """BlockStreamer._release_dead (host-copy reuse for replaced modules): a dead module's host
+    tensor is offered for reuse only when nothing else holds it -- no other Python reference,
+    no view on its storage -- and every dead entry leaves the table (no GPU needed: the
+    streams are not touched)."""
+    import weakref
+
+    import torch.nn as nn
+
+    from lightcompress_amd.residency import BlockStreamer
+    st = BlockStreamer.__new__(BlockStreamer)   # host-side state only
+    st.host, st.stats = {}, {'host_released': 0}
+    keep_ref = {}
+
+    def entry(name, shape, hold=None):
+        m = nn.Module()
+        t = torch.empty(shape)
+        m.register_buffer('w', t)
+        st.host[(id(m), '_buffers', 'w')] = (weakref.ref(m), t)
+        if hold == 'ref':
+            keep_ref[name] = t
+        elif hold == 'view':
+            keep_ref[name] = t[1:]
+        return m
+    live = entry('live', (4, 4))
+    free = entry('free', (4, 8))
+    held = entry('held', (4, 8), 'ref')
+    viewed = entry('viewed', (2, 8), 'view')
+    del free, held, viewed
+    pool = st._release_dead()
+    assert {k: len(v) for k, v in pool.items()} == {((4, 8), torch.float32): 1}
+    assert all(t is not keep_ref['held'] for t in pool[((4, 8), torch.float32)])
+    assert st.stats['host_released'] == 3
+    assert list(st.host) == [(id(live), '_buffers', 'w')]
