@@ -215,11 +215,18 @@ int lcq_tree_sum(const void* const* parts, int np, int64_t n, float alpha, void*
  * (use_qtorch, quant.py:1061-1080): q = float_quantize(w / s + 0) * s in fp32 with the
  * saturating native cast, symmetric qparams with qmax = finfo.max (qmin, qmax,
  * sym, z_in, z_out are ignored); the per-channel form is gptq_fp8.yml's column loop.
+ * nprev > 0 (left-looking near updates, gptq.py:244 restricted to this block's columns):
+ * before its loop the kernel applies, for each of the nprev full 128-column blocks right
+ * before col0 in order, W[:, col0 : col0 + count] -= Err_j @ U[rows of block j, same columns],
+ * Err_j being rows [128 j, 128 j + 128) of the k-major err_prev (row stride ld_err) -- each
+ * product the k-ordered fp32 fmaf chain of lcq_gptq_trailing, rounded, then subtracted: the
+ * same bits as one lcq_gptq_trailing(c1 = col0, c2 >= col0 + count) after each earlier block.
  * ------------------------------------------------------------------------------------- */
 int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, const void* U,
                    int64_t ldu, int64_t group, int qmin, int qmax, int sym, int fmt,
                    const void* s_in, const void* z_in, void* s_out, void* z_out,
-                   int64_t ng_total, void* err, int64_t ld_err, void* losses, void* stream);
+                   int64_t ng_total, void* err, int64_t ld_err, void* losses,
+                   const void* err_prev, int nprev, void* stream);
 
 /* GPTQ static groups (gptq.py:224-227, static_groups: True): the same block loop with fixed
  * qparams per (row, ORIGINAL group): permuted column c uses s_in / z_in [rows, ngc] at group
@@ -227,7 +234,8 @@ int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, int count, c
 int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t col0, int count,
                         const void* U, int64_t ldu, int qmin, int qmax, const void* s_in,
                         const void* z_in, const int32_t* col_group, int64_t ngc, void* err,
-                        int64_t ld_err, void* losses, void* stream);
+                        int64_t ld_err, void* losses, const void* err_prev, int nprev,
+                        void* stream);
 
 /* C = beta C + alpha A op(B) on row-major fp32 views (the fp32 updates of the recursive
  * factorisation behind U, gptq_core._chol_inv_rec: `addmm_` of the reference-equivalent

@@ -62,9 +62,9 @@ SIGNATURES = {
     'lcq_hessian_grouped_workspace_bytes': ([_vp, _int, _i64], _i64),
     'lcq_hessian_grouped': ([_vp, _int, _i64, _vp, _int, _vp, _f32, _vp, _i64, _vp], _int),
     'lcq_gptq_block': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _int, _int, _int, _int,
-                        _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp], _int),
+                        _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp], _int),
     'lcq_gptq_block_cols': ([_vp, _i64, _i64, _i64, _int, _vp, _i64, _int, _int, _vp, _vp, _vp,
-                             _i64, _vp, _i64, _vp, _vp], _int),
+                             _i64, _vp, _i64, _vp, _vp, _int, _vp], _int),
     'lcq_chol_inv_tile': ([_vp, _i64, _int, _vp, _i64, _vp, _i64, _vp, _i64, _vp], _int),
     'lcq_gptq_trailing': ([_vp, _i64, _i64, _i64, _int, _i64, _i64, _vp, _i64, _vp, _i64, _vp],
                           _int),

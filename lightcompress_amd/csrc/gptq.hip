@@ -37,6 +37,10 @@ struct GptqArgs {
   float* losses;      // optional [rows, ld]
   const int32_t* cgroup;  // static groups: group of every (permuted) column, [ld]
   int64_t ngc;            // static groups: groups per row of s_in / z_in
+  // left-looking near updates: the k-major errors [nprev * 128][ld_err] of the nprev full
+  // blocks right before col0 (columns col0 - 128 nprev .. col0 - 1 of the superblock)
+  const float* err_prev;
+  int nprev;
 };
 
 // 16 lanes per row, 8 consecutive block columns per lane (16 rows per 256-thread workgroup:
@@ -62,11 +66,104 @@ constexpr int ubase(int c) {  // sum over rows i < c of (GB - ustart(i))
   return GB * c - 8 * (c >> 2) * ((c >> 2) - 1) - 4 * (c >> 2) * (c & 3);
 }
 constexpr int UPACK = ubase(GB);
+static_assert(UPACK >= 64 * 132, "a staged U half of the near updates fits the U block's LDS");
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// The near updates of the superblock, left-looking (gptq.py:244 restricted to this block's
+// columns): for every earlier block j of the superblock, in order,
+//   W[:, block] -= Err_j @ U[rows of j, block]
+// each product an fp32 MFMA chain over k = 0 .. 127 in order (v_mfma_f32_16x16x4_f32, lane
+// group g supplying k = 4 s + g at step s: the k-ordered fmaf chain of lcq_gptq_trailing's
+// kernels, bit for bit), rounded, then subtracted -- the same per-element operations, in the
+// same order, as one lcq_gptq_trailing launch after each earlier block, without those launches
+// and their dependent-kernel gaps. U_j goes through LDS (the U block's area, staged only
+// afterwards) in halves of 64 k-rows x 128 columns, rows padded to 132 floats (the four lane
+// groups of a B read hit distinct banks), the next half prefetched into registers while the
+// current one is multiplied; each wave computes 16 rows x 32 columns; the product tile goes
+// back through LDS to the row-per-16-lanes layout of the loop.
+constexpr int NU_LD = 132;   // padded row of a staged U half (64 x 132 floats = UPACK)
+
+__device__ __forceinline__ void nu_fetch(const GptqArgs& a, int j, int half, int tid,
+                                         float4 (&pf)[8]) {
+  const float* src = a.U + (a.col0 - (int64_t)(a.nprev - j) * GB + 64 * half) * a.ldu + a.col0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {   // 2048 float4 of 64 rows x 32 float4
+    const int idx = q * 256 + tid, row = idx >> 5, c4 = (idx & 31) * 4;
+    pf[q] = c4 < a.count ? *reinterpret_cast<const float4*>(src + (int64_t)row * a.ldu + c4)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void near_updates(const GptqArgs& a, float (&w)[8], float* lds,
+                                             int tid, int64_t rbase, int cb) {
+  const int lane = tid & 63, wv = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const int64_t arow = rbase + r16;
+  const bool arow_ok = arow < a.rows;
+  const int c0 = 32 * wv + r16, c1 = c0 + 16;
+  const int rloc = tid >> 4;
+  float4 pf[8];
+  nu_fetch(a, 0, 0, tid, pf);
+  for (int j = 0; j < a.nprev; ++j) {
+    const float* ej = a.err_prev + (int64_t)j * GB * a.ld_err + (arow_ok ? arow : 0);
+    v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      float av[16];
+#pragma unroll
+      for (int st = 0; st < 16; ++st)
+        av[st] = arow_ok ? ej[(int64_t)(64 * half + 4 * st + g) * a.ld_err] : 0.f;
+      __syncthreads();   // the previous half / product tile has been read
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int idx = q * 256 + tid, row = idx >> 5, c4 = (idx & 31) * 4;
+        *reinterpret_cast<float4*>(lds + row * NU_LD + c4) = pf[q];
+      }
+      __syncthreads();
+      if (half == 0) nu_fetch(a, j, 1, tid, pf);
+      else if (j + 1 < a.nprev) nu_fetch(a, j + 1, 0, tid, pf);
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const float* br = lds + (4 * st + g) * NU_LD;
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[st], br[c0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[st], br[c1], acc1, 0, 0, 0);
+      }
+    }
+    __syncthreads();   // the second half has been read
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {   // lane: column r16 of its tile, rows 4 g + v
+      lds[(4 * g + v) * NU_LD + c0] = acc0[v];
+      lds[(4 * g + v) * NU_LD + c1] = acc1[v];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CPL; ++k)
+      if (cb + k < a.count) w[k] = w[k] - lds[rloc * NU_LD + cb + k];
+  }
+  __syncthreads();   // LDS free for the U block
+}
 
 template <int GS, int FMT>
 __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
   __shared__ __attribute__((aligned(16))) float u[UPACK];
   const int tid = threadIdx.x;
+  const int sub = tid & (LPR - 1);
+  const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + (tid / LPR);
+  const bool valid = r < a.rows;  // invalid lanes still run (shuffles), never store
+  const int cb = sub * CPL;       // first block column of this lane
+  float* wrow = a.W + (valid ? r : 0) * a.ld + a.col0;
+  float w[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; k += 4) {
+    if (valid && cb + k + 3 < a.count) {
+      const float4 v = *reinterpret_cast<const float4*>(wrow + cb + k);
+      w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[k + q] = (valid && cb + k + q < a.count) ? wrow[cb + k + q] : 0.f;
+    }
+  }
+  if (a.nprev > 0) near_updates(a, w, u, tid, (int64_t)blockIdx.x * (256 / LPR), cb);
   for (int i = tid >> 1; i < GB; i += 128) {   // two threads per row, 16-B pieces
     for (int j4 = (i >> 2) + (tid & 1); j4 < GB / 4; j4 += 2) {
       const int j = 4 * j4;
@@ -85,22 +182,6 @@ __global__ void __launch_bounds__(256) k_gptq_block(GptqArgs a) {
     }
   }
   __syncthreads();
-  const int sub = tid & (LPR - 1);
-  const int64_t r = (int64_t)blockIdx.x * (256 / LPR) + (tid / LPR);
-  const bool valid = r < a.rows;  // invalid lanes still run (shuffles), never store
-  const int cb = sub * CPL;       // first block column of this lane
-  float* wrow = a.W + (valid ? r : 0) * a.ld + a.col0;
-  float w[CPL];
-#pragma unroll
-  for (int k = 0; k < CPL; k += 4) {
-    if (valid && cb + k + 3 < a.count) {
-      const float4 v = *reinterpret_cast<const float4*>(wrow + cb + k);
-      w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) w[k + q] = (valid && cb + k + q < a.count) ? wrow[cb + k + q] : 0.f;
-    }
-  }
   // group qparams from the block-start weights (gptq.py:215-223 reads W, not W1); GS >= 32
   // so a lane's 8 columns lie in one group of GS / 8 adjacent lanes
   float qs, qz;
@@ -231,8 +312,10 @@ extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, i
                               const void* U, int64_t ldu, int64_t group, int qmin, int qmax,
                               int sym, int fmt, const void* s_in, const void* z_in, void* s_out,
                               void* z_out, int64_t ng_total, void* err, int64_t ld_err,
-                              void* losses, void* stream) {
+                              void* losses, const void* err_prev, int nprev, void* stream) {
   LCQ_REQUIRE(rows > 0 && ld > 0 && count > 0 && count <= GB, "bad block shape");
+  LCQ_REQUIRE(nprev >= 0 && (nprev == 0 || err_prev != nullptr) && col0 >= (int64_t)nprev * GB,
+              "nprev earlier blocks need err_prev and col0 >= 128 nprev");
   LCQ_REQUIRE(col0 >= 0 && col0 + count <= ld && col0 + count <= ldu, "block out of range");
   LCQ_REQUIRE(col0 % GB == 0, "col0 must be a multiple of the 128-column blocksize");
   LCQ_REQUIRE(ld % 4 == 0 && ldu % 4 == 0, "row lengths must be multiples of 4 (16-B rows)");
@@ -259,6 +342,8 @@ extern "C" int lcq_gptq_block(void* W, int64_t rows, int64_t ld, int64_t col0, i
   a.err = reinterpret_cast<float*>(err);
   a.ld_err = ld_err;
   a.losses = reinterpret_cast<float*>(losses);
+  a.err_prev = reinterpret_cast<const float*>(err_prev);
+  a.nprev = nprev;
   LCQ_REQUIRE(ld_err >= rows, "ld_err < rows");
   LCQ_REQUIRE(group == 0 || group == 32 || group == 64 || group == 128,
               "group must be 0 (per-row qparams), 32, 64 or 128");
@@ -422,8 +507,10 @@ extern "C" int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t co
                                    const void* U, int64_t ldu, int qmin, int qmax,
                                    const void* s_in, const void* z_in, const int32_t* col_group,
                                    int64_t ngc, void* err, int64_t ld_err, void* losses,
-                                   void* stream) {
+                                   const void* err_prev, int nprev, void* stream) {
   LCQ_REQUIRE(rows > 0 && ld > 0 && count > 0 && count <= GB, "bad block shape");
+  LCQ_REQUIRE(nprev >= 0 && (nprev == 0 || err_prev != nullptr) && col0 >= (int64_t)nprev * GB,
+              "nprev earlier blocks need err_prev and col0 >= 128 nprev");
   LCQ_REQUIRE(col0 >= 0 && col0 + count <= ld && col0 + count <= ldu, "block out of range");
   LCQ_REQUIRE(col0 % GB == 0, "col0 must be a multiple of the 128-column blocksize");
   LCQ_REQUIRE(ld % 4 == 0 && ldu % 4 == 0, "row lengths must be multiples of 4 (16-B rows)");
@@ -441,6 +528,8 @@ extern "C" int lcq_gptq_block_cols(void* W, int64_t rows, int64_t ld, int64_t co
   a.err = reinterpret_cast<float*>(err);
   a.ld_err = ld_err;
   a.losses = reinterpret_cast<float*>(losses);
+  a.err_prev = reinterpret_cast<const float*>(err_prev);
+  a.nprev = nprev;
   const dim3 grid((unsigned)((rows + (256 / LPR) - 1) / (256 / LPR)));
   hipLaunchKernelGGL((k_gptq_block<-1, 0>), grid, 256, 0, as_stream(stream), a);
   return check_launch("lcq_gptq_block_cols");

@@ -481,6 +481,9 @@ def prepare(W: torch.Tensor, H: torch.Tensor, actorder: bool, percdamp: float):
     return prepare_weight(W, perm, dead), U, perm
 
 
+LEFT_LOOKING = True   # module switch for A/B runs and tests (False: a trailing launch per block)
+
+
 @torch.no_grad()
 def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: int | None,
                 qmin: int, qmax: int, fixed=None, losses: bool = False,
@@ -491,10 +494,11 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     Per 128-column block: the HIP kernel runs the in-block sequential loop (bit-exact rank-1
     updates). The reference then applies ``W[:, i2:] -= Err @ U[i1:i2, i2:]`` to every later
     column; here that update is two-level: inside a superblock of ``superblock`` columns each
-    block updates only the rest of its superblock, and the far columns receive the
-    superblock's stacked errors in ONE K = superblock update (same terms, grouped differently
-    -> T2; every element still has a fixed k order, so row sharding stays bit-identical).
-    fp32 MFMA kernel (``lcq_gptq_trailing``). ``ncols_q`` (OWQ): only the first ncols_q
+    block's columns receive the earlier blocks' updates (left-looking, inside the block kernel:
+    the same products and order as one ``lcq_gptq_trailing`` per block), and the far columns
+    receive the superblock's stacked errors in ONE K = superblock update (same terms, grouped
+    differently -> T2; every element still has a fixed k order, so row sharding stays
+    bit-identical). ``ncols_q`` (OWQ): only the first ncols_q
     columns are quantized; every block's error still updates all later columns.
 
     ``col_qparams`` (per_group with a searched range, calib_algo mse): a function of a
@@ -538,16 +542,18 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
     elif group is None or static:
         s_in = fixed[0].reshape(-1).float().contiguous()
         z_in = None if sym else fixed[1].reshape(-1).float().contiguous()
-    # (Splitting each near update into the next block's columns on the compute stream and the
-    # rest on a side stream beside the next block kernel measured slower on every Llama-3-8B
-    # subset shape, e.g. 17.4 -> 19.4 ms at 4096 x 14336: scripts/column_loop_rate.py,
-    # profiles/r4_column_loop.txt.)
+    # Near updates (the rest of the superblock after each block): left-looking inside the next
+    # block kernels (lcq_gptq_block nprev > 0: the same products in the same order, bit for
+    # bit, without a trailing launch and its dependent-kernel gap per block), except where the
+    # host needs the block-start columns before the kernel (searched qparams).
+    left = LEFT_LOOKING and not searched
     for sb0 in range(0, ncq, SB):
         sb1 = min(sb0 + SB, ncq)
         for i1 in range(sb0, sb1, BLOCK):
             i2 = min(i1 + BLOCK, sb1)
             cnt = i2 - i1
             e = errT[i1 - sb0:]
+            npv = (i1 - sb0) // BLOCK if left else 0
             if searched:  # groups starting in this block, from the block-start columns
                 for g0 in range(-(-i1 // group) * group, i2, group):
                     sg, zg = col_qparams(W[:, g0:min(g0 + group, ncq)])
@@ -555,11 +561,12 @@ def column_loop(W: torch.Tensor, U: torch.Tensor, bit: int, sym: bool, group: in
                     if z_srch is not None:
                         z_srch[:, g0 // group] = zg.reshape(-1)
             if static:
-                ops.gptq_block_cols(W, i1, cnt, U, qmin, qmax, s_in, z_in, col_group, e, L)
+                ops.gptq_block_cols(W, i1, cnt, U, qmin, qmax, s_in, z_in, col_group, e, L,
+                                    err_prev=errT, nprev=npv)
             else:
                 ops.gptq_block(W, i1, cnt, U, group or 0, qmin, qmax, sym, s_out, z_out, e, L,
-                               s_in, z_in, fp8=fp8)
-            if i2 < sb1:  # near columns: the rest of this superblock
+                               s_in, z_in, fp8=fp8, err_prev=errT, nprev=npv)
+            if not left and i2 < sb1:  # near columns: the rest of this superblock
                 ops.gptq_trailing(W, i1, cnt, i2, e, U, c2=sb1)
         if sb1 < cols:    # far columns: the whole superblock's errors at once
             ops.gptq_trailing(W, sb0, sb1 - sb0, sb1, errT, U, c2=cols)

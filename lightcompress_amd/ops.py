@@ -260,31 +260,46 @@ def tree_sum(parts, alpha: float = 1.0, out: torch.Tensor | None = None) -> torc
     return out
 
 
+def _err_prev(err_prev, nprev: int, err: torch.Tensor, rows: int):
+    """(pointer, nprev) of the left-looking near updates: err_prev the k-major errors of the
+    nprev blocks before this one, with the same row stride as err."""
+    if not nprev:
+        return None, 0
+    if (err_prev is None or err_prev.shape[0] < 128 * nprev
+            or _ld_err(err_prev, rows) != _ld_err(err, rows)):
+        raise ValueError('err_prev must be k-major [>= 128 nprev, ld_err] like err')
+    return N.ptr(err_prev), int(nprev)
+
+
 def gptq_block(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, group: int,
                qmin: int, qmax: int, sym: bool, s_out, z_out, err: torch.Tensor,
-               losses=None, s_in=None, z_in=None, fp8=None):
+               losses=None, s_in=None, z_in=None, fp8=None, err_prev=None, nprev: int = 0):
     """One 128-column GPTQ block in place on fp32 W (see include/lcq.h lcq_gptq_block);
     err is k-major [128, rows]. fp8 (torch.float8_e4m3fn / float8_e5m2): FloatQuantizer's
-    quant_dequant instead of the integer one (qmin / qmax / sym / zeros ignored)."""
+    quant_dequant instead of the integer one (qmin / qmax / sym / zeros ignored). nprev > 0:
+    the near updates of the nprev blocks before col0 (their errors in err_prev) are applied
+    first, inside the kernel (left-looking)."""
     rows, ld = W.shape
     ng_total = s_out.shape[1] if s_out is not None else 0
     fmt = 0 if fp8 is None else N.dt(fp8)
+    ep, npv = _err_prev(err_prev, nprev, err, rows)
     N.call('lcq_gptq_block', N.ptr(W), rows, ld, int(col0), int(count), N.ptr(U), U.shape[1],
            int(group), int(qmin), int(qmax), int(sym), fmt, N.ptr(s_in), N.ptr(z_in), N.ptr(s_out),
-           N.ptr(z_out), int(ng_total), N.ptr(err), _ld_err(err, rows), N.ptr(losses),
+           N.ptr(z_out), int(ng_total), N.ptr(err), _ld_err(err, rows), N.ptr(losses), ep, npv,
            N.stream_of(W))
 
 
 def gptq_block_cols(W: torch.Tensor, col0: int, count: int, U: torch.Tensor, qmin: int,
                     qmax: int, s_in: torch.Tensor, z_in, col_group: torch.Tensor,
-                    err: torch.Tensor, losses=None):
+                    err: torch.Tensor, losses=None, err_prev=None, nprev: int = 0):
     """gptq_block with static per-(row, original group) qparams s_in / z_in [rows, ngc] and
     the permuted column -> group map col_group (int32 [ld])."""
     rows, ld = W.shape
     ngc = s_in.numel() // rows
+    ep, npv = _err_prev(err_prev, nprev, err, rows)
     N.call('lcq_gptq_block_cols', N.ptr(W), rows, ld, int(col0), int(count), N.ptr(U), U.shape[1],
            int(qmin), int(qmax), N.ptr(s_in), N.ptr(z_in), N.ptr(col_group), int(ngc), N.ptr(err),
-           _ld_err(err, rows), N.ptr(losses), N.stream_of(W))
+           _ld_err(err, rows), N.ptr(losses), ep, npv, N.stream_of(W))
 
 
 def _ld_err(err: torch.Tensor, rows: int) -> int:

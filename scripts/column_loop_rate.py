@@ -1,6 +1,7 @@
 """Probe: GPTQ's blocked column loop (gptq_core.column_loop) alone on the Llama-3-8B subset
 shapes -- wall time (host included) vs the summed device time of its kernels, per superblock
-size. (Round 4 also A/B'd a side-stream pipeline of the near-column updates here: slower,
+size, with the near updates left-looking inside the block kernels or as one trailing launch
+per block (round 6). (Round 4 also A/B'd a side-stream pipeline of the near-column updates here: slower,
 removed; profiles/r4_column_loop.txt.)
 usage: column_loop_rate.py"""
 import sys
@@ -50,7 +51,13 @@ def run(rows, cols, sb, reps=3):
 
 
 for rows, cols in SHAPES:
-    for sb in (512, 1024, 2048):
-        wall, dms, W = run(rows, cols, sb)
-        print(f'rows {rows:6d} cols {cols:6d} sb {sb:5d}: wall {wall:7.2f} ms  device sum '
-              f'{dms:7.2f} ms', flush=True)
+    for sb in (1024, 2048):
+        res = {}
+        for left in (False, True):
+            gptq_core.LEFT_LOOKING = left
+            wall, dms, W = run(rows, cols, sb)
+            res[left] = W
+            print(f'rows {rows:6d} cols {cols:6d} sb {sb:5d} {"left-looking" if left else "trailing    "}'
+                  f': wall {wall:7.2f} ms  device sum {dms:7.2f} ms', flush=True)
+        print(f'  identical: {torch.equal(res[False], res[True])}', flush=True)
+gptq_core.LEFT_LOOKING = True
