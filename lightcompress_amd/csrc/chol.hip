@@ -1022,6 +1022,75 @@ __global__ void __launch_bounds__(256) k_gemm_f32_sk_fixup(Args a, SkArgs sk) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// k_gemm_f32_small: the recursion's small products (M, N <= 512, K <= 1024, all multiples of
+// 32 / 128: the 128- to 512-level updates of the chain), which as one to sixteen 64^2 LDS-DMA
+// workgroups ran at 0.4-13 TF/s (~10 us for a 128^3 product, profiles/r6_chain_small.txt):
+// latency of four dependent 32-k chunks on four CUs. Here one 32 x 32 output tile per
+// 256-thread workgroup (4 x more workgroups), a 16 x 16 v_mfma_f32_16x16x4_f32 tile per wave,
+// both operands straight from global memory (L2) into registers, four 32-k chunks per load
+// batch with the next batch in flight under the current one's 32 MFMAs. The k order is the
+// LDS-DMA kernels' (k_gemm_f32d_*: in 32-k chunk c, lane group g supplies k = 32 c + 8 g + s at
+// step s), so every element gets the same fmaf chain and the products are bit-identical to
+// the kernel they replace; epilogue C = beta C + alpha acc as there.
+template <int BT>
+__global__ void __launch_bounds__(256) k_gemm_f32_small(Args a) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int64_t row = (int64_t)blockIdx.y * 32 + (w >> 1) * 16 + r16;
+  const int64_t col = (int64_t)blockIdx.x * 32 + (w & 1) * 16 + r16;
+  const float* ap = a.A + row * a.lda + 8 * g;
+  const float* bp = BT ? a.B + col * a.ldb + 8 * g : a.B + (int64_t)(8 * g) * a.ldb + col;
+  const int nb = (int)(a.K / 128);   // load batches of four 32-k chunks
+  auto load = [&](int bt_, float (&av)[32], float (&bv)[32]) {
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int k0 = 128 * bt_ + 32 * cc;   // this lane's 8 k: k0 + 8 g + 0..7
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float4 v = *reinterpret_cast<const float4*>(ap + k0 + 4 * h);
+        av[8 * cc + 4 * h] = v.x; av[8 * cc + 4 * h + 1] = v.y;
+        av[8 * cc + 4 * h + 2] = v.z; av[8 * cc + 4 * h + 3] = v.w;
+      }
+      if constexpr (BT) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 v = *reinterpret_cast<const float4*>(bp + k0 + 4 * h);
+          bv[8 * cc + 4 * h] = v.x; bv[8 * cc + 4 * h + 1] = v.y;
+          bv[8 * cc + 4 * h + 2] = v.z; bv[8 * cc + 4 * h + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) bv[8 * cc + s] = bp[(int64_t)(k0 + s) * a.ldb];
+      }
+    }
+  };
+  v4f32 acc = {0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const float (&av)[32], const float (&bv)[32]) {
+#pragma unroll
+    for (int s = 0; s < 32; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+  };
+  float a0[32], b0[32], a1[32], b1[32];
+  load(0, a0, b0);
+  for (int c = 0; c < nb; c += 2) {
+    if (c + 1 < nb) load(c + 1, a1, b1);
+    mma(a0, b0);
+    if (c + 1 < nb) {
+      if (c + 2 < nb) load(c + 2, a0, b0);
+      mma(a1, b1);
+    }
+  }
+  // 16x16 MFMA tile: lane holds column r16, rows 4 g + v
+  const int64_t c_out = (int64_t)blockIdx.x * 32 + (w & 1) * 16 + r16;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int64_t r = (int64_t)blockIdx.y * 32 + (w >> 1) * 16 + 4 * g + v;
+    float* p = a.C + r * a.ldc + c_out;
+    const float val = a.alpha * acc[v];
+    *p = a.beta == 0.f ? val : __fmaf_rn(a.beta, *p, val);
+  }
+}
+
 }  // namespace f32g
 }  // namespace lcq
 
@@ -1064,6 +1133,15 @@ static int gemm_f32_impl(int64_t M, int64_t N, int64_t K, float alpha, const voi
   a.vec = al(A) && al(B) && lda % 4 == 0 && ldb % 4 == 0;
   if (K == 0) a.alpha = 0.f;  // C = beta C
   hipStream_t st = as_stream(stream);
+  // the small products of the chain: 32 x 32 tiles from registers (k_gemm_f32_small); a
+  // whole-product launch only (plan_m == M), so row-range launches never change kernel
+  if (plan_m == M && M <= 512 && N <= 512 && K >= 128 && K <= 1024 && M % 32 == 0 &&
+      N % 32 == 0 && K % 128 == 0 && a.vec) {
+    const dim3 grid((unsigned)(N / 32), (unsigned)(M / 32));
+    if (bt) hipLaunchKernelGGL(f32g::k_gemm_f32_small<1>, grid, 256, 0, st, a);
+    else hipLaunchKernelGGL(f32g::k_gemm_f32_small<0>, grid, 256, 0, st, a);
+    return check_launch("lcq_gemm_f32: small");
+  }
   // 128^2 tiles where they fill the chip, 64^2 below (4x the workgroups)
   const int64_t t128 = ((N + 127) / 128) * ((plan_m + 127) / 128);
   const bool big = t128 >= 256;
