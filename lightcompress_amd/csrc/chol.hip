@@ -1113,6 +1113,15 @@ extern "C" int64_t lcq_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K)
 // plan_m: the row count the kernel variant (tile size, LDS-DMA or register staging) is chosen
 // for -- M itself, or the full product's rows when this launch computes a row range of it
 // (lcq_gemm_f32_rows: the same variant, hence the same per-element k order, on every rank)
+// k_gemm_f32_small's range (probe builds vary it: -DLCQ_PROBE_SMALL_MN / _K)
+#ifndef LCQ_PROBE_SMALL_MN
+#define LCQ_PROBE_SMALL_MN 512
+#endif
+#ifndef LCQ_PROBE_SMALL_K
+#define LCQ_PROBE_SMALL_K 1024
+#endif
+constexpr int64_t SMALL_MN = LCQ_PROBE_SMALL_MN, SMALL_K = LCQ_PROBE_SMALL_K;
+
 static int gemm_f32_impl(int64_t M, int64_t N, int64_t K, float alpha, const void* A,
                          int64_t lda, const void* B, int64_t ldb, int bt, float beta, void* C,
                          int64_t ldc, void* ws, int64_t ws_bytes, void* stream,
@@ -1135,7 +1144,7 @@ static int gemm_f32_impl(int64_t M, int64_t N, int64_t K, float alpha, const voi
   hipStream_t st = as_stream(stream);
   // the small products of the chain: 32 x 32 tiles from registers (k_gemm_f32_small); a
   // whole-product launch only (plan_m == M), so row-range launches never change kernel
-  if (plan_m == M && M <= 512 && N <= 512 && K >= 128 && K <= 1024 && M % 32 == 0 &&
+  if (plan_m == M && M <= SMALL_MN && N <= SMALL_MN && K >= 128 && K <= SMALL_K && M % 32 == 0 &&
       N % 32 == 0 && K % 128 == 0 && a.vec) {
     const dim3 grid((unsigned)(N / 32), (unsigned)(M / 32));
     if (bt) hipLaunchKernelGGL(f32g::k_gemm_f32_small<1>, grid, 256, 0, st, a);
