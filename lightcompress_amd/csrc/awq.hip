@@ -1014,6 +1014,247 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))   
   best_min[oi] = dt_bits<DT>(bmin);
 }
 
+// ----------------------------------------------------------------------------------------
+// Token-lane form with the candidates staged in LDS (k_auto_clip_tw): the AWQ headline's
+// auto-clip (G = 128, minmax qparams, weight-only, T <= 512 sampled tokens).
+// k_auto_clip_tl fed the candidates through scalar loads, whose latency (one lgkmcnt(0) per
+// 16 products: scalar loads return out of order) left the VALU issuing 1 instruction per ~7
+// cycles, and each of its 64-token waves re-read every candidate row (8x the table at 512
+// tokens). Here one workgroup of 8 waves holds ALL T tokens (lane = token, its 128 x values
+// of the group widened in VGPRs) and walks TW_RPW rows of one group in sets of TW_R rows:
+//  * a set's candidate rows ([TW_R][11][128] fp32, the k_clip_qtable table) come into one of
+//    two LDS buffers by LDS-DMA, issued one set ahead (no VGPRs, no wait inside the compute);
+//  * the compute reads them as wave-uniform ds_read_b128 broadcasts (4 per 16 products, the
+//    next 16 in flight under the current 16's 32 VALU): per product pair one v_pk_mul_f32,
+//    two v_cvt_pk_bf16_f32, one v_pk_add_f32, the 8 partial sums and halving tree of dot_rows;
+//  * each (row, step)'s per-token errors (DT bits) go to an LDS row [pair][token]; one set
+//    later one wave (rotating) sums each pair's T errors sequentially in token order -- the
+//    order k_auto_clip and k_auto_clip_tl use -- and picks the first strict minimum.
+// LDS: 2 x 22.5 KB candidates + 2 x 40.6 KB error rows = 126 KB: one workgroup per CU.
+// Bit-identical to k_auto_clip (tests/test_awq_gpu.py).
+// ----------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) char lds_char_t;
+constexpr int TW_WAVES = 8;             // 512 lanes = up to 512 sampled tokens
+constexpr int TW_R = 4;                  // rows per LDS set
+constexpr int TW_RPW = 64;               // rows per workgroup
+constexpr int TW_EPAD = 520;             // u16 per (row, step) error row: 512 tokens + pad
+constexpr int TW_NS = 10;
+constexpr int TW_P = TW_NS + 1;
+constexpr int TW_CAND = TW_R * TW_P * TL_G;           // floats per candidate buffer
+constexpr int TW_PAIRS = TW_R * TW_NS;                // (row, step) pairs per set
+constexpr int TW_LDS = 2 * TW_CAND * 4 + 2 * TW_PAIRS * TW_EPAD * 2 + TW_PAIRS * 4;
+static_assert(TW_CAND * 4 % 1024 == 0, "candidate buffer = whole 1 KB DMA pieces");
+static_assert(TW_PAIRS <= 64, "one summing lane per (row, step) pair");
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tw_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  void* q = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)bytes, 0x00020000);
+}
+
+// 16 products of this lane's token with 16 candidates (4 float4 from LDS), into the partial
+// sums acc_{k mod 8} exactly as mac16 / dot_rows form them
+template <int DT>
+__device__ __forceinline__ void mac16v(const float (&xf)[TL_G], int k0, const float4 (&q)[4],
+                                       v2f& a0, v2f& a1, v2f& a2, v2f& a3) {
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const int k = k0 + 8 * o;
+    const float4 u = q[2 * o], v = q[2 * o + 1];
+    v2f p0 = v2f{xf[k], xf[k + 1]} * v2f{u.x, u.y};
+    v2f p1 = v2f{xf[k + 2], xf[k + 3]} * v2f{u.z, u.w};
+    v2f p2 = v2f{xf[k + 4], xf[k + 5]} * v2f{v.x, v.y};
+    v2f p3 = v2f{xf[k + 6], xf[k + 7]} * v2f{v.z, v.w};
+    p0 = dtr2<DT>(p0);
+    p1 = dtr2<DT>(p1);
+    p2 = dtr2<DT>(p2);
+    p3 = dtr2<DT>(p3);
+    a0 += p0;
+    a1 += p1;
+    a2 += p2;
+    a3 += p3;
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(64 * TW_WAVES)
+    k_auto_clip_tw(const uint16_t* __restrict__ x, int64_t ic, int T,
+                   const float* __restrict__ qt, uint32_t qt_bytes, const float* __restrict__ om,
+                   int64_t row0, int64_t nrows, const float* __restrict__ factors, int clip_sym,
+                   uint16_t* __restrict__ best_max, uint16_t* __restrict__ best_min) {
+  constexpr int G = TL_G, NS = TW_NS, P = TW_P;
+  extern __shared__ __attribute__((aligned(16))) float tw_lds[];
+  float* cand = tw_lds;                                                     // [2][R][P][G]
+  uint16_t* ebuf = reinterpret_cast<uint16_t*>(tw_lds + 2 * TW_CAND);       // [2][pairs][EPAD]
+  float* sums = reinterpret_cast<float*>(ebuf + 2 * TW_PAIRS * TW_EPAD);    // [pairs]
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = w * 64 + lane;
+  const int64_t g = blockIdx.y, ng = ic / G;
+  const int64_t rw0 = (int64_t)blockIdx.x * TW_RPW;
+  const int64_t nr = nrows - rw0 < TW_RPW ? nrows - rw0 : TW_RPW;
+  const int nsets = (int)((nr + TW_R - 1) / TW_R);
+  const __amdgpu_buffer_rsrc_t rs = tw_rsrc(qt, qt_bytes);
+
+  // set s's candidate rows -> cand[s & 1]: 1 KB pieces m = w, w + 8, ... of the 22 per set;
+  // 16-B chunk c = 64 m + lane is float4 `c % 352` of the set's row `c / 352`. Issued as
+  // inline asm: with the builtin the compiler's waitcnt pass puts a vmcnt(0) before the next
+  // ds_read (it cannot tell the DMA's LDS range from the reads'), exposing the whole DMA
+  // latency once per set; the kernel waits for its DMA itself before each set's barrier.
+  // M0 (the wave's LDS destination) is saved and restored inside the statement.
+  auto dma_set = [&](int s) {
+    const uint32_t base = (uint32_t)(size_t)(lds_char_t*)(cand + (s & 1) * TW_CAND);
+    for (int m = w; m < TW_CAND * 4 / 1024; m += TW_WAVES) {
+      const int c = m * 64 + lane;
+      const int rr = c / (P * G / 4), within = c % (P * G / 4);
+      int64_t lr = rw0 + (int64_t)s * TW_R + rr;
+      if (lr > nrows - 1) lr = nrows - 1;
+      const uint32_t off = (uint32_t)(((lr * ng + g) * P * G) * 4 + within * 16);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(base + m * 1024);
+      uint32_t sv;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\t"
+          "s_mov_b32 m0, %1\n\t"
+          "s_nop 0\n\t"
+          "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+          "s_mov_b32 m0, %0"
+          : "=&s"(sv)
+          : "s"(dst), "v"(off), "s"(rs)
+          : "memory");
+    }
+  };
+
+  // one set's error rows: token-order sums, then the first strict minimum per row
+  auto sum_pick = [&](int s) {
+    const uint16_t* eb = ebuf + (s & 1) * TW_PAIRS * TW_EPAD;
+    if (lane < TW_PAIRS) {
+      const uint16_t* src = eb + lane * TW_EPAD;
+      float run = 0.f;
+      int u = 0;
+      for (; u + 8 <= T; u += 8) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src + u);
+        const uint32_t a[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          run += dt_val<DT>((uint16_t)(a[j] & 0xffffu));
+          run += dt_val<DT>((uint16_t)(a[j] >> 16));
+        }
+      }
+      for (; u < T; ++u) run += dt_val<DT>(src[u]);
+      sums[lane] = run;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const int64_t lr = rw0 + (int64_t)s * TW_R + lane;
+    if (lane < TW_R && lr < nrows) {
+      const float omax = om[(lr * ng + g) * 2], omin = om[(lr * ng + g) * 2 + 1];
+      float bmax = omax, bmin = omin, best = dtr<DT>(1e9f);
+      for (int st = 0; st < NS; ++st) {
+        const float em = dtr<DT>(sums[lane * NS + st] / (float)T);
+        if (em < best) {
+          best = em;
+          const float f = factors[st];
+          bmax = dtr<DT>(omax * f);
+          bmin = clip_sym ? -bmax : dtr<DT>(omin * f);
+        }
+      }
+      const int64_t oi = (row0 + lr) * ng + g;
+      best_max[oi] = dt_bits<DT>(bmax);
+      best_min[oi] = dt_bits<DT>(bmin);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  dma_set(0);
+  float xf[G];
+  {
+    const uint16_t* xr = x + (int64_t)(t < T ? t : 0) * ic + g * G;
+#pragma unroll
+    for (int i = 0; i < G / 8; ++i) {
+      const uint4 v = t < T ? *reinterpret_cast<const uint4*>(xr + 8 * i) : make_uint4(0, 0, 0, 0);
+      widen4<DT>(make_uint2(v.x, v.y), &xf[8 * i]);
+      widen4<DT>(make_uint2(v.z, v.w), &xf[8 * i + 4]);
+    }
+  }
+  for (int s = 0; s < nsets; ++s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // cand[s & 1] landed; set s - 1's error rows complete
+    if (s >= 1 && w == (s - 1) % TW_WAVES) sum_pick(s - 1);
+    if (s + 1 < nsets) dma_set(s + 1);
+    const float* cs = cand + (s & 1) * TW_CAND;
+    uint16_t* eb = ebuf + (s & 1) * TW_PAIRS * TW_EPAD + t;
+    // the set's R x P candidate rows are one contiguous walk: chunk c + 2's reads are issued
+    // under chunk c's products, across pass boundaries too (the walk's last two prefetches
+    // read the 32 floats after the buffer: LDS in bounds, unused)
+    float4 q0[4], q1[4];
+#ifdef LCQ_PROBE_TW_DEEP
+    float4 qd[4];
+#endif
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      q0[j] = reinterpret_cast<const float4*>(cs)[j];
+      q1[j] = reinterpret_cast<const float4*>(cs + 16)[j];
+#ifdef LCQ_PROBE_TW_DEEP
+      qd[j] = reinterpret_cast<const float4*>(cs + 32)[j];
+#endif
+    }
+    float org = 0.f;
+#pragma unroll 1
+    for (int rp = 0; rp < TW_R * P; ++rp) {
+      const float* qp = cs + rp * G;
+      v2f a0 = v2f{0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+#ifdef LCQ_PROBE_TW_DEEP
+      // three chunks in flight: chunk c + 3 is read under chunk c
+#pragma unroll
+      for (int c = 0; c < G / 16; ++c) {
+        float4 qn[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qn[j] = reinterpret_cast<const float4*>(qp + 16 * (c + 3))[j];
+        mac16v<DT>(xf, 16 * c, q0, a0, a1, a2, a3);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          q0[j] = q1[j];
+          q1[j] = qd[j];
+          qd[j] = qn[j];
+        }
+      }
+#else
+#pragma unroll
+      for (int c = 0; c < G / 16; c += 2) {
+        float4 q2[4], q3[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q2[j] = reinterpret_cast<const float4*>(qp + 16 * (c + 2))[j];
+        mac16v<DT>(xf, 16 * c, q0, a0, a1, a2, a3);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q3[j] = reinterpret_cast<const float4*>(qp + 16 * (c + 3))[j];
+        mac16v<DT>(xf, 16 * (c + 1), q1, a0, a1, a2, a3);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          q0[j] = q2[j];
+          q1[j] = q3[j];
+        }
+      }
+#endif
+      const v2f l01 = a0 + a2, l23 = a1 + a3;   // l_m = acc_m + acc_{m+4}
+      const v2f s2 = l01 + l23;                 // (l0 + l2, l1 + l3)
+      const float d = dtr<DT>(s2.x + s2.y);
+      const int r = rp / P, p = rp - r * P;
+      if (p == 0) {
+        org = d;
+      } else {
+        const float dd = dtr<DT>(d - org);
+        eb[(r * NS + p - 1) * TW_EPAD] = dt_bits<DT>(dtr<DT>(dd * dd));
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (w == (nsets - 1) % TW_WAVES) sum_pick(nsets - 1);
+}
+
 // x [T, ic] in DT -> fp32 (the scalar-operand token stream of k_auto_clip_rl)
 template <int DT>
 __global__ void __launch_bounds__(256) k_widen_f32(const uint16_t* __restrict__ x, int64_t n8,
@@ -1274,15 +1515,17 @@ static constexpr int64_t CL_ROW_UNIT = 192;   // chunk rows: whole workgroups of
 static constexpr int TL_NS = 10;   // the kernels' shrink-step count
 static constexpr int64_t CL_PAIR_MIN_ROWGROUPS = 65536;   // automatic choice, see below
 
-// A/B probe hook (scripts/clip_rate.py): 0 = automatic, 1 = token-lane, 2 = row-lane.
-// Process-wide; not for production use. Automatic (profiles/r6_clip_rate.txt, Llama-3-8B
-// shapes): the token-lane kernel while the row-groups leave the lane-pair k_auto_clip's grid
-// short of the chip (v_proj 1024 x 4096: 2.46 vs 3.23 ms), k_auto_clip (lcq_auto_clip_search_act)
-// from 65536 row-groups up (o / gate / up / down: 8.25 / 27.1 ms against 10.2 / 34.6 for the
-// token-lane and 11.4 / 49.5 for the row-lane kernel). All three give the same bits.
+// A/B probe hook (scripts/clip_rate.py): 0 = automatic, 1 = token-lane (scalar candidates),
+// 2 = row-lane, 3 = token-lane with LDS candidates (k_auto_clip_tw). Process-wide; not for
+// production use. Automatic: k_auto_clip_tw whenever the sampled tokens fit its 512 lanes (it
+// wins at every Llama-3-8B shape: v / o / gate,up / down 1.80 / 6.63 / 24.9 / 24.1 ms against
+// 2.44 / 10.4 / 34.5 / 35.5 for the scalar-candidate token-lane kernel and 3.25 / 8.22 / 27.1 /
+// 27.1 for k_auto_clip, profiles/r6_clip_rate_tw.txt); above 512 tokens the round-6 rule: the
+// scalar-candidate kernel below 65536 row-groups, k_auto_clip (lcq_auto_clip_search_act) from
+// there. All four give the same bits.
 static int g_clip_variant = 0;
 extern "C" int lcq_auto_clip_force_variant(int v) {
-  LCQ_REQUIRE(v >= 0 && v <= 2, "variant: 0, 1 or 2");
+  LCQ_REQUIRE(v >= 0 && v <= 3, "variant: 0, 1, 2 or 3");
   g_clip_variant = v;
   return LCQ_OK;
 }
@@ -1290,7 +1533,8 @@ extern "C" int lcq_auto_clip_force_variant(int v) {
 extern "C" int64_t lcq_auto_clip_workspace_bytes(int64_t oc, int64_t ic, int64_t T, int group,
                                                  int nsteps) {
   if (group != TL_G || oc <= 0 || ic <= 0 || T <= 0 || ic % TL_G || nsteps != TL_NS) return 0;
-  if (g_clip_variant == 0 && oc * (ic / TL_G) >= CL_PAIR_MIN_ROWGROUPS) return 0;  // k_auto_clip
+  if (g_clip_variant == 0 && T > 64 * TW_WAVES && oc * (ic / TL_G) >= CL_PAIR_MIN_ROWGROUPS)
+    return 0;  // k_auto_clip
   const int64_t per = tl_row_bytes(ic, nsteps);
   int64_t rows = ((int64_t)1 << 30) / per / CL_ROW_UNIT * CL_ROW_UNIT;
   if (rows < CL_ROW_UNIT) rows = CL_ROW_UNIT;
@@ -1308,11 +1552,16 @@ extern "C" int lcq_auto_clip_search_ws(const void* w, const void* x, const void*
                         T < ((int64_t)1 << 31) && oc > 0;
   const int64_t per = shape_ok ? tl_row_bytes(ic, nsteps) : 0;
   const int64_t xbytes = shape_ok ? T * ic * 4 : 0;
-  const int64_t chunk =
+  int64_t chunk =
       per && ws_bytes > xbytes ? (ws_bytes - xbytes) / per / CL_ROW_UNIT * CL_ROW_UNIT : 0;
+  // a chunk's table stays below 2 GiB (32-bit DMA offsets of k_auto_clip_tw)
+  if (per && chunk * per >= ((int64_t)1 << 31))
+    chunk = (((int64_t)1 << 31) - 1) / per / CL_ROW_UNIT * CL_ROW_UNIT;
   const bool al16 = ((reinterpret_cast<uintptr_t>(workspace) | reinterpret_cast<uintptr_t>(x)) &
                      15) == 0;
-  const bool pair_wins = g_clip_variant == 0 && oc * (ic / TL_G) >= CL_PAIR_MIN_ROWGROUPS;
+  const bool tw_fits = T <= 64 * TW_WAVES;
+  const bool pair_wins =
+      g_clip_variant == 0 && !tw_fits && oc * (ic / TL_G) >= CL_PAIR_MIN_ROWGROUPS;
   if (qx != nullptr || mse_steps != 0 || chunk < CL_ROW_UNIT || workspace == nullptr || !al16 ||
       (dtype != LCQ_BF16 && dtype != LCQ_F16) || qmax <= qmin || pair_wins)
     return lcq_auto_clip_search_act(w, x, qx, dtype, oc, ic, T, group, nsteps, factors, qmin,
@@ -1321,7 +1570,16 @@ extern "C" int lcq_auto_clip_search_ws(const void* w, const void* x, const void*
   hipStream_t st = as_stream(stream);
   const int64_t ng = ic / TL_G;
   const bool rl = g_clip_variant == 2;
-  float* xt = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + chunk * per);
+  const bool tw = (g_clip_variant == 0 || g_clip_variant == 3) && tw_fits;
+  if (tw) {
+    auto kb = k_auto_clip_tw<LCQ_BF16>;
+    auto kh = k_auto_clip_tw<LCQ_F16>;
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kb),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, TW_LDS);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kh),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, TW_LDS);
+  }
+  float* xt =reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + chunk * per);
   float* qt = reinterpret_cast<float*>(workspace);
   const auto* wp = reinterpret_cast<const uint16_t*>(w);
   const auto* xp = reinterpret_cast<const uint16_t*>(x);
@@ -1341,10 +1599,15 @@ extern "C" int lcq_auto_clip_search_ws(const void* w, const void* x, const void*
     const dim3 g1((unsigned)((nr + CROWS - 1) / CROWS), (unsigned)ng);
     const dim3 g2((unsigned)((nr + TL_ROWS_PER_WG - 1) / TL_ROWS_PER_WG), (unsigned)ng);
     const dim3 g3((unsigned)((nr + 63) / 64), (unsigned)ng);
+    const dim3 g4((unsigned)((nr + TW_RPW - 1) / TW_RPW), (unsigned)ng);
+    const uint32_t qtb = (uint32_t)(nr * ng * (int64_t)(nsteps + 1) * TL_G * 4);
     if (dtype == LCQ_BF16) {
       hipLaunchKernelGGL((k_clip_qtable<LCQ_BF16, TL_G>), g1, 2 * CROWS, 0, st, wp, ic, r0, nr,
                          nsteps, fp, (float)qmin, (float)qmax, sym, clip_sym, qt, om);
-      if (rl)
+      if (tw)
+        hipLaunchKernelGGL((k_auto_clip_tw<LCQ_BF16>), g4, 64 * TW_WAVES, TW_LDS, st, xp, ic,
+                           (int)T, qt, qtb, om, r0, nr, fp, clip_sym, bx, bn);
+      else if (rl)
         hipLaunchKernelGGL((k_auto_clip_rl<LCQ_BF16, TL_NS>), g3, 64, 0, st, xt, ic, (int)T, qt,
                            om, r0, nr, fp, clip_sym, bx, bn);
       else
@@ -1353,7 +1616,10 @@ extern "C" int lcq_auto_clip_search_ws(const void* w, const void* x, const void*
     } else {
       hipLaunchKernelGGL((k_clip_qtable<LCQ_F16, TL_G>), g1, 2 * CROWS, 0, st, wp, ic, r0, nr,
                          nsteps, fp, (float)qmin, (float)qmax, sym, clip_sym, qt, om);
-      if (rl)
+      if (tw)
+        hipLaunchKernelGGL((k_auto_clip_tw<LCQ_F16>), g4, 64 * TW_WAVES, TW_LDS, st, xp, ic,
+                           (int)T, qt, qtb, om, r0, nr, fp, clip_sym, bx, bn);
+      else if (rl)
         hipLaunchKernelGGL((k_auto_clip_rl<LCQ_F16, TL_NS>), g3, 64, 0, st, xt, ic, (int)T, qt,
                            om, r0, nr, fp, clip_sym, bx, bn);
       else

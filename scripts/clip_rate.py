@@ -30,9 +30,9 @@ for oc, ic in [(1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 
         qmin, qmax = (-8, 7) if sym else (0, 15)
         res = {}
         lib = N.load()
-        for tl in ('row-lane  ', 'token-lane', 'lane-pair '):
+        for tl in ('token-lds ', 'token-lane', 'lane-pair '):
             ops.CLIP_TOKEN_LANE = tl != 'lane-pair '
-            lib.lcq_auto_clip_force_variant(1 if tl == 'token-lane' else 2)
+            lib.lcq_auto_clip_force_variant({'token-lane': 1, 'token-lds ': 3}.get(tl, 2))
             res[tl] = ops.auto_clip_search(w, x, 128, 10, 20, qmin, qmax, sym, sym, qx=qx)
             torch.cuda.synchronize()
             ts = []
@@ -45,7 +45,7 @@ for oc, ic in [(1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1))
             ms = statistics.median(ts)
-            if sym and tl == 'row-lane  ':
+            if sym and tl == 'token-lds ':
                 tot_ms += ms
             prods = oc * ic * 512 * 11
             print(f'{oc}x{ic} sym={sym} {tl}: {ms:7.2f} ms  {prods / ms / 1e9:6.1f} G products/s',
@@ -55,4 +55,4 @@ for oc, ic in [(1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 
         print(f'  bit-identical: {same}', flush=True)
 ops.CLIP_TOKEN_LANE = True
 N.load().lcq_auto_clip_force_variant(0)
-print(f'one Llama-3-8B block (v, o, gate, up, down; sym, row-lane): {tot_ms:.1f} ms')
+print(f'one Llama-3-8B block (v, o, gate, up, down; sym, token-lds): {tot_ms:.1f} ms')

@@ -127,7 +127,7 @@ def test_auto_clip_vs_reference(dev, name):
     assert torch.equal(bits(w), bits(c['w_clipped']))
 
 
-@pytest.mark.parametrize('variant', [2, 1])
+@pytest.mark.parametrize('variant', [3, 2, 1])
 @pytest.mark.parametrize('oc,ic,T,dt,sym,clip_sym,small_ws', [
     (1024, 4096, 512, torch.bfloat16, True, True, False),     # v_proj, the AWQ headline
     (100, 384, 300, torch.bfloat16, False, False, True),      # ragged rows / tokens
@@ -136,7 +136,8 @@ def test_auto_clip_vs_reference(dev, name):
 def test_auto_clip_scalar_operand_matches_pair_kernel(dev, monkeypatch, variant, oc, ic, T, dt,
                                                       sym, clip_sym, small_ws):
     """lcq_auto_clip_search_ws (the candidate table + the row-lane kernel with the tokens as
-    scalar operands, or the token-lane kernel with the candidates as scalar operands) is
+    scalar operands, the token-lane kernel with the candidates as scalar operands, or the
+    token-lane kernel with the candidates staged in LDS, k_auto_clip_tw) is
     bit-identical to k_auto_clip (lcq_auto_clip_search_act) -- the same products, 8-way
     partial sums, halving tree and token-order error sums -- including ragged tokens and rows,
     fp16, and row chunks of a small workspace."""
