@@ -339,8 +339,9 @@ PEAK_CLIP_GPRODUCTS = 1024 * 2.4 / 2 * 32   # 3.93e4 G products/s
 def clip_roofline(kern):
     """The auto-clip search (AutoClipper.auto_clip_layer, auto_clip.py:83-191) against its
     VALU issue bound: products per second over the launches' HIP-event time, both entries
-    together (lcq_auto_clip_search_ws runs the layers below 65536 row-groups on the token-lane
-    kernel, lcq_auto_clip_search_act the rest on the lane-pair k_auto_clip)."""
+    together (lcq_auto_clip_search_ws runs every layer of the headline on k_clip_qtable +
+    k_auto_clip_tw while the sampled tokens fit 512 lanes; lcq_auto_clip_search_act is the
+    lane-pair k_auto_clip for the other configurations)."""
     ts = [kern[k] for k in ('lcq_auto_clip_search_ws', 'lcq_auto_clip_search_act')
           if kern.get(k) and kern[k].get('flops')]
     if not ts:
@@ -349,14 +350,13 @@ def clip_roofline(kern):
     ms = sum(t['total_ms'] for t in ts)
     launches = sum(t['launches'] for t in ts)
     gp = flops / (ms * 1e-3) / 1e9
-    return {'kernel': ('k_auto_clip (two weight rows per lane pair; layers of >= 65536 '
-                       'row-groups) + k_clip_qtable / k_auto_clip_tl (one lane per token, the '
-                       'candidates as scalar operands; v_proj)'),
+    return {'kernel': ('k_clip_qtable + k_auto_clip_tw (one lane per sampled token, all 512 '
+                       'in one 8-wave workgroup, candidate rows staged in LDS by LDS-DMA)'),
             'bound': 'valu', 'achieved': round(gp, 1), 'peak': PEAK_CLIP_GPRODUCTS,
             'unit': 'G products/s', 'frac': round(gp / PEAK_CLIP_GPRODUCTS, 4),
             'avg_launch_ms': round(ms / launches, 4), 'launches': launches,
             'products_per_launch': flops / launches,
-            'pmc_source': 'profiles/r6_clip_pmc.txt'}
+            'pmc_source': 'profiles/r6_clip_tw_pmc.txt'}
 
 
 def cpu_baseline_awq(args, budget_s):

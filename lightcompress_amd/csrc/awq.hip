@@ -1190,38 +1190,16 @@ __global__ void __launch_bounds__(64 * TW_WAVES)
     // under chunk c's products, across pass boundaries too (the walk's last two prefetches
     // read the 32 floats after the buffer: LDS in bounds, unused)
     float4 q0[4], q1[4];
-#ifdef LCQ_PROBE_TW_DEEP
-    float4 qd[4];
-#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       q0[j] = reinterpret_cast<const float4*>(cs)[j];
       q1[j] = reinterpret_cast<const float4*>(cs + 16)[j];
-#ifdef LCQ_PROBE_TW_DEEP
-      qd[j] = reinterpret_cast<const float4*>(cs + 32)[j];
-#endif
     }
     float org = 0.f;
 #pragma unroll 1
     for (int rp = 0; rp < TW_R * P; ++rp) {
       const float* qp = cs + rp * G;
       v2f a0 = v2f{0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
-#ifdef LCQ_PROBE_TW_DEEP
-      // three chunks in flight: chunk c + 3 is read under chunk c
-#pragma unroll
-      for (int c = 0; c < G / 16; ++c) {
-        float4 qn[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) qn[j] = reinterpret_cast<const float4*>(qp + 16 * (c + 3))[j];
-        mac16v<DT>(xf, 16 * c, q0, a0, a1, a2, a3);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          q0[j] = q1[j];
-          q1[j] = qd[j];
-          qd[j] = qn[j];
-        }
-      }
-#else
 #pragma unroll
       for (int c = 0; c < G / 16; c += 2) {
         float4 q2[4], q3[4];
@@ -1237,7 +1215,6 @@ __global__ void __launch_bounds__(64 * TW_WAVES)
           q1[j] = q3[j];
         }
       }
-#endif
       const v2f l01 = a0 + a2, l23 = a1 + a3;   // l_m = acc_m + acc_{m+4}
       const v2f s2 = l01 + l23;                 // (l0 + l2, l1 + l3)
       const float d = dtr<DT>(s2.x + s2.y);
