@@ -1,7 +1,7 @@
-# round 6 (u): the full GPU suite, smoke and the driver's bench command (--steps 20 --warmup 5)
-# on the code after the left-looking column loop and the small chain products
+# round 6 (final): the full GPU suite, smoke and the driver bench command (--steps 20 --warmup 5)
+# on the final code (k_auto_clip_tw automatic, left-looking column loop, small chain products)
 set -o pipefail
-O=gpurun_out/r6u
+O=gpurun_out/r6z
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread --maxfail 5 \
   > $O/gputest_full.log 2>&1
