@@ -397,12 +397,12 @@ int lcq_auto_clip_search_act(const void* w, const void* x, const void* qx, int d
 
 /* lcq_auto_clip_search_act with a caller workspace of lcq_auto_clip_workspace_bytes(oc, ic, T,
  * group, nsteps) bytes (16-byte aligned; 0 = not applicable). Weight-only searches (qx NULL)
- * with group 128, min/max qparams, nsteps 10 and fewer than 65536 row-groups (oc * ic / 128:
- * where the lane-pair kernel's grid leaves the chip short) run the scalar-operand kernels: the
- * candidate weights of every (row, step) tabulated once in the workspace (row chunks of at most
- * 1 GiB), then one lane per token with the candidates as scalar operands. Results are
- * bit-identical to lcq_auto_clip_search_act, which every other case (larger layers, and a
- * workspace too small for 192 rows) runs. */
+ * with group 128, min/max qparams and nsteps 10 tabulate the candidate weights of every
+ * (row, step) once in the workspace (row chunks of at most 1 GiB) and then run: with T <= 512
+ * sampled tokens, one lane per token, all T tokens in one workgroup, the candidate rows staged
+ * in LDS (k_auto_clip_tw); above 512 tokens, below 65536 row-groups, one lane per token with the
+ * candidates as scalar operands. Results are bit-identical to lcq_auto_clip_search_act, which
+ * every other case (larger layers above 512 tokens, a workspace too small for 192 rows) runs. */
 int64_t lcq_auto_clip_workspace_bytes(int64_t oc, int64_t ic, int64_t T, int group, int nsteps);
 int lcq_auto_clip_search_ws(const void* w, const void* x, const void* qx, int dtype, int64_t oc,
                             int64_t ic, int64_t T, int group, int nsteps, const void* factors,
@@ -411,9 +411,9 @@ int lcq_auto_clip_search_ws(const void* w, const void* x, const void* qx, int dt
                             void* workspace, int64_t ws_bytes, void* stream);
 
 /* A/B probe hook of lcq_auto_clip_search_ws (scripts/clip_rate.py): 0 = automatic, 1 = the
- * token-lane kernel at every size (one lane per token, candidates as scalar operands), 2 = the
- * row-lane kernel (one lane per weight row, tokens as scalar operands). Process-wide; not for
- * production use. */
+ * token-lane kernel with scalar-operand candidates at every size, 2 = the row-lane kernel (one
+ * lane per weight row, tokens as scalar operands), 3 = k_auto_clip_tw (LDS candidates; T <= 512).
+ * Process-wide; not for production use. */
 int lcq_auto_clip_force_variant(int variant);
 
 /* AutoClipper.auto_clip_layer for per_channel integer weights (group = ic, auto_clip.py:96-99;
